@@ -1,0 +1,282 @@
+/*
+ * swim.h — C ABI of the lockstep SWIM simulation engine (libswimgpu.so).
+ *
+ * One engine handle simulates N virtual scalecube-cluster members in lockstep virtual time.
+ * It replaces, for all N members at once, the three protocol objects that
+ * ClusterImpl.doStart0 constructs (cluster/src/main/java/io/scalecube/cluster/ClusterImpl.java:260-291):
+ *   FailureDetectorImpl   (cluster/.../fdetector/FailureDetectorImpl.java:75-99)
+ *   GossipProtocolImpl    (cluster/.../gossip/GossipProtocolImpl.java:81-104)
+ *   MembershipProtocolImpl(cluster/.../membership/MembershipProtocolImpl.java:120-168)
+ * plus the Transport + NetworkEmulator underneath them
+ * (cluster-testlib/.../utils/NetworkEmulatorTransport.java:49-83, NetworkEmulator.java:167-202,349-369).
+ *
+ * Plain C: integers, pointers and sizes only.  Every function returns an int32 status
+ * (SWIM_OK or a negative SWIM_E* code); nothing throws across the ABI.  A handle is
+ * single-threaded, mirroring the reference's one-scheduler-per-member confinement
+ * (ClusterImpl.java:257).  The engine owns all device memory; callers own output buffers.
+ *
+ * The same ABI is exported by the CPU oracle (oracle/liboracle_swim.so, test infrastructure
+ * only) so that parity tests drive both through identical code.
+ */
+#ifndef SWIM_H
+#define SWIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------------------ */
+#define SWIM_OK 0
+#define SWIM_EINVAL (-1)     /* bad argument / unsupported configuration */
+#define SWIM_ENOMEM (-2)     /* device or host allocation failed */
+#define SWIM_EDEVICE (-3)    /* HIP runtime error or no MI355X device */
+#define SWIM_ECAPACITY (-4)  /* a fixed-capacity structure overflowed; state is no longer exact */
+#define SWIM_ESTATE (-5)     /* operation not valid in the member's current state */
+
+/* ---- member status (MemberStatus.java:3-19, declaration order) ------------------------ */
+#define SWIM_ALIVE 0
+#define SWIM_SUSPECT 1
+#define SWIM_LEAVING 2
+#define SWIM_DEAD 3
+
+/* ---- membership event types (MembershipEvent.java:15-20, declaration order) ----------- */
+#define SWIM_EV_ADDED 0
+#define SWIM_EV_REMOVED 1
+#define SWIM_EV_LEAVING 2
+#define SWIM_EV_UPDATED 3
+/* FailureDetectorEvent (FailureDetectorEvent.java:8-33), only when record_fd_events = 1 */
+#define SWIM_EV_FD_ALIVE 16
+#define SWIM_EV_FD_SUSPECT 17
+#define SWIM_EV_FD_DEAD 18
+
+/* ---- canonical intra-tick phases ---------------------------------------- */
+#define SWIM_PHASE_TIMERS 1  /* suspicion timeouts      (MembershipProtocolImpl.java:825-834) */
+#define SWIM_PHASE_FD 2      /* ping / ping-req / ack    (FailureDetectorImpl.java:126-210)   */
+#define SWIM_PHASE_GOSSIP 3  /* one gossip round         (GossipProtocolImpl.java:141-215)    */
+#define SWIM_PHASE_SYNC 4    /* SYNC requests delivered  (MembershipProtocolImpl.java:394-415)*/
+#define SWIM_PHASE_SYNCACK 5 /* SYNC_ACKs delivered      (MembershipProtocolImpl.java:385-391)*/
+#define SWIM_PHASE_CONTROL 6 /* host control ops (leave, join) applied between ticks          */
+
+/*
+ * Packed view cell: one 64-bit word per (viewer, subject).  This is also the readback format of
+ * swim_read_view.  It holds the viewer's MembershipRecord for the subject
+ * (MembershipRecord.java:20-22) plus the per-subject bits the reference keeps in side maps:
+ * `members` (MembershipProtocolImpl.java:89), `aliveEmittedSet` (:91), the MetadataStore entry
+ * (MetadataStoreImpl.java:104-143) and the suspicion task (:105, :805-823).
+ *   bits  0..31  incarnation (int32, MembershipRecord.java:22)
+ *   bits 32..33  status (SWIM_ALIVE / SWIM_SUSPECT / SWIM_LEAVING; DEAD is never stored)
+ *   bit  34      in_table       — row present in membershipTable
+ *   bit  35      in_members     — subject present in the `members` map
+ *   bit  36      alive_emitted  — subject present in aliveEmittedSet
+ *   bit  37      has_timer      — a suspicion timeout task is scheduled
+ *   bit  38      has_metadata   — MetadataStore holds metadata for the subject
+ *   bits 39..63  timer deadline tick (mod 2^25), valid when has_timer
+ */
+#define SWIM_CELL_INC(c) ((int32_t)(uint32_t)((c)&0xffffffffull))
+#define SWIM_CELL_STATUS(c) ((uint32_t)(((c) >> 32) & 3u))
+#define SWIM_CELL_IN_TABLE(c) ((uint32_t)(((c) >> 34) & 1u))
+#define SWIM_CELL_IN_MEMBERS(c) ((uint32_t)(((c) >> 35) & 1u))
+#define SWIM_CELL_ALIVE_EMITTED(c) ((uint32_t)(((c) >> 36) & 1u))
+#define SWIM_CELL_HAS_TIMER(c) ((uint32_t)(((c) >> 37) & 1u))
+#define SWIM_CELL_HAS_METADATA(c) ((uint32_t)(((c) >> 38) & 1u))
+#define SWIM_CELL_DEADLINE(c) ((uint32_t)((c) >> 39))
+#define SWIM_DEADLINE_MASK 0x1ffffffu
+
+/*
+ * Protocol configuration.  Field-for-field mirror of the reference knobs
+ * (FailureDetectorConfig.java:9-25, GossipConfig.java:9-25, MembershipConfig.java:14-32,
+ * ClusterConfig.java:28-38) plus engine knobs.  All times are milliseconds of virtual time.
+ */
+typedef struct swim_config {
+  /* FailureDetectorConfig */
+  int32_t ping_interval;      /* DEFAULT_PING_INTERVAL = 1000 */
+  int32_t ping_timeout;       /* DEFAULT_PING_TIMEOUT = 500 (must be < ping_interval) */
+  int32_t ping_req_members;   /* DEFAULT_PING_REQ_MEMBERS = 3 (<= 16) */
+  /* GossipConfig */
+  int32_t gossip_interval;    /* DEFAULT_GOSSIP_INTERVAL = 200 */
+  int32_t gossip_fanout;      /* DEFAULT_GOSSIP_FANOUT = 3 (<= 16) */
+  int32_t gossip_repeat_mult; /* DEFAULT_GOSSIP_REPEAT_MULT = 3 */
+  int32_t gossip_segmentation_threshold; /* GOSSIP_SEGMENTATION_THRESHOLD = 1000 */
+  /* MembershipConfig */
+  int32_t sync_interval;      /* DEFAULT_SYNC_INTERVAL = 30000 */
+  int32_t sync_timeout;       /* DEFAULT_SYNC_TIMEOUT = 3000 */
+  int32_t suspicion_mult;     /* DEFAULT_SUSPICION_MULT = 5 */
+  int32_t removed_members_history_size; /* 42 (monitoring only; kept for config fidelity) */
+  /* ClusterConfig */
+  int32_t metadata_timeout;   /* DEFAULT_METADATA_TIMEOUT = 3000 */
+  /* ---- engine knobs (no reference counterpart) ---- */
+  int32_t tick_ms;            /* 0 = gcd of every interval/timeout above */
+  int32_t sync_stagger;       /* 1 = each initial member's periodic SYNC gets a random phase */
+  int32_t record_fd_events;   /* 1 = FailureDetectorEvents appear in the event stream */
+  uint32_t gossip_capacity;   /* max live GossipStates per member (0 = default 256) */
+  uint32_t collector_capacity;/* max distinct gossipers whose SequenceIdCollector a member holds
+                                 (power of two; 0 = default 256) */
+  uint32_t event_capacity;    /* undrained events the engine may buffer (0 = default 1<<22) */
+  uint32_t reserved[8];
+} swim_config;
+
+/* preset: 0 = defaultConfig/defaultLanConfig, 1 = defaultWanConfig, 2 = defaultLocalConfig
+ * (ClusterConfig.java:54-93) */
+int32_t swim_config_default(swim_config* cfg, int32_t preset);
+
+/* ClusterMath (ClusterMath.java:38-135) */
+int32_t swim_ceil_log2(int32_t num);                                       /* :133-135 */
+int32_t swim_gossip_periods_to_spread(int32_t repeat_mult, int32_t cluster_size); /* :111-113 */
+int32_t swim_gossip_periods_to_sweep(int32_t repeat_mult, int32_t cluster_size);  /* :99-102 */
+int64_t swim_suspicion_timeout(int32_t suspicion_mult, int32_t cluster_size,
+                               int64_t ping_interval);                      /* :123-125 */
+
+typedef struct swim_engine swim_engine;
+
+/*
+ * Create an engine with `capacity` member slots (slot = member address; member ids are slot
+ * numbers).  Slots [0, n_initial) start up and fully converged: every table holds every initial
+ * member ALIVE at incarnation 0 and every ping / gossip list is a seeded shuffle.  Slots
+ * [n_initial, capacity) are free until swim_join.  `seed` keys the counter-based Philox RNG that
+ * replaces ThreadLocalRandom / Collections.shuffle.
+ */
+int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initial, uint64_t seed,
+                    swim_engine** out);
+int32_t swim_destroy(swim_engine* e);
+
+/* Advance virtual time.  swim_step advances `periods` * (ping_interval / tick) ticks. */
+int32_t swim_step_ticks(swim_engine* e, uint32_t ticks);
+int32_t swim_step(swim_engine* e, uint32_t periods);
+int32_t swim_now(const swim_engine* e, uint64_t* tick, uint32_t* tick_ms, uint32_t* ticks_per_period);
+
+/* ---- seeds (MembershipConfig.seedMembers, MembershipProtocolImpl.java:143,461-472) ------ */
+int32_t swim_set_seeds(swim_engine* e, const uint32_t* seeds, uint32_t n_seeds);
+
+/* ---- lifecycle --------------------------------------------------------------------------- */
+/* Stop member m's transport abruptly (TransportImpl.stop): sends to it fail at the sender. */
+int32_t swim_kill(swim_engine* e, uint32_t m);
+/* Graceful shutdown (ClusterImpl.doShutdown :508-517): LEAVING inc+1 gossip now
+ * (MembershipProtocolImpl.leaveCluster :233-242); the member stops once that gossip's spread()
+ * completes (GossipProtocolImpl.java:167-180). stop_after = 0 only publishes LEAVING. */
+int32_t swim_leave(swim_engine* e, uint32_t m, int32_t stop_after);
+/* Start a fresh member in free slot m (ClusterImpl.doStart0 + MembershipProtocolImpl.start0
+ * :250-291): initial SYNC to every seed during the next tick. */
+int32_t swim_join(swim_engine* e, uint32_t m);
+
+/* ---- network emulator (NetworkEmulator.java) ----------------------------------------------
+ * Outbound loss is decided at the sender and fails the send immediately (:167-181); inbound
+ * blocking silently drops at the receiver (NetworkEmulatorTransport.java:69-83). */
+/* setDefaultOutboundSettings(lossPercent, 0) (:80-83); m = UINT32_MAX applies to every member */
+int32_t swim_set_default_loss(swim_engine* e, uint32_t m, int32_t loss_percent);
+/* outboundSettings(dst, loss, 0) on src (:69-73); loss_percent < 0 removes the override
+ * (unblockOutbound :134-139) */
+int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t loss_percent);
+/* inboundSettings(src, shallPass) on dst (:219-223); shall_pass < 0 removes the override */
+int32_t swim_set_link_inbound(swim_engine* e, uint32_t dst, uint32_t src, int32_t shall_pass);
+/* setDefaultInboundSettings(shallPass) (:230-233); m = UINT32_MAX applies to every member */
+int32_t swim_set_default_inbound(swim_engine* e, uint32_t m, int32_t shall_pass);
+/* Partition shorthand: outbound between members of different groups is blocked (100 % loss at
+ * the sender, NetworkEmulator.blockOutbound :117-121).  groups = NULL heals the partition. */
+int32_t swim_set_partition(swim_engine* e, const uint16_t* group_of_member);
+
+/* ---- readback --------------------------------------------------------------------------- */
+/* Viewer's whole row, `capacity` packed cells (format above). */
+int32_t swim_read_view(swim_engine* e, uint32_t viewer, uint64_t* out_cells);
+
+typedef struct swim_event {
+  uint64_t tick;
+  uint32_t viewer;
+  uint32_t subject;
+  uint32_t type;  /* SWIM_EV_* */
+  uint32_t phase; /* SWIM_PHASE_* */
+  uint32_t minor; /* order within (tick, viewer, phase) */
+  uint32_t pad;
+} swim_event;
+/* Events in canonical order (tick, viewer, phase, minor).  *n_out = events copied; events that
+ * did not fit stay buffered for the next call. */
+int32_t swim_drain_events(swim_engine* e, swim_event* out, size_t cap, size_t* n_out);
+
+typedef struct swim_stats {
+  uint64_t ticks;
+  uint64_t pings;             /* doPing with a target            */
+  uint64_t ping_reqs;         /* doPingReq launches              */
+  uint64_t fd_events;         /* FailureDetectorEvents published */
+  uint64_t gossips_created;   /* createAndPutGossip              */
+  uint64_t gossip_messages;   /* GOSSIP_REQ messages sent        */
+  uint64_t gossip_accepted;   /* first receipts (collector add)  */
+  uint64_t syncs;             /* SYNC messages sent              */
+  uint64_t sync_acks;         /* SYNC_ACK messages delivered     */
+  uint64_t sync_records;      /* records merged by syncMembership */
+  uint64_t fetches;           /* GET_METADATA round trips issued */
+  uint64_t fetch_ok;
+  uint64_t timers_fired;
+  uint64_t events;
+  uint64_t capacity_errors;
+  uint64_t reserved[9];
+} swim_stats;
+int32_t swim_get_stats(swim_engine* e, swim_stats* out);
+
+/* ---- full-state readback for parity tests (not needed by a Java host) --------------------- */
+typedef struct swim_member_state {
+  uint8_t up;
+  uint8_t joined;
+  uint8_t leave_pending;     /* graceful leave waiting for its gossip to spread */
+  uint8_t join_pending;      /* initial sync scheduled for the next tick */
+  int32_t remote_idx;        /* GossipProtocolImpl.remoteMembersIndex */
+  uint64_t fd_period;        /* FailureDetectorImpl.currentPeriod */
+  uint32_t ping_cursor;      /* FailureDetectorImpl.pingMemberIndex */
+  uint32_t ping_len;
+  uint32_t remote_len;
+  uint32_t gossip_len;       /* live GossipStates */
+  uint64_t gossip_period;    /* GossipProtocolImpl.currentPeriod */
+  uint64_t gossip_counter;   /* GossipProtocolImpl.gossipCounter */
+  uint32_t table_size;       /* membershipTable.size() */
+  uint32_t members_size;     /* members.size() */
+  int64_t fd_start, gossip_start, sync_start; /* timer phases (ticks); sync_start valid if sync_on */
+  uint8_t sync_on;
+  uint8_t pad[3];
+  uint32_t ack_target;       /* pending ping-req launch (ack timeout) */
+  uint64_t ack_due;          /* 0 = none */
+  uint32_t relay_target;     /* pending relay timeouts */
+  uint32_t relay_pending;
+  uint64_t relay_due;        /* 0 = none */
+  uint32_t leave_gossiper;   /* id of the LEAVING gossip a graceful leave waits on */
+  uint32_t pad2;
+  uint64_t leave_seq;
+} swim_member_state;
+int32_t swim_read_member(swim_engine* e, uint32_t m, swim_member_state* out);
+/* FailureDetectorImpl.pingMembers / GossipProtocolImpl.remoteMembers in list order */
+int32_t swim_read_ping_list(swim_engine* e, uint32_t m, uint32_t* out, uint32_t cap, uint32_t* len);
+int32_t swim_read_remote_list(swim_engine* e, uint32_t m, uint32_t* out, uint32_t cap, uint32_t* len);
+
+typedef struct swim_gossip {
+  uint32_t gossiper;          /* Gossip.gossiperId */
+  uint32_t subject;           /* MembershipRecord carried as the gossip payload */
+  uint64_t seq;               /* Gossip.sequenceId */
+  int32_t inc;
+  uint32_t status;
+  uint64_t infection_period;  /* GossipState.infectionPeriod */
+  uint32_t infected[2];       /* GossipState.infected (UINT32_MAX = empty slot) */
+} swim_gossip;
+/* Live gossips of member m in canonical (insertion) order. */
+int32_t swim_read_gossips(swim_engine* e, uint32_t m, swim_gossip* out, uint32_t cap, uint32_t* len);
+
+typedef struct swim_interval {
+  uint64_t lo, hi;
+} swim_interval;
+/* SequenceIdCollector of (m, gossiper): closed intervals in ascending order. */
+int32_t swim_read_collector(swim_engine* e, uint32_t m, uint32_t gossiper, swim_interval* out,
+                            uint32_t cap, uint32_t* len);
+
+/* ---- known-answer hooks (run the engine's own merge / dedupe code on given inputs) --------- */
+/* Philox4x32-10 block used by every draw site. */
+int32_t swim_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* MembershipRecord.isOverrides for n cases; case i = cases[5i..5i+4] =
+ * {r1_status, r1_inc, r0_present, r0_status, r0_inc}; out[i] = 0/1 (MembershipRecordTest). */
+int32_t swim_kat_overrides(const int32_t* cases, uint32_t n, uint8_t* out);
+/* One SequenceIdCollector driven by n ops (SequenceIdCollectorTest):
+ * kinds[i] = 0 add(values[i]) -> 1/0, 1 contains(values[i]) -> 1/0, 2 size() -> count, 3 clear() -> 0. */
+int32_t swim_kat_collector(const uint8_t* kinds, const int64_t* values, uint32_t n, int64_t* results);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SWIM_H */

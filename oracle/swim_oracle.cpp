@@ -1,0 +1,1256 @@
+// swim_oracle.cpp — CPU lockstep restatement of scalecube-cluster's protocol layer.
+//
+// TEST INFRASTRUCTURE ONLY.  This file is the parity oracle and the CPU baseline of bench.py.
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it; the product
+// (libswimgpu.so and the swimgpu package) never links, loads or falls back to it.
+//
+// It follows the reference Java line by line, with the sequential data structures the Java uses
+// (ArrayList ping/remote lists, a TreeMap interval set per gossiper, an insertion-ordered gossip
+// map, per-member tables), and fixes the canonical intra-tick order documented in DESIGN.md §3.
+// Citations are to /root/reference/cluster/src/main/java/io/scalecube/cluster/ unless noted.
+//
+// Parity status: pinned by the reference's own known-answer tests (MembershipRecordTest,
+// SequenceIdCollectorTest, ClusterMath values) and by scenario goldens restating
+// FailureDetectorTest / MembershipProtocolTest / GossipProtocolTest outcomes (tests/).  The JVM
+// reference itself cannot run here (no JDK), so the RNG-stream is defined by swim_rng.h, not by
+// the JVM's ThreadLocalRandom.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <new>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "swim.h"
+#include "swim_rng.h"
+
+namespace {
+
+constexpr uint32_t NONE = 0xffffffffu;
+
+// ----------------------------------------------------------------------------- Philox4x32-10
+void philox4x32_10(const uint32_t in[4], const uint32_t k[2], uint32_t out[4]) {
+  uint32_t c0 = in[0], c1 = in[1], c2 = in[2], c3 = in[3];
+  uint32_t k0 = k[0], k1 = k[1];
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+inline uint32_t next_int(uint32_t w, uint32_t bound) { return (uint32_t)(((uint64_t)w * bound) >> 32); }
+
+// ----------------------------------------------------------------------------- records
+enum Reason { FD_EVENT, MEMBERSHIP_GOSSIP, SYNC, INITIAL_SYNC, SUSPICION_TIMEOUT };  // :58-64
+
+struct Record {  // MembershipRecord.java:20-22
+  uint32_t member;
+  uint32_t status;
+  int32_t inc;
+};
+
+// MembershipRecord.isOverrides (MembershipRecord.java:67-88); r0 == nullptr for "no record".
+bool is_overrides(const Record& r1, const Record* r0) {
+  if (!r0) return r1.status == SWIM_ALIVE || r1.status == SWIM_LEAVING;
+  if (r1.status == r0->status && r1.inc == r0->inc) return false;  // equals (member equal)
+  if (r0->status == SWIM_DEAD) return false;
+  if (r1.status == SWIM_DEAD) return true;
+  if (r1.inc == r0->inc) return r1.status == SWIM_SUSPECT && (r0->status == SWIM_ALIVE || r0->status == SWIM_LEAVING);
+  return r1.inc > r0->inc;
+}
+
+// ----------------------------------------------------------------------------- SequenceIdCollector
+// gossip/SequenceIdCollector.java:11-94 — closed intervals [a,b] in a TreeMap.
+struct SeqCollector {
+  std::map<int64_t, int64_t> iv;
+  static bool in_range(std::map<int64_t, int64_t>::iterator it, bool ok, int64_t x) {
+    return ok && it->first <= x && x <= it->second;
+  }
+  static bool next_to(std::map<int64_t, int64_t>::iterator it, bool ok, int64_t x) {
+    return ok && (x + 1 == it->first || x - 1 == it->second);
+  }
+  bool contains(int64_t x) {  // :32-35
+    auto it = iv.upper_bound(x);
+    if (it == iv.begin()) return false;
+    --it;
+    return in_range(it, true, x);
+  }
+  bool add(int64_t x) {  // :43-72
+    auto fl = iv.upper_bound(x);
+    bool has_fl = fl != iv.begin();
+    if (has_fl) --fl;
+    if (in_range(fl, has_fl, x)) return false;
+    auto ce = iv.lower_bound(x);
+    bool has_ce = ce != iv.end();
+    bool nf = next_to(fl, has_fl, x), nc = next_to(ce, has_ce, x);
+    if (nf && nc) {
+      int64_t a = fl->first, b = ce->second;
+      iv.erase(fl->first);
+      iv.erase(ce->first);
+      iv[a] = b;
+    } else if (nf) {
+      int64_t a = fl->first;
+      iv.erase(a);
+      iv[a] = x;
+    } else if (nc) {
+      int64_t b = ce->second;
+      iv.erase(ce->first);
+      iv[x] = b;
+    } else {
+      iv[x] = x;
+    }
+    return true;
+  }
+  size_t size() const { return iv.size(); }
+  void clear() { iv.clear(); }
+};
+
+// GossipState (gossip/GossipState.java:9-49) with its Gossip (Gossip.java, id = gossiper-seq)
+struct GossipState {
+  uint32_t gossiper;
+  uint64_t seq;
+  Record rec;
+  uint64_t infection_period;
+  std::vector<uint32_t> infected;  // HashSet<String>, kept in insertion order
+  bool is_infected(uint32_t m) const {
+    return std::find(infected.begin(), infected.end(), m) != infected.end();
+  }
+  void add_infected(uint32_t m) {
+    if (!is_infected(m)) infected.push_back(m);
+  }
+};
+
+struct Member {
+  bool up = false, joined = false, join_pending = false, join_now = false;
+  bool leave_pending = false, leave_done = false;
+  uint32_t leave_gossiper = NONE;
+  uint64_t leave_seq = 0;
+  // ---- FailureDetectorImpl (:48-50)
+  uint64_t fd_period = 0;
+  std::vector<uint32_t> ping_members;
+  uint32_t ping_index = 0;
+  uint32_t ack_target = NONE;
+  uint64_t ack_due = 0;
+  uint32_t relay_target = NONE, relay_pending = 0;
+  uint64_t relay_due = 0;
+  // ---- GossipProtocolImpl (:48-55)
+  uint64_t g_period = 0, g_counter = 0, period_used = 0;
+  std::unordered_map<uint32_t, SeqCollector> collectors;
+  std::vector<GossipState> gossips;  // insertion order == canonical order
+  std::vector<uint32_t> remote;
+  int32_t remote_index = -1;
+  // ---- MembershipProtocolImpl: table / members / aliveEmittedSet / metadata / timers live in
+  // the packed row (swim.h cell format), one word per subject.
+  std::vector<uint64_t> row;
+  uint32_t table_size = 0, members_size = 0;
+  std::vector<uint32_t> fd_sync;  // SYNCs requested by FD ALIVE events this tick (:427-442)
+  // timer phases
+  int64_t fd_start = 0, g_start = 0, sync_start = 0;
+  bool sync_on = false;
+  // per-tick bookkeeping
+  uint32_t ev_minor = 0, fetch_ctr = 0;
+};
+
+// cell helpers
+constexpr uint64_t B_IN_TABLE = 1ull << 34, B_IN_MEMBERS = 1ull << 35, B_ALIVE_EMITTED = 1ull << 36,
+                   B_HAS_TIMER = 1ull << 37, B_HAS_METADATA = 1ull << 38;
+inline int32_t c_inc(uint64_t c) { return (int32_t)(uint32_t)c; }
+inline uint32_t c_status(uint64_t c) { return (uint32_t)((c >> 32) & 3u); }
+inline bool c_has(uint64_t c, uint64_t bit) { return (c & bit) != 0; }
+inline uint32_t c_deadline(uint64_t c) { return (uint32_t)(c >> 39); }
+inline uint64_t c_with_record(uint64_t c, uint32_t status, int32_t inc) {
+  return (c & ~0x3ffffffffull) | (uint64_t)(uint32_t)inc | ((uint64_t)status << 32);
+}
+inline uint64_t c_with_deadline(uint64_t c, uint64_t tick) {
+  return (c & ((1ull << 39) - 1)) | ((tick & SWIM_DEADLINE_MASK) << 39);
+}
+
+struct LinkKey {
+  uint32_t a, b;
+  bool operator<(const LinkKey& o) const { return a < o.a || (a == o.a && b < o.b); }
+};
+
+struct SyncReq {
+  uint32_t from, to, ordinal;
+  bool initial, outfail, delivered, acked;
+};
+
+struct PendingAlive {
+  Record r1;
+};
+
+}  // namespace
+
+struct swim_engine {
+  swim_config cfg{};
+  uint32_t n = 0;
+  uint64_t seed = 0;
+  uint32_t key[2]{};
+  uint64_t T = 0;
+  uint32_t tick_ms = 0, P = 0, to_ticks = 0, relay_ticks = 0, G = 0, S = 0, sync_to_ticks = 0;
+  std::vector<Member> m;
+  std::vector<uint32_t> seeds;
+  std::vector<uint8_t> is_seed;
+  // network emulator
+  std::vector<int32_t> default_loss;
+  std::vector<uint8_t> default_inbound;
+  std::map<LinkKey, int32_t> link_loss;     // (src,dst) -> loss %
+  std::map<LinkKey, uint8_t> link_inbound;  // (dst,src) -> shallPass
+  bool partition = false;
+  std::vector<uint16_t> group;
+  // timers: deadline tick -> (viewer, subject)
+  std::map<uint64_t, std::vector<std::pair<uint32_t, uint32_t>>> timer_queue;
+  std::vector<swim_event> events;
+  swim_stats st{};
+
+  // ------------------------------------------------------------------------- RNG
+  uint32_t draw(uint32_t member, uint32_t stream, uint32_t sub24, uint32_t sub32, uint64_t tick) const {
+    uint32_t c[4] = {member, (uint32_t)tick, (stream << 24) | (sub24 & 0xffffffu), sub32};
+    uint32_t o[4];
+    philox4x32_10(c, key, o);
+    return o[0];
+  }
+  uint32_t draw(uint32_t member, uint32_t stream, uint32_t sub24, uint32_t sub32) const {
+    return draw(member, stream, sub24, sub32, T);
+  }
+  static bool lost(int32_t pct, uint32_t w) { return pct > 0 && (pct >= 100 || (int32_t)next_int(w, 100) < pct); }
+
+  // ------------------------------------------------------------------------- NetworkEmulator
+  // OutboundSettings resolution (NetworkEmulator.java:59-61), partition shorthand first.
+  int32_t out_loss(uint32_t a, uint32_t b) const {
+    if (partition && group[a] != group[b]) return 100;
+    auto it = link_loss.find({a, b});
+    if (it != link_loss.end()) return it->second;
+    return default_loss[a];
+  }
+  // InboundSettings of receiver b for sender a (NetworkEmulator.java:212-214)
+  bool in_pass(uint32_t b, uint32_t a) const {
+    auto it = link_inbound.find({b, a});
+    if (it != link_inbound.end()) return it->second != 0;
+    return default_inbound[b] != 0;
+  }
+  // tryFailOutbound (:167-181) + a stopped destination refusing the connection
+  bool out_fail(uint32_t a, uint32_t b, uint32_t w) const { return !m[b].up || lost(out_loss(a, b), w); }
+
+  // ------------------------------------------------------------------------- events
+  void emit(uint32_t v, uint32_t subject, uint32_t type, uint32_t phase, uint32_t minor) {
+    swim_event e{};
+    e.tick = T;
+    e.viewer = v;
+    e.subject = subject;
+    e.type = type;
+    e.phase = phase;
+    e.minor = minor;
+    events.push_back(e);
+    st.events++;
+  }
+  uint32_t next_minor(uint32_t v) { return m[v].ev_minor++; }
+
+  // FailureDetectorImpl.onMemberEvent (:321-346) + GossipProtocolImpl.onMemberEvent (:238-261)
+  void on_member_added(uint32_t v, uint32_t s, uint32_t phase, uint32_t minor) {
+    auto& pm = m[v].ping_members;
+    uint32_t size = (uint32_t)pm.size();
+    uint32_t idx = size > 0 ? next_int(draw(v, SWIM_STREAM_PING_INSERT, phase, minor), size) : 0;
+    pm.insert(pm.begin() + idx, s);
+    m[v].remote.push_back(s);
+  }
+  void on_member_removed(uint32_t v, uint32_t s) {
+    auto& pm = m[v].ping_members;
+    auto it = std::find(pm.begin(), pm.end(), s);
+    if (it != pm.end()) pm.erase(it);
+    auto& rm = m[v].remote;
+    auto it2 = std::find(rm.begin(), rm.end(), s);
+    if (it2 != rm.end()) rm.erase(it2);
+    m[v].collectors.erase(s);  // sequenceIdCollectors.remove(member.id()) (:242)
+  }
+  void publish_event(uint32_t v, uint32_t s, uint32_t type, uint32_t phase, uint32_t minor) {
+    emit(v, s, type, phase, minor);
+    if (type == SWIM_EV_ADDED) on_member_added(v, s, phase, minor);
+    if (type == SWIM_EV_REMOVED) on_member_removed(v, s);
+  }
+  uint32_t ev_minor_for(uint32_t v, uint32_t phase, uint32_t subject) {
+    return phase == SWIM_PHASE_TIMERS ? subject : next_minor(v);
+  }
+
+  // ------------------------------------------------------------------------- gossip origination
+  // spreadMembershipGossip (MembershipProtocolImpl.java:845-860) -> GossipProtocolImpl.spread ->
+  // createAndPutGossip (GossipProtocolImpl.java:190-199)
+  void spread_gossip(uint32_t v, const Record& r) {
+    Member& mv = m[v];
+    GossipState g;
+    g.gossiper = v;
+    g.seq = mv.g_counter++;
+    g.rec = r;
+    g.infection_period = mv.g_period;
+    mv.gossips.push_back(g);
+    mv.collectors[v].add((int64_t)g.seq);
+    st.gossips_created++;
+  }
+
+  // ------------------------------------------------------------------------- timers
+  // scheduleSuspicionTimeoutTask (:805-823): computeIfAbsent, timeout from the table size now.
+  void schedule_timer(uint32_t v, uint32_t s) {
+    uint64_t& c = m[v].row[s];
+    if (c_has(c, B_HAS_TIMER)) return;
+    int64_t ms = swim_suspicion_timeout(cfg.suspicion_mult, (int32_t)m[v].table_size, cfg.ping_interval);
+    uint64_t deadline = T + (uint64_t)(ms / tick_ms);
+    c = c_with_deadline(c | B_HAS_TIMER, deadline);
+    timer_queue[deadline].push_back({v, s});
+  }
+  // cancelSuspicionTimeoutTask (:797-803)
+  void cancel_timer(uint32_t v, uint32_t s) { m[v].row[s] &= ~B_HAS_TIMER; }
+
+  // ------------------------------------------------------------------------- metadata fetch
+  // MetadataStoreImpl.fetchMetadata (:146-185) round trip + onMetadataRequest (:201-240).
+  bool fetch_ok(uint32_t v, uint32_t s, uint32_t phase) {
+    uint32_t f = m[v].fetch_ctr++;
+    uint32_t w1 = draw(v, SWIM_STREAM_FETCH_REQ, phase, f);
+    uint32_t w2 = draw(v, SWIM_STREAM_FETCH_RESP, phase, f);
+    st.fetches++;
+    bool ok = !out_fail(v, s, w1) && in_pass(s, v) && !out_fail(s, v, w2) && in_pass(v, s);
+    if (ok) st.fetch_ok++;
+    return ok;
+  }
+
+  // ------------------------------------------------------------------------- updateMembership
+  // MembershipProtocolImpl.updateMembership (:569-664).  ALIVE admissions whose metadata fetch
+  // succeeds are appended to `pending` and applied by apply_alive at the caller's flush point.
+  void update_membership(uint32_t v, const Record& r1, Reason reason, uint32_t phase,
+                         std::vector<PendingAlive>& pending) {
+    Member& mv = m[v];
+    const uint32_t s = r1.member;
+    uint64_t& c = mv.row[s];
+    // (namespace filter :575-586: every simulated member shares one namespace)
+    const bool present = c_has(c, B_IN_TABLE);
+    Record r0v{s, c_status(c), c_inc(c)};
+    const Record* r0 = present ? &r0v : nullptr;
+    const bool r0_leaving = present && r0v.status == SWIM_LEAVING;
+    if (!r0_leaving && !is_overrides(r1, r0)) return;  // :593-602
+
+    if (s == v) {  // onSelfMemberDetected (:686-708)
+      int32_t cur = std::max(r0v.inc, r1.inc);
+      Record r2{v, r0v.status, cur + 1};
+      c = c_with_record(c, r2.status, r2.inc);
+      spread_gossip(v, r2);
+      return;
+    }
+    if (r1.status == SWIM_LEAVING) {  // onLeavingDetected (:710-733)
+      if (!present) { mv.table_size++; }
+      c = c_with_record(c | B_IN_TABLE, SWIM_LEAVING, r1.inc);
+      if (present && (r0v.status == SWIM_ALIVE ||
+                      (r0v.status == SWIM_SUSPECT && c_has(c, B_ALIVE_EMITTED)))) {
+        publish_event(v, s, SWIM_EV_LEAVING, phase, ev_minor_for(v, phase, s));
+      }
+      if (!present || r0v.status != SWIM_LEAVING) {
+        schedule_timer(v, s);
+        spread_gossip(v, r1);
+      }
+      return;
+    }
+    if (r1.status == SWIM_DEAD) {  // onDeadMemberDetected (:740-767)
+      cancel_timer(v, s);
+      if (!c_has(c, B_IN_MEMBERS)) return;
+      c = 0;
+      mv.table_size--;
+      mv.members_size--;
+      publish_event(v, s, SWIM_EV_REMOVED, phase, ev_minor_for(v, phase, s));
+      return;
+    }
+    if (r1.status == SWIM_SUSPECT) {  // :621-628
+      if (!r0_leaving) {
+        if (!present) mv.table_size++;  // unreachable: SUSPECT never overrides a missing row
+        c = c_with_record(c | B_IN_TABLE, SWIM_SUSPECT, r1.inc);
+      }
+      schedule_timer(v, s);
+      if (reason != MEMBERSHIP_GOSSIP && reason != INITIAL_SYNC) spread_gossip(v, r1);
+      return;
+    }
+    // ALIVE (:630-660)
+    if (r0_leaving) {  // onAliveAfterLeaving (:666-684)
+      if (!c_has(c, B_IN_MEMBERS)) { c |= B_IN_MEMBERS; mv.members_size++; }
+      if (!c_has(c, B_ALIVE_EMITTED)) {
+        c |= B_ALIVE_EMITTED;
+        publish_event(v, s, SWIM_EV_ADDED, phase, ev_minor_for(v, phase, s));
+        publish_event(v, s, SWIM_EV_LEAVING, phase, ev_minor_for(v, phase, s));
+      }
+      return;
+    }
+    if (!present || r0v.inc < r1.inc) {
+      if (fetch_ok(v, s, phase)) pending.push_back(PendingAlive{r1});
+    }
+  }
+
+  // doOnSuccess of the fetch (:648-656) + onAliveMemberDetected (:769-795)
+  void apply_alive(uint32_t v, const Record& r1, Reason reason, uint32_t phase) {
+    Member& mv = m[v];
+    const uint32_t s = r1.member;
+    cancel_timer(v, s);
+    if (reason != MEMBERSHIP_GOSSIP && reason != INITIAL_SYNC) spread_gossip(v, r1);
+    uint64_t& c = mv.row[s];
+    c |= B_HAS_METADATA;  // metadataStore.updateMetadata
+    const bool exists = c_has(c, B_IN_MEMBERS);
+    if (!c_has(c, B_IN_TABLE)) mv.table_size++;
+    if (!exists) mv.members_size++;
+    c = c_with_record(c | B_IN_TABLE | B_IN_MEMBERS, SWIM_ALIVE, r1.inc);
+    if (!exists) {
+      // metadata never changes in the simulation, so an existing member yields no UPDATED
+      publish_event(v, s, SWIM_EV_ADDED, phase, ev_minor_for(v, phase, s));
+      c |= B_ALIVE_EMITTED;
+    }
+  }
+
+  void flush_pending(uint32_t v, std::vector<PendingAlive>& pending, Reason reason, uint32_t phase) {
+    for (auto& p : pending) apply_alive(v, p.r1, reason, phase);
+    pending.clear();
+  }
+
+  // ------------------------------------------------------------------------- phase A: timers
+  // onSuspicionTimeout (:825-834), due (viewer, subject) pairs in ascending order.
+  void phase_timers() {
+    auto it = timer_queue.find(T);
+    if (it == timer_queue.end()) return;
+    auto due = std::move(it->second);
+    timer_queue.erase(it);
+    std::sort(due.begin(), due.end());
+    due.erase(std::unique(due.begin(), due.end()), due.end());
+    std::vector<PendingAlive> none;
+    for (auto& vs : due) {
+      uint32_t v = vs.first, s = vs.second;
+      if (!m[v].up) continue;
+      uint64_t& c = m[v].row[s];
+      if (!c_has(c, B_HAS_TIMER) || c_deadline(c) != (uint32_t)(T & SWIM_DEADLINE_MASK)) continue;
+      c &= ~B_HAS_TIMER;
+      st.timers_fired++;
+      if (c_has(c, B_IN_TABLE)) {
+        Record dead{s, SWIM_DEAD, c_inc(c)};
+        update_membership(v, dead, SUSPICION_TIMEOUT, SWIM_PHASE_TIMERS, none);
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------------- phase B: FD
+  // publishPingResult (:377-380) -> MembershipProtocolImpl.onFailureDetectorEvent (:418-449)
+  void publish_fd(uint32_t v, uint32_t t, uint32_t status) {
+    st.fd_events++;
+    if (cfg.record_fd_events)
+      emit(v, t, SWIM_EV_FD_ALIVE + (status == SWIM_ALIVE ? 0 : status == SWIM_SUSPECT ? 1 : 2),
+           SWIM_PHASE_FD, next_minor(v));
+    uint64_t c = m[v].row[t];
+    if (!c_has(c, B_IN_TABLE)) return;
+    if (c_status(c) == status) return;
+    if (status == SWIM_ALIVE) {
+      m[v].fd_sync.push_back(t);
+      return;
+    }
+    std::vector<PendingAlive> none;
+    update_membership(v, Record{t, status, c_inc(c)}, FD_EVENT, SWIM_PHASE_FD, none);
+  }
+
+  // Collections.shuffle (for i = size; i > 1; i--) swap(i-1, nextInt(i))
+  void shuffle(uint32_t v, std::vector<uint32_t>& list, uint32_t stream) {
+    for (uint32_t i = (uint32_t)list.size(); i > 1; --i) {
+      uint32_t j = next_int(draw(v, stream, 0, i), i);
+      std::swap(list[i - 1], list[j]);
+    }
+  }
+
+  // selectPingMember (:352-361)
+  uint32_t select_ping_member(uint32_t v) {
+    auto& pm = m[v].ping_members;
+    if (pm.empty()) return NONE;
+    if (m[v].ping_index >= pm.size()) {
+      m[v].ping_index = 0;
+      shuffle(v, pm, SWIM_STREAM_FD_SHUFFLE);
+    }
+    return pm[m[v].ping_index++];
+  }
+
+  // selectPingReqMembers (:363-375): uniformly random ordered k-subset of pingMembers \ {target},
+  // drawn by a forward partial Fisher-Yates over the candidate positions.
+  std::vector<uint32_t> select_ping_req_members(uint32_t v, uint32_t t) {
+    std::vector<uint32_t> out;
+    const int32_t k = cfg.ping_req_members;
+    if (k <= 0) return out;
+    const auto& pm = m[v].ping_members;
+    int64_t pos = -1;
+    for (size_t i = 0; i < pm.size(); ++i)
+      if (pm[i] == t) { pos = (int64_t)i; break; }
+    const uint32_t cnt = (uint32_t)pm.size() - (pos >= 0 ? 1u : 0u);
+    if (cnt == 0) return out;
+    const uint32_t r = std::min<uint32_t>((uint32_t)k, cnt);
+    std::vector<std::pair<uint32_t, uint32_t>> sw;  // sparse position -> value
+    auto get = [&](uint32_t p) {
+      for (auto& e : sw) if (e.first == p) return e.second;
+      return p;
+    };
+    auto set = [&](uint32_t p, uint32_t val) {
+      for (auto& e : sw) if (e.first == p) { e.second = val; return; }
+      sw.push_back({p, val});
+    };
+    for (uint32_t i = 0; i < r; ++i) {
+      uint32_t j = i + next_int(draw(v, SWIM_STREAM_RELAY_SELECT, i, 0), cnt - i);
+      uint32_t vi = get(i), vj = get(j);
+      set(i, vj);
+      set(j, vi);
+      uint32_t x = vj;
+      out.push_back((pos >= 0 && (int64_t)x >= pos) ? pm[x + 1] : pm[x]);
+    }
+    return out;
+  }
+
+  // doPing's error branch (:153-170) + doPingReq (:173-210).  Every pending relay request shares
+  // the ping's correlation id, so the first relayed ack that reaches the issuer completes all of
+  // them (TransportImpl.requestResponse :214-238 filters listen() by cid only).
+  void ping_req(uint32_t v, uint32_t t) {
+    std::vector<uint32_t> relays = select_ping_req_members(v, t);
+    if (relays.empty()) {  // timeLeft <= 0 is excluded by config validation
+      publish_fd(v, t, SWIM_SUSPECT);
+      return;
+    }
+    st.ping_reqs++;
+    std::vector<uint32_t> pending;
+    for (uint32_t j = 0; j < relays.size(); ++j) {
+      if (out_fail(v, relays[j], draw(v, SWIM_STREAM_PINGREQ_OUT, j, 0)))
+        publish_fd(v, t, SWIM_SUSPECT);  // immediate outbound error
+      else
+        pending.push_back(j);
+    }
+    if (pending.empty()) return;
+    int64_t arrived = -1;
+    for (uint32_t j : pending) {
+      uint32_t r = relays[j];
+      if (in_pass(r, v) && !out_fail(r, t, draw(v, SWIM_STREAM_TRANSIT_PING_OUT, j, 0)) &&
+          in_pass(t, r) && !out_fail(t, r, draw(v, SWIM_STREAM_TRANSIT_ACK_OUT, j, 0)) &&
+          in_pass(r, t) && !out_fail(r, v, draw(v, SWIM_STREAM_RELAY_ACK_OUT, j, 0))) {
+        arrived = j;
+        break;
+      }
+    }
+    if (arrived >= 0 && in_pass(v, relays[(size_t)arrived])) {
+      for (size_t i = 0; i < pending.size(); ++i) publish_fd(v, t, SWIM_ALIVE);
+    } else {
+      Member& mv = m[v];
+      mv.relay_due = T + relay_ticks;
+      mv.relay_target = t;
+      mv.relay_pending = (uint32_t)pending.size();
+    }
+  }
+
+  bool fd_due(const Member& mv) const {
+    return mv.up && (int64_t)T > mv.fd_start && ((int64_t)T - mv.fd_start) % P == 0;
+  }
+  bool gossip_due(const Member& mv) const {
+    return mv.up && (int64_t)T > mv.g_start && ((int64_t)T - mv.g_start) % G == 0;
+  }
+  bool sync_due(const Member& mv) const {
+    return mv.up && mv.sync_on && (int64_t)T > mv.sync_start && ((int64_t)T - mv.sync_start) % S == 0;
+  }
+
+  void phase_fd() {
+    for (uint32_t v = 0; v < n; ++v) {
+      Member& mv = m[v];
+      if (!mv.up) continue;
+      mv.ev_minor = 0;
+      if (mv.relay_due == T) {  // relay timeouts (:200-209)
+        uint32_t t = mv.relay_target, k = mv.relay_pending;
+        mv.relay_due = 0;
+        for (uint32_t i = 0; i < k; ++i) publish_fd(v, t, SWIM_SUSPECT);
+      }
+      if (mv.ack_due == T) {  // pingTimeout elapsed (:153-170)
+        uint32_t t = mv.ack_target;
+        mv.ack_due = 0;
+        ping_req(v, t);
+      }
+      if (fd_due(mv)) {  // doPing (:126-171)
+        mv.fd_period++;
+        uint32_t t = select_ping_member(v);
+        if (t == NONE) continue;
+        st.pings++;
+        if (out_fail(v, t, draw(v, SWIM_STREAM_PING_OUT, 0, 0))) {
+          ping_req(v, t);  // outbound error -> ping-req right away
+        } else if (in_pass(t, v) && !out_fail(t, v, draw(v, SWIM_STREAM_ACK_OUT, 0, 0)) && in_pass(v, t)) {
+          publish_fd(v, t, SWIM_ALIVE);  // onPing answers DEST_OK (:227-259)
+        } else {
+          mv.ack_due = T + to_ticks;
+          mv.ack_target = t;
+        }
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------------- phase C: gossip
+  struct GMsg {
+    uint32_t to, from, pos;
+    GossipState g;
+  };
+
+  // selectGossipMembers (GossipProtocolImpl.java:322-343)
+  std::vector<uint32_t> select_gossip_members(uint32_t v) {
+    Member& mv = m[v];
+    const uint32_t F = (uint32_t)cfg.gossip_fanout;
+    if (mv.remote.size() < F) return mv.remote;
+    if (mv.remote_index < 0 || (uint32_t)mv.remote_index + F > mv.remote.size()) {
+      shuffle(v, mv.remote, SWIM_STREAM_GOSSIP_SHUFFLE);
+      mv.remote_index = 0;
+    }
+    std::vector<uint32_t> sel(mv.remote.begin() + mv.remote_index, mv.remote.begin() + mv.remote_index + F);
+    mv.remote_index += (int32_t)F;
+    return sel;
+  }
+
+  void phase_gossip() {
+    std::vector<uint32_t> due;
+    for (uint32_t v = 0; v < n; ++v)
+      if (gossip_due(m[v])) due.push_back(v);
+    if (due.empty()) return;
+    // C1: period++ and checkGossipSegmentation (:141-146, :217-236)
+    for (uint32_t v : due) {
+      Member& mv = m[v];
+      mv.period_used = mv.g_period++;
+      for (auto& kv : mv.collectors)
+        if (kv.second.size() > (size_t)cfg.gossip_segmentation_threshold) kv.second.clear();
+    }
+    // C2: spread to selected members, sweep, complete futures (:148-183)
+    std::vector<GMsg> msgs;
+    for (uint32_t v : due) {
+      Member& mv = m[v];
+      if (mv.gossips.empty()) continue;
+      const uint64_t period = mv.period_used;
+      std::vector<uint32_t> targets = select_gossip_members(v);
+      const int32_t size1 = (int32_t)mv.remote.size() + 1;
+      const uint64_t spread = (uint64_t)swim_gossip_periods_to_spread(cfg.gossip_repeat_mult, size1);
+      const uint64_t sweep = (uint64_t)swim_gossip_periods_to_sweep(cfg.gossip_repeat_mult, size1);
+      for (uint32_t j = 0; j < targets.size(); ++j) {
+        uint32_t t = targets[j];
+        for (uint32_t p = 0; p < mv.gossips.size(); ++p) {  // selectGossipsToSend (:311-320)
+          const GossipState& g = mv.gossips[p];
+          if (!(g.infection_period + spread >= period)) continue;
+          if (g.is_infected(t)) continue;
+          st.gossip_messages++;
+          if (out_fail(v, t, draw(v, SWIM_STREAM_GOSSIP_OUT, j, p))) continue;
+          if (!in_pass(t, v)) continue;
+          msgs.push_back(GMsg{t, v, p, g});
+        }
+      }
+      // sweep (:158-164, :350-358)
+      std::vector<GossipState> keep;
+      keep.reserve(mv.gossips.size());
+      for (auto& g : mv.gossips)
+        if (!(period > g.infection_period + sweep)) keep.push_back(std::move(g));
+      mv.gossips.swap(keep);
+      // futures (:167-180, :360-368): only the graceful-leave future has an observer here
+      if (mv.leave_pending) {
+        for (auto& g : mv.gossips)
+          if (period > g.infection_period + spread && g.gossiper == mv.leave_gossiper && g.seq == mv.leave_seq)
+            mv.leave_done = true;
+      }
+    }
+    if (msgs.empty()) return;
+    // C3: onGossipReq at every receiver, canonical order (sender, slab position) (:201-215)
+    std::stable_sort(msgs.begin(), msgs.end(), [](const GMsg& a, const GMsg& b) {
+      if (a.to != b.to) return a.to < b.to;
+      if (a.from != b.from) return a.from < b.from;
+      return a.pos < b.pos;
+    });
+    uint32_t cur = NONE;
+    std::vector<PendingAlive> pending;
+    for (auto& msg : msgs) {
+      const uint32_t r = msg.to;
+      Member& mr = m[r];
+      if (r != cur) {
+        cur = r;
+        mr.ev_minor = 0;
+        mr.fetch_ctr = 0;
+      }
+      if (!mr.up) continue;
+      const GossipState& g = msg.g;
+      if (!mr.collectors[g.gossiper].add((int64_t)g.seq)) continue;
+      st.gossip_accepted++;
+      GossipState* state = nullptr;
+      for (auto& x : mr.gossips)
+        if (x.gossiper == g.gossiper && x.seq == g.seq) { state = &x; break; }
+      if (state == nullptr) {
+        GossipState ns;
+        ns.gossiper = g.gossiper;
+        ns.seq = g.seq;
+        ns.rec = g.rec;
+        ns.infection_period = mr.g_period;
+        ns.infected.push_back(msg.from);
+        mr.gossips.push_back(ns);
+        // onMembershipGossip (:452-459)
+        update_membership(r, g.rec, MEMBERSHIP_GOSSIP, SWIM_PHASE_GOSSIP, pending);
+        flush_pending(r, pending, MEMBERSHIP_GOSSIP, SWIM_PHASE_GOSSIP);
+      } else {
+        state->add_infected(msg.from);
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------------- phase D: SYNC
+  // selectSyncAddress (:461-472): uniform over seeds U otherMembers, by seeded rejection sampling.
+  uint32_t select_sync_address(uint32_t v) {
+    const Member& mv = m[v];
+    uint32_t count = mv.members_size - 1;
+    for (uint32_t s : seeds)
+      if (s != v && !c_has(mv.row[s], B_IN_MEMBERS)) count++;
+    if (count == 0) return NONE;
+    auto in_set = [&](uint32_t x) { return x != v && (c_has(mv.row[x], B_IN_MEMBERS) || is_seed[x]); };
+    for (uint32_t i = 0; i < SWIM_SYNC_SELECT_ATTEMPTS; ++i) {
+      uint32_t x = next_int(draw(v, SWIM_STREAM_SYNC_SELECT, 0, i), n);
+      if (in_set(x)) return x;
+    }
+    uint32_t k = next_int(draw(v, SWIM_STREAM_SYNC_SELECT, 1, 0), count);
+    for (uint32_t x = 0; x < n; ++x)
+      if (in_set(x) && k-- == 0) return x;
+    return NONE;
+  }
+
+  // syncMembership (:491-509): records in ascending subject order; fetch completions afterwards.
+  void sync_membership(uint32_t v, const std::vector<uint64_t>& content, Reason reason, uint32_t phase) {
+    std::vector<PendingAlive> pending;
+    for (uint32_t x = 0; x < n; ++x) {
+      uint64_t c = content[x];
+      if (!c_has(c, B_IN_TABLE)) continue;
+      st.sync_records++;
+      update_membership(v, Record{x, c_status(c), c_inc(c)}, reason, phase, pending);
+    }
+    flush_pending(v, pending, reason, phase);
+  }
+
+  void phase_sync() {
+    std::vector<SyncReq> reqs;
+    for (uint32_t v = 0; v < n; ++v) {
+      Member& mv = m[v];
+      if (!mv.up) { mv.fd_sync.clear(); continue; }
+      uint32_t k = 0;
+      if (sync_due(mv)) {  // doSync (:339-357)
+        uint32_t t = select_sync_address(v);
+        if (t != NONE) reqs.push_back(SyncReq{v, t, k++, false, false, false, false});
+      }
+      for (uint32_t t : mv.fd_sync) reqs.push_back(SyncReq{v, t, k++, false, false, false, false});
+      mv.fd_sync.clear();
+      if (mv.join_now) {  // start0 initial sync to every seed (:250-291)
+        for (uint32_t s : seeds)
+          if (s != v) reqs.push_back(SyncReq{v, s, k++, true, false, false, false});
+      }
+    }
+    if (reqs.empty()) {
+      finish_joins(reqs);
+      return;
+    }
+    // request content: the sender's table when the SYNC is prepared (:485-489)
+    std::map<uint32_t, std::vector<uint64_t>> content;
+    for (auto& q : reqs)
+      if (!content.count(q.from)) content[q.from] = m[q.from].row;
+    std::vector<size_t> delivered;
+    for (size_t i = 0; i < reqs.size(); ++i) {
+      SyncReq& q = reqs[i];
+      st.syncs++;
+      if (out_fail(q.from, q.to, draw(q.from, SWIM_STREAM_SYNC_OUT, q.ordinal, 0))) { q.outfail = true; continue; }
+      if (!in_pass(q.to, q.from)) continue;
+      q.delivered = true;
+      delivered.push_back(i);
+    }
+    std::stable_sort(delivered.begin(), delivered.end(), [&](size_t a, size_t b) {
+      if (reqs[a].to != reqs[b].to) return reqs[a].to < reqs[b].to;
+      if (reqs[a].from != reqs[b].from) return reqs[a].from < reqs[b].from;
+      return reqs[a].ordinal < reqs[b].ordinal;
+    });
+    // D1: onSync at each receiver (:394-415)
+    uint32_t cur = NONE;
+    for (size_t i : delivered) {
+      SyncReq& q = reqs[i];
+      if (q.to != cur) {
+        cur = q.to;
+        m[cur].ev_minor = 0;
+        m[cur].fetch_ctr = 0;
+      }
+      sync_membership(q.to, content[q.from], SYNC, SWIM_PHASE_SYNC);
+    }
+    // SYNC_ACK content: the receiver's table once all its requests are merged
+    std::map<uint32_t, std::vector<uint64_t>> ack_content;
+    struct Ack { uint32_t to, from, rank; bool initial; };
+    std::vector<Ack> acks;
+    cur = NONE;
+    uint32_t rank = 0;
+    for (size_t i : delivered) {
+      SyncReq& q = reqs[i];
+      if (q.to != cur) { cur = q.to; rank = 0; ack_content[cur] = m[cur].row; }
+      uint32_t qr = rank++;
+      if (out_fail(q.to, q.from, draw(q.to, SWIM_STREAM_SYNCACK_OUT, qr, 0))) continue;
+      if (!in_pass(q.from, q.to)) continue;
+      q.acked = true;
+      acks.push_back(Ack{q.from, q.to, qr, q.initial});
+    }
+    std::stable_sort(acks.begin(), acks.end(), [](const Ack& a, const Ack& b) {
+      if (a.to != b.to) return a.to < b.to;
+      if (a.from != b.from) return a.from < b.from;
+      return a.rank < b.rank;
+    });
+    // D2: SYNC_ACK merge at the original sender (:363-391), INITIAL_SYNC for start0's requests
+    cur = NONE;
+    for (auto& a : acks) {
+      if (a.to != cur) {
+        cur = a.to;
+        m[cur].ev_minor = 0;
+        m[cur].fetch_ctr = 0;
+      }
+      st.sync_acks++;
+      sync_membership(a.to, ack_content[a.from], a.initial ? INITIAL_SYNC : SYNC, SWIM_PHASE_SYNCACK);
+    }
+    finish_joins(reqs);
+  }
+
+  // start0's doFinally (:285-289): periodic sync starts once every seed answered or failed fast,
+  // else after syncTimeout.
+  void finish_joins(const std::vector<SyncReq>& reqs) {
+    for (uint32_t v = 0; v < n; ++v) {
+      Member& mv = m[v];
+      if (!mv.join_now) continue;
+      bool complete = true;
+      for (auto& q : reqs)
+        if (q.from == v && q.initial && !(q.outfail || q.acked)) complete = false;
+      mv.sync_on = true;
+      mv.sync_start = (int64_t)T + (complete ? 0 : (int64_t)sync_to_ticks);
+      mv.join_now = false;
+    }
+  }
+
+  // ------------------------------------------------------------------------- tick
+  void start_joins() {
+    for (uint32_t v = 0; v < n; ++v) {
+      Member& mv = m[v];
+      if (!mv.join_pending) continue;
+      mv.join_pending = false;
+      mv.up = true;
+      mv.joined = true;
+      mv.join_now = true;
+      mv.fd_start = (int64_t)T;
+      mv.g_start = (int64_t)T;
+      mv.row[v] = B_IN_TABLE | B_IN_MEMBERS;  // ALIVE inc 0 (MembershipProtocolImpl :146-149)
+      mv.table_size = 1;
+      mv.members_size = 1;
+    }
+  }
+
+  void step_tick() {
+    T += 1;
+    st.ticks++;
+    start_joins();
+    phase_timers();
+    phase_fd();
+    phase_gossip();
+    phase_sync();
+    for (uint32_t v = 0; v < n; ++v) {  // graceful leave completes: dispose + transport.stop
+      if (m[v].leave_done) {
+        m[v].leave_done = false;
+        m[v].leave_pending = false;
+        m[v].up = false;
+      }
+    }
+  }
+};
+
+// =============================================================================== C ABI
+extern "C" {
+
+int32_t swim_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  if (!ctr || !key || !out) return SWIM_EINVAL;
+  philox4x32_10(ctr, key, out);
+  return SWIM_OK;
+}
+
+int32_t swim_kat_overrides(const int32_t* cases, uint32_t n, uint8_t* out) {
+  if (n && (!cases || !out)) return SWIM_EINVAL;
+  for (uint32_t i = 0; i < n; ++i) {
+    const int32_t* k = cases + 5 * i;
+    Record r1{0, (uint32_t)k[0], k[1]};
+    Record r0{0, (uint32_t)k[3], k[4]};
+    out[i] = is_overrides(r1, k[2] ? &r0 : nullptr) ? 1 : 0;
+  }
+  return SWIM_OK;
+}
+
+int32_t swim_kat_collector(const uint8_t* kinds, const int64_t* values, uint32_t n, int64_t* results) {
+  if (n && (!kinds || !values || !results)) return SWIM_EINVAL;
+  SeqCollector c;
+  for (uint32_t i = 0; i < n; ++i) {
+    switch (kinds[i]) {
+      case 0: results[i] = c.add(values[i]) ? 1 : 0; break;
+      case 1: results[i] = c.contains(values[i]) ? 1 : 0; break;
+      case 2: results[i] = (int64_t)c.size(); break;
+      case 3: c.clear(); results[i] = 0; break;
+      default: return SWIM_EINVAL;
+    }
+  }
+  return SWIM_OK;
+}
+
+int32_t swim_ceil_log2(int32_t num) {  // ClusterMath.java:133-135 (32 - numberOfLeadingZeros)
+  uint32_t u = (uint32_t)num;
+  int32_t nlz = 32;
+  while (u) { u >>= 1; nlz--; }
+  return 32 - nlz;
+}
+int32_t swim_gossip_periods_to_spread(int32_t repeat_mult, int32_t cluster_size) {
+  return repeat_mult * swim_ceil_log2(cluster_size);
+}
+int32_t swim_gossip_periods_to_sweep(int32_t repeat_mult, int32_t cluster_size) {
+  return 2 * (swim_gossip_periods_to_spread(repeat_mult, cluster_size) + 1);
+}
+int64_t swim_suspicion_timeout(int32_t suspicion_mult, int32_t cluster_size, int64_t ping_interval) {
+  return (int64_t)(suspicion_mult * swim_ceil_log2(cluster_size)) * ping_interval;
+}
+
+int32_t swim_config_default(swim_config* c, int32_t preset) {
+  if (!c) return SWIM_EINVAL;
+  std::memset(c, 0, sizeof(*c));
+  c->ping_interval = 1000;
+  c->ping_timeout = 500;
+  c->ping_req_members = 3;
+  c->gossip_interval = 200;
+  c->gossip_fanout = 3;
+  c->gossip_repeat_mult = 3;
+  c->gossip_segmentation_threshold = 1000;
+  c->sync_interval = 30000;
+  c->sync_timeout = 3000;
+  c->suspicion_mult = 5;
+  c->removed_members_history_size = 42;
+  c->metadata_timeout = 3000;
+  c->sync_stagger = 1;
+  if (preset == 1) {  // WAN
+    c->ping_timeout = 3000;
+    c->ping_interval = 5000;
+    c->gossip_fanout = 4;
+    c->suspicion_mult = 6;
+    c->sync_interval = 60000;
+    c->metadata_timeout = 10000;
+  } else if (preset == 2) {  // Local
+    c->ping_timeout = 200;
+    c->ping_interval = 1000;
+    c->ping_req_members = 1;
+    c->gossip_repeat_mult = 2;
+    c->gossip_interval = 100;
+    c->suspicion_mult = 3;
+    c->sync_interval = 15000;
+    c->metadata_timeout = 1000;
+  } else if (preset != 0) {
+    return SWIM_EINVAL;
+  }
+  return SWIM_OK;
+}
+
+static uint32_t gcd_u(uint32_t a, uint32_t b) {
+  while (b) { uint32_t t = a % b; a = b; b = t; }
+  return a;
+}
+
+int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initial, uint64_t seed,
+                    swim_engine** out) {
+  if (!cfg || !out || capacity == 0 || n_initial > capacity || capacity > (1u << 24)) return SWIM_EINVAL;
+  const swim_config& c = *cfg;
+  if (c.ping_interval <= 0 || c.ping_timeout <= 0 || c.ping_timeout >= c.ping_interval ||
+      c.gossip_interval <= 0 || c.sync_interval <= 0 || c.sync_timeout <= 0 || c.metadata_timeout <= 0 ||
+      c.suspicion_mult <= 0 || c.gossip_fanout <= 0 || c.gossip_fanout > 16 || c.ping_req_members > 16 ||
+      c.gossip_repeat_mult <= 0)
+    return SWIM_EINVAL;
+  uint32_t tick = (uint32_t)c.tick_ms;
+  if (tick == 0) {
+    tick = gcd_u((uint32_t)c.ping_interval, (uint32_t)c.ping_timeout);
+    tick = gcd_u(tick, (uint32_t)c.gossip_interval);
+    tick = gcd_u(tick, (uint32_t)c.sync_interval);
+    tick = gcd_u(tick, (uint32_t)c.sync_timeout);
+  }
+  if (c.ping_interval % tick || c.ping_timeout % tick || c.gossip_interval % tick || c.sync_interval % tick ||
+      c.sync_timeout % tick)
+    return SWIM_EINVAL;
+  swim_engine* e = new (std::nothrow) swim_engine();
+  if (!e) return SWIM_ENOMEM;
+  e->cfg = c;
+  e->n = capacity;
+  e->seed = seed;
+  e->key[0] = (uint32_t)seed;
+  e->key[1] = (uint32_t)(seed >> 32);
+  e->tick_ms = tick;
+  e->P = (uint32_t)c.ping_interval / tick;
+  e->to_ticks = (uint32_t)c.ping_timeout / tick;
+  e->relay_ticks = e->P - e->to_ticks;
+  e->G = (uint32_t)c.gossip_interval / tick;
+  e->S = (uint32_t)c.sync_interval / tick;
+  e->sync_to_ticks = (uint32_t)c.sync_timeout / tick;
+  try {
+    e->m.resize(capacity);
+    e->is_seed.assign(capacity, 0);
+    e->default_loss.assign(capacity, 0);
+    e->default_inbound.assign(capacity, 1);
+    e->group.assign(capacity, 0);
+    for (auto& mm : e->m) mm.row.assign(capacity, 0);
+  } catch (...) {
+    delete e;
+    return SWIM_ENOMEM;
+  }
+  // Converged initial cluster.  Initialisation may use threads; ticks never do.
+  const uint64_t conv = B_IN_TABLE | B_IN_MEMBERS | B_ALIVE_EMITTED | B_HAS_METADATA;
+  auto init_range = [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t v = lo; v < hi; ++v) {
+      Member& mv = e->m[v];
+      mv.up = mv.joined = true;
+      for (uint32_t s = 0; s < n_initial; ++s) mv.row[s] = conv;
+      mv.row[v] = B_IN_TABLE | B_IN_MEMBERS;  // self: ALIVE inc 0
+      mv.table_size = n_initial;
+      mv.members_size = n_initial;
+      mv.ping_members.reserve(n_initial ? n_initial - 1 : 0);
+      for (uint32_t s = 0; s < n_initial; ++s)
+        if (s != v) mv.ping_members.push_back(s);
+      mv.remote = mv.ping_members;
+      for (uint32_t i = (uint32_t)mv.ping_members.size(); i > 1; --i) {
+        uint32_t j = next_int(e->draw(v, SWIM_STREAM_INIT_PING, 0, i, 0), i);
+        std::swap(mv.ping_members[i - 1], mv.ping_members[j]);
+      }
+      for (uint32_t i = (uint32_t)mv.remote.size(); i > 1; --i) {
+        uint32_t j = next_int(e->draw(v, SWIM_STREAM_INIT_REMOTE, 0, i, 0), i);
+        std::swap(mv.remote[i - 1], mv.remote[j]);
+      }
+      mv.remote_index = 0;
+      mv.sync_on = true;
+      mv.sync_start = c.sync_stagger ? -(int64_t)next_int(e->draw(v, SWIM_STREAM_INIT_SYNC_PHASE, 0, 0, 0), e->S) : 0;
+    }
+  };
+  unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (n_initial < 4096) hw = 1;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < hw; ++t) {
+    uint32_t lo = (uint32_t)((uint64_t)n_initial * t / hw), hi = (uint32_t)((uint64_t)n_initial * (t + 1) / hw);
+    if (hw == 1) init_range(lo, hi); else th.emplace_back(init_range, lo, hi);
+  }
+  for (auto& x : th) x.join();
+  *out = e;
+  return SWIM_OK;
+}
+
+int32_t swim_destroy(swim_engine* e) {
+  delete e;
+  return SWIM_OK;
+}
+
+int32_t swim_step_ticks(swim_engine* e, uint32_t ticks) {
+  if (!e) return SWIM_EINVAL;
+  for (uint32_t i = 0; i < ticks; ++i) e->step_tick();
+  return SWIM_OK;
+}
+
+int32_t swim_step(swim_engine* e, uint32_t periods) {
+  if (!e) return SWIM_EINVAL;
+  return swim_step_ticks(e, periods * e->P);
+}
+
+int32_t swim_now(const swim_engine* e, uint64_t* tick, uint32_t* tick_ms, uint32_t* tpp) {
+  if (!e) return SWIM_EINVAL;
+  if (tick) *tick = e->T;
+  if (tick_ms) *tick_ms = e->tick_ms;
+  if (tpp) *tpp = e->P;
+  return SWIM_OK;
+}
+
+int32_t swim_set_seeds(swim_engine* e, const uint32_t* seeds, uint32_t n_seeds) {
+  if (!e || (n_seeds && !seeds)) return SWIM_EINVAL;
+  std::vector<uint32_t> s;
+  for (uint32_t i = 0; i < n_seeds; ++i) {
+    if (seeds[i] >= e->n) return SWIM_EINVAL;
+    if (std::find(s.begin(), s.end(), seeds[i]) == s.end()) s.push_back(seeds[i]);  // LinkedHashSet
+  }
+  e->seeds = s;
+  std::fill(e->is_seed.begin(), e->is_seed.end(), 0);
+  for (uint32_t x : s) e->is_seed[x] = 1;
+  return SWIM_OK;
+}
+
+int32_t swim_kill(swim_engine* e, uint32_t mm) {
+  if (!e || mm >= e->n) return SWIM_EINVAL;
+  if (!e->m[mm].up) return SWIM_ESTATE;
+  e->m[mm].up = false;
+  e->m[mm].leave_pending = false;
+  return SWIM_OK;
+}
+
+int32_t swim_leave(swim_engine* e, uint32_t v, int32_t stop_after) {
+  if (!e || v >= e->n) return SWIM_EINVAL;
+  Member& mv = e->m[v];
+  if (!mv.up) return SWIM_ESTATE;
+  // leaveCluster (:233-242)
+  uint64_t& c = mv.row[v];
+  Record r{v, SWIM_LEAVING, c_inc(c) + 1};
+  c = c_with_record(c, r.status, r.inc);
+  e->spread_gossip(v, r);
+  if (stop_after) {
+    mv.leave_pending = true;
+    mv.leave_gossiper = v;
+    mv.leave_seq = mv.g_counter - 1;
+  }
+  return SWIM_OK;
+}
+
+int32_t swim_join(swim_engine* e, uint32_t v) {
+  if (!e || v >= e->n) return SWIM_EINVAL;
+  Member& mv = e->m[v];
+  if (mv.joined || mv.up || mv.join_pending) return SWIM_ESTATE;
+  mv.join_pending = true;
+  return SWIM_OK;
+}
+
+int32_t swim_set_default_loss(swim_engine* e, uint32_t mm, int32_t pct) {
+  if (!e || pct < 0 || pct > 100) return SWIM_EINVAL;
+  if (mm == 0xffffffffu) { std::fill(e->default_loss.begin(), e->default_loss.end(), pct); return SWIM_OK; }
+  if (mm >= e->n) return SWIM_EINVAL;
+  e->default_loss[mm] = pct;
+  return SWIM_OK;
+}
+
+int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t pct) {
+  if (!e || src >= e->n || dst >= e->n || pct > 100) return SWIM_EINVAL;
+  if (pct < 0) e->link_loss.erase({src, dst}); else e->link_loss[{src, dst}] = pct;
+  return SWIM_OK;
+}
+
+int32_t swim_set_link_inbound(swim_engine* e, uint32_t dst, uint32_t src, int32_t pass) {
+  if (!e || src >= e->n || dst >= e->n) return SWIM_EINVAL;
+  if (pass < 0) e->link_inbound.erase({dst, src}); else e->link_inbound[{dst, src}] = pass ? 1 : 0;
+  return SWIM_OK;
+}
+
+int32_t swim_set_default_inbound(swim_engine* e, uint32_t mm, int32_t pass) {
+  if (!e) return SWIM_EINVAL;
+  if (mm == 0xffffffffu) { std::fill(e->default_inbound.begin(), e->default_inbound.end(), pass ? 1 : 0); return SWIM_OK; }
+  if (mm >= e->n) return SWIM_EINVAL;
+  e->default_inbound[mm] = pass ? 1 : 0;
+  return SWIM_OK;
+}
+
+int32_t swim_set_partition(swim_engine* e, const uint16_t* g) {
+  if (!e) return SWIM_EINVAL;
+  if (!g) { e->partition = false; return SWIM_OK; }
+  e->partition = true;
+  std::memcpy(e->group.data(), g, sizeof(uint16_t) * e->n);
+  return SWIM_OK;
+}
+
+int32_t swim_read_view(swim_engine* e, uint32_t v, uint64_t* out) {
+  if (!e || v >= e->n || !out) return SWIM_EINVAL;
+  std::memcpy(out, e->m[v].row.data(), sizeof(uint64_t) * e->n);
+  return SWIM_OK;
+}
+
+int32_t swim_drain_events(swim_engine* e, swim_event* out, size_t cap, size_t* n_out) {
+  if (!e || (cap && !out)) return SWIM_EINVAL;
+  std::stable_sort(e->events.begin(), e->events.end(), [](const swim_event& a, const swim_event& b) {
+    if (a.tick != b.tick) return a.tick < b.tick;
+    if (a.viewer != b.viewer) return a.viewer < b.viewer;
+    if (a.phase != b.phase) return a.phase < b.phase;
+    return a.minor < b.minor;
+  });
+  size_t k = std::min(cap, e->events.size());
+  if (k) std::memcpy(out, e->events.data(), k * sizeof(swim_event));
+  e->events.erase(e->events.begin(), e->events.begin() + (ptrdiff_t)k);
+  if (n_out) *n_out = k;
+  return SWIM_OK;
+}
+
+int32_t swim_get_stats(swim_engine* e, swim_stats* out) {
+  if (!e || !out) return SWIM_EINVAL;
+  *out = e->st;
+  return SWIM_OK;
+}
+
+int32_t swim_read_member(swim_engine* e, uint32_t v, swim_member_state* o) {
+  if (!e || v >= e->n || !o) return SWIM_EINVAL;
+  const Member& mv = e->m[v];
+  std::memset(o, 0, sizeof(*o));
+  o->up = mv.up;
+  o->joined = mv.joined;
+  o->leave_pending = mv.leave_pending;
+  o->join_pending = mv.join_pending;
+  o->remote_idx = mv.remote_index;
+  o->fd_period = mv.fd_period;
+  o->ping_cursor = mv.ping_index;
+  o->ping_len = (uint32_t)mv.ping_members.size();
+  o->remote_len = (uint32_t)mv.remote.size();
+  o->gossip_len = (uint32_t)mv.gossips.size();
+  o->gossip_period = mv.g_period;
+  o->gossip_counter = mv.g_counter;
+  o->table_size = mv.table_size;
+  o->members_size = mv.members_size;
+  o->fd_start = mv.fd_start;
+  o->gossip_start = mv.g_start;
+  o->sync_start = mv.sync_start;
+  o->sync_on = mv.sync_on;
+  o->ack_target = mv.ack_due ? mv.ack_target : 0xffffffffu;
+  o->ack_due = mv.ack_due;
+  o->relay_target = mv.relay_due ? mv.relay_target : 0xffffffffu;
+  o->relay_pending = mv.relay_due ? mv.relay_pending : 0;
+  o->relay_due = mv.relay_due;
+  o->leave_gossiper = mv.leave_pending ? mv.leave_gossiper : 0xffffffffu;
+  o->leave_seq = mv.leave_pending ? mv.leave_seq : 0;
+  return SWIM_OK;
+}
+
+static int32_t copy_list(const std::vector<uint32_t>& l, uint32_t* out, uint32_t cap, uint32_t* len) {
+  if (len) *len = (uint32_t)l.size();
+  if (out) std::memcpy(out, l.data(), sizeof(uint32_t) * std::min<size_t>(cap, l.size()));
+  return SWIM_OK;
+}
+
+int32_t swim_read_ping_list(swim_engine* e, uint32_t v, uint32_t* out, uint32_t cap, uint32_t* len) {
+  if (!e || v >= e->n) return SWIM_EINVAL;
+  return copy_list(e->m[v].ping_members, out, cap, len);
+}
+
+int32_t swim_read_remote_list(swim_engine* e, uint32_t v, uint32_t* out, uint32_t cap, uint32_t* len) {
+  if (!e || v >= e->n) return SWIM_EINVAL;
+  return copy_list(e->m[v].remote, out, cap, len);
+}
+
+int32_t swim_read_gossips(swim_engine* e, uint32_t v, swim_gossip* out, uint32_t cap, uint32_t* len) {
+  if (!e || v >= e->n) return SWIM_EINVAL;
+  const auto& gs = e->m[v].gossips;
+  if (len) *len = (uint32_t)gs.size();
+  for (uint32_t i = 0; i < gs.size() && i < cap && out; ++i) {
+    const GossipState& g = gs[i];
+    swim_gossip& o = out[i];
+    o.gossiper = g.gossiper;
+    o.subject = g.rec.member;
+    o.seq = g.seq;
+    o.inc = g.rec.inc;
+    o.status = g.rec.status;
+    o.infection_period = g.infection_period;
+    o.infected[0] = g.infected.size() > 0 ? g.infected[0] : 0xffffffffu;
+    o.infected[1] = g.infected.size() > 1 ? g.infected[1] : 0xffffffffu;
+  }
+  return SWIM_OK;
+}
+
+int32_t swim_read_collector(swim_engine* e, uint32_t v, uint32_t gossiper, swim_interval* out, uint32_t cap,
+                            uint32_t* len) {
+  if (!e || v >= e->n) return SWIM_EINVAL;
+  auto& cols = e->m[v].collectors;
+  auto it = cols.find(gossiper);
+  if (it == cols.end()) { if (len) *len = 0; return SWIM_OK; }
+  if (len) *len = (uint32_t)it->second.iv.size();
+  uint32_t i = 0;
+  for (auto& kv : it->second.iv) {
+    if (i >= cap || !out) break;
+    out[i].lo = (uint64_t)kv.first;
+    out[i].hi = (uint64_t)kv.second;
+    ++i;
+  }
+  return SWIM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,397 @@
+"""ctypes mirror of include/swim.h (the engine's C ABI).
+
+`bind(lib)` declares every prototype on a loaded CDLL.  `Engine` is a thin, typed wrapper over
+one `swim_engine*` handle; it is backend-agnostic (it only needs a library exporting the ABI),
+which is what lets the parity tests drive the CPU oracle and the GPU engine through one code path.
+The product entry point (`swimgpu.SimulatedCluster`) always binds libswimgpu.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from ctypes import POINTER, byref
+
+import numpy as np
+
+SWIM_OK = 0
+SWIM_EINVAL = -1
+SWIM_ENOMEM = -2
+SWIM_EDEVICE = -3
+SWIM_ECAPACITY = -4
+SWIM_ESTATE = -5
+_ERRORS = {
+    SWIM_EINVAL: "SWIM_EINVAL (bad argument / unsupported configuration)",
+    SWIM_ENOMEM: "SWIM_ENOMEM (allocation failed)",
+    SWIM_EDEVICE: "SWIM_EDEVICE (HIP runtime error)",
+    SWIM_ECAPACITY: "SWIM_ECAPACITY (fixed-capacity structure overflowed)",
+    SWIM_ESTATE: "SWIM_ESTATE (invalid in the member's current state)",
+}
+
+ALIVE, SUSPECT, LEAVING, DEAD = 0, 1, 2, 3
+EV_ADDED, EV_REMOVED, EV_LEAVING, EV_UPDATED = 0, 1, 2, 3
+EV_FD_ALIVE, EV_FD_SUSPECT, EV_FD_DEAD = 16, 17, 18
+PHASE_TIMERS, PHASE_FD, PHASE_GOSSIP, PHASE_SYNC, PHASE_SYNCACK, PHASE_CONTROL = 1, 2, 3, 4, 5, 6
+ALL_MEMBERS = 0xFFFFFFFF
+
+
+class SwimError(RuntimeError):
+    def __init__(self, fn: str, code: int):
+        super().__init__(f"{fn} failed: {_ERRORS.get(code, code)}")
+        self.code = code
+
+
+class swim_config(C.Structure):
+    _fields_ = [
+        ("ping_interval", C.c_int32),
+        ("ping_timeout", C.c_int32),
+        ("ping_req_members", C.c_int32),
+        ("gossip_interval", C.c_int32),
+        ("gossip_fanout", C.c_int32),
+        ("gossip_repeat_mult", C.c_int32),
+        ("gossip_segmentation_threshold", C.c_int32),
+        ("sync_interval", C.c_int32),
+        ("sync_timeout", C.c_int32),
+        ("suspicion_mult", C.c_int32),
+        ("removed_members_history_size", C.c_int32),
+        ("metadata_timeout", C.c_int32),
+        ("tick_ms", C.c_int32),
+        ("sync_stagger", C.c_int32),
+        ("record_fd_events", C.c_int32),
+        ("gossip_capacity", C.c_uint32),
+        ("collector_capacity", C.c_uint32),
+        ("event_capacity", C.c_uint32),
+        ("reserved", C.c_uint32 * 8),
+    ]
+
+
+class swim_event(C.Structure):
+    _fields_ = [
+        ("tick", C.c_uint64),
+        ("viewer", C.c_uint32),
+        ("subject", C.c_uint32),
+        ("type", C.c_uint32),
+        ("phase", C.c_uint32),
+        ("minor", C.c_uint32),
+        ("pad", C.c_uint32),
+    ]
+
+
+EVENT_DTYPE = np.dtype(
+    [("tick", "<u8"), ("viewer", "<u4"), ("subject", "<u4"), ("type", "<u4"), ("phase", "<u4"),
+     ("minor", "<u4"), ("pad", "<u4")])
+
+
+class swim_stats(C.Structure):
+    _fields_ = [(name, C.c_uint64) for name in (
+        "ticks", "pings", "ping_reqs", "fd_events", "gossips_created", "gossip_messages",
+        "gossip_accepted", "syncs", "sync_acks", "sync_records", "fetches", "fetch_ok",
+        "timers_fired", "events", "capacity_errors")] + [("reserved", C.c_uint64 * 9)]
+
+
+class swim_member_state(C.Structure):
+    _fields_ = [
+        ("up", C.c_uint8),
+        ("joined", C.c_uint8),
+        ("leave_pending", C.c_uint8),
+        ("join_pending", C.c_uint8),
+        ("remote_idx", C.c_int32),
+        ("fd_period", C.c_uint64),
+        ("ping_cursor", C.c_uint32),
+        ("ping_len", C.c_uint32),
+        ("remote_len", C.c_uint32),
+        ("gossip_len", C.c_uint32),
+        ("gossip_period", C.c_uint64),
+        ("gossip_counter", C.c_uint64),
+        ("table_size", C.c_uint32),
+        ("members_size", C.c_uint32),
+        ("fd_start", C.c_int64),
+        ("gossip_start", C.c_int64),
+        ("sync_start", C.c_int64),
+        ("sync_on", C.c_uint8),
+        ("pad", C.c_uint8 * 3),
+        ("ack_target", C.c_uint32),
+        ("ack_due", C.c_uint64),
+        ("relay_target", C.c_uint32),
+        ("relay_pending", C.c_uint32),
+        ("relay_due", C.c_uint64),
+        ("leave_gossiper", C.c_uint32),
+        ("pad2", C.c_uint32),
+        ("leave_seq", C.c_uint64),
+    ]
+
+
+class swim_gossip(C.Structure):
+    _fields_ = [
+        ("gossiper", C.c_uint32),
+        ("subject", C.c_uint32),
+        ("seq", C.c_uint64),
+        ("inc", C.c_int32),
+        ("status", C.c_uint32),
+        ("infection_period", C.c_uint64),
+        ("infected", C.c_uint32 * 2),
+    ]
+
+
+GOSSIP_DTYPE = np.dtype(
+    [("gossiper", "<u4"), ("subject", "<u4"), ("seq", "<u8"), ("inc", "<i4"), ("status", "<u4"),
+     ("infection_period", "<u8"), ("infected", "<u4", (2,))])
+
+
+class swim_interval(C.Structure):
+    _fields_ = [("lo", C.c_uint64), ("hi", C.c_uint64)]
+
+
+_u32p = POINTER(C.c_uint32)
+_u64p = POINTER(C.c_uint64)
+_engp = C.c_void_p
+
+PROTOTYPES = {
+    "swim_config_default": (C.c_int32, [POINTER(swim_config), C.c_int32]),
+    "swim_ceil_log2": (C.c_int32, [C.c_int32]),
+    "swim_gossip_periods_to_spread": (C.c_int32, [C.c_int32, C.c_int32]),
+    "swim_gossip_periods_to_sweep": (C.c_int32, [C.c_int32, C.c_int32]),
+    "swim_suspicion_timeout": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
+    "swim_create": (C.c_int32, [POINTER(swim_config), C.c_uint32, C.c_uint32, C.c_uint64, POINTER(_engp)]),
+    "swim_destroy": (C.c_int32, [_engp]),
+    "swim_step_ticks": (C.c_int32, [_engp, C.c_uint32]),
+    "swim_step": (C.c_int32, [_engp, C.c_uint32]),
+    "swim_now": (C.c_int32, [_engp, _u64p, _u32p, _u32p]),
+    "swim_set_seeds": (C.c_int32, [_engp, _u32p, C.c_uint32]),
+    "swim_kill": (C.c_int32, [_engp, C.c_uint32]),
+    "swim_leave": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
+    "swim_join": (C.c_int32, [_engp, C.c_uint32]),
+    "swim_set_default_loss": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
+    "swim_set_link_loss": (C.c_int32, [_engp, C.c_uint32, C.c_uint32, C.c_int32]),
+    "swim_set_link_inbound": (C.c_int32, [_engp, C.c_uint32, C.c_uint32, C.c_int32]),
+    "swim_set_default_inbound": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
+    "swim_set_partition": (C.c_int32, [_engp, POINTER(C.c_uint16)]),
+    "swim_read_view": (C.c_int32, [_engp, C.c_uint32, _u64p]),
+    "swim_drain_events": (C.c_int32, [_engp, POINTER(swim_event), C.c_size_t, POINTER(C.c_size_t)]),
+    "swim_get_stats": (C.c_int32, [_engp, POINTER(swim_stats)]),
+    "swim_read_member": (C.c_int32, [_engp, C.c_uint32, POINTER(swim_member_state)]),
+    "swim_read_ping_list": (C.c_int32, [_engp, C.c_uint32, _u32p, C.c_uint32, _u32p]),
+    "swim_read_remote_list": (C.c_int32, [_engp, C.c_uint32, _u32p, C.c_uint32, _u32p]),
+    "swim_read_gossips": (C.c_int32, [_engp, C.c_uint32, POINTER(swim_gossip), C.c_uint32, _u32p]),
+    "swim_read_collector": (C.c_int32, [_engp, C.c_uint32, C.c_uint32, POINTER(swim_interval), C.c_uint32, _u32p]),
+    "swim_philox": (C.c_int32, [_u32p, _u32p, _u32p]),
+    "swim_kat_overrides": (C.c_int32, [POINTER(C.c_int32), C.c_uint32, POINTER(C.c_uint8)]),
+    "swim_kat_collector": (C.c_int32, [POINTER(C.c_uint8), POINTER(C.c_int64), C.c_uint32, POINTER(C.c_int64)]),
+}
+
+
+def bind(lib: C.CDLL) -> C.CDLL:
+    """Declare every swim.h prototype on `lib`; raises AttributeError if a symbol is missing."""
+    for name, (res, args) in PROTOTYPES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def _check(fn: str, rc: int) -> None:
+    if rc != SWIM_OK:
+        raise SwimError(fn, rc)
+
+
+def default_config(lib: C.CDLL, preset: int = 0, **overrides) -> swim_config:
+    cfg = swim_config()
+    _check("swim_config_default", lib.swim_config_default(byref(cfg), preset))
+    for k, v in overrides.items():
+        if not hasattr(cfg, k):
+            raise AttributeError(f"swim_config has no field {k!r}")
+        setattr(cfg, k, v)
+    return cfg
+
+
+class Engine:
+    """One engine handle over any library exporting the swim.h ABI."""
+
+    def __init__(self, lib: C.CDLL, cfg: swim_config, capacity: int, n_initial: int, seed: int):
+        self.lib = lib
+        self.cfg = cfg
+        self.capacity = int(capacity)
+        h = _engp()
+        _check("swim_create", lib.swim_create(byref(cfg), capacity, n_initial, seed, byref(h)))
+        self._h = h
+
+    # -- lifecycle ------------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.lib.swim_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def step(self, periods: int = 1) -> None:
+        _check("swim_step", self.lib.swim_step(self._h, periods))
+
+    def step_ticks(self, ticks: int = 1) -> None:
+        _check("swim_step_ticks", self.lib.swim_step_ticks(self._h, ticks))
+
+    def now(self) -> tuple[int, int, int]:
+        t, ms, tpp = C.c_uint64(), C.c_uint32(), C.c_uint32()
+        _check("swim_now", self.lib.swim_now(self._h, byref(t), byref(ms), byref(tpp)))
+        return t.value, ms.value, tpp.value
+
+    # -- control --------------------------------------------------------------------------
+    def set_seeds(self, seeds) -> None:
+        arr = (C.c_uint32 * len(seeds))(*seeds)
+        _check("swim_set_seeds", self.lib.swim_set_seeds(self._h, arr, len(seeds)))
+
+    def kill(self, m: int) -> None:
+        _check("swim_kill", self.lib.swim_kill(self._h, m))
+
+    def leave(self, m: int, stop_after: bool = True) -> None:
+        _check("swim_leave", self.lib.swim_leave(self._h, m, 1 if stop_after else 0))
+
+    def join(self, m: int) -> None:
+        _check("swim_join", self.lib.swim_join(self._h, m))
+
+    def set_default_loss(self, loss_percent: int, m: int = ALL_MEMBERS) -> None:
+        _check("swim_set_default_loss", self.lib.swim_set_default_loss(self._h, m, loss_percent))
+
+    def set_link_loss(self, src: int, dst: int, loss_percent: int) -> None:
+        _check("swim_set_link_loss", self.lib.swim_set_link_loss(self._h, src, dst, loss_percent))
+
+    def set_link_inbound(self, dst: int, src: int, shall_pass: int) -> None:
+        _check("swim_set_link_inbound", self.lib.swim_set_link_inbound(self._h, dst, src, shall_pass))
+
+    def set_default_inbound(self, shall_pass: bool, m: int = ALL_MEMBERS) -> None:
+        _check("swim_set_default_inbound", self.lib.swim_set_default_inbound(self._h, m, 1 if shall_pass else 0))
+
+    def set_partition(self, groups) -> None:
+        if groups is None:
+            _check("swim_set_partition", self.lib.swim_set_partition(self._h, None))
+            return
+        g = np.ascontiguousarray(groups, dtype=np.uint16)
+        assert g.shape == (self.capacity,)
+        _check("swim_set_partition", self.lib.swim_set_partition(self._h, g.ctypes.data_as(POINTER(C.c_uint16))))
+
+    # -- readback -------------------------------------------------------------------------
+    def read_view(self, viewer: int) -> np.ndarray:
+        out = np.empty(self.capacity, dtype=np.uint64)
+        _check("swim_read_view", self.lib.swim_read_view(self._h, viewer, out.ctypes.data_as(_u64p)))
+        return out
+
+    def drain_events(self, cap: int = 1 << 20) -> np.ndarray:
+        chunks = []
+        while True:
+            buf = np.zeros(cap, dtype=EVENT_DTYPE)
+            n = C.c_size_t()
+            _check("swim_drain_events", self.lib.swim_drain_events(
+                self._h, buf.ctypes.data_as(POINTER(swim_event)), cap, byref(n)))
+            chunks.append(buf[: n.value])
+            if n.value < cap:
+                break
+        return np.concatenate(chunks) if chunks else np.zeros(0, dtype=EVENT_DTYPE)
+
+    def stats(self) -> dict:
+        s = swim_stats()
+        _check("swim_get_stats", self.lib.swim_get_stats(self._h, byref(s)))
+        return {name: getattr(s, name) for name, _ in swim_stats._fields_ if name != "reserved"}
+
+    def read_member(self, m: int) -> dict:
+        s = swim_member_state()
+        _check("swim_read_member", self.lib.swim_read_member(self._h, m, byref(s)))
+        return {name: getattr(s, name) for name, _ in swim_member_state._fields_ if not name.startswith("pad")}
+
+    def _read_list(self, fn: str, m: int) -> np.ndarray:
+        ln = C.c_uint32()
+        _check(fn, getattr(self.lib, fn)(self._h, m, None, 0, byref(ln)))
+        out = np.empty(ln.value, dtype=np.uint32)
+        if ln.value:
+            _check(fn, getattr(self.lib, fn)(self._h, m, out.ctypes.data_as(_u32p), ln.value, byref(ln)))
+        return out
+
+    def read_ping_list(self, m: int) -> np.ndarray:
+        return self._read_list("swim_read_ping_list", m)
+
+    def read_remote_list(self, m: int) -> np.ndarray:
+        return self._read_list("swim_read_remote_list", m)
+
+    def read_gossips(self, m: int) -> np.ndarray:
+        ln = C.c_uint32()
+        _check("swim_read_gossips", self.lib.swim_read_gossips(self._h, m, None, 0, byref(ln)))
+        out = np.zeros(ln.value, dtype=GOSSIP_DTYPE)
+        if ln.value:
+            _check("swim_read_gossips", self.lib.swim_read_gossips(
+                self._h, m, out.ctypes.data_as(POINTER(swim_gossip)), ln.value, byref(ln)))
+        return out
+
+    def read_collector(self, m: int, gossiper: int) -> list[tuple[int, int]]:
+        ln = C.c_uint32()
+        _check("swim_read_collector", self.lib.swim_read_collector(self._h, m, gossiper, None, 0, byref(ln)))
+        if ln.value == 0:
+            return []
+        out = (swim_interval * ln.value)()
+        _check("swim_read_collector", self.lib.swim_read_collector(self._h, m, gossiper, out, ln.value, byref(ln)))
+        return [(x.lo, x.hi) for x in out]
+
+
+def philox(lib, ctr, key):
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    _check("swim_philox", lib.swim_philox(c, k, o))
+    return list(o)
+
+
+def kat_overrides(lib, cases) -> list[bool]:
+    """cases: iterable of (r1_status, r1_inc, r0) with r0 = None or (status, inc)."""
+    flat = []
+    for r1s, r1i, r0 in cases:
+        flat += [r1s, r1i, 0, 0, 0] if r0 is None else [r1s, r1i, 1, r0[0], r0[1]]
+    n = len(flat) // 5
+    arr = (C.c_int32 * len(flat))(*flat)
+    out = (C.c_uint8 * n)()
+    _check("swim_kat_overrides", lib.swim_kat_overrides(arr, n, out))
+    return [bool(x) for x in out]
+
+
+def kat_collector(lib, ops) -> list[int]:
+    """ops: list of ("add"|"contains"|"size"|"clear", value)."""
+    codes = {"add": 0, "contains": 1, "size": 2, "clear": 3}
+    n = len(ops)
+    kinds = (C.c_uint8 * n)(*[codes[o[0]] for o in ops])
+    vals = (C.c_int64 * n)(*[int(o[1]) if len(o) > 1 else 0 for o in ops])
+    res = (C.c_int64 * n)()
+    _check("swim_kat_collector", lib.swim_kat_collector(kinds, vals, n, res))
+    return list(res)
+
+
+# -- cell decoding (swim.h "Packed view cell") ----------------------------------------------
+def cell_inc(c):
+    return (np.asarray(c, dtype=np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+
+
+def cell_status(c):
+    return ((np.asarray(c, dtype=np.uint64) >> np.uint64(32)) & np.uint64(3)).astype(np.uint32)
+
+
+def cell_flag(c, bit: int):
+    return ((np.asarray(c, dtype=np.uint64) >> np.uint64(bit)) & np.uint64(1)).astype(bool)
+
+
+def cell_in_table(c):
+    return cell_flag(c, 34)
+
+
+def cell_in_members(c):
+    return cell_flag(c, 35)
+
+
+def cell_has_timer(c):
+    return cell_flag(c, 37)
+
+
+def cell_deadline(c):
+    return (np.asarray(c, dtype=np.uint64) >> np.uint64(39)).astype(np.uint32)

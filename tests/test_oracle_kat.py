@@ -1,0 +1,134 @@
+"""Pins the CPU oracle against the reference's own known-answer tests.
+
+* MembershipRecordTest.java:34-108 — the isOverrides truth table.
+* SequenceIdCollectorTest.java:19-114 — interval-set dedupe.
+* ClusterMath values quoted in SURVEY.md §6 / BASELINE.md (ClusterMath.java:65-135).
+* Philox4x32-10 known-answer vectors (Random123 kat_vectors), the RNG hook of DESIGN.md §4.
+
+The same KATs run against libswimgpu.so's device code in test_gpu_parity.py.
+"""
+import pytest
+
+import oracle
+from swimgpu import abi
+from swimgpu.abi import ALIVE, DEAD, LEAVING, SUSPECT
+
+# (r1, r0, expected) exactly as MembershipRecordTest asserts them
+OVERRIDE_CASES = []
+_r0s = [None] + [(s, i) for s in (ALIVE, SUSPECT, DEAD) for i in (0, 1, 2)]
+_expect = {
+    # testDeadOverride (:46-62): r1 = DEAD 1
+    (DEAD, 1): [False, True, True, True, True, True, True, False, False, False],
+    # testAliveOverride (:64-80): r1 = ALIVE 1
+    (ALIVE, 1): [True, True, False, False, True, False, False, False, False, False],
+    # testSuspectOverride (:82-98): r1 = SUSPECT 1
+    (SUSPECT, 1): [False, True, True, False, True, False, False, False, False, False],
+}
+for r1, exp in _expect.items():
+    for r0, e in zip(_r0s, exp):
+        OVERRIDE_CASES.append((r1, r0, e))
+# testEqualRecordNotOverriding (:100-105)
+OVERRIDE_CASES += [((ALIVE, 1), (ALIVE, 1), False), ((SUSPECT, 1), (SUSPECT, 1), False),
+                   ((DEAD, 1), (DEAD, 1), False)]
+# LEAVING rows of the truth table used by updateMembership (MembershipRecord.java:68-87)
+OVERRIDE_CASES += [((LEAVING, 0), None, True), ((SUSPECT, 3), (LEAVING, 3), True),
+                   ((ALIVE, 3), (LEAVING, 3), False), ((LEAVING, 4), (ALIVE, 3), True),
+                   ((LEAVING, 3), (ALIVE, 3), False)]
+
+
+def _override_inputs():
+    return [(r1[0], r1[1], r0) for r1, r0, _ in OVERRIDE_CASES], [e for *_, e in OVERRIDE_CASES]
+
+
+def check_overrides(lib):
+    cases, expected = _override_inputs()
+    assert abi.kat_overrides(lib, cases) == expected
+
+
+# SequenceIdCollectorTest, one op-list per @Test with the expected results
+COLLECTOR_CASES = {
+    "testEmpty": ([("contains", 0)], [0]),
+    "testOneElement": ([("add", 10), ("size",), ("contains", 10)], [1, 1, 1]),
+    "testIsHeldNotExistedElements": ([("add", 10), ("contains", 9), ("contains", 11)], [1, 0, 0]),
+    "testAddExistedElement": ([("add", 10), ("add", 10)], [1, 0]),
+    "testClear": ([("add", 10), ("clear",), ("contains", 10)], [1, 0, 0]),
+    "testLowestAndHighestElementInRange": (
+        [("add", i) for i in range(10)] + [("contains", 0), ("contains", 9), ("add", 0), ("add", 9)],
+        [1] * 10 + [1, 1, 0, 0]),
+    "testJoinLowerRange": (
+        [("add", 10), ("add", 11), ("size",)] + [("add", i) for i in range(20, 30)] + [("size",), ("add", 19), ("size",)],
+        [1, 1, 1] + [1] * 10 + [2, 1, 2]),
+    "testJoinUpperRange": (
+        [("add", 10), ("add", 9), ("size",)] + [("add", i) for i in range(20, 30)] + [("size",), ("add", 30), ("size",)],
+        [1, 1, 1] + [1] * 10 + [2, 1, 2]),
+    "testJoinTwoRange": (
+        [("add", 10), ("add", 12), ("size",), ("add", 11), ("size",)] + [("add", i) for i in range(20, 25)]
+        + [("add", i) for i in range(26, 30)] + [("size",), ("add", 25), ("size",)],
+        [1, 1, 2, 1, 1] + [1] * 9 + [3, 1, 2]),
+}
+
+
+def check_collector(lib):
+    for name, (ops, expected) in COLLECTOR_CASES.items():
+        assert abi.kat_collector(lib, ops) == expected, name
+
+
+PHILOX_KAT = [  # Random123 kat_vectors: philox4x32 10 <ctr> <key> <expected>
+    ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+    ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+    ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+     (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+]
+
+
+def check_philox(lib):
+    for ctr, key, exp in PHILOX_KAT:
+        assert tuple(abi.philox(lib, ctr, key)) == exp
+
+
+# ClusterMath: N -> (spread, sweep, suspicion s, max msgs/gossip/node) for LAN
+CLUSTER_MATH = {3: (6, 14, 10, 18), 1024: (33, 68, 55, 99), 16384: (45, 92, 75, 135),
+                65536: (51, 104, 85, 153), 262144: (57, 116, 95, 171)}
+
+
+def check_cluster_math(lib):
+    for n, (spread, sweep, susp_s, msgs) in CLUSTER_MATH.items():
+        assert lib.swim_gossip_periods_to_spread(3, n) == spread
+        assert lib.swim_gossip_periods_to_sweep(3, n) == sweep
+        assert lib.swim_suspicion_timeout(5, n, 1000) == susp_s * 1000
+        assert 3 * 3 * lib.swim_ceil_log2(n) == msgs
+    assert lib.swim_ceil_log2(0) == 0 and lib.swim_ceil_log2(1) == 1 and lib.swim_ceil_log2(-1) == 32
+
+
+@pytest.fixture(scope="module")
+def olib():
+    return oracle.lib()
+
+
+def test_oracle_overrides_truth_table(olib):
+    check_overrides(olib)
+
+
+def test_oracle_sequence_id_collector(olib):
+    check_collector(olib)
+
+
+def test_oracle_philox_kat(olib):
+    check_philox(olib)
+
+
+def test_oracle_cluster_math(olib):
+    check_cluster_math(olib)
+
+
+def test_oracle_config_presets(olib):
+    lan = abi.default_config(olib, 0)
+    assert (lan.ping_interval, lan.ping_timeout, lan.ping_req_members) == (1000, 500, 3)
+    assert (lan.gossip_interval, lan.gossip_fanout, lan.gossip_repeat_mult) == (200, 3, 3)
+    assert (lan.sync_interval, lan.sync_timeout, lan.suspicion_mult, lan.metadata_timeout) == (30000, 3000, 5, 3000)
+    wan = abi.default_config(olib, 1)
+    assert (wan.ping_interval, wan.ping_timeout, wan.gossip_fanout, wan.suspicion_mult) == (5000, 3000, 4, 6)
+    assert (wan.sync_interval, wan.metadata_timeout) == (60000, 10000)
+    loc = abi.default_config(olib, 2)
+    assert (loc.ping_interval, loc.ping_timeout, loc.ping_req_members) == (1000, 200, 1)
+    assert (loc.gossip_interval, loc.gossip_repeat_mult, loc.suspicion_mult, loc.sync_interval) == (100, 2, 3, 15000)
