@@ -1,0 +1,507 @@
+// swim_device.h — device data layout and per-viewer protocol logic of the lockstep SWIM engine.
+//
+// Layout: everything is structure-of-arrays in HBM, row-major per viewer.
+//   cells   u64[N][N]   packed view cell per (viewer, subject)  — swim.h cell format
+//   ping    u32[N][N]   FailureDetectorImpl.pingMembers of each viewer (ArrayList order)
+//   remote  u32[N][N]   GossipProtocolImpl.remoteMembers of each viewer
+//   slab    GossipDev[N][gcap]  live GossipStates, insertion order
+//   coll    CollDev[N][hcap]    SequenceIdCollector per (viewer, gossiper), open addressing
+//   mem     MemberDev[N]        scalar per-member protocol state
+//
+// The functions below run on ONE thread that owns viewer v for the duration of a phase (the
+// canonical sequential semantics of DESIGN.md §3); parallelism is across viewers, and inside
+// SYNC row merges across subjects (swim_kernels.h).  Citations are to
+// /root/reference/cluster/src/main/java/io/scalecube/cluster/ unless noted.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/swim.h"
+#include "../../include/swim_rng.h"
+
+namespace swimdev {
+
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr int KIV = 6;         // inline intervals per SequenceIdCollector
+constexpr int FD_SYNC_MAX = 33;  // FD-triggered SYNCs per member per tick (<= 2k+1)
+
+// error bits (stats.capacity_errors / SWIM_ECAPACITY)
+enum : uint32_t {
+  ERR_SLAB = 1u << 0, ERR_INTERVALS = 1u << 1, ERR_HASH = 1u << 2, ERR_WHEEL = 1u << 3,
+  ERR_EVENTS = 1u << 4, ERR_MSGS = 1u << 5, ERR_SNAP = 1u << 6, ERR_INFECTED = 1u << 7,
+  ERR_FDSYNC = 1u << 8, ERR_INS = 1u << 9, ERR_REQS = 1u << 10, ERR_PEND = 1u << 11,
+};
+
+// stats slots (swim_stats order)
+enum { ST_TICKS, ST_PINGS, ST_PING_REQS, ST_FD_EVENTS, ST_GOSSIPS_CREATED, ST_GOSSIP_MESSAGES,
+       ST_GOSSIP_ACCEPTED, ST_SYNCS, ST_SYNC_ACKS, ST_SYNC_RECORDS, ST_FETCHES, ST_FETCH_OK,
+       ST_TIMERS_FIRED, ST_EVENTS, ST_CAPACITY_ERRORS, ST_COUNT = 24 };
+
+enum Reason { R_FD_EVENT, R_GOSSIP, R_SYNC, R_INITIAL_SYNC, R_TIMEOUT };
+
+constexpr uint64_t B_IN_TABLE = 1ull << 34, B_IN_MEMBERS = 1ull << 35, B_ALIVE_EMITTED = 1ull << 36,
+                   B_HAS_TIMER = 1ull << 37, B_HAS_METADATA = 1ull << 38;
+
+struct alignas(16) MemberDev {
+  uint64_t fd_period, ack_due, relay_due, g_period, g_counter, period_used, leave_seq;
+  int64_t fd_start, g_start, sync_start;
+  uint32_t ping_cursor, ping_len, ack_target, relay_target, relay_pending;
+  uint32_t remote_len;
+  int32_t remote_idx;
+  uint32_t gossip_len, table_size, members_size, leave_gossiper;
+  uint32_t ev_minor, fetch_ctr, fd_sync_cnt, ins_rank, init_total, init_done;
+  uint8_t up, joined, join_now, join_pending, leave_pending, leave_done, sync_on, pad;
+};
+
+struct GossipDev {  // GossipState + Gossip + MembershipRecord payload, 32 B
+  uint32_t gossiper, subject, seq, inf_period;
+  int32_t inc;
+  uint32_t status;
+  uint32_t inf0, inf1;  // GossipState.infected (NONE = empty)
+};
+
+struct CollDev {  // SequenceIdCollector: up to KIV closed intervals, ascending
+  uint32_t key;   // gossiper + 1; 0 = empty slot
+  uint32_t n;
+  uint32_t cleared;  // 1 once cleared/removed: a GossipState may outlive its collector entries
+  uint32_t pad;
+  uint32_t lo[KIV], hi[KIV];
+};
+
+struct LinkDev {  // NetworkEmulator per-link override, sorted by (a, b)
+  uint32_t a, b;
+  int32_t out_loss;  // outboundSettings(b) on a; -1 = none
+  int32_t in_pass;   // inboundSettings(b) on a (a receives from b); -1 = none
+};
+
+struct GMsgFull {
+  uint32_t to, from, pos, slot;
+  uint32_t gossiper, seq, subject, status;
+  int32_t inc;
+  uint32_t pad[3];
+};
+
+struct SyncReq {  // SYNC (request) or SYNC_ACK
+  uint32_t from, to, ordinal, slot;
+  uint32_t flags;  // bit0 initial, bit1 outfail, bit2 delivered, bit3 acked
+  uint32_t pad[3];
+};
+
+struct InsOp {  // deferred pingMembers.add(nextInt(size), member) of an ADDED event
+  uint32_t v, s, phase, minor, rank, pad[3];
+};
+
+struct Ctx {
+  uint32_t n, gcap, hcap, wheel_mask, wheel_cap;
+  uint32_t P, to_ticks, relay_ticks, G, S, sync_to_ticks, tick_ms;
+  int32_t ping_interval, suspicion_mult, repeat_mult, fanout, ping_req_members, seg_threshold, record_fd;
+  uint32_t key0, key1;
+  uint64_t T;
+  uint64_t* cells;
+  MemberDev* mem;
+  uint32_t* ping;
+  uint32_t* remote;
+  GossipDev* slab;
+  CollDev* coll;
+  uint32_t* fd_sync;
+  uint64_t* wheel;
+  uint32_t* wheel_cnt;
+  swim_event* ev;
+  uint32_t* ev_cnt;
+  uint32_t ev_cap;
+  // network emulator
+  uint8_t* default_loss;
+  uint8_t* default_inbound;
+  uint16_t* group;
+  uint32_t partition;
+  LinkDev* links;
+  uint32_t n_links;
+  uint8_t* is_seed;
+  uint32_t* seeds;
+  uint32_t n_seeds;
+  // deferred list ops
+  InsOp* ins;
+  uint32_t* ins_total;
+  uint32_t ins_cap;
+  uint32_t* ins_cnt;       // per viewer
+  uint32_t* ins_list;      // viewers with ops
+  uint32_t* ins_list_cnt;
+  uint32_t* compact_flag;  // per viewer
+  uint32_t* compact_list;
+  uint32_t* compact_cnt;
+  unsigned long long* stats;
+  uint32_t* err;
+};
+
+// ------------------------------------------------------------------------------- Philox4x32-10
+__device__ __forceinline__ uint32_t philox_w0(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return c0;
+}
+
+__device__ __forceinline__ void philox4(const uint32_t in[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
+  uint32_t c0 = in[0], c1 = in[1], c2 = in[2], c3 = in[3];
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+__device__ __forceinline__ uint32_t draw_at(const Ctx& c, uint32_t member, uint64_t tick, uint32_t stream,
+                                            uint32_t sub24, uint32_t sub32) {
+  return philox_w0(member, (uint32_t)tick, (stream << 24) | (sub24 & 0xffffffu), sub32, c.key0, c.key1);
+}
+__device__ __forceinline__ uint32_t draw(const Ctx& c, uint32_t member, uint32_t stream, uint32_t sub24, uint32_t sub32) {
+  return draw_at(c, member, c.T, stream, sub24, sub32);
+}
+__device__ __forceinline__ uint32_t next_int(uint32_t w, uint32_t bound) {
+  return (uint32_t)(((uint64_t)w * bound) >> 32);
+}
+__device__ __forceinline__ bool lost(int32_t pct, uint32_t w) {
+  return pct > 0 && (pct >= 100 || (int32_t)next_int(w, 100) < pct);
+}
+
+// ------------------------------------------------------------------------------- cells
+__device__ __forceinline__ int32_t c_inc(uint64_t c) { return (int32_t)(uint32_t)c; }
+__device__ __forceinline__ uint32_t c_status(uint64_t c) { return (uint32_t)((c >> 32) & 3u); }
+__device__ __forceinline__ bool c_has(uint64_t c, uint64_t b) { return (c & b) != 0; }
+__device__ __forceinline__ uint32_t c_deadline(uint64_t c) { return (uint32_t)(c >> 39); }
+__device__ __forceinline__ uint64_t c_with_record(uint64_t c, uint32_t st, int32_t inc) {
+  return (c & ~0x3ffffffffull) | (uint64_t)(uint32_t)inc | ((uint64_t)st << 32);
+}
+__device__ __forceinline__ uint64_t c_with_deadline(uint64_t c, uint64_t tick) {
+  return (c & ((1ull << 39) - 1)) | ((tick & SWIM_DEADLINE_MASK) << 39);
+}
+__device__ __forceinline__ uint64_t* row(const Ctx& c, uint32_t v) { return c.cells + (size_t)v * c.n; }
+
+__device__ __forceinline__ void set_err(const Ctx& c, uint32_t bit) { atomicOr(c.err, bit); }
+__device__ __forceinline__ void stat_add(const Ctx& c, int slot, unsigned long long x) {
+  if (x) atomicAdd(&c.stats[slot], x);
+}
+
+// MembershipRecord.isOverrides (MembershipRecord.java:67-88); r0p = false for "no record"
+__device__ __forceinline__ bool is_overrides(uint32_t s1, int32_t i1, bool r0p, uint32_t s0, int32_t i0) {
+  if (!r0p) return s1 == SWIM_ALIVE || s1 == SWIM_LEAVING;
+  if (s1 == s0 && i1 == i0) return false;
+  if (s0 == SWIM_DEAD) return false;
+  if (s1 == SWIM_DEAD) return true;
+  if (i1 == i0) return s1 == SWIM_SUSPECT && (s0 == SWIM_ALIVE || s0 == SWIM_LEAVING);
+  return i1 > i0;
+}
+
+// ------------------------------------------------------------------------------- network emulator
+__device__ __forceinline__ const LinkDev* find_link(const Ctx& c, uint32_t a, uint32_t b) {
+  uint32_t lo = 0, hi = c.n_links;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    const LinkDev& L = c.links[mid];
+    if (L.a < a || (L.a == a && L.b < b)) lo = mid + 1; else hi = mid;
+  }
+  if (lo < c.n_links && c.links[lo].a == a && c.links[lo].b == b) return &c.links[lo];
+  return nullptr;
+}
+// NetworkEmulator.outboundSettings(dst) on src (NetworkEmulator.java:59-61)
+__device__ __forceinline__ int32_t out_loss(const Ctx& c, uint32_t a, uint32_t b) {
+  if (c.partition && c.group[a] != c.group[b]) return 100;
+  if (c.n_links) {
+    const LinkDev* L = find_link(c, a, b);
+    if (L && L->out_loss >= 0) return L->out_loss;
+  }
+  return c.default_loss[a];
+}
+// NetworkEmulator.inboundSettings(src).shallPass() on receiver b (NetworkEmulator.java:212-214)
+__device__ __forceinline__ bool in_pass(const Ctx& c, uint32_t b, uint32_t a) {
+  if (c.n_links) {
+    const LinkDev* L = find_link(c, b, a);
+    if (L && L->in_pass >= 0) return L->in_pass != 0;
+  }
+  return c.default_inbound[b] != 0;
+}
+// tryFailOutbound (NetworkEmulator.java:167-181) + a stopped destination refusing the connection
+__device__ __forceinline__ bool out_fail(const Ctx& c, uint32_t a, uint32_t b, uint32_t w) {
+  return !c.mem[b].up || lost(out_loss(c, a, b), w);
+}
+
+// ------------------------------------------------------------------------------- collectors
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+__device__ inline CollDev* coll_find(const Ctx& c, uint32_t v, uint32_t gossiper) {
+  CollDev* base = c.coll + (size_t)v * c.hcap;
+  uint32_t mask = c.hcap - 1, h = hash32(gossiper) & mask, key = gossiper + 1;
+  for (uint32_t i = 0; i < c.hcap; ++i) {
+    CollDev* e = base + ((h + i) & mask);
+    if (e->key == key) return e;
+    if (e->key == 0) return nullptr;
+  }
+  return nullptr;
+}
+// ensureSequence (GossipProtocolImpl.java:279-281)
+__device__ inline CollDev* coll_ensure(const Ctx& c, uint32_t v, uint32_t gossiper) {
+  CollDev* base = c.coll + (size_t)v * c.hcap;
+  uint32_t mask = c.hcap - 1, h = hash32(gossiper) & mask, key = gossiper + 1;
+  for (uint32_t i = 0; i < c.hcap; ++i) {
+    CollDev* e = base + ((h + i) & mask);
+    if (e->key == key) return e;
+    if (e->key == 0) {
+      e->key = key;
+      e->n = 0;
+      e->cleared = 0;
+      return e;
+    }
+  }
+  set_err(c, ERR_HASH);
+  return nullptr;
+}
+// SequenceIdCollector.contains (SequenceIdCollector.java:32-35)
+__device__ inline bool coll_contains(const CollDev* e, uint32_t x) {
+  if (!e) return false;
+  for (int i = (int)e->n - 1; i >= 0; --i)
+    if (e->lo[i] <= x) return x <= e->hi[i];
+  return false;
+}
+// SequenceIdCollector.add (SequenceIdCollector.java:43-72)
+__device__ inline bool coll_add(const Ctx& c, CollDev* e, uint32_t x) {
+  if (!e) return true;
+  int n = (int)e->n, fl = -1;
+  for (int i = n - 1; i >= 0; --i)
+    if (e->lo[i] <= x) { fl = i; break; }
+  if (fl >= 0 && x <= e->hi[fl]) return false;
+  int ce = fl + 1;  // first interval with lo > x (lo == x would have been the floor)
+  bool nf = fl >= 0 && (int64_t)x - 1 == (int64_t)e->hi[fl];
+  bool nc = ce < n && (int64_t)x + 1 == (int64_t)e->lo[ce];
+  if (nf && nc) {
+    e->hi[fl] = e->hi[ce];
+    for (int i = ce; i + 1 < n; ++i) { e->lo[i] = e->lo[i + 1]; e->hi[i] = e->hi[i + 1]; }
+    e->n = n - 1;
+  } else if (nf) {
+    e->hi[fl] = x;
+  } else if (nc) {
+    e->lo[ce] = x;
+  } else {
+    if (n == KIV) { set_err(c, ERR_INTERVALS); return true; }
+    for (int i = n; i > ce; --i) { e->lo[i] = e->lo[i - 1]; e->hi[i] = e->hi[i - 1]; }
+    e->lo[ce] = x;
+    e->hi[ce] = x;
+    e->n = n + 1;
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------------------- events
+__device__ inline void emit(const Ctx& c, uint32_t v, uint32_t s, uint32_t type, uint32_t phase, uint32_t minor) {
+  uint32_t i = atomicAdd(c.ev_cnt, 1u);
+  if (i >= c.ev_cap) { set_err(c, ERR_EVENTS); return; }
+  swim_event e;
+  e.tick = c.T;
+  e.viewer = v;
+  e.subject = s;
+  e.type = type;
+  e.phase = phase;
+  e.minor = minor;
+  e.pad = 0;
+  c.ev[i] = e;
+}
+
+// FailureDetectorImpl.onMemberEvent (:321-346) + GossipProtocolImpl.onMemberEvent (:238-261) for
+// ADDED: the remote list append is O(1) and done now; the pingMembers insert is deferred to the
+// phase's list kernel, which applies a viewer's inserts in event order.
+__device__ inline void on_added(const Ctx& c, uint32_t v, uint32_t s, uint32_t phase, uint32_t minor) {
+  MemberDev& m = c.mem[v];
+  c.remote[(size_t)v * c.n + m.remote_len] = s;
+  m.remote_len++;
+  uint32_t rank = m.ins_rank++;
+  if (rank == 0) {
+    uint32_t li = atomicAdd(c.ins_list_cnt, 1u);
+    c.ins_list[li] = v;
+  }
+  c.ins_cnt[v] = rank + 1;
+  uint32_t i = atomicAdd(c.ins_total, 1u);
+  if (i >= c.ins_cap) { set_err(c, ERR_INS); return; }
+  InsOp op;
+  op.v = v; op.s = s; op.phase = phase; op.minor = minor; op.rank = rank;
+  op.pad[0] = op.pad[1] = op.pad[2] = 0;
+  c.ins[i] = op;
+}
+
+// REMOVED: GossipProtocolImpl drops the member's SequenceIdCollector (:242); both lists drop the
+// member in the phase's compaction kernel (they hold exactly the viewer's other `members`).
+// Safe under entry-parallel timer processing: only the (v, s) collector entry is written.
+__device__ inline void on_removed(const Ctx& c, uint32_t v, uint32_t s) {
+  CollDev* e = coll_find(c, v, s);
+  if (e) {
+    e->n = 0;
+    e->cleared = 1;
+  }
+  if (atomicExch(&c.compact_flag[v], 1u) == 0u) c.compact_list[atomicAdd(c.compact_cnt, 1u)] = v;
+}
+
+__device__ inline void publish_event(const Ctx& c, uint32_t v, uint32_t s, uint32_t type, uint32_t phase,
+                                     uint32_t minor) {
+  emit(c, v, s, type, phase, minor);
+  if (type == SWIM_EV_ADDED) on_added(c, v, s, phase, minor);
+  if (type == SWIM_EV_REMOVED) on_removed(c, v, s);
+}
+
+__device__ __forceinline__ uint32_t next_minor(const Ctx& c, uint32_t v, uint32_t phase, uint32_t s) {
+  return phase == SWIM_PHASE_TIMERS ? s : c.mem[v].ev_minor++;
+}
+
+// ------------------------------------------------------------------------------- gossip origination
+// spreadMembershipGossip (MembershipProtocolImpl.java:845-860) -> createAndPutGossip (GossipProtocolImpl.java:190-199)
+__device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject, uint32_t status, int32_t inc) {
+  MemberDev& m = c.mem[v];
+  if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); return; }
+  GossipDev g;
+  g.gossiper = v;
+  g.seq = (uint32_t)m.g_counter;
+  g.subject = subject;
+  g.status = status;
+  g.inc = inc;
+  g.inf_period = (uint32_t)m.g_period;
+  g.inf0 = NONE;
+  g.inf1 = NONE;
+  c.slab[(size_t)v * c.gcap + m.gossip_len] = g;
+  m.gossip_len++;
+  m.g_counter++;
+  CollDev* e = coll_ensure(c, v, v);
+  coll_add(c, e, g.seq);
+  stat_add(c, ST_GOSSIPS_CREATED, 1);
+}
+
+// ------------------------------------------------------------------------------- timers
+// scheduleSuspicionTimeoutTask (MembershipProtocolImpl.java:805-823)
+__device__ __forceinline__ int32_t ceil_log2(uint32_t x) { return x ? 32 - __clz(x) : 0; }
+__device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
+  uint64_t* cp = row(c, v) + s;
+  uint64_t cell = *cp;
+  if (c_has(cell, B_HAS_TIMER)) return;
+  uint64_t ms = (uint64_t)c.suspicion_mult * (uint64_t)ceil_log2(c.mem[v].table_size) * (uint64_t)c.ping_interval;
+  uint64_t deadline = c.T + ms / c.tick_ms;
+  *cp = c_with_deadline(cell | B_HAS_TIMER, deadline);
+  uint32_t b = (uint32_t)(deadline & c.wheel_mask);
+  uint32_t i = atomicAdd(&c.wheel_cnt[b], 1u);
+  if (i >= c.wheel_cap) { set_err(c, ERR_WHEEL); return; }
+  c.wheel[(size_t)b * c.wheel_cap + i] = ((uint64_t)v << 32) | s;
+}
+
+// ------------------------------------------------------------------------------- metadata fetch
+// MetadataStoreImpl.fetchMetadata (:146-185) + onMetadataRequest (:201-240): one round trip.
+__device__ inline bool fetch_ok(const Ctx& c, uint32_t v, uint32_t s, uint32_t phase) {
+  uint32_t f = c.mem[v].fetch_ctr++;
+  uint32_t w1 = draw(c, v, SWIM_STREAM_FETCH_REQ, phase, f);
+  uint32_t w2 = draw(c, v, SWIM_STREAM_FETCH_RESP, phase, f);
+  stat_add(c, ST_FETCHES, 1);
+  bool ok = !out_fail(c, v, s, w1) && in_pass(c, s, v) && !out_fail(c, s, v, w2) && in_pass(c, v, s);
+  if (ok) stat_add(c, ST_FETCH_OK, 1);
+  return ok;
+}
+
+// ------------------------------------------------------------------------------- updateMembership
+// MembershipProtocolImpl.updateMembership (:569-664).  Returns true when an ALIVE admission's
+// metadata fetch succeeded: the caller applies it (apply_alive) at its flush point.
+__device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, uint32_t st1, int32_t inc1,
+                                         int reason, uint32_t phase) {
+  MemberDev& m = c.mem[v];
+  uint64_t* cp = row(c, v) + s;
+  uint64_t cell = *cp;
+  const bool present = c_has(cell, B_IN_TABLE);
+  const uint32_t st0 = c_status(cell);
+  const int32_t inc0 = c_inc(cell);
+  const bool r0_leaving = present && st0 == SWIM_LEAVING;
+  if (!r0_leaving && !is_overrides(st1, inc1, present, st0, inc0)) return false;  // :593-602
+
+  if (s == v) {  // onSelfMemberDetected (:686-708)
+    int32_t cur = inc0 > inc1 ? inc0 : inc1;
+    *cp = c_with_record(cell, st0, cur + 1);
+    spread_gossip(c, v, v, st0, cur + 1);
+    return false;
+  }
+  if (st1 == SWIM_LEAVING) {  // onLeavingDetected (:710-733)
+    if (!present) m.table_size++;
+    cell = c_with_record(cell | B_IN_TABLE, SWIM_LEAVING, inc1);
+    *cp = cell;
+    if (present && (st0 == SWIM_ALIVE || (st0 == SWIM_SUSPECT && c_has(cell, B_ALIVE_EMITTED))))
+      publish_event(c, v, s, SWIM_EV_LEAVING, phase, next_minor(c, v, phase, s));
+    if (!present || st0 != SWIM_LEAVING) {
+      schedule_timer(c, v, s);
+      spread_gossip(c, v, s, SWIM_LEAVING, inc1);
+    }
+    return false;
+  }
+  if (st1 == SWIM_DEAD) {  // onDeadMemberDetected (:740-767)
+    cell &= ~B_HAS_TIMER;
+    if (!c_has(cell, B_IN_MEMBERS)) { *cp = cell; return false; }
+    *cp = 0;
+    atomicSub(&m.table_size, 1u);  // atomic: timer buckets are processed entry-parallel
+    atomicSub(&m.members_size, 1u);
+    publish_event(c, v, s, SWIM_EV_REMOVED, phase, next_minor(c, v, phase, s));
+    return false;
+  }
+  if (st1 == SWIM_SUSPECT) {  // :621-628
+    if (!r0_leaving) {
+      if (!present) m.table_size++;
+      *cp = c_with_record(cell | B_IN_TABLE, SWIM_SUSPECT, inc1);
+    }
+    schedule_timer(c, v, s);
+    if (reason != R_GOSSIP && reason != R_INITIAL_SYNC) spread_gossip(c, v, s, SWIM_SUSPECT, inc1);
+    return false;
+  }
+  // ALIVE (:630-660)
+  if (r0_leaving) {  // onAliveAfterLeaving (:666-684)
+    if (!c_has(cell, B_IN_MEMBERS)) { cell |= B_IN_MEMBERS; m.members_size++; }
+    if (!c_has(cell, B_ALIVE_EMITTED)) {
+      cell |= B_ALIVE_EMITTED;
+      *cp = cell;
+      publish_event(c, v, s, SWIM_EV_ADDED, phase, next_minor(c, v, phase, s));
+      publish_event(c, v, s, SWIM_EV_LEAVING, phase, next_minor(c, v, phase, s));
+    } else {
+      *cp = cell;
+    }
+    return false;
+  }
+  if (!present || inc0 < inc1) return fetch_ok(c, v, s, phase);
+  return false;
+}
+
+// doOnSuccess of the metadata fetch (:648-656) + onAliveMemberDetected (:769-795)
+__device__ inline void apply_alive(const Ctx& c, uint32_t v, uint32_t s, int32_t inc1, int reason, uint32_t phase) {
+  MemberDev& m = c.mem[v];
+  uint64_t* cp = row(c, v) + s;
+  *cp &= ~B_HAS_TIMER;  // cancelSuspicionTimeoutTask
+  if (reason != R_GOSSIP && reason != R_INITIAL_SYNC) spread_gossip(c, v, s, SWIM_ALIVE, inc1);
+  uint64_t cell = *cp | B_HAS_METADATA;
+  const bool exists = c_has(cell, B_IN_MEMBERS);
+  if (!c_has(cell, B_IN_TABLE)) m.table_size++;
+  if (!exists) m.members_size++;
+  cell = c_with_record(cell | B_IN_TABLE | B_IN_MEMBERS, SWIM_ALIVE, inc1);
+  if (!exists) cell |= B_ALIVE_EMITTED;
+  *cp = cell;
+  if (!exists) publish_event(c, v, s, SWIM_EV_ADDED, phase, next_minor(c, v, phase, s));
+}
+
+// Collections.shuffle: for (i = size; i > 1; i--) swap(i-1, nextInt(i))
+__device__ inline void shuffle_list(const Ctx& c, uint32_t v, uint32_t* list, uint32_t len, uint32_t stream) {
+  for (uint32_t i = len; i > 1; --i) {
+    uint32_t j = next_int(draw(c, v, stream, 0, i), i);
+    uint32_t t = list[i - 1];
+    list[i - 1] = list[j];
+    list[j] = t;
+  }
+}
+
+}  // namespace swimdev

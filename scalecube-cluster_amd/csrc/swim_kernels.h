@@ -1,0 +1,899 @@
+// swim_kernels.h — the HIP kernels of one lockstep tick.
+//
+// Phase A  k_timers, k_compact                       suspicion timeouts, list removals
+// Phase B  k_fd                                       ping / ping-req / ack resolution + FD events
+// Phase C  k_gossip_seg, k_gossip_emit, k_alloc, k_scatter_msgs, k_gossip_deliver
+// Phase D  k_sync_collect, k_snap_mark, k_snap_copy, k_scatter_reqs, k_sync_merge (D1 and D2)
+// lists    k_ins_scatter, k_ins_apply                 deferred pingMembers inserts of ADDED events
+// tick end k_end_tick
+//
+// Every kernel reads its work size from device memory (grid-stride over device counters), so the
+// host never synchronises inside a tick.
+#pragma once
+#include "swim_device.h"
+
+namespace swimdev {
+
+// per-tick scratch counters, zeroed by one hipMemsetAsync at the start of every tick
+struct Counters {
+  uint32_t msg_total, msg_recv_cnt, msg_cursor;
+  uint32_t req_total, req_recv_cnt, req_cursor;
+  uint32_t ack_total, ack_recv_cnt, ack_cursor;
+  uint32_t ins_total, ins_list_cnt, ins_cursor;
+  uint32_t compact_cnt;
+  uint32_t snap_total;
+  uint32_t pad[2];
+};
+
+struct Bufs {
+  Counters* k;
+  GMsgFull* msgs;      // produced in emit order
+  GMsgFull* msgs_out;  // grouped by receiver
+  uint32_t msg_cap;
+  uint32_t* msg_cnt;   // per receiver
+  uint32_t* msg_start;
+  uint32_t* msg_recv;  // receivers with messages
+  SyncReq* reqs;
+  SyncReq* reqs_out;
+  uint32_t req_cap;
+  uint32_t* req_cnt;
+  uint32_t* req_start;
+  uint32_t* req_recv;
+  SyncReq* acks;
+  SyncReq* acks_out;
+  uint32_t* ack_cnt;
+  uint32_t* ack_start;
+  uint32_t* ack_recv;
+  InsOp* ins_out;
+  uint32_t* ins_start;
+  uint64_t* snap;       // snapshot rows
+  uint32_t snap_cap;
+  uint32_t* snap_idx;   // per member: slot or NONE
+  uint32_t* snap_list;
+  uint64_t* pend;       // per sync-merge workgroup: pending ALIVE admissions
+};
+
+// ------------------------------------------------------------------------------- init
+__global__ void k_init_rows(Ctx c, uint32_t n_initial) {
+  const uint64_t conv = B_IN_TABLE | B_IN_MEMBERS | B_ALIVE_EMITTED | B_HAS_METADATA;
+  for (uint32_t v = blockIdx.x; v < c.n; v += gridDim.x) {
+    uint64_t* r = row(c, v);
+    const bool init = v < n_initial;
+    for (uint32_t s = threadIdx.x; s < c.n; s += blockDim.x)
+      r[s] = (init && s < n_initial) ? (s == v ? (B_IN_TABLE | B_IN_MEMBERS) : conv) : 0ull;
+  }
+}
+
+// initial members: converged state, seeded Fisher-Yates ping / remote lists
+__global__ void k_init_members(Ctx c, uint32_t n_initial, int32_t sync_stagger) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= c.n) return;
+  MemberDev m{};
+  m.ack_target = NONE;
+  m.relay_target = NONE;
+  m.leave_gossiper = NONE;
+  m.remote_idx = -1;
+  if (v < n_initial) {
+    m.up = 1;
+    m.joined = 1;
+    m.table_size = n_initial;
+    m.members_size = n_initial;
+    uint32_t* pl = c.ping + (size_t)v * c.n;
+    uint32_t* rl = c.remote + (size_t)v * c.n;
+    uint32_t k = 0;
+    for (uint32_t s = 0; s < n_initial; ++s)
+      if (s != v) { pl[k] = s; rl[k] = s; ++k; }
+    for (uint32_t i = k; i > 1; --i) {
+      uint32_t j = next_int(draw_at(c, v, 0, SWIM_STREAM_INIT_PING, 0, i), i);
+      uint32_t t = pl[i - 1]; pl[i - 1] = pl[j]; pl[j] = t;
+    }
+    for (uint32_t i = k; i > 1; --i) {
+      uint32_t j = next_int(draw_at(c, v, 0, SWIM_STREAM_INIT_REMOTE, 0, i), i);
+      uint32_t t = rl[i - 1]; rl[i - 1] = rl[j]; rl[j] = t;
+    }
+    m.ping_len = k;
+    m.remote_len = k;
+    m.remote_idx = 0;
+    m.sync_on = 1;
+    m.sync_start = sync_stagger ? -(int64_t)next_int(draw_at(c, v, 0, SWIM_STREAM_INIT_SYNC_PHASE, 0, 0), c.S) : 0;
+  }
+  c.mem[v] = m;
+}
+
+// ------------------------------------------------------------------------------- block scan helper
+// exclusive scan of one uint32 per thread across the workgroup; returns the total in *total
+template <int BLOCK>
+__device__ inline uint32_t block_exclusive_scan(uint32_t x, uint32_t* s_wave, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int w = 0; w < BLOCK / 64; ++w) { uint32_t t = s_wave[w]; s_wave[w] = acc; acc += t; }
+    s_wave[BLOCK / 64] = acc;
+  }
+  __syncthreads();
+  uint32_t r = s_wave[wave] + incl - x;
+  *total = s_wave[BLOCK / 64];
+  __syncthreads();
+  return r;
+}
+
+// ------------------------------------------------------------------------------- start joins
+__global__ void k_start_joins(Ctx c) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= c.n) return;
+  MemberDev& m = c.mem[v];
+  if (!m.join_pending) return;
+  m.join_pending = 0;
+  m.up = 1;
+  m.joined = 1;
+  m.join_now = 1;
+  m.fd_start = (int64_t)c.T;
+  m.g_start = (int64_t)c.T;
+  row(c, v)[v] = B_IN_TABLE | B_IN_MEMBERS;
+  m.table_size = 1;
+  m.members_size = 1;
+}
+
+// ------------------------------------------------------------------------------- phase A
+// onSuspicionTimeout (MembershipProtocolImpl.java:825-834) for every due (viewer, subject).
+// Entries of one viewer are independent (each touches only its own cell; counters are atomic),
+// so the bucket is processed entry-parallel; event order is canonicalised by minor = subject.
+__global__ void k_timers(Ctx c, uint32_t bucket) {
+  const uint32_t cnt = min(c.wheel_cnt[bucket], c.wheel_cap);
+  const uint64_t* ent = c.wheel + (size_t)bucket * c.wheel_cap;
+  const uint32_t tmask = (uint32_t)(c.T & SWIM_DEADLINE_MASK);
+  unsigned long long fired = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+    uint64_t e = ent[i];
+    uint32_t v = (uint32_t)(e >> 32), s = (uint32_t)e;
+    if (!c.mem[v].up) continue;
+    unsigned long long* cp = (unsigned long long*)(row(c, v) + s);
+    unsigned long long old = *cp;
+    bool claimed = false;
+    while (c_has(old, B_HAS_TIMER) && c_deadline(old) == tmask) {
+      unsigned long long prev = atomicCAS(cp, old, old & ~B_HAS_TIMER);
+      if (prev == old) { claimed = true; break; }
+      old = prev;
+    }
+    if (!claimed) continue;
+    fired++;
+    if (c_has(old, B_IN_TABLE)) update_membership(c, v, s, SWIM_DEAD, c_inc(old), R_TIMEOUT, SWIM_PHASE_TIMERS);
+  }
+  stat_add(c, ST_TIMERS_FIRED, fired);
+}
+
+// REMOVED -> pingMembers.remove / remoteMembers.remove (FailureDetectorImpl.java:323-333,
+// GossipProtocolImpl.java:240-251): both lists hold exactly the viewer's other `members`, so the
+// removal is a stable compaction keeping in_members entries.
+template <int BLOCK>
+__device__ void compact_list(const Ctx& c, uint32_t v, uint32_t* list, uint32_t& len) {
+  __shared__ uint32_t s_wave[BLOCK / 64 + 1];
+  const uint64_t* r = row(c, v);
+  uint32_t out = 0;
+  for (uint32_t base = 0; base < len; base += BLOCK) {
+    uint32_t i = base + threadIdx.x;
+    uint32_t val = 0, keep = 0;
+    if (i < len) { val = list[i]; keep = c_has(r[val], B_IN_MEMBERS) ? 1u : 0u; }
+    uint32_t total;
+    uint32_t pos = block_exclusive_scan<BLOCK>(keep, s_wave, &total);
+    if (keep) list[out + pos] = val;
+    out += total;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) len = out;
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_compact(Ctx c, Counters* k) {
+  const uint32_t cnt = k->compact_cnt;
+  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+    uint32_t v = c.compact_list[i];
+    MemberDev& m = c.mem[v];
+    compact_list<256>(c, v, c.ping + (size_t)v * c.n, m.ping_len);
+    compact_list<256>(c, v, c.remote + (size_t)v * c.n, m.remote_len);
+    if (threadIdx.x == 0) c.compact_flag[v] = 0;
+  }
+}
+
+// ------------------------------------------------------------------------------- phase B
+// publishPingResult (FailureDetectorImpl.java:377-380) -> onFailureDetectorEvent (:418-449)
+__device__ inline void publish_fd(const Ctx& c, uint32_t v, uint32_t t, uint32_t status, unsigned long long& nev) {
+  nev++;
+  MemberDev& m = c.mem[v];
+  if (c.record_fd)
+    emit(c, v, t, SWIM_EV_FD_ALIVE + (status == SWIM_ALIVE ? 0 : status == SWIM_SUSPECT ? 1 : 2), SWIM_PHASE_FD,
+         m.ev_minor++);
+  uint64_t cell = row(c, v)[t];
+  if (!c_has(cell, B_IN_TABLE)) return;
+  if (c_status(cell) == status) return;
+  if (status == SWIM_ALIVE) {
+    if (m.fd_sync_cnt >= FD_SYNC_MAX) { set_err(c, ERR_FDSYNC); return; }
+    c.fd_sync[(size_t)v * FD_SYNC_MAX + m.fd_sync_cnt++] = t;
+    return;
+  }
+  update_membership(c, v, t, status, c_inc(cell), R_FD_EVENT, SWIM_PHASE_FD);
+}
+
+// selectPingReqMembers (:363-375) as a forward partial Fisher-Yates over pingMembers \ {target}
+__device__ inline uint32_t select_relays(const Ctx& c, uint32_t v, uint32_t t, uint32_t* out) {
+  const int32_t k = c.ping_req_members;
+  if (k <= 0) return 0;
+  const MemberDev& m = c.mem[v];
+  const uint32_t* pl = c.ping + (size_t)v * c.n;
+  int64_t pos = -1;
+  for (uint32_t i = 0; i < m.ping_len; ++i)
+    if (pl[i] == t) { pos = i; break; }
+  const uint32_t cnt = m.ping_len - (pos >= 0 ? 1u : 0u);
+  if (cnt == 0) return 0;
+  const uint32_t r = min((uint32_t)k, cnt);
+  uint32_t swp_pos[32], swp_val[32];
+  uint32_t nsw = 0;
+  for (uint32_t i = 0; i < r; ++i) {
+    uint32_t j = i + next_int(draw(c, v, SWIM_STREAM_RELAY_SELECT, i, 0), cnt - i);
+    uint32_t vi = i, vj = j;
+    for (uint32_t q = 0; q < nsw; ++q) { if (swp_pos[q] == i) vi = swp_val[q]; if (swp_pos[q] == j) vj = swp_val[q]; }
+    // set(i, vj); set(j, vi)
+    bool fi = false, fj = false;
+    for (uint32_t q = 0; q < nsw; ++q) {
+      if (swp_pos[q] == i) { swp_val[q] = vj; fi = true; }
+      else if (swp_pos[q] == j) { swp_val[q] = vi; fj = true; }
+    }
+    if (!fi) { swp_pos[nsw] = i; swp_val[nsw] = vj; nsw++; }
+    if (!fj && j != i) { swp_pos[nsw] = j; swp_val[nsw] = vi; nsw++; }
+    if (j == i) { /* set(i, vj) then set(j, vi) with vi == vj: already consistent */ }
+    out[i] = (pos >= 0 && (int64_t)vj >= pos) ? pl[vj + 1] : pl[vj];
+  }
+  return r;
+}
+
+// doPing's error branch (:153-170) + doPingReq (:173-210); the relays share the ping's correlation
+// id, so the first relayed ack to reach the issuer completes every pending relay request.
+__device__ inline void ping_req(const Ctx& c, uint32_t v, uint32_t t, unsigned long long& nev,
+                                unsigned long long& nreq) {
+  uint32_t relays[16];
+  uint32_t nr = select_relays(c, v, t, relays);
+  if (nr == 0) { publish_fd(c, v, t, SWIM_SUSPECT, nev); return; }
+  nreq++;
+  uint32_t pending_mask = 0, npend = 0;
+  for (uint32_t j = 0; j < nr; ++j) {
+    if (out_fail(c, v, relays[j], draw(c, v, SWIM_STREAM_PINGREQ_OUT, j, 0))) publish_fd(c, v, t, SWIM_SUSPECT, nev);
+    else { pending_mask |= 1u << j; npend++; }
+  }
+  if (npend == 0) return;
+  int32_t arrived = -1;
+  for (uint32_t j = 0; j < nr; ++j) {
+    if (!(pending_mask & (1u << j))) continue;
+    uint32_t r = relays[j];
+    if (in_pass(c, r, v) && !out_fail(c, r, t, draw(c, v, SWIM_STREAM_TRANSIT_PING_OUT, j, 0)) &&
+        in_pass(c, t, r) && !out_fail(c, t, r, draw(c, v, SWIM_STREAM_TRANSIT_ACK_OUT, j, 0)) &&
+        in_pass(c, r, t) && !out_fail(c, r, v, draw(c, v, SWIM_STREAM_RELAY_ACK_OUT, j, 0))) {
+      arrived = (int32_t)j;
+      break;
+    }
+  }
+  if (arrived >= 0 && in_pass(c, v, relays[arrived])) {
+    for (uint32_t i = 0; i < npend; ++i) publish_fd(c, v, t, SWIM_ALIVE, nev);
+  } else {
+    MemberDev& m = c.mem[v];
+    m.relay_due = c.T + c.relay_ticks;
+    m.relay_target = t;
+    m.relay_pending = npend;
+  }
+}
+
+__global__ void k_fd(Ctx c) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= c.n) return;
+  MemberDev& m = c.mem[v];
+  if (!m.up) return;
+  const bool due = (int64_t)c.T > m.fd_start && ((int64_t)c.T - m.fd_start) % c.P == 0;
+  if (!due && m.relay_due != c.T && m.ack_due != c.T) return;
+  m.ev_minor = 0;
+  unsigned long long nev = 0, nreq = 0, npings = 0;
+  if (m.relay_due == c.T) {  // relay timeouts (:200-209)
+    uint32_t t = m.relay_target, k = m.relay_pending;
+    m.relay_due = 0;
+    for (uint32_t i = 0; i < k; ++i) publish_fd(c, v, t, SWIM_SUSPECT, nev);
+  }
+  if (m.ack_due == c.T) {  // pingTimeout elapsed
+    uint32_t t = m.ack_target;
+    m.ack_due = 0;
+    ping_req(c, v, t, nev, nreq);
+  }
+  if (due) {  // doPing (:126-171), selectPingMember (:352-361)
+    m.fd_period++;
+    if (m.ping_len > 0) {
+      uint32_t* pl = c.ping + (size_t)v * c.n;
+      if (m.ping_cursor >= m.ping_len) {
+        m.ping_cursor = 0;
+        shuffle_list(c, v, pl, m.ping_len, SWIM_STREAM_FD_SHUFFLE);
+      }
+      uint32_t t = pl[m.ping_cursor++];
+      npings++;
+      if (out_fail(c, v, t, draw(c, v, SWIM_STREAM_PING_OUT, 0, 0))) {
+        ping_req(c, v, t, nev, nreq);
+      } else if (in_pass(c, t, v) && !out_fail(c, t, v, draw(c, v, SWIM_STREAM_ACK_OUT, 0, 0)) && in_pass(c, v, t)) {
+        publish_fd(c, v, t, SWIM_ALIVE, nev);
+      } else {
+        m.ack_due = c.T + c.to_ticks;
+        m.ack_target = t;
+      }
+    }
+  }
+  stat_add(c, ST_FD_EVENTS, nev);
+  stat_add(c, ST_PING_REQS, nreq);
+  stat_add(c, ST_PINGS, npings);
+}
+
+// ------------------------------------------------------------------------------- phase C
+__device__ __forceinline__ bool gossip_due(const Ctx& c, const MemberDev& m) {
+  return m.up && (int64_t)c.T > m.g_start && ((int64_t)c.T - m.g_start) % c.G == 0;
+}
+
+// checkGossipSegmentation (GossipProtocolImpl.java:217-236); only launched when the threshold is
+// below the inline interval capacity (otherwise a clear can never trigger).
+__global__ void k_gossip_seg(Ctx c) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= c.n) return;
+  const MemberDev& m = c.mem[v];
+  if (!gossip_due(c, m)) return;
+  CollDev* base = c.coll + (size_t)v * c.hcap;
+  for (uint32_t i = 0; i < c.hcap; ++i)
+    if (base[i].key && (int32_t)base[i].n > c.seg_threshold) { base[i].n = 0; base[i].cleared = 1; }
+}
+
+// doSpreadGossip (:141-184): period++, select members, send, sweep, complete futures.
+__global__ void k_gossip_emit(Ctx c, Bufs b) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= c.n) return;
+  MemberDev& m = c.mem[v];
+  if (!gossip_due(c, m)) return;
+  const uint64_t period = m.g_period++;
+  m.period_used = period;
+  if (m.gossip_len == 0) return;
+  // selectGossipMembers (:322-343)
+  uint32_t targets[16];
+  uint32_t nt = 0;
+  uint32_t* rl = c.remote + (size_t)v * c.n;
+  const uint32_t F = (uint32_t)c.fanout;
+  if (m.remote_len < F) {
+    for (uint32_t i = 0; i < m.remote_len; ++i) targets[nt++] = rl[i];
+  } else {
+    if (m.remote_idx < 0 || (uint32_t)m.remote_idx + F > m.remote_len) {
+      shuffle_list(c, v, rl, m.remote_len, SWIM_STREAM_GOSSIP_SHUFFLE);
+      m.remote_idx = 0;
+    }
+    for (uint32_t i = 0; i < F; ++i) targets[nt++] = rl[m.remote_idx + i];
+    m.remote_idx += (int32_t)F;
+  }
+  const int32_t size1 = (int32_t)m.remote_len + 1;
+  const uint64_t spread = (uint64_t)(c.repeat_mult * ceil_log2((uint32_t)size1));
+  const uint64_t sweep = 2 * (spread + 1);
+  GossipDev* slab = c.slab + (size_t)v * c.gcap;
+  unsigned long long nmsg = 0;
+  for (uint32_t j = 0; j < nt; ++j) {
+    const uint32_t t = targets[j];
+    const bool t_up = c.mem[t].up != 0;
+    const int32_t loss = out_loss(c, v, t);
+    const bool pass = in_pass(c, t, v);
+    for (uint32_t p = 0; p < m.gossip_len; ++p) {  // selectGossipsToSend (:311-320)
+      const GossipDev g = slab[p];
+      if (!((uint64_t)g.inf_period + spread >= period)) continue;
+      if (g.inf0 == t || g.inf1 == t) continue;
+      nmsg++;
+      if (!t_up || lost(loss, draw(c, v, SWIM_STREAM_GOSSIP_OUT, j, p)) || !pass) continue;
+      // certain duplicate at the receiver: its collector already holds the sequence id and can
+      // only grow until delivery
+      if (coll_contains(coll_find(c, t, g.gossiper), g.seq)) continue;
+      uint32_t i = atomicAdd(&b.k->msg_total, 1u);
+      if (i >= b.msg_cap) { set_err(c, ERR_MSGS); continue; }
+      uint32_t slot = atomicAdd(&b.msg_cnt[t], 1u);
+      if (slot == 0) b.msg_recv[atomicAdd(&b.k->msg_recv_cnt, 1u)] = t;
+      GMsgFull msg;
+      msg.to = t; msg.from = v; msg.pos = p; msg.slot = slot;
+      msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
+      msg.inc = g.inc; msg.pad[0] = msg.pad[1] = msg.pad[2] = 0;
+      b.msgs[i] = msg;
+    }
+  }
+  stat_add(c, ST_GOSSIP_MESSAGES, nmsg);
+  // sweep (:158-164, :350-358), order preserving
+  uint32_t w = 0;
+  for (uint32_t p = 0; p < m.gossip_len; ++p) {
+    GossipDev g = slab[p];
+    if (period > (uint64_t)g.inf_period + sweep) continue;
+    if (w != p) slab[w] = g;
+    ++w;
+  }
+  m.gossip_len = w;
+  // futures (:167-180): the graceful-leave future stops the member at the end of the tick
+  if (m.leave_pending) {
+    for (uint32_t p = 0; p < w; ++p) {
+      const GossipDev& g = slab[p];
+      if (period > (uint64_t)g.inf_period + spread && g.gossiper == m.leave_gossiper && g.seq == (uint32_t)m.leave_seq)
+        m.leave_done = 1;
+    }
+  }
+}
+
+// group-by-receiver: region start per receiver, then scatter by (start + arrival slot)
+__global__ void k_alloc(const uint32_t* list, const uint32_t* list_cnt, const uint32_t* cnt, uint32_t* start,
+                        uint32_t* cursor) {
+  const uint32_t n = *list_cnt;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    uint32_t r = list[i];
+    start[r] = atomicAdd(cursor, cnt[r]);
+  }
+}
+
+__global__ void k_scatter_msgs(Bufs b) {
+  const uint32_t n = min(b.k->msg_total, b.msg_cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const GMsgFull m = b.msgs[i];
+    b.msgs_out[b.msg_start[m.to] + m.slot] = m;
+  }
+}
+
+__device__ __forceinline__ uint64_t msg_key(const GMsgFull& m) { return ((uint64_t)m.from << 32) | m.pos; }
+
+// heap sort of one receiver's messages by (sender, slab position)
+__device__ inline void sort_msgs(GMsgFull* a, uint32_t n) {
+  if (n < 2) return;
+  if (n <= 16) {
+    for (uint32_t i = 1; i < n; ++i) {
+      GMsgFull x = a[i];
+      uint64_t kx = msg_key(x);
+      int32_t j = (int32_t)i - 1;
+      while (j >= 0 && msg_key(a[j]) > kx) { a[j + 1] = a[j]; --j; }
+      a[j + 1] = x;
+    }
+    return;
+  }
+  auto sift = [&](uint32_t start, uint32_t end) {
+    uint32_t root = start;
+    while (2 * root + 1 < end) {
+      uint32_t ch = 2 * root + 1;
+      if (ch + 1 < end && msg_key(a[ch]) < msg_key(a[ch + 1])) ch++;
+      if (msg_key(a[root]) < msg_key(a[ch])) { GMsgFull t = a[root]; a[root] = a[ch]; a[ch] = t; root = ch; }
+      else return;
+    }
+  };
+  for (int64_t s = (int64_t)n / 2 - 1; s >= 0; --s) sift((uint32_t)s, n);
+  for (uint32_t e = n - 1; e > 0; --e) {
+    GMsgFull t = a[0]; a[0] = a[e]; a[e] = t;
+    sift(0, e);
+  }
+}
+
+// onGossipReq (GossipProtocolImpl.java:201-215) at each receiver, canonical order (sender, pos)
+__global__ void k_gossip_deliver(Ctx c, Bufs b) {
+  const uint32_t nrecv = b.k->msg_recv_cnt;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrecv; i += gridDim.x * blockDim.x) {
+    const uint32_t r = b.msg_recv[i];
+    const uint32_t k = b.msg_cnt[r];
+    GMsgFull* a = b.msgs_out + b.msg_start[r];
+    b.msg_cnt[r] = 0;
+    MemberDev& m = c.mem[r];
+    if (!m.up) continue;
+    sort_msgs(a, k);
+    m.ev_minor = 0;
+    m.fetch_ctr = 0;
+    unsigned long long acc = 0;
+    GossipDev* slab = c.slab + (size_t)r * c.gcap;
+    for (uint32_t q = 0; q < k; ++q) {
+      const GMsgFull g = a[q];
+      CollDev* col = coll_ensure(c, r, g.gossiper);
+      if (!col) continue;
+      const bool was_cleared = col->cleared != 0;
+      if (!coll_add(c, col, g.seq)) continue;
+      acc++;
+      int32_t found = -1;
+      if (was_cleared) {  // a GossipState can outlive its collector entry only after a clear
+        for (uint32_t p = 0; p < m.gossip_len; ++p)
+          if (slab[p].gossiper == g.gossiper && slab[p].seq == g.seq) { found = (int32_t)p; break; }
+      }
+      if (found < 0) {
+        if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); continue; }
+        GossipDev ns;
+        ns.gossiper = g.gossiper; ns.seq = g.seq; ns.subject = g.subject; ns.status = g.status; ns.inc = g.inc;
+        ns.inf_period = (uint32_t)m.g_period;
+        ns.inf0 = g.from;
+        ns.inf1 = NONE;
+        slab[m.gossip_len++] = ns;
+        // onMembershipGossip (MembershipProtocolImpl.java:452-459)
+        if (update_membership(c, r, g.subject, g.status, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP))
+          apply_alive(c, r, g.subject, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP);
+      } else {
+        GossipDev& st = slab[found];
+        if (st.inf0 != g.from && st.inf1 != g.from) {
+          if (st.inf0 == NONE) st.inf0 = g.from;
+          else if (st.inf1 == NONE) st.inf1 = g.from;
+          else set_err(c, ERR_INFECTED);
+        }
+      }
+    }
+    stat_add(c, ST_GOSSIP_ACCEPTED, acc);
+  }
+}
+
+// ------------------------------------------------------------------------------- list inserts
+__global__ void k_ins_scatter(Ctx c, Bufs b) {
+  const uint32_t n = min(*c.ins_total, c.ins_cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const InsOp op = c.ins[i];
+    b.ins_out[b.ins_start[op.v] + op.rank] = op;
+  }
+}
+
+// pingMembers.add(nextInt(size), member) (FailureDetectorImpl.java:334-345), in event order
+__global__ void __launch_bounds__(256) k_ins_apply(Ctx c, Bufs b) {
+  __shared__ uint32_t s_idx;
+  const uint32_t nv = *c.ins_list_cnt;
+  for (uint32_t i = blockIdx.x; i < nv; i += gridDim.x) {
+    const uint32_t v = c.ins_list[i];
+    const uint32_t k = c.ins_cnt[v];
+    const InsOp* ops = b.ins_out + b.ins_start[v];
+    MemberDev& m = c.mem[v];
+    uint32_t* pl = c.ping + (size_t)v * c.n;
+    for (uint32_t q = 0; q < k; ++q) {
+      const InsOp op = ops[q];
+      const uint32_t size = m.ping_len;
+      if (threadIdx.x == 0)
+        s_idx = size > 0 ? next_int(draw(c, v, SWIM_STREAM_PING_INSERT, op.phase, op.minor), size) : 0;
+      __syncthreads();
+      const uint32_t idx = s_idx;
+      // shift [idx, size) right by one, tail chunk first
+      for (int64_t hi = (int64_t)size; hi > (int64_t)idx; hi -= 256) {
+        int64_t lo = hi - 256 < (int64_t)idx ? (int64_t)idx : hi - 256;
+        int64_t p = lo + threadIdx.x;
+        uint32_t val = 0;
+        if (p < hi) val = pl[p];
+        __syncthreads();
+        if (p < hi) pl[p + 1] = val;
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) {
+        pl[idx] = op.s;
+        m.ping_len = size + 1;
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      c.ins_cnt[v] = 0;
+      m.ins_rank = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------- phase D
+// selectSyncAddress (MembershipProtocolImpl.java:461-472): uniform over seeds U otherMembers by
+// seeded rejection sampling.
+__device__ inline uint32_t select_sync_address(const Ctx& c, uint32_t v) {
+  const MemberDev& m = c.mem[v];
+  const uint64_t* r = row(c, v);
+  uint32_t count = m.members_size - 1;
+  for (uint32_t i = 0; i < c.n_seeds; ++i) {
+    uint32_t s = c.seeds[i];
+    if (s != v && !c_has(r[s], B_IN_MEMBERS)) count++;
+  }
+  if (count == 0) return NONE;
+  for (uint32_t i = 0; i < SWIM_SYNC_SELECT_ATTEMPTS; ++i) {
+    uint32_t x = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 0, i), c.n);
+    if (x != v && (c_has(r[x], B_IN_MEMBERS) || c.is_seed[x])) return x;
+  }
+  uint32_t k = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 1, 0), count);
+  for (uint32_t x = 0; x < c.n; ++x)
+    if (x != v && (c_has(r[x], B_IN_MEMBERS) || c.is_seed[x])) {
+      if (k == 0) return x;
+      --k;
+    }
+  return NONE;
+}
+
+enum : uint32_t { RQ_INITIAL = 1, RQ_OUTFAIL = 2, RQ_DELIVERED = 4, RQ_ACKED = 8 };
+
+__device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t to, uint32_t ordinal, bool initial) {
+  MemberDev& m = c.mem[v];
+  SyncReq q;
+  q.from = v; q.to = to; q.ordinal = ordinal; q.slot = 0; q.flags = initial ? RQ_INITIAL : 0;
+  q.pad[0] = q.pad[1] = q.pad[2] = 0;
+  if (initial) m.init_total++;
+  if (out_fail(c, v, to, draw(c, v, SWIM_STREAM_SYNC_OUT, ordinal, 0))) {
+    q.flags |= RQ_OUTFAIL;
+    if (initial) m.init_done++;
+  } else if (in_pass(c, to, v)) {
+    q.flags |= RQ_DELIVERED;
+    q.slot = atomicAdd(&b.req_cnt[to], 1u);
+    if (q.slot == 0) b.req_recv[atomicAdd(&b.k->req_recv_cnt, 1u)] = to;
+  }
+  uint32_t i = atomicAdd(&b.k->req_total, 1u);
+  if (i >= b.req_cap) { set_err(c, ERR_REQS); return; }
+  b.reqs[i] = q;
+}
+
+// doSync (:339-357), FD-triggered SYNCs (:427-442) and start0's initial SYNC to every seed (:250-291)
+__global__ void k_sync_collect(Ctx c, Bufs b) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= c.n) return;
+  MemberDev& m = c.mem[v];
+  if (!m.up) { m.fd_sync_cnt = 0; return; }
+  uint32_t k = 0;
+  unsigned long long nsync = 0;
+  if (m.sync_on && (int64_t)c.T > m.sync_start && ((int64_t)c.T - m.sync_start) % c.S == 0) {
+    uint32_t t = select_sync_address(c, v);
+    if (t != NONE) { add_req(c, b, v, t, k++, false); nsync++; }
+  }
+  for (uint32_t i = 0; i < m.fd_sync_cnt; ++i) {
+    add_req(c, b, v, c.fd_sync[(size_t)v * FD_SYNC_MAX + i], k++, false);
+    nsync++;
+  }
+  m.fd_sync_cnt = 0;
+  if (m.join_now) {
+    m.init_total = 0;
+    m.init_done = 0;
+    for (uint32_t i = 0; i < c.n_seeds; ++i) {
+      uint32_t s = c.seeds[i];
+      if (s != v) { add_req(c, b, v, s, k++, true); nsync++; }
+    }
+  }
+  stat_add(c, ST_SYNCS, nsync);
+}
+
+// Rows read as SYNC / SYNC_ACK content must be the sender's table as it was when the message was
+// prepared.  When that sender is itself a receiver in the same sub-phase its row is copied first.
+__global__ void k_snap_mark(Ctx c, Bufs b, const SyncReq* items, const uint32_t* total, uint32_t cap,
+                            const uint32_t* recv_cnt) {
+  const uint32_t n = min(*total, cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const SyncReq q = items[i];
+    if (!(q.flags & RQ_DELIVERED)) continue;
+    const uint32_t src = q.from;
+    if (recv_cnt[src] == 0) continue;
+    if (atomicCAS(&b.snap_idx[src], NONE, NONE - 1) == NONE) {
+      uint32_t slot = atomicAdd(&b.k->snap_total, 1u);
+      if (slot >= b.snap_cap) { set_err(c, ERR_SNAP); b.snap_idx[src] = NONE; continue; }
+      b.snap_list[slot] = src;
+      b.snap_idx[src] = slot;
+    }
+  }
+}
+
+__global__ void k_snap_copy(Ctx c, Bufs b) {
+  const uint32_t ns = min(b.k->snap_total, b.snap_cap);
+  const uint32_t chunks = (c.n + 4095) / 4096;
+  for (uint32_t w = blockIdx.x; w < ns * chunks; w += gridDim.x) {
+    uint32_t slot = w / chunks, ch = w % chunks;
+    const uint64_t* src = row(c, b.snap_list[slot]);
+    uint64_t* dst = b.snap + (size_t)slot * c.n;
+    for (uint32_t s = ch * 4096 + threadIdx.x; s < min(c.n, (ch + 1) * 4096); s += blockDim.x) dst[s] = src[s];
+  }
+}
+
+__global__ void k_snap_reset(Bufs b) {
+  const uint32_t ns = b.k->snap_total < b.snap_cap ? b.k->snap_total : b.snap_cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x)
+    b.snap_idx[b.snap_list[i]] = NONE;
+  __syncthreads();
+}
+
+__global__ void k_scatter_reqs(const SyncReq* items, const uint32_t* total, uint32_t cap, const uint32_t* start,
+                               SyncReq* out) {
+  const uint32_t n = min(*total, cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const SyncReq q = items[i];
+    if (!(q.flags & RQ_DELIVERED)) continue;
+    out[start[q.to] + q.slot] = q;
+  }
+}
+
+// SYNC_ACKs are produced with RQ_DELIVERED already set; this marks (to, slot) bookkeeping
+__device__ inline void add_ack(const Ctx& c, const Bufs& b, uint32_t to, uint32_t from, uint32_t rank, bool initial) {
+  SyncReq a;
+  a.from = from; a.to = to; a.ordinal = rank; a.flags = RQ_DELIVERED | (initial ? RQ_INITIAL : 0);
+  a.pad[0] = a.pad[1] = a.pad[2] = 0;
+  a.slot = atomicAdd(&b.ack_cnt[to], 1u);
+  if (a.slot == 0) b.ack_recv[atomicAdd(&b.k->ack_recv_cnt, 1u)] = to;
+  uint32_t i = atomicAdd(&b.k->ack_total, 1u);
+  if (i >= b.req_cap) { set_err(c, ERR_REQS); return; }
+  b.acks[i] = a;
+}
+
+constexpr int MERGE_BLOCK = 1024;
+constexpr int MERGE_CPT = 8;  // subjects per thread per tile
+constexpr int MERGE_TILE = MERGE_BLOCK * MERGE_CPT;
+
+// syncMembership (MembershipProtocolImpl.java:491-509) of one SYNC / SYNC_ACK into viewer v's row.
+// Workgroup-parallel over subjects: every thread classifies 8 consecutive (content, row) cell pairs;
+// records whose updateMembership would change nothing are skipped, the rest are compacted in
+// subject order and handed to thread 0, which runs the sequential merge on them.  ALIVE
+// admissions (fetch succeeded) are applied after the whole message, as the reference applies them
+// when the metadata round trips complete.
+__device__ inline bool sync_complex(uint64_t r1, uint64_t r0) {
+  const uint32_t s1 = c_status(r1);
+  const int32_t i1 = c_inc(r1);
+  const bool p0 = c_has(r0, B_IN_TABLE);
+  const uint32_t s0 = c_status(r0);
+  const int32_t i0 = c_inc(r0);
+  const bool r0_leaving = p0 && s0 == SWIM_LEAVING;
+  if (!r0_leaving && !is_overrides(s1, i1, p0, s0, i0)) return false;
+  if (r0_leaving && s1 == SWIM_LEAVING && i1 == i0) return false;
+  return true;
+}
+
+__device__ void merge_row(const Ctx& c, uint32_t v, const uint64_t* __restrict__ content, int reason, uint32_t phase,
+                          uint64_t* pend) {
+  __shared__ uint32_t s_list[MERGE_TILE];
+  __shared__ uint32_t s_wave[MERGE_BLOCK / 64 + 1];
+  uint64_t* __restrict__ rv = row(c, v);
+  const uint32_t n = c.n;
+  unsigned long long recs = 0;
+  uint32_t npend = 0;
+  for (uint32_t base = 0; base < n; base += MERGE_TILE) {
+    const uint32_t x0 = base + threadIdx.x * MERGE_CPT;
+    uint32_t flags = 0;
+    if (x0 + MERGE_CPT <= n) {
+      uint64_t a[MERGE_CPT], r[MERGE_CPT];
+#pragma unroll
+      for (int q = 0; q < MERGE_CPT; q += 2) {
+        const ulonglong2 va = *reinterpret_cast<const ulonglong2*>(content + x0 + q);
+        a[q] = va.x; a[q + 1] = va.y;
+      }
+#pragma unroll
+      for (int q = 0; q < MERGE_CPT; q += 2) {
+        const ulonglong2 vr = *reinterpret_cast<const ulonglong2*>(rv + x0 + q);
+        r[q] = vr.x; r[q + 1] = vr.y;
+      }
+#pragma unroll
+      for (int q = 0; q < MERGE_CPT; ++q) {
+        if (c_has(a[q], B_IN_TABLE)) {
+          recs++;
+          if (sync_complex(a[q], r[q])) flags |= 1u << q;
+        }
+      }
+    } else {
+      for (int q = 0; q < MERGE_CPT; ++q) {
+        const uint32_t x = x0 + q;
+        if (x >= n) break;
+        const uint64_t a = content[x];
+        if (c_has(a, B_IN_TABLE)) {
+          recs++;
+          if (sync_complex(a, rv[x])) flags |= 1u << q;
+        }
+      }
+    }
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan<MERGE_BLOCK>((uint32_t)__popc(flags), s_wave, &total);
+    if (total == 0) continue;  // uniform: total is the same in every thread
+    uint32_t o = off;
+    for (int q = 0; q < MERGE_CPT; ++q)
+      if (flags & (1u << q)) s_list[o++] = x0 + q;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (uint32_t i = 0; i < total; ++i) {
+        const uint32_t x = s_list[i];
+        const uint64_t a = content[x];
+        if (update_membership(c, v, x, c_status(a), c_inc(a), reason, phase))
+          pend[npend++] = ((uint64_t)x << 32) | (uint32_t)c_inc(a);
+      }
+    }
+    __syncthreads();
+  }
+  // wave-reduce the record count
+  for (int d = 32; d > 0; d >>= 1) recs += __shfl_down(recs, d, 64);
+  if ((threadIdx.x & 63) == 0) stat_add(c, ST_SYNC_RECORDS, recs);
+  if (threadIdx.x == 0) {
+    for (uint32_t i = 0; i < npend; ++i)
+      apply_alive(c, v, (uint32_t)(pend[i] >> 32), (int32_t)(uint32_t)pend[i], reason, phase);
+  }
+  __syncthreads();
+}
+
+__device__ inline void sort_reqs(SyncReq* a, uint32_t n) {
+  for (uint32_t i = 1; i < n; ++i) {
+    SyncReq x = a[i];
+    int32_t j = (int32_t)i - 1;
+    while (j >= 0 && (a[j].from > x.from || (a[j].from == x.from && a[j].ordinal > x.ordinal))) { a[j + 1] = a[j]; --j; }
+    a[j + 1] = x;
+  }
+}
+
+// D1 (acks == false): onSync at each receiver, then its SYNC_ACKs.  D2 (acks == true): the
+// SYNC_ACK merge at the original senders (MembershipProtocolImpl.java:363-415).
+__global__ void __launch_bounds__(MERGE_BLOCK) k_sync_merge(Ctx c, Bufs b, int d2) {
+  const uint32_t* recv = d2 ? b.ack_recv : b.req_recv;
+  const uint32_t nrecv = d2 ? b.k->ack_recv_cnt : b.k->req_recv_cnt;
+  uint32_t* cnt = d2 ? b.ack_cnt : b.req_cnt;
+  const uint32_t* start = d2 ? b.ack_start : b.req_start;
+  SyncReq* inbox_all = d2 ? b.acks_out : b.reqs_out;
+  const uint32_t phase = d2 ? SWIM_PHASE_SYNCACK : SWIM_PHASE_SYNC;
+  uint64_t* pend = b.pend + (size_t)blockIdx.x * c.n;
+  for (uint32_t i = blockIdx.x; i < nrecv; i += gridDim.x) {
+    const uint32_t s = recv[i];
+    const uint32_t k = cnt[s];
+    SyncReq* inbox = inbox_all + start[s];
+    if (threadIdx.x == 0) {
+      sort_reqs(inbox, k);
+      c.mem[s].ev_minor = 0;
+      c.mem[s].fetch_ctr = 0;
+    }
+    __syncthreads();
+    for (uint32_t q = 0; q < k; ++q) {
+      const SyncReq rq = inbox[q];
+      const uint32_t si = b.snap_idx[rq.from];
+      const uint64_t* content = si < b.snap_cap ? b.snap + (size_t)si * c.n : row(c, rq.from);
+      const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
+      merge_row(c, s, content, reason, phase, pend);
+    }
+    if (threadIdx.x == 0) {
+      if (!d2) {
+        for (uint32_t q = 0; q < k; ++q) {
+          const SyncReq rq = inbox[q];
+          if (out_fail(c, s, rq.from, draw(c, s, SWIM_STREAM_SYNCACK_OUT, q, 0))) continue;
+          if (!in_pass(c, rq.from, s)) continue;
+          if (rq.flags & RQ_INITIAL) atomicAdd(&c.mem[rq.from].init_done, 1u);
+          add_ack(c, b, rq.from, s, q, (rq.flags & RQ_INITIAL) != 0);
+        }
+      } else {
+        stat_add(c, ST_SYNC_ACKS, k);
+      }
+      cnt[s] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------- end of tick
+// start0's doFinally (:285-289) for members that joined this tick; graceful leaves complete.
+__global__ void k_end_tick(Ctx c) {
+  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= c.n) return;
+  MemberDev& m = c.mem[v];
+  if (m.join_now) {
+    m.sync_on = 1;
+    m.sync_start = (int64_t)c.T + (m.init_done == m.init_total ? 0 : (int64_t)c.sync_to_ticks);
+    m.join_now = 0;
+  }
+  if (m.leave_done) {
+    m.leave_done = 0;
+    m.leave_pending = 0;
+    m.up = 0;
+  }
+}
+
+// ------------------------------------------------------------------------------- KAT kernels
+__global__ void k_kat_overrides(const int32_t* cases, uint32_t n, uint8_t* out) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t* k = cases + 5 * i;
+  out[i] = is_overrides((uint32_t)k[0], k[1], k[2] != 0, (uint32_t)k[3], k[4]) ? 1 : 0;
+}
+
+__global__ void k_kat_collector(Ctx c, const uint8_t* kinds, const int64_t* values, uint32_t n, int64_t* res,
+                                CollDev* e) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  e->key = 1; e->n = 0; e->cleared = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t x = (uint32_t)values[i];
+    switch (kinds[i]) {
+      case 0: res[i] = coll_add(c, e, x) ? 1 : 0; break;
+      case 1: res[i] = coll_contains(e, x) ? 1 : 0; break;
+      case 2: res[i] = e->n; break;
+      default: e->n = 0; res[i] = 0; break;
+    }
+  }
+}
+
+__global__ void k_kat_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) philox4(ctr, key[0], key[1], out);
+}
+
+}  // namespace swimdev

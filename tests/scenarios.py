@@ -1,0 +1,135 @@
+"""Deterministic lockstep scenarios shared by the oracle tests, the GPU parity tests and the
+golden-fixture generator.  Each restates a configuration of BASELINE.json or a scenario of the
+reference's own test suites (FailureDetectorTest, MembershipProtocolTest, GossipProtocolTest) as a
+schedule of control operations at given ticks.
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+from swimgpu import abi
+
+
+@dataclasses.dataclass
+class Scenario:
+    name: str
+    capacity: int
+    n_initial: int
+    ticks: int
+    seed: int = 1
+    preset: int = 0
+    cfg: dict = dataclasses.field(default_factory=dict)
+    seeds: tuple = ()
+    ops: list = dataclasses.field(default_factory=list)  # (tick, op, args...) applied before tick+1
+    check_every: int = 10
+
+
+def apply_op(e: abi.Engine, op, args):
+    if op == "kill":
+        e.kill(*args)
+    elif op == "leave":
+        e.leave(*args)
+    elif op == "join":
+        e.join(*args)
+    elif op == "loss":
+        e.set_default_loss(*args)
+    elif op == "link_loss":
+        e.set_link_loss(*args)
+    elif op == "link_in":
+        e.set_link_inbound(*args)
+    elif op == "default_in":
+        e.set_default_inbound(*args)
+    elif op == "partition":
+        e.set_partition(None if args[0] is None else np.asarray(args[0], dtype=np.uint16))
+    else:
+        raise ValueError(op)
+
+
+def make_engine(lib, sc: Scenario) -> abi.Engine:
+    cfg = abi.default_config(lib, sc.preset, **sc.cfg)
+    e = abi.Engine(lib, cfg, sc.capacity, sc.n_initial, sc.seed)
+    if sc.seeds:
+        e.set_seeds(list(sc.seeds))
+    return e
+
+
+def run(e: abi.Engine, sc: Scenario, on_check=None):
+    """Advance `e` through the scenario; call on_check(tick) every check_every ticks and at the end."""
+    ops = sorted(sc.ops, key=lambda x: x[0])
+    t = 0
+    oi = 0
+    while t < sc.ticks:
+        while oi < len(ops) and ops[oi][0] <= t:
+            apply_op(e, ops[oi][1], ops[oi][2:])
+            oi += 1
+        nxt = min(sc.ticks, t + sc.check_every)
+        if oi < len(ops):
+            nxt = min(nxt, max(ops[oi][0], t + 1))
+        e.step_ticks(nxt - t)
+        t = nxt
+        if on_check and (t % sc.check_every == 0 or t == sc.ticks):
+            on_check(t)
+
+
+def _partition(n, split):
+    g = np.zeros(n, dtype=np.uint16)
+    g[split:] = 1
+    return g
+
+
+def catalog() -> list[Scenario]:
+    """Small scenarios (oracle-fast) used for bit-exact parity."""
+    fd_test = dict(ping_interval=200, ping_timeout=100, ping_req_members=2, gossip_interval=100,
+                   gossip_repeat_mult=2, sync_interval=15000, suspicion_mult=3, metadata_timeout=1000,
+                   record_fd_events=1)
+    mp_test = dict(sync_interval=500, sync_timeout=100, ping_interval=200, ping_timeout=100, metadata_timeout=100,
+                   record_fd_events=1)
+    return [
+        # BASELINE config 1: 3 members, LAN defaults, kill member 1 at period 5, run 30 periods
+        Scenario("config1_kill", 3, 3, 300, seed=11, ops=[(50, "kill", 1)]),
+        # FailureDetectorTest.testTrustedDespiteBadNetwork (:117-147): A->B outbound blocked
+        Scenario("fd_trusted_despite_bad_network", 3, 3, 60, seed=3, cfg=fd_test, ops=[(0, "link_loss", 0, 1, 100)]),
+        # FailureDetectorTest.testSuspected (:80-115): all outbound blocked
+        Scenario("fd_all_blocked", 3, 3, 80, seed=4, cfg=fd_test,
+                 ops=[(0, "link_loss", a, b, 100) for a in range(3) for b in range(3)]),
+        # FailureDetectorTest.testSuspectedMemberWithBadNetworkGetsPartitioned (:180-240) + recovery
+        Scenario("fd_isolated_then_recover", 4, 4, 160, seed=5, cfg=fd_test,
+                 ops=[(0, "link_loss", 0, b, 100) for b in range(4)] + [(40, "link_loss", 0, b, -1) for b in range(4)]),
+        # MembershipProtocolTest.testMemberLostNetworkDueNoOutboundThenRecover (:330-384)
+        Scenario("mp_member_lost_network", 3, 3, 40, seed=6, cfg=mp_test, seeds=(0, 1, 2),
+                 ops=[(10, "link_loss", 1, 0, 100), (10, "link_loss", 1, 2, 100), (10, "link_loss", 0, 1, 100),
+                      (10, "link_loss", 2, 1, 100), (20, "link_loss", 1, 0, -1), (20, "link_loss", 1, 2, -1),
+                      (20, "link_loss", 0, 1, -1), (20, "link_loss", 2, 1, -1)]),
+        # MembershipProtocolTest.testLongNetworkPartitionDueNoOutboundThenRemoved (:511-562)
+        Scenario("mp_long_partition_removed", 4, 4, 700, seed=7, cfg=mp_test, seeds=(0, 1, 2, 3),
+                 ops=[(20, "partition", [0, 0, 1, 1]), (600, "partition", None)]),
+        # MembershipProtocolTest.testNetworkPartitionManyDueNoInboundThenRemovedThenRecover (:1035-1109)
+        Scenario("mp_inbound_blocked_removed_recover", 4, 4, 700, seed=8, cfg=mp_test, seeds=(0, 1, 2, 3),
+                 ops=[(20, "default_in", 0, abi.ALL_MEMBERS), (400, "default_in", 1, abi.ALL_MEMBERS)]),
+        # MembershipProtocolTest.testLeaveCluster (:73-105): graceful shutdown -> LEAVING, REMOVED
+        Scenario("mp_leave_cluster", 3, 3, 400, seed=9, cfg=mp_test, seeds=(0, 1, 2), ops=[(40, "leave", 1, 1)]),
+        # joins through seeds (MembershipProtocolTest.testInitialPhaseOk :259-282, limited seeds)
+        Scenario("mp_joins_via_seed", 12, 6, 400, seed=10, cfg=mp_test, seeds=(0,),
+                 ops=[(5, "join", 6), (5, "join", 7), (23, "join", 8), (41, "join", 9), (41, "join", 10),
+                      (77, "join", 11), (150, "kill", 3)]),
+        # 64 members, 5 % uniform loss + kills, LAN defaults (config 3 in miniature)
+        Scenario("loss5_kills_64", 64, 64, 600, seed=12, cfg=dict(record_fd_events=1),
+                 ops=[(0, "loss", 5, abi.ALL_MEMBERS), (100, "kill", 9), (250, "kill", 40), (300, "kill", 41)],
+                 check_every=50),
+        # 48 members, churn: kills and joins through two seeds under 2 % loss
+        Scenario("churn_48", 48, 40, 800, seed=13, seeds=(0, 1),
+                 ops=[(0, "loss", 2, abi.ALL_MEMBERS)] + [(60 * i, "kill", 2 + 3 * i) for i in range(1, 6)]
+                 + [(60 * i + 7, "join", 39 + i) for i in range(1, 9)] + [(333, "leave", 20, 1)],
+                 check_every=50),
+        # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
+        Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),
+                 cfg=dict(sync_interval=5000), ops=[(100, "partition", _partition(32, 16)), (1100, "partition", None)],
+                 check_every=100),
+    ]
+
+
+def config2() -> Scenario:
+    """BASELINE config 2: 1,024 members, 0 % loss, kill member 17 at period 10, 150 periods."""
+    return Scenario("config2_1024", 1024, 1024, 1500, seed=2, ops=[(100, "kill", 17)], check_every=100)
