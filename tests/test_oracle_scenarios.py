@@ -1,0 +1,279 @@
+"""The reference's own scenario tests, restated on the lockstep oracle (virtual time).
+
+Each test mirrors one JUnit test: same topology, same fault schedule, same test configuration, and
+the same final-state assertions (trusted / suspected sets, event sequences, FD event statuses).
+Wall-clock sleeps (BaseTest.awaitSeconds / awaitSuspicion) become virtual-time steps.  The same
+scenarios run bit-exactly on the GPU in test_gpu_parity.py / test_gpu_scenarios.py.
+"""
+import pytest
+
+import oracle
+from swimgpu import abi
+from swimgpu.cluster import ClusterConfig, MembershipEvent, MemberStatus, SimulatedCluster
+
+Type = MembershipEvent.Type
+
+# MembershipProtocolTest.testConfig (:1111-1121)
+PING_INTERVAL = 200
+TEST_SYNC_INTERVAL = 500
+
+
+def mp_config(n):
+    return (ClusterConfig.default_config()
+            .membership(seed_members=tuple(range(n)), sync_interval=TEST_SYNC_INTERVAL, sync_timeout=100)
+            .failure_detector(ping_interval=PING_INTERVAL, ping_timeout=100)
+            .with_metadata_timeout(100))
+
+
+# FailureDetectorTest.createFd (:401-408): local config, pingTimeout 100, pingInterval 200, 2 relays.
+# The FD tests run the detector against a static member list; a huge suspicion multiplier keeps the
+# full stack from removing suspected members during the test window.
+def fd_config():
+    return (ClusterConfig.default_local_config()
+            .failure_detector(ping_timeout=100, ping_interval=200, ping_req_members=2)
+            .membership(suspicion_mult=1000))
+
+
+def make(config, n, seed=1, engine=None, lib=None, **knobs):
+    lib = lib or oracle.lib()
+    cfg = config.to_abi(lib, record_fd_events=1, **knobs)
+    e = engine or abi.Engine(lib, cfg, n, n, seed)
+    return SimulatedCluster.from_engine(e, config)
+
+
+def trusted(c, m):
+    return sorted(x.id for x in c.membership(m).members_by_status(MemberStatus.ALIVE))
+
+
+def suspected(c, m):
+    return sorted(x.id for x in c.membership(m).members_by_status(MemberStatus.SUSPECT))
+
+
+def next_fd_status(c, m, others):
+    """FailureDetectorTest.listenNextEventFor: first FD event per other member."""
+    first = {}
+    for ev in c.failure_detector(m).listen():
+        first.setdefault(ev.member.id, ev.status)
+    return {o: first.get(o) for o in others}
+
+
+# ------------------------------------------------------------------------------ FailureDetectorTest
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_fd_trusted(seed):  # :51-78
+    c = make(fd_config(), 3, seed)
+    c.step(4)
+    for m in range(3):
+        assert set(next_fd_status(c, m, [o for o in range(3) if o != m]).values()) == {MemberStatus.ALIVE}
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_fd_suspected(seed):  # :80-115
+    c = make(fd_config(), 3, seed)
+    for m in range(3):
+        c.network_emulator(m).block_outbound(0, 1, 2)
+    c.step(2)
+    for m in range(3):
+        assert set(next_fd_status(c, m, [o for o in range(3) if o != m]).values()) == {MemberStatus.SUSPECT}
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5])
+def test_fd_trusted_despite_bad_network(seed):  # :117-147
+    c = make(fd_config(), 3, seed)
+    c.network_emulator(0).block_outbound(1)
+    c.step(4)
+    for m in range(3):
+        evs = c.failure_detector(m).listen()
+        assert evs and all(e.status == MemberStatus.ALIVE for e in evs)
+
+
+def test_fd_suspected_member_with_bad_network_gets_partitioned():  # :180-240
+    c = make(fd_config(), 4, 7)
+    c.network_emulator(0).block_outbound(0, 1, 2, 3)
+    c.step(4)
+    assert set(next_fd_status(c, 0, [1, 2, 3]).values()) == {MemberStatus.SUSPECT}
+    for m in (1, 2, 3):
+        assert next_fd_status(c, m, [0])[0] == MemberStatus.SUSPECT
+    c.network_emulator(0).unblock_all_outbound()
+    c.await_seconds(4)
+    c.step(0)
+    for m in range(4):
+        c.failure_detector(m).listen()
+    c.step(4)
+    for m in range(4):
+        assert set(next_fd_status(c, m, [o for o in range(4) if o != m]).values()) == {MemberStatus.ALIVE}
+
+
+def test_fd_suspected_member_with_normal_network_gets_partitioned():  # :242-300
+    c = make(fd_config(), 4, 8)
+    for m in (0, 1, 2):
+        c.network_emulator(m).block_outbound(3)
+    c.step(4)
+    for m in (0, 1, 2):
+        assert next_fd_status(c, m, [3])[3] == MemberStatus.SUSPECT
+    assert set(next_fd_status(c, 3, [0, 1, 2]).values()) == {MemberStatus.SUSPECT}
+    for m in (0, 1, 2):
+        c.network_emulator(m).unblock_all_outbound()
+    c.await_seconds(4)
+    for m in range(4):
+        c.failure_detector(m).listen()
+    c.step(4)
+    for m in range(4):
+        assert set(next_fd_status(c, m, [o for o in range(4) if o != m]).values()) == {MemberStatus.ALIVE}
+
+
+def test_fd_member_status_change_after_network_recovery():  # :302-342
+    c = make(fd_config(), 2, 9)
+    c.network_emulator(0).block_outbound(1)
+    c.network_emulator(1).block_outbound(0)
+    c.step(2)
+    assert next_fd_status(c, 0, [1])[1] == MemberStatus.SUSPECT
+    assert next_fd_status(c, 1, [0])[0] == MemberStatus.SUSPECT
+    c.network_emulator(0).unblock_all_outbound()
+    c.network_emulator(1).unblock_all_outbound()
+    c.await_seconds(2)
+    c.failure_detector(0).listen()
+    c.failure_detector(1).listen()
+    c.step(2)
+    assert next_fd_status(c, 0, [1])[1] == MemberStatus.ALIVE
+    assert next_fd_status(c, 1, [0])[0] == MemberStatus.ALIVE
+
+
+# ------------------------------------------------------------------------------ MembershipProtocolTest
+def test_mp_initial_phase_ok():  # :259-282
+    c = make(mp_config(3), 3)
+    c.await_seconds(1)
+    for m in range(3):
+        assert trusted(c, m) == [0, 1, 2] and suspected(c, m) == []
+
+
+def test_mp_network_partition_due_no_outbound_then_recover():  # :284-328
+    c = make(mp_config(3), 3, 2)
+    c.await_seconds(3)
+    for m in range(3):
+        c.network_emulator(m).block_outbound(0, 1, 2)
+    c.await_suspicion(3)
+    for m in range(3):
+        assert trusted(c, m) == [m] and suspected(c, m) == []
+    for m in range(3):
+        c.network_emulator(m).unblock_all_outbound()
+    c.await_seconds(TEST_SYNC_INTERVAL * 2 / 1000)
+    for m in range(3):
+        assert trusted(c, m) == [0, 1, 2] and suspected(c, m) == []
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_mp_member_lost_network_due_no_outbound_then_recover(seed):  # :330-384
+    c = make(mp_config(3), 3, seed)
+    c.await_seconds(1)
+    for m in range(3):
+        assert trusted(c, m) == [0, 1, 2]
+    c.network_emulator(1).block_outbound(0, 2)
+    c.network_emulator(0).block_outbound(1)
+    c.network_emulator(2).block_outbound(1)
+    c.await_seconds(1)
+    assert trusted(c, 0) == [0, 2] and suspected(c, 0) == [1]
+    assert trusted(c, 1) == [1] and suspected(c, 1) == [0, 2]
+    assert trusted(c, 2) == [0, 2] and suspected(c, 2) == [1]
+    for m in range(3):
+        c.network_emulator(m).unblock_all_outbound()
+    c.await_seconds(1)
+    for m in range(3):
+        assert trusted(c, m) == [0, 1, 2] and suspected(c, m) == []
+
+
+def test_mp_network_partition_twice_due_no_outbound_then_recover():  # :386-454
+    c = make(mp_config(3), 3, 4)
+    c.await_seconds(1)
+    c.network_emulator(1).block_outbound(0, 2)
+    c.network_emulator(0).block_outbound(1)
+    c.network_emulator(2).block_outbound(1)
+    c.await_seconds(1)
+    assert suspected(c, 0) == [1] and suspected(c, 1) == [0, 2] and suspected(c, 2) == [1]
+    c.network_emulator(0).block_outbound(2)
+    c.network_emulator(2).block_outbound(0)
+    c.await_seconds(1)
+    for m in range(3):
+        assert trusted(c, m) == [m] and suspected(c, m) == [o for o in range(3) if o != m]
+    for m in range(3):
+        c.network_emulator(m).unblock_all_outbound()
+    c.await_seconds(1)
+    for m in range(3):
+        assert trusted(c, m) == [0, 1, 2] and suspected(c, m) == []
+
+
+def test_mp_long_network_partition_due_no_outbound_then_removed():  # :511-562
+    c = make(mp_config(4), 4, 5)
+    c.await_seconds(1)
+    c.network_emulator(0).block_outbound(2, 3)
+    c.network_emulator(1).block_outbound(2, 3)
+    c.network_emulator(2).block_outbound(0, 1)
+    c.network_emulator(3).block_outbound(0, 1)
+    c.await_seconds(2)
+    assert trusted(c, 0) == [0, 1] and suspected(c, 0) == [2, 3]
+    assert trusted(c, 2) == [2, 3] and suspected(c, 2) == [0, 1]
+    c.await_suspicion(4)
+    for m, side in ((0, [0, 1]), (1, [0, 1]), (2, [2, 3]), (3, [2, 3])):
+        assert trusted(c, m) == side and suspected(c, m) == []
+
+
+def test_mp_network_partition_many_due_no_inbound_then_removed_then_recover():  # :1035-1109
+    c = make(mp_config(4), 4, 6)
+    c.await_seconds(1)
+    for m in range(4):
+        c.membership(m).listen()
+    for m in range(4):
+        c.network_emulator(m).block_all_inbound()
+    c.await_seconds(2)
+    for m in range(4):
+        assert trusted(c, m) == [m] and suspected(c, m) == [o for o in range(4) if o != m]
+    c.await_suspicion(4)
+    for m in range(4):
+        removed = sorted(e.member.id for e in c.membership(m).listen() if e.is_removed())
+        assert removed == [o for o in range(4) if o != m]
+    for m in range(4):
+        c.network_emulator(m).unblock_all_inbound()
+    c.await_seconds(3)
+    for m in range(4):
+        assert trusted(c, m) == [0, 1, 2, 3] and suspected(c, m) == []
+
+
+def test_mp_leave_cluster():  # :73-105
+    c = make(mp_config(3), 3, 7)
+    c.await_seconds(2)
+    for m in range(3):
+        c.membership(m).listen()
+    c.shutdown(1)
+    c.await_seconds(2)
+    c.await_suspicion(3)
+    for m in (0, 2):
+        evs = [e for e in c.membership(m).listen() if not e.is_added()]
+        assert [(e.member.id, e.type) for e in evs[:2]] == [(1, Type.LEAVING), (1, Type.REMOVED)]
+
+
+# ------------------------------------------------------------------------------ BASELINE configs
+def test_config1_three_members_kill_one():
+    """BASELINE config 1: LAN defaults, kill member 1 at period 5; both survivors remove it."""
+    c = make(ClusterConfig.default_lan_config(), 3, 11)
+    c.step(5)
+    c.kill(1)
+    c.step(25)
+    for m in (0, 2):
+        evs = c.membership(m).listen()
+        assert [(e.member.id, e.type) for e in evs] == [(1, Type.REMOVED)]
+        assert trusted(c, m) == [0, 2]
+        # removal lands after suspicion timeout (5 * ceilLog2(3) * 1 s = 10 s) + detection
+        assert 15_000 <= evs[0].timestamp <= 18_000
+
+
+def test_config2_1024_single_failure_converges():
+    """BASELINE config 2: 1,024 members, kill 17 at period 10; every live member removes it once,
+    within detection + suspicion timeout (55 s at N=1024) + gossip dissemination."""
+    lib = oracle.lib()
+    c = make(ClusterConfig.default_lan_config(), 1024, 2, lib=lib)
+    c.step(10)
+    c.kill(17)
+    c.step(140)
+    removed = {v: [e for e in c.membership(v).listen() if e.is_removed()] for v in range(1024)}
+    assert all(len(removed[v]) == 1 and removed[v][0].member.id == 17 for v in range(1024) if v != 17)
+    t_rem = [removed[v][0].timestamp / 1000 for v in range(1024) if v != 17]
+    assert min(t_rem) >= 10 + 55 and max(t_rem) <= 10 + 55 + 20
