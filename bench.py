@@ -1,0 +1,159 @@
+"""Headline benchmark: simulated member-protocol-periods/sec at N=65,536 (BASELINE.json `metric`).
+
+One step = one SWIM protocol period (ping_interval of virtual time: 10 ticks of 100 ms with the LAN
+defaults) for all N members: FD pings / ping-reqs, 5 gossip rounds, staggered periodic SYNC
+(N/300 full-table exchanges per tick), suspicion timers and event compaction — the whole hot path of
+SURVEY.md §8 on synthetic input (a converged N-member cluster losing one member every 20 periods).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--members 65536]
+
+Prints ONE JSON line with `value` (whole-job member-periods/s), the `roofline` object of the
+dominant kernel (k_sync_merge, the SYNC row merge; HIP events on the engine's stream) and the
+`cpu_baseline` (the CPU oracle, 1 thread, bounded sample, rank 0 / N=1 only).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "scalecube-cluster_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s)
+KILL_EVERY = 20
+KILL_FIRST = 10
+
+
+def kill_schedule(n, periods_lo, periods_hi):
+    """Members killed at the start of each period in [lo, hi): one every KILL_EVERY periods."""
+    out = {}
+    for p in range(periods_lo, periods_hi):
+        if p >= KILL_FIRST and (p - KILL_FIRST) % KILL_EVERY == 0:
+            j = (p - KILL_FIRST) // KILL_EVERY
+            out[p] = (17 + 7919 * j) % n
+    return out
+
+
+def make_config(lib, device=0):
+    from swimgpu import abi
+    return abi.default_config(lib, 0, sync_stagger=1, record_fd_events=0, device=device)
+
+
+def run_periods(e, p0, p1):
+    sched = kill_schedule(e.capacity, p0, p1)
+    p = p0
+    while p < p1:
+        if p in sched:
+            e.kill(sched[p])
+        nxt = min([q for q in sched if q > p] + [p1])
+        e.step(nxt - p)
+        p = nxt
+
+
+def cpu_baseline(n, periods):
+    """The CPU oracle (oracle/liboracle_swim.so, 1 thread for the timed ticks) on the same N and
+    workload, bounded to `periods` periods from the converged start."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    from swimgpu import abi
+    lib = oracle.lib()
+    cfg = abi.default_config(lib, 0, sync_stagger=1, record_fd_events=0)
+    e = abi.Engine(lib, cfg, n, n, 1)
+    t0 = time.perf_counter()
+    run_periods(e, 0, periods)
+    dt = time.perf_counter() - t0
+    e.close()
+    return {"value": n * periods / dt, "unit": "member-periods/s", "cores": 1, "kind": "port",
+            "sample": f"CPU oracle (C++ lockstep restatement, 1 thread), N={n}, LAN defaults, "
+                      f"periods 0..{periods} from the converged start ({dt:.1f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--members", type=int, default=65536)
+    ap.add_argument("--cpu-periods", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    torch.cuda.set_device(local_rank)
+
+    import swimgpu
+    from swimgpu import abi
+    lib = swimgpu.load_library()
+    n = args.members
+    e = abi.Engine(lib, make_config(lib, local_rank), n, n, 1 + rank)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    run_periods(e, 0, args.warmup)
+    e.drain_events()
+    barrier()
+    e.profile_enable(True)
+    t0 = time.perf_counter()
+    run_periods(e, args.warmup, args.warmup + args.steps)
+    barrier()
+    dt = time.perf_counter() - t0
+    prof = e.profile_merge()
+    stats = e.stats()
+    e.drain_events()
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if stats["capacity_errors"]:
+        raise SystemExit(f"capacity error during the benchmark: {stats['capacity_errors']:#x}")
+
+    value = n * args.steps * world / dt
+    avg_ms = prof["total_ms"] / max(1, prof["launches"])
+    achieved = prof["alg_bytes"] / max(1e-12, prof["total_ms"] / 1e3) / 1e9
+    line = {
+        "metric": "simulated member-protocol-periods/sec at N=65,536; achieved HBM GB/s",
+        "value": value,
+        "unit": "member-periods/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic",
+        "config": {"workload": f"config4-lan: N={n} members per GPU, LAN defaults (ping 1 s / gossip 200 ms / "
+                               f"sync 30 s staggered), 0% loss, one member killed every {KILL_EVERY} periods",
+                   "members": n, "tick_ms": 100, "parallelism": f"replicas x{world}" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "kernel": "k_sync_merge", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "launches": prof["launches"], "avg_launch_ms": avg_ms,
+                     "alg_bytes_per_launch": prof["alg_bytes"] / max(1, prof["launches"]),
+                     "merge_ms_share": prof["total_ms"] / (dt * 1e3)},
+        "stats": {k: stats[k] for k in ("syncs", "sync_records", "gossip_messages", "gossips_created", "pings",
+                                         "timers_fired", "events")},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        e.close()
+        line["cpu_baseline"] = cpu_baseline(n, args.cpu_periods)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

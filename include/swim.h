@@ -115,7 +115,8 @@ typedef struct swim_config {
   uint32_t collector_capacity;/* max distinct gossipers whose SequenceIdCollector a member holds
                                  (power of two; 0 = default 256) */
   uint32_t event_capacity;    /* undrained events the engine may buffer (0 = default 1<<22) */
-  uint32_t reserved[8];
+  int32_t device;             /* HIP device ordinal the engine runs on (one engine per GPU) */
+  uint32_t reserved[7];
 } swim_config;
 
 /* preset: 0 = defaultConfig/defaultLanConfig, 1 = defaultWanConfig, 2 = defaultLocalConfig
@@ -265,6 +266,22 @@ typedef struct swim_interval {
 /* SequenceIdCollector of (m, gossiper): closed intervals in ascending order. */
 int32_t swim_read_collector(swim_engine* e, uint32_t m, uint32_t gossiper, swim_interval* out,
                             uint32_t cap, uint32_t* len);
+
+/* ---- measurement ---------------------------------------------------------------------------
+ * Per-kernel timing of the SYNC row-merge kernel (the dominant HBM stream), measured with HIP
+ * events recorded around every launch on the engine's own stream.  `alg_bytes` counts algorithmic
+ * bytes: per merged SYNC / SYNC_ACK message the content row and the receiver row (2 x N x 8 B) plus
+ * 8 B per record that changed the receiver's table.  enable = 0 stops recording; enable = 1
+ * (re)starts it from zero.  The CPU oracle reports zeros. */
+typedef struct swim_kernel_profile {
+  uint64_t launches;
+  double total_ms;
+  uint64_t messages;   /* SYNC + SYNC_ACK messages merged */
+  uint64_t records;    /* records that changed a table (sequential merge path) */
+  uint64_t alg_bytes;
+} swim_kernel_profile;
+int32_t swim_profile_enable(swim_engine* e, int32_t enable);
+int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out);
 
 /* ---- known-answer hooks (run the engine's own merge / dedupe code on given inputs) --------- */
 /* Philox4x32-10 block used by every draw site. */

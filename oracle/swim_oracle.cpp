@@ -868,6 +868,14 @@ int32_t swim_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4
   return SWIM_OK;
 }
 
+int32_t swim_profile_enable(swim_engine* e, int32_t) { return e ? SWIM_OK : SWIM_EINVAL; }
+
+int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out) {
+  if (!e || !out) return SWIM_EINVAL;
+  std::memset(out, 0, sizeof(*out));
+  return SWIM_OK;
+}
+
 int32_t swim_kat_overrides(const int32_t* cases, uint32_t n, uint8_t* out) {
   if (n && (!cases || !out)) return SWIM_EINVAL;
   for (uint32_t i = 0; i < n; ++i) {

@@ -46,6 +46,7 @@ hipError_t dalloc(T** p, size_t count) {
 
 struct swim_engine {
   swim_config cfg{};
+  int32_t device = 0;
   uint32_t n = 0, tick_ms = 0, P = 0, G = 0, S = 0;
   uint64_t T = 0;
   hipStream_t stream = nullptr;
@@ -64,9 +65,17 @@ struct swim_engine {
   uint64_t host_ticks = 0, host_events = 0;
   uint32_t err_seen = 0;
   std::vector<void*> allocs;
+  // swim_profile_*: HIP events around every k_sync_merge launch on `stream`
+  bool prof = false;
+  std::vector<hipEvent_t> prof_ev;
+  uint32_t prof_used = 0;
+  double prof_ms = 0;
+  uint64_t prof_launches = 0;
+  unsigned long long prof_base_msgs = 0, prof_base_recs = 0;
 
   ~swim_engine() {
     if (stream) hipStreamSynchronize(stream);
+    for (hipEvent_t ev : prof_ev) hipEventDestroy(ev);
     for (void* p : allocs) hipFree(p);
     if (stream) hipStreamDestroy(stream);
   }
@@ -89,6 +98,25 @@ static int32_t hip_status() {
 
 static uint32_t grid_for(uint32_t n, uint32_t block) { return std::max(1u, (n + block - 1) / block); }
 
+static void prof_flush(swim_engine* e) {
+  for (uint32_t i = 0; i < e->prof_used; ++i) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e->prof_ev[2 * i], e->prof_ev[2 * i + 1]) == hipSuccess) e->prof_ms += ms;
+  }
+  e->prof_launches += e->prof_used;
+  e->prof_used = 0;
+}
+
+static void launch_merge(swim_engine* e, int d2) {
+  const bool p = e->prof && 2 * (e->prof_used + 1) <= e->prof_ev.size();
+  if (p) hipEventRecord(e->prof_ev[2 * e->prof_used], e->stream);
+  k_sync_merge<<<kMergeGrid, MERGE_BLOCK, 0, e->stream>>>(e->c, e->b, d2);
+  if (p) {
+    hipEventRecord(e->prof_ev[2 * e->prof_used + 1], e->stream);
+    e->prof_used++;
+  }
+}
+
 static int32_t sync_and_collect(swim_engine* e) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return hip_status() ? SWIM_EDEVICE : SWIM_EDEVICE;
   uint32_t cnt = 0, err = 0;
@@ -105,6 +133,7 @@ static int32_t sync_and_collect(swim_engine* e) {
     if (hipMemcpy(e->c.ev_cnt, &zero, 4, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
   }
   e->err_seen |= err;
+  if (e->prof) prof_flush(e);
   return err ? SWIM_ECAPACITY : SWIM_OK;
 }
 
@@ -154,14 +183,14 @@ static void run_tick(swim_engine* e) {
   k_snap_copy<<<256, 256, 0, s>>>(c, b);
   k_alloc<<<64, 256, 0, s>>>(b.req_recv, &e->k->req_recv_cnt, b.req_cnt, b.req_start, &e->k->req_cursor);
   k_scatter_reqs<<<64, 256, 0, s>>>(b.reqs, &e->k->req_total, b.req_cap, b.req_start, b.reqs_out);
-  k_sync_merge<<<kMergeGrid, MERGE_BLOCK, 0, s>>>(c, b, 0);
+  launch_merge(e, 0);
   k_snap_reset<<<4, 256, 0, s>>>(b);
   hipMemsetAsync(&e->k->snap_total, 0, sizeof(uint32_t), s);
   k_snap_mark<<<64, 256, 0, s>>>(c, b, b.acks, &e->k->ack_total, b.req_cap, b.ack_cnt);
   k_snap_copy<<<256, 256, 0, s>>>(c, b);
   k_alloc<<<64, 256, 0, s>>>(b.ack_recv, &e->k->ack_recv_cnt, b.ack_cnt, b.ack_start, &e->k->ack_cursor);
   k_scatter_reqs<<<64, 256, 0, s>>>(b.acks, &e->k->ack_total, b.req_cap, b.ack_start, b.acks_out);
-  k_sync_merge<<<kMergeGrid, MERGE_BLOCK, 0, s>>>(c, b, 1);
+  launch_merge(e, 1);
   k_snap_reset<<<4, 256, 0, s>>>(b);
   run_ins_pipeline(e);
   // ---- end of tick
@@ -172,6 +201,7 @@ static int32_t upload_links(swim_engine* e) {
   auto& L = e->links_h;
   std::sort(L.begin(), L.end(), [](const LinkDev& x, const LinkDev& y) { return x.a < y.a || (x.a == y.a && x.b < y.b); });
   if (L.size() > e->links_dev_cap) {
+    if (hipSetDevice(e->device) != hipSuccess) return SWIM_EDEVICE;
     uint32_t cap = next_pow2((uint32_t)L.size());
     LinkDev* p = nullptr;
     if (!e->alloc(&p, cap)) return SWIM_ENOMEM;
@@ -294,10 +324,13 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
     return SWIM_EINVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SWIM_EDEVICE;
+  if (cf.device < 0 || cf.device >= ndev) return SWIM_EINVAL;
+  if (hipSetDevice(cf.device) != hipSuccess) return SWIM_EDEVICE;
 
   swim_engine* e = new (std::nothrow) swim_engine();
   if (!e) return SWIM_ENOMEM;
   e->cfg = cf;
+  e->device = cf.device;
   e->n = capacity;
   e->tick_ms = tick;
   e->P = (uint32_t)cf.ping_interval / tick;
@@ -395,6 +428,7 @@ int32_t swim_destroy(swim_engine* e) {
 
 int32_t swim_step_ticks(swim_engine* e, uint32_t ticks) {
   if (!e) return SWIM_EINVAL;
+  if (hipSetDevice(e->device) != hipSuccess) return SWIM_EDEVICE;
   int32_t rc = SWIM_OK;
   for (uint32_t i = 0; i < ticks; ++i) {
     run_tick(e);
@@ -669,6 +703,39 @@ int32_t swim_read_collector(swim_engine* e, uint32_t v, uint32_t gossiper, swim_
     }
     break;
   }
+  return SWIM_OK;
+}
+
+int32_t swim_profile_enable(swim_engine* e, int32_t enable) {
+  if (!e) return SWIM_EINVAL;
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  if (e->prof_ev.empty()) {
+    e->prof_ev.resize(4 * kDrainEvery + 4);
+    for (auto& ev : e->prof_ev)
+      if (hipEventCreate(&ev) != hipSuccess) return SWIM_EDEVICE;
+  }
+  e->prof_used = 0;
+  e->prof_ms = 0;
+  e->prof_launches = 0;
+  unsigned long long st[ST_COUNT];
+  if (hipMemcpy(st, e->c.stats, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+  e->prof_base_msgs = st[ST_MERGE_MSGS];
+  e->prof_base_recs = st[ST_MERGE_RECORDS];
+  e->prof = enable != 0;
+  return SWIM_OK;
+}
+
+int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out) {
+  if (!e || !out) return SWIM_EINVAL;
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  prof_flush(e);
+  unsigned long long st[ST_COUNT];
+  if (hipMemcpy(st, e->c.stats, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+  out->launches = e->prof_launches;
+  out->total_ms = e->prof_ms;
+  out->messages = st[ST_MERGE_MSGS] - e->prof_base_msgs;
+  out->records = st[ST_MERGE_RECORDS] - e->prof_base_recs;
+  out->alg_bytes = out->messages * (uint64_t)e->n * 16ull + out->records * 8ull;
   return SWIM_OK;
 }
 

@@ -35,7 +35,9 @@ enum : uint32_t {
 // stats slots (swim_stats order)
 enum { ST_TICKS, ST_PINGS, ST_PING_REQS, ST_FD_EVENTS, ST_GOSSIPS_CREATED, ST_GOSSIP_MESSAGES,
        ST_GOSSIP_ACCEPTED, ST_SYNCS, ST_SYNC_ACKS, ST_SYNC_RECORDS, ST_FETCHES, ST_FETCH_OK,
-       ST_TIMERS_FIRED, ST_EVENTS, ST_CAPACITY_ERRORS, ST_COUNT = 24 };
+       ST_TIMERS_FIRED, ST_EVENTS, ST_CAPACITY_ERRORS,
+       ST_MERGE_MSGS, ST_MERGE_RECORDS,  // swim_profile_merge accounting
+       ST_COUNT = 24 };
 
 enum Reason { R_FD_EVENT, R_GOSSIP, R_SYNC, R_INITIAL_SYNC, R_TIMEOUT };
 

@@ -717,7 +717,7 @@ constexpr int MERGE_TILE = MERGE_BLOCK * MERGE_CPT;
 // subject order and handed to thread 0, which runs the sequential merge on them.  ALIVE
 // admissions (fetch succeeded) are applied after the whole message, as the reference applies them
 // when the metadata round trips complete.
-__device__ inline bool sync_complex(uint64_t r1, uint64_t r0) {
+__device__ inline bool sync_complex(uint64_t r1, uint64_t r0, bool self) {
   const uint32_t s1 = c_status(r1);
   const int32_t i1 = c_inc(r1);
   const bool p0 = c_has(r0, B_IN_TABLE);
@@ -725,7 +725,9 @@ __device__ inline bool sync_complex(uint64_t r1, uint64_t r0) {
   const int32_t i0 = c_inc(r0);
   const bool r0_leaving = p0 && s0 == SWIM_LEAVING;
   if (!r0_leaving && !is_overrides(s1, i1, p0, s0, i0)) return false;
-  if (r0_leaving && s1 == SWIM_LEAVING && i1 == i0) return false;
+  // an identical LEAVING record over a LEAVING row is a no-op put, except on the viewer's own row,
+  // where it re-runs onSelfMemberDetected (MembershipProtocolImpl.java:593-607)
+  if (r0_leaving && s1 == SWIM_LEAVING && i1 == i0 && !self) return false;
   return true;
 }
 
@@ -735,7 +737,7 @@ __device__ void merge_row(const Ctx& c, uint32_t v, const uint64_t* __restrict__
   __shared__ uint32_t s_wave[MERGE_BLOCK / 64 + 1];
   uint64_t* __restrict__ rv = row(c, v);
   const uint32_t n = c.n;
-  unsigned long long recs = 0;
+  unsigned long long recs = 0, changed = 0;
   uint32_t npend = 0;
   for (uint32_t base = 0; base < n; base += MERGE_TILE) {
     const uint32_t x0 = base + threadIdx.x * MERGE_CPT;
@@ -756,7 +758,7 @@ __device__ void merge_row(const Ctx& c, uint32_t v, const uint64_t* __restrict__
       for (int q = 0; q < MERGE_CPT; ++q) {
         if (c_has(a[q], B_IN_TABLE)) {
           recs++;
-          if (sync_complex(a[q], r[q])) flags |= 1u << q;
+          if (sync_complex(a[q], r[q], x0 + q == v)) flags |= 1u << q;
         }
       }
     } else {
@@ -766,7 +768,7 @@ __device__ void merge_row(const Ctx& c, uint32_t v, const uint64_t* __restrict__
         const uint64_t a = content[x];
         if (c_has(a, B_IN_TABLE)) {
           recs++;
-          if (sync_complex(a, rv[x])) flags |= 1u << q;
+          if (sync_complex(a, rv[x], x == v)) flags |= 1u << q;
         }
       }
     }
@@ -778,6 +780,7 @@ __device__ void merge_row(const Ctx& c, uint32_t v, const uint64_t* __restrict__
       if (flags & (1u << q)) s_list[o++] = x0 + q;
     __syncthreads();
     if (threadIdx.x == 0) {
+      changed += total;
       for (uint32_t i = 0; i < total; ++i) {
         const uint32_t x = s_list[i];
         const uint64_t a = content[x];
@@ -791,6 +794,7 @@ __device__ void merge_row(const Ctx& c, uint32_t v, const uint64_t* __restrict__
   for (int d = 32; d > 0; d >>= 1) recs += __shfl_down(recs, d, 64);
   if ((threadIdx.x & 63) == 0) stat_add(c, ST_SYNC_RECORDS, recs);
   if (threadIdx.x == 0) {
+    stat_add(c, ST_MERGE_RECORDS, changed);
     for (uint32_t i = 0; i < npend; ++i)
       apply_alive(c, v, (uint32_t)(pend[i] >> 32), (int32_t)(uint32_t)pend[i], reason, phase);
   }
@@ -821,6 +825,7 @@ __global__ void __launch_bounds__(MERGE_BLOCK) k_sync_merge(Ctx c, Bufs b, int d
     const uint32_t k = cnt[s];
     SyncReq* inbox = inbox_all + start[s];
     if (threadIdx.x == 0) {
+      stat_add(c, ST_MERGE_MSGS, k);
       sort_reqs(inbox, k);
       c.mem[s].ev_minor = 0;
       c.mem[s].fetch_ctr = 0;

@@ -59,7 +59,8 @@ class swim_config(C.Structure):
         ("gossip_capacity", C.c_uint32),
         ("collector_capacity", C.c_uint32),
         ("event_capacity", C.c_uint32),
-        ("reserved", C.c_uint32 * 8),
+        ("device", C.c_int32),
+        ("reserved", C.c_uint32 * 7),
     ]
 
 
@@ -140,6 +141,11 @@ class swim_interval(C.Structure):
     _fields_ = [("lo", C.c_uint64), ("hi", C.c_uint64)]
 
 
+class swim_kernel_profile(C.Structure):
+    _fields_ = [("launches", C.c_uint64), ("total_ms", C.c_double), ("messages", C.c_uint64),
+                ("records", C.c_uint64), ("alg_bytes", C.c_uint64)]
+
+
 _u32p = POINTER(C.c_uint32)
 _u64p = POINTER(C.c_uint64)
 _engp = C.c_void_p
@@ -172,6 +178,8 @@ PROTOTYPES = {
     "swim_read_remote_list": (C.c_int32, [_engp, C.c_uint32, _u32p, C.c_uint32, _u32p]),
     "swim_read_gossips": (C.c_int32, [_engp, C.c_uint32, POINTER(swim_gossip), C.c_uint32, _u32p]),
     "swim_read_collector": (C.c_int32, [_engp, C.c_uint32, C.c_uint32, POINTER(swim_interval), C.c_uint32, _u32p]),
+    "swim_profile_enable": (C.c_int32, [_engp, C.c_int32]),
+    "swim_profile_merge": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_philox": (C.c_int32, [_u32p, _u32p, _u32p]),
     "swim_kat_overrides": (C.c_int32, [POINTER(C.c_int32), C.c_uint32, POINTER(C.c_uint8)]),
     "swim_kat_collector": (C.c_int32, [POINTER(C.c_uint8), POINTER(C.c_int64), C.c_uint32, POINTER(C.c_int64)]),
@@ -326,6 +334,14 @@ class Engine:
             _check("swim_read_gossips", self.lib.swim_read_gossips(
                 self._h, m, out.ctypes.data_as(POINTER(swim_gossip)), ln.value, byref(ln)))
         return out
+
+    def profile_enable(self, on: bool = True) -> None:
+        _check("swim_profile_enable", self.lib.swim_profile_enable(self._h, 1 if on else 0))
+
+    def profile_merge(self) -> dict:
+        p = swim_kernel_profile()
+        _check("swim_profile_merge", self.lib.swim_profile_merge(self._h, byref(p)))
+        return {name: getattr(p, name) for name, _ in swim_kernel_profile._fields_}
 
     def read_collector(self, m: int, gossiper: int) -> list[tuple[int, int]]:
         ln = C.c_uint32()
