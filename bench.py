@@ -26,9 +26,15 @@ KILL_EVERY = 20
 KILL_FIRST = 10
 
 
+WORKLOAD = "quiet"
+
+
 def kill_schedule(n, periods_lo, periods_hi):
-    """Members killed at the start of each period in [lo, hi): one every KILL_EVERY periods."""
+    """Members killed at the start of each period in [lo, hi): one every KILL_EVERY periods
+    (workload "failures"; the "quiet" workload kills nobody)."""
     out = {}
+    if WORKLOAD == "quiet":
+        return out
     for p in range(periods_lo, periods_hi):
         if p >= KILL_FIRST and (p - KILL_FIRST) % KILL_EVERY == 0:
             j = (p - KILL_FIRST) // KILL_EVERY
@@ -78,7 +84,11 @@ def main():
     ap.add_argument("--members", type=int, default=65536)
     ap.add_argument("--cpu-periods", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=("quiet", "failures"), default="quiet")
+    ap.add_argument("--gossip-capacity", type=int, default=0)
     args = ap.parse_args()
+    global WORKLOAD
+    WORKLOAD = args.workload
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -94,21 +104,26 @@ def main():
     from swimgpu import abi
     lib = swimgpu.load_library()
     n = args.members
-    e = abi.Engine(lib, make_config(lib, local_rank), n, n, 1 + rank)
+    cfg = make_config(lib, local_rank)
+    cfg.gossip_capacity = args.gossip_capacity
+    e = abi.Engine(lib, cfg, n, n, 1 + rank)
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    run_periods(e, 0, args.warmup)
-    e.drain_events()
-    barrier()
-    e.profile_enable(True)
-    t0 = time.perf_counter()
-    run_periods(e, args.warmup, args.warmup + args.steps)
-    barrier()
-    dt = time.perf_counter() - t0
+    try:
+        run_periods(e, 0, args.warmup)
+        e.drain_events()
+        barrier()
+        e.profile_enable(True)
+        t0 = time.perf_counter()
+        run_periods(e, args.warmup, args.warmup + args.steps)
+        barrier()
+        dt = time.perf_counter() - t0
+    except abi.SwimError as ex:
+        raise SystemExit(f"{ex}; engine error bits {e.stats()['capacity_errors']:#x}")
     prof = e.profile_merge()
     stats = e.stats()
     e.drain_events()
@@ -135,8 +150,10 @@ def main():
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",
-        "config": {"workload": f"config4-lan: N={n} members per GPU, LAN defaults (ping 1 s / gossip 200 ms / "
-                               f"sync 30 s staggered), 0% loss, one member killed every {KILL_EVERY} periods",
+        "config": {"workload": f"config4-lan-{args.workload}: N={n} members per GPU, LAN defaults (ping 1 s / "
+                               f"gossip 200 ms / sync 30 s staggered), 0% loss, "
+                               + ("no faults" if args.workload == "quiet"
+                                  else f"one member killed every {KILL_EVERY} periods"),
                    "members": n, "tick_ms": 100, "parallelism": f"replicas x{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": "k_sync_merge", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,

@@ -111,7 +111,7 @@ typedef struct swim_config {
   int32_t tick_ms;            /* 0 = gcd of every interval/timeout above */
   int32_t sync_stagger;       /* 1 = each initial member's periodic SYNC gets a random phase */
   int32_t record_fd_events;   /* 1 = FailureDetectorEvents appear in the event stream */
-  uint32_t gossip_capacity;   /* max live GossipStates per member (0 = default 256) */
+  uint32_t gossip_capacity;   /* max live GossipStates per member (0 = default 1024) */
   uint32_t collector_capacity;/* max distinct gossipers whose SequenceIdCollector a member holds
                                  (power of two; 0 = default 256) */
   uint32_t event_capacity;    /* undrained events the engine may buffer (0 = default 1<<22) */

@@ -342,7 +342,7 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
   Bufs& b = e->b;
   const uint32_t n = capacity;
   c.n = n;
-  c.gcap = cf.gossip_capacity ? cf.gossip_capacity : 256;
+  c.gcap = cf.gossip_capacity ? cf.gossip_capacity : 1024;
   c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 256);
   c.P = e->P;
   c.to_ticks = (uint32_t)cf.ping_timeout / tick;
