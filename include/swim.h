@@ -113,7 +113,7 @@ typedef struct swim_config {
   int32_t record_fd_events;   /* 1 = FailureDetectorEvents appear in the event stream */
   uint32_t gossip_capacity;   /* max live GossipStates per member (0 = default 1024) */
   uint32_t collector_capacity;/* max distinct gossipers whose SequenceIdCollector a member holds
-                                 (power of two; 0 = default 256) */
+                                 (power of two; 0 = default 1024) */
   uint32_t event_capacity;    /* undrained events the engine may buffer (0 = default 1<<22) */
   int32_t device;             /* HIP device ordinal the engine runs on (one engine per GPU) */
   uint32_t reserved[7];

@@ -12,14 +12,15 @@
 #include <new>
 #include <vector>
 
-#include "swim_kernels.h"
+#include "swim_phases.h"
 
 using namespace swimdev;
 
 namespace {
 
 constexpr uint32_t kDrainEvery = 256;
-constexpr uint32_t kMergeGrid = 256;
+constexpr uint32_t kClassifyGrid = 2048;  // grid-stride over (message, chunk) work units
+constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
 
 uint32_t gcd_u(uint32_t a, uint32_t b) {
   while (b) { uint32_t t = a % b; a = b; b = t; }
@@ -107,10 +108,10 @@ static void prof_flush(swim_engine* e) {
   e->prof_used = 0;
 }
 
-static void launch_merge(swim_engine* e, int d2) {
+static void launch_classify(swim_engine* e, int d2) {
   const bool p = e->prof && 2 * (e->prof_used + 1) <= e->prof_ev.size();
   if (p) hipEventRecord(e->prof_ev[2 * e->prof_used], e->stream);
-  k_sync_merge<<<kMergeGrid, MERGE_BLOCK, 0, e->stream>>>(e->c, e->b, d2);
+  k_sync_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(e->c, e->b, d2);
   if (p) {
     hipEventRecord(e->prof_ev[2 * e->prof_used + 1], e->stream);
     e->prof_used++;
@@ -179,19 +180,11 @@ static void run_tick(swim_engine* e) {
   }
   // ---- D: SYNC / SYNC_ACK
   k_sync_collect<<<gm, 256, 0, s>>>(c, b);
-  k_snap_mark<<<64, 256, 0, s>>>(c, b, b.reqs, &e->k->req_total, b.req_cap, b.req_cnt);
-  k_snap_copy<<<256, 256, 0, s>>>(c, b);
-  k_alloc<<<64, 256, 0, s>>>(b.req_recv, &e->k->req_recv_cnt, b.req_cnt, b.req_start, &e->k->req_cursor);
-  k_scatter_reqs<<<64, 256, 0, s>>>(b.reqs, &e->k->req_total, b.req_cap, b.req_start, b.reqs_out);
-  launch_merge(e, 0);
-  k_snap_reset<<<4, 256, 0, s>>>(b);
-  hipMemsetAsync(&e->k->snap_total, 0, sizeof(uint32_t), s);
-  k_snap_mark<<<64, 256, 0, s>>>(c, b, b.acks, &e->k->ack_total, b.req_cap, b.ack_cnt);
-  k_snap_copy<<<256, 256, 0, s>>>(c, b);
-  k_alloc<<<64, 256, 0, s>>>(b.ack_recv, &e->k->ack_recv_cnt, b.ack_cnt, b.ack_start, &e->k->ack_cursor);
-  k_scatter_reqs<<<64, 256, 0, s>>>(b.acks, &e->k->ack_total, b.req_cap, b.ack_start, b.acks_out);
-  launch_merge(e, 1);
-  k_snap_reset<<<4, 256, 0, s>>>(b);
+  for (int d2 = 0; d2 < 2; ++d2) {
+    k_sync_prep<<<1, 1024, 0, s>>>(c, b, d2);
+    launch_classify(e, d2);
+    k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(c, b, d2);
+  }
   run_ins_pipeline(e);
   // ---- end of tick
   k_end_tick<<<gm, 256, 0, s>>>(c);
@@ -343,7 +336,7 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
   const uint32_t n = capacity;
   c.n = n;
   c.gcap = cf.gossip_capacity ? cf.gossip_capacity : 1024;
-  c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 256);
+  c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 1024);
   c.P = e->P;
   c.to_ticks = (uint32_t)cf.ping_timeout / tick;
   c.relay_ticks = e->P - c.to_ticks;
@@ -365,9 +358,11 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
   c.wheel_cap = std::max<uint32_t>(4096, 2 * n);
   c.ev_cap = cf.event_capacity ? cf.event_capacity : (1u << 22);
   c.ins_cap = std::max<uint32_t>(1u << 16, 4 * n);
-  b.msg_cap = std::max<uint32_t>(1u << 20, 16 * n);
+  b.msg_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 256ull * n));
   b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
   b.snap_cap = 64;
+  b.chunks = (n + SYNC_CHUNK - 1) / SYNC_CHUNK;
+  b.pool_cap = std::max<uint32_t>(1u << 22, 16 * n);
 
   const size_t nn = (size_t)n * n;
   bool ok = e->alloc(&c.cells, nn) && e->alloc(&c.mem, n) && e->alloc(&c.ping, nn) && e->alloc(&c.remote, nn) &&
@@ -385,7 +380,8 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
             e->alloc(&b.acks_out, b.req_cap) && e->alloc(&b.ack_cnt, n) && e->alloc(&b.ack_start, n) &&
             e->alloc(&b.ack_recv, n) && e->alloc(&b.ins_out, c.ins_cap) && e->alloc(&b.ins_start, n) &&
             e->alloc(&b.snap, (size_t)b.snap_cap * n) && e->alloc(&b.snap_idx, n) && e->alloc(&b.snap_list, b.snap_cap) &&
-            e->alloc(&b.pend, (size_t)kMergeGrid * n) && e->alloc(&e->kat_coll, 1);
+            e->alloc(&b.snap_cnt, 1) && e->alloc(&b.item_chunk, (size_t)b.req_cap * b.chunks) &&
+            e->alloc(&b.pool, b.pool_cap) && e->alloc(&b.pend, (size_t)kApplyGrid * n) && e->alloc(&e->kat_coll, 1);
   if (!ok) { delete e; return SWIM_ENOMEM; }
   c.links = e->c.links;
   e->links_dev_cap = 1;
@@ -410,6 +406,7 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
   hipMemsetAsync(b.req_cnt, 0, 4 * (size_t)n, s);
   hipMemsetAsync(b.ack_cnt, 0, 4 * (size_t)n, s);
   hipMemsetAsync(b.snap_idx, 0xff, 4 * (size_t)n, s);
+  hipMemsetAsync(b.snap_cnt, 0, 4, s);
   c.T = 0;
   k_init_rows<<<std::min<uint32_t>(n, 65535), 256, 0, s>>>(c, n_initial);
   k_init_members<<<grid_for(n, 64), 64, 0, s>>>(c, n_initial, cf.sync_stagger);

@@ -3,7 +3,7 @@
 // Phase A  k_timers, k_compact                       suspicion timeouts, list removals
 // Phase B  k_fd                                       ping / ping-req / ack resolution + FD events
 // Phase C  k_gossip_seg, k_gossip_emit, k_alloc, k_scatter_msgs, k_gossip_deliver
-// Phase D  k_sync_collect, k_snap_mark, k_snap_copy, k_scatter_reqs, k_sync_merge (D1 and D2)
+// Phase D  k_sync_collect, k_sync_prep, k_sync_classify, k_sync_apply (swim_sync.h; SYNC and SYNC_ACK)
 // lists    k_ins_scatter, k_ins_apply                 deferred pingMembers inserts of ADDED events
 // tick end k_end_tick
 //
@@ -21,7 +21,7 @@ struct Counters {
   uint32_t ack_total, ack_recv_cnt, ack_cursor;
   uint32_t ins_total, ins_list_cnt, ins_cursor;
   uint32_t compact_cnt;
-  uint32_t snap_total;
+  uint32_t pool_cursor;  // complex-record pool of the SYNC classify kernel
   uint32_t pad[2];
 };
 
@@ -50,7 +50,12 @@ struct Bufs {
   uint32_t snap_cap;
   uint32_t* snap_idx;   // per member: slot or NONE
   uint32_t* snap_list;
-  uint64_t* pend;       // per sync-merge workgroup: pending ALIVE admissions
+  uint32_t* snap_cnt;   // claims made by the last k_sync_prep (persistent across ticks)
+  uint64_t* pend;       // per sync-apply workgroup: pending ALIVE admissions
+  uint2* item_chunk;    // per (message, chunk): (pool base, complex count)
+  uint32_t* pool;       // subjects whose record may change the receiver, chunk-ordered
+  uint32_t pool_cap;
+  uint32_t chunks;      // ceil(N / SYNC_CHUNK)
 };
 
 // ------------------------------------------------------------------------------- init
@@ -648,213 +653,8 @@ __global__ void k_sync_collect(Ctx c, Bufs b) {
   stat_add(c, ST_SYNCS, nsync);
 }
 
-// Rows read as SYNC / SYNC_ACK content must be the sender's table as it was when the message was
-// prepared.  When that sender is itself a receiver in the same sub-phase its row is copied first.
-__global__ void k_snap_mark(Ctx c, Bufs b, const SyncReq* items, const uint32_t* total, uint32_t cap,
-                            const uint32_t* recv_cnt) {
-  const uint32_t n = min(*total, cap);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const SyncReq q = items[i];
-    if (!(q.flags & RQ_DELIVERED)) continue;
-    const uint32_t src = q.from;
-    if (recv_cnt[src] == 0) continue;
-    if (atomicCAS(&b.snap_idx[src], NONE, NONE - 1) == NONE) {
-      uint32_t slot = atomicAdd(&b.k->snap_total, 1u);
-      if (slot >= b.snap_cap) { set_err(c, ERR_SNAP); b.snap_idx[src] = NONE; continue; }
-      b.snap_list[slot] = src;
-      b.snap_idx[src] = slot;
-    }
-  }
-}
+#include "swim_sync.h"
 
-__global__ void k_snap_copy(Ctx c, Bufs b) {
-  const uint32_t ns = min(b.k->snap_total, b.snap_cap);
-  const uint32_t chunks = (c.n + 4095) / 4096;
-  for (uint32_t w = blockIdx.x; w < ns * chunks; w += gridDim.x) {
-    uint32_t slot = w / chunks, ch = w % chunks;
-    const uint64_t* src = row(c, b.snap_list[slot]);
-    uint64_t* dst = b.snap + (size_t)slot * c.n;
-    for (uint32_t s = ch * 4096 + threadIdx.x; s < min(c.n, (ch + 1) * 4096); s += blockDim.x) dst[s] = src[s];
-  }
-}
-
-__global__ void k_snap_reset(Bufs b) {
-  const uint32_t ns = b.k->snap_total < b.snap_cap ? b.k->snap_total : b.snap_cap;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x)
-    b.snap_idx[b.snap_list[i]] = NONE;
-  __syncthreads();
-}
-
-__global__ void k_scatter_reqs(const SyncReq* items, const uint32_t* total, uint32_t cap, const uint32_t* start,
-                               SyncReq* out) {
-  const uint32_t n = min(*total, cap);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const SyncReq q = items[i];
-    if (!(q.flags & RQ_DELIVERED)) continue;
-    out[start[q.to] + q.slot] = q;
-  }
-}
-
-// SYNC_ACKs are produced with RQ_DELIVERED already set; this marks (to, slot) bookkeeping
-__device__ inline void add_ack(const Ctx& c, const Bufs& b, uint32_t to, uint32_t from, uint32_t rank, bool initial) {
-  SyncReq a;
-  a.from = from; a.to = to; a.ordinal = rank; a.flags = RQ_DELIVERED | (initial ? RQ_INITIAL : 0);
-  a.pad[0] = a.pad[1] = a.pad[2] = 0;
-  a.slot = atomicAdd(&b.ack_cnt[to], 1u);
-  if (a.slot == 0) b.ack_recv[atomicAdd(&b.k->ack_recv_cnt, 1u)] = to;
-  uint32_t i = atomicAdd(&b.k->ack_total, 1u);
-  if (i >= b.req_cap) { set_err(c, ERR_REQS); return; }
-  b.acks[i] = a;
-}
-
-constexpr int MERGE_BLOCK = 1024;
-constexpr int MERGE_CPT = 8;  // subjects per thread per tile
-constexpr int MERGE_TILE = MERGE_BLOCK * MERGE_CPT;
-
-// syncMembership (MembershipProtocolImpl.java:491-509) of one SYNC / SYNC_ACK into viewer v's row.
-// Workgroup-parallel over subjects: every thread classifies 8 consecutive (content, row) cell pairs;
-// records whose updateMembership would change nothing are skipped, the rest are compacted in
-// subject order and handed to thread 0, which runs the sequential merge on them.  ALIVE
-// admissions (fetch succeeded) are applied after the whole message, as the reference applies them
-// when the metadata round trips complete.
-__device__ inline bool sync_complex(uint64_t r1, uint64_t r0, bool self) {
-  const uint32_t s1 = c_status(r1);
-  const int32_t i1 = c_inc(r1);
-  const bool p0 = c_has(r0, B_IN_TABLE);
-  const uint32_t s0 = c_status(r0);
-  const int32_t i0 = c_inc(r0);
-  const bool r0_leaving = p0 && s0 == SWIM_LEAVING;
-  if (!r0_leaving && !is_overrides(s1, i1, p0, s0, i0)) return false;
-  // an identical LEAVING record over a LEAVING row is a no-op put, except on the viewer's own row,
-  // where it re-runs onSelfMemberDetected (MembershipProtocolImpl.java:593-607)
-  if (r0_leaving && s1 == SWIM_LEAVING && i1 == i0 && !self) return false;
-  return true;
-}
-
-__device__ void merge_row(const Ctx& c, uint32_t v, const uint64_t* __restrict__ content, int reason, uint32_t phase,
-                          uint64_t* pend) {
-  __shared__ uint32_t s_list[MERGE_TILE];
-  __shared__ uint32_t s_wave[MERGE_BLOCK / 64 + 1];
-  uint64_t* __restrict__ rv = row(c, v);
-  const uint32_t n = c.n;
-  unsigned long long recs = 0, changed = 0;
-  uint32_t npend = 0;
-  for (uint32_t base = 0; base < n; base += MERGE_TILE) {
-    const uint32_t x0 = base + threadIdx.x * MERGE_CPT;
-    uint32_t flags = 0;
-    if (x0 + MERGE_CPT <= n) {
-      uint64_t a[MERGE_CPT], r[MERGE_CPT];
-#pragma unroll
-      for (int q = 0; q < MERGE_CPT; q += 2) {
-        const ulonglong2 va = *reinterpret_cast<const ulonglong2*>(content + x0 + q);
-        a[q] = va.x; a[q + 1] = va.y;
-      }
-#pragma unroll
-      for (int q = 0; q < MERGE_CPT; q += 2) {
-        const ulonglong2 vr = *reinterpret_cast<const ulonglong2*>(rv + x0 + q);
-        r[q] = vr.x; r[q + 1] = vr.y;
-      }
-#pragma unroll
-      for (int q = 0; q < MERGE_CPT; ++q) {
-        if (c_has(a[q], B_IN_TABLE)) {
-          recs++;
-          if (sync_complex(a[q], r[q], x0 + q == v)) flags |= 1u << q;
-        }
-      }
-    } else {
-      for (int q = 0; q < MERGE_CPT; ++q) {
-        const uint32_t x = x0 + q;
-        if (x >= n) break;
-        const uint64_t a = content[x];
-        if (c_has(a, B_IN_TABLE)) {
-          recs++;
-          if (sync_complex(a, rv[x], x == v)) flags |= 1u << q;
-        }
-      }
-    }
-    uint32_t total;
-    const uint32_t off = block_exclusive_scan<MERGE_BLOCK>((uint32_t)__popc(flags), s_wave, &total);
-    if (total == 0) continue;  // uniform: total is the same in every thread
-    uint32_t o = off;
-    for (int q = 0; q < MERGE_CPT; ++q)
-      if (flags & (1u << q)) s_list[o++] = x0 + q;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      changed += total;
-      for (uint32_t i = 0; i < total; ++i) {
-        const uint32_t x = s_list[i];
-        const uint64_t a = content[x];
-        if (update_membership(c, v, x, c_status(a), c_inc(a), reason, phase))
-          pend[npend++] = ((uint64_t)x << 32) | (uint32_t)c_inc(a);
-      }
-    }
-    __syncthreads();
-  }
-  // wave-reduce the record count
-  for (int d = 32; d > 0; d >>= 1) recs += __shfl_down(recs, d, 64);
-  if ((threadIdx.x & 63) == 0) stat_add(c, ST_SYNC_RECORDS, recs);
-  if (threadIdx.x == 0) {
-    stat_add(c, ST_MERGE_RECORDS, changed);
-    for (uint32_t i = 0; i < npend; ++i)
-      apply_alive(c, v, (uint32_t)(pend[i] >> 32), (int32_t)(uint32_t)pend[i], reason, phase);
-  }
-  __syncthreads();
-}
-
-__device__ inline void sort_reqs(SyncReq* a, uint32_t n) {
-  for (uint32_t i = 1; i < n; ++i) {
-    SyncReq x = a[i];
-    int32_t j = (int32_t)i - 1;
-    while (j >= 0 && (a[j].from > x.from || (a[j].from == x.from && a[j].ordinal > x.ordinal))) { a[j + 1] = a[j]; --j; }
-    a[j + 1] = x;
-  }
-}
-
-// D1 (acks == false): onSync at each receiver, then its SYNC_ACKs.  D2 (acks == true): the
-// SYNC_ACK merge at the original senders (MembershipProtocolImpl.java:363-415).
-__global__ void __launch_bounds__(MERGE_BLOCK) k_sync_merge(Ctx c, Bufs b, int d2) {
-  const uint32_t* recv = d2 ? b.ack_recv : b.req_recv;
-  const uint32_t nrecv = d2 ? b.k->ack_recv_cnt : b.k->req_recv_cnt;
-  uint32_t* cnt = d2 ? b.ack_cnt : b.req_cnt;
-  const uint32_t* start = d2 ? b.ack_start : b.req_start;
-  SyncReq* inbox_all = d2 ? b.acks_out : b.reqs_out;
-  const uint32_t phase = d2 ? SWIM_PHASE_SYNCACK : SWIM_PHASE_SYNC;
-  uint64_t* pend = b.pend + (size_t)blockIdx.x * c.n;
-  for (uint32_t i = blockIdx.x; i < nrecv; i += gridDim.x) {
-    const uint32_t s = recv[i];
-    const uint32_t k = cnt[s];
-    SyncReq* inbox = inbox_all + start[s];
-    if (threadIdx.x == 0) {
-      stat_add(c, ST_MERGE_MSGS, k);
-      sort_reqs(inbox, k);
-      c.mem[s].ev_minor = 0;
-      c.mem[s].fetch_ctr = 0;
-    }
-    __syncthreads();
-    for (uint32_t q = 0; q < k; ++q) {
-      const SyncReq rq = inbox[q];
-      const uint32_t si = b.snap_idx[rq.from];
-      const uint64_t* content = si < b.snap_cap ? b.snap + (size_t)si * c.n : row(c, rq.from);
-      const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
-      merge_row(c, s, content, reason, phase, pend);
-    }
-    if (threadIdx.x == 0) {
-      if (!d2) {
-        for (uint32_t q = 0; q < k; ++q) {
-          const SyncReq rq = inbox[q];
-          if (out_fail(c, s, rq.from, draw(c, s, SWIM_STREAM_SYNCACK_OUT, q, 0))) continue;
-          if (!in_pass(c, rq.from, s)) continue;
-          if (rq.flags & RQ_INITIAL) atomicAdd(&c.mem[rq.from].init_done, 1u);
-          add_ack(c, b, rq.from, s, q, (rq.flags & RQ_INITIAL) != 0);
-        }
-      } else {
-        stat_add(c, ST_SYNC_ACKS, k);
-      }
-      cnt[s] = 0;
-    }
-    __syncthreads();
-  }
-}
 
 // ------------------------------------------------------------------------------- end of tick
 // start0's doFinally (:285-289) for members that joined this tick; graceful leaves complete.

@@ -1,0 +1,314 @@
+// swim_sync.h — phase D kernels: SYNC / SYNC_ACK delivery and the row merge (included inside
+// namespace swimdev by swim_phases.h).
+//
+// syncMembership (MembershipProtocolImpl.java:491-509) runs updateMembership on every record of a
+// full table; with a 30 s sync interval N/300 members start a SYNC every tick, so the dominant cost
+// of a protocol period is streaming (content row, receiver row) pairs.  It is split in three:
+//
+//   k_sync_prep      one workgroup: group delivered messages by receiver, canonical inbox order,
+//                    snapshot claims for rows that are both read and merged into in this sub-phase
+//   k_sync_classify  the HBM stream: one 256-thread workgroup per (message, 4,096-subject chunk),
+//                    16 consecutive subjects per thread with 16-B loads; a record is "complex" unless
+//                    updateMembership would provably do nothing; complex subjects of a chunk are
+//                    block-scan compacted into a pool in subject order
+//   k_sync_apply     one workgroup per receiver: lane 0 runs the exact sequential updateMembership on
+//                    the complex subjects in (message, chunk, subject) order, then the ALIVE
+//                    admissions whose metadata fetch succeeded; a later message to a receiver whose
+//                    row already changed this sub-phase is re-classified in-workgroup.
+
+constexpr int SYNC_CHUNK = 4096;
+constexpr int CLS_BLOCK = 256;
+constexpr int CLS_CPT = SYNC_CHUNK / CLS_BLOCK;  // 16 subjects per thread
+constexpr int APPLY_BLOCK = 256;
+constexpr int APPLY_CPT = 8;
+constexpr int APPLY_TILE = APPLY_BLOCK * APPLY_CPT;
+
+// true unless updateMembership(r1 = content cell) on row cell r0 provably changes nothing
+__device__ inline bool sync_complex(uint64_t r1, uint64_t r0, bool self) {
+  const uint32_t s1 = c_status(r1);
+  const int32_t i1 = c_inc(r1);
+  const bool p0 = c_has(r0, B_IN_TABLE);
+  const uint32_t s0 = c_status(r0);
+  const int32_t i0 = c_inc(r0);
+  const bool r0_leaving = p0 && s0 == SWIM_LEAVING;
+  if (!r0_leaving && !is_overrides(s1, i1, p0, s0, i0)) return false;  // :593-602
+  // an identical LEAVING record over a LEAVING row is a no-op put, except on the viewer's own row,
+  // where it re-runs onSelfMemberDetected (:604-607)
+  if (r0_leaving && s1 == SWIM_LEAVING && i1 == i0 && !self) return false;
+  return true;
+}
+
+__device__ inline void sort_reqs(SyncReq* a, uint32_t n) {
+  for (uint32_t i = 1; i < n; ++i) {
+    SyncReq x = a[i];
+    int32_t j = (int32_t)i - 1;
+    while (j >= 0 && (a[j].from > x.from || (a[j].from == x.from && a[j].ordinal > x.ordinal))) { a[j + 1] = a[j]; --j; }
+    a[j + 1] = x;
+  }
+}
+
+struct SubPhase {  // the SYNC (d2 = 0) or SYNC_ACK (d2 = 1) buffers
+  SyncReq* items;
+  uint32_t total;
+  uint32_t* recv;
+  uint32_t nrecv;
+  uint32_t* cnt;
+  uint32_t* start;
+  SyncReq* out;
+  uint32_t* nitems;
+};
+
+__device__ inline SubPhase sub_phase(const Bufs& b, int d2) {
+  SubPhase p;
+  if (!d2) {
+    p.items = b.reqs; p.total = min(b.k->req_total, b.req_cap); p.recv = b.req_recv; p.nrecv = b.k->req_recv_cnt;
+    p.cnt = b.req_cnt; p.start = b.req_start; p.out = b.reqs_out; p.nitems = &b.k->req_cursor;
+  } else {
+    p.items = b.acks; p.total = min(b.k->ack_total, b.req_cap); p.recv = b.ack_recv; p.nrecv = b.k->ack_recv_cnt;
+    p.cnt = b.ack_cnt; p.start = b.ack_start; p.out = b.acks_out; p.nitems = &b.k->ack_cursor;
+  }
+  return p;
+}
+
+__global__ void __launch_bounds__(1024) k_sync_prep(Ctx c, Bufs b, int d2) {
+  __shared__ uint32_t s_cursor;
+  const SubPhase p = sub_phase(b, d2);
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  // release the previous sub-phase's snapshot claims
+  const uint32_t prev = min(*b.snap_cnt, b.snap_cap);
+  for (uint32_t i = tid; i < prev; i += nt) b.snap_idx[b.snap_list[i]] = NONE;
+  if (tid == 0) s_cursor = 0;
+  __syncthreads();
+  if (tid == 0) *b.snap_cnt = 0;
+  // one contiguous inbox per receiver
+  for (uint32_t i = tid; i < p.nrecv; i += nt) {
+    const uint32_t r = p.recv[i];
+    p.start[r] = atomicAdd(&s_cursor, p.cnt[r]);
+  }
+  __syncthreads();
+  if (tid == 0) *p.nitems = s_cursor;
+  for (uint32_t i = tid; i < p.total; i += nt) {
+    const SyncReq q = p.items[i];
+    if (q.flags & RQ_DELIVERED) p.out[p.start[q.to] + q.slot] = q;
+  }
+  __syncthreads();
+  // canonical order inside an inbox: (sender, ordinal)
+  for (uint32_t i = tid; i < p.nrecv; i += nt) {
+    const uint32_t r = p.recv[i];
+    sort_reqs(p.out + p.start[r], p.cnt[r]);
+  }
+  __syncthreads();
+  // message content = the sender's table when the message was prepared: a sender that is itself
+  // merged into during this sub-phase gets its row snapshotted by k_sync_classify
+  const uint32_t ni = s_cursor;
+  for (uint32_t i = tid; i < ni; i += nt) {
+    const uint32_t src = p.out[i].from;
+    if (p.cnt[src] == 0) continue;
+    if (atomicCAS(&b.snap_idx[src], NONE, NONE - 1) == NONE) {
+      const uint32_t slot = atomicAdd(b.snap_cnt, 1u);
+      if (slot >= b.snap_cap) { set_err(c, ERR_SNAP); b.snap_idx[src] = NONE; continue; }
+      b.snap_list[slot] = src;
+      b.snap_idx[src] = slot;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(Ctx c, Bufs b, int d2) {
+  __shared__ uint32_t s_wave[CLS_BLOCK / 64 + 1];
+  __shared__ uint32_t s_base;
+  const SubPhase p = sub_phase(b, d2);
+  const uint32_t ni = *p.nitems;
+  const uint32_t chunks = b.chunks, n = c.n;
+  unsigned long long recs = 0, msgs = 0, cplx = 0;
+  for (uint32_t w = blockIdx.x; w < ni * chunks; w += gridDim.x) {
+    const uint32_t i = w / chunks, ch = w - i * chunks;
+    const SyncReq q = p.out[i];
+    const uint32_t r = q.to, src = q.from;
+    const uint64_t* __restrict__ content = row(c, src);
+    const uint64_t* __restrict__ rv = row(c, r);
+    const uint32_t si = b.snap_idx[src];
+    uint64_t* snapdst = si < b.snap_cap ? b.snap + (size_t)si * n : nullptr;
+    if (ch == 0) msgs++;
+    const uint32_t x0 = ch * SYNC_CHUNK + threadIdx.x * CLS_CPT;
+    uint32_t flags = 0;
+    if (x0 + CLS_CPT <= n && ((reinterpret_cast<uintptr_t>(content + x0) | reinterpret_cast<uintptr_t>(rv + x0)) & 15) == 0) {
+      uint64_t a[CLS_CPT], o[CLS_CPT];
+#pragma unroll
+      for (int k = 0; k < CLS_CPT; k += 2) {
+        const ulonglong2 va = *reinterpret_cast<const ulonglong2*>(content + x0 + k);
+        a[k] = va.x; a[k + 1] = va.y;
+      }
+#pragma unroll
+      for (int k = 0; k < CLS_CPT; k += 2) {
+        const ulonglong2 vo = *reinterpret_cast<const ulonglong2*>(rv + x0 + k);
+        o[k] = vo.x; o[k + 1] = vo.y;
+      }
+      if (snapdst) {
+#pragma unroll
+        for (int k = 0; k < CLS_CPT; k += 2)
+          *reinterpret_cast<ulonglong2*>(snapdst + x0 + k) = make_ulonglong2(a[k], a[k + 1]);
+      }
+#pragma unroll
+      for (int k = 0; k < CLS_CPT; ++k) {
+        const bool rec = c_has(a[k], B_IN_TABLE);
+        recs += rec;
+        if (rec && sync_complex(a[k], o[k], x0 + k == r)) flags |= 1u << k;
+      }
+    } else {
+      for (int k = 0; k < CLS_CPT; ++k) {
+        const uint32_t x = x0 + k;
+        if (x >= n) break;
+        const uint64_t a = content[x];
+        if (snapdst) snapdst[x] = a;
+        if (c_has(a, B_IN_TABLE)) {
+          recs++;
+          if (sync_complex(a, rv[x], x == r)) flags |= 1u << k;
+        }
+      }
+    }
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan<CLS_BLOCK>((uint32_t)__popc(flags), s_wave, &total);
+    if (total) {
+      if (threadIdx.x == 0) {
+        uint32_t base = atomicAdd(&b.k->pool_cursor, total);
+        if (base + total > b.pool_cap) { set_err(c, ERR_PEND); base = 0; }
+        s_base = base;
+      }
+      __syncthreads();
+      const uint32_t base = s_base;
+      if (base + total <= b.pool_cap) {
+        uint32_t o2 = base + off;
+        for (int k = 0; k < CLS_CPT; ++k)
+          if (flags & (1u << k)) b.pool[o2++] = x0 + k;
+      }
+      if (threadIdx.x == 0) { b.item_chunk[(size_t)i * chunks + ch] = make_uint2(base, total); cplx += total; }
+      __syncthreads();
+    } else if (threadIdx.x == 0) {
+      b.item_chunk[(size_t)i * chunks + ch] = make_uint2(0, 0);
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) recs += __shfl_down(recs, d, 64);
+  if ((threadIdx.x & 63) == 0) stat_add(c, ST_SYNC_RECORDS, recs);
+  if (threadIdx.x == 0) {
+    stat_add(c, ST_MERGE_MSGS, msgs);
+    stat_add(c, ST_MERGE_RECORDS, cplx);
+  }
+}
+
+// In-workgroup merge of one message (used when the receiver's row changed earlier in this
+// sub-phase, so the precomputed classification may be stale).  Returns through *s_mod whether any
+// record could change the row.
+__device__ void merge_row_wg(const Ctx& c, uint32_t v, const uint64_t* __restrict__ content, int reason,
+                             uint32_t phase, uint64_t* pend, uint32_t& npend, uint32_t* s_list, uint32_t* s_wave,
+                             uint32_t* s_mod) {
+  uint64_t* __restrict__ rv = row(c, v);
+  const uint32_t n = c.n;
+  for (uint32_t base = 0; base < n; base += APPLY_TILE) {
+    const uint32_t x0 = base + threadIdx.x * APPLY_CPT;
+    uint32_t flags = 0;
+    for (int k = 0; k < APPLY_CPT; ++k) {
+      const uint32_t x = x0 + k;
+      if (x >= n) break;
+      const uint64_t a = content[x];
+      if (c_has(a, B_IN_TABLE) && sync_complex(a, rv[x], x == v)) flags |= 1u << k;
+    }
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan<APPLY_BLOCK>((uint32_t)__popc(flags), s_wave, &total);
+    if (total == 0) continue;
+    uint32_t o = off;
+    for (int k = 0; k < APPLY_CPT; ++k)
+      if (flags & (1u << k)) s_list[o++] = x0 + k;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      *s_mod = 1;
+      for (uint32_t i = 0; i < total; ++i) {
+        const uint32_t x = s_list[i];
+        const uint64_t a = content[x];
+        if (update_membership(c, v, x, c_status(a), c_inc(a), reason, phase))
+          pend[npend++] = ((uint64_t)x << 32) | (uint32_t)c_inc(a);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// SYNC_ACK bookkeeping: (receiver, slot) for grouping by the original sender
+__device__ inline void add_ack(const Ctx& c, const Bufs& b, uint32_t to, uint32_t from, uint32_t rank, bool initial) {
+  SyncReq a;
+  a.from = from; a.to = to; a.ordinal = rank; a.flags = RQ_DELIVERED | (initial ? RQ_INITIAL : 0);
+  a.pad[0] = a.pad[1] = a.pad[2] = 0;
+  a.slot = atomicAdd(&b.ack_cnt[to], 1u);
+  if (a.slot == 0) b.ack_recv[atomicAdd(&b.k->ack_recv_cnt, 1u)] = to;
+  uint32_t i = atomicAdd(&b.k->ack_total, 1u);
+  if (i >= b.req_cap) { set_err(c, ERR_REQS); return; }
+  b.acks[i] = a;
+}
+
+// D1 (d2 = 0): onSync at each receiver, then its SYNC_ACKs.  D2 (d2 = 1): the SYNC_ACK merge at
+// the original senders (MembershipProtocolImpl.java:363-415).
+__global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(Ctx c, Bufs b, int d2) {
+  __shared__ uint32_t s_list[APPLY_TILE];
+  __shared__ uint32_t s_wave[APPLY_BLOCK / 64 + 1];
+  __shared__ uint32_t s_mod;
+  const SubPhase p = sub_phase(b, d2);
+  const uint32_t phase = d2 ? SWIM_PHASE_SYNCACK : SWIM_PHASE_SYNC;
+  const uint32_t chunks = b.chunks;
+  uint64_t* pend = b.pend + (size_t)blockIdx.x * c.n;
+  for (uint32_t i = blockIdx.x; i < p.nrecv; i += gridDim.x) {
+    const uint32_t s = p.recv[i];
+    const uint32_t k = p.cnt[s];
+    const uint32_t first = p.start[s];
+    if (threadIdx.x == 0) {
+      c.mem[s].ev_minor = 0;
+      c.mem[s].fetch_ctr = 0;
+      s_mod = 0;
+    }
+    __syncthreads();
+    for (uint32_t q = 0; q < k; ++q) {
+      const SyncReq rq = p.out[first + q];
+      const uint32_t si = b.snap_idx[rq.from];
+      const uint64_t* content = si < b.snap_cap ? b.snap + (size_t)si * c.n : row(c, rq.from);
+      const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
+      uint32_t npend = 0;
+      const uint32_t mod = s_mod;
+      __syncthreads();  // every lane has read s_mod before lane 0 may set it
+      if (mod == 0) {  // precomputed classification is exact: the row is unchanged
+        if (threadIdx.x == 0) {
+          const uint2* ic = b.item_chunk + (size_t)(first + q) * chunks;
+          for (uint32_t ch = 0; ch < chunks; ++ch) {
+            const uint2 e = ic[ch];
+            if (e.y) s_mod = 1;
+            for (uint32_t j = 0; j < e.y; ++j) {
+              const uint32_t x = b.pool[e.x + j];
+              const uint64_t a = content[x];
+              if (update_membership(c, s, x, c_status(a), c_inc(a), reason, phase))
+                pend[npend++] = ((uint64_t)x << 32) | (uint32_t)c_inc(a);
+            }
+          }
+        }
+      } else {
+        merge_row_wg(c, s, content, reason, phase, pend, npend, s_list, s_wave, &s_mod);
+      }
+      if (threadIdx.x == 0) {
+        for (uint32_t j = 0; j < npend; ++j)
+          apply_alive(c, s, (uint32_t)(pend[j] >> 32), (int32_t)(uint32_t)pend[j], reason, phase);
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      if (!d2) {
+        for (uint32_t q = 0; q < k; ++q) {
+          const SyncReq rq = p.out[first + q];
+          if (out_fail(c, s, rq.from, draw(c, s, SWIM_STREAM_SYNCACK_OUT, q, 0))) continue;
+          if (!in_pass(c, rq.from, s)) continue;
+          if (rq.flags & RQ_INITIAL) atomicAdd(&c.mem[rq.from].init_done, 1u);
+          add_ack(c, b, rq.from, s, q, (rq.flags & RQ_INITIAL) != 0);
+        }
+      } else {
+        stat_add(c, ST_SYNC_ACKS, k);
+      }
+      p.cnt[s] = 0;
+    }
+    __syncthreads();
+  }
+}
