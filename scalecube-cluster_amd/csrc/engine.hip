@@ -138,16 +138,13 @@ static int32_t sync_and_collect(swim_engine* e) {
   return err ? SWIM_ECAPACITY : SWIM_OK;
 }
 
-static void run_ins_pipeline(swim_engine* e) {
-  Ctx& c = e->c;
-  Bufs& b = e->b;
-  hipStream_t s = e->stream;
-  k_alloc<<<64, 256, 0, s>>>(c.ins_list, c.ins_list_cnt, c.ins_cnt, b.ins_start, &e->k->ins_cursor);
-  k_ins_scatter<<<256, 256, 0, s>>>(c, b);
-  k_ins_apply<<<512, 256, 0, s>>>(c, b);
-  hipMemsetAsync(&e->k->ins_total, 0, 3 * sizeof(uint32_t), s);  // ins_total, ins_list_cnt, ins_cursor
+// deferred pingMembers inserts of the phase's ADDED events (Ctx points at that phase's counters)
+static void run_ins_pipeline(swim_engine* e, const Ctx& c) {
+  k_ins_prep<<<1, 1024, 0, e->stream>>>(c, e->b);
+  k_ins_apply<<<512, 256, 0, e->stream>>>(c, e->b);
 }
 
+// One tick = 15 kernels (21 on gossip ticks) on one stream; no host synchronisation.
 static void run_tick(swim_engine* e) {
   e->T += 1;
   e->host_ticks += 1;
@@ -157,7 +154,6 @@ static void run_tick(swim_engine* e) {
   hipStream_t s = e->stream;
   const uint32_t n = e->n;
   const uint32_t gm = grid_for(n, 256);
-  hipMemsetAsync(e->k, 0, sizeof(Counters), s);
   if (e->joins_pending) {
     k_start_joins<<<gm, 256, 0, s>>>(c);
     e->joins_pending = false;
@@ -165,8 +161,7 @@ static void run_tick(swim_engine* e) {
   // ---- A: suspicion timeouts
   const uint32_t bucket = (uint32_t)(e->T & c.wheel_mask);
   k_timers<<<256, 256, 0, s>>>(c, bucket);
-  hipMemsetAsync(&c.wheel_cnt[bucket], 0, sizeof(uint32_t), s);
-  k_compact<<<256, 256, 0, s>>>(c, e->k);
+  k_compact<<<256, 256, 0, s>>>(c, e->k, bucket);
   // ---- B: failure detector
   k_fd<<<gm, 256, 0, s>>>(c);
   // ---- C: gossip round
@@ -176,18 +171,21 @@ static void run_tick(swim_engine* e) {
     k_alloc<<<64, 256, 0, s>>>(b.msg_recv, &e->k->msg_recv_cnt, b.msg_cnt, b.msg_start, &e->k->msg_cursor);
     k_scatter_msgs<<<512, 256, 0, s>>>(b);
     k_gossip_deliver<<<gm, 256, 0, s>>>(c, b);
-    run_ins_pipeline(e);
+    run_ins_pipeline(e, c);
   }
-  // ---- D: SYNC / SYNC_ACK
-  k_sync_collect<<<gm, 256, 0, s>>>(c, b);
+  // ---- D: SYNC / SYNC_ACK (list inserts use the second set of counters)
+  Ctx cd = c;
+  cd.ins_total = &e->k->ins_total2;
+  cd.ins_list_cnt = &e->k->ins_list_cnt2;
+  k_sync_collect<<<gm, 256, 0, s>>>(cd, b);
   for (int d2 = 0; d2 < 2; ++d2) {
-    k_sync_prep<<<1, 1024, 0, s>>>(c, b, d2);
+    k_sync_prep<<<1, 1024, 0, s>>>(cd, b, d2);
     launch_classify(e, d2);
-    k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(c, b, d2);
+    k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(cd, b, d2);
   }
-  run_ins_pipeline(e);
-  // ---- end of tick
-  k_end_tick<<<gm, 256, 0, s>>>(c);
+  run_ins_pipeline(e, cd);
+  // ---- end of tick (also zeroes the per-tick counters)
+  k_end_tick<<<gm, 256, 0, s>>>(c, e->k);
 }
 
 static int32_t upload_links(swim_engine* e) {
@@ -381,6 +379,7 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
             e->alloc(&b.ack_recv, n) && e->alloc(&b.ins_out, c.ins_cap) && e->alloc(&b.ins_start, n) &&
             e->alloc(&b.snap, (size_t)b.snap_cap * n) && e->alloc(&b.snap_idx, n) && e->alloc(&b.snap_list, b.snap_cap) &&
             e->alloc(&b.snap_cnt, 1) && e->alloc(&b.item_chunk, (size_t)b.req_cap * b.chunks) &&
+            e->alloc(&b.item_total, b.req_cap) &&
             e->alloc(&b.pool, b.pool_cap) && e->alloc(&b.pend, (size_t)kApplyGrid * n) && e->alloc(&e->kat_coll, 1);
   if (!ok) { delete e; return SWIM_ENOMEM; }
   c.links = e->c.links;

@@ -232,9 +232,19 @@ __device__ __forceinline__ bool in_pass(const Ctx& c, uint32_t b, uint32_t a) {
   }
   return c.default_inbound[b] != 0;
 }
-// tryFailOutbound (NetworkEmulator.java:167-181) + a stopped destination refusing the connection
-__device__ __forceinline__ bool out_fail(const Ctx& c, uint32_t a, uint32_t b, uint32_t w) {
-  return !c.mem[b].up || lost(out_loss(c, a, b), w);
+// lost() with the Philox draw evaluated only when the loss percentage needs it (0 % and 100 %
+// are decided without a draw; draws are keyed, so skipping one shifts nothing)
+__device__ __forceinline__ bool lost_k(const Ctx& c, int32_t pct, uint32_t member, uint32_t stream, uint32_t sub24,
+                                       uint32_t sub32) {
+  if (pct <= 0) return false;
+  if (pct >= 100) return true;
+  return (int32_t)next_int(draw(c, member, stream, sub24, sub32), 100) < pct;
+}
+// tryFailOutbound (NetworkEmulator.java:167-181) + a stopped destination refusing the connection;
+// the draw is keyed (member, stream, sub24, sub32)
+__device__ __forceinline__ bool out_fail(const Ctx& c, uint32_t a, uint32_t b, uint32_t member, uint32_t stream,
+                                         uint32_t sub24, uint32_t sub32) {
+  return !c.mem[b].up || lost_k(c, out_loss(c, a, b), member, stream, sub24, sub32);
 }
 
 // ------------------------------------------------------------------------------- collectors
@@ -405,10 +415,9 @@ __device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
 // MetadataStoreImpl.fetchMetadata (:146-185) + onMetadataRequest (:201-240): one round trip.
 __device__ inline bool fetch_ok(const Ctx& c, uint32_t v, uint32_t s, uint32_t phase) {
   uint32_t f = c.mem[v].fetch_ctr++;
-  uint32_t w1 = draw(c, v, SWIM_STREAM_FETCH_REQ, phase, f);
-  uint32_t w2 = draw(c, v, SWIM_STREAM_FETCH_RESP, phase, f);
   stat_add(c, ST_FETCHES, 1);
-  bool ok = !out_fail(c, v, s, w1) && in_pass(c, s, v) && !out_fail(c, s, v, w2) && in_pass(c, v, s);
+  bool ok = !out_fail(c, v, s, v, SWIM_STREAM_FETCH_REQ, phase, f) && in_pass(c, s, v) &&
+            !out_fail(c, s, v, v, SWIM_STREAM_FETCH_RESP, phase, f) && in_pass(c, v, s);
   if (ok) stat_add(c, ST_FETCH_OK, 1);
   return ok;
 }

@@ -19,10 +19,11 @@ struct Counters {
   uint32_t msg_total, msg_recv_cnt, msg_cursor;
   uint32_t req_total, req_recv_cnt, req_cursor;
   uint32_t ack_total, ack_recv_cnt, ack_cursor;
-  uint32_t ins_total, ins_list_cnt, ins_cursor;
+  uint32_t ins_total, ins_list_cnt, ins_cursor;     // list inserts of the gossip phase
+  uint32_t ins_total2, ins_list_cnt2, ins_cursor2;  // list inserts of the SYNC phase
   uint32_t compact_cnt;
   uint32_t pool_cursor;  // complex-record pool of the SYNC classify kernel
-  uint32_t pad[2];
+  uint32_t pad[3];
 };
 
 struct Bufs {
@@ -53,6 +54,7 @@ struct Bufs {
   uint32_t* snap_cnt;   // claims made by the last k_sync_prep (persistent across ticks)
   uint64_t* pend;       // per sync-apply workgroup: pending ALIVE admissions
   uint2* item_chunk;    // per (message, chunk): (pool base, complex count)
+  uint32_t* item_total; // per message: complex count over all chunks
   uint32_t* pool;       // subjects whose record may change the receiver, chunk-ordered
   uint32_t pool_cap;
   uint32_t chunks;      // ceil(N / SYNC_CHUNK)
@@ -197,7 +199,9 @@ __device__ void compact_list(const Ctx& c, uint32_t v, uint32_t* list, uint32_t&
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(256) k_compact(Ctx c, Counters* k) {
+__global__ void __launch_bounds__(256) k_compact(Ctx c, Counters* k, uint32_t bucket) {
+  // k_timers has drained this tick's wheel bucket
+  if (blockIdx.x == 0 && threadIdx.x == 0) c.wheel_cnt[bucket] = 0;
   const uint32_t cnt = k->compact_cnt;
   for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
     uint32_t v = c.compact_list[i];
@@ -269,7 +273,7 @@ __device__ inline void ping_req(const Ctx& c, uint32_t v, uint32_t t, unsigned l
   nreq++;
   uint32_t pending_mask = 0, npend = 0;
   for (uint32_t j = 0; j < nr; ++j) {
-    if (out_fail(c, v, relays[j], draw(c, v, SWIM_STREAM_PINGREQ_OUT, j, 0))) publish_fd(c, v, t, SWIM_SUSPECT, nev);
+    if (out_fail(c, v, relays[j], v, SWIM_STREAM_PINGREQ_OUT, j, 0)) publish_fd(c, v, t, SWIM_SUSPECT, nev);
     else { pending_mask |= 1u << j; npend++; }
   }
   if (npend == 0) return;
@@ -277,9 +281,9 @@ __device__ inline void ping_req(const Ctx& c, uint32_t v, uint32_t t, unsigned l
   for (uint32_t j = 0; j < nr; ++j) {
     if (!(pending_mask & (1u << j))) continue;
     uint32_t r = relays[j];
-    if (in_pass(c, r, v) && !out_fail(c, r, t, draw(c, v, SWIM_STREAM_TRANSIT_PING_OUT, j, 0)) &&
-        in_pass(c, t, r) && !out_fail(c, t, r, draw(c, v, SWIM_STREAM_TRANSIT_ACK_OUT, j, 0)) &&
-        in_pass(c, r, t) && !out_fail(c, r, v, draw(c, v, SWIM_STREAM_RELAY_ACK_OUT, j, 0))) {
+    if (in_pass(c, r, v) && !out_fail(c, r, t, v, SWIM_STREAM_TRANSIT_PING_OUT, j, 0) &&
+        in_pass(c, t, r) && !out_fail(c, t, r, v, SWIM_STREAM_TRANSIT_ACK_OUT, j, 0) &&
+        in_pass(c, r, t) && !out_fail(c, r, v, v, SWIM_STREAM_RELAY_ACK_OUT, j, 0)) {
       arrived = (int32_t)j;
       break;
     }
@@ -323,9 +327,9 @@ __global__ void k_fd(Ctx c) {
       }
       uint32_t t = pl[m.ping_cursor++];
       npings++;
-      if (out_fail(c, v, t, draw(c, v, SWIM_STREAM_PING_OUT, 0, 0))) {
+      if (out_fail(c, v, t, v, SWIM_STREAM_PING_OUT, 0, 0)) {
         ping_req(c, v, t, nev, nreq);
-      } else if (in_pass(c, t, v) && !out_fail(c, t, v, draw(c, v, SWIM_STREAM_ACK_OUT, 0, 0)) && in_pass(c, v, t)) {
+      } else if (in_pass(c, t, v) && !out_fail(c, t, v, v, SWIM_STREAM_ACK_OUT, 0, 0) && in_pass(c, v, t)) {
         publish_fd(c, v, t, SWIM_ALIVE, nev);
       } else {
         m.ack_due = c.T + c.to_ticks;
@@ -394,7 +398,7 @@ __global__ void k_gossip_emit(Ctx c, Bufs b) {
       if (!((uint64_t)g.inf_period + spread >= period)) continue;
       if (g.inf0 == t || g.inf1 == t) continue;
       nmsg++;
-      if (!t_up || lost(loss, draw(c, v, SWIM_STREAM_GOSSIP_OUT, j, p)) || !pass) continue;
+      if (!t_up || lost_k(c, loss, v, SWIM_STREAM_GOSSIP_OUT, j, p) || !pass) continue;
       // certain duplicate at the receiver: its collector already holds the sequence id and can
       // only grow until delivery
       if (coll_contains(coll_find(c, t, g.gossiper), g.seq)) continue;
@@ -530,9 +534,19 @@ __global__ void k_gossip_deliver(Ctx c, Bufs b) {
 }
 
 // ------------------------------------------------------------------------------- list inserts
-__global__ void k_ins_scatter(Ctx c, Bufs b) {
+// one workgroup: a contiguous op region per viewer, ops placed by their per-viewer rank
+__global__ void __launch_bounds__(1024) k_ins_prep(Ctx c, Bufs b) {
+  __shared__ uint32_t s_cursor;
+  if (threadIdx.x == 0) s_cursor = 0;
+  __syncthreads();
+  const uint32_t nv = *c.ins_list_cnt;
+  for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x) {
+    const uint32_t v = c.ins_list[i];
+    b.ins_start[v] = atomicAdd(&s_cursor, c.ins_cnt[v]);
+  }
+  __syncthreads();
   const uint32_t n = min(*c.ins_total, c.ins_cap);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
     const InsOp op = c.ins[i];
     b.ins_out[b.ins_start[op.v] + op.rank] = op;
   }
@@ -612,7 +626,7 @@ __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t
   q.from = v; q.to = to; q.ordinal = ordinal; q.slot = 0; q.flags = initial ? RQ_INITIAL : 0;
   q.pad[0] = q.pad[1] = q.pad[2] = 0;
   if (initial) m.init_total++;
-  if (out_fail(c, v, to, draw(c, v, SWIM_STREAM_SYNC_OUT, ordinal, 0))) {
+  if (out_fail(c, v, to, v, SWIM_STREAM_SYNC_OUT, ordinal, 0)) {
     q.flags |= RQ_OUTFAIL;
     if (initial) m.init_done++;
   } else if (in_pass(c, to, v)) {
@@ -658,8 +672,10 @@ __global__ void k_sync_collect(Ctx c, Bufs b) {
 
 // ------------------------------------------------------------------------------- end of tick
 // start0's doFinally (:285-289) for members that joined this tick; graceful leaves complete.
-__global__ void k_end_tick(Ctx c) {
+__global__ void k_end_tick(Ctx c, Counters* k) {
   uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  // every other kernel of the tick has completed: reset the per-tick scratch counters
+  if (v < sizeof(Counters) / 4) reinterpret_cast<uint32_t*>(k)[v] = 0;
   if (v >= c.n) return;
   MemberDev& m = c.mem[v];
   if (m.join_now) {

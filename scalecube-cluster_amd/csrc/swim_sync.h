@@ -102,6 +102,7 @@ __global__ void __launch_bounds__(1024) k_sync_prep(Ctx c, Bufs b, int d2) {
   // merged into during this sub-phase gets its row snapshotted by k_sync_classify
   const uint32_t ni = s_cursor;
   for (uint32_t i = tid; i < ni; i += nt) {
+    b.item_total[i] = 0;
     const uint32_t src = p.out[i].from;
     if (p.cnt[src] == 0) continue;
     if (atomicCAS(&b.snap_idx[src], NONE, NONE - 1) == NONE) {
@@ -114,8 +115,7 @@ __global__ void __launch_bounds__(1024) k_sync_prep(Ctx c, Bufs b, int d2) {
 }
 
 __global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(Ctx c, Bufs b, int d2) {
-  __shared__ uint32_t s_wave[CLS_BLOCK / 64 + 1];
-  __shared__ uint32_t s_base;
+  __shared__ uint32_t s_bits[SYNC_CHUNK / 32];
   const SubPhase p = sub_phase(b, d2);
   const uint32_t ni = *p.nitems;
   const uint32_t chunks = b.chunks, n = c.n;
@@ -129,63 +129,80 @@ __global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(Ctx c, Bufs b, int 
     const uint32_t si = b.snap_idx[src];
     uint64_t* snapdst = si < b.snap_cap ? b.snap + (size_t)si * n : nullptr;
     if (ch == 0) msgs++;
-    const uint32_t x0 = ch * SYNC_CHUNK + threadIdx.x * CLS_CPT;
-    uint32_t flags = 0;
-    if (x0 + CLS_CPT <= n && ((reinterpret_cast<uintptr_t>(content + x0) | reinterpret_cast<uintptr_t>(rv + x0)) & 15) == 0) {
-      uint64_t a[CLS_CPT], o[CLS_CPT];
+    // coalesced: load j of lane t covers subjects base + j*512 + 2t, +1 (1 KiB per wave-instruction)
+    const uint32_t base = ch * SYNC_CHUNK;
+    uint32_t flags = 0;  // bit 2j+h = subject base + j*512 + 2*tid + h
+    if (base + SYNC_CHUNK <= n && ((reinterpret_cast<uintptr_t>(content + base) | reinterpret_cast<uintptr_t>(rv + base)) & 15) == 0) {
+      ulonglong2 a[CLS_CPT / 2], o[CLS_CPT / 2];
 #pragma unroll
-      for (int k = 0; k < CLS_CPT; k += 2) {
-        const ulonglong2 va = *reinterpret_cast<const ulonglong2*>(content + x0 + k);
-        a[k] = va.x; a[k + 1] = va.y;
-      }
+      for (int j = 0; j < CLS_CPT / 2; ++j)
+        a[j] = *reinterpret_cast<const ulonglong2*>(content + base + j * 2 * CLS_BLOCK + 2 * threadIdx.x);
 #pragma unroll
-      for (int k = 0; k < CLS_CPT; k += 2) {
-        const ulonglong2 vo = *reinterpret_cast<const ulonglong2*>(rv + x0 + k);
-        o[k] = vo.x; o[k + 1] = vo.y;
-      }
+      for (int j = 0; j < CLS_CPT / 2; ++j)
+        o[j] = *reinterpret_cast<const ulonglong2*>(rv + base + j * 2 * CLS_BLOCK + 2 * threadIdx.x);
       if (snapdst) {
 #pragma unroll
-        for (int k = 0; k < CLS_CPT; k += 2)
-          *reinterpret_cast<ulonglong2*>(snapdst + x0 + k) = make_ulonglong2(a[k], a[k + 1]);
+        for (int j = 0; j < CLS_CPT / 2; ++j)
+          *reinterpret_cast<ulonglong2*>(snapdst + base + j * 2 * CLS_BLOCK + 2 * threadIdx.x) = a[j];
       }
 #pragma unroll
-      for (int k = 0; k < CLS_CPT; ++k) {
-        const bool rec = c_has(a[k], B_IN_TABLE);
-        recs += rec;
-        if (rec && sync_complex(a[k], o[k], x0 + k == r)) flags |= 1u << k;
+      for (int j = 0; j < CLS_CPT / 2; ++j) {
+        const uint32_t x = base + j * 2 * CLS_BLOCK + 2 * threadIdx.x;
+        const bool r0 = c_has(a[j].x, B_IN_TABLE), r1 = c_has(a[j].y, B_IN_TABLE);
+        recs += (uint32_t)r0 + (uint32_t)r1;
+        if (r0 && sync_complex(a[j].x, o[j].x, x == r)) flags |= 1u << (2 * j);
+        if (r1 && sync_complex(a[j].y, o[j].y, x + 1 == r)) flags |= 1u << (2 * j + 1);
       }
     } else {
-      for (int k = 0; k < CLS_CPT; ++k) {
-        const uint32_t x = x0 + k;
-        if (x >= n) break;
-        const uint64_t a = content[x];
-        if (snapdst) snapdst[x] = a;
-        if (c_has(a, B_IN_TABLE)) {
-          recs++;
-          if (sync_complex(a, rv[x], x == r)) flags |= 1u << k;
+      for (int j = 0; j < CLS_CPT / 2; ++j)
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t x = base + j * 2 * CLS_BLOCK + 2 * threadIdx.x + h;
+          if (x >= n) continue;
+          const uint64_t a = content[x];
+          if (snapdst) snapdst[x] = a;
+          if (c_has(a, B_IN_TABLE)) {
+            recs++;
+            if (sync_complex(a, rv[x], x == r)) flags |= 1u << (2 * j + h);
+          }
+        }
+    }
+    // almost every chunk has no record that can change the receiver: one barrier decides it
+    if (!__syncthreads_or(flags != 0)) {
+      if (threadIdx.x == 0) b.item_chunk[(size_t)i * chunks + ch] = make_uint2(0, 0);
+      continue;
+    }
+    // rare path: subject-ordered compaction through an LDS bitmap (bit x - base)
+    for (uint32_t wdx = threadIdx.x; wdx < SYNC_CHUNK / 32; wdx += CLS_BLOCK) s_bits[wdx] = 0;
+    __syncthreads();
+    for (int k = 0; k < CLS_CPT; ++k)
+      if (flags & (1u << k)) {
+        const uint32_t off = (k >> 1) * 2 * CLS_BLOCK + 2 * threadIdx.x + (k & 1);
+        atomicOr(&s_bits[off >> 5], 1u << (off & 31));
+      }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t total = 0;
+      for (uint32_t wdx = 0; wdx < SYNC_CHUNK / 32; ++wdx) total += __popc(s_bits[wdx]);
+      uint32_t pb = atomicAdd(&b.k->pool_cursor, total);
+      if (pb + total > b.pool_cap) {
+        set_err(c, ERR_PEND);
+        total = 0;
+      } else {
+        uint32_t o2 = pb;
+        for (uint32_t wdx = 0; wdx < SYNC_CHUNK / 32; ++wdx) {
+          uint32_t bits = s_bits[wdx];
+          while (bits) {
+            const uint32_t bit = __ffs(bits) - 1;
+            bits &= bits - 1;
+            b.pool[o2++] = base + wdx * 32 + bit;
+          }
         }
       }
+      b.item_chunk[(size_t)i * chunks + ch] = make_uint2(pb, total);
+      atomicAdd(&b.item_total[i], total);
+      cplx += total;
     }
-    uint32_t total;
-    const uint32_t off = block_exclusive_scan<CLS_BLOCK>((uint32_t)__popc(flags), s_wave, &total);
-    if (total) {
-      if (threadIdx.x == 0) {
-        uint32_t base = atomicAdd(&b.k->pool_cursor, total);
-        if (base + total > b.pool_cap) { set_err(c, ERR_PEND); base = 0; }
-        s_base = base;
-      }
-      __syncthreads();
-      const uint32_t base = s_base;
-      if (base + total <= b.pool_cap) {
-        uint32_t o2 = base + off;
-        for (int k = 0; k < CLS_CPT; ++k)
-          if (flags & (1u << k)) b.pool[o2++] = x0 + k;
-      }
-      if (threadIdx.x == 0) { b.item_chunk[(size_t)i * chunks + ch] = make_uint2(base, total); cplx += total; }
-      __syncthreads();
-    } else if (threadIdx.x == 0) {
-      b.item_chunk[(size_t)i * chunks + ch] = make_uint2(0, 0);
-    }
+    __syncthreads();
   }
   for (int d = 32; d > 0; d >>= 1) recs += __shfl_down(recs, d, 64);
   if ((threadIdx.x & 63) == 0) stat_add(c, ST_SYNC_RECORDS, recs);
@@ -273,7 +290,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(Ctx c, Bufs b, int d
       const uint32_t mod = s_mod;
       __syncthreads();  // every lane has read s_mod before lane 0 may set it
       if (mod == 0) {  // precomputed classification is exact: the row is unchanged
-        if (threadIdx.x == 0) {
+        if (threadIdx.x == 0 && b.item_total[first + q] != 0) {
           const uint2* ic = b.item_chunk + (size_t)(first + q) * chunks;
           for (uint32_t ch = 0; ch < chunks; ++ch) {
             const uint2 e = ic[ch];
@@ -299,7 +316,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(Ctx c, Bufs b, int d
       if (!d2) {
         for (uint32_t q = 0; q < k; ++q) {
           const SyncReq rq = p.out[first + q];
-          if (out_fail(c, s, rq.from, draw(c, s, SWIM_STREAM_SYNCACK_OUT, q, 0))) continue;
+          if (out_fail(c, s, rq.from, s, SWIM_STREAM_SYNCACK_OUT, q, 0)) continue;
           if (!in_pass(c, rq.from, s)) continue;
           if (rq.flags & RQ_INITIAL) atomicAdd(&c.mem[rq.from].init_done, 1u);
           add_ack(c, b, rq.from, s, q, (rq.flags & RQ_INITIAL) != 0);
