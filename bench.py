@@ -8,7 +8,7 @@ SURVEY.md §8 on synthetic input (a converged N-member cluster losing one member
     python bench.py [--gpus N] [--steps K] [--warmup W] [--members 65536]
 
 Prints ONE JSON line with `value` (whole-job member-periods/s), the `roofline` object of the
-dominant kernel (k_sync_merge, the SYNC row merge; HIP events on the engine's stream) and the
+dominant kernel (k_sync_classify, the SYNC record classification; HIP events on the engine's stream) and the
 `cpu_baseline` (the CPU oracle, 1 thread, bounded sample, rank 0 / N=1 only).
 """
 import argparse
@@ -155,11 +155,11 @@ def main():
                                + ("no faults" if args.workload == "quiet"
                                   else f"one member killed every {KILL_EVERY} periods"),
                    "members": n, "tick_ms": 100, "parallelism": f"replicas x{world}" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "kernel": "k_sync_merge", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+        "roofline": {"bound": "hbm", "kernel": "k_sync_classify", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                      "launches": prof["launches"], "avg_launch_ms": avg_ms,
                      "alg_bytes_per_launch": prof["alg_bytes"] / max(1, prof["launches"]),
-                     "merge_ms_share": prof["total_ms"] / (dt * 1e3)},
+                     "kernel_time_share": prof["total_ms"] / (dt * 1e3)},
         "stats": {k: stats[k] for k in ("syncs", "sync_records", "gossip_messages", "gossips_created", "pings",
                                          "timers_fired", "events")},
     }

@@ -99,6 +99,18 @@ static int32_t hip_status() {
 
 static uint32_t grid_for(uint32_t n, uint32_t block) { return std::max(1u, (n + block - 1) / block); }
 
+// device counters are replicated ST_REPL times; sum them
+static int32_t read_stats(swim_engine* e, unsigned long long* st) {
+  std::vector<unsigned long long> rep((size_t)ST_COUNT * ST_REPL);
+  if (hipMemcpy(rep.data(), e->c.stats, sizeof(unsigned long long) * rep.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    return SWIM_EDEVICE;
+  for (int s = 0; s < ST_COUNT; ++s) {
+    st[s] = 0;
+    for (int r = 0; r < ST_REPL; ++r) st[s] += rep[(size_t)s * ST_REPL + r];
+  }
+  return SWIM_OK;
+}
+
 static void prof_flush(swim_engine* e) {
   for (uint32_t i = 0; i < e->prof_used; ++i) {
     float ms = 0.f;
@@ -370,7 +382,7 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
             e->alloc(&c.default_loss, n) && e->alloc(&c.default_inbound, n) && e->alloc(&c.group, n) &&
             e->alloc(&c.links, 1) && e->alloc(&c.is_seed, n) && e->alloc(&c.seeds, n) && e->alloc(&c.ins, c.ins_cap) &&
             e->alloc(&c.ins_cnt, n) && e->alloc(&c.ins_list, n) && e->alloc(&c.compact_flag, n) &&
-            e->alloc(&c.compact_list, n) && e->alloc(&c.stats, ST_COUNT) && e->alloc(&c.err, 1) &&
+            e->alloc(&c.compact_list, n) && e->alloc(&c.stats, (size_t)ST_COUNT * ST_REPL) && e->alloc(&c.err, 1) &&
             e->alloc(&e->k, 1) && e->alloc(&b.msgs, b.msg_cap) && e->alloc(&b.msgs_out, b.msg_cap) &&
             e->alloc(&b.msg_cnt, n) && e->alloc(&b.msg_start, n) && e->alloc(&b.msg_recv, n) &&
             e->alloc(&b.reqs, b.req_cap) && e->alloc(&b.reqs_out, b.req_cap) && e->alloc(&b.req_cnt, n) &&
@@ -398,7 +410,7 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
   hipMemsetAsync(c.is_seed, 0, n, s);
   hipMemsetAsync(c.ins_cnt, 0, 4 * (size_t)n, s);
   hipMemsetAsync(c.compact_flag, 0, 4 * (size_t)n, s);
-  hipMemsetAsync(c.stats, 0, 8 * ST_COUNT, s);
+  hipMemsetAsync(c.stats, 0, 8 * (size_t)ST_COUNT * ST_REPL, s);
   hipMemsetAsync(c.err, 0, 4, s);
   hipMemsetAsync(e->k, 0, sizeof(Counters), s);
   hipMemsetAsync(b.msg_cnt, 0, 4 * (size_t)n, s);
@@ -582,7 +594,7 @@ int32_t swim_get_stats(swim_engine* e, swim_stats* out) {
   if (!e || !out) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
   unsigned long long st[ST_COUNT];
-  if (hipMemcpy(st, e->c.stats, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+  if (read_stats(e, st) != SWIM_OK) return SWIM_EDEVICE;
   std::memset(out, 0, sizeof(*out));
   out->ticks = e->host_ticks;
   out->pings = st[ST_PINGS];
@@ -714,7 +726,7 @@ int32_t swim_profile_enable(swim_engine* e, int32_t enable) {
   e->prof_ms = 0;
   e->prof_launches = 0;
   unsigned long long st[ST_COUNT];
-  if (hipMemcpy(st, e->c.stats, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+  if (read_stats(e, st) != SWIM_OK) return SWIM_EDEVICE;
   e->prof_base_msgs = st[ST_MERGE_MSGS];
   e->prof_base_recs = st[ST_MERGE_RECORDS];
   e->prof = enable != 0;
@@ -726,7 +738,7 @@ int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
   prof_flush(e);
   unsigned long long st[ST_COUNT];
-  if (hipMemcpy(st, e->c.stats, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+  if (read_stats(e, st) != SWIM_OK) return SWIM_EDEVICE;
   out->launches = e->prof_launches;
   out->total_ms = e->prof_ms;
   out->messages = st[ST_MERGE_MSGS] - e->prof_base_msgs;

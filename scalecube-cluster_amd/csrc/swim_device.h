@@ -190,8 +190,17 @@ __device__ __forceinline__ uint64_t c_with_deadline(uint64_t c, uint64_t tick) {
 __device__ __forceinline__ uint64_t* row(const Ctx& c, uint32_t v) { return c.cells + (size_t)v * c.n; }
 
 __device__ __forceinline__ void set_err(const Ctx& c, uint32_t bit) { atomicOr(c.err, bit); }
+// Counters are replicated ST_REPL times (summed on readback) so that thousands of workgroups never
+// serialise on one address (MI355X_MICROARCH.md: one contended address is ~14x slower).
+constexpr int ST_REPL = 64;
 __device__ __forceinline__ void stat_add(const Ctx& c, int slot, unsigned long long x) {
-  if (x) atomicAdd(&c.stats[slot], x);
+  if (x) atomicAdd(&c.stats[slot * ST_REPL + (blockIdx.x & (ST_REPL - 1))], x);
+}
+// wave-reduced counter add; every lane of the wave must be active (call after reconvergence)
+__device__ __forceinline__ void wave_stat_add(const Ctx& c, int slot, unsigned long long x) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+  if ((threadIdx.x & 63) == 0) stat_add(c, slot, x);
 }
 
 // MembershipRecord.isOverrides (MembershipRecord.java:67-88); r0p = false for "no record"

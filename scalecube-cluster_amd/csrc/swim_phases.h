@@ -174,7 +174,7 @@ __global__ void k_timers(Ctx c, uint32_t bucket) {
     fired++;
     if (c_has(old, B_IN_TABLE)) update_membership(c, v, s, SWIM_DEAD, c_inc(old), R_TIMEOUT, SWIM_PHASE_TIMERS);
   }
-  stat_add(c, ST_TIMERS_FIRED, fired);
+  wave_stat_add(c, ST_TIMERS_FIRED, fired);
 }
 
 // REMOVED -> pingMembers.remove / remoteMembers.remove (FailureDetectorImpl.java:323-333,
@@ -298,15 +298,13 @@ __device__ inline void ping_req(const Ctx& c, uint32_t v, uint32_t t, unsigned l
   }
 }
 
-__global__ void k_fd(Ctx c) {
-  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= c.n) return;
+__device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& nev, unsigned long long& nreq,
+                                 unsigned long long& npings) {
   MemberDev& m = c.mem[v];
   if (!m.up) return;
   const bool due = (int64_t)c.T > m.fd_start && ((int64_t)c.T - m.fd_start) % c.P == 0;
   if (!due && m.relay_due != c.T && m.ack_due != c.T) return;
   m.ev_minor = 0;
-  unsigned long long nev = 0, nreq = 0, npings = 0;
   if (m.relay_due == c.T) {  // relay timeouts (:200-209)
     uint32_t t = m.relay_target, k = m.relay_pending;
     m.relay_due = 0;
@@ -337,9 +335,16 @@ __global__ void k_fd(Ctx c) {
       }
     }
   }
-  stat_add(c, ST_FD_EVENTS, nev);
-  stat_add(c, ST_PING_REQS, nreq);
-  stat_add(c, ST_PINGS, npings);
+}
+
+// launched with a multiple of 64 threads per block: every lane reaches the wave-reduced counters
+__global__ void k_fd(Ctx c) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long nev = 0, nreq = 0, npings = 0;
+  if (v < c.n) fd_member(c, v, nev, nreq, npings);
+  wave_stat_add(c, ST_FD_EVENTS, nev);
+  wave_stat_add(c, ST_PING_REQS, nreq);
+  wave_stat_add(c, ST_PINGS, npings);
 }
 
 // ------------------------------------------------------------------------------- phase C
@@ -360,14 +365,12 @@ __global__ void k_gossip_seg(Ctx c) {
 }
 
 // doSpreadGossip (:141-184): period++, select members, send, sweep, complete futures.
-__global__ void k_gossip_emit(Ctx c, Bufs b) {
-  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= c.n) return;
+__device__ inline unsigned long long gossip_emit_member(const Ctx& c, const Bufs& b, uint32_t v) {
   MemberDev& m = c.mem[v];
-  if (!gossip_due(c, m)) return;
+  if (!gossip_due(c, m)) return 0;
   const uint64_t period = m.g_period++;
   m.period_used = period;
-  if (m.gossip_len == 0) return;
+  if (m.gossip_len == 0) return 0;
   // selectGossipMembers (:322-343)
   uint32_t targets[16];
   uint32_t nt = 0;
@@ -413,7 +416,6 @@ __global__ void k_gossip_emit(Ctx c, Bufs b) {
       b.msgs[i] = msg;
     }
   }
-  stat_add(c, ST_GOSSIP_MESSAGES, nmsg);
   // sweep (:158-164, :350-358), order preserving
   uint32_t w = 0;
   for (uint32_t p = 0; p < m.gossip_len; ++p) {
@@ -431,6 +433,13 @@ __global__ void k_gossip_emit(Ctx c, Bufs b) {
         m.leave_done = 1;
     }
   }
+  return nmsg;
+}
+
+__global__ void k_gossip_emit(Ctx c, Bufs b) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long nmsg = v < c.n ? gossip_emit_member(c, b, v) : 0;
+  wave_stat_add(c, ST_GOSSIP_MESSAGES, nmsg);
 }
 
 // group-by-receiver: region start per receiver, then scatter by (start + arrival slot)
@@ -485,6 +494,7 @@ __device__ inline void sort_msgs(GMsgFull* a, uint32_t n) {
 // onGossipReq (GossipProtocolImpl.java:201-215) at each receiver, canonical order (sender, pos)
 __global__ void k_gossip_deliver(Ctx c, Bufs b) {
   const uint32_t nrecv = b.k->msg_recv_cnt;
+  unsigned long long acc = 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrecv; i += gridDim.x * blockDim.x) {
     const uint32_t r = b.msg_recv[i];
     const uint32_t k = b.msg_cnt[r];
@@ -495,7 +505,6 @@ __global__ void k_gossip_deliver(Ctx c, Bufs b) {
     sort_msgs(a, k);
     m.ev_minor = 0;
     m.fetch_ctr = 0;
-    unsigned long long acc = 0;
     GossipDev* slab = c.slab + (size_t)r * c.gcap;
     for (uint32_t q = 0; q < k; ++q) {
       const GMsgFull g = a[q];
@@ -529,8 +538,8 @@ __global__ void k_gossip_deliver(Ctx c, Bufs b) {
         }
       }
     }
-    stat_add(c, ST_GOSSIP_ACCEPTED, acc);
   }
+  wave_stat_add(c, ST_GOSSIP_ACCEPTED, acc);
 }
 
 // ------------------------------------------------------------------------------- list inserts
@@ -640,11 +649,9 @@ __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t
 }
 
 // doSync (:339-357), FD-triggered SYNCs (:427-442) and start0's initial SYNC to every seed (:250-291)
-__global__ void k_sync_collect(Ctx c, Bufs b) {
-  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= c.n) return;
+__device__ inline unsigned long long sync_collect_member(const Ctx& c, const Bufs& b, uint32_t v) {
   MemberDev& m = c.mem[v];
-  if (!m.up) { m.fd_sync_cnt = 0; return; }
+  if (!m.up) { m.fd_sync_cnt = 0; return 0; }
   uint32_t k = 0;
   unsigned long long nsync = 0;
   if (m.sync_on && (int64_t)c.T > m.sync_start && ((int64_t)c.T - m.sync_start) % c.S == 0) {
@@ -664,7 +671,13 @@ __global__ void k_sync_collect(Ctx c, Bufs b) {
       if (s != v) { add_req(c, b, v, s, k++, true); nsync++; }
     }
   }
-  stat_add(c, ST_SYNCS, nsync);
+  return nsync;
+}
+
+__global__ void k_sync_collect(Ctx c, Bufs b) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long nsync = v < c.n ? sync_collect_member(c, b, v) : 0;
+  wave_stat_add(c, ST_SYNCS, nsync);
 }
 
 #include "swim_sync.h"
