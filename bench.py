@@ -7,6 +7,12 @@ SURVEY.md §8 on synthetic input (a converged N-member cluster losing one member
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--members 65536]
 
+With N > 1 (launched by torch.distributed.run, one process per GPU) the SAME N-member cluster is
+row-sharded over the N GPUs (swim_create_shard): each rank owns members [r*N/G, (r+1)*N/G) and the
+cross-shard GOSSIP_REQ / SYNC / SYNC_ACK traffic moves by RCCL send/recv over xGMI inside the
+library.  Total work is fixed, so `scaling` is "strong".  torch.distributed (gloo) only broadcasts
+the RCCL bootstrap id and brackets the timed region with barriers.
+
 Prints ONE JSON line with `value` (whole-job member-periods/s), the `roofline` object of the
 dominant kernel (k_sync_classify, the SYNC record classification; HIP events on the engine's stream) and the
 `cpu_baseline` (the CPU oracle, 1 thread, bounded sample, rank 0 / N=1 only).
@@ -86,6 +92,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=("quiet", "failures"), default="quiet")
     ap.add_argument("--gossip-capacity", type=int, default=0)
+    ap.add_argument("--local-shards", type=int, default=1,
+                    help="single-process sharded test rig (cfg.local_shards); measurement of the exchange only")
     args = ap.parse_args()
     global WORKLOAD
     WORKLOAD = args.workload
@@ -106,7 +114,13 @@ def main():
     n = args.members
     cfg = make_config(lib, local_rank)
     cfg.gossip_capacity = args.gossip_capacity
-    e = abi.Engine(lib, cfg, n, n, 1 + rank)
+    cfg.local_shards = args.local_shards
+    if world > 1:
+        obj = [abi.comm_unique_id(lib) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        e = abi.Engine(lib, cfg, n, n, 1, rank=rank, world=world, comm_id=obj[0])
+    else:
+        e = abi.Engine(lib, cfg, n, n, 1)
 
     def barrier():
         if world > 1:
@@ -131,10 +145,16 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        keys = ("syncs", "sync_records", "gossip_messages", "gossips_created", "pings", "timers_fired", "events")
+        st = torch.tensor([float(stats[k]) for k in keys] + [float(prof["alg_bytes"]), prof["total_ms"],
+                                                             float(prof["launches"])], dtype=torch.float64)
+        dist.all_reduce(st, op=dist.ReduceOp.SUM)
+        stats.update({k: int(v) for k, v in zip(keys, st[:len(keys)].tolist())})
+        prof = {"alg_bytes": st[-3].item(), "total_ms": st[-2].item(), "launches": int(st[-1].item())}
     if stats["capacity_errors"]:
         raise SystemExit(f"capacity error during the benchmark: {stats['capacity_errors']:#x}")
 
-    value = n * args.steps * world / dt
+    value = n * args.steps / dt  # one cluster of n members, sharded over `world` GPUs
     avg_ms = prof["total_ms"] / max(1, prof["launches"])
     achieved = prof["alg_bytes"] / max(1e-12, prof["total_ms"] / 1e3) / 1e9
     line = {
@@ -146,20 +166,23 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",
-        "config": {"workload": f"config4-lan-{args.workload}: N={n} members per GPU, LAN defaults (ping 1 s / "
+        "config": {"workload": f"config4-lan-{args.workload}: N={n} members (one cluster), LAN defaults (ping 1 s / "
                                f"gossip 200 ms / sync 30 s staggered), 0% loss, "
                                + ("no faults" if args.workload == "quiet"
                                   else f"one member killed every {KILL_EVERY} periods"),
-                   "members": n, "tick_ms": 100, "parallelism": f"replicas x{world}" if world > 1 else "single"},
+                   "members": n, "tick_ms": 100,
+                   "parallelism": (f"rows sharded over {world} GPUs, RCCL send/recv over xGMI" if world > 1 else
+                                   f"single GPU, {args.local_shards} in-process shards" if args.local_shards > 1
+                                   else "single GPU")},
         "roofline": {"bound": "hbm", "kernel": "k_sync_classify", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                      "launches": prof["launches"], "avg_launch_ms": avg_ms,
                      "alg_bytes_per_launch": prof["alg_bytes"] / max(1, prof["launches"]),
-                     "kernel_time_share": prof["total_ms"] / (dt * 1e3)},
+                     "kernel_time_share": prof["total_ms"] / (dt * 1e3 * world)},
         "stats": {k: stats[k] for k in ("syncs", "sync_records", "gossip_messages", "gossips_created", "pings",
                                          "timers_fired", "events")},
     }

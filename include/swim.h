@@ -116,7 +116,10 @@ typedef struct swim_config {
                                  (power of two; 0 = default 1024) */
   uint32_t event_capacity;    /* undrained events the engine may buffer (0 = default 1<<22) */
   int32_t device;             /* HIP device ordinal the engine runs on (one engine per GPU) */
-  uint32_t reserved[7];
+  int32_t local_shards;       /* swim_create only: > 1 runs the cluster as this many row shards in
+                                 one process on `device`, exchanging cross-shard messages with
+                                 device copies (the single-GPU test rig of swim_create_shard) */
+  uint32_t reserved[6];
 } swim_config;
 
 /* preset: 0 = defaultConfig/defaultLanConfig, 1 = defaultWanConfig, 2 = defaultLocalConfig
@@ -142,6 +145,24 @@ typedef struct swim_engine swim_engine;
 int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initial, uint64_t seed,
                     swim_engine** out);
 int32_t swim_destroy(swim_engine* e);
+
+/*
+ * Multi-GPU: one process per GPU, member rows sharded by viewer.  Rank r of `world`
+ * owns viewers [r*ceil(N/world), (r+1)*ceil(N/world)); GOSSIP_REQ, SYNC and SYNC_ACK traffic to
+ * other shards moves by RCCL send/recv over xGMI inside swim_step.  Rank 0 calls
+ * swim_comm_unique_id and the host broadcasts the SWIM_COMM_ID_BYTES bytes to every rank (the
+ * reference has no counterpart: its members are separate JVM objects talking over TCP,
+ * ClusterImpl.java:260-291 + TransportImpl.java:214-238).  Every swim_* call on a sharded engine is
+ * collective: all ranks make the same calls in the same order (control ops are replicated, reads of
+ * rows / members / lists / gossips / collectors are answered only by the owning rank and return
+ * SWIM_EINVAL elsewhere; events and stats are those of the rank's own viewers).
+ */
+#define SWIM_COMM_ID_BYTES 128
+int32_t swim_comm_unique_id(uint8_t* out /* SWIM_COMM_ID_BYTES */);
+int32_t swim_create_shard(const swim_config* cfg, uint32_t capacity, uint32_t n_initial, uint64_t seed,
+                          int32_t rank, int32_t world, const uint8_t* comm_id, swim_engine** out);
+/* rank / world of the engine and the viewer range [lo, lo + count) it answers reads for */
+int32_t swim_shard_info(const swim_engine* e, int32_t* rank, int32_t* world, uint32_t* lo, uint32_t* count);
 
 /* Advance virtual time.  swim_step advances `periods` * (ping_interval / tick) ticks. */
 int32_t swim_step_ticks(swim_engine* e, uint32_t ticks);

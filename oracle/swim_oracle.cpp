@@ -1049,6 +1049,30 @@ int32_t swim_destroy(swim_engine* e) {
   return SWIM_OK;
 }
 
+// Row sharding is a deployment of the same lockstep semantics: a sharded GPU run
+// must equal the unsharded one bit for bit.  The oracle is the unsharded restatement, so it only
+// accepts world = 1 and answers for the whole cluster.
+int32_t swim_comm_unique_id(uint8_t* out) {
+  if (!out) return SWIM_EINVAL;
+  std::memset(out, 0, SWIM_COMM_ID_BYTES);
+  return SWIM_OK;
+}
+
+int32_t swim_create_shard(const swim_config* cfg, uint32_t capacity, uint32_t n_initial, uint64_t seed, int32_t rank,
+                          int32_t world, const uint8_t*, swim_engine** out) {
+  if (world != 1 || rank != 0) return SWIM_EINVAL;
+  return swim_create(cfg, capacity, n_initial, seed, out);
+}
+
+int32_t swim_shard_info(const swim_engine* e, int32_t* rank, int32_t* world, uint32_t* lo, uint32_t* count) {
+  if (!e) return SWIM_EINVAL;
+  if (rank) *rank = 0;
+  if (world) *world = 1;
+  if (lo) *lo = 0;
+  if (count) *count = e->n;
+  return SWIM_OK;
+}
+
 int32_t swim_step_ticks(swim_engine* e, uint32_t ticks) {
   if (!e) return SWIM_EINVAL;
   for (uint32_t i = 0; i < ticks; ++i) e->step_tick();

@@ -1,10 +1,20 @@
 // engine.hip — host orchestration and C ABI (include/swim.h) of libswimgpu.so.
 //
-// One swim_engine owns all device memory of one simulated cluster on the current HIP device and
-// advances it tick by tick with the kernel sequence of swim_kernels.h on one HIP stream.  No host
-// synchronisation happens inside a tick; the host syncs once per swim_step_ticks call (and every
-// kDrainEvery ticks) to move events to the host buffer and to check the capacity-error word.
+// A swim_engine simulates one cluster of N members whose view rows are sharded by viewer
+// (DESIGN.md §7).  It holds the shards it runs in this process:
+//   * unsharded (world = 1): one shard owning every row — the single-GPU engine;
+//   * local group (cfg.local_shards = G > 1): all G shards in this process on one device, exchanging
+//     cross-shard messages with device-to-device copies (the bit-exact test rig of the sharded path);
+//   * RCCL (swim_create_shard): one shard per process / GPU, exchanging with ncclSend / ncclRecv
+//     over xGMI.
+// Both multi-shard modes run the same exchange plan (counts per destination shard -> packed content
+// rows -> segments concatenated in source-shard order); only the copy primitive differs.
+//
+// Per tick every shard runs the kernel sequence of swim_phases.h on the engine's stream.  An
+// unsharded engine never synchronises inside a tick; a sharded one synchronises once per exchange
+// (gossip round, SYNC, SYNC_ACK) to learn the per-destination counts.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -21,6 +31,7 @@ namespace {
 constexpr uint32_t kDrainEvery = 256;
 constexpr uint32_t kClassifyGrid = 2048;  // grid-stride over (message, chunk) work units
 constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
+constexpr uint32_t kStopCap = 4096;
 
 uint32_t gcd_u(uint32_t a, uint32_t b) {
   while (b) { uint32_t t = a % b; a = b; b = t; }
@@ -43,48 +54,97 @@ hipError_t dalloc(T** p, size_t count) {
   return hipMalloc((void**)p, sizeof(T) * (count ? count : 1));
 }
 
+uint32_t grid_for(uint32_t n, uint32_t block) { return std::max(1u, (n + block - 1) / block); }
+
 }  // namespace
 
-struct swim_engine {
-  swim_config cfg{};
-  int32_t device = 0;
-  uint32_t n = 0, tick_ms = 0, P = 0, G = 0, S = 0;
-  uint64_t T = 0;
-  hipStream_t stream = nullptr;
+// One shard: the device state of rows [lo, lo + nl) plus the replicated arrays.
+struct Shard {
   Ctx c{};
   Bufs b{};
   Counters* k = nullptr;
-  CollDev* kat_coll = nullptr;
-  // host mirrors
-  std::vector<uint8_t> g_residue;  // gossip timer residues mod G in use
-  std::vector<uint32_t> seeds;
-  std::vector<uint8_t> is_seed_h;
-  std::vector<LinkDev> links_h;
-  uint32_t links_dev_cap = 0;
-  bool joins_pending = false;
-  std::vector<swim_event> events;
-  uint64_t host_ticks = 0, host_events = 0;
-  uint32_t err_seen = 0;
+  Xc* x = nullptr;
   std::vector<void*> allocs;
-  // swim_profile_*: HIP events around every k_sync_merge launch on `stream`
-  bool prof = false;
+  // received cross-shard traffic (grown on demand; sizes are known on the host before each copy)
+  GMsgFull* rx_msgs = nullptr;
+  SyncReq* rx_reqs = nullptr;
+  uint64_t* rx_rows = nullptr;
+  uint32_t* rx_stops = nullptr;
+  uint64_t* tx_rows = nullptr;
+  size_t rx_msg_cap = 0, rx_req_cap = 0, rx_row_cap = 0, tx_row_cap = 0, rx_stop_cap = 0;
+  uint32_t n_rx_msgs = 0, n_rx_reqs = 0, n_rx_stops = 0;
+  uint32_t links_dev_cap = 0;
+  // swim_profile_*: HIP events around every k_sync_classify launch on the engine's stream
   std::vector<hipEvent_t> prof_ev;
   uint32_t prof_used = 0;
   double prof_ms = 0;
   uint64_t prof_launches = 0;
   unsigned long long prof_base_msgs = 0, prof_base_recs = 0;
 
-  ~swim_engine() {
-    if (stream) hipStreamSynchronize(stream);
-    for (hipEvent_t ev : prof_ev) hipEventDestroy(ev);
-    for (void* p : allocs) hipFree(p);
-    if (stream) hipStreamDestroy(stream);
-  }
   template <typename T>
   bool alloc(T** p, size_t count) {
     if (dalloc(p, count) != hipSuccess) return false;
     allocs.push_back((void*)*p);
     return true;
+  }
+  template <typename T>
+  bool grow(T** p, size_t* cap, size_t need) {
+    if (need <= *cap) return true;
+    size_t nc = std::max<size_t>(need, *cap * 2);
+    T* q = nullptr;
+    if (dalloc(&q, nc) != hipSuccess) return false;
+    if (*p) {
+      allocs.erase(std::remove(allocs.begin(), allocs.end(), (void*)*p), allocs.end());
+      hipFree(*p);
+    }
+    *p = q;
+    *cap = nc;
+    allocs.push_back((void*)q);
+    return true;
+  }
+};
+
+struct swim_engine {
+  swim_config cfg{};
+  int32_t device = 0;
+  uint32_t n = 0, tick_ms = 0, P = 0, G = 0, S = 0, sz = 0;
+  uint64_t T = 0;
+  int32_t rank = 0, world = 1;  // this process's shard (RCCL) and the cluster's shard count
+  bool rccl = false;
+  ncclComm_t comm = nullptr;
+  hipStream_t stream = nullptr;
+  std::vector<Shard> sh;  // local shards, in shard order
+  CollDev* kat_coll = nullptr;
+  uint32_t* d_cnt = nullptr;  // RCCL: received per-peer counts
+  uint32_t* h_cnt = nullptr;  // pinned host mirror
+  // host mirrors of replicated control state
+  std::vector<uint8_t> g_residue;  // gossip timer residues mod G in use
+  std::vector<uint32_t> seeds;
+  std::vector<uint8_t> is_seed_h, joined_h, join_pending_h;
+  std::vector<LinkDev> links_h;
+  std::vector<uint32_t> joins;  // joins starting at the next tick
+  std::vector<swim_event> events;
+  uint64_t host_ticks = 0, host_events = 0;
+  uint32_t err_seen = 0;
+  bool prof = false;
+
+  ~swim_engine() {
+    if (stream) hipStreamSynchronize(stream);
+    for (Shard& s : sh) {
+      for (hipEvent_t ev : s.prof_ev) hipEventDestroy(ev);
+      for (void* p : s.allocs) hipFree(p);
+    }
+    if (kat_coll) hipFree(kat_coll);
+    if (d_cnt) hipFree(d_cnt);
+    if (h_cnt) hipHostFree(h_cnt);
+    if (comm) ncclCommDestroy(comm);
+    if (stream) hipStreamDestroy(stream);
+  }
+  // the local shard owning member v, or nullptr (RCCL: owned by another process)
+  Shard* owner_of(uint32_t v) {
+    const uint32_t o = v / sz;
+    if (!rccl) return &sh[o];
+    return (int32_t)o == rank ? &sh[0] : nullptr;
   }
 };
 
@@ -97,123 +157,344 @@ static int32_t hip_status() {
   return SWIM_OK;
 }
 
-static uint32_t grid_for(uint32_t n, uint32_t block) { return std::max(1u, (n + block - 1) / block); }
+static int32_t nccl_ok(ncclResult_t r) {
+  if (r == ncclSuccess) return SWIM_OK;
+  std::fprintf(stderr, "libswimgpu: RCCL error %s\n", ncclGetErrorString(r));
+  return SWIM_EDEVICE;
+}
 
-// device counters are replicated ST_REPL times; sum them
+// device counters are replicated ST_REPL times; sum them over every local shard
 static int32_t read_stats(swim_engine* e, unsigned long long* st) {
   std::vector<unsigned long long> rep((size_t)ST_COUNT * ST_REPL);
-  if (hipMemcpy(rep.data(), e->c.stats, sizeof(unsigned long long) * rep.size(), hipMemcpyDeviceToHost) != hipSuccess)
-    return SWIM_EDEVICE;
-  for (int s = 0; s < ST_COUNT; ++s) {
-    st[s] = 0;
-    for (int r = 0; r < ST_REPL; ++r) st[s] += rep[(size_t)s * ST_REPL + r];
+  for (int s = 0; s < ST_COUNT; ++s) st[s] = 0;
+  for (Shard& sd : e->sh) {
+    if (hipMemcpy(rep.data(), sd.c.stats, sizeof(unsigned long long) * rep.size(), hipMemcpyDeviceToHost) != hipSuccess)
+      return SWIM_EDEVICE;
+    for (int s = 0; s < ST_COUNT; ++s)
+      for (int r = 0; r < ST_REPL; ++r) st[s] += rep[(size_t)s * ST_REPL + r];
   }
   return SWIM_OK;
 }
 
-static void prof_flush(swim_engine* e) {
-  for (uint32_t i = 0; i < e->prof_used; ++i) {
+static void prof_flush(Shard& s) {
+  for (uint32_t i = 0; i < s.prof_used; ++i) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, e->prof_ev[2 * i], e->prof_ev[2 * i + 1]) == hipSuccess) e->prof_ms += ms;
+    if (hipEventElapsedTime(&ms, s.prof_ev[2 * i], s.prof_ev[2 * i + 1]) == hipSuccess) s.prof_ms += ms;
   }
-  e->prof_launches += e->prof_used;
-  e->prof_used = 0;
+  s.prof_launches += s.prof_used;
+  s.prof_used = 0;
 }
 
-static void launch_classify(swim_engine* e, int d2) {
-  const bool p = e->prof && 2 * (e->prof_used + 1) <= e->prof_ev.size();
-  if (p) hipEventRecord(e->prof_ev[2 * e->prof_used], e->stream);
-  k_sync_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(e->c, e->b, d2);
+static void launch_classify(swim_engine* e, Shard& s, int d2) {
+  const bool p = e->prof && 2 * (s.prof_used + 1) <= s.prof_ev.size();
+  if (p) hipEventRecord(s.prof_ev[2 * s.prof_used], e->stream);
+  k_sync_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(s.c, s.b, d2);
   if (p) {
-    hipEventRecord(e->prof_ev[2 * e->prof_used + 1], e->stream);
-    e->prof_used++;
+    hipEventRecord(s.prof_ev[2 * s.prof_used + 1], e->stream);
+    s.prof_used++;
   }
 }
 
 static int32_t sync_and_collect(swim_engine* e) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return hip_status() ? SWIM_EDEVICE : SWIM_EDEVICE;
-  uint32_t cnt = 0, err = 0;
-  if (hipMemcpy(&cnt, e->c.ev_cnt, 4, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
-  if (hipMemcpy(&err, e->c.err, 4, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
-  cnt = std::min(cnt, e->c.ev_cap);
-  if (cnt) {
-    size_t old = e->events.size();
-    e->events.resize(old + cnt);
-    if (hipMemcpy(e->events.data() + old, e->c.ev, sizeof(swim_event) * cnt, hipMemcpyDeviceToHost) != hipSuccess)
-      return SWIM_EDEVICE;
-    e->host_events += cnt;
-    uint32_t zero = 0;
-    if (hipMemcpy(e->c.ev_cnt, &zero, 4, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
+  uint32_t err_all = 0;
+  for (Shard& s : e->sh) {
+    uint32_t cnt = 0, err = 0;
+    if (hipMemcpy(&cnt, s.c.ev_cnt, 4, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+    if (hipMemcpy(&err, s.c.err, 4, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+    cnt = std::min(cnt, s.c.ev_cap);
+    if (cnt) {
+      size_t old = e->events.size();
+      e->events.resize(old + cnt);
+      if (hipMemcpy(e->events.data() + old, s.c.ev, sizeof(swim_event) * cnt, hipMemcpyDeviceToHost) != hipSuccess)
+        return SWIM_EDEVICE;
+      e->host_events += cnt;
+      uint32_t zero = 0;
+      if (hipMemcpy(s.c.ev_cnt, &zero, 4, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
+    }
+    err_all |= err;
+    if (e->prof) prof_flush(s);
   }
-  e->err_seen |= err;
-  if (e->prof) prof_flush(e);
-  return err ? SWIM_ECAPACITY : SWIM_OK;
+  e->err_seen |= err_all;
+  return err_all ? SWIM_ECAPACITY : SWIM_OK;
+}
+
+// ------------------------------------------------------------------------------- exchange
+// Per-destination counts of every local shard's outgoing traffic (and, with RCCL, the counts every
+// peer sends here).  `kind`: 0 gossip messages + stops, 1 SYNC, 2 SYNC_ACK.
+struct Counts {
+  uint32_t tx[MAXW][MAXW];  // [src][dst] (RCCL: only row `rank` is valid)
+  uint32_t rx[MAXW];        // RCCL: count arriving from each peer
+  uint32_t stop_tx[MAXW];   // [src]
+  uint32_t stop_rx[MAXW];   // RCCL: stop count of each peer
+};
+
+static int32_t read_counts(swim_engine* e, int kind, Counts* ct) {
+  std::memset(ct, 0, sizeof(*ct));
+  const uint32_t W = (uint32_t)e->world;
+  hipStream_t s = e->stream;
+  if (e->rccl) {
+    Shard& sd = e->sh[0];
+    uint32_t* send = kind == 0 ? sd.x->msg : kind == 1 ? sd.x->req : sd.x->ack;
+    if (ncclGroupStart() != ncclSuccess) return SWIM_EDEVICE;
+    ncclAllToAll(send, e->d_cnt, 1, ncclUint32, e->comm, s);
+    if (kind == 0) ncclAllGather(&sd.x->stop, e->d_cnt + MAXW, 1, ncclUint32, e->comm, s);
+    if (nccl_ok(ncclGroupEnd()) != SWIM_OK) return SWIM_EDEVICE;
+    hipMemcpyAsync(e->h_cnt, e->d_cnt, sizeof(uint32_t) * 2 * MAXW, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(e->h_cnt + 2 * MAXW, sd.x, sizeof(Xc), hipMemcpyDeviceToHost, s);
+    if (hipStreamSynchronize(s) != hipSuccess) return SWIM_EDEVICE;
+    const Xc* hx = reinterpret_cast<const Xc*>(e->h_cnt + 2 * MAXW);
+    const uint32_t* own = kind == 0 ? hx->msg : kind == 1 ? hx->req : hx->ack;
+    const uint32_t cap = kind == 0 ? sd.b.tx_msg_cap : sd.b.tx_req_cap;
+    for (uint32_t d = 0; d < W; ++d) {
+      ct->tx[e->rank][d] = std::min(own[d], cap);
+      ct->rx[d] = std::min(e->h_cnt[d], cap);
+      ct->stop_rx[d] = kind == 0 ? std::min(e->h_cnt[MAXW + d], kStopCap) : 0;
+    }
+    ct->stop_tx[e->rank] = kind == 0 ? std::min(hx->stop, kStopCap) : 0;
+    return SWIM_OK;
+  }
+  std::vector<Xc> hx(W);
+  for (uint32_t r = 0; r < W; ++r) hipMemcpyAsync(&hx[r], e->sh[r].x, sizeof(Xc), hipMemcpyDeviceToHost, s);
+  if (hipStreamSynchronize(s) != hipSuccess) return SWIM_EDEVICE;
+  for (uint32_t r = 0; r < W; ++r) {
+    const uint32_t* own = kind == 0 ? hx[r].msg : kind == 1 ? hx[r].req : hx[r].ack;
+    const uint32_t cap = kind == 0 ? e->sh[r].b.tx_msg_cap : e->sh[r].b.tx_req_cap;
+    for (uint32_t d = 0; d < W; ++d) ct->tx[r][d] = std::min(own[d], cap);
+    ct->stop_tx[r] = kind == 0 ? std::min(hx[r].stop, kStopCap) : 0;
+  }
+  return SWIM_OK;
+}
+
+// E1: GOSSIP_REQs for receivers on other shards + completed graceful leaves (broadcast)
+static int32_t exchange_msgs(swim_engine* e) {
+  Counts ct;
+  if (int32_t rc = read_counts(e, 0, &ct)) return rc;
+  const uint32_t W = (uint32_t)e->world;
+  hipStream_t s = e->stream;
+  if (e->rccl) {
+    Shard& sd = e->sh[0];
+    const uint32_t me = (uint32_t)e->rank;
+    size_t nm = 0, ns = 0;
+    for (uint32_t p = 0; p < W; ++p) if (p != me) { nm += ct.rx[p]; ns += ct.stop_rx[p]; }
+    if (!sd.grow(&sd.rx_msgs, &sd.rx_msg_cap, nm) || !sd.grow(&sd.rx_stops, &sd.rx_stop_cap, ns)) return SWIM_ENOMEM;
+    if (ncclGroupStart() != ncclSuccess) return SWIM_EDEVICE;
+    size_t om = 0, os = 0;
+    for (uint32_t p = 0; p < W; ++p) {
+      if (p == me) continue;
+      if (ct.tx[me][p]) ncclSend(sd.b.tx_msgs + (size_t)p * sd.b.tx_msg_cap, ct.tx[me][p] * sizeof(GMsgFull), ncclUint8, p, e->comm, s);
+      if (ct.stop_tx[me]) ncclSend(sd.b.tx_stops, ct.stop_tx[me] * 4, ncclUint8, p, e->comm, s);
+      if (ct.rx[p]) ncclRecv(sd.rx_msgs + om, ct.rx[p] * sizeof(GMsgFull), ncclUint8, p, e->comm, s);
+      if (ct.stop_rx[p]) ncclRecv(sd.rx_stops + os, ct.stop_rx[p] * 4, ncclUint8, p, e->comm, s);
+      om += ct.rx[p];
+      os += ct.stop_rx[p];
+    }
+    if (nccl_ok(ncclGroupEnd()) != SWIM_OK) return SWIM_EDEVICE;
+    sd.n_rx_msgs = (uint32_t)om;
+    sd.n_rx_stops = (uint32_t)os;
+    return SWIM_OK;
+  }
+  for (uint32_t d = 0; d < W; ++d) {
+    Shard& dst = e->sh[d];
+    size_t nm = 0, ns = 0;
+    for (uint32_t r = 0; r < W; ++r) if (r != d) { nm += ct.tx[r][d]; ns += ct.stop_tx[r]; }
+    if (!dst.grow(&dst.rx_msgs, &dst.rx_msg_cap, nm) || !dst.grow(&dst.rx_stops, &dst.rx_stop_cap, ns)) return SWIM_ENOMEM;
+    size_t om = 0, os = 0;
+    for (uint32_t r = 0; r < W; ++r) {
+      if (r == d) continue;
+      Shard& src = e->sh[r];
+      if (ct.tx[r][d])
+        hipMemcpyAsync(dst.rx_msgs + om, src.b.tx_msgs + (size_t)d * src.b.tx_msg_cap, ct.tx[r][d] * sizeof(GMsgFull),
+                       hipMemcpyDeviceToDevice, s);
+      if (ct.stop_tx[r])
+        hipMemcpyAsync(dst.rx_stops + os, src.b.tx_stops, ct.stop_tx[r] * 4, hipMemcpyDeviceToDevice, s);
+      om += ct.tx[r][d];
+      os += ct.stop_tx[r];
+    }
+    dst.n_rx_msgs = (uint32_t)om;
+    dst.n_rx_stops = (uint32_t)os;
+  }
+  return SWIM_OK;
+}
+
+// pack the content rows of shard `sd`'s outgoing SYNC (kind 1) / SYNC_ACK (kind 2) per destination
+static int32_t pack_rows(swim_engine* e, Shard& sd, uint32_t src_idx, int kind, const Counts& ct, PackPlan* plan) {
+  std::memset(plan, 0, sizeof(*plan));
+  uint32_t tot = 0;
+  for (uint32_t d = 0; d < (uint32_t)e->world; ++d) {
+    plan->cnt[d] = d == src_idx ? 0 : ct.tx[src_idx][d];
+    plan->off[d] = tot;
+    tot += plan->cnt[d];
+  }
+  if (!tot) return SWIM_OK;
+  if (!sd.grow(&sd.tx_rows, &sd.tx_row_cap, (size_t)tot * e->n)) return SWIM_ENOMEM;
+  const SyncReq* tx = kind == 1 ? sd.b.tx_reqs : sd.b.tx_acks;
+  k_pack_rows<<<std::min<uint32_t>(tot, 1024), 256, 0, e->stream>>>(sd.c, tx, sd.b.tx_req_cap, *plan, sd.tx_rows);
+  return SWIM_OK;
+}
+
+// E2 / E3: SYNC (kind 1) or SYNC_ACK (kind 2) headers + content rows for receivers on other shards
+static int32_t exchange_sync(swim_engine* e, int kind) {
+  Counts ct;
+  if (int32_t rc = read_counts(e, kind, &ct)) return rc;
+  const uint32_t W = (uint32_t)e->world;
+  const size_t row_bytes = (size_t)e->n * 8;
+  hipStream_t s = e->stream;
+  if (e->rccl) {
+    Shard& sd = e->sh[0];
+    const uint32_t me = (uint32_t)e->rank;
+    PackPlan plan;
+    if (int32_t rc = pack_rows(e, sd, me, kind, ct, &plan)) return rc;
+    size_t nr = 0;
+    for (uint32_t p = 0; p < W; ++p) if (p != me) nr += ct.rx[p];
+    if (!sd.grow(&sd.rx_reqs, &sd.rx_req_cap, nr) || !sd.grow(&sd.rx_rows, &sd.rx_row_cap, nr * e->n)) return SWIM_ENOMEM;
+    const SyncReq* tx = kind == 1 ? sd.b.tx_reqs : sd.b.tx_acks;
+    if (ncclGroupStart() != ncclSuccess) return SWIM_EDEVICE;
+    size_t o = 0;
+    for (uint32_t p = 0; p < W; ++p) {
+      if (p == me) continue;
+      if (plan.cnt[p]) {
+        ncclSend(tx + (size_t)p * sd.b.tx_req_cap, plan.cnt[p] * sizeof(SyncReq), ncclUint8, p, e->comm, s);
+        ncclSend(sd.tx_rows + (size_t)plan.off[p] * e->n, plan.cnt[p] * row_bytes, ncclUint8, p, e->comm, s);
+      }
+      if (ct.rx[p]) {
+        ncclRecv(sd.rx_reqs + o, ct.rx[p] * sizeof(SyncReq), ncclUint8, p, e->comm, s);
+        ncclRecv(sd.rx_rows + o * e->n, ct.rx[p] * row_bytes, ncclUint8, p, e->comm, s);
+      }
+      o += ct.rx[p];
+    }
+    if (nccl_ok(ncclGroupEnd()) != SWIM_OK) return SWIM_EDEVICE;
+    sd.n_rx_reqs = (uint32_t)o;
+    return SWIM_OK;
+  }
+  std::vector<PackPlan> plans(W);
+  for (uint32_t r = 0; r < W; ++r)
+    if (int32_t rc = pack_rows(e, e->sh[r], r, kind, ct, &plans[r])) return rc;
+  for (uint32_t d = 0; d < W; ++d) {
+    Shard& dst = e->sh[d];
+    size_t nr = 0;
+    for (uint32_t r = 0; r < W; ++r) if (r != d) nr += ct.tx[r][d];
+    if (!dst.grow(&dst.rx_reqs, &dst.rx_req_cap, nr) || !dst.grow(&dst.rx_rows, &dst.rx_row_cap, nr * e->n))
+      return SWIM_ENOMEM;
+    size_t o = 0;
+    for (uint32_t r = 0; r < W; ++r) {
+      if (r == d || !ct.tx[r][d]) continue;
+      Shard& src = e->sh[r];
+      const SyncReq* tx = kind == 1 ? src.b.tx_reqs : src.b.tx_acks;
+      hipMemcpyAsync(dst.rx_reqs + o, tx + (size_t)d * src.b.tx_req_cap, ct.tx[r][d] * sizeof(SyncReq),
+                     hipMemcpyDeviceToDevice, s);
+      hipMemcpyAsync(dst.rx_rows + o * e->n, src.tx_rows + (size_t)plans[r].off[d] * e->n, ct.tx[r][d] * row_bytes,
+                     hipMemcpyDeviceToDevice, s);
+      o += ct.tx[r][d];
+    }
+    dst.n_rx_reqs = (uint32_t)o;
+  }
+  return SWIM_OK;
 }
 
 // deferred pingMembers inserts of the phase's ADDED events (Ctx points at that phase's counters)
-static void run_ins_pipeline(swim_engine* e, const Ctx& c) {
-  k_ins_prep<<<1, 1024, 0, e->stream>>>(c, e->b);
-  k_ins_apply<<<512, 256, 0, e->stream>>>(c, e->b);
+static void run_ins_pipeline(swim_engine* e, Shard& sd, const Ctx& c) {
+  k_ins_prep<<<1, 1024, 0, e->stream>>>(c, sd.b);
+  k_ins_apply<<<512, 256, 0, e->stream>>>(c, sd.b);
 }
 
-// One tick = 15 kernels (21 on gossip ticks) on one stream; no host synchronisation.
-static void run_tick(swim_engine* e) {
+static Ctx sync_ctx(Shard& sd) {  // list inserts of the SYNC phase use the second set of counters
+  Ctx cd = sd.c;
+  cd.ins_total = &sd.k->ins_total2;
+  cd.ins_list_cnt = &sd.k->ins_list_cnt2;
+  return cd;
+}
+
+static void bind_rx(Shard& sd) {
+  sd.b.rx_msgs = sd.rx_msgs;
+  sd.b.rx_reqs = sd.rx_reqs;
+  sd.b.rx_rows = sd.rx_rows;
+  sd.b.rx_stops = sd.rx_stops;
+}
+
+// One tick: ~15 kernels per shard (21 on gossip ticks); a sharded engine adds three exchanges.
+static int32_t run_tick(swim_engine* e) {
   e->T += 1;
   e->host_ticks += 1;
-  Ctx& c = e->c;
-  Bufs& b = e->b;
-  c.T = e->T;
   hipStream_t s = e->stream;
-  const uint32_t n = e->n;
-  const uint32_t gm = grid_for(n, 256);
-  if (e->joins_pending) {
-    k_start_joins<<<gm, 256, 0, s>>>(c);
-    e->joins_pending = false;
+  const bool multi = e->world > 1;
+  const bool gossip_tick = e->g_residue[e->T % e->G] != 0;
+  for (Shard& sd : e->sh) {
+    sd.c.T = e->T;
+    sd.n_rx_msgs = sd.n_rx_reqs = sd.n_rx_stops = 0;
   }
-  // ---- A: suspicion timeouts
-  const uint32_t bucket = (uint32_t)(e->T & c.wheel_mask);
-  k_timers<<<256, 256, 0, s>>>(c, bucket);
-  k_compact<<<256, 256, 0, s>>>(c, e->k, bucket);
-  // ---- B: failure detector
-  k_fd<<<gm, 256, 0, s>>>(c);
-  // ---- C: gossip round
-  if (e->g_residue[e->T % e->G]) {
-    if (c.seg_threshold < KIV) k_gossip_seg<<<gm, 256, 0, s>>>(c);
-    k_gossip_emit<<<gm, 256, 0, s>>>(c, b);
-    k_alloc<<<64, 256, 0, s>>>(b.msg_recv, &e->k->msg_recv_cnt, b.msg_cnt, b.msg_start, &e->k->msg_cursor);
-    k_scatter_msgs<<<512, 256, 0, s>>>(b);
-    k_gossip_deliver<<<gm, 256, 0, s>>>(c, b);
-    run_ins_pipeline(e, c);
+  if (!e->joins.empty()) {
+    for (Shard& sd : e->sh)
+      for (uint32_t m : e->joins) hipMemsetAsync(sd.c.up + m, 1, 1, s);
+    for (Shard& sd : e->sh) k_start_joins<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sd.c);
+    e->joins.clear();
   }
-  // ---- D: SYNC / SYNC_ACK (list inserts use the second set of counters)
-  Ctx cd = c;
-  cd.ins_total = &e->k->ins_total2;
-  cd.ins_list_cnt = &e->k->ins_list_cnt2;
-  k_sync_collect<<<gm, 256, 0, s>>>(cd, b);
+  for (Shard& sd : e->sh) {
+    Ctx& c = sd.c;
+    const uint32_t gm = grid_for(c.nl, 256);
+    // ---- A: suspicion timeouts
+    const uint32_t bucket = (uint32_t)(e->T & c.wheel_mask);
+    k_timers<<<256, 256, 0, s>>>(c, bucket);
+    k_compact<<<256, 256, 0, s>>>(c, sd.k, bucket);
+    // ---- B: failure detector
+    k_fd<<<gm, 256, 0, s>>>(c);
+    // ---- C: gossip round (emit)
+    if (gossip_tick) {
+      if (c.seg_threshold < KIV) k_gossip_seg<<<gm, 256, 0, s>>>(c);
+      k_gossip_emit<<<gm, 256, 0, s>>>(c, sd.b);
+    }
+  }
+  if (gossip_tick) {
+    if (multi)
+      if (int32_t rc = exchange_msgs(e)) return rc;
+    for (Shard& sd : e->sh) {
+      Ctx& c = sd.c;
+      bind_rx(sd);
+      if (sd.n_rx_msgs) k_recv_msgs<<<std::min<uint32_t>(grid_for(sd.n_rx_msgs, 256), 1024), 256, 0, s>>>(c, sd.b, sd.n_rx_msgs);
+      k_alloc<<<64, 256, 0, s>>>(sd.b.msg_recv, &sd.k->msg_recv_cnt, sd.b.msg_cnt, sd.b.msg_start, &sd.k->msg_cursor, c.lo);
+      k_scatter_msgs<<<512, 256, 0, s>>>(sd.b, c.lo);
+      k_gossip_deliver<<<grid_for(c.nl, 256), 256, 0, s>>>(c, sd.b);
+      run_ins_pipeline(e, sd, c);
+    }
+  }
+  // ---- D: SYNC / SYNC_ACK
+  for (Shard& sd : e->sh) k_sync_collect<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sync_ctx(sd), sd.b);
   for (int d2 = 0; d2 < 2; ++d2) {
-    k_sync_prep<<<1, 1024, 0, s>>>(cd, b, d2);
-    launch_classify(e, d2);
-    k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(cd, b, d2);
+    if (multi)
+      if (int32_t rc = exchange_sync(e, 1 + d2)) return rc;
+    for (Shard& sd : e->sh) {
+      const Ctx cd = sync_ctx(sd);
+      bind_rx(sd);
+      if (sd.n_rx_reqs) k_recv_sync<<<std::min<uint32_t>(grid_for(sd.n_rx_reqs, 256), 256), 256, 0, s>>>(cd, sd.b, d2, sd.n_rx_reqs);
+      k_sync_prep<<<1, 1024, 0, s>>>(cd, sd.b, d2);
+      launch_classify(e, sd, d2);
+      k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(cd, sd.b, d2);
+    }
   }
-  run_ins_pipeline(e, cd);
-  // ---- end of tick (also zeroes the per-tick counters)
-  k_end_tick<<<gm, 256, 0, s>>>(c, e->k);
+  for (Shard& sd : e->sh) {
+    run_ins_pipeline(e, sd, sync_ctx(sd));
+    // ---- end of tick (also zeroes the per-tick counters and applies other shards' stops)
+    const uint32_t ge = grid_for(std::max<uint32_t>(std::max<uint32_t>(sd.c.nl, sd.n_rx_stops), 64), 256);
+    k_end_tick<<<ge, 256, 0, s>>>(sd.c, sd.k, sd.x, sd.rx_stops, sd.n_rx_stops);
+  }
+  return SWIM_OK;
 }
 
 static int32_t upload_links(swim_engine* e) {
   auto& L = e->links_h;
   std::sort(L.begin(), L.end(), [](const LinkDev& x, const LinkDev& y) { return x.a < y.a || (x.a == y.a && x.b < y.b); });
-  if (L.size() > e->links_dev_cap) {
-    if (hipSetDevice(e->device) != hipSuccess) return SWIM_EDEVICE;
-    uint32_t cap = next_pow2((uint32_t)L.size());
-    LinkDev* p = nullptr;
-    if (!e->alloc(&p, cap)) return SWIM_ENOMEM;
-    e->c.links = p;
-    e->links_dev_cap = cap;
+  for (Shard& sd : e->sh) {
+    if (L.size() > sd.links_dev_cap) {
+      uint32_t cap = next_pow2((uint32_t)L.size());
+      LinkDev* p = nullptr;
+      if (!sd.alloc(&p, cap)) return SWIM_ENOMEM;
+      sd.c.links = p;
+      sd.links_dev_cap = cap;
+    }
+    if (!L.empty() && hipMemcpy(sd.c.links, L.data(), sizeof(LinkDev) * L.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return SWIM_EDEVICE;
+    sd.c.n_links = (uint32_t)L.size();
   }
-  if (!L.empty() && hipMemcpy(e->c.links, L.data(), sizeof(LinkDev) * L.size(), hipMemcpyHostToDevice) != hipSuccess)
-    return SWIM_EDEVICE;
-  e->c.n_links = (uint32_t)L.size();
   return SWIM_OK;
 }
 
@@ -230,22 +511,34 @@ static void prune_links(swim_engine* e) {
   L.erase(std::remove_if(L.begin(), L.end(), [](const LinkDev& x) { return x.out_loss < 0 && x.in_pass < 0; }), L.end());
 }
 
-template <typename F>
-static int32_t member_field_write(swim_engine* e, uint32_t m, size_t offset, const F& val) {
+static int32_t read_member_dev(swim_engine* e, Shard& sd, uint32_t m, MemberDev* out) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  char* base = reinterpret_cast<char*>(e->c.mem + m) + offset;
-  return hipMemcpy(base, &val, sizeof(F), hipMemcpyHostToDevice) == hipSuccess ? SWIM_OK : SWIM_EDEVICE;
+  return hipMemcpy(out, sd.c.mem + (m - sd.c.lo), sizeof(MemberDev), hipMemcpyDeviceToHost) == hipSuccess ? SWIM_OK
+                                                                                                          : SWIM_EDEVICE;
 }
-
-static int32_t read_member_dev(swim_engine* e, uint32_t m, MemberDev* out) {
+static int32_t write_member_dev(Shard& sd, uint32_t m, const MemberDev& in) {
+  return hipMemcpy(sd.c.mem + (m - sd.c.lo), &in, sizeof(MemberDev), hipMemcpyHostToDevice) == hipSuccess ? SWIM_OK
+                                                                                                         : SWIM_EDEVICE;
+}
+static int32_t read_up(swim_engine* e, uint32_t m, uint8_t* up) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  return hipMemcpy(out, e->c.mem + m, sizeof(MemberDev), hipMemcpyDeviceToHost) == hipSuccess ? SWIM_OK : SWIM_EDEVICE;
+  return hipMemcpy(up, e->sh[0].c.up + m, 1, hipMemcpyDeviceToHost) == hipSuccess ? SWIM_OK : SWIM_EDEVICE;
+}
+// replicated byte array write on every local shard
+static int32_t set_replicated(swim_engine* e, size_t field_off, uint32_t m, uint8_t v, bool all) {
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  for (Shard& sd : e->sh) {
+    uint8_t* base = *reinterpret_cast<uint8_t**>(reinterpret_cast<char*>(&sd.c) + field_off);
+    hipError_t r = all ? hipMemset(base, v, e->n) : hipMemcpy(base + m, &v, 1, hipMemcpyHostToDevice);
+    if (r != hipSuccess) return SWIM_EDEVICE;
+  }
+  return SWIM_OK;
 }
 
 // leaveCluster (MembershipProtocolImpl.java:233-242) on the device: LEAVING inc+1, spread gossip
 __global__ void k_leave(Ctx c, uint32_t v, int32_t stop_after) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  MemberDev& m = c.mem[v];
+  MemberDev& m = mem(c, v);
   uint64_t* cp = row(c, v) + v;
   int32_t inc = c_inc(*cp) + 1;
   *cp = c_with_record(*cp, SWIM_LEAVING, inc);
@@ -255,6 +548,177 @@ __global__ void k_leave(Ctx c, uint32_t v, int32_t stop_after) {
     m.leave_gossiper = v;
     m.leave_seq = m.g_counter - 1;
   }
+}
+
+static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n_initial, uint64_t seed) {
+  const swim_config& cf = e->cfg;
+  Ctx& c = sd.c;
+  Bufs& b = sd.b;
+  const uint32_t n = e->n;
+  c.n = n;
+  c.sz = e->sz;
+  c.rank = shard;
+  c.world = (uint32_t)e->world;
+  c.lo = std::min(n, shard * e->sz);
+  c.nl = std::min(n, c.lo + e->sz) - c.lo;
+  const uint32_t nl = c.nl;
+  c.gcap = cf.gossip_capacity ? cf.gossip_capacity : 1024;
+  c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 1024);
+  c.P = e->P;
+  c.to_ticks = (uint32_t)cf.ping_timeout / e->tick_ms;
+  c.relay_ticks = e->P - c.to_ticks;
+  c.G = e->G;
+  c.S = e->S;
+  c.sync_to_ticks = (uint32_t)cf.sync_timeout / e->tick_ms;
+  c.tick_ms = e->tick_ms;
+  c.ping_interval = cf.ping_interval;
+  c.suspicion_mult = cf.suspicion_mult;
+  c.repeat_mult = cf.gossip_repeat_mult;
+  c.fanout = cf.gossip_fanout;
+  c.ping_req_members = cf.ping_req_members;
+  c.seg_threshold = cf.gossip_segmentation_threshold;
+  c.record_fd = cf.record_fd_events;
+  c.key0 = (uint32_t)seed;
+  c.key1 = (uint32_t)(seed >> 32);
+  const uint64_t max_timer = (uint64_t)cf.suspicion_mult * (uint64_t)host_ceil_log2((int32_t)n) * e->P;
+  c.wheel_mask = next_pow2((uint32_t)max_timer + 2) - 1;
+  c.wheel_cap = std::max<uint32_t>(4096, 2 * std::max(nl, 1u));
+  c.ev_cap = cf.event_capacity ? cf.event_capacity : (1u << 22);
+  c.ins_cap = std::max<uint32_t>(1u << 16, 4 * nl);
+  b.msg_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 256ull * nl));
+  b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
+  b.snap_cap = 64;
+  b.chunks = (n + SYNC_CHUNK - 1) / SYNC_CHUNK;
+  b.pool_cap = std::max<uint32_t>(1u << 22, 16 * n);
+  const bool multi = e->world > 1;
+  b.tx_msg_cap = multi ? b.msg_cap : 0;
+  b.tx_req_cap = multi ? b.req_cap : 0;
+  b.tx_stop_cap = multi ? kStopCap : 0;
+
+  const size_t nn = (size_t)nl * n;
+  bool ok = sd.alloc(&c.cells, nn) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
+            sd.alloc(&c.remote, nn) && sd.alloc(&c.slab, (size_t)nl * c.gcap) && sd.alloc(&c.coll, (size_t)nl * c.hcap) &&
+            sd.alloc(&c.fd_sync, (size_t)nl * FD_SYNC_MAX) &&
+            sd.alloc(&c.wheel, (size_t)(c.wheel_mask + 1) * c.wheel_cap) && sd.alloc(&c.wheel_cnt, c.wheel_mask + 1) &&
+            sd.alloc(&c.ev, c.ev_cap) && sd.alloc(&c.ev_cnt, 1) && sd.alloc(&c.default_loss, n) &&
+            sd.alloc(&c.default_inbound, n) && sd.alloc(&c.group, n) && sd.alloc(&c.links, 1) &&
+            sd.alloc(&c.is_seed, n) && sd.alloc(&c.seeds, n) && sd.alloc(&c.ins, c.ins_cap) && sd.alloc(&c.ins_cnt, nl) &&
+            sd.alloc(&c.ins_list, nl) && sd.alloc(&c.compact_flag, nl) && sd.alloc(&c.compact_list, nl) &&
+            sd.alloc(&c.stats, (size_t)ST_COUNT * ST_REPL) && sd.alloc(&c.err, 1) && sd.alloc(&sd.k, 1) &&
+            sd.alloc(&sd.x, 1) && sd.alloc(&b.msgs, b.msg_cap) && sd.alloc(&b.msgs_out, b.msg_cap) &&
+            sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.msg_start, nl) && sd.alloc(&b.msg_recv, nl) &&
+            sd.alloc(&b.reqs, b.req_cap) && sd.alloc(&b.reqs_out, b.req_cap) && sd.alloc(&b.req_cnt, nl) &&
+            sd.alloc(&b.req_start, nl) && sd.alloc(&b.req_recv, nl) && sd.alloc(&b.acks, b.req_cap) &&
+            sd.alloc(&b.acks_out, b.req_cap) && sd.alloc(&b.ack_cnt, nl) && sd.alloc(&b.ack_start, nl) &&
+            sd.alloc(&b.ack_recv, nl) && sd.alloc(&b.ins_out, c.ins_cap) && sd.alloc(&b.ins_start, nl) &&
+            sd.alloc(&b.snap, (size_t)b.snap_cap * n) && sd.alloc(&b.snap_idx, nl) && sd.alloc(&b.snap_list, b.snap_cap) &&
+            sd.alloc(&b.snap_cnt, 1) && sd.alloc(&b.item_chunk, (size_t)b.req_cap * b.chunks) &&
+            sd.alloc(&b.item_total, b.req_cap) && sd.alloc(&b.pool, b.pool_cap) &&
+            sd.alloc(&b.pend, (size_t)kApplyGrid * n);
+  if (ok && multi)
+    ok = sd.alloc(&b.tx_msgs, (size_t)e->world * b.tx_msg_cap) && sd.alloc(&b.tx_reqs, (size_t)e->world * b.tx_req_cap) &&
+         sd.alloc(&b.tx_acks, (size_t)e->world * b.tx_req_cap) && sd.alloc(&b.tx_stops, b.tx_stop_cap);
+  if (!ok) return SWIM_ENOMEM;
+  sd.links_dev_cap = 1;
+  c.ins_total = &sd.k->ins_total;
+  c.ins_list_cnt = &sd.k->ins_list_cnt;
+  c.compact_cnt = &sd.k->compact_cnt;
+  b.k = sd.k;
+  b.x = sd.x;
+  hipStream_t s = e->stream;
+  hipMemsetAsync(c.coll, 0, sizeof(CollDev) * (size_t)nl * c.hcap, s);
+  hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1), s);
+  hipMemsetAsync(c.ev_cnt, 0, 4, s);
+  hipMemsetAsync(c.up, 0, n, s);
+  hipMemsetAsync(c.up, 1, n_initial, s);
+  hipMemsetAsync(c.default_loss, 0, n, s);
+  hipMemsetAsync(c.default_inbound, 1, n, s);
+  hipMemsetAsync(c.group, 0, 2 * (size_t)n, s);
+  hipMemsetAsync(c.is_seed, 0, n, s);
+  hipMemsetAsync(c.ins_cnt, 0, 4 * (size_t)nl, s);
+  hipMemsetAsync(c.compact_flag, 0, 4 * (size_t)nl, s);
+  hipMemsetAsync(c.stats, 0, 8 * (size_t)ST_COUNT * ST_REPL, s);
+  hipMemsetAsync(c.err, 0, 4, s);
+  hipMemsetAsync(sd.k, 0, sizeof(Counters), s);
+  hipMemsetAsync(sd.x, 0, sizeof(Xc), s);
+  hipMemsetAsync(b.msg_cnt, 0, 4 * (size_t)nl, s);
+  hipMemsetAsync(b.req_cnt, 0, 4 * (size_t)nl, s);
+  hipMemsetAsync(b.ack_cnt, 0, 4 * (size_t)nl, s);
+  hipMemsetAsync(b.snap_idx, 0xff, 4 * (size_t)nl, s);
+  hipMemsetAsync(b.snap_cnt, 0, 4, s);
+  c.T = 0;
+  if (nl) {
+    k_init_rows<<<std::min<uint32_t>(nl, 65535), 256, 0, s>>>(c, n_initial);
+    k_init_members<<<grid_for(nl, 64), 64, 0, s>>>(c, n_initial, cf.sync_stagger);
+  }
+  return SWIM_OK;
+}
+
+static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t n_initial, uint64_t seed, int32_t rank,
+                             int32_t world, bool rccl, const uint8_t* comm_id, swim_engine** out) {
+  if (!cfg || !out || capacity < 2 || n_initial > capacity || capacity > (1u << 24)) return SWIM_EINVAL;
+  const swim_config& cf = *cfg;
+  if (cf.ping_interval <= 0 || cf.ping_timeout <= 0 || cf.ping_timeout >= cf.ping_interval || cf.gossip_interval <= 0 ||
+      cf.sync_interval <= 0 || cf.sync_timeout <= 0 || cf.metadata_timeout <= 0 || cf.suspicion_mult <= 0 ||
+      cf.gossip_fanout <= 0 || cf.gossip_fanout > 16 || cf.ping_req_members > 16 || cf.gossip_repeat_mult <= 0)
+    return SWIM_EINVAL;
+  if (world < 1 || world > MAXW || rank < 0 || rank >= world || (uint32_t)world > capacity) return SWIM_EINVAL;
+  uint32_t tick = (uint32_t)cf.tick_ms;
+  if (tick == 0) {
+    tick = gcd_u((uint32_t)cf.ping_interval, (uint32_t)cf.ping_timeout);
+    tick = gcd_u(tick, (uint32_t)cf.gossip_interval);
+    tick = gcd_u(tick, (uint32_t)cf.sync_interval);
+    tick = gcd_u(tick, (uint32_t)cf.sync_timeout);
+  }
+  if (cf.ping_interval % tick || cf.ping_timeout % tick || cf.gossip_interval % tick || cf.sync_interval % tick ||
+      cf.sync_timeout % tick)
+    return SWIM_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SWIM_EDEVICE;
+  if (cf.device < 0 || cf.device >= ndev) return SWIM_EINVAL;
+  if (hipSetDevice(cf.device) != hipSuccess) return SWIM_EDEVICE;
+
+  swim_engine* e = new (std::nothrow) swim_engine();
+  if (!e) return SWIM_ENOMEM;
+  e->cfg = cf;
+  e->device = cf.device;
+  e->n = capacity;
+  e->tick_ms = tick;
+  e->P = (uint32_t)cf.ping_interval / tick;
+  e->G = (uint32_t)cf.gossip_interval / tick;
+  e->S = (uint32_t)cf.sync_interval / tick;
+  e->rank = rank;
+  e->world = world;
+  e->rccl = rccl;
+  e->sz = (capacity + (uint32_t)world - 1) / (uint32_t)world;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return SWIM_EDEVICE; }
+  e->sh.resize(rccl ? 1 : (size_t)world);
+  for (size_t i = 0; i < e->sh.size(); ++i) {
+    int32_t rc = alloc_shard(e, e->sh[i], rccl ? (uint32_t)rank : (uint32_t)i, n_initial, seed);
+    if (rc != SWIM_OK) { delete e; return rc; }
+  }
+  if (hipMalloc((void**)&e->kat_coll, sizeof(CollDev)) != hipSuccess) { delete e; return SWIM_ENOMEM; }
+  if (world > 1) {
+    if (hipMalloc((void**)&e->d_cnt, sizeof(uint32_t) * 2 * MAXW) != hipSuccess ||
+        hipHostMalloc((void**)&e->h_cnt, sizeof(uint32_t) * 2 * MAXW + sizeof(Xc)) != hipSuccess) {
+      delete e;
+      return SWIM_ENOMEM;
+    }
+  }
+  if (hipStreamSynchronize(e->stream) != hipSuccess || hip_status() != SWIM_OK) { delete e; return SWIM_EDEVICE; }
+  if (rccl) {
+    ncclUniqueId id;
+    std::memcpy(&id, comm_id, sizeof(id));
+    if (nccl_ok(ncclCommInitRank(&e->comm, world, id, rank)) != SWIM_OK) { delete e; return SWIM_EDEVICE; }
+  }
+  e->g_residue.assign(e->G, 0);
+  e->g_residue[0] = 1;
+  e->is_seed_h.assign(capacity, 0);
+  e->joined_h.assign(capacity, 0);
+  std::fill(e->joined_h.begin(), e->joined_h.begin() + n_initial, 1);
+  e->join_pending_h.assign(capacity, 0);
+  *out = e;
+  return SWIM_OK;
 }
 
 extern "C" {
@@ -309,123 +773,32 @@ int64_t swim_suspicion_timeout(int32_t suspicion_mult, int32_t cluster_size, int
 }
 
 int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initial, uint64_t seed, swim_engine** out) {
-  if (!cfg || !out || capacity < 2 || n_initial > capacity || capacity > (1u << 24)) return SWIM_EINVAL;
-  const swim_config& cf = *cfg;
-  if (cf.ping_interval <= 0 || cf.ping_timeout <= 0 || cf.ping_timeout >= cf.ping_interval || cf.gossip_interval <= 0 ||
-      cf.sync_interval <= 0 || cf.sync_timeout <= 0 || cf.metadata_timeout <= 0 || cf.suspicion_mult <= 0 ||
-      cf.gossip_fanout <= 0 || cf.gossip_fanout > 16 || cf.ping_req_members > 16 || cf.gossip_repeat_mult <= 0)
-    return SWIM_EINVAL;
-  uint32_t tick = (uint32_t)cf.tick_ms;
-  if (tick == 0) {
-    tick = gcd_u((uint32_t)cf.ping_interval, (uint32_t)cf.ping_timeout);
-    tick = gcd_u(tick, (uint32_t)cf.gossip_interval);
-    tick = gcd_u(tick, (uint32_t)cf.sync_interval);
-    tick = gcd_u(tick, (uint32_t)cf.sync_timeout);
-  }
-  if (cf.ping_interval % tick || cf.ping_timeout % tick || cf.gossip_interval % tick || cf.sync_interval % tick ||
-      cf.sync_timeout % tick)
-    return SWIM_EINVAL;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SWIM_EDEVICE;
-  if (cf.device < 0 || cf.device >= ndev) return SWIM_EINVAL;
-  if (hipSetDevice(cf.device) != hipSuccess) return SWIM_EDEVICE;
+  if (!cfg) return SWIM_EINVAL;
+  const int32_t shards = cfg->local_shards > 1 ? cfg->local_shards : 1;
+  return create_engine(cfg, capacity, n_initial, seed, 0, shards, false, nullptr, out);
+}
 
-  swim_engine* e = new (std::nothrow) swim_engine();
-  if (!e) return SWIM_ENOMEM;
-  e->cfg = cf;
-  e->device = cf.device;
-  e->n = capacity;
-  e->tick_ms = tick;
-  e->P = (uint32_t)cf.ping_interval / tick;
-  e->G = (uint32_t)cf.gossip_interval / tick;
-  e->S = (uint32_t)cf.sync_interval / tick;
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return SWIM_EDEVICE; }
+int32_t swim_comm_unique_id(uint8_t* out) {
+  if (!out) return SWIM_EINVAL;
+  ncclUniqueId id;
+  if (nccl_ok(ncclGetUniqueId(&id)) != SWIM_OK) return SWIM_EDEVICE;
+  std::memcpy(out, &id, sizeof(id));
+  return SWIM_OK;
+}
 
-  Ctx& c = e->c;
-  Bufs& b = e->b;
-  const uint32_t n = capacity;
-  c.n = n;
-  c.gcap = cf.gossip_capacity ? cf.gossip_capacity : 1024;
-  c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 1024);
-  c.P = e->P;
-  c.to_ticks = (uint32_t)cf.ping_timeout / tick;
-  c.relay_ticks = e->P - c.to_ticks;
-  c.G = e->G;
-  c.S = e->S;
-  c.sync_to_ticks = (uint32_t)cf.sync_timeout / tick;
-  c.tick_ms = tick;
-  c.ping_interval = cf.ping_interval;
-  c.suspicion_mult = cf.suspicion_mult;
-  c.repeat_mult = cf.gossip_repeat_mult;
-  c.fanout = cf.gossip_fanout;
-  c.ping_req_members = cf.ping_req_members;
-  c.seg_threshold = cf.gossip_segmentation_threshold;
-  c.record_fd = cf.record_fd_events;
-  c.key0 = (uint32_t)seed;
-  c.key1 = (uint32_t)(seed >> 32);
-  const uint64_t max_timer = (uint64_t)cf.suspicion_mult * (uint64_t)host_ceil_log2((int32_t)n) * e->P;
-  c.wheel_mask = next_pow2((uint32_t)max_timer + 2) - 1;
-  c.wheel_cap = std::max<uint32_t>(4096, 2 * n);
-  c.ev_cap = cf.event_capacity ? cf.event_capacity : (1u << 22);
-  c.ins_cap = std::max<uint32_t>(1u << 16, 4 * n);
-  b.msg_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 256ull * n));
-  b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
-  b.snap_cap = 64;
-  b.chunks = (n + SYNC_CHUNK - 1) / SYNC_CHUNK;
-  b.pool_cap = std::max<uint32_t>(1u << 22, 16 * n);
+int32_t swim_create_shard(const swim_config* cfg, uint32_t capacity, uint32_t n_initial, uint64_t seed, int32_t rank,
+                          int32_t world, const uint8_t* comm_id, swim_engine** out) {
+  if (!cfg || (world > 1 && !comm_id)) return SWIM_EINVAL;
+  if (world <= 1) return create_engine(cfg, capacity, n_initial, seed, 0, 1, false, nullptr, out);
+  return create_engine(cfg, capacity, n_initial, seed, rank, world, true, comm_id, out);
+}
 
-  const size_t nn = (size_t)n * n;
-  bool ok = e->alloc(&c.cells, nn) && e->alloc(&c.mem, n) && e->alloc(&c.ping, nn) && e->alloc(&c.remote, nn) &&
-            e->alloc(&c.slab, (size_t)n * c.gcap) && e->alloc(&c.coll, (size_t)n * c.hcap) &&
-            e->alloc(&c.fd_sync, (size_t)n * FD_SYNC_MAX) && e->alloc(&c.wheel, (size_t)(c.wheel_mask + 1) * c.wheel_cap) &&
-            e->alloc(&c.wheel_cnt, c.wheel_mask + 1) && e->alloc(&c.ev, c.ev_cap) && e->alloc(&c.ev_cnt, 1) &&
-            e->alloc(&c.default_loss, n) && e->alloc(&c.default_inbound, n) && e->alloc(&c.group, n) &&
-            e->alloc(&c.links, 1) && e->alloc(&c.is_seed, n) && e->alloc(&c.seeds, n) && e->alloc(&c.ins, c.ins_cap) &&
-            e->alloc(&c.ins_cnt, n) && e->alloc(&c.ins_list, n) && e->alloc(&c.compact_flag, n) &&
-            e->alloc(&c.compact_list, n) && e->alloc(&c.stats, (size_t)ST_COUNT * ST_REPL) && e->alloc(&c.err, 1) &&
-            e->alloc(&e->k, 1) && e->alloc(&b.msgs, b.msg_cap) && e->alloc(&b.msgs_out, b.msg_cap) &&
-            e->alloc(&b.msg_cnt, n) && e->alloc(&b.msg_start, n) && e->alloc(&b.msg_recv, n) &&
-            e->alloc(&b.reqs, b.req_cap) && e->alloc(&b.reqs_out, b.req_cap) && e->alloc(&b.req_cnt, n) &&
-            e->alloc(&b.req_start, n) && e->alloc(&b.req_recv, n) && e->alloc(&b.acks, b.req_cap) &&
-            e->alloc(&b.acks_out, b.req_cap) && e->alloc(&b.ack_cnt, n) && e->alloc(&b.ack_start, n) &&
-            e->alloc(&b.ack_recv, n) && e->alloc(&b.ins_out, c.ins_cap) && e->alloc(&b.ins_start, n) &&
-            e->alloc(&b.snap, (size_t)b.snap_cap * n) && e->alloc(&b.snap_idx, n) && e->alloc(&b.snap_list, b.snap_cap) &&
-            e->alloc(&b.snap_cnt, 1) && e->alloc(&b.item_chunk, (size_t)b.req_cap * b.chunks) &&
-            e->alloc(&b.item_total, b.req_cap) &&
-            e->alloc(&b.pool, b.pool_cap) && e->alloc(&b.pend, (size_t)kApplyGrid * n) && e->alloc(&e->kat_coll, 1);
-  if (!ok) { delete e; return SWIM_ENOMEM; }
-  c.links = e->c.links;
-  e->links_dev_cap = 1;
-  c.ins_total = &e->k->ins_total;
-  c.ins_list_cnt = &e->k->ins_list_cnt;
-  c.compact_cnt = &e->k->compact_cnt;
-  b.k = e->k;
-  hipStream_t s = e->stream;
-  hipMemsetAsync(c.coll, 0, sizeof(CollDev) * (size_t)n * c.hcap, s);
-  hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1), s);
-  hipMemsetAsync(c.ev_cnt, 0, 4, s);
-  hipMemsetAsync(c.default_loss, 0, n, s);
-  hipMemsetAsync(c.default_inbound, 1, n, s);
-  hipMemsetAsync(c.group, 0, 2 * (size_t)n, s);
-  hipMemsetAsync(c.is_seed, 0, n, s);
-  hipMemsetAsync(c.ins_cnt, 0, 4 * (size_t)n, s);
-  hipMemsetAsync(c.compact_flag, 0, 4 * (size_t)n, s);
-  hipMemsetAsync(c.stats, 0, 8 * (size_t)ST_COUNT * ST_REPL, s);
-  hipMemsetAsync(c.err, 0, 4, s);
-  hipMemsetAsync(e->k, 0, sizeof(Counters), s);
-  hipMemsetAsync(b.msg_cnt, 0, 4 * (size_t)n, s);
-  hipMemsetAsync(b.req_cnt, 0, 4 * (size_t)n, s);
-  hipMemsetAsync(b.ack_cnt, 0, 4 * (size_t)n, s);
-  hipMemsetAsync(b.snap_idx, 0xff, 4 * (size_t)n, s);
-  hipMemsetAsync(b.snap_cnt, 0, 4, s);
-  c.T = 0;
-  k_init_rows<<<std::min<uint32_t>(n, 65535), 256, 0, s>>>(c, n_initial);
-  k_init_members<<<grid_for(n, 64), 64, 0, s>>>(c, n_initial, cf.sync_stagger);
-  if (hipStreamSynchronize(s) != hipSuccess || hip_status() != SWIM_OK) { delete e; return SWIM_EDEVICE; }
-  e->g_residue.assign(e->G, 0);
-  e->g_residue[0] = 1;
-  e->is_seed_h.assign(n, 0);
-  *out = e;
+int32_t swim_shard_info(const swim_engine* e, int32_t* rank, int32_t* world, uint32_t* lo, uint32_t* count) {
+  if (!e) return SWIM_EINVAL;
+  if (rank) *rank = e->rank;
+  if (world) *world = e->world;
+  if (lo) *lo = e->rccl ? e->sh[0].c.lo : 0;
+  if (count) *count = e->rccl ? e->sh[0].c.nl : e->n;
   return SWIM_OK;
 }
 
@@ -437,16 +810,25 @@ int32_t swim_destroy(swim_engine* e) {
 int32_t swim_step_ticks(swim_engine* e, uint32_t ticks) {
   if (!e) return SWIM_EINVAL;
   if (hipSetDevice(e->device) != hipSuccess) return SWIM_EDEVICE;
-  int32_t rc = SWIM_OK;
   for (uint32_t i = 0; i < ticks; ++i) {
-    run_tick(e);
+    if (int32_t rc = run_tick(e)) return rc;
     if ((i + 1) % kDrainEvery == 0) {
       int32_t r = sync_and_collect(e);
       if (r == SWIM_EDEVICE) return r;
     }
   }
   if (hip_status() != SWIM_OK) return SWIM_EDEVICE;
-  rc = sync_and_collect(e);
+  int32_t rc = sync_and_collect(e);
+  if (rc == SWIM_EDEVICE) return rc;
+  if (e->rccl) {  // every rank reports a capacity error if any rank saw one
+    uint32_t mine = e->err_seen ? 1u : 0u, any = 0;
+    hipMemcpy(e->d_cnt, &mine, 4, hipMemcpyHostToDevice);
+    if (nccl_ok(ncclAllReduce(e->d_cnt, e->d_cnt + 1, 1, ncclUint32, ncclMax, e->comm, e->stream)) != SWIM_OK)
+      return SWIM_EDEVICE;
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+    hipMemcpy(&any, e->d_cnt + 1, 4, hipMemcpyDeviceToHost);
+    if (any) rc = SWIM_ECAPACITY;
+  }
   return rc;
 }
 
@@ -474,52 +856,64 @@ int32_t swim_set_seeds(swim_engine* e, const uint32_t* seeds, uint32_t n_seeds) 
   std::fill(e->is_seed_h.begin(), e->is_seed_h.end(), 0);
   for (uint32_t x : s) e->is_seed_h[x] = 1;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  if (!s.empty() && hipMemcpy(e->c.seeds, s.data(), 4 * s.size(), hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
-  if (hipMemcpy(e->c.is_seed, e->is_seed_h.data(), e->n, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
-  e->c.n_seeds = (uint32_t)s.size();
+  for (Shard& sd : e->sh) {
+    if (!s.empty() && hipMemcpy(sd.c.seeds, s.data(), 4 * s.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return SWIM_EDEVICE;
+    if (hipMemcpy(sd.c.is_seed, e->is_seed_h.data(), e->n, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
+    sd.c.n_seeds = (uint32_t)s.size();
+  }
   return SWIM_OK;
 }
 
 int32_t swim_kill(swim_engine* e, uint32_t m) {
   if (!e || m >= e->n) return SWIM_EINVAL;
-  MemberDev md;
-  if (read_member_dev(e, m, &md) != SWIM_OK) return SWIM_EDEVICE;
-  if (!md.up) return SWIM_ESTATE;
-  md.up = 0;
-  md.leave_pending = 0;
-  return hipMemcpy(e->c.mem + m, &md, sizeof(MemberDev), hipMemcpyHostToDevice) == hipSuccess ? SWIM_OK : SWIM_EDEVICE;
+  uint8_t up = 0;
+  if (read_up(e, m, &up) != SWIM_OK) return SWIM_EDEVICE;
+  if (!up) return SWIM_ESTATE;
+  if (set_replicated(e, offsetof(Ctx, up), m, 0, false) != SWIM_OK) return SWIM_EDEVICE;
+  if (Shard* sd = e->owner_of(m)) {
+    MemberDev md;
+    if (read_member_dev(e, *sd, m, &md) != SWIM_OK) return SWIM_EDEVICE;
+    md.leave_pending = 0;
+    return write_member_dev(*sd, m, md);
+  }
+  return SWIM_OK;
 }
 
 int32_t swim_leave(swim_engine* e, uint32_t m, int32_t stop_after) {
   if (!e || m >= e->n) return SWIM_EINVAL;
-  MemberDev md;
-  if (read_member_dev(e, m, &md) != SWIM_OK) return SWIM_EDEVICE;
-  if (!md.up) return SWIM_ESTATE;
-  e->c.T = e->T;
-  k_leave<<<1, 64, 0, e->stream>>>(e->c, m, stop_after);
+  uint8_t up = 0;
+  if (read_up(e, m, &up) != SWIM_OK) return SWIM_EDEVICE;
+  if (!up) return SWIM_ESTATE;
+  Shard* sd = e->owner_of(m);
+  if (!sd) return SWIM_OK;  // RCCL: the owning rank runs it
+  sd->c.T = e->T;
+  k_leave<<<1, 64, 0, e->stream>>>(sd->c, m, stop_after);
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
   return hip_status();
 }
 
 int32_t swim_join(swim_engine* e, uint32_t m) {
   if (!e || m >= e->n) return SWIM_EINVAL;
-  MemberDev md;
-  if (read_member_dev(e, m, &md) != SWIM_OK) return SWIM_EDEVICE;
-  if (md.joined || md.up || md.join_pending) return SWIM_ESTATE;
-  md.join_pending = 1;
-  if (hipMemcpy(e->c.mem + m, &md, sizeof(MemberDev), hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
-  e->joins_pending = true;
+  uint8_t up = 0;
+  if (read_up(e, m, &up) != SWIM_OK) return SWIM_EDEVICE;
+  if (e->joined_h[m] || up || e->join_pending_h[m]) return SWIM_ESTATE;
+  if (Shard* sd = e->owner_of(m)) {
+    MemberDev md;
+    if (read_member_dev(e, *sd, m, &md) != SWIM_OK) return SWIM_EDEVICE;
+    md.join_pending = 1;
+    if (write_member_dev(*sd, m, md) != SWIM_OK) return SWIM_EDEVICE;
+  }
+  e->joined_h[m] = 1;
+  e->joins.push_back(m);
   e->g_residue[(e->T + 1) % e->G] = 1;  // the joiner's gossip timer phase
   return SWIM_OK;
 }
 
 int32_t swim_set_default_loss(swim_engine* e, uint32_t m, int32_t pct) {
   if (!e || pct < 0 || pct > 100) return SWIM_EINVAL;
-  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  if (m == 0xffffffffu) return hipMemset(e->c.default_loss, pct, e->n) == hipSuccess ? SWIM_OK : SWIM_EDEVICE;
-  if (m >= e->n) return SWIM_EINVAL;
-  uint8_t v = (uint8_t)pct;
-  return hipMemcpy(e->c.default_loss + m, &v, 1, hipMemcpyHostToDevice) == hipSuccess ? SWIM_OK : SWIM_EDEVICE;
+  if (m != 0xffffffffu && m >= e->n) return SWIM_EINVAL;
+  return set_replicated(e, offsetof(Ctx, default_loss), m, (uint8_t)pct, m == 0xffffffffu);
 }
 
 int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t pct) {
@@ -550,26 +944,27 @@ int32_t swim_set_link_inbound(swim_engine* e, uint32_t dst, uint32_t src, int32_
 
 int32_t swim_set_default_inbound(swim_engine* e, uint32_t m, int32_t pass) {
   if (!e) return SWIM_EINVAL;
-  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  if (m == 0xffffffffu) return hipMemset(e->c.default_inbound, pass ? 1 : 0, e->n) == hipSuccess ? SWIM_OK : SWIM_EDEVICE;
-  if (m >= e->n) return SWIM_EINVAL;
-  uint8_t v = pass ? 1 : 0;
-  return hipMemcpy(e->c.default_inbound + m, &v, 1, hipMemcpyHostToDevice) == hipSuccess ? SWIM_OK : SWIM_EDEVICE;
+  if (m != 0xffffffffu && m >= e->n) return SWIM_EINVAL;
+  return set_replicated(e, offsetof(Ctx, default_inbound), m, pass ? 1 : 0, m == 0xffffffffu);
 }
 
 int32_t swim_set_partition(swim_engine* e, const uint16_t* g) {
   if (!e) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  if (!g) { e->c.partition = 0; return SWIM_OK; }
-  if (hipMemcpy(e->c.group, g, 2 * (size_t)e->n, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
-  e->c.partition = 1;
+  for (Shard& sd : e->sh) {
+    if (!g) { sd.c.partition = 0; continue; }
+    if (hipMemcpy(sd.c.group, g, 2 * (size_t)e->n, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
+    sd.c.partition = 1;
+  }
   return SWIM_OK;
 }
 
 int32_t swim_read_view(swim_engine* e, uint32_t v, uint64_t* out) {
   if (!e || v >= e->n || !out) return SWIM_EINVAL;
+  Shard* sd = e->owner_of(v);
+  if (!sd) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  return hipMemcpy(out, e->c.cells + (size_t)v * e->n, 8 * (size_t)e->n, hipMemcpyDeviceToHost) == hipSuccess
+  return hipMemcpy(out, sd->c.cells + (size_t)(v - sd->c.lo) * e->n, 8 * (size_t)e->n, hipMemcpyDeviceToHost) == hipSuccess
              ? SWIM_OK : SWIM_EDEVICE;
 }
 
@@ -616,10 +1011,14 @@ int32_t swim_get_stats(swim_engine* e, swim_stats* out) {
 
 int32_t swim_read_member(swim_engine* e, uint32_t v, swim_member_state* o) {
   if (!e || v >= e->n || !o) return SWIM_EINVAL;
+  Shard* sd = e->owner_of(v);
+  if (!sd) return SWIM_EINVAL;
   MemberDev m;
-  if (read_member_dev(e, v, &m) != SWIM_OK) return SWIM_EDEVICE;
+  if (read_member_dev(e, *sd, v, &m) != SWIM_OK) return SWIM_EDEVICE;
+  uint8_t up = 0;
+  if (read_up(e, v, &up) != SWIM_OK) return SWIM_EDEVICE;
   std::memset(o, 0, sizeof(*o));
-  o->up = m.up;
+  o->up = up;
   o->joined = m.joined;
   o->leave_pending = m.leave_pending;
   o->join_pending = m.join_pending;
@@ -647,39 +1046,47 @@ int32_t swim_read_member(swim_engine* e, uint32_t v, swim_member_state* o) {
   return SWIM_OK;
 }
 
-static int32_t read_list(swim_engine* e, uint32_t v, const uint32_t* base, uint32_t len, uint32_t* out, uint32_t cap,
-                         uint32_t* lenp) {
+static int32_t read_list(swim_engine* e, Shard& sd, uint32_t v, const uint32_t* base, uint32_t len, uint32_t* out,
+                         uint32_t cap, uint32_t* lenp) {
   if (lenp) *lenp = len;
   if (out && cap && len) {
     uint32_t k = std::min(cap, len);
-    if (hipMemcpy(out, base + (size_t)v * e->n, 4 * (size_t)k, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+    if (hipMemcpy(out, base + (size_t)(v - sd.c.lo) * e->n, 4 * (size_t)k, hipMemcpyDeviceToHost) != hipSuccess)
+      return SWIM_EDEVICE;
   }
   return SWIM_OK;
 }
 
 int32_t swim_read_ping_list(swim_engine* e, uint32_t v, uint32_t* out, uint32_t cap, uint32_t* len) {
   if (!e || v >= e->n) return SWIM_EINVAL;
+  Shard* sd = e->owner_of(v);
+  if (!sd) return SWIM_EINVAL;
   MemberDev m;
-  if (read_member_dev(e, v, &m) != SWIM_OK) return SWIM_EDEVICE;
-  return read_list(e, v, e->c.ping, m.ping_len, out, cap, len);
+  if (read_member_dev(e, *sd, v, &m) != SWIM_OK) return SWIM_EDEVICE;
+  return read_list(e, *sd, v, sd->c.ping, m.ping_len, out, cap, len);
 }
 
 int32_t swim_read_remote_list(swim_engine* e, uint32_t v, uint32_t* out, uint32_t cap, uint32_t* len) {
   if (!e || v >= e->n) return SWIM_EINVAL;
+  Shard* sd = e->owner_of(v);
+  if (!sd) return SWIM_EINVAL;
   MemberDev m;
-  if (read_member_dev(e, v, &m) != SWIM_OK) return SWIM_EDEVICE;
-  return read_list(e, v, e->c.remote, m.remote_len, out, cap, len);
+  if (read_member_dev(e, *sd, v, &m) != SWIM_OK) return SWIM_EDEVICE;
+  return read_list(e, *sd, v, sd->c.remote, m.remote_len, out, cap, len);
 }
 
 int32_t swim_read_gossips(swim_engine* e, uint32_t v, swim_gossip* out, uint32_t cap, uint32_t* len) {
   if (!e || v >= e->n) return SWIM_EINVAL;
+  Shard* sd = e->owner_of(v);
+  if (!sd) return SWIM_EINVAL;
   MemberDev m;
-  if (read_member_dev(e, v, &m) != SWIM_OK) return SWIM_EDEVICE;
+  if (read_member_dev(e, *sd, v, &m) != SWIM_OK) return SWIM_EDEVICE;
   if (len) *len = m.gossip_len;
   uint32_t k = std::min(cap, m.gossip_len);
   if (!out || !k) return SWIM_OK;
   std::vector<GossipDev> g(k);
-  if (hipMemcpy(g.data(), e->c.slab + (size_t)v * e->c.gcap, sizeof(GossipDev) * k, hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpy(g.data(), sd->c.slab + (size_t)(v - sd->c.lo) * sd->c.gcap, sizeof(GossipDev) * k,
+                hipMemcpyDeviceToHost) != hipSuccess)
     return SWIM_EDEVICE;
   for (uint32_t i = 0; i < k; ++i) {
     out[i].gossiper = g[i].gossiper;
@@ -696,10 +1103,12 @@ int32_t swim_read_gossips(swim_engine* e, uint32_t v, swim_gossip* out, uint32_t
 
 int32_t swim_read_collector(swim_engine* e, uint32_t v, uint32_t gossiper, swim_interval* out, uint32_t cap, uint32_t* len) {
   if (!e || v >= e->n) return SWIM_EINVAL;
+  Shard* sd = e->owner_of(v);
+  if (!sd) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  std::vector<CollDev> tab(e->c.hcap);
-  if (hipMemcpy(tab.data(), e->c.coll + (size_t)v * e->c.hcap, sizeof(CollDev) * e->c.hcap, hipMemcpyDeviceToHost) !=
-      hipSuccess)
+  std::vector<CollDev> tab(sd->c.hcap);
+  if (hipMemcpy(tab.data(), sd->c.coll + (size_t)(v - sd->c.lo) * sd->c.hcap, sizeof(CollDev) * sd->c.hcap,
+                hipMemcpyDeviceToHost) != hipSuccess)
     return SWIM_EDEVICE;
   if (len) *len = 0;
   for (const CollDev& d : tab) {
@@ -717,18 +1126,20 @@ int32_t swim_read_collector(swim_engine* e, uint32_t v, uint32_t gossiper, swim_
 int32_t swim_profile_enable(swim_engine* e, int32_t enable) {
   if (!e) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  if (e->prof_ev.empty()) {
-    e->prof_ev.resize(4 * kDrainEvery + 4);
-    for (auto& ev : e->prof_ev)
-      if (hipEventCreate(&ev) != hipSuccess) return SWIM_EDEVICE;
+  for (Shard& sd : e->sh) {
+    if (sd.prof_ev.empty()) {
+      sd.prof_ev.resize(4 * kDrainEvery + 4);
+      for (auto& ev : sd.prof_ev)
+        if (hipEventCreate(&ev) != hipSuccess) return SWIM_EDEVICE;
+    }
+    sd.prof_used = 0;
+    sd.prof_ms = 0;
+    sd.prof_launches = 0;
   }
-  e->prof_used = 0;
-  e->prof_ms = 0;
-  e->prof_launches = 0;
   unsigned long long st[ST_COUNT];
   if (read_stats(e, st) != SWIM_OK) return SWIM_EDEVICE;
-  e->prof_base_msgs = st[ST_MERGE_MSGS];
-  e->prof_base_recs = st[ST_MERGE_RECORDS];
+  e->sh[0].prof_base_msgs = st[ST_MERGE_MSGS];
+  e->sh[0].prof_base_recs = st[ST_MERGE_RECORDS];
   e->prof = enable != 0;
   return SWIM_OK;
 }
@@ -736,13 +1147,17 @@ int32_t swim_profile_enable(swim_engine* e, int32_t enable) {
 int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out) {
   if (!e || !out) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  prof_flush(e);
+  out->launches = 0;
+  out->total_ms = 0;
+  for (Shard& sd : e->sh) {
+    prof_flush(sd);
+    out->launches += sd.prof_launches;
+    out->total_ms += sd.prof_ms;
+  }
   unsigned long long st[ST_COUNT];
   if (read_stats(e, st) != SWIM_OK) return SWIM_EDEVICE;
-  out->launches = e->prof_launches;
-  out->total_ms = e->prof_ms;
-  out->messages = st[ST_MERGE_MSGS] - e->prof_base_msgs;
-  out->records = st[ST_MERGE_RECORDS] - e->prof_base_recs;
+  out->messages = st[ST_MERGE_MSGS] - e->sh[0].prof_base_msgs;
+  out->records = st[ST_MERGE_RECORDS] - e->sh[0].prof_base_recs;
   out->alg_bytes = out->messages * (uint64_t)e->n * 16ull + out->records * 8ull;
   return SWIM_OK;
 }

@@ -44,6 +44,8 @@ enum Reason { R_FD_EVENT, R_GOSSIP, R_SYNC, R_INITIAL_SYNC, R_TIMEOUT };
 constexpr uint64_t B_IN_TABLE = 1ull << 34, B_IN_MEMBERS = 1ull << 35, B_ALIVE_EMITTED = 1ull << 36,
                    B_HAS_TIMER = 1ull << 37, B_HAS_METADATA = 1ull << 38;
 
+// Per-member scalar state of an OWNED member (index v - Ctx.lo).  Whether a member's transport
+// is up is replicated on every shard (Ctx.up), because every sender reads it.
 struct alignas(16) MemberDev {
   uint64_t fd_period, ack_due, relay_due, g_period, g_counter, period_used, leave_seq;
   int64_t fd_start, g_start, sync_start;
@@ -52,7 +54,7 @@ struct alignas(16) MemberDev {
   int32_t remote_idx;
   uint32_t gossip_len, table_size, members_size, leave_gossiper;
   uint32_t ev_minor, fetch_ctr, fd_sync_cnt, ins_rank, init_total, init_done;
-  uint8_t up, joined, join_now, join_pending, leave_pending, leave_done, sync_on, pad;
+  uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, pad[2];
 };
 
 struct GossipDev {  // GossipState + Gossip + MembershipRecord payload, 32 B
@@ -85,22 +87,28 @@ struct GMsgFull {
 
 struct SyncReq {  // SYNC (request) or SYNC_ACK
   uint32_t from, to, ordinal, slot;
-  uint32_t flags;  // bit0 initial, bit1 outfail, bit2 delivered, bit3 acked
-  uint32_t pad[3];
+  uint32_t flags;    // bit0 initial, bit1 outfail, bit2 delivered
+  uint32_t content;  // NONE: `from` is owned here (row / snapshot); else index into the received rows
+  uint32_t pad[2];
 };
 
 struct InsOp {  // deferred pingMembers.add(nextInt(size), member) of an ADDED event
   uint32_t v, s, phase, minor, rank, pad[3];
 };
 
+// Row sharding: shard r owns viewers [lo, lo + nl) with lo = r * sz.  Every array
+// indexed by viewer (cells, lists, slab, collectors, mem, per-viewer counters) holds owned rows only
+// and is indexed by v - lo; the network emulator, seeds and `up` are replicated.
 struct Ctx {
   uint32_t n, gcap, hcap, wheel_mask, wheel_cap;
+  uint32_t lo, nl, sz, rank, world;
   uint32_t P, to_ticks, relay_ticks, G, S, sync_to_ticks, tick_ms;
   int32_t ping_interval, suspicion_mult, repeat_mult, fanout, ping_req_members, seg_threshold, record_fd;
   uint32_t key0, key1;
   uint64_t T;
   uint64_t* cells;
   MemberDev* mem;
+  uint8_t* up;  // replicated: member's transport is running
   uint32_t* ping;
   uint32_t* remote;
   GossipDev* slab;
@@ -187,7 +195,13 @@ __device__ __forceinline__ uint64_t c_with_record(uint64_t c, uint32_t st, int32
 __device__ __forceinline__ uint64_t c_with_deadline(uint64_t c, uint64_t tick) {
   return (c & ((1ull << 39) - 1)) | ((tick & SWIM_DEADLINE_MASK) << 39);
 }
-__device__ __forceinline__ uint64_t* row(const Ctx& c, uint32_t v) { return c.cells + (size_t)v * c.n; }
+__device__ __forceinline__ uint64_t* row(const Ctx& c, uint32_t v) { return c.cells + (size_t)(v - c.lo) * c.n; }
+__device__ __forceinline__ MemberDev& mem(const Ctx& c, uint32_t v) { return c.mem[v - c.lo]; }
+__device__ __forceinline__ uint32_t* ping_list(const Ctx& c, uint32_t v) { return c.ping + (size_t)(v - c.lo) * c.n; }
+__device__ __forceinline__ uint32_t* remote_list(const Ctx& c, uint32_t v) { return c.remote + (size_t)(v - c.lo) * c.n; }
+__device__ __forceinline__ GossipDev* slab_of(const Ctx& c, uint32_t v) { return c.slab + (size_t)(v - c.lo) * c.gcap; }
+__device__ __forceinline__ bool owned(const Ctx& c, uint32_t v) { return v - c.lo < c.nl; }
+__device__ __forceinline__ uint32_t owner(const Ctx& c, uint32_t v) { return v / c.sz; }
 
 __device__ __forceinline__ void set_err(const Ctx& c, uint32_t bit) { atomicOr(c.err, bit); }
 // Counters are replicated ST_REPL times (summed on readback) so that thousands of workgroups never
@@ -253,7 +267,7 @@ __device__ __forceinline__ bool lost_k(const Ctx& c, int32_t pct, uint32_t membe
 // the draw is keyed (member, stream, sub24, sub32)
 __device__ __forceinline__ bool out_fail(const Ctx& c, uint32_t a, uint32_t b, uint32_t member, uint32_t stream,
                                          uint32_t sub24, uint32_t sub32) {
-  return !c.mem[b].up || lost_k(c, out_loss(c, a, b), member, stream, sub24, sub32);
+  return !c.up[b] || lost_k(c, out_loss(c, a, b), member, stream, sub24, sub32);
 }
 
 // ------------------------------------------------------------------------------- collectors
@@ -262,7 +276,7 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   return x;
 }
 __device__ inline CollDev* coll_find(const Ctx& c, uint32_t v, uint32_t gossiper) {
-  CollDev* base = c.coll + (size_t)v * c.hcap;
+  CollDev* base = c.coll + (size_t)(v - c.lo) * c.hcap;
   uint32_t mask = c.hcap - 1, h = hash32(gossiper) & mask, key = gossiper + 1;
   for (uint32_t i = 0; i < c.hcap; ++i) {
     CollDev* e = base + ((h + i) & mask);
@@ -273,7 +287,7 @@ __device__ inline CollDev* coll_find(const Ctx& c, uint32_t v, uint32_t gossiper
 }
 // ensureSequence (GossipProtocolImpl.java:279-281)
 __device__ inline CollDev* coll_ensure(const Ctx& c, uint32_t v, uint32_t gossiper) {
-  CollDev* base = c.coll + (size_t)v * c.hcap;
+  CollDev* base = c.coll + (size_t)(v - c.lo) * c.hcap;
   uint32_t mask = c.hcap - 1, h = hash32(gossiper) & mask, key = gossiper + 1;
   for (uint32_t i = 0; i < c.hcap; ++i) {
     CollDev* e = base + ((h + i) & mask);
@@ -342,15 +356,15 @@ __device__ inline void emit(const Ctx& c, uint32_t v, uint32_t s, uint32_t type,
 // ADDED: the remote list append is O(1) and done now; the pingMembers insert is deferred to the
 // phase's list kernel, which applies a viewer's inserts in event order.
 __device__ inline void on_added(const Ctx& c, uint32_t v, uint32_t s, uint32_t phase, uint32_t minor) {
-  MemberDev& m = c.mem[v];
-  c.remote[(size_t)v * c.n + m.remote_len] = s;
+  MemberDev& m = mem(c, v);
+  remote_list(c, v)[m.remote_len] = s;
   m.remote_len++;
   uint32_t rank = m.ins_rank++;
   if (rank == 0) {
     uint32_t li = atomicAdd(c.ins_list_cnt, 1u);
     c.ins_list[li] = v;
   }
-  c.ins_cnt[v] = rank + 1;
+  c.ins_cnt[v - c.lo] = rank + 1;
   uint32_t i = atomicAdd(c.ins_total, 1u);
   if (i >= c.ins_cap) { set_err(c, ERR_INS); return; }
   InsOp op;
@@ -368,7 +382,7 @@ __device__ inline void on_removed(const Ctx& c, uint32_t v, uint32_t s) {
     e->n = 0;
     e->cleared = 1;
   }
-  if (atomicExch(&c.compact_flag[v], 1u) == 0u) c.compact_list[atomicAdd(c.compact_cnt, 1u)] = v;
+  if (atomicExch(&c.compact_flag[v - c.lo], 1u) == 0u) c.compact_list[atomicAdd(c.compact_cnt, 1u)] = v;
 }
 
 __device__ inline void publish_event(const Ctx& c, uint32_t v, uint32_t s, uint32_t type, uint32_t phase,
@@ -379,13 +393,13 @@ __device__ inline void publish_event(const Ctx& c, uint32_t v, uint32_t s, uint3
 }
 
 __device__ __forceinline__ uint32_t next_minor(const Ctx& c, uint32_t v, uint32_t phase, uint32_t s) {
-  return phase == SWIM_PHASE_TIMERS ? s : c.mem[v].ev_minor++;
+  return phase == SWIM_PHASE_TIMERS ? s : mem(c, v).ev_minor++;
 }
 
 // ------------------------------------------------------------------------------- gossip origination
 // spreadMembershipGossip (MembershipProtocolImpl.java:845-860) -> createAndPutGossip (GossipProtocolImpl.java:190-199)
 __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject, uint32_t status, int32_t inc) {
-  MemberDev& m = c.mem[v];
+  MemberDev& m = mem(c, v);
   if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); return; }
   GossipDev g;
   g.gossiper = v;
@@ -396,7 +410,7 @@ __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject,
   g.inf_period = (uint32_t)m.g_period;
   g.inf0 = NONE;
   g.inf1 = NONE;
-  c.slab[(size_t)v * c.gcap + m.gossip_len] = g;
+  slab_of(c, v)[m.gossip_len] = g;
   m.gossip_len++;
   m.g_counter++;
   CollDev* e = coll_ensure(c, v, v);
@@ -411,7 +425,7 @@ __device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
   uint64_t* cp = row(c, v) + s;
   uint64_t cell = *cp;
   if (c_has(cell, B_HAS_TIMER)) return;
-  uint64_t ms = (uint64_t)c.suspicion_mult * (uint64_t)ceil_log2(c.mem[v].table_size) * (uint64_t)c.ping_interval;
+  uint64_t ms = (uint64_t)c.suspicion_mult * (uint64_t)ceil_log2(mem(c, v).table_size) * (uint64_t)c.ping_interval;
   uint64_t deadline = c.T + ms / c.tick_ms;
   *cp = c_with_deadline(cell | B_HAS_TIMER, deadline);
   uint32_t b = (uint32_t)(deadline & c.wheel_mask);
@@ -423,7 +437,7 @@ __device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
 // ------------------------------------------------------------------------------- metadata fetch
 // MetadataStoreImpl.fetchMetadata (:146-185) + onMetadataRequest (:201-240): one round trip.
 __device__ inline bool fetch_ok(const Ctx& c, uint32_t v, uint32_t s, uint32_t phase) {
-  uint32_t f = c.mem[v].fetch_ctr++;
+  uint32_t f = mem(c, v).fetch_ctr++;
   stat_add(c, ST_FETCHES, 1);
   bool ok = !out_fail(c, v, s, v, SWIM_STREAM_FETCH_REQ, phase, f) && in_pass(c, s, v) &&
             !out_fail(c, s, v, v, SWIM_STREAM_FETCH_RESP, phase, f) && in_pass(c, v, s);
@@ -436,7 +450,7 @@ __device__ inline bool fetch_ok(const Ctx& c, uint32_t v, uint32_t s, uint32_t p
 // metadata fetch succeeded: the caller applies it (apply_alive) at its flush point.
 __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, uint32_t st1, int32_t inc1,
                                          int reason, uint32_t phase) {
-  MemberDev& m = c.mem[v];
+  MemberDev& m = mem(c, v);
   uint64_t* cp = row(c, v) + s;
   uint64_t cell = *cp;
   const bool present = c_has(cell, B_IN_TABLE);
@@ -500,7 +514,7 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
 
 // doOnSuccess of the metadata fetch (:648-656) + onAliveMemberDetected (:769-795)
 __device__ inline void apply_alive(const Ctx& c, uint32_t v, uint32_t s, int32_t inc1, int reason, uint32_t phase) {
-  MemberDev& m = c.mem[v];
+  MemberDev& m = mem(c, v);
   uint64_t* cp = row(c, v) + s;
   *cp &= ~B_HAS_TIMER;  // cancelSuspicionTimeoutTask
   if (reason != R_GOSSIP && reason != R_INITIAL_SYNC) spread_gossip(c, v, s, SWIM_ALIVE, inc1);

@@ -26,8 +26,29 @@ struct Counters {
   uint32_t pad[3];
 };
 
+// per-tick message counts by destination shard (sharded engines), zeroed by k_end_tick
+constexpr int MAXW = 16;
+struct Xc {
+  uint32_t msg[MAXW], req[MAXW], ack[MAXW];
+  uint32_t stop;
+  uint32_t pad[3];
+};
+
 struct Bufs {
   Counters* k;
+  // cross-shard exchange; an unsharded engine (world == 1) never touches these
+  Xc* x;
+  GMsgFull* tx_msgs;  // [world][tx_msg_cap] GOSSIP_REQs for receivers owned by another shard
+  uint32_t tx_msg_cap;
+  SyncReq* tx_reqs;   // [world][tx_req_cap] SYNCs whose receiver is owned by another shard
+  SyncReq* tx_acks;   // [world][tx_req_cap] SYNC_ACKs whose receiver is owned by another shard
+  uint32_t tx_req_cap;
+  uint32_t* tx_stops; // members whose graceful leave completed this tick (broadcast)
+  uint32_t tx_stop_cap;
+  const GMsgFull* rx_msgs;
+  const SyncReq* rx_reqs;
+  const uint64_t* rx_rows;  // content rows of received SYNC / SYNC_ACKs, indexed by SyncReq.content
+  const uint32_t* rx_stops;
   GMsgFull* msgs;      // produced in emit order
   GMsgFull* msgs_out;  // grouped by receiver
   uint32_t msg_cap;
@@ -63,7 +84,7 @@ struct Bufs {
 // ------------------------------------------------------------------------------- init
 __global__ void k_init_rows(Ctx c, uint32_t n_initial) {
   const uint64_t conv = B_IN_TABLE | B_IN_MEMBERS | B_ALIVE_EMITTED | B_HAS_METADATA;
-  for (uint32_t v = blockIdx.x; v < c.n; v += gridDim.x) {
+  for (uint32_t v = c.lo + blockIdx.x; v < c.lo + c.nl; v += gridDim.x) {
     uint64_t* r = row(c, v);
     const bool init = v < n_initial;
     for (uint32_t s = threadIdx.x; s < c.n; s += blockDim.x)
@@ -73,20 +94,20 @@ __global__ void k_init_rows(Ctx c, uint32_t n_initial) {
 
 // initial members: converged state, seeded Fisher-Yates ping / remote lists
 __global__ void k_init_members(Ctx c, uint32_t n_initial, int32_t sync_stagger) {
-  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= c.n) return;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c.nl) return;
+  const uint32_t v = c.lo + i;
   MemberDev m{};
   m.ack_target = NONE;
   m.relay_target = NONE;
   m.leave_gossiper = NONE;
   m.remote_idx = -1;
   if (v < n_initial) {
-    m.up = 1;
     m.joined = 1;
     m.table_size = n_initial;
     m.members_size = n_initial;
-    uint32_t* pl = c.ping + (size_t)v * c.n;
-    uint32_t* rl = c.remote + (size_t)v * c.n;
+    uint32_t* pl = ping_list(c, v);
+    uint32_t* rl = remote_list(c, v);
     uint32_t k = 0;
     for (uint32_t s = 0; s < n_initial; ++s)
       if (s != v) { pl[k] = s; rl[k] = s; ++k; }
@@ -104,7 +125,7 @@ __global__ void k_init_members(Ctx c, uint32_t n_initial, int32_t sync_stagger) 
     m.sync_on = 1;
     m.sync_start = sync_stagger ? -(int64_t)next_int(draw_at(c, v, 0, SWIM_STREAM_INIT_SYNC_PHASE, 0, 0), c.S) : 0;
   }
-  c.mem[v] = m;
+  c.mem[i] = m;
 }
 
 // ------------------------------------------------------------------------------- block scan helper
@@ -133,13 +154,14 @@ __device__ inline uint32_t block_exclusive_scan(uint32_t x, uint32_t* s_wave, ui
 }
 
 // ------------------------------------------------------------------------------- start joins
+// (the host has already set the replicated up[v] on every shard)
 __global__ void k_start_joins(Ctx c) {
-  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= c.n) return;
-  MemberDev& m = c.mem[v];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c.nl) return;
+  const uint32_t v = c.lo + i;
+  MemberDev& m = c.mem[i];
   if (!m.join_pending) return;
   m.join_pending = 0;
-  m.up = 1;
   m.joined = 1;
   m.join_now = 1;
   m.fd_start = (int64_t)c.T;
@@ -161,7 +183,7 @@ __global__ void k_timers(Ctx c, uint32_t bucket) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
     uint64_t e = ent[i];
     uint32_t v = (uint32_t)(e >> 32), s = (uint32_t)e;
-    if (!c.mem[v].up) continue;
+    if (!c.up[v]) continue;
     unsigned long long* cp = (unsigned long long*)(row(c, v) + s);
     unsigned long long old = *cp;
     bool claimed = false;
@@ -205,10 +227,10 @@ __global__ void __launch_bounds__(256) k_compact(Ctx c, Counters* k, uint32_t bu
   const uint32_t cnt = k->compact_cnt;
   for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
     uint32_t v = c.compact_list[i];
-    MemberDev& m = c.mem[v];
-    compact_list<256>(c, v, c.ping + (size_t)v * c.n, m.ping_len);
-    compact_list<256>(c, v, c.remote + (size_t)v * c.n, m.remote_len);
-    if (threadIdx.x == 0) c.compact_flag[v] = 0;
+    MemberDev& m = mem(c, v);
+    compact_list<256>(c, v, ping_list(c, v), m.ping_len);
+    compact_list<256>(c, v, remote_list(c, v), m.remote_len);
+    if (threadIdx.x == 0) c.compact_flag[v - c.lo] = 0;
   }
 }
 
@@ -216,7 +238,7 @@ __global__ void __launch_bounds__(256) k_compact(Ctx c, Counters* k, uint32_t bu
 // publishPingResult (FailureDetectorImpl.java:377-380) -> onFailureDetectorEvent (:418-449)
 __device__ inline void publish_fd(const Ctx& c, uint32_t v, uint32_t t, uint32_t status, unsigned long long& nev) {
   nev++;
-  MemberDev& m = c.mem[v];
+  MemberDev& m = mem(c, v);
   if (c.record_fd)
     emit(c, v, t, SWIM_EV_FD_ALIVE + (status == SWIM_ALIVE ? 0 : status == SWIM_SUSPECT ? 1 : 2), SWIM_PHASE_FD,
          m.ev_minor++);
@@ -225,7 +247,7 @@ __device__ inline void publish_fd(const Ctx& c, uint32_t v, uint32_t t, uint32_t
   if (c_status(cell) == status) return;
   if (status == SWIM_ALIVE) {
     if (m.fd_sync_cnt >= FD_SYNC_MAX) { set_err(c, ERR_FDSYNC); return; }
-    c.fd_sync[(size_t)v * FD_SYNC_MAX + m.fd_sync_cnt++] = t;
+    c.fd_sync[(size_t)(v - c.lo) * FD_SYNC_MAX + m.fd_sync_cnt++] = t;
     return;
   }
   update_membership(c, v, t, status, c_inc(cell), R_FD_EVENT, SWIM_PHASE_FD);
@@ -235,8 +257,8 @@ __device__ inline void publish_fd(const Ctx& c, uint32_t v, uint32_t t, uint32_t
 __device__ inline uint32_t select_relays(const Ctx& c, uint32_t v, uint32_t t, uint32_t* out) {
   const int32_t k = c.ping_req_members;
   if (k <= 0) return 0;
-  const MemberDev& m = c.mem[v];
-  const uint32_t* pl = c.ping + (size_t)v * c.n;
+  const MemberDev& m = mem(c, v);
+  const uint32_t* pl = ping_list(c, v);
   int64_t pos = -1;
   for (uint32_t i = 0; i < m.ping_len; ++i)
     if (pl[i] == t) { pos = i; break; }
@@ -291,7 +313,7 @@ __device__ inline void ping_req(const Ctx& c, uint32_t v, uint32_t t, unsigned l
   if (arrived >= 0 && in_pass(c, v, relays[arrived])) {
     for (uint32_t i = 0; i < npend; ++i) publish_fd(c, v, t, SWIM_ALIVE, nev);
   } else {
-    MemberDev& m = c.mem[v];
+    MemberDev& m = mem(c, v);
     m.relay_due = c.T + c.relay_ticks;
     m.relay_target = t;
     m.relay_pending = npend;
@@ -300,8 +322,8 @@ __device__ inline void ping_req(const Ctx& c, uint32_t v, uint32_t t, unsigned l
 
 __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& nev, unsigned long long& nreq,
                                  unsigned long long& npings) {
-  MemberDev& m = c.mem[v];
-  if (!m.up) return;
+  MemberDev& m = mem(c, v);
+  if (!c.up[v]) return;
   const bool due = (int64_t)c.T > m.fd_start && ((int64_t)c.T - m.fd_start) % c.P == 0;
   if (!due && m.relay_due != c.T && m.ack_due != c.T) return;
   m.ev_minor = 0;
@@ -318,7 +340,7 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
   if (due) {  // doPing (:126-171), selectPingMember (:352-361)
     m.fd_period++;
     if (m.ping_len > 0) {
-      uint32_t* pl = c.ping + (size_t)v * c.n;
+      uint32_t* pl = ping_list(c, v);
       if (m.ping_cursor >= m.ping_len) {
         m.ping_cursor = 0;
         shuffle_list(c, v, pl, m.ping_len, SWIM_STREAM_FD_SHUFFLE);
@@ -339,42 +361,51 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
 
 // launched with a multiple of 64 threads per block: every lane reaches the wave-reduced counters
 __global__ void k_fd(Ctx c) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long nev = 0, nreq = 0, npings = 0;
-  if (v < c.n) fd_member(c, v, nev, nreq, npings);
+  if (i < c.nl) fd_member(c, c.lo + i, nev, nreq, npings);
   wave_stat_add(c, ST_FD_EVENTS, nev);
   wave_stat_add(c, ST_PING_REQS, nreq);
   wave_stat_add(c, ST_PINGS, npings);
 }
 
 // ------------------------------------------------------------------------------- phase C
-__device__ __forceinline__ bool gossip_due(const Ctx& c, const MemberDev& m) {
-  return m.up && (int64_t)c.T > m.g_start && ((int64_t)c.T - m.g_start) % c.G == 0;
+__device__ __forceinline__ bool gossip_due(const Ctx& c, uint32_t v, const MemberDev& m) {
+  return c.up[v] && (int64_t)c.T > m.g_start && ((int64_t)c.T - m.g_start) % c.G == 0;
 }
 
 // checkGossipSegmentation (GossipProtocolImpl.java:217-236); only launched when the threshold is
 // below the inline interval capacity (otherwise a clear can never trigger).
 __global__ void k_gossip_seg(Ctx c) {
-  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= c.n) return;
-  const MemberDev& m = c.mem[v];
-  if (!gossip_due(c, m)) return;
-  CollDev* base = c.coll + (size_t)v * c.hcap;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c.nl) return;
+  const MemberDev& m = c.mem[i];
+  if (!gossip_due(c, c.lo + i, m)) return;
+  CollDev* base = c.coll + (size_t)i * c.hcap;
   for (uint32_t i = 0; i < c.hcap; ++i)
     if (base[i].key && (int32_t)base[i].n > c.seg_threshold) { base[i].n = 0; base[i].cleared = 1; }
 }
 
+// a GOSSIP_REQ for a receiver owned by this shard joins the receiver's inbox
+__device__ inline void deliver_local_msg(const Ctx& c, const Bufs& b, GMsgFull msg) {
+  const uint32_t i = atomicAdd(&b.k->msg_total, 1u);
+  if (i >= b.msg_cap) { set_err(c, ERR_MSGS); return; }
+  msg.slot = atomicAdd(&b.msg_cnt[msg.to - c.lo], 1u);
+  if (msg.slot == 0) b.msg_recv[atomicAdd(&b.k->msg_recv_cnt, 1u)] = msg.to;
+  b.msgs[i] = msg;
+}
+
 // doSpreadGossip (:141-184): period++, select members, send, sweep, complete futures.
 __device__ inline unsigned long long gossip_emit_member(const Ctx& c, const Bufs& b, uint32_t v) {
-  MemberDev& m = c.mem[v];
-  if (!gossip_due(c, m)) return 0;
+  MemberDev& m = mem(c, v);
+  if (!gossip_due(c, v, m)) return 0;
   const uint64_t period = m.g_period++;
   m.period_used = period;
   if (m.gossip_len == 0) return 0;
   // selectGossipMembers (:322-343)
   uint32_t targets[16];
   uint32_t nt = 0;
-  uint32_t* rl = c.remote + (size_t)v * c.n;
+  uint32_t* rl = remote_list(c, v);
   const uint32_t F = (uint32_t)c.fanout;
   if (m.remote_len < F) {
     for (uint32_t i = 0; i < m.remote_len; ++i) targets[nt++] = rl[i];
@@ -389,11 +420,12 @@ __device__ inline unsigned long long gossip_emit_member(const Ctx& c, const Bufs
   const int32_t size1 = (int32_t)m.remote_len + 1;
   const uint64_t spread = (uint64_t)(c.repeat_mult * ceil_log2((uint32_t)size1));
   const uint64_t sweep = 2 * (spread + 1);
-  GossipDev* slab = c.slab + (size_t)v * c.gcap;
+  GossipDev* slab = slab_of(c, v);
   unsigned long long nmsg = 0;
   for (uint32_t j = 0; j < nt; ++j) {
     const uint32_t t = targets[j];
-    const bool t_up = c.mem[t].up != 0;
+    const bool t_up = c.up[t] != 0;
+    const bool local = owned(c, t);
     const int32_t loss = out_loss(c, v, t);
     const bool pass = in_pass(c, t, v);
     for (uint32_t p = 0; p < m.gossip_len; ++p) {  // selectGossipsToSend (:311-320)
@@ -402,18 +434,21 @@ __device__ inline unsigned long long gossip_emit_member(const Ctx& c, const Bufs
       if (g.inf0 == t || g.inf1 == t) continue;
       nmsg++;
       if (!t_up || lost_k(c, loss, v, SWIM_STREAM_GOSSIP_OUT, j, p) || !pass) continue;
+      GMsgFull msg;
+      msg.to = t; msg.from = v; msg.pos = p; msg.slot = 0;
+      msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
+      msg.inc = g.inc; msg.pad[0] = msg.pad[1] = msg.pad[2] = 0;
+      if (!local) {  // another shard's receiver: it filters duplicates on arrival (k_recv_msgs)
+        const uint32_t d = owner(c, t);
+        const uint32_t i = atomicAdd(&b.x->msg[d], 1u);
+        if (i >= b.tx_msg_cap) { set_err(c, ERR_MSGS); continue; }
+        b.tx_msgs[(size_t)d * b.tx_msg_cap + i] = msg;
+        continue;
+      }
       // certain duplicate at the receiver: its collector already holds the sequence id and can
       // only grow until delivery
       if (coll_contains(coll_find(c, t, g.gossiper), g.seq)) continue;
-      uint32_t i = atomicAdd(&b.k->msg_total, 1u);
-      if (i >= b.msg_cap) { set_err(c, ERR_MSGS); continue; }
-      uint32_t slot = atomicAdd(&b.msg_cnt[t], 1u);
-      if (slot == 0) b.msg_recv[atomicAdd(&b.k->msg_recv_cnt, 1u)] = t;
-      GMsgFull msg;
-      msg.to = t; msg.from = v; msg.pos = p; msg.slot = slot;
-      msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
-      msg.inc = g.inc; msg.pad[0] = msg.pad[1] = msg.pad[2] = 0;
-      b.msgs[i] = msg;
+      deliver_local_msg(c, b, msg);
     }
   }
   // sweep (:158-164, :350-358), order preserving
@@ -432,31 +467,45 @@ __device__ inline unsigned long long gossip_emit_member(const Ctx& c, const Bufs
       if (period > (uint64_t)g.inf_period + spread && g.gossiper == m.leave_gossiper && g.seq == (uint32_t)m.leave_seq)
         m.leave_done = 1;
     }
+    if (m.leave_done && c.world > 1) {  // every shard stops sending to v at the end of this tick
+      const uint32_t i = atomicAdd(&b.x->stop, 1u);
+      if (i < b.tx_stop_cap) b.tx_stops[i] = v; else set_err(c, ERR_MSGS);
+    }
   }
   return nmsg;
 }
 
 __global__ void k_gossip_emit(Ctx c, Bufs b) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned long long nmsg = v < c.n ? gossip_emit_member(c, b, v) : 0;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long nmsg = i < c.nl ? gossip_emit_member(c, b, c.lo + i) : 0;
   wave_stat_add(c, ST_GOSSIP_MESSAGES, nmsg);
+}
+
+// GOSSIP_REQs arriving from other shards: drop provable duplicates (the emitter could not see
+// this shard's collectors), then join the local message list exactly as a local send does
+__global__ void k_recv_msgs(Ctx c, Bufs b, uint32_t nrx) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrx; i += gridDim.x * blockDim.x) {
+    const GMsgFull msg = b.rx_msgs[i];
+    if (coll_contains(coll_find(c, msg.to, msg.gossiper), msg.seq)) continue;
+    deliver_local_msg(c, b, msg);
+  }
 }
 
 // group-by-receiver: region start per receiver, then scatter by (start + arrival slot)
 __global__ void k_alloc(const uint32_t* list, const uint32_t* list_cnt, const uint32_t* cnt, uint32_t* start,
-                        uint32_t* cursor) {
+                        uint32_t* cursor, uint32_t lo) {
   const uint32_t n = *list_cnt;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    uint32_t r = list[i];
+    uint32_t r = list[i] - lo;
     start[r] = atomicAdd(cursor, cnt[r]);
   }
 }
 
-__global__ void k_scatter_msgs(Bufs b) {
+__global__ void k_scatter_msgs(Bufs b, uint32_t lo) {
   const uint32_t n = min(b.k->msg_total, b.msg_cap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const GMsgFull m = b.msgs[i];
-    b.msgs_out[b.msg_start[m.to] + m.slot] = m;
+    b.msgs_out[b.msg_start[m.to - lo] + m.slot] = m;
   }
 }
 
@@ -497,15 +546,15 @@ __global__ void k_gossip_deliver(Ctx c, Bufs b) {
   unsigned long long acc = 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrecv; i += gridDim.x * blockDim.x) {
     const uint32_t r = b.msg_recv[i];
-    const uint32_t k = b.msg_cnt[r];
-    GMsgFull* a = b.msgs_out + b.msg_start[r];
-    b.msg_cnt[r] = 0;
-    MemberDev& m = c.mem[r];
-    if (!m.up) continue;
+    const uint32_t k = b.msg_cnt[r - c.lo];
+    GMsgFull* a = b.msgs_out + b.msg_start[r - c.lo];
+    b.msg_cnt[r - c.lo] = 0;
+    MemberDev& m = mem(c, r);
+    if (!c.up[r]) continue;
     sort_msgs(a, k);
     m.ev_minor = 0;
     m.fetch_ctr = 0;
-    GossipDev* slab = c.slab + (size_t)r * c.gcap;
+    GossipDev* slab = slab_of(c, r);
     for (uint32_t q = 0; q < k; ++q) {
       const GMsgFull g = a[q];
       CollDev* col = coll_ensure(c, r, g.gossiper);
@@ -550,14 +599,14 @@ __global__ void __launch_bounds__(1024) k_ins_prep(Ctx c, Bufs b) {
   __syncthreads();
   const uint32_t nv = *c.ins_list_cnt;
   for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x) {
-    const uint32_t v = c.ins_list[i];
+    const uint32_t v = c.ins_list[i] - c.lo;
     b.ins_start[v] = atomicAdd(&s_cursor, c.ins_cnt[v]);
   }
   __syncthreads();
   const uint32_t n = min(*c.ins_total, c.ins_cap);
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
     const InsOp op = c.ins[i];
-    b.ins_out[b.ins_start[op.v] + op.rank] = op;
+    b.ins_out[b.ins_start[op.v - c.lo] + op.rank] = op;
   }
 }
 
@@ -567,10 +616,10 @@ __global__ void __launch_bounds__(256) k_ins_apply(Ctx c, Bufs b) {
   const uint32_t nv = *c.ins_list_cnt;
   for (uint32_t i = blockIdx.x; i < nv; i += gridDim.x) {
     const uint32_t v = c.ins_list[i];
-    const uint32_t k = c.ins_cnt[v];
-    const InsOp* ops = b.ins_out + b.ins_start[v];
-    MemberDev& m = c.mem[v];
-    uint32_t* pl = c.ping + (size_t)v * c.n;
+    const uint32_t k = c.ins_cnt[v - c.lo];
+    const InsOp* ops = b.ins_out + b.ins_start[v - c.lo];
+    MemberDev& m = mem(c, v);
+    uint32_t* pl = ping_list(c, v);
     for (uint32_t q = 0; q < k; ++q) {
       const InsOp op = ops[q];
       const uint32_t size = m.ping_len;
@@ -595,7 +644,7 @@ __global__ void __launch_bounds__(256) k_ins_apply(Ctx c, Bufs b) {
       __syncthreads();
     }
     if (threadIdx.x == 0) {
-      c.ins_cnt[v] = 0;
+      c.ins_cnt[v - c.lo] = 0;
       m.ins_rank = 0;
     }
     __syncthreads();
@@ -606,7 +655,7 @@ __global__ void __launch_bounds__(256) k_ins_apply(Ctx c, Bufs b) {
 // selectSyncAddress (MembershipProtocolImpl.java:461-472): uniform over seeds U otherMembers by
 // seeded rejection sampling.
 __device__ inline uint32_t select_sync_address(const Ctx& c, uint32_t v) {
-  const MemberDev& m = c.mem[v];
+  const MemberDev& m = mem(c, v);
   const uint64_t* r = row(c, v);
   uint32_t count = m.members_size - 1;
   for (uint32_t i = 0; i < c.n_seeds; ++i) {
@@ -627,31 +676,44 @@ __device__ inline uint32_t select_sync_address(const Ctx& c, uint32_t v) {
   return NONE;
 }
 
-enum : uint32_t { RQ_INITIAL = 1, RQ_OUTFAIL = 2, RQ_DELIVERED = 4, RQ_ACKED = 8 };
+enum : uint32_t { RQ_INITIAL = 1, RQ_OUTFAIL = 2, RQ_DELIVERED = 4 };
+
+// a delivered SYNC / SYNC_ACK joins its receiver's inbox (the receiver is owned by this shard)
+__device__ inline void enqueue_sync(const Ctx& c, SyncReq q, SyncReq* items, uint32_t* total, uint32_t* cnt,
+                                    uint32_t* recv, uint32_t* recv_cnt, uint32_t cap) {
+  q.slot = atomicAdd(&cnt[q.to - c.lo], 1u);
+  if (q.slot == 0) recv[atomicAdd(recv_cnt, 1u)] = q.to;
+  const uint32_t i = atomicAdd(total, 1u);
+  if (i >= cap) { set_err(c, ERR_REQS); return; }
+  items[i] = q;
+}
 
 __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t to, uint32_t ordinal, bool initial) {
-  MemberDev& m = c.mem[v];
+  MemberDev& m = mem(c, v);
   SyncReq q;
   q.from = v; q.to = to; q.ordinal = ordinal; q.slot = 0; q.flags = initial ? RQ_INITIAL : 0;
-  q.pad[0] = q.pad[1] = q.pad[2] = 0;
+  q.content = NONE; q.pad[0] = q.pad[1] = 0;
   if (initial) m.init_total++;
   if (out_fail(c, v, to, v, SWIM_STREAM_SYNC_OUT, ordinal, 0)) {
-    q.flags |= RQ_OUTFAIL;
     if (initial) m.init_done++;
-  } else if (in_pass(c, to, v)) {
-    q.flags |= RQ_DELIVERED;
-    q.slot = atomicAdd(&b.req_cnt[to], 1u);
-    if (q.slot == 0) b.req_recv[atomicAdd(&b.k->req_recv_cnt, 1u)] = to;
+    return;
   }
-  uint32_t i = atomicAdd(&b.k->req_total, 1u);
-  if (i >= b.req_cap) { set_err(c, ERR_REQS); return; }
-  b.reqs[i] = q;
+  if (!in_pass(c, to, v)) return;  // inbound-blocked at the receiver: silently dropped
+  q.flags |= RQ_DELIVERED;
+  if (!owned(c, to)) {  // content (this row) travels with the request: k_pack_rows
+    const uint32_t d = owner(c, to);
+    const uint32_t i = atomicAdd(&b.x->req[d], 1u);
+    if (i >= b.tx_req_cap) { set_err(c, ERR_REQS); return; }
+    b.tx_reqs[(size_t)d * b.tx_req_cap + i] = q;
+    return;
+  }
+  enqueue_sync(c, q, b.reqs, &b.k->req_total, b.req_cnt, b.req_recv, &b.k->req_recv_cnt, b.req_cap);
 }
 
 // doSync (:339-357), FD-triggered SYNCs (:427-442) and start0's initial SYNC to every seed (:250-291)
 __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Bufs& b, uint32_t v) {
-  MemberDev& m = c.mem[v];
-  if (!m.up) { m.fd_sync_cnt = 0; return 0; }
+  MemberDev& m = mem(c, v);
+  if (!c.up[v]) { m.fd_sync_cnt = 0; return 0; }
   uint32_t k = 0;
   unsigned long long nsync = 0;
   if (m.sync_on && (int64_t)c.T > m.sync_start && ((int64_t)c.T - m.sync_start) % c.S == 0) {
@@ -659,7 +721,7 @@ __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Buf
     if (t != NONE) { add_req(c, b, v, t, k++, false); nsync++; }
   }
   for (uint32_t i = 0; i < m.fd_sync_cnt; ++i) {
-    add_req(c, b, v, c.fd_sync[(size_t)v * FD_SYNC_MAX + i], k++, false);
+    add_req(c, b, v, c.fd_sync[(size_t)(v - c.lo) * FD_SYNC_MAX + i], k++, false);
     nsync++;
   }
   m.fd_sync_cnt = 0;
@@ -675,8 +737,8 @@ __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Buf
 }
 
 __global__ void k_sync_collect(Ctx c, Bufs b) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned long long nsync = v < c.n ? sync_collect_member(c, b, v) : 0;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long nsync = i < c.nl ? sync_collect_member(c, b, c.lo + i) : 0;
   wave_stat_add(c, ST_SYNCS, nsync);
 }
 
@@ -685,12 +747,15 @@ __global__ void k_sync_collect(Ctx c, Bufs b) {
 
 // ------------------------------------------------------------------------------- end of tick
 // start0's doFinally (:285-289) for members that joined this tick; graceful leaves complete.
-__global__ void k_end_tick(Ctx c, Counters* k) {
-  uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void k_end_tick(Ctx c, Counters* k, Xc* x, const uint32_t* rx_stops, uint32_t n_rx_stops) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   // every other kernel of the tick has completed: reset the per-tick scratch counters
-  if (v < sizeof(Counters) / 4) reinterpret_cast<uint32_t*>(k)[v] = 0;
-  if (v >= c.n) return;
-  MemberDev& m = c.mem[v];
+  if (i < sizeof(Counters) / 4) reinterpret_cast<uint32_t*>(k)[i] = 0;
+  if (x && i < sizeof(Xc) / 4) reinterpret_cast<uint32_t*>(x)[i] = 0;
+  if (i < n_rx_stops) c.up[rx_stops[i]] = 0;  // graceful leaves completed on other shards
+  if (i >= c.nl) return;
+  const uint32_t v = c.lo + i;
+  MemberDev& m = c.mem[i];
   if (m.join_now) {
     m.sync_on = 1;
     m.sync_start = (int64_t)c.T + (m.init_done == m.init_total ? 0 : (int64_t)c.sync_to_ticks);
@@ -699,7 +764,7 @@ __global__ void k_end_tick(Ctx c, Counters* k) {
   if (m.leave_done) {
     m.leave_done = 0;
     m.leave_pending = 0;
-    m.up = 0;
+    c.up[v] = 0;
   }
 }
 

@@ -70,31 +70,70 @@ __device__ inline SubPhase sub_phase(const Bufs& b, int d2) {
   return p;
 }
 
+// SYNCs / SYNC_ACKs arriving from other shards (content row = rx_rows[k]) join their inboxes
+__global__ void k_recv_sync(Ctx c, Bufs b, int d2, uint32_t nrx) {
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nrx; k += gridDim.x * blockDim.x) {
+    SyncReq q = b.rx_reqs[k];
+    q.content = k;
+    if (!d2) enqueue_sync(c, q, b.reqs, &b.k->req_total, b.req_cnt, b.req_recv, &b.k->req_recv_cnt, b.req_cap);
+    else enqueue_sync(c, q, b.acks, &b.k->ack_total, b.ack_cnt, b.ack_recv, &b.k->ack_recv_cnt, b.req_cap);
+  }
+}
+
+// content rows of this shard's outgoing SYNC / SYNC_ACKs, packed per destination in tx order (the
+// sender's table when the message is prepared, prepareSyncDataMsg :485-489)
+struct PackPlan {
+  uint32_t cnt[MAXW];
+  uint32_t off[MAXW];  // first packed row of destination d
+};
+__global__ void k_pack_rows(Ctx c, const SyncReq* tx, uint32_t tx_cap, PackPlan plan, uint64_t* out) {
+  for (uint32_t d = 0; d < c.world; ++d) {
+    for (uint32_t k = blockIdx.x; k < plan.cnt[d]; k += gridDim.x) {
+      const SyncReq q = tx[(size_t)d * tx_cap + k];
+      const uint64_t* src = row(c, q.from);
+      uint64_t* dst = out + (size_t)(plan.off[d] + k) * c.n;
+      if (c.n & 1) {  // rows are only 8-B aligned
+        for (uint32_t x = threadIdx.x; x < c.n; x += blockDim.x) dst[x] = src[x];
+      } else {
+        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src);
+        ulonglong2* d2 = reinterpret_cast<ulonglong2*>(dst);
+        for (uint32_t x = threadIdx.x; x < c.n / 2; x += blockDim.x) d2[x] = s2[x];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ const uint64_t* sync_content(const Ctx& c, const Bufs& b, const SyncReq& q) {
+  if (q.content != NONE) return b.rx_rows + (size_t)q.content * c.n;
+  const uint32_t si = b.snap_idx[q.from - c.lo];
+  return si < b.snap_cap ? b.snap + (size_t)si * c.n : row(c, q.from);
+}
+
 __global__ void __launch_bounds__(1024) k_sync_prep(Ctx c, Bufs b, int d2) {
   __shared__ uint32_t s_cursor;
   const SubPhase p = sub_phase(b, d2);
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
   // release the previous sub-phase's snapshot claims
   const uint32_t prev = min(*b.snap_cnt, b.snap_cap);
-  for (uint32_t i = tid; i < prev; i += nt) b.snap_idx[b.snap_list[i]] = NONE;
+  for (uint32_t i = tid; i < prev; i += nt) b.snap_idx[b.snap_list[i] - c.lo] = NONE;
   if (tid == 0) s_cursor = 0;
   __syncthreads();
   if (tid == 0) *b.snap_cnt = 0;
   // one contiguous inbox per receiver
   for (uint32_t i = tid; i < p.nrecv; i += nt) {
-    const uint32_t r = p.recv[i];
+    const uint32_t r = p.recv[i] - c.lo;
     p.start[r] = atomicAdd(&s_cursor, p.cnt[r]);
   }
   __syncthreads();
   if (tid == 0) *p.nitems = s_cursor;
   for (uint32_t i = tid; i < p.total; i += nt) {
     const SyncReq q = p.items[i];
-    if (q.flags & RQ_DELIVERED) p.out[p.start[q.to] + q.slot] = q;
+    p.out[p.start[q.to - c.lo] + q.slot] = q;
   }
   __syncthreads();
   // canonical order inside an inbox: (sender, ordinal)
   for (uint32_t i = tid; i < p.nrecv; i += nt) {
-    const uint32_t r = p.recv[i];
+    const uint32_t r = p.recv[i] - c.lo;
     sort_reqs(p.out + p.start[r], p.cnt[r]);
   }
   __syncthreads();
@@ -103,13 +142,14 @@ __global__ void __launch_bounds__(1024) k_sync_prep(Ctx c, Bufs b, int d2) {
   const uint32_t ni = s_cursor;
   for (uint32_t i = tid; i < ni; i += nt) {
     b.item_total[i] = 0;
-    const uint32_t src = p.out[i].from;
-    if (p.cnt[src] == 0) continue;
-    if (atomicCAS(&b.snap_idx[src], NONE, NONE - 1) == NONE) {
+    if (p.out[i].content != NONE) continue;  // content arrived from another shard: already a copy
+    const uint32_t src = p.out[i].from, sl = src - c.lo;
+    if (p.cnt[sl] == 0) continue;
+    if (atomicCAS(&b.snap_idx[sl], NONE, NONE - 1) == NONE) {
       const uint32_t slot = atomicAdd(b.snap_cnt, 1u);
-      if (slot >= b.snap_cap) { set_err(c, ERR_SNAP); b.snap_idx[src] = NONE; continue; }
+      if (slot >= b.snap_cap) { set_err(c, ERR_SNAP); b.snap_idx[sl] = NONE; continue; }
       b.snap_list[slot] = src;
-      b.snap_idx[src] = slot;
+      b.snap_idx[sl] = slot;
     }
   }
 }
@@ -124,9 +164,10 @@ __global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(Ctx c, Bufs b, int 
     const uint32_t i = w / chunks, ch = w - i * chunks;
     const SyncReq q = p.out[i];
     const uint32_t r = q.to, src = q.from;
-    const uint64_t* __restrict__ content = row(c, src);
+    const bool remote = q.content != NONE;
+    const uint64_t* __restrict__ content = remote ? b.rx_rows + (size_t)q.content * n : row(c, src);
     const uint64_t* __restrict__ rv = row(c, r);
-    const uint32_t si = b.snap_idx[src];
+    const uint32_t si = remote ? NONE : b.snap_idx[src - c.lo];
     uint64_t* snapdst = si < b.snap_cap ? b.snap + (size_t)si * n : nullptr;
     if (ch == 0) msgs++;
     // coalesced: load j of lane t covers subjects base + j*512 + 2t, +1 (1 KiB per wave-instruction)
@@ -249,16 +290,19 @@ __device__ void merge_row_wg(const Ctx& c, uint32_t v, const uint64_t* __restric
   }
 }
 
-// SYNC_ACK bookkeeping: (receiver, slot) for grouping by the original sender
+// SYNC_ACK from `from` (the SYNC receiver) back to `to` (the SYNC sender)
 __device__ inline void add_ack(const Ctx& c, const Bufs& b, uint32_t to, uint32_t from, uint32_t rank, bool initial) {
   SyncReq a;
-  a.from = from; a.to = to; a.ordinal = rank; a.flags = RQ_DELIVERED | (initial ? RQ_INITIAL : 0);
-  a.pad[0] = a.pad[1] = a.pad[2] = 0;
-  a.slot = atomicAdd(&b.ack_cnt[to], 1u);
-  if (a.slot == 0) b.ack_recv[atomicAdd(&b.k->ack_recv_cnt, 1u)] = to;
-  uint32_t i = atomicAdd(&b.k->ack_total, 1u);
-  if (i >= b.req_cap) { set_err(c, ERR_REQS); return; }
-  b.acks[i] = a;
+  a.from = from; a.to = to; a.ordinal = rank; a.slot = 0; a.flags = RQ_DELIVERED | (initial ? RQ_INITIAL : 0);
+  a.content = NONE; a.pad[0] = a.pad[1] = 0;
+  if (!owned(c, to)) {  // content (this row after the SYNC merges) travels with the ack
+    const uint32_t d = owner(c, to);
+    const uint32_t i = atomicAdd(&b.x->ack[d], 1u);
+    if (i >= b.tx_req_cap) { set_err(c, ERR_REQS); return; }
+    b.tx_acks[(size_t)d * b.tx_req_cap + i] = a;
+    return;
+  }
+  enqueue_sync(c, a, b.acks, &b.k->ack_total, b.ack_cnt, b.ack_recv, &b.k->ack_recv_cnt, b.req_cap);
 }
 
 // D1 (d2 = 0): onSync at each receiver, then its SYNC_ACKs.  D2 (d2 = 1): the SYNC_ACK merge at
@@ -273,18 +317,17 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(Ctx c, Bufs b, int d
   uint64_t* pend = b.pend + (size_t)blockIdx.x * c.n;
   for (uint32_t i = blockIdx.x; i < p.nrecv; i += gridDim.x) {
     const uint32_t s = p.recv[i];
-    const uint32_t k = p.cnt[s];
-    const uint32_t first = p.start[s];
+    const uint32_t k = p.cnt[s - c.lo];
+    const uint32_t first = p.start[s - c.lo];
     if (threadIdx.x == 0) {
-      c.mem[s].ev_minor = 0;
-      c.mem[s].fetch_ctr = 0;
+      mem(c, s).ev_minor = 0;
+      mem(c, s).fetch_ctr = 0;
       s_mod = 0;
     }
     __syncthreads();
     for (uint32_t q = 0; q < k; ++q) {
       const SyncReq rq = p.out[first + q];
-      const uint32_t si = b.snap_idx[rq.from];
-      const uint64_t* content = si < b.snap_cap ? b.snap + (size_t)si * c.n : row(c, rq.from);
+      const uint64_t* content = sync_content(c, b, rq);
       const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
       uint32_t npend = 0;
       const uint32_t mod = s_mod;
@@ -318,13 +361,16 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(Ctx c, Bufs b, int d
           const SyncReq rq = p.out[first + q];
           if (out_fail(c, s, rq.from, s, SWIM_STREAM_SYNCACK_OUT, q, 0)) continue;
           if (!in_pass(c, rq.from, s)) continue;
-          if (rq.flags & RQ_INITIAL) atomicAdd(&c.mem[rq.from].init_done, 1u);
           add_ack(c, b, rq.from, s, q, (rq.flags & RQ_INITIAL) != 0);
         }
       } else {
+        // start0's initial-sync completion counts the acks of its INITIAL SYNCs (:270-284)
+        uint32_t init = 0;
+        for (uint32_t q = 0; q < k; ++q) init += (p.out[first + q].flags & RQ_INITIAL) ? 1u : 0u;
+        mem(c, s).init_done += init;
         stat_add(c, ST_SYNC_ACKS, k);
       }
-      p.cnt[s] = 0;
+      p.cnt[s - c.lo] = 0;
     }
     __syncthreads();
   }

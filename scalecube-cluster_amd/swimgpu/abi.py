@@ -60,7 +60,8 @@ class swim_config(C.Structure):
         ("collector_capacity", C.c_uint32),
         ("event_capacity", C.c_uint32),
         ("device", C.c_int32),
-        ("reserved", C.c_uint32 * 7),
+        ("local_shards", C.c_int32),
+        ("reserved", C.c_uint32 * 6),
     ]
 
 
@@ -158,6 +159,10 @@ PROTOTYPES = {
     "swim_suspicion_timeout": (C.c_int64, [C.c_int32, C.c_int32, C.c_int64]),
     "swim_create": (C.c_int32, [POINTER(swim_config), C.c_uint32, C.c_uint32, C.c_uint64, POINTER(_engp)]),
     "swim_destroy": (C.c_int32, [_engp]),
+    "swim_comm_unique_id": (C.c_int32, [POINTER(C.c_uint8)]),
+    "swim_create_shard": (C.c_int32, [POINTER(swim_config), C.c_uint32, C.c_uint32, C.c_uint64, C.c_int32, C.c_int32,
+                                      POINTER(C.c_uint8), POINTER(_engp)]),
+    "swim_shard_info": (C.c_int32, [_engp, POINTER(C.c_int32), POINTER(C.c_int32), _u32p, _u32p]),
     "swim_step_ticks": (C.c_int32, [_engp, C.c_uint32]),
     "swim_step": (C.c_int32, [_engp, C.c_uint32]),
     "swim_now": (C.c_int32, [_engp, _u64p, _u32p, _u32p]),
@@ -210,16 +215,42 @@ def default_config(lib: C.CDLL, preset: int = 0, **overrides) -> swim_config:
     return cfg
 
 
-class Engine:
-    """One engine handle over any library exporting the swim.h ABI."""
+COMM_ID_BYTES = 128
 
-    def __init__(self, lib: C.CDLL, cfg: swim_config, capacity: int, n_initial: int, seed: int):
+
+def comm_unique_id(lib: C.CDLL) -> bytes:
+    """swim_comm_unique_id: rank 0 creates the RCCL bootstrap id the other ranks join with."""
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    _check("swim_comm_unique_id", lib.swim_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Engine:
+    """One engine handle over any library exporting the swim.h ABI.
+
+    With `world > 1` the handle is rank `rank`'s shard of a multi-process cluster
+    (swim_create_shard; every call is collective across the ranks, see swim.h)."""
+
+    def __init__(self, lib: C.CDLL, cfg: swim_config, capacity: int, n_initial: int, seed: int,
+                 rank: int = 0, world: int = 1, comm_id: bytes | None = None):
         self.lib = lib
         self.cfg = cfg
         self.capacity = int(capacity)
         h = _engp()
-        _check("swim_create", lib.swim_create(byref(cfg), capacity, n_initial, seed, byref(h)))
+        if world > 1:
+            if comm_id is None or len(comm_id) != COMM_ID_BYTES:
+                raise ValueError("a sharded engine needs the 128-byte id from comm_unique_id() on rank 0")
+            cid = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(comm_id)
+            _check("swim_create_shard", lib.swim_create_shard(byref(cfg), capacity, n_initial, seed, rank, world,
+                                                              cid, byref(h)))
+        else:
+            _check("swim_create", lib.swim_create(byref(cfg), capacity, n_initial, seed, byref(h)))
         self._h = h
+
+    def shard_info(self) -> dict:
+        r, w, lo, cnt = C.c_int32(), C.c_int32(), C.c_uint32(), C.c_uint32()
+        _check("swim_shard_info", self.lib.swim_shard_info(self._h, byref(r), byref(w), byref(lo), byref(cnt)))
+        return {"rank": r.value, "world": w.value, "lo": lo.value, "count": cnt.value}
 
     # -- lifecycle ------------------------------------------------------------------------
     def close(self) -> None:

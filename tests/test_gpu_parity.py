@@ -6,6 +6,8 @@ aliveEmitted / metadata / timer bits and deadlines), per-member FD / gossip / me
 ping and remote lists in order, live gossips with infection periods and infected sets, and every
 SequenceIdCollector.  Events (canonical order) and counters are compared at the end.
 """
+import dataclasses
+
 import numpy as np
 import pytest
 
@@ -88,3 +90,20 @@ def test_gpu_parity_config2_1024(glib, olib):
     rem = events[(events["type"] == abi.EV_REMOVED) & (events["subject"] == 17)]
     assert sorted(set(rem["viewer"].tolist())) == [v for v in range(1024) if v != 17]
     assert len(rem) == 1023
+
+
+# ---- the sharded path: the cluster's rows split over 2 / 3 shards that exchange
+# GOSSIP_REQ / SYNC / SYNC_ACK traffic exactly as the RCCL ranks do (cfg.local_shards), compared with
+# the UNSHARDED oracle: sharding must not change a single bit.  3 shards over 4 members leaves the
+# last shard empty; over 3 members every shard owns one row.
+@pytest.mark.parametrize("shards", [2, 3])
+@pytest.mark.parametrize("sc", scenarios.catalog(), ids=lambda s: s.name)
+def test_gpu_sharded_parity_scenario(glib, olib, sc, shards):
+    _run_parity(glib, olib, dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": shards}))
+
+
+def test_gpu_sharded_parity_config2_1024(glib, olib):
+    sc = scenarios.config2()
+    sc = dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": 4})
+    members = list(range(0, 1024, 37)) + [17, 18, 255, 256, 1023]
+    _run_parity(glib, olib, sc, members=members, collectors=False)
