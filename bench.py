@@ -115,10 +115,11 @@ def main():
     cfg = make_config(lib, local_rank)
     cfg.gossip_capacity = args.gossip_capacity
     cfg.local_shards = args.local_shards
+    se = None
     if world > 1:
-        obj = [abi.comm_unique_id(lib) if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        e = abi.Engine(lib, cfg, n, n, 1, rank=rank, world=world, comm_id=obj[0])
+        from swimgpu.dist import ShardedEngine
+        se = ShardedEngine(lib, cfg, n, n, 1)
+        e = se.engine
     else:
         e = abi.Engine(lib, cfg, n, n, 1)
 
@@ -141,16 +142,12 @@ def main():
     prof = e.profile_merge()
     stats = e.stats()
     e.drain_events()
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        keys = ("syncs", "sync_records", "gossip_messages", "gossips_created", "pings", "timers_fired", "events")
-        st = torch.tensor([float(stats[k]) for k in keys] + [float(prof["alg_bytes"]), prof["total_ms"],
-                                                             float(prof["launches"])], dtype=torch.float64)
+    if se is not None:
+        dt = se.max_time(dt)
+        stats = se.stats()
+        st = torch.tensor([float(prof["alg_bytes"]), prof["total_ms"], float(prof["launches"])], dtype=torch.float64)
         dist.all_reduce(st, op=dist.ReduceOp.SUM)
-        stats.update({k: int(v) for k, v in zip(keys, st[:len(keys)].tolist())})
-        prof = {"alg_bytes": st[-3].item(), "total_ms": st[-2].item(), "launches": int(st[-1].item())}
+        prof = {"alg_bytes": st[0].item(), "total_ms": st[1].item(), "launches": int(st[2].item())}
     if stats["capacity_errors"]:
         raise SystemExit(f"capacity error during the benchmark: {stats['capacity_errors']:#x}")
 

@@ -591,7 +591,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.chunks = (n + SYNC_CHUNK - 1) / SYNC_CHUNK;
   b.pool_cap = std::max<uint32_t>(1u << 22, 16 * n);
   const bool multi = e->world > 1;
-  b.tx_msg_cap = multi ? b.msg_cap : 0;
+  // tx capacities must be identical on every rank: both ends of a send clamp the count with them
+  b.tx_msg_cap = multi ? (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 256ull * e->sz)) : 0;
   b.tx_req_cap = multi ? b.req_cap : 0;
   b.tx_stop_cap = multi ? kStopCap : 0;
 
