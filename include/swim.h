@@ -289,10 +289,12 @@ int32_t swim_read_collector(swim_engine* e, uint32_t m, uint32_t gossiper, swim_
                             uint32_t cap, uint32_t* len);
 
 /* ---- measurement ---------------------------------------------------------------------------
- * Per-kernel timing of the SYNC row-merge kernel (the dominant HBM stream), measured with HIP
- * events recorded around every launch on the engine's own stream.  `alg_bytes` counts algorithmic
- * bytes: per merged SYNC / SYNC_ACK message the content row and the receiver row (2 x N x 8 B) plus
- * 8 B per record that changed the receiver's table.  enable = 0 stops recording; enable = 1
+ * Per-kernel timing of the SYNC classification kernel (k_sync_classify, the dominant HBM stream),
+ * measured with HIP events recorded on the engine's own stream around one launch in seven (an event
+ * pair drains the stream, so timing every launch would distort the run being measured).  For those
+ * sampled launches: `launches`, `total_ms`, `messages` / `records` they processed, and `alg_bytes`:
+ * per merged SYNC / SYNC_ACK message the record words of the content row and of the receiver row
+ * (2 x N x 4 B) plus 4 B per record routed to the sequential merge.  enable = 0 stops recording; enable = 1
  * (re)starts it from zero.  The CPU oracle reports zeros. */
 typedef struct swim_kernel_profile {
   uint64_t launches;

@@ -29,9 +29,10 @@ using namespace swimdev;
 namespace {
 
 constexpr uint32_t kDrainEvery = 256;
-constexpr uint32_t kClassifyGrid = 2048;  // grid-stride over (message, chunk) work units
+constexpr uint32_t kClassifyGrid = 1024;  // 4,096 waves: the resident capacity at 110 VGPRs (4 waves / SIMD)
 constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
 constexpr uint32_t kStopCap = 4096;
+constexpr uint32_t kProfEvery = 7;  // odd: samples alternate between the SYNC and SYNC_ACK launches
 
 uint32_t gcd_u(uint32_t a, uint32_t b) {
   while (b) { uint32_t t = a % b; a = b; b = t; }
@@ -68,18 +69,20 @@ struct Shard {
   // received cross-shard traffic (grown on demand; sizes are known on the host before each copy)
   GMsgFull* rx_msgs = nullptr;
   SyncReq* rx_reqs = nullptr;
-  uint64_t* rx_rows = nullptr;
+  uint32_t* rx_rows = nullptr;
   uint32_t* rx_stops = nullptr;
-  uint64_t* tx_rows = nullptr;
+  uint32_t* tx_rows = nullptr;
   size_t rx_msg_cap = 0, rx_req_cap = 0, rx_row_cap = 0, tx_row_cap = 0, rx_stop_cap = 0;
   uint32_t n_rx_msgs = 0, n_rx_reqs = 0, n_rx_stops = 0;
   uint32_t links_dev_cap = 0;
   // swim_profile_*: HIP events around every k_sync_classify launch on the engine's stream
   std::vector<hipEvent_t> prof_ev;
   uint32_t prof_used = 0;
+  uint64_t prof_seen = 0;  // classify launches since profiling was enabled
+  unsigned long long* prof_slots = nullptr;  // per sampled launch: {messages, complex records}
   double prof_ms = 0;
+  unsigned long long prof_msgs = 0, prof_recs = 0;
   uint64_t prof_launches = 0;
-  unsigned long long prof_base_msgs = 0, prof_base_recs = 0;
 
   template <typename T>
   bool alloc(T** p, size_t count) {
@@ -177,18 +180,26 @@ static int32_t read_stats(swim_engine* e, unsigned long long* st) {
 }
 
 static void prof_flush(Shard& s) {
+  if (!s.prof_used) return;
+  std::vector<unsigned long long> slots(2 * (size_t)s.prof_used);
+  hipMemcpy(slots.data(), s.prof_slots, sizeof(unsigned long long) * slots.size(), hipMemcpyDeviceToHost);
+  hipMemset(s.prof_slots, 0, sizeof(unsigned long long) * slots.size());
   for (uint32_t i = 0; i < s.prof_used; ++i) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, s.prof_ev[2 * i], s.prof_ev[2 * i + 1]) == hipSuccess) s.prof_ms += ms;
+    s.prof_msgs += slots[2 * i];
+    s.prof_recs += slots[2 * i + 1];
   }
   s.prof_launches += s.prof_used;
   s.prof_used = 0;
 }
 
+// HIP events are recorded around one classify launch in kProfEvery: an event pair drains the
+// stream (measured ~6 us bubble each side), so timing every launch would distort the timed region
 static void launch_classify(swim_engine* e, Shard& s, int d2) {
-  const bool p = e->prof && 2 * (s.prof_used + 1) <= s.prof_ev.size();
+  const bool p = e->prof && (s.prof_seen++ % kProfEvery) == 0 && 2 * (s.prof_used + 1) <= s.prof_ev.size();
   if (p) hipEventRecord(s.prof_ev[2 * s.prof_used], e->stream);
-  k_sync_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(s.c, s.b, d2);
+  k_sync_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(s.c, s.b, d2, p ? s.prof_slots + 2 * s.prof_used : nullptr);
   if (p) {
     hipEventRecord(s.prof_ev[2 * s.prof_used + 1], e->stream);
     s.prof_used++;
@@ -338,7 +349,7 @@ static int32_t exchange_sync(swim_engine* e, int kind) {
   Counts ct;
   if (int32_t rc = read_counts(e, kind, &ct)) return rc;
   const uint32_t W = (uint32_t)e->world;
-  const size_t row_bytes = (size_t)e->n * 8;
+  const size_t row_bytes = (size_t)e->n * 4;  // a SYNC carries the record words of a row
   hipStream_t s = e->stream;
   if (e->rccl) {
     Shard& sd = e->sh[0];
@@ -539,9 +550,9 @@ static int32_t set_replicated(swim_engine* e, size_t field_off, uint32_t m, uint
 __global__ void k_leave(Ctx c, uint32_t v, int32_t stop_after) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   MemberDev& m = mem(c, v);
-  uint64_t* cp = row(c, v) + v;
-  int32_t inc = c_inc(*cp) + 1;
-  *cp = c_with_record(*cp, SWIM_LEAVING, inc);
+  const uint64_t cell = cell_get(c, v, v);
+  const int32_t inc = c_inc(cell) + 1;
+  cell_put(c, v, v, c_with_record(cell, SWIM_LEAVING, inc));
   spread_gossip(c, v, v, SWIM_LEAVING, inc);
   if (stop_after) {
     m.leave_pending = 1;
@@ -597,7 +608,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.tx_stop_cap = multi ? kStopCap : 0;
 
   const size_t nn = (size_t)nl * n;
-  bool ok = sd.alloc(&c.cells, nn) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
+  bool ok = sd.alloc(&c.recs, nn) && sd.alloc(&c.aux, nn) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
             sd.alloc(&c.remote, nn) && sd.alloc(&c.slab, (size_t)nl * c.gcap) && sd.alloc(&c.coll, (size_t)nl * c.hcap) &&
             sd.alloc(&c.fd_sync, (size_t)nl * FD_SYNC_MAX) &&
             sd.alloc(&c.wheel, (size_t)(c.wheel_mask + 1) * c.wheel_cap) && sd.alloc(&c.wheel_cnt, c.wheel_mask + 1) &&
@@ -965,8 +976,16 @@ int32_t swim_read_view(swim_engine* e, uint32_t v, uint64_t* out) {
   Shard* sd = e->owner_of(v);
   if (!sd) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  return hipMemcpy(out, sd->c.cells + (size_t)(v - sd->c.lo) * e->n, 8 * (size_t)e->n, hipMemcpyDeviceToHost) == hipSuccess
-             ? SWIM_OK : SWIM_EDEVICE;
+  // compose the swim.h packed cells from the split record / aux words (swim_device.h)
+  std::vector<uint32_t> r(e->n), a(e->n);
+  const size_t off = (size_t)(v - sd->c.lo) * e->n;
+  if (hipMemcpy(r.data(), sd->c.recs + off, 4 * (size_t)e->n, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(a.data(), sd->c.aux + off, 4 * (size_t)e->n, hipMemcpyDeviceToHost) != hipSuccess)
+    return SWIM_EDEVICE;
+  for (uint32_t x = 0; x < e->n; ++x)
+    out[x] = (uint64_t)(r[x] & REC_INC_MASK) | ((uint64_t)((r[x] >> 29) & 3u) << 32) | ((uint64_t)(r[x] >> 31) << 34) |
+             ((uint64_t)(a[x] & 0xfu) << 35) | ((uint64_t)(a[x] >> 4) << 39);
+  return SWIM_OK;
 }
 
 int32_t swim_drain_events(swim_engine* e, swim_event* out, size_t cap, size_t* n_out) {
@@ -1132,15 +1151,15 @@ int32_t swim_profile_enable(swim_engine* e, int32_t enable) {
       sd.prof_ev.resize(4 * kDrainEvery + 4);
       for (auto& ev : sd.prof_ev)
         if (hipEventCreate(&ev) != hipSuccess) return SWIM_EDEVICE;
+      if (!sd.alloc(&sd.prof_slots, sd.prof_ev.size())) return SWIM_ENOMEM;
     }
+    hipMemset(sd.prof_slots, 0, sizeof(unsigned long long) * sd.prof_ev.size());
     sd.prof_used = 0;
+    sd.prof_seen = 0;
     sd.prof_ms = 0;
     sd.prof_launches = 0;
+    sd.prof_msgs = sd.prof_recs = 0;
   }
-  unsigned long long st[ST_COUNT];
-  if (read_stats(e, st) != SWIM_OK) return SWIM_EDEVICE;
-  e->sh[0].prof_base_msgs = st[ST_MERGE_MSGS];
-  e->sh[0].prof_base_recs = st[ST_MERGE_RECORDS];
   e->prof = enable != 0;
   return SWIM_OK;
 }
@@ -1148,18 +1167,15 @@ int32_t swim_profile_enable(swim_engine* e, int32_t enable) {
 int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out) {
   if (!e || !out) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  out->launches = 0;
-  out->total_ms = 0;
+  std::memset(out, 0, sizeof(*out));
   for (Shard& sd : e->sh) {
     prof_flush(sd);
     out->launches += sd.prof_launches;
     out->total_ms += sd.prof_ms;
+    out->messages += sd.prof_msgs;
+    out->records += sd.prof_recs;
   }
-  unsigned long long st[ST_COUNT];
-  if (read_stats(e, st) != SWIM_OK) return SWIM_EDEVICE;
-  out->messages = st[ST_MERGE_MSGS] - e->sh[0].prof_base_msgs;
-  out->records = st[ST_MERGE_RECORDS] - e->sh[0].prof_base_recs;
-  out->alg_bytes = out->messages * (uint64_t)e->n * 16ull + out->records * 8ull;
+  out->alg_bytes = out->messages * (uint64_t)e->n * 8ull + out->records * 4ull;
   return SWIM_OK;
 }
 

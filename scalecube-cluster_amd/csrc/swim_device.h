@@ -29,7 +29,7 @@ constexpr int FD_SYNC_MAX = 33;  // FD-triggered SYNCs per member per tick (<= 2
 enum : uint32_t {
   ERR_SLAB = 1u << 0, ERR_INTERVALS = 1u << 1, ERR_HASH = 1u << 2, ERR_WHEEL = 1u << 3,
   ERR_EVENTS = 1u << 4, ERR_MSGS = 1u << 5, ERR_SNAP = 1u << 6, ERR_INFECTED = 1u << 7,
-  ERR_FDSYNC = 1u << 8, ERR_INS = 1u << 9, ERR_REQS = 1u << 10, ERR_PEND = 1u << 11,
+  ERR_FDSYNC = 1u << 8, ERR_INS = 1u << 9, ERR_REQS = 1u << 10, ERR_PEND = 1u << 11, ERR_INC = 1u << 12,
 };
 
 // stats slots (swim_stats order)
@@ -89,7 +89,8 @@ struct SyncReq {  // SYNC (request) or SYNC_ACK
   uint32_t from, to, ordinal, slot;
   uint32_t flags;    // bit0 initial, bit1 outfail, bit2 delivered
   uint32_t content;  // NONE: `from` is owned here (row / snapshot); else index into the received rows
-  uint32_t pad[2];
+  uint32_t snap;     // k_sync_prep: snapshot slot of `from`'s row in this sub-phase, or NONE
+  uint32_t pad;
 };
 
 struct InsOp {  // deferred pingMembers.add(nextInt(size), member) of an ADDED event
@@ -106,7 +107,9 @@ struct Ctx {
   int32_t ping_interval, suspicion_mult, repeat_mult, fanout, ping_req_members, seg_threshold, record_fd;
   uint32_t key0, key1;
   uint64_t T;
-  uint64_t* cells;
+  // the view cell of (viewer, subject) is stored split in two u32 words (layout below)
+  uint32_t* recs;  // [nl][n] MembershipRecord: what SYNC carries and the merge filter reads
+  uint32_t* aux;   // [nl][n] the viewer-local side maps (members / aliveEmitted / metadata / timer)
   MemberDev* mem;
   uint8_t* up;  // replicated: member's transport is running
   uint32_t* ping;
@@ -195,7 +198,35 @@ __device__ __forceinline__ uint64_t c_with_record(uint64_t c, uint32_t st, int32
 __device__ __forceinline__ uint64_t c_with_deadline(uint64_t c, uint64_t tick) {
   return (c & ((1ull << 39) - 1)) | ((tick & SWIM_DEADLINE_MASK) << 39);
 }
-__device__ __forceinline__ uint64_t* row(const Ctx& c, uint32_t v) { return c.cells + (size_t)(v - c.lo) * c.n; }
+__device__ __forceinline__ void set_err(const Ctx& c, uint32_t bit) { atomicOr(c.err, bit); }
+
+// ---- split cell storage.  The swim.h packed u64 cell stays the logical format
+// (cell_get / cell_put); the hot SYNC stream touches only the record words.
+//   rec: bits 0..28 incarnation (0 .. 2^29-2, else ERR_INC), 29..30 status, 31 in_table
+//   aux: bit 0 in_members, 1 alive_emitted, 2 has_timer, 3 has_metadata, 4..28 timer deadline
+constexpr uint32_t REC_INC_MASK = 0x1fffffffu;
+constexpr uint32_t REC_IN_TABLE = 0x80000000u;
+constexpr uint32_t A_IN_MEMBERS = 1u, A_ALIVE_EMITTED = 2u, A_HAS_TIMER = 4u, A_HAS_METADATA = 8u;
+__device__ __forceinline__ int32_t r_inc(uint32_t r) { return (int32_t)(r & REC_INC_MASK); }
+__device__ __forceinline__ uint32_t r_status(uint32_t r) { return (r >> 29) & 3u; }
+__device__ __forceinline__ bool r_in_table(uint32_t r) { return (r & REC_IN_TABLE) != 0; }
+__device__ __forceinline__ uint32_t* rec_row(const Ctx& c, uint32_t v) { return c.recs + (size_t)(v - c.lo) * c.n; }
+__device__ __forceinline__ uint32_t* aux_row(const Ctx& c, uint32_t v) { return c.aux + (size_t)(v - c.lo) * c.n; }
+__device__ __forceinline__ uint64_t compose_cell(uint32_t r, uint32_t a) {
+  return (uint64_t)(r & REC_INC_MASK) | ((uint64_t)r_status(r) << 32) | ((uint64_t)(r >> 31) << 34) |
+         ((uint64_t)(a & 0xfu) << 35) | ((uint64_t)(a >> 4) << 39);
+}
+__device__ __forceinline__ uint64_t cell_get(const Ctx& c, uint32_t v, uint32_t s) {
+  const size_t i = (size_t)(v - c.lo) * c.n + s;
+  return compose_cell(c.recs[i], c.aux[i]);
+}
+__device__ __forceinline__ void cell_put(const Ctx& c, uint32_t v, uint32_t s, uint64_t cell) {
+  const size_t i = (size_t)(v - c.lo) * c.n + s;
+  const uint32_t inc = (uint32_t)cell;
+  if (inc >= REC_INC_MASK) set_err(c, ERR_INC);
+  c.recs[i] = (inc & REC_INC_MASK) | ((uint32_t)((cell >> 32) & 3u) << 29) | ((uint32_t)((cell >> 34) & 1u) << 31);
+  c.aux[i] = (uint32_t)((cell >> 35) & 0xfu) | ((uint32_t)((cell >> 39) & SWIM_DEADLINE_MASK) << 4);
+}
 __device__ __forceinline__ MemberDev& mem(const Ctx& c, uint32_t v) { return c.mem[v - c.lo]; }
 __device__ __forceinline__ uint32_t* ping_list(const Ctx& c, uint32_t v) { return c.ping + (size_t)(v - c.lo) * c.n; }
 __device__ __forceinline__ uint32_t* remote_list(const Ctx& c, uint32_t v) { return c.remote + (size_t)(v - c.lo) * c.n; }
@@ -203,7 +234,6 @@ __device__ __forceinline__ GossipDev* slab_of(const Ctx& c, uint32_t v) { return
 __device__ __forceinline__ bool owned(const Ctx& c, uint32_t v) { return v - c.lo < c.nl; }
 __device__ __forceinline__ uint32_t owner(const Ctx& c, uint32_t v) { return v / c.sz; }
 
-__device__ __forceinline__ void set_err(const Ctx& c, uint32_t bit) { atomicOr(c.err, bit); }
 // Counters are replicated ST_REPL times (summed on readback) so that thousands of workgroups never
 // serialise on one address (MI355X_MICROARCH.md: one contended address is ~14x slower).
 constexpr int ST_REPL = 64;
@@ -422,12 +452,12 @@ __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject,
 // scheduleSuspicionTimeoutTask (MembershipProtocolImpl.java:805-823)
 __device__ __forceinline__ int32_t ceil_log2(uint32_t x) { return x ? 32 - __clz(x) : 0; }
 __device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
-  uint64_t* cp = row(c, v) + s;
-  uint64_t cell = *cp;
-  if (c_has(cell, B_HAS_TIMER)) return;
+  uint32_t* ap = aux_row(c, v) + s;
+  const uint32_t a = *ap;
+  if (a & A_HAS_TIMER) return;
   uint64_t ms = (uint64_t)c.suspicion_mult * (uint64_t)ceil_log2(mem(c, v).table_size) * (uint64_t)c.ping_interval;
   uint64_t deadline = c.T + ms / c.tick_ms;
-  *cp = c_with_deadline(cell | B_HAS_TIMER, deadline);
+  *ap = (a & 0xfu) | A_HAS_TIMER | ((uint32_t)(deadline & SWIM_DEADLINE_MASK) << 4);
   uint32_t b = (uint32_t)(deadline & c.wheel_mask);
   uint32_t i = atomicAdd(&c.wheel_cnt[b], 1u);
   if (i >= c.wheel_cap) { set_err(c, ERR_WHEEL); return; }
@@ -451,8 +481,7 @@ __device__ inline bool fetch_ok(const Ctx& c, uint32_t v, uint32_t s, uint32_t p
 __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, uint32_t st1, int32_t inc1,
                                          int reason, uint32_t phase) {
   MemberDev& m = mem(c, v);
-  uint64_t* cp = row(c, v) + s;
-  uint64_t cell = *cp;
+  uint64_t cell = cell_get(c, v, s);
   const bool present = c_has(cell, B_IN_TABLE);
   const uint32_t st0 = c_status(cell);
   const int32_t inc0 = c_inc(cell);
@@ -461,14 +490,14 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
 
   if (s == v) {  // onSelfMemberDetected (:686-708)
     int32_t cur = inc0 > inc1 ? inc0 : inc1;
-    *cp = c_with_record(cell, st0, cur + 1);
+    cell_put(c, v, s, c_with_record(cell, st0, cur + 1));
     spread_gossip(c, v, v, st0, cur + 1);
     return false;
   }
   if (st1 == SWIM_LEAVING) {  // onLeavingDetected (:710-733)
     if (!present) m.table_size++;
     cell = c_with_record(cell | B_IN_TABLE, SWIM_LEAVING, inc1);
-    *cp = cell;
+    cell_put(c, v, s, cell);
     if (present && (st0 == SWIM_ALIVE || (st0 == SWIM_SUSPECT && c_has(cell, B_ALIVE_EMITTED))))
       publish_event(c, v, s, SWIM_EV_LEAVING, phase, next_minor(c, v, phase, s));
     if (!present || st0 != SWIM_LEAVING) {
@@ -479,8 +508,8 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
   }
   if (st1 == SWIM_DEAD) {  // onDeadMemberDetected (:740-767)
     cell &= ~B_HAS_TIMER;
-    if (!c_has(cell, B_IN_MEMBERS)) { *cp = cell; return false; }
-    *cp = 0;
+    if (!c_has(cell, B_IN_MEMBERS)) { cell_put(c, v, s, cell); return false; }
+    cell_put(c, v, s, 0);
     atomicSub(&m.table_size, 1u);  // atomic: timer buckets are processed entry-parallel
     atomicSub(&m.members_size, 1u);
     publish_event(c, v, s, SWIM_EV_REMOVED, phase, next_minor(c, v, phase, s));
@@ -489,7 +518,7 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
   if (st1 == SWIM_SUSPECT) {  // :621-628
     if (!r0_leaving) {
       if (!present) m.table_size++;
-      *cp = c_with_record(cell | B_IN_TABLE, SWIM_SUSPECT, inc1);
+      cell_put(c, v, s, c_with_record(cell | B_IN_TABLE, SWIM_SUSPECT, inc1));
     }
     schedule_timer(c, v, s);
     if (reason != R_GOSSIP && reason != R_INITIAL_SYNC) spread_gossip(c, v, s, SWIM_SUSPECT, inc1);
@@ -500,11 +529,11 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
     if (!c_has(cell, B_IN_MEMBERS)) { cell |= B_IN_MEMBERS; m.members_size++; }
     if (!c_has(cell, B_ALIVE_EMITTED)) {
       cell |= B_ALIVE_EMITTED;
-      *cp = cell;
+      cell_put(c, v, s, cell);
       publish_event(c, v, s, SWIM_EV_ADDED, phase, next_minor(c, v, phase, s));
       publish_event(c, v, s, SWIM_EV_LEAVING, phase, next_minor(c, v, phase, s));
     } else {
-      *cp = cell;
+      cell_put(c, v, s, cell);
     }
     return false;
   }
@@ -515,16 +544,15 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
 // doOnSuccess of the metadata fetch (:648-656) + onAliveMemberDetected (:769-795)
 __device__ inline void apply_alive(const Ctx& c, uint32_t v, uint32_t s, int32_t inc1, int reason, uint32_t phase) {
   MemberDev& m = mem(c, v);
-  uint64_t* cp = row(c, v) + s;
-  *cp &= ~B_HAS_TIMER;  // cancelSuspicionTimeoutTask
+  // cancelSuspicionTimeoutTask
+  uint64_t cell = (cell_get(c, v, s) & ~B_HAS_TIMER) | B_HAS_METADATA;
   if (reason != R_GOSSIP && reason != R_INITIAL_SYNC) spread_gossip(c, v, s, SWIM_ALIVE, inc1);
-  uint64_t cell = *cp | B_HAS_METADATA;
   const bool exists = c_has(cell, B_IN_MEMBERS);
   if (!c_has(cell, B_IN_TABLE)) m.table_size++;
   if (!exists) m.members_size++;
   cell = c_with_record(cell | B_IN_TABLE | B_IN_MEMBERS, SWIM_ALIVE, inc1);
   if (!exists) cell |= B_ALIVE_EMITTED;
-  *cp = cell;
+  cell_put(c, v, s, cell);
   if (!exists) publish_event(c, v, s, SWIM_EV_ADDED, phase, next_minor(c, v, phase, s));
 }
 

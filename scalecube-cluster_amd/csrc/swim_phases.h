@@ -47,7 +47,7 @@ struct Bufs {
   uint32_t tx_stop_cap;
   const GMsgFull* rx_msgs;
   const SyncReq* rx_reqs;
-  const uint64_t* rx_rows;  // content rows of received SYNC / SYNC_ACKs, indexed by SyncReq.content
+  const uint32_t* rx_rows;  // record rows of received SYNC / SYNC_ACKs, indexed by SyncReq.content
   const uint32_t* rx_stops;
   GMsgFull* msgs;      // produced in emit order
   GMsgFull* msgs_out;  // grouped by receiver
@@ -68,7 +68,7 @@ struct Bufs {
   uint32_t* ack_recv;
   InsOp* ins_out;
   uint32_t* ins_start;
-  uint64_t* snap;       // snapshot rows
+  uint32_t* snap;       // snapshot record rows
   uint32_t snap_cap;
   uint32_t* snap_idx;   // per member: slot or NONE
   uint32_t* snap_list;
@@ -83,12 +83,16 @@ struct Bufs {
 
 // ------------------------------------------------------------------------------- init
 __global__ void k_init_rows(Ctx c, uint32_t n_initial) {
-  const uint64_t conv = B_IN_TABLE | B_IN_MEMBERS | B_ALIVE_EMITTED | B_HAS_METADATA;
+  const uint32_t conv_aux = A_IN_MEMBERS | A_ALIVE_EMITTED | A_HAS_METADATA;
   for (uint32_t v = c.lo + blockIdx.x; v < c.lo + c.nl; v += gridDim.x) {
-    uint64_t* r = row(c, v);
+    uint32_t* r = rec_row(c, v);
+    uint32_t* a = aux_row(c, v);
     const bool init = v < n_initial;
-    for (uint32_t s = threadIdx.x; s < c.n; s += blockDim.x)
-      r[s] = (init && s < n_initial) ? (s == v ? (B_IN_TABLE | B_IN_MEMBERS) : conv) : 0ull;
+    for (uint32_t s = threadIdx.x; s < c.n; s += blockDim.x) {
+      const bool in = init && s < n_initial;
+      r[s] = in ? REC_IN_TABLE : 0u;  // ALIVE, incarnation 0
+      a[s] = in ? (s == v ? A_IN_MEMBERS : conv_aux) : 0u;
+    }
   }
 }
 
@@ -166,7 +170,7 @@ __global__ void k_start_joins(Ctx c) {
   m.join_now = 1;
   m.fd_start = (int64_t)c.T;
   m.g_start = (int64_t)c.T;
-  row(c, v)[v] = B_IN_TABLE | B_IN_MEMBERS;
+  cell_put(c, v, v, B_IN_TABLE | B_IN_MEMBERS);
   m.table_size = 1;
   m.members_size = 1;
 }
@@ -184,17 +188,18 @@ __global__ void k_timers(Ctx c, uint32_t bucket) {
     uint64_t e = ent[i];
     uint32_t v = (uint32_t)(e >> 32), s = (uint32_t)e;
     if (!c.up[v]) continue;
-    unsigned long long* cp = (unsigned long long*)(row(c, v) + s);
-    unsigned long long old = *cp;
+    uint32_t* ap = aux_row(c, v) + s;
+    uint32_t old = *ap;
     bool claimed = false;
-    while (c_has(old, B_HAS_TIMER) && c_deadline(old) == tmask) {
-      unsigned long long prev = atomicCAS(cp, old, old & ~B_HAS_TIMER);
+    while ((old & A_HAS_TIMER) && (old >> 4) == tmask) {
+      const uint32_t prev = atomicCAS(ap, old, old & ~A_HAS_TIMER);
       if (prev == old) { claimed = true; break; }
       old = prev;
     }
     if (!claimed) continue;
     fired++;
-    if (c_has(old, B_IN_TABLE)) update_membership(c, v, s, SWIM_DEAD, c_inc(old), R_TIMEOUT, SWIM_PHASE_TIMERS);
+    const uint32_t r = rec_row(c, v)[s];
+    if (r_in_table(r)) update_membership(c, v, s, SWIM_DEAD, r_inc(r), R_TIMEOUT, SWIM_PHASE_TIMERS);
   }
   wave_stat_add(c, ST_TIMERS_FIRED, fired);
 }
@@ -205,12 +210,12 @@ __global__ void k_timers(Ctx c, uint32_t bucket) {
 template <int BLOCK>
 __device__ void compact_list(const Ctx& c, uint32_t v, uint32_t* list, uint32_t& len) {
   __shared__ uint32_t s_wave[BLOCK / 64 + 1];
-  const uint64_t* r = row(c, v);
+  const uint32_t* a = aux_row(c, v);
   uint32_t out = 0;
   for (uint32_t base = 0; base < len; base += BLOCK) {
     uint32_t i = base + threadIdx.x;
     uint32_t val = 0, keep = 0;
-    if (i < len) { val = list[i]; keep = c_has(r[val], B_IN_MEMBERS) ? 1u : 0u; }
+    if (i < len) { val = list[i]; keep = (a[val] & A_IN_MEMBERS) ? 1u : 0u; }
     uint32_t total;
     uint32_t pos = block_exclusive_scan<BLOCK>(keep, s_wave, &total);
     if (keep) list[out + pos] = val;
@@ -242,7 +247,7 @@ __device__ inline void publish_fd(const Ctx& c, uint32_t v, uint32_t t, uint32_t
   if (c.record_fd)
     emit(c, v, t, SWIM_EV_FD_ALIVE + (status == SWIM_ALIVE ? 0 : status == SWIM_SUSPECT ? 1 : 2), SWIM_PHASE_FD,
          m.ev_minor++);
-  uint64_t cell = row(c, v)[t];
+  const uint64_t cell = cell_get(c, v, t);
   if (!c_has(cell, B_IN_TABLE)) return;
   if (c_status(cell) == status) return;
   if (status == SWIM_ALIVE) {
@@ -656,20 +661,20 @@ __global__ void __launch_bounds__(256) k_ins_apply(Ctx c, Bufs b) {
 // seeded rejection sampling.
 __device__ inline uint32_t select_sync_address(const Ctx& c, uint32_t v) {
   const MemberDev& m = mem(c, v);
-  const uint64_t* r = row(c, v);
+  const uint32_t* a = aux_row(c, v);
   uint32_t count = m.members_size - 1;
   for (uint32_t i = 0; i < c.n_seeds; ++i) {
     uint32_t s = c.seeds[i];
-    if (s != v && !c_has(r[s], B_IN_MEMBERS)) count++;
+    if (s != v && !(a[s] & A_IN_MEMBERS)) count++;
   }
   if (count == 0) return NONE;
   for (uint32_t i = 0; i < SWIM_SYNC_SELECT_ATTEMPTS; ++i) {
     uint32_t x = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 0, i), c.n);
-    if (x != v && (c_has(r[x], B_IN_MEMBERS) || c.is_seed[x])) return x;
+    if (x != v && ((a[x] & A_IN_MEMBERS) || c.is_seed[x])) return x;
   }
   uint32_t k = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 1, 0), count);
   for (uint32_t x = 0; x < c.n; ++x)
-    if (x != v && (c_has(r[x], B_IN_MEMBERS) || c.is_seed[x])) {
+    if (x != v && ((a[x] & A_IN_MEMBERS) || c.is_seed[x])) {
       if (k == 0) return x;
       --k;
     }
@@ -692,7 +697,7 @@ __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t
   MemberDev& m = mem(c, v);
   SyncReq q;
   q.from = v; q.to = to; q.ordinal = ordinal; q.slot = 0; q.flags = initial ? RQ_INITIAL : 0;
-  q.content = NONE; q.pad[0] = q.pad[1] = 0;
+  q.content = NONE; q.snap = NONE; q.pad = 0;
   if (initial) m.init_total++;
   if (out_fail(c, v, to, v, SWIM_STREAM_SYNC_OUT, ordinal, 0)) {
     if (initial) m.init_done++;

@@ -7,8 +7,9 @@
 //
 //   k_sync_prep      one workgroup: group delivered messages by receiver, canonical inbox order,
 //                    snapshot claims for rows that are both read and merged into in this sub-phase
-//   k_sync_classify  the HBM stream: one 256-thread workgroup per (message, 4,096-subject chunk),
-//                    16 consecutive subjects per thread with 16-B loads; a record is "complex" unless
+//   k_sync_classify  the HBM stream: one wave per (message, 1,024-subject chunk), 16 subjects per
+//                    lane as four 16-B loads of record words per row (content row + receiver row =
+//                    8 B per subject), software-pipelined across units; a record is "complex" unless
 //                    updateMembership would provably do nothing; complex subjects of a chunk are
 //                    block-scan compacted into a pool in subject order
 //   k_sync_apply     one workgroup per receiver: lane 0 runs the exact sequential updateMembership on
@@ -16,20 +17,20 @@
 //                    admissions whose metadata fetch succeeded; a later message to a receiver whose
 //                    row already changed this sub-phase is re-classified in-workgroup.
 
-constexpr int SYNC_CHUNK = 4096;
+constexpr int SYNC_CHUNK = 1024;                 // subjects per classify unit (one wave)
 constexpr int CLS_BLOCK = 256;
-constexpr int CLS_CPT = SYNC_CHUNK / CLS_BLOCK;  // 16 subjects per thread
+constexpr int CLS_LOADS = SYNC_CHUNK / 256;      // 16-B record loads per lane per row
 constexpr int APPLY_BLOCK = 256;
 constexpr int APPLY_CPT = 8;
 constexpr int APPLY_TILE = APPLY_BLOCK * APPLY_CPT;
 
-// true unless updateMembership(r1 = content cell) on row cell r0 provably changes nothing
-__device__ inline bool sync_complex(uint64_t r1, uint64_t r0, bool self) {
-  const uint32_t s1 = c_status(r1);
-  const int32_t i1 = c_inc(r1);
-  const bool p0 = c_has(r0, B_IN_TABLE);
-  const uint32_t s0 = c_status(r0);
-  const int32_t i0 = c_inc(r0);
+// true unless updateMembership(r1 = content record) on the row record r0 provably changes nothing
+__device__ inline bool sync_complex(uint32_t r1, uint32_t r0, bool self) {
+  const uint32_t s1 = r_status(r1);
+  const int32_t i1 = r_inc(r1);
+  const bool p0 = r_in_table(r0);
+  const uint32_t s0 = r_status(r0);
+  const int32_t i0 = r_inc(r0);
   const bool r0_leaving = p0 && s0 == SWIM_LEAVING;
   if (!r0_leaving && !is_overrides(s1, i1, p0, s0, i0)) return false;  // :593-602
   // an identical LEAVING record over a LEAVING row is a no-op put, except on the viewer's own row,
@@ -86,27 +87,28 @@ struct PackPlan {
   uint32_t cnt[MAXW];
   uint32_t off[MAXW];  // first packed row of destination d
 };
-__global__ void k_pack_rows(Ctx c, const SyncReq* tx, uint32_t tx_cap, PackPlan plan, uint64_t* out) {
+__global__ void k_pack_rows(Ctx c, const SyncReq* tx, uint32_t tx_cap, PackPlan plan, uint32_t* out) {
   for (uint32_t d = 0; d < c.world; ++d) {
     for (uint32_t k = blockIdx.x; k < plan.cnt[d]; k += gridDim.x) {
       const SyncReq q = tx[(size_t)d * tx_cap + k];
-      const uint64_t* src = row(c, q.from);
-      uint64_t* dst = out + (size_t)(plan.off[d] + k) * c.n;
-      if (c.n & 1) {  // rows are only 8-B aligned
+      const uint32_t* src = rec_row(c, q.from);
+      uint32_t* dst = out + (size_t)(plan.off[d] + k) * c.n;
+      if (c.n & 3) {  // rows are only 4-B aligned
         for (uint32_t x = threadIdx.x; x < c.n; x += blockDim.x) dst[x] = src[x];
       } else {
-        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src);
-        ulonglong2* d2 = reinterpret_cast<ulonglong2*>(dst);
-        for (uint32_t x = threadIdx.x; x < c.n / 2; x += blockDim.x) d2[x] = s2[x];
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        for (uint32_t x = threadIdx.x; x < c.n / 4; x += blockDim.x) d4[x] = s4[x];
       }
     }
   }
 }
 
-__device__ __forceinline__ const uint64_t* sync_content(const Ctx& c, const Bufs& b, const SyncReq& q) {
+// the record row a SYNC / SYNC_ACK carries: received copy, snapshot, or the sender's live row
+__device__ __forceinline__ const uint32_t* sync_content(const Ctx& c, const Bufs& b, const SyncReq& q) {
   if (q.content != NONE) return b.rx_rows + (size_t)q.content * c.n;
   const uint32_t si = b.snap_idx[q.from - c.lo];
-  return si < b.snap_cap ? b.snap + (size_t)si * c.n : row(c, q.from);
+  return si < b.snap_cap ? b.snap + (size_t)si * c.n : rec_row(c, q.from);
 }
 
 __global__ void __launch_bounds__(1024) k_sync_prep(Ctx c, Bufs b, int d2) {
@@ -152,114 +154,196 @@ __global__ void __launch_bounds__(1024) k_sync_prep(Ctx c, Bufs b, int d2) {
       b.snap_idx[sl] = slot;
     }
   }
+  __syncthreads();
+  __threadfence_block();
+  // every message records its sender's snapshot slot (classify reads it with the header)
+  for (uint32_t i = tid; i < ni; i += nt) {
+    SyncReq& q = p.out[i];
+    q.snap = q.content != NONE ? NONE : b.snap_idx[q.from - c.lo];
+  }
 }
 
-__global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(Ctx c, Bufs b, int d2) {
-  __shared__ uint32_t s_bits[SYNC_CHUNK / 32];
+// One (message, chunk) unit per wave: 64 lanes x 16 subjects = SYNC_CHUNK subjects, i.e. four
+// 16-B loads of record words per lane from the content row and four from the receiver row.  Each
+// wave owns a contiguous range of units, so consecutive units share the message header (loaded once
+// per message), and walks it with a one-deep software pipeline: the next unit's rows are in flight
+// while the current one is classified.  Complex subjects are compacted into the pool in subject
+// order with a ballot and a wave scan (no workgroup barriers).
+struct ClsHdr {
+  const uint32_t* content;
+  const uint32_t* rv;
+  uint32_t* snapdst;
+  uint32_t i, r;
+};
+
+__device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SubPhase& p, uint32_t i, ClsHdr& h) {
+  const SyncReq q = p.out[i];
+  const bool remote = q.content != NONE;
+  h.content = remote ? b.rx_rows + (size_t)q.content * c.n : rec_row(c, q.from);
+  h.rv = rec_row(c, q.to);
+  h.snapdst = q.snap < b.snap_cap ? b.snap + (size_t)q.snap * c.n : nullptr;
+  h.i = i;
+  h.r = q.to;
+}
+
+__device__ __forceinline__ void cls_rows(const Ctx& c, const ClsHdr& h, uint32_t ch, uint32_t lane, uint4* a, uint4* o) {
+  const uint32_t n = c.n, base = ch * SYNC_CHUNK;
+  const bool full = base + SYNC_CHUNK <= n && ((reinterpret_cast<uintptr_t>(h.content + base) |
+                                                reinterpret_cast<uintptr_t>(h.rv + base)) & 15) == 0;
+  if (full) {
+#pragma unroll
+    for (int j = 0; j < CLS_LOADS; ++j) a[j] = *reinterpret_cast<const uint4*>(h.content + base + j * 256 + 4 * lane);
+#pragma unroll
+    for (int j = 0; j < CLS_LOADS; ++j) o[j] = *reinterpret_cast<const uint4*>(h.rv + base + j * 256 + 4 * lane);
+    return;
+  }
+  // ragged tail of a row (N not a multiple of SYNC_CHUNK) or rows only 4-B aligned
+#pragma unroll
+  for (int j = 0; j < CLS_LOADS; ++j) {
+    uint32_t av[4], ov[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t x = base + j * 256 + 4 * lane + q;
+      av[q] = x < n ? h.content[x] : 0u;  // 0 = not in the table: never complex
+      ov[q] = x < n ? h.rv[x] : 0u;
+    }
+    a[j] = make_uint4(av[0], av[1], av[2], av[3]);
+    o[j] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+  }
+}
+
+// prof (profiled launches only): {messages merged, complex records} of this launch
+__global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(Ctx c, Bufs b, int d2, unsigned long long* prof) {
   const SubPhase p = sub_phase(b, d2);
   const uint32_t ni = *p.nitems;
   const uint32_t chunks = b.chunks, n = c.n;
-  unsigned long long recs = 0, msgs = 0, cplx = 0;
-  for (uint32_t w = blockIdx.x; w < ni * chunks; w += gridDim.x) {
-    const uint32_t i = w / chunks, ch = w - i * chunks;
-    const SyncReq q = p.out[i];
-    const uint32_t r = q.to, src = q.from;
-    const bool remote = q.content != NONE;
-    const uint64_t* __restrict__ content = remote ? b.rx_rows + (size_t)q.content * n : row(c, src);
-    const uint64_t* __restrict__ rv = row(c, r);
-    const uint32_t si = remote ? NONE : b.snap_idx[src - c.lo];
-    uint64_t* snapdst = si < b.snap_cap ? b.snap + (size_t)si * n : nullptr;
-    if (ch == 0) msgs++;
-    // coalesced: load j of lane t covers subjects base + j*512 + 2t, +1 (1 KiB per wave-instruction)
-    const uint32_t base = ch * SYNC_CHUNK;
-    uint32_t flags = 0;  // bit 2j+h = subject base + j*512 + 2*tid + h
-    if (base + SYNC_CHUNK <= n && ((reinterpret_cast<uintptr_t>(content + base) | reinterpret_cast<uintptr_t>(rv + base)) & 15) == 0) {
-      ulonglong2 a[CLS_CPT / 2], o[CLS_CPT / 2];
-#pragma unroll
-      for (int j = 0; j < CLS_CPT / 2; ++j)
-        a[j] = *reinterpret_cast<const ulonglong2*>(content + base + j * 2 * CLS_BLOCK + 2 * threadIdx.x);
-#pragma unroll
-      for (int j = 0; j < CLS_CPT / 2; ++j)
-        o[j] = *reinterpret_cast<const ulonglong2*>(rv + base + j * 2 * CLS_BLOCK + 2 * threadIdx.x);
-      if (snapdst) {
-#pragma unroll
-        for (int j = 0; j < CLS_CPT / 2; ++j)
-          *reinterpret_cast<ulonglong2*>(snapdst + base + j * 2 * CLS_BLOCK + 2 * threadIdx.x) = a[j];
-      }
-#pragma unroll
-      for (int j = 0; j < CLS_CPT / 2; ++j) {
-        const uint32_t x = base + j * 2 * CLS_BLOCK + 2 * threadIdx.x;
-        const bool r0 = c_has(a[j].x, B_IN_TABLE), r1 = c_has(a[j].y, B_IN_TABLE);
-        recs += (uint32_t)r0 + (uint32_t)r1;
-        if (r0 && sync_complex(a[j].x, o[j].x, x == r)) flags |= 1u << (2 * j);
-        if (r1 && sync_complex(a[j].y, o[j].y, x + 1 == r)) flags |= 1u << (2 * j + 1);
-      }
-    } else {
-      for (int j = 0; j < CLS_CPT / 2; ++j)
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t x = base + j * 2 * CLS_BLOCK + 2 * threadIdx.x + h;
-          if (x >= n) continue;
-          const uint64_t a = content[x];
-          if (snapdst) snapdst[x] = a;
-          if (c_has(a, B_IN_TABLE)) {
-            recs++;
-            if (sync_complex(a, rv[x], x == r)) flags |= 1u << (2 * j + h);
-          }
-        }
-    }
-    // almost every chunk has no record that can change the receiver: one barrier decides it
-    if (!__syncthreads_or(flags != 0)) {
-      if (threadIdx.x == 0) b.item_chunk[(size_t)i * chunks + ch] = make_uint2(0, 0);
-      continue;
-    }
-    // rare path: subject-ordered compaction through an LDS bitmap (bit x - base)
-    for (uint32_t wdx = threadIdx.x; wdx < SYNC_CHUNK / 32; wdx += CLS_BLOCK) s_bits[wdx] = 0;
-    __syncthreads();
-    for (int k = 0; k < CLS_CPT; ++k)
-      if (flags & (1u << k)) {
-        const uint32_t off = (k >> 1) * 2 * CLS_BLOCK + 2 * threadIdx.x + (k & 1);
-        atomicOr(&s_bits[off >> 5], 1u << (off & 31));
-      }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t total = 0;
-      for (uint32_t wdx = 0; wdx < SYNC_CHUNK / 32; ++wdx) total += __popc(s_bits[wdx]);
-      uint32_t pb = atomicAdd(&b.k->pool_cursor, total);
-      if (pb + total > b.pool_cap) {
-        set_err(c, ERR_PEND);
-        total = 0;
-      } else {
-        uint32_t o2 = pb;
-        for (uint32_t wdx = 0; wdx < SYNC_CHUNK / 32; ++wdx) {
-          uint32_t bits = s_bits[wdx];
-          while (bits) {
-            const uint32_t bit = __ffs(bits) - 1;
-            bits &= bits - 1;
-            b.pool[o2++] = base + wdx * 32 + bit;
-          }
-        }
-      }
-      b.item_chunk[(size_t)i * chunks + ch] = make_uint2(pb, total);
-      atomicAdd(&b.item_total[i], total);
-      cplx += total;
-    }
-    __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (CLS_BLOCK / 64) + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * (CLS_BLOCK / 64);
+  const uint64_t total = (uint64_t)ni * chunks;
+  const uint32_t u0 = (uint32_t)(total * wid / nw), u1 = (uint32_t)(total * (wid + 1) / nw);
+  unsigned long long recs = 0, cplx = 0;
+  __shared__ unsigned long long s_recs[CLS_BLOCK / 64];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    stat_add(c, ST_MERGE_MSGS, ni);
+    if (prof) prof[0] = ni;
   }
+  if (u0 < u1) {
+    ClsHdr hc, hn;
+    uint4 a[CLS_LOADS], o[CLS_LOADS], an[CLS_LOADS], on[CLS_LOADS];
+    cls_hdr(c, b, p, u0 / chunks, hc);
+    cls_rows(c, hc, u0 - hc.i * chunks, lane, a, o);
+    hn = hc;
+    for (uint32_t u = u0; u < u1; ++u) {
+      const uint32_t ch = u - hc.i * chunks;
+      const bool more = u + 1 < u1;
+      if (more) {
+        const uint32_t i2 = (u + 1) / chunks;
+        if (i2 != hn.i) cls_hdr(c, b, p, i2, hn);
+        cls_rows(c, hn, u + 1 - i2 * chunks, lane, an, on);
+      }
+      const uint32_t base = ch * SYNC_CHUNK;
+      if (hc.snapdst) {
+#pragma unroll
+        for (int j = 0; j < CLS_LOADS; ++j) {
+          const uint32_t av[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t x = base + j * 256 + 4 * lane + q;
+            if (x < n) hc.snapdst[x] = av[q];
+          }
+        }
+      }
+      uint32_t flags = 0;  // bit 4j+q = subject base + j*256 + 4*lane + q
+      uint32_t diff = 0;
+#pragma unroll
+      for (int j = 0; j < CLS_LOADS; ++j) {
+        diff |= (a[j].x ^ o[j].x) | (a[j].y ^ o[j].y) | (a[j].z ^ o[j].z) | (a[j].w ^ o[j].w);
+        recs += (a[j].x >> 31) + (a[j].y >> 31) + (a[j].z >> 31) + (a[j].w >> 31);
+      }
+      // identical records never change the row (isOverrides(equal) is false and an identical
+      // LEAVING over LEAVING is a no-op) except on the viewer's own subject: the fast path of a
+      // converged cluster, where nearly every lane of nearly every unit compares equal
+      const uint32_t off = hc.r - base;
+      const bool self_here = off < SYNC_CHUNK && ((off & 255u) >> 2) == lane;
+      if (diff != 0 || self_here) {
+#pragma unroll
+        for (int j = 0; j < CLS_LOADS; ++j) {
+          const uint32_t x = base + j * 256 + 4 * lane;
+          const uint32_t av[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
+          const uint32_t ov[4] = {o[j].x, o[j].y, o[j].z, o[j].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (r_in_table(av[q]) && sync_complex(av[q], ov[q], x + q == hc.r)) flags |= 1u << (4 * j + q);
+        }
+      }
+      uint2 res = make_uint2(0, 0);
+      if (__ballot(flags != 0)) {
+        // rare path: subject order = (j, lane, q); one wave scan of the four per-j counts
+        uint64_t cnt = 0;
+#pragma unroll
+        for (int j = 0; j < CLS_LOADS; ++j) cnt |= (uint64_t)__popc((flags >> (4 * j)) & 0xfu) << (16 * j);
+        uint64_t incl = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint64_t y = __shfl_up(incl, d, 64);
+          if (lane >= (uint32_t)d) incl += y;
+        }
+        const uint64_t tot = __shfl(incl, 63, 64);
+        const uint64_t excl = incl - cnt;
+        uint32_t t = 0, jbase[CLS_LOADS];
+#pragma unroll
+        for (int j = 0; j < CLS_LOADS; ++j) { jbase[j] = t; t += (uint32_t)(tot >> (16 * j)) & 0xffffu; }
+        uint32_t pb = 0;
+        if (lane == 0) pb = atomicAdd(&b.k->pool_cursor, t);
+        pb = __shfl(pb, 0, 64);
+        if (pb + t > b.pool_cap) {
+          if (lane == 0) set_err(c, ERR_PEND);
+          t = 0;
+        } else {
+#pragma unroll
+          for (int j = 0; j < CLS_LOADS; ++j) {
+            uint32_t o2 = pb + jbase[j] + ((uint32_t)(excl >> (16 * j)) & 0xffffu);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (flags & (1u << (4 * j + q))) b.pool[o2++] = base + j * 256 + 4 * lane + q;
+          }
+        }
+        res = make_uint2(pb, t);
+        if (lane == 0 && t) atomicAdd(&b.item_total[hc.i], t);
+        cplx += t;
+      }
+      if (lane == 0) b.item_chunk[(size_t)hc.i * chunks + ch] = res;
+      if (more) {
+        hc = hn;
+#pragma unroll
+        for (int j = 0; j < CLS_LOADS; ++j) { a[j] = an[j]; o[j] = on[j]; }
+      }
+    }
+  }
+  // one counter update per workgroup (4,096 waves on one replicated counter would serialise)
+#pragma unroll
   for (int d = 32; d > 0; d >>= 1) recs += __shfl_down(recs, d, 64);
-  if ((threadIdx.x & 63) == 0) stat_add(c, ST_SYNC_RECORDS, recs);
-  if (threadIdx.x == 0) {
-    stat_add(c, ST_MERGE_MSGS, msgs);
+  if (lane == 0) s_recs[threadIdx.x >> 6] = recs;
+  if (lane == 0 && cplx) {
     stat_add(c, ST_MERGE_RECORDS, cplx);
+    if (prof) atomicAdd(prof + 1, cplx);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < CLS_BLOCK / 64; ++w) t += s_recs[w];
+    stat_add(c, ST_SYNC_RECORDS, t);
   }
 }
 
 // In-workgroup merge of one message (used when the receiver's row changed earlier in this
 // sub-phase, so the precomputed classification may be stale).  Returns through *s_mod whether any
 // record could change the row.
-__device__ void merge_row_wg(const Ctx& c, uint32_t v, const uint64_t* __restrict__ content, int reason,
+__device__ void merge_row_wg(const Ctx& c, uint32_t v, const uint32_t* __restrict__ content, int reason,
                              uint32_t phase, uint64_t* pend, uint32_t& npend, uint32_t* s_list, uint32_t* s_wave,
                              uint32_t* s_mod) {
-  uint64_t* __restrict__ rv = row(c, v);
+  const uint32_t* __restrict__ rv = rec_row(c, v);
   const uint32_t n = c.n;
   for (uint32_t base = 0; base < n; base += APPLY_TILE) {
     const uint32_t x0 = base + threadIdx.x * APPLY_CPT;
@@ -267,8 +351,8 @@ __device__ void merge_row_wg(const Ctx& c, uint32_t v, const uint64_t* __restric
     for (int k = 0; k < APPLY_CPT; ++k) {
       const uint32_t x = x0 + k;
       if (x >= n) break;
-      const uint64_t a = content[x];
-      if (c_has(a, B_IN_TABLE) && sync_complex(a, rv[x], x == v)) flags |= 1u << k;
+      const uint32_t a = content[x];
+      if (r_in_table(a) && sync_complex(a, rv[x], x == v)) flags |= 1u << k;
     }
     uint32_t total;
     const uint32_t off = block_exclusive_scan<APPLY_BLOCK>((uint32_t)__popc(flags), s_wave, &total);
@@ -281,9 +365,9 @@ __device__ void merge_row_wg(const Ctx& c, uint32_t v, const uint64_t* __restric
       *s_mod = 1;
       for (uint32_t i = 0; i < total; ++i) {
         const uint32_t x = s_list[i];
-        const uint64_t a = content[x];
-        if (update_membership(c, v, x, c_status(a), c_inc(a), reason, phase))
-          pend[npend++] = ((uint64_t)x << 32) | (uint32_t)c_inc(a);
+        const uint32_t a = content[x];
+        if (update_membership(c, v, x, r_status(a), r_inc(a), reason, phase))
+          pend[npend++] = ((uint64_t)x << 32) | (uint32_t)r_inc(a);
       }
     }
     __syncthreads();
@@ -294,7 +378,7 @@ __device__ void merge_row_wg(const Ctx& c, uint32_t v, const uint64_t* __restric
 __device__ inline void add_ack(const Ctx& c, const Bufs& b, uint32_t to, uint32_t from, uint32_t rank, bool initial) {
   SyncReq a;
   a.from = from; a.to = to; a.ordinal = rank; a.slot = 0; a.flags = RQ_DELIVERED | (initial ? RQ_INITIAL : 0);
-  a.content = NONE; a.pad[0] = a.pad[1] = 0;
+  a.content = NONE; a.snap = NONE; a.pad = 0;
   if (!owned(c, to)) {  // content (this row after the SYNC merges) travels with the ack
     const uint32_t d = owner(c, to);
     const uint32_t i = atomicAdd(&b.x->ack[d], 1u);
@@ -327,7 +411,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(Ctx c, Bufs b, int d
     __syncthreads();
     for (uint32_t q = 0; q < k; ++q) {
       const SyncReq rq = p.out[first + q];
-      const uint64_t* content = sync_content(c, b, rq);
+      const uint32_t* content = sync_content(c, b, rq);
       const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
       uint32_t npend = 0;
       const uint32_t mod = s_mod;
@@ -340,9 +424,9 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(Ctx c, Bufs b, int d
             if (e.y) s_mod = 1;
             for (uint32_t j = 0; j < e.y; ++j) {
               const uint32_t x = b.pool[e.x + j];
-              const uint64_t a = content[x];
-              if (update_membership(c, s, x, c_status(a), c_inc(a), reason, phase))
-                pend[npend++] = ((uint64_t)x << 32) | (uint32_t)c_inc(a);
+              const uint32_t a = content[x];
+              if (update_membership(c, s, x, r_status(a), r_inc(a), reason, phase))
+                pend[npend++] = ((uint64_t)x << 32) | (uint32_t)r_inc(a);
             }
           }
         }
