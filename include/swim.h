@@ -112,8 +112,9 @@ typedef struct swim_config {
   int32_t sync_stagger;       /* 1 = each initial member's periodic SYNC gets a random phase */
   int32_t record_fd_events;   /* 1 = FailureDetectorEvents appear in the event stream */
   uint32_t gossip_capacity;   /* max live GossipStates per member (0 = default 1024) */
-  uint32_t collector_capacity;/* max distinct gossipers whose SequenceIdCollector a member holds
-                                 (power of two; 0 = default 1024) */
+  uint32_t collector_capacity;/* hash slots for the SequenceIdCollectors a member holds, one per
+                                 distinct gossiper heard (power of two; 0 = default 4096; keep the
+                                 load well below 1: open addressing) */
   uint32_t event_capacity;    /* undrained events the engine may buffer (0 = default 1<<22) */
   int32_t device;             /* HIP device ordinal the engine runs on (one engine per GPU) */
   int32_t local_shards;       /* swim_create only: > 1 runs the cluster as this many row shards in

@@ -31,6 +31,7 @@ namespace {
 constexpr uint32_t kDrainEvery = 256;
 constexpr uint32_t kClassifyGrid = 1024;  // 4,096 waves: the resident capacity at 110 VGPRs (4 waves / SIMD)
 constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
+constexpr uint32_t kEmitGrid = 2048;      // 8,192 waves, one gossip sender at a time each
 constexpr uint32_t kStopCap = 4096;
 constexpr uint32_t kProfEvery = 7;  // odd: samples alternate between the SYNC and SYNC_ACK launches
 
@@ -75,6 +76,10 @@ struct Shard {
   size_t rx_msg_cap = 0, rx_req_cap = 0, rx_row_cap = 0, tx_row_cap = 0, rx_stop_cap = 0;
   uint32_t n_rx_msgs = 0, n_rx_reqs = 0, n_rx_stops = 0;
   uint32_t links_dev_cap = 0;
+  // device-resident launch parameters (swim_phases.h Params) and the last uploaded image
+  Params* d_par = nullptr;
+  Params up{};
+  bool up_valid = false;
   // swim_profile_*: HIP events around every k_sync_classify launch on the engine's stream
   std::vector<hipEvent_t> prof_ev;
   uint32_t prof_used = 0;
@@ -117,9 +122,10 @@ struct swim_engine {
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
   std::vector<Shard> sh;  // local shards, in shard order
-  CollDev* kat_coll = nullptr;
   uint32_t* d_cnt = nullptr;  // RCCL: received per-peer counts
   uint32_t* h_cnt = nullptr;  // pinned host mirror
+  Params* h_par = nullptr;    // pinned staging ring for Params uploads
+  uint32_t par_slot = 0;
   // host mirrors of replicated control state
   std::vector<uint8_t> g_residue;  // gossip timer residues mod G in use
   std::vector<uint32_t> seeds;
@@ -137,9 +143,9 @@ struct swim_engine {
       for (hipEvent_t ev : s.prof_ev) hipEventDestroy(ev);
       for (void* p : s.allocs) hipFree(p);
     }
-    if (kat_coll) hipFree(kat_coll);
     if (d_cnt) hipFree(d_cnt);
     if (h_cnt) hipHostFree(h_cnt);
+    if (h_par) hipHostFree(h_par);
     if (comm) ncclCommDestroy(comm);
     if (stream) hipStreamDestroy(stream);
   }
@@ -199,7 +205,7 @@ static void prof_flush(Shard& s) {
 static void launch_classify(swim_engine* e, Shard& s, int d2) {
   const bool p = e->prof && (s.prof_seen++ % kProfEvery) == 0 && 2 * (s.prof_used + 1) <= s.prof_ev.size();
   if (p) hipEventRecord(s.prof_ev[2 * s.prof_used], e->stream);
-  k_sync_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(s.c, s.b, d2, p ? s.prof_slots + 2 * s.prof_used : nullptr);
+  k_sync_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(s.d_par, e->T, d2, p ? s.prof_slots + 2 * s.prof_used : nullptr);
   if (p) {
     hipEventRecord(s.prof_ev[2 * s.prof_used + 1], e->stream);
     s.prof_used++;
@@ -208,6 +214,7 @@ static void launch_classify(swim_engine* e, Shard& s, int d2) {
 
 static int32_t sync_and_collect(swim_engine* e) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return hip_status() ? SWIM_EDEVICE : SWIM_EDEVICE;
+  e->par_slot = 0;  // every staged Params upload has completed
   uint32_t err_all = 0;
   for (Shard& s : e->sh) {
     uint32_t cnt = 0, err = 0;
@@ -403,12 +410,6 @@ static int32_t exchange_sync(swim_engine* e, int kind) {
   return SWIM_OK;
 }
 
-// deferred pingMembers inserts of the phase's ADDED events (Ctx points at that phase's counters)
-static void run_ins_pipeline(swim_engine* e, Shard& sd, const Ctx& c) {
-  k_ins_prep<<<1, 1024, 0, e->stream>>>(c, sd.b);
-  k_ins_apply<<<512, 256, 0, e->stream>>>(c, sd.b);
-}
-
 static Ctx sync_ctx(Shard& sd) {  // list inserts of the SYNC phase use the second set of counters
   Ctx cd = sd.c;
   cd.ins_total = &sd.k->ins_total2;
@@ -423,70 +424,99 @@ static void bind_rx(Shard& sd) {
   sd.b.rx_stops = sd.rx_stops;
 }
 
-// One tick: ~15 kernels per shard (21 on gossip ticks); a sharded engine adds three exchanges.
+// Upload the shard's launch parameters when any field differs from the image the device holds.
+// Uploads go through a pinned staging ring on the engine's stream, so they are ordered with the
+// kernels; the ring wraps only after a stream synchronisation.
+constexpr uint32_t kParRing = 64;
+static void sync_params(swim_engine* e, Shard& sd) {
+  bind_rx(sd);
+  Params p;
+  std::memset(&p, 0, sizeof p);
+  p.c = sd.c;
+  p.cs = sync_ctx(sd);
+  p.b = sd.b;
+  p.c.T = p.cs.T = 0;  // the tick travels as a kernel argument
+  if (sd.up_valid && std::memcmp(&p, &sd.up, sizeof p) == 0) return;
+  if (e->par_slot == kParRing) {
+    hipStreamSynchronize(e->stream);
+    e->par_slot = 0;
+  }
+  Params* stage = e->h_par + e->par_slot++;
+  std::memcpy(stage, &p, sizeof p);
+  hipMemcpyAsync(sd.d_par, stage, sizeof p, hipMemcpyHostToDevice, e->stream);
+  sd.up = p;
+  sd.up_valid = true;
+}
+
+// deferred pingMembers inserts of the phase's ADDED events
+static void run_ins_pipeline(swim_engine* e, Shard& sd, int sync_phase) {
+  k_ins_apply<<<512, 256, 0, e->stream>>>(sd.d_par, e->T, sync_phase);
+}
+
+// One tick: ~11 kernels per shard (16 on gossip ticks); a sharded engine adds three exchanges.
 static int32_t run_tick(swim_engine* e) {
   e->T += 1;
   e->host_ticks += 1;
   hipStream_t s = e->stream;
+  const uint64_t T = e->T;
   const bool multi = e->world > 1;
   const bool gossip_tick = e->g_residue[e->T % e->G] != 0;
   for (Shard& sd : e->sh) {
     sd.c.T = e->T;
     sd.n_rx_msgs = sd.n_rx_reqs = sd.n_rx_stops = 0;
+    sync_params(e, sd);
   }
   if (!e->joins.empty()) {
     for (Shard& sd : e->sh)
       for (uint32_t m : e->joins) hipMemsetAsync(sd.c.up + m, 1, 1, s);
-    for (Shard& sd : e->sh) k_start_joins<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sd.c);
+    for (Shard& sd : e->sh) k_start_joins<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sd.d_par, T);
     e->joins.clear();
   }
   for (Shard& sd : e->sh) {
-    Ctx& c = sd.c;
-    const uint32_t gm = grid_for(c.nl, 256);
+    const uint32_t gm = grid_for(sd.c.nl, 256);
     // ---- A: suspicion timeouts
-    const uint32_t bucket = (uint32_t)(e->T & c.wheel_mask);
-    k_timers<<<256, 256, 0, s>>>(c, bucket);
-    k_compact<<<256, 256, 0, s>>>(c, sd.k, bucket);
-    // ---- B: failure detector
-    k_fd<<<gm, 256, 0, s>>>(c);
+    k_timers<<<256, 256, 0, s>>>(sd.d_par, T);
+    // ---- B: list compaction of the timer phase's REMOVED + failure detector
+    k_fd<<<gm, 256, 0, s>>>(sd.d_par, T);
     // ---- C: gossip round (emit)
     if (gossip_tick) {
-      if (c.seg_threshold < KIV) k_gossip_seg<<<gm, 256, 0, s>>>(c);
-      k_gossip_emit<<<gm, 256, 0, s>>>(c, sd.b);
+      if (sd.c.seg_threshold < KIV) k_gossip_seg<<<gm, 256, 0, s>>>(sd.d_par, T);
+      k_gossip_round<<<gm, 256, 0, s>>>(sd.d_par, T);
+      k_gossip_emit<<<kEmitGrid, 64 * EMIT_WAVES, 0, s>>>(sd.d_par, T);
     }
   }
   if (gossip_tick) {
     if (multi)
       if (int32_t rc = exchange_msgs(e)) return rc;
     for (Shard& sd : e->sh) {
-      Ctx& c = sd.c;
-      bind_rx(sd);
-      if (sd.n_rx_msgs) k_recv_msgs<<<std::min<uint32_t>(grid_for(sd.n_rx_msgs, 256), 1024), 256, 0, s>>>(c, sd.b, sd.n_rx_msgs);
-      k_alloc<<<64, 256, 0, s>>>(sd.b.msg_recv, &sd.k->msg_recv_cnt, sd.b.msg_cnt, sd.b.msg_start, &sd.k->msg_cursor, c.lo);
-      k_scatter_msgs<<<512, 256, 0, s>>>(sd.b, c.lo);
-      k_gossip_deliver<<<grid_for(c.nl, 256), 256, 0, s>>>(c, sd.b);
-      run_ins_pipeline(e, sd, c);
+      if (multi) sync_params(e, sd);
+      if (sd.n_rx_msgs)
+        k_recv_msgs<<<std::min<uint32_t>(grid_for(sd.n_rx_msgs, 256), 1024), 256, 0, s>>>(sd.d_par, T, sd.n_rx_msgs);
+      k_alloc<<<64, 256, 0, s>>>(sd.b.msg_recv, &sd.k->msg_recv_cnt, sd.b.msg_cnt, sd.b.msg_start, &sd.k->msg_cursor, sd.c.lo);
+      k_scatter_msgs<<<512, 256, 0, s>>>(sd.d_par, T);
+      k_gossip_deliver<<<std::min<uint32_t>(1024, grid_for(sd.c.nl, DLV_BLOCK)), DLV_BLOCK, 0, s>>>(sd.d_par, T);
+      run_ins_pipeline(e, sd, 0);
     }
   }
   // ---- D: SYNC / SYNC_ACK
-  for (Shard& sd : e->sh) k_sync_collect<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sync_ctx(sd), sd.b);
+  for (Shard& sd : e->sh) k_sync_collect<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sd.d_par, T);
   for (int d2 = 0; d2 < 2; ++d2) {
     if (multi)
       if (int32_t rc = exchange_sync(e, 1 + d2)) return rc;
     for (Shard& sd : e->sh) {
-      const Ctx cd = sync_ctx(sd);
-      bind_rx(sd);
-      if (sd.n_rx_reqs) k_recv_sync<<<std::min<uint32_t>(grid_for(sd.n_rx_reqs, 256), 256), 256, 0, s>>>(cd, sd.b, d2, sd.n_rx_reqs);
-      k_sync_prep<<<1, 1024, 0, s>>>(cd, sd.b, d2);
+      if (multi) sync_params(e, sd);
+      if (sd.n_rx_reqs)
+        k_recv_sync<<<std::min<uint32_t>(grid_for(sd.n_rx_reqs, 256), 256), 256, 0, s>>>(sd.d_par, T, d2, sd.n_rx_reqs);
+      k_sync_prep<<<1, 1024, 0, s>>>(sd.d_par, T, d2);
       launch_classify(e, sd, d2);
-      k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(cd, sd.b, d2);
+      k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(sd.d_par, T, d2);
     }
   }
   for (Shard& sd : e->sh) {
-    run_ins_pipeline(e, sd, sync_ctx(sd));
+    run_ins_pipeline(e, sd, 1);
     // ---- end of tick (also zeroes the per-tick counters and applies other shards' stops)
     const uint32_t ge = grid_for(std::max<uint32_t>(std::max<uint32_t>(sd.c.nl, sd.n_rx_stops), 64), 256);
-    k_end_tick<<<ge, 256, 0, s>>>(sd.c, sd.k, sd.x, sd.rx_stops, sd.n_rx_stops);
+    k_end_tick<<<ge, 256, 0, s>>>(sd.d_par, T, sd.n_rx_stops);
   }
   return SWIM_OK;
 }
@@ -574,7 +604,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.nl = std::min(n, c.lo + e->sz) - c.lo;
   const uint32_t nl = c.nl;
   c.gcap = cf.gossip_capacity ? cf.gossip_capacity : 1024;
-  c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 1024);
+  c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 4096);
+  c.spill_cap = std::max<uint32_t>(1u << 20, 64 * std::max(nl, 1u));
   c.P = e->P;
   c.to_ticks = (uint32_t)cf.ping_timeout / e->tick_ms;
   c.relay_ticks = e->P - c.to_ticks;
@@ -610,23 +641,24 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   const size_t nn = (size_t)nl * n;
   bool ok = sd.alloc(&c.recs, nn) && sd.alloc(&c.aux, nn) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
             sd.alloc(&c.remote, nn) && sd.alloc(&c.slab, (size_t)nl * c.gcap) && sd.alloc(&c.coll, (size_t)nl * c.hcap) &&
+            sd.alloc(&c.spill, c.spill_cap) && sd.alloc(&c.spill_cnt, 1) &&
             sd.alloc(&c.fd_sync, (size_t)nl * FD_SYNC_MAX) &&
             sd.alloc(&c.wheel, (size_t)(c.wheel_mask + 1) * c.wheel_cap) && sd.alloc(&c.wheel_cnt, c.wheel_mask + 1) &&
             sd.alloc(&c.ev, c.ev_cap) && sd.alloc(&c.ev_cnt, 1) && sd.alloc(&c.default_loss, n) &&
             sd.alloc(&c.default_inbound, n) && sd.alloc(&c.group, n) && sd.alloc(&c.links, 1) &&
-            sd.alloc(&c.is_seed, n) && sd.alloc(&c.seeds, n) && sd.alloc(&c.ins, c.ins_cap) && sd.alloc(&c.ins_cnt, nl) &&
-            sd.alloc(&c.ins_list, nl) && sd.alloc(&c.compact_flag, nl) && sd.alloc(&c.compact_list, nl) &&
+            sd.alloc(&c.is_seed, n) && sd.alloc(&c.seeds, n) && sd.alloc(&c.ins, c.ins_cap) &&
+            sd.alloc(&c.ins_list, nl) && sd.alloc(&c.compact_flag, nl) &&
             sd.alloc(&c.stats, (size_t)ST_COUNT * ST_REPL) && sd.alloc(&c.err, 1) && sd.alloc(&sd.k, 1) &&
             sd.alloc(&sd.x, 1) && sd.alloc(&b.msgs, b.msg_cap) && sd.alloc(&b.msgs_out, b.msg_cap) &&
             sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.msg_start, nl) && sd.alloc(&b.msg_recv, nl) &&
             sd.alloc(&b.reqs, b.req_cap) && sd.alloc(&b.reqs_out, b.req_cap) && sd.alloc(&b.req_cnt, nl) &&
             sd.alloc(&b.req_start, nl) && sd.alloc(&b.req_recv, nl) && sd.alloc(&b.acks, b.req_cap) &&
             sd.alloc(&b.acks_out, b.req_cap) && sd.alloc(&b.ack_cnt, nl) && sd.alloc(&b.ack_start, nl) &&
-            sd.alloc(&b.ack_recv, nl) && sd.alloc(&b.ins_out, c.ins_cap) && sd.alloc(&b.ins_start, nl) &&
+            sd.alloc(&b.ack_recv, nl) && 
             sd.alloc(&b.snap, (size_t)b.snap_cap * n) && sd.alloc(&b.snap_idx, nl) && sd.alloc(&b.snap_list, b.snap_cap) &&
             sd.alloc(&b.snap_cnt, 1) && sd.alloc(&b.item_chunk, (size_t)b.req_cap * b.chunks) &&
             sd.alloc(&b.item_total, b.req_cap) && sd.alloc(&b.pool, b.pool_cap) &&
-            sd.alloc(&b.pend, (size_t)kApplyGrid * n);
+            sd.alloc(&b.pend, (size_t)kApplyGrid * n) && sd.alloc(&sd.d_par, 1) && sd.alloc(&b.senders, nl);
   if (ok && multi)
     ok = sd.alloc(&b.tx_msgs, (size_t)e->world * b.tx_msg_cap) && sd.alloc(&b.tx_reqs, (size_t)e->world * b.tx_req_cap) &&
          sd.alloc(&b.tx_acks, (size_t)e->world * b.tx_req_cap) && sd.alloc(&b.tx_stops, b.tx_stop_cap);
@@ -634,11 +666,11 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   sd.links_dev_cap = 1;
   c.ins_total = &sd.k->ins_total;
   c.ins_list_cnt = &sd.k->ins_list_cnt;
-  c.compact_cnt = &sd.k->compact_cnt;
   b.k = sd.k;
   b.x = sd.x;
   hipStream_t s = e->stream;
-  hipMemsetAsync(c.coll, 0, sizeof(CollDev) * (size_t)nl * c.hcap, s);
+  hipMemsetAsync(c.coll, 0, sizeof(CollEnt) * (size_t)nl * c.hcap, s);
+  hipMemsetAsync(c.spill_cnt, 0, 4, s);
   hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1), s);
   hipMemsetAsync(c.ev_cnt, 0, 4, s);
   hipMemsetAsync(c.up, 0, n, s);
@@ -647,7 +679,6 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(c.default_inbound, 1, n, s);
   hipMemsetAsync(c.group, 0, 2 * (size_t)n, s);
   hipMemsetAsync(c.is_seed, 0, n, s);
-  hipMemsetAsync(c.ins_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(c.compact_flag, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(c.stats, 0, 8 * (size_t)ST_COUNT * ST_REPL, s);
   hipMemsetAsync(c.err, 0, 4, s);
@@ -709,7 +740,7 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
     int32_t rc = alloc_shard(e, e->sh[i], rccl ? (uint32_t)rank : (uint32_t)i, n_initial, seed);
     if (rc != SWIM_OK) { delete e; return rc; }
   }
-  if (hipMalloc((void**)&e->kat_coll, sizeof(CollDev)) != hipSuccess) { delete e; return SWIM_ENOMEM; }
+  if (hipHostMalloc((void**)&e->h_par, sizeof(Params) * kParRing) != hipSuccess) { delete e; return SWIM_ENOMEM; }
   if (world > 1) {
     if (hipMalloc((void**)&e->d_cnt, sizeof(uint32_t) * 2 * MAXW) != hipSuccess ||
         hipHostMalloc((void**)&e->h_cnt, sizeof(uint32_t) * 2 * MAXW + sizeof(Xc)) != hipSuccess) {
@@ -1126,17 +1157,23 @@ int32_t swim_read_collector(swim_engine* e, uint32_t v, uint32_t gossiper, swim_
   Shard* sd = e->owner_of(v);
   if (!sd) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  std::vector<CollDev> tab(sd->c.hcap);
-  if (hipMemcpy(tab.data(), sd->c.coll + (size_t)(v - sd->c.lo) * sd->c.hcap, sizeof(CollDev) * sd->c.hcap,
+  std::vector<CollEnt> tab(sd->c.hcap);
+  if (hipMemcpy(tab.data(), sd->c.coll + (size_t)(v - sd->c.lo) * sd->c.hcap, sizeof(CollEnt) * sd->c.hcap,
                 hipMemcpyDeviceToHost) != hipSuccess)
     return SWIM_EDEVICE;
   if (len) *len = 0;
-  for (const CollDev& d : tab) {
+  for (const CollEnt& d : tab) {
     if (d.key != gossiper + 1) continue;
-    if (len) *len = d.n;
-    for (uint32_t i = 0; i < d.n && i < cap && out; ++i) {
-      out[i].lo = d.lo[i];
-      out[i].hi = d.hi[i];
+    const uint32_t n = d.meta & 7u;
+    CollDev sp{};
+    if (n == COLL_SPILLED &&
+        hipMemcpy(&sp, sd->c.spill + (d.meta >> 8), sizeof(CollDev), hipMemcpyDeviceToHost) != hipSuccess)
+      return SWIM_EDEVICE;
+    const uint32_t cnt = n == COLL_SPILLED ? sp.n : n;
+    if (len) *len = cnt;
+    for (uint32_t i = 0; i < cnt && i < cap && out; ++i) {
+      out[i].lo = n == COLL_SPILLED ? sp.lo[i] : d.lo;
+      out[i].hi = n == COLL_SPILLED ? sp.hi[i] : d.hi;
     }
     break;
   }
@@ -1213,22 +1250,26 @@ int32_t swim_kat_collector(const uint8_t* kinds, const int64_t* values, uint32_t
   uint8_t* dk = nullptr;
   int64_t* dv = nullptr;
   int64_t* dr = nullptr;
-  CollDev* de = nullptr;
+  CollEnt* de = nullptr;
+  CollDev* dsp = nullptr;
   uint32_t* derr = nullptr;
   if (hipMalloc((void**)&dk, n) != hipSuccess || hipMalloc((void**)&dv, 8 * (size_t)n) != hipSuccess ||
-      hipMalloc((void**)&dr, 8 * (size_t)n) != hipSuccess || hipMalloc((void**)&de, sizeof(CollDev)) != hipSuccess ||
-      hipMalloc((void**)&derr, 4) != hipSuccess)
+      hipMalloc((void**)&dr, 8 * (size_t)n) != hipSuccess || hipMalloc((void**)&de, sizeof(CollEnt)) != hipSuccess ||
+      hipMalloc((void**)&dsp, sizeof(CollDev) * n + 4) != hipSuccess || hipMalloc((void**)&derr, 8) != hipSuccess)
     return SWIM_EDEVICE;
   hipMemcpy(dk, kinds, n, hipMemcpyHostToDevice);
   hipMemcpy(dv, values, 8 * (size_t)n, hipMemcpyHostToDevice);
-  hipMemset(derr, 0, 4);
+  hipMemset(derr, 0, 8);
   Ctx c{};
   c.err = derr;
+  c.spill = dsp;
+  c.spill_cnt = derr + 1;
+  c.spill_cap = n;
   k_kat_collector<<<1, 64>>>(c, dk, dv, n, dr, de);
   hipError_t r = hipMemcpy(results, dr, 8 * (size_t)n, hipMemcpyDeviceToHost);
   uint32_t err = 0;
   hipMemcpy(&err, derr, 4, hipMemcpyDeviceToHost);
-  hipFree(dk); hipFree(dv); hipFree(dr); hipFree(de); hipFree(derr);
+  hipFree(dk); hipFree(dv); hipFree(dr); hipFree(de); hipFree(dsp); hipFree(derr);
   if (r != hipSuccess) return SWIM_EDEVICE;
   return err ? SWIM_ECAPACITY : hip_status();
 }

@@ -53,7 +53,8 @@ struct alignas(16) MemberDev {
   uint32_t remote_len;
   int32_t remote_idx;
   uint32_t gossip_len, table_size, members_size, leave_gossiper;
-  uint32_t ev_minor, fetch_ctr, fd_sync_cnt, ins_rank, init_total, init_done;
+  uint32_t ev_minor, fetch_ctr, fd_sync_cnt, init_total, init_done;
+  uint32_t ins_rank, ins_head, ins_tail;  // this phase's deferred pingMembers inserts (op chain)
   uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, pad[2];
 };
 
@@ -64,11 +65,18 @@ struct GossipDev {  // GossipState + Gossip + MembershipRecord payload, 32 B
   uint32_t inf0, inf1;  // GossipState.infected (NONE = empty)
 };
 
-struct CollDev {  // SequenceIdCollector: up to KIV closed intervals, ascending
+// SequenceIdCollector (SequenceIdCollector.java) of (viewer, gossiper), 16 B: a collector holds one
+// interval almost always (a gossiper's sequence ids reach a member in order), so the interval is
+// inline and a collector that needs more spills to a 64-B CollDev of up to KIV intervals.
+struct CollEnt {
   uint32_t key;   // gossiper + 1; 0 = empty slot
-  uint32_t n;
-  uint32_t cleared;  // 1 once cleared/removed: a GossipState may outlive its collector entries
-  uint32_t pad;
+  uint32_t lo, hi;
+  uint32_t meta;  // bits 0..2: inline interval count (0 / 1) or COLL_SPILLED; bit 3: cleared;
+                  // bits 8..31: spill index
+};
+constexpr uint32_t COLL_SPILLED = 7u, COLL_CLEARED = 8u;
+struct CollDev {  // spilled SequenceIdCollector: up to KIV closed intervals, ascending
+  uint32_t n, pad[3];
   uint32_t lo[KIV], hi[KIV];
 };
 
@@ -94,7 +102,7 @@ struct SyncReq {  // SYNC (request) or SYNC_ACK
 };
 
 struct InsOp {  // deferred pingMembers.add(nextInt(size), member) of an ADDED event
-  uint32_t v, s, phase, minor, rank, pad[3];
+  uint32_t s, phase, minor, next;  // next: the viewer's following op in event order (chain)
 };
 
 // Row sharding: shard r owns viewers [lo, lo + nl) with lo = r * sz.  Every array
@@ -115,7 +123,10 @@ struct Ctx {
   uint32_t* ping;
   uint32_t* remote;
   GossipDev* slab;
-  CollDev* coll;
+  CollEnt* coll;       // [nl][hcap] open addressing by gossiper
+  CollDev* spill;      // spilled multi-interval collectors
+  uint32_t* spill_cnt;
+  uint32_t spill_cap;
   uint32_t* fd_sync;
   uint64_t* wheel;
   uint32_t* wheel_cnt;
@@ -136,12 +147,9 @@ struct Ctx {
   InsOp* ins;
   uint32_t* ins_total;
   uint32_t ins_cap;
-  uint32_t* ins_cnt;       // per viewer
   uint32_t* ins_list;      // viewers with ops
   uint32_t* ins_list_cnt;
-  uint32_t* compact_flag;  // per viewer
-  uint32_t* compact_list;
-  uint32_t* compact_cnt;
+  uint32_t* compact_flag;  // per viewer: lists hold a REMOVED member (compacted before its next FD step)
   unsigned long long* stats;
   uint32_t* err;
 };
@@ -305,43 +313,49 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
 }
-__device__ inline CollDev* coll_find(const Ctx& c, uint32_t v, uint32_t gossiper) {
-  CollDev* base = c.coll + (size_t)(v - c.lo) * c.hcap;
+__device__ inline CollEnt* coll_find(const Ctx& c, uint32_t v, uint32_t gossiper) {
+  CollEnt* base = c.coll + (size_t)(v - c.lo) * c.hcap;
   uint32_t mask = c.hcap - 1, h = hash32(gossiper) & mask, key = gossiper + 1;
   for (uint32_t i = 0; i < c.hcap; ++i) {
-    CollDev* e = base + ((h + i) & mask);
-    if (e->key == key) return e;
-    if (e->key == 0) return nullptr;
+    CollEnt* e = base + ((h + i) & mask);
+    const uint32_t k = e->key;
+    if (k == key) return e;
+    if (k == 0) return nullptr;
   }
   return nullptr;
 }
 // ensureSequence (GossipProtocolImpl.java:279-281)
-__device__ inline CollDev* coll_ensure(const Ctx& c, uint32_t v, uint32_t gossiper) {
-  CollDev* base = c.coll + (size_t)(v - c.lo) * c.hcap;
+__device__ inline CollEnt* coll_ensure(const Ctx& c, uint32_t v, uint32_t gossiper) {
+  CollEnt* base = c.coll + (size_t)(v - c.lo) * c.hcap;
   uint32_t mask = c.hcap - 1, h = hash32(gossiper) & mask, key = gossiper + 1;
   for (uint32_t i = 0; i < c.hcap; ++i) {
-    CollDev* e = base + ((h + i) & mask);
+    CollEnt* e = base + ((h + i) & mask);
     if (e->key == key) return e;
     if (e->key == 0) {
       e->key = key;
-      e->n = 0;
-      e->cleared = 0;
+      e->lo = e->hi = 0;
+      e->meta = 0;
       return e;
     }
   }
   set_err(c, ERR_HASH);
   return nullptr;
 }
-// SequenceIdCollector.contains (SequenceIdCollector.java:32-35)
-__device__ inline bool coll_contains(const CollDev* e, uint32_t x) {
-  if (!e) return false;
+// SequenceIdCollector.contains (SequenceIdCollector.java:32-35) on a KIV-interval set
+__device__ inline bool coll_dev_contains(const CollDev* e, uint32_t x) {
   for (int i = (int)e->n - 1; i >= 0; --i)
     if (e->lo[i] <= x) return x <= e->hi[i];
   return false;
 }
-// SequenceIdCollector.add (SequenceIdCollector.java:43-72)
-__device__ inline bool coll_add(const Ctx& c, CollDev* e, uint32_t x) {
-  if (!e) return true;
+__device__ inline bool coll_contains(const Ctx& c, const CollEnt* e, uint32_t x) {
+  if (!e) return false;
+  const uint32_t n = e->meta & 7u;
+  if (n == 1) return e->lo <= x && x <= e->hi;
+  if (n == COLL_SPILLED) return coll_dev_contains(c.spill + (e->meta >> 8), x);
+  return false;
+}
+// SequenceIdCollector.add (SequenceIdCollector.java:43-72) on a KIV-interval set
+__device__ inline bool coll_dev_add(const Ctx& c, CollDev* e, uint32_t x) {
   int n = (int)e->n, fl = -1;
   for (int i = n - 1; i >= 0; --i)
     if (e->lo[i] <= x) { fl = i; break; }
@@ -366,6 +380,35 @@ __device__ inline bool coll_add(const Ctx& c, CollDev* e, uint32_t x) {
   }
   return true;
 }
+__device__ inline bool coll_add(const Ctx& c, CollEnt* e, uint32_t x) {
+  if (!e) return true;
+  const uint32_t n = e->meta & 7u;
+  if (n == COLL_SPILLED) return coll_dev_add(c, c.spill + (e->meta >> 8), x);
+  if (n == 0) {
+    e->lo = e->hi = x;
+    e->meta = (e->meta & ~7u) | 1u;
+    return true;
+  }
+  if (e->lo <= x && x <= e->hi) return false;
+  if ((int64_t)x == (int64_t)e->hi + 1) { e->hi = x; return true; }
+  if ((int64_t)x + 1 == (int64_t)e->lo) { e->lo = x; return true; }
+  // a second disjoint interval: spill
+  const uint32_t i = atomicAdd(c.spill_cnt, 1u);
+  if (i >= c.spill_cap || i >= (1u << 24)) { set_err(c, ERR_INTERVALS); return true; }
+  CollDev* d = c.spill + i;
+  d->n = 1;
+  d->lo[0] = e->lo;
+  d->hi[0] = e->hi;
+  e->meta = (e->meta & COLL_CLEARED) | COLL_SPILLED | (i << 8);
+  return coll_dev_add(c, d, x);
+}
+// number of intervals (checkGossipSegmentation's size())
+__device__ inline uint32_t coll_size(const Ctx& c, const CollEnt* e) {
+  const uint32_t n = e->meta & 7u;
+  return n == COLL_SPILLED ? c.spill[e->meta >> 8].n : n;
+}
+// clear() / remove: no intervals, marked cleared (a GossipState may outlive its collector entries)
+__device__ inline void coll_clear(CollEnt* e) { e->meta = COLL_CLEARED; }
 
 // ------------------------------------------------------------------------------- events
 __device__ inline void emit(const Ctx& c, uint32_t v, uint32_t s, uint32_t type, uint32_t phase, uint32_t minor) {
@@ -389,30 +432,31 @@ __device__ inline void on_added(const Ctx& c, uint32_t v, uint32_t s, uint32_t p
   MemberDev& m = mem(c, v);
   remote_list(c, v)[m.remote_len] = s;
   m.remote_len++;
-  uint32_t rank = m.ins_rank++;
-  if (rank == 0) {
-    uint32_t li = atomicAdd(c.ins_list_cnt, 1u);
-    c.ins_list[li] = v;
-  }
-  c.ins_cnt[v - c.lo] = rank + 1;
-  uint32_t i = atomicAdd(c.ins_total, 1u);
+  // a viewer's ADDED events of one phase come from the one thread that owns it in that phase, so
+  // its ops form a chain in event order with no grouping pass
+  const uint32_t i = atomicAdd(c.ins_total, 1u);
   if (i >= c.ins_cap) { set_err(c, ERR_INS); return; }
   InsOp op;
-  op.v = v; op.s = s; op.phase = phase; op.minor = minor; op.rank = rank;
-  op.pad[0] = op.pad[1] = op.pad[2] = 0;
+  op.s = s; op.phase = phase; op.minor = minor; op.next = NONE;
   c.ins[i] = op;
+  if (m.ins_rank++ == 0) {
+    m.ins_head = i;
+    c.ins_list[atomicAdd(c.ins_list_cnt, 1u)] = v;
+  } else {
+    c.ins[m.ins_tail].next = i;
+  }
+  m.ins_tail = i;
 }
 
 // REMOVED: GossipProtocolImpl drops the member's SequenceIdCollector (:242); both lists drop the
-// member in the phase's compaction kernel (they hold exactly the viewer's other `members`).
+// member before the viewer's next FD step (k_fd; they hold exactly the viewer's other `members`).
+// REMOVED only arises in the timer phase (DEAD is never gossiped or synced, and the FD publishes no
+// DEAD without DEST_GONE), and nothing reads the lists between the timers and the FD step.
 // Safe under entry-parallel timer processing: only the (v, s) collector entry is written.
 __device__ inline void on_removed(const Ctx& c, uint32_t v, uint32_t s) {
-  CollDev* e = coll_find(c, v, s);
-  if (e) {
-    e->n = 0;
-    e->cleared = 1;
-  }
-  if (atomicExch(&c.compact_flag[v - c.lo], 1u) == 0u) c.compact_list[atomicAdd(c.compact_cnt, 1u)] = v;
+  CollEnt* e = coll_find(c, v, s);
+  if (e) coll_clear(e);
+  c.compact_flag[v - c.lo] = 1u;
 }
 
 __device__ inline void publish_event(const Ctx& c, uint32_t v, uint32_t s, uint32_t type, uint32_t phase,
@@ -443,7 +487,7 @@ __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject,
   slab_of(c, v)[m.gossip_len] = g;
   m.gossip_len++;
   m.g_counter++;
-  CollDev* e = coll_ensure(c, v, v);
+  CollEnt* e = coll_ensure(c, v, v);
   coll_add(c, e, g.seq);
   stat_add(c, ST_GOSSIPS_CREATED, 1);
 }

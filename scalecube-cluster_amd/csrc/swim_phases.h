@@ -1,10 +1,11 @@
 // swim_kernels.h — the HIP kernels of one lockstep tick.
 //
-// Phase A  k_timers, k_compact                       suspicion timeouts, list removals
-// Phase B  k_fd                                       ping / ping-req / ack resolution + FD events
+// Phase A  k_timers                                   suspicion timeouts
+// Phase B  k_fd                                       list compaction after REMOVED, then ping /
+//                                                     ping-req / ack resolution + FD events
 // Phase C  k_gossip_seg, k_gossip_emit, k_alloc, k_scatter_msgs, k_gossip_deliver
 // Phase D  k_sync_collect, k_sync_prep, k_sync_classify, k_sync_apply (swim_sync.h; SYNC and SYNC_ACK)
-// lists    k_ins_scatter, k_ins_apply                 deferred pingMembers inserts of ADDED events
+// lists    k_ins_apply                                deferred pingMembers inserts of ADDED events
 // tick end k_end_tick
 //
 // Every kernel reads its work size from device memory (grid-stride over device counters), so the
@@ -19,11 +20,11 @@ struct Counters {
   uint32_t msg_total, msg_recv_cnt, msg_cursor;
   uint32_t req_total, req_recv_cnt, req_cursor;
   uint32_t ack_total, ack_recv_cnt, ack_cursor;
-  uint32_t ins_total, ins_list_cnt, ins_cursor;     // list inserts of the gossip phase
-  uint32_t ins_total2, ins_list_cnt2, ins_cursor2;  // list inserts of the SYNC phase
-  uint32_t compact_cnt;
+  uint32_t ins_total, ins_list_cnt;    // list inserts of the gossip phase
+  uint32_t ins_total2, ins_list_cnt2;  // list inserts of the SYNC phase
   uint32_t pool_cursor;  // complex-record pool of the SYNC classify kernel
-  uint32_t pad[3];
+  uint32_t sender_cnt;   // senders of this tick's gossip round with live gossips
+  uint32_t pad[2];
 };
 
 // per-tick message counts by destination shard (sharded engines), zeroed by k_end_tick
@@ -66,8 +67,6 @@ struct Bufs {
   uint32_t* ack_cnt;
   uint32_t* ack_start;
   uint32_t* ack_recv;
-  InsOp* ins_out;
-  uint32_t* ins_start;
   uint32_t* snap;       // snapshot record rows
   uint32_t snap_cap;
   uint32_t* snap_idx;   // per member: slot or NONE
@@ -76,10 +75,33 @@ struct Bufs {
   uint64_t* pend;       // per sync-apply workgroup: pending ALIVE admissions
   uint2* item_chunk;    // per (message, chunk): (pool base, complex count)
   uint32_t* item_total; // per message: complex count over all chunks
+  uint32_t* senders;    // local indices of this round's senders with live gossips
   uint32_t* pool;       // subjects whose record may change the receiver, chunk-ordered
   uint32_t pool_cap;
   uint32_t chunks;      // ceil(N / SYNC_CHUNK)
 };
+
+// Device-resident launch parameters.  Per-tick kernels receive only a pointer to these and the tick
+// number instead of ~700 B of Ctx + Bufs by value: kernel arguments are read by dependent rounds of
+// scalar loads that miss a cold scalar cache at every launch (~2 us each; measured 2-16 us of
+// prologue per kernel), while this block sits in ordinary cached device memory.  The host uploads
+// it only when a field changes (engine.hip, sync_params).
+struct Params {
+  Ctx c;   // T is taken from the kernel argument
+  Ctx cs;  // the SYNC phase's context (its own list-insert counters)
+  Bufs b;
+};
+__device__ __forceinline__ Ctx pctx(const Params* __restrict__ P, uint64_t T) {
+  Ctx c = P->c;
+  c.T = T;
+  return c;
+}
+__device__ __forceinline__ Ctx pctx_sync(const Params* __restrict__ P, uint64_t T) {
+  Ctx c = P->cs;
+  c.T = T;
+  return c;
+}
+#define KP const Params* __restrict__ P, uint64_t T
 
 // ------------------------------------------------------------------------------- init
 __global__ void k_init_rows(Ctx c, uint32_t n_initial) {
@@ -159,7 +181,8 @@ __device__ inline uint32_t block_exclusive_scan(uint32_t x, uint32_t* s_wave, ui
 
 // ------------------------------------------------------------------------------- start joins
 // (the host has already set the replicated up[v] on every shard)
-__global__ void k_start_joins(Ctx c) {
+__global__ void k_start_joins(KP) {
+  const Ctx c = pctx(P, T);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= c.nl) return;
   const uint32_t v = c.lo + i;
@@ -179,7 +202,9 @@ __global__ void k_start_joins(Ctx c) {
 // onSuspicionTimeout (MembershipProtocolImpl.java:825-834) for every due (viewer, subject).
 // Entries of one viewer are independent (each touches only its own cell; counters are atomic),
 // so the bucket is processed entry-parallel; event order is canonicalised by minor = subject.
-__global__ void k_timers(Ctx c, uint32_t bucket) {
+__global__ void k_timers(KP) {
+  const Ctx c = pctx(P, T);
+  const uint32_t bucket = (uint32_t)(T & c.wheel_mask);
   const uint32_t cnt = min(c.wheel_cnt[bucket], c.wheel_cap);
   const uint64_t* ent = c.wheel + (size_t)bucket * c.wheel_cap;
   const uint32_t tmask = (uint32_t)(c.T & SWIM_DEADLINE_MASK);
@@ -224,19 +249,6 @@ __device__ void compact_list(const Ctx& c, uint32_t v, uint32_t* list, uint32_t&
   }
   if (threadIdx.x == 0) len = out;
   __syncthreads();
-}
-
-__global__ void __launch_bounds__(256) k_compact(Ctx c, Counters* k, uint32_t bucket) {
-  // k_timers has drained this tick's wheel bucket
-  if (blockIdx.x == 0 && threadIdx.x == 0) c.wheel_cnt[bucket] = 0;
-  const uint32_t cnt = k->compact_cnt;
-  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-    uint32_t v = c.compact_list[i];
-    MemberDev& m = mem(c, v);
-    compact_list<256>(c, v, ping_list(c, v), m.ping_len);
-    compact_list<256>(c, v, remote_list(c, v), m.remote_len);
-    if (threadIdx.x == 0) c.compact_flag[v - c.lo] = 0;
-  }
 }
 
 // ------------------------------------------------------------------------------- phase B
@@ -364,9 +376,30 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
   }
 }
 
-// launched with a multiple of 64 threads per block: every lane reaches the wave-reduced counters
-__global__ void k_fd(Ctx c) {
+// 256-thread workgroups, one viewer per thread.  First the workgroup compacts the ping / remote
+// lists of its viewers that lost a member in this tick's timer phase (a per-viewer dependency, so
+// no separate launch), then every thread runs its viewer's FD step.
+__global__ void __launch_bounds__(256) k_fd(KP) {
+  const Ctx c = pctx(P, T);
+  const uint32_t bucket = (uint32_t)(T & c.wheel_mask);
+  __shared__ uint32_t s_list[256];
+  __shared__ uint32_t s_cnt;
+  if (blockIdx.x == 0 && threadIdx.x == 0) c.wheel_cnt[bucket] = 0;  // k_timers drained the bucket
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool flagged = i < c.nl && c.compact_flag[i] != 0;
+  if (flagged) s_list[atomicAdd(&s_cnt, 1u)] = i;
+  __syncthreads();
+  const uint32_t nc = s_cnt;
+  for (uint32_t k = 0; k < nc; ++k) {
+    const uint32_t v = c.lo + s_list[k];
+    MemberDev& m = mem(c, v);
+    compact_list<256>(c, v, ping_list(c, v), m.ping_len);
+    compact_list<256>(c, v, remote_list(c, v), m.remote_len);
+  }
+  if (flagged) c.compact_flag[i] = 0;
+  __syncthreads();  // the compacted lengths are visible to every thread
   unsigned long long nev = 0, nreq = 0, npings = 0;
   if (i < c.nl) fd_member(c, c.lo + i, nev, nreq, npings);
   wave_stat_add(c, ST_FD_EVENTS, nev);
@@ -381,14 +414,15 @@ __device__ __forceinline__ bool gossip_due(const Ctx& c, uint32_t v, const Membe
 
 // checkGossipSegmentation (GossipProtocolImpl.java:217-236); only launched when the threshold is
 // below the inline interval capacity (otherwise a clear can never trigger).
-__global__ void k_gossip_seg(Ctx c) {
+__global__ void k_gossip_seg(KP) {
+  const Ctx c = pctx(P, T);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= c.nl) return;
   const MemberDev& m = c.mem[i];
   if (!gossip_due(c, c.lo + i, m)) return;
-  CollDev* base = c.coll + (size_t)i * c.hcap;
-  for (uint32_t i = 0; i < c.hcap; ++i)
-    if (base[i].key && (int32_t)base[i].n > c.seg_threshold) { base[i].n = 0; base[i].cleared = 1; }
+  CollEnt* base = c.coll + (size_t)i * c.hcap;
+  for (uint32_t j = 0; j < c.hcap; ++j)
+    if (base[j].key && (int32_t)coll_size(c, base + j) > c.seg_threshold) coll_clear(base + j);
 }
 
 // a GOSSIP_REQ for a receiver owned by this shard joins the receiver's inbox
@@ -400,98 +434,171 @@ __device__ inline void deliver_local_msg(const Ctx& c, const Bufs& b, GMsgFull m
   b.msgs[i] = msg;
 }
 
-// doSpreadGossip (:141-184): period++, select members, send, sweep, complete futures.
-__device__ inline unsigned long long gossip_emit_member(const Ctx& c, const Bufs& b, uint32_t v) {
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// doSpreadGossip (:141-184), wave-parallel.  Each wave owns the senders wid, wid + nw, ... and
+// first checks up to 64 of them at once (lane l: sender base + l * nw): every due sender advances
+// its period (:143); a sender with live gossips then gets the whole wave: lane 0 selects the
+// targets (:322-343), the (target, slab position) pairs of selectGossipsToSend (:311-320) are
+// spread over the lanes — loss draws and receiver-collector probes of 64 pairs in flight together,
+// one enqueue atomic per (target, pass) — then the order-preserving sweep and the futures.
+constexpr int EMIT_WAVES = 4;
+__device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs& b, uint32_t v, uint64_t period,
+                                                        uint32_t glen, uint32_t lane, uint32_t* s_t) {
   MemberDev& m = mem(c, v);
-  if (!gossip_due(c, v, m)) return 0;
-  const uint64_t period = m.g_period++;
-  m.period_used = period;
-  if (m.gossip_len == 0) return 0;
-  // selectGossipMembers (:322-343)
-  uint32_t targets[16];
-  uint32_t nt = 0;
-  uint32_t* rl = remote_list(c, v);
+  const uint32_t rlen = m.remote_len;
   const uint32_t F = (uint32_t)c.fanout;
-  if (m.remote_len < F) {
-    for (uint32_t i = 0; i < m.remote_len; ++i) targets[nt++] = rl[i];
-  } else {
-    if (m.remote_idx < 0 || (uint32_t)m.remote_idx + F > m.remote_len) {
-      shuffle_list(c, v, rl, m.remote_len, SWIM_STREAM_GOSSIP_SHUFFLE);
-      m.remote_idx = 0;
+  if (lane == 0) {  // selectGossipMembers (:322-343)
+    uint32_t* rl = remote_list(c, v);
+    uint32_t nt = 0;
+    if (rlen < F) {
+      for (uint32_t i = 0; i < rlen; ++i) s_t[1 + nt++] = rl[i];
+    } else {
+      if (m.remote_idx < 0 || (uint32_t)m.remote_idx + F > rlen) {
+        shuffle_list(c, v, rl, rlen, SWIM_STREAM_GOSSIP_SHUFFLE);
+        m.remote_idx = 0;
+      }
+      for (uint32_t i = 0; i < F; ++i) s_t[1 + nt++] = rl[m.remote_idx + i];
+      m.remote_idx += (int32_t)F;
     }
-    for (uint32_t i = 0; i < F; ++i) targets[nt++] = rl[m.remote_idx + i];
-    m.remote_idx += (int32_t)F;
+    s_t[0] = nt;
   }
-  const int32_t size1 = (int32_t)m.remote_len + 1;
-  const uint64_t spread = (uint64_t)(c.repeat_mult * ceil_log2((uint32_t)size1));
+  __syncwarp();
+  const uint32_t nt = s_t[0];
+  const uint64_t spread = (uint64_t)(c.repeat_mult * ceil_log2(rlen + 1));
   const uint64_t sweep = 2 * (spread + 1);
   GossipDev* slab = slab_of(c, v);
   unsigned long long nmsg = 0;
-  for (uint32_t j = 0; j < nt; ++j) {
-    const uint32_t t = targets[j];
-    const bool t_up = c.up[t] != 0;
-    const bool local = owned(c, t);
-    const int32_t loss = out_loss(c, v, t);
-    const bool pass = in_pass(c, t, v);
-    for (uint32_t p = 0; p < m.gossip_len; ++p) {  // selectGossipsToSend (:311-320)
-      const GossipDev g = slab[p];
-      if (!((uint64_t)g.inf_period + spread >= period)) continue;
-      if (g.inf0 == t || g.inf1 == t) continue;
-      nmsg++;
-      if (!t_up || lost_k(c, loss, v, SWIM_STREAM_GOSSIP_OUT, j, p) || !pass) continue;
+  const uint32_t pairs = nt * glen;
+  for (uint32_t q0 = 0; q0 < pairs; q0 += 64) {
+    const uint32_t q = q0 + lane;
+    const bool act = q < pairs;
+    const uint32_t j = act ? q / glen : 0, p = act ? q - j * glen : 0;
+    const uint32_t t = s_t[1 + j];
+    GossipDev g;
+    bool send = false, mat = false;
+    if (act) {
+      g = slab[p];
+      send = (uint64_t)g.inf_period + spread >= period && g.inf0 != t && g.inf1 != t;
+      // delivered copies; a receiver on this shard that already holds the sequence id drops it
+      // (its collector only grows until delivery), another shard filters on arrival
+      mat = send && c.up[t] && in_pass(c, t, v) && !lost_k(c, out_loss(c, v, t), v, SWIM_STREAM_GOSSIP_OUT, j, p) &&
+            !(owned(c, t) && coll_contains(c, coll_find(c, t, g.gossiper), g.seq));
+    }
+    nmsg += send ? 1u : 0u;
+    if (!__ballot(mat)) continue;
+    // one enqueue per target present in this pass: lane jj issues target jj's atomics
+    uint32_t base = 0, slot = 0, cnt_mine = 0, pre = 0;
+    for (uint32_t jj = 0; jj < nt; ++jj) {
+      const uint64_t mk = __ballot(mat && j == jj);
+      if (lane == jj) cnt_mine = (uint32_t)__popcll(mk);
+      if (j == jj) pre = lanes_below(mk);
+    }
+    if (lane < nt && cnt_mine) {
+      const uint32_t tj = s_t[1 + lane];
+      if (owned(c, tj)) {
+        base = atomicAdd(&b.k->msg_total, cnt_mine);
+        slot = atomicAdd(&b.msg_cnt[tj - c.lo], cnt_mine);
+        if (slot == 0) b.msg_recv[atomicAdd(&b.k->msg_recv_cnt, 1u)] = tj;
+      } else {
+        base = atomicAdd(&b.x->msg[owner(c, tj)], cnt_mine);
+      }
+    }
+    base = __shfl(base, (int)j, 64);
+    slot = __shfl(slot, (int)j, 64);
+    if (mat) {
       GMsgFull msg;
-      msg.to = t; msg.from = v; msg.pos = p; msg.slot = 0;
+      msg.to = t; msg.from = v; msg.pos = p; msg.slot = slot + pre;
       msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
       msg.inc = g.inc; msg.pad[0] = msg.pad[1] = msg.pad[2] = 0;
-      if (!local) {  // another shard's receiver: it filters duplicates on arrival (k_recv_msgs)
+      if (owned(c, t)) {
+        if (base + pre < b.msg_cap) b.msgs[base + pre] = msg; else set_err(c, ERR_MSGS);
+      } else {
         const uint32_t d = owner(c, t);
-        const uint32_t i = atomicAdd(&b.x->msg[d], 1u);
-        if (i >= b.tx_msg_cap) { set_err(c, ERR_MSGS); continue; }
-        b.tx_msgs[(size_t)d * b.tx_msg_cap + i] = msg;
-        continue;
+        if (base + pre < b.tx_msg_cap) b.tx_msgs[(size_t)d * b.tx_msg_cap + base + pre] = msg; else set_err(c, ERR_MSGS);
       }
-      // certain duplicate at the receiver: its collector already holds the sequence id and can
-      // only grow until delivery
-      if (coll_contains(coll_find(c, t, g.gossiper), g.seq)) continue;
-      deliver_local_msg(c, b, msg);
     }
   }
-  // sweep (:158-164, :350-358), order preserving
+  // sweep (:158-164, :350-358), order preserving: a chunk's survivors land at or below their own
+  // positions, all of which the wave has already read
   uint32_t w = 0;
-  for (uint32_t p = 0; p < m.gossip_len; ++p) {
-    GossipDev g = slab[p];
-    if (period > (uint64_t)g.inf_period + sweep) continue;
-    if (w != p) slab[w] = g;
-    ++w;
-  }
-  m.gossip_len = w;
-  // futures (:167-180): the graceful-leave future stops the member at the end of the tick
-  if (m.leave_pending) {
-    for (uint32_t p = 0; p < w; ++p) {
-      const GossipDev& g = slab[p];
-      if (period > (uint64_t)g.inf_period + spread && g.gossiper == m.leave_gossiper && g.seq == (uint32_t)m.leave_seq)
-        m.leave_done = 1;
+  bool done = false;
+  const bool leaving = m.leave_pending != 0;
+  for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
+    const uint32_t p = p0 + lane;
+    GossipDev g;
+    bool keep = false;
+    if (p < glen) {
+      g = slab[p];
+      keep = !(period > (uint64_t)g.inf_period + sweep);
     }
-    if (m.leave_done && c.world > 1) {  // every shard stops sending to v at the end of this tick
-      const uint32_t i = atomicAdd(&b.x->stop, 1u);
-      if (i < b.tx_stop_cap) b.tx_stops[i] = v; else set_err(c, ERR_MSGS);
+    const uint64_t mask = __ballot(keep);
+    if (keep) {
+      slab[w + lanes_below(mask)] = g;
+      // futures (:167-180): the graceful-leave future stops the member at the end of the tick
+      if (leaving && period > (uint64_t)g.inf_period + spread && g.gossiper == m.leave_gossiper &&
+          g.seq == (uint32_t)m.leave_seq)
+        done = true;
+    }
+    w += (uint32_t)__popcll(mask);
+  }
+  const bool any_done = __ballot(done) != 0;
+  if (lane == 0) {
+    m.gossip_len = w;
+    if (any_done) {
+      m.leave_done = 1;
+      if (c.world > 1) {  // every shard stops sending to v at the end of this tick
+        const uint32_t i = atomicAdd(&b.x->stop, 1u);
+        if (i < b.tx_stop_cap) b.tx_stops[i] = v; else set_err(c, ERR_MSGS);
+      }
     }
   }
+  __syncwarp();
   return nmsg;
 }
 
-__global__ void k_gossip_emit(Ctx c, Bufs b) {
+// doSpreadGossip's first steps for every due sender, one thread each: period++ (:143) and, when it
+// holds live gossips (:149-151), a place in the round's sender list
+__global__ void k_gossip_round(KP) {
+  const Ctx c = pctx(P, T);
+  const Bufs b = P->b;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned long long nmsg = i < c.nl ? gossip_emit_member(c, b, c.lo + i) : 0;
+  if (i >= c.nl) return;
+  MemberDev& m = c.mem[i];
+  if (!gossip_due(c, c.lo + i, m)) return;
+  const uint64_t period = m.g_period;
+  m.g_period = period + 1;
+  m.period_used = period;
+  if (m.gossip_len == 0) return;  // no target selection, no shuffle draw
+  b.senders[atomicAdd(&b.k->sender_cnt, 1u)] = i;
+}
+
+// the rest of the round for the listed senders: one sender per wave at a time
+__global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP) {
+  __shared__ uint32_t s_t[EMIT_WAVES][17];
+  const Ctx c = pctx(P, T);
+  const Bufs b = P->b;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t ns = b.k->sender_cnt;
+  unsigned long long nmsg = 0;
+  for (uint32_t k = __builtin_amdgcn_readfirstlane(blockIdx.x * EMIT_WAVES + wv); k < ns; k += gridDim.x * EMIT_WAVES) {
+    const uint32_t i = b.senders[k];
+    const MemberDev& m = c.mem[i];
+    nmsg += gossip_emit_sender(c, b, c.lo + i, m.g_period - 1, m.gossip_len, lane, s_t[wv]);
+  }
   wave_stat_add(c, ST_GOSSIP_MESSAGES, nmsg);
 }
 
 // GOSSIP_REQs arriving from other shards: drop provable duplicates (the emitter could not see
 // this shard's collectors), then join the local message list exactly as a local send does
-__global__ void k_recv_msgs(Ctx c, Bufs b, uint32_t nrx) {
+__global__ void k_recv_msgs(KP, uint32_t nrx) {
+  const Ctx c = pctx(P, T);
+  const Bufs b = P->b;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrx; i += gridDim.x * blockDim.x) {
     const GMsgFull msg = b.rx_msgs[i];
-    if (coll_contains(coll_find(c, msg.to, msg.gossiper), msg.seq)) continue;
+    if (coll_contains(c, coll_find(c, msg.to, msg.gossiper), msg.seq)) continue;
     deliver_local_msg(c, b, msg);
   }
 }
@@ -506,11 +613,14 @@ __global__ void k_alloc(const uint32_t* list, const uint32_t* list_cnt, const ui
   }
 }
 
-__global__ void k_scatter_msgs(Bufs b, uint32_t lo) {
+__global__ void k_scatter_msgs(KP) {
+  const Bufs b = P->b;
+  const uint32_t lo = P->c.lo;
   const uint32_t n = min(b.k->msg_total, b.msg_cap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const GMsgFull m = b.msgs[i];
-    b.msgs_out[b.msg_start[m.to - lo] + m.slot] = m;
+    const uint64_t at = (uint64_t)b.msg_start[m.to - lo] + m.slot;
+    if (at < b.msg_cap) b.msgs_out[at] = m;  // beyond: the buffer overflowed (ERR_MSGS is set)
   }
 }
 
@@ -545,94 +655,170 @@ __device__ inline void sort_msgs(GMsgFull* a, uint32_t n) {
   }
 }
 
-// onGossipReq (GossipProtocolImpl.java:201-215) at each receiver, canonical order (sender, pos)
-__global__ void k_gossip_deliver(Ctx c, Bufs b) {
+// onGossipReq (GossipProtocolImpl.java:201-215) for one received message, in canonical order
+__device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, GossipDev* slab, const GMsgFull& g) {
+  CollEnt* col = coll_ensure(c, r, g.gossiper);
+  if (!col) return false;
+  const bool was_cleared = (col->meta & COLL_CLEARED) != 0;
+  if (!coll_add(c, col, g.seq)) return false;
+  int32_t found = -1;
+  if (was_cleared) {  // a GossipState can outlive its collector entry only after a clear
+    for (uint32_t p = 0; p < m.gossip_len; ++p)
+      if (slab[p].gossiper == g.gossiper && slab[p].seq == g.seq) { found = (int32_t)p; break; }
+  }
+  if (found < 0) {
+    if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); return true; }
+    GossipDev ns;
+    ns.gossiper = g.gossiper; ns.seq = g.seq; ns.subject = g.subject; ns.status = g.status; ns.inc = g.inc;
+    ns.inf_period = (uint32_t)m.g_period;
+    ns.inf0 = g.from;
+    ns.inf1 = NONE;
+    slab[m.gossip_len++] = ns;
+    // onMembershipGossip (MembershipProtocolImpl.java:452-459)
+    if (update_membership(c, r, g.subject, g.status, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP))
+      apply_alive(c, r, g.subject, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP);
+  } else {
+    GossipDev& st = slab[found];
+    if (st.inf0 != g.from && st.inf1 != g.from) {
+      if (st.inf0 == NONE) st.inf0 = g.from;
+      else if (st.inf1 == NONE) st.inf1 = g.from;
+      else set_err(c, ERR_INFECTED);
+    }
+  }
+  return true;
+}
+
+// One receiver per thread (the onGossipReq chain of a receiver is sequential, so concurrency comes
+// from many receivers): the inbox keys (sender, slab position) are insertion-sorted in an LDS slice
+// laid out [slot][thread] (conflict-free), then processed in that order.  Inboxes above DLV_SORT
+// messages are deferred to the workgroup: one wave bitonic-sorts up to DLV_BIG keys in LDS and its
+// lane 0 processes them; larger inboxes are sorted in place in global memory.
+constexpr int DLV_BLOCK = 256;
+constexpr int DLV_SORT = 24;
+constexpr int DLV_BIG = 512;
+__device__ inline unsigned long long deliver_sorted(const Ctx& c, uint32_t r, const GMsgFull* a, uint32_t k,
+                                                    const uint8_t* ix8, uint32_t ix8_stride, const uint16_t* ix16) {
+  MemberDev& m = mem(c, r);
+  m.ev_minor = 0;
+  m.fetch_ctr = 0;
+  GossipDev* slab = slab_of(c, r);
+  unsigned long long acc = 0;
+  for (uint32_t q = 0; q < k; ++q) {
+    const uint32_t at = ix8 ? ix8[q * ix8_stride] : ix16 ? ix16[q] : q;
+    if (on_gossip_req(c, r, m, slab, a[at])) acc++;
+  }
+  return acc;
+}
+
+__global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
+  const Ctx c = pctx(P, T);
+  const Bufs b = P->b;
+  __shared__ uint64_t s_key[DLV_SORT][DLV_BLOCK];
+  __shared__ uint8_t s_ix[DLV_SORT][DLV_BLOCK];
+  __shared__ uint64_t s_bkey[DLV_BLOCK / 64][DLV_BIG];
+  __shared__ uint16_t s_bix[DLV_BLOCK / 64][DLV_BIG];
+  __shared__ uint32_t s_big_r[DLV_BLOCK], s_big_k[DLV_BLOCK], s_big_start[DLV_BLOCK];
+  __shared__ uint32_t s_nbig;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) s_nbig = 0;
+  __syncthreads();
   const uint32_t nrecv = b.k->msg_recv_cnt;
   unsigned long long acc = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrecv; i += gridDim.x * blockDim.x) {
+  for (uint32_t i = blockIdx.x * DLV_BLOCK + tid; i < nrecv; i += gridDim.x * DLV_BLOCK) {
     const uint32_t r = b.msg_recv[i];
     const uint32_t k = b.msg_cnt[r - c.lo];
-    GMsgFull* a = b.msgs_out + b.msg_start[r - c.lo];
+    const uint32_t start = b.msg_start[r - c.lo];
     b.msg_cnt[r - c.lo] = 0;
-    MemberDev& m = mem(c, r);
     if (!c.up[r]) continue;
-    sort_msgs(a, k);
-    m.ev_minor = 0;
-    m.fetch_ctr = 0;
-    GossipDev* slab = slab_of(c, r);
-    for (uint32_t q = 0; q < k; ++q) {
-      const GMsgFull g = a[q];
-      CollDev* col = coll_ensure(c, r, g.gossiper);
-      if (!col) continue;
-      const bool was_cleared = col->cleared != 0;
-      if (!coll_add(c, col, g.seq)) continue;
-      acc++;
-      int32_t found = -1;
-      if (was_cleared) {  // a GossipState can outlive its collector entry only after a clear
-        for (uint32_t p = 0; p < m.gossip_len; ++p)
-          if (slab[p].gossiper == g.gossiper && slab[p].seq == g.seq) { found = (int32_t)p; break; }
-      }
-      if (found < 0) {
-        if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); continue; }
-        GossipDev ns;
-        ns.gossiper = g.gossiper; ns.seq = g.seq; ns.subject = g.subject; ns.status = g.status; ns.inc = g.inc;
-        ns.inf_period = (uint32_t)m.g_period;
-        ns.inf0 = g.from;
-        ns.inf1 = NONE;
-        slab[m.gossip_len++] = ns;
-        // onMembershipGossip (MembershipProtocolImpl.java:452-459)
-        if (update_membership(c, r, g.subject, g.status, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP))
-          apply_alive(c, r, g.subject, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP);
-      } else {
-        GossipDev& st = slab[found];
-        if (st.inf0 != g.from && st.inf1 != g.from) {
-          if (st.inf0 == NONE) st.inf0 = g.from;
-          else if (st.inf1 == NONE) st.inf1 = g.from;
-          else set_err(c, ERR_INFECTED);
+    if ((uint64_t)start + k > b.msg_cap) {  // the message buffer overflowed (ERR_MSGS already set)
+      set_err(c, ERR_MSGS);
+      continue;
+    }
+    GMsgFull* a = b.msgs_out + start;
+    if (k <= (uint32_t)DLV_SORT) {
+      for (uint32_t q = 0; q < k; ++q) {
+        const uint64_t kx = ((uint64_t)a[q].from << 32) | a[q].pos;  // keys are unique
+        int32_t j = (int32_t)q - 1;
+        while (j >= 0 && s_key[j][tid] > kx) {
+          s_key[j + 1][tid] = s_key[j][tid];
+          s_ix[j + 1][tid] = s_ix[j][tid];
+          --j;
         }
+        s_key[j + 1][tid] = kx;
+        s_ix[j + 1][tid] = (uint8_t)q;
+      }
+      acc += deliver_sorted(c, r, a, k, &s_ix[0][tid], DLV_BLOCK, nullptr);
+      continue;
+    }
+    if (k <= (uint32_t)DLV_BIG) {
+      const uint32_t slot = atomicAdd(&s_nbig, 1u);
+      if (slot < DLV_BLOCK) {
+        s_big_r[slot] = r;
+        s_big_k[slot] = k;
+        s_big_start[slot] = start;
+        continue;
       }
     }
+    sort_msgs(a, k);
+    acc += deliver_sorted(c, r, a, k, nullptr, 0, nullptr);
+  }
+  __syncthreads();
+  const uint32_t nbig = min(s_nbig, (uint32_t)DLV_BLOCK);
+  uint64_t* key = s_bkey[wv];
+  uint16_t* ix = s_bix[wv];
+  for (uint32_t bi = wv; bi < nbig; bi += DLV_BLOCK / 64) {
+    const uint32_t r = s_big_r[bi], k = s_big_k[bi];
+    const GMsgFull* a = b.msgs_out + s_big_start[bi];
+    uint32_t P = 64;
+    while (P < k) P <<= 1;
+    for (uint32_t q = lane; q < P; q += 64) {
+      key[q] = q < k ? (((uint64_t)a[q].from << 32) | a[q].pos) : ~0ull;
+      ix[q] = (uint16_t)q;
+    }
+    __syncwarp();
+    for (uint32_t size = 2; size <= P; size <<= 1)
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (uint32_t t = lane; t < P / 2; t += 64) {
+          const uint32_t lo = 2 * stride * (t / stride) + (t % stride), hi = lo + stride;
+          const bool asc = (lo & size) == 0;
+          const uint64_t kl = key[lo], kh = key[hi];
+          if ((kl > kh) == asc) {
+            key[lo] = kh; key[hi] = kl;
+            const uint16_t tmp = ix[lo]; ix[lo] = ix[hi]; ix[hi] = tmp;
+          }
+        }
+        __syncwarp();
+      }
+    if (lane == 0) acc += deliver_sorted(c, r, a, k, nullptr, 0, ix);
+    __syncwarp();  // the wave's LDS region is reused by its next receiver
   }
   wave_stat_add(c, ST_GOSSIP_ACCEPTED, acc);
 }
 
 // ------------------------------------------------------------------------------- list inserts
-// one workgroup: a contiguous op region per viewer, ops placed by their per-viewer rank
-__global__ void __launch_bounds__(1024) k_ins_prep(Ctx c, Bufs b) {
-  __shared__ uint32_t s_cursor;
-  if (threadIdx.x == 0) s_cursor = 0;
-  __syncthreads();
-  const uint32_t nv = *c.ins_list_cnt;
-  for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x) {
-    const uint32_t v = c.ins_list[i] - c.lo;
-    b.ins_start[v] = atomicAdd(&s_cursor, c.ins_cnt[v]);
-  }
-  __syncthreads();
-  const uint32_t n = min(*c.ins_total, c.ins_cap);
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const InsOp op = c.ins[i];
-    b.ins_out[b.ins_start[op.v - c.lo] + op.rank] = op;
-  }
-}
-
-// pingMembers.add(nextInt(size), member) (FailureDetectorImpl.java:334-345), in event order
-__global__ void __launch_bounds__(256) k_ins_apply(Ctx c, Bufs b) {
-  __shared__ uint32_t s_idx;
+// pingMembers.add(nextInt(size), member) (FailureDetectorImpl.java:334-345), in event order: one
+// workgroup per viewer with inserts walks the viewer's op chain; each insert shifts the tail right
+// by one, tail chunk first.
+__global__ void __launch_bounds__(256) k_ins_apply(KP, int sync_phase) {
+  const Ctx c = sync_phase ? pctx_sync(P, T) : pctx(P, T);
+  __shared__ uint32_t s_idx, s_s, s_next;
   const uint32_t nv = *c.ins_list_cnt;
   for (uint32_t i = blockIdx.x; i < nv; i += gridDim.x) {
     const uint32_t v = c.ins_list[i];
-    const uint32_t k = c.ins_cnt[v - c.lo];
-    const InsOp* ops = b.ins_out + b.ins_start[v - c.lo];
     MemberDev& m = mem(c, v);
+    const uint32_t k = m.ins_rank;
     uint32_t* pl = ping_list(c, v);
+    uint32_t cur = m.ins_head;
     for (uint32_t q = 0; q < k; ++q) {
-      const InsOp op = ops[q];
       const uint32_t size = m.ping_len;
-      if (threadIdx.x == 0)
+      if (threadIdx.x == 0) {
+        const InsOp op = c.ins[cur];
         s_idx = size > 0 ? next_int(draw(c, v, SWIM_STREAM_PING_INSERT, op.phase, op.minor), size) : 0;
+        s_s = op.s;
+        s_next = op.next;
+      }
       __syncthreads();
       const uint32_t idx = s_idx;
-      // shift [idx, size) right by one, tail chunk first
       for (int64_t hi = (int64_t)size; hi > (int64_t)idx; hi -= 256) {
         int64_t lo = hi - 256 < (int64_t)idx ? (int64_t)idx : hi - 256;
         int64_t p = lo + threadIdx.x;
@@ -643,15 +829,13 @@ __global__ void __launch_bounds__(256) k_ins_apply(Ctx c, Bufs b) {
         __syncthreads();
       }
       if (threadIdx.x == 0) {
-        pl[idx] = op.s;
+        pl[idx] = s_s;
         m.ping_len = size + 1;
       }
+      cur = s_next;
       __syncthreads();
     }
-    if (threadIdx.x == 0) {
-      c.ins_cnt[v - c.lo] = 0;
-      m.ins_rank = 0;
-    }
+    if (threadIdx.x == 0) m.ins_rank = 0;
     __syncthreads();
   }
 }
@@ -741,7 +925,9 @@ __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Buf
   return nsync;
 }
 
-__global__ void k_sync_collect(Ctx c, Bufs b) {
+__global__ void k_sync_collect(KP) {
+  const Ctx c = pctx_sync(P, T);
+  const Bufs b = P->b;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const unsigned long long nsync = i < c.nl ? sync_collect_member(c, b, c.lo + i) : 0;
   wave_stat_add(c, ST_SYNCS, nsync);
@@ -752,7 +938,11 @@ __global__ void k_sync_collect(Ctx c, Bufs b) {
 
 // ------------------------------------------------------------------------------- end of tick
 // start0's doFinally (:285-289) for members that joined this tick; graceful leaves complete.
-__global__ void k_end_tick(Ctx c, Counters* k, Xc* x, const uint32_t* rx_stops, uint32_t n_rx_stops) {
+__global__ void k_end_tick(KP, uint32_t n_rx_stops) {
+  const Ctx c = pctx(P, T);
+  Counters* k = P->b.k;
+  Xc* x = P->c.world > 1 ? P->b.x : nullptr;
+  const uint32_t* rx_stops = P->b.rx_stops;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   // every other kernel of the tick has completed: reset the per-tick scratch counters
   if (i < sizeof(Counters) / 4) reinterpret_cast<uint32_t*>(k)[i] = 0;
@@ -781,17 +971,18 @@ __global__ void k_kat_overrides(const int32_t* cases, uint32_t n, uint8_t* out) 
   out[i] = is_overrides((uint32_t)k[0], k[1], k[2] != 0, (uint32_t)k[3], k[4]) ? 1 : 0;
 }
 
+// SequenceIdCollectorTest through the engine's own collector code (inline entry + spill pool)
 __global__ void k_kat_collector(Ctx c, const uint8_t* kinds, const int64_t* values, uint32_t n, int64_t* res,
-                                CollDev* e) {
+                                CollEnt* e) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  e->key = 1; e->n = 0; e->cleared = 0;
+  e->key = 1; e->lo = e->hi = 0; e->meta = 0;
   for (uint32_t i = 0; i < n; ++i) {
     uint32_t x = (uint32_t)values[i];
     switch (kinds[i]) {
       case 0: res[i] = coll_add(c, e, x) ? 1 : 0; break;
-      case 1: res[i] = coll_contains(e, x) ? 1 : 0; break;
-      case 2: res[i] = e->n; break;
-      default: e->n = 0; res[i] = 0; break;
+      case 1: res[i] = coll_contains(c, e, x) ? 1 : 0; break;
+      case 2: res[i] = coll_size(c, e); break;
+      default: coll_clear(e); res[i] = 0; break;
     }
   }
 }

@@ -72,7 +72,9 @@ __device__ inline SubPhase sub_phase(const Bufs& b, int d2) {
 }
 
 // SYNCs / SYNC_ACKs arriving from other shards (content row = rx_rows[k]) join their inboxes
-__global__ void k_recv_sync(Ctx c, Bufs b, int d2, uint32_t nrx) {
+__global__ void k_recv_sync(KP, int d2, uint32_t nrx) {
+  const Ctx c = pctx_sync(P, T);
+  const Bufs b = P->b;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nrx; k += gridDim.x * blockDim.x) {
     SyncReq q = b.rx_reqs[k];
     q.content = k;
@@ -111,7 +113,9 @@ __device__ __forceinline__ const uint32_t* sync_content(const Ctx& c, const Bufs
   return si < b.snap_cap ? b.snap + (size_t)si * c.n : rec_row(c, q.from);
 }
 
-__global__ void __launch_bounds__(1024) k_sync_prep(Ctx c, Bufs b, int d2) {
+__global__ void __launch_bounds__(1024) k_sync_prep(KP, int d2) {
+  const Ctx c = pctx_sync(P, T);
+  const Bufs b = P->b;
   __shared__ uint32_t s_cursor;
   const SubPhase p = sub_phase(b, d2);
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -213,7 +217,9 @@ __device__ __forceinline__ void cls_rows(const Ctx& c, const ClsHdr& h, uint32_t
 }
 
 // prof (profiled launches only): {messages merged, complex records} of this launch
-__global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(Ctx c, Bufs b, int d2, unsigned long long* prof) {
+__global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(KP, int d2, unsigned long long* prof) {
+  const Ctx c = pctx_sync(P, T);
+  const Bufs b = P->b;
   const SubPhase p = sub_phase(b, d2);
   const uint32_t ni = *p.nitems;
   const uint32_t chunks = b.chunks, n = c.n;
@@ -391,7 +397,9 @@ __device__ inline void add_ack(const Ctx& c, const Bufs& b, uint32_t to, uint32_
 
 // D1 (d2 = 0): onSync at each receiver, then its SYNC_ACKs.  D2 (d2 = 1): the SYNC_ACK merge at
 // the original senders (MembershipProtocolImpl.java:363-415).
-__global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(Ctx c, Bufs b, int d2) {
+__global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2) {
+  const Ctx c = pctx_sync(P, T);
+  const Bufs b = P->b;
   __shared__ uint32_t s_list[APPLY_TILE];
   __shared__ uint32_t s_wave[APPLY_BLOCK / 64 + 1];
   __shared__ uint32_t s_mod;
