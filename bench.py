@@ -64,6 +64,21 @@ def run_periods(e, p0, p1):
         p = nxt
 
 
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this bench
+    (tools/profile.sh -> tools/prof_summary.py -> profiles/<round>_<workload>_pmc.json: separate
+    FETCH_SIZE and WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}_pmc.json")))
+    if not paths:
+        return None, None
+    doc = json.load(open(paths[-1]))
+    k = doc.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k["hbm_bytes_per_launch"], os.path.relpath(paths[-1], REPO)
+
+
 def cpu_baseline(n, periods):
     """The CPU oracle (oracle/liboracle_swim.so, 1 thread for the timed ticks) on the same N and
     workload, bounded to `periods` periods from the converged start."""
@@ -154,6 +169,7 @@ def main():
     value = n * args.steps / dt  # one cluster of n members, sharded over `world` GPUs
     avg_ms = prof["total_ms"] / max(1, prof["launches"])
     achieved = prof["alg_bytes"] / max(1e-12, prof["total_ms"] / 1e3) / 1e9
+    traffic, traffic_src = pmc_traffic("k_sync_classify", f"{args.workload}{n // 1024}k")
     line = {
         "metric": "simulated member-protocol-periods/sec at N=65,536; achieved HBM GB/s",
         "value": value,
@@ -176,7 +192,9 @@ def main():
                                    f"single GPU, {args.local_shards} in-process shards" if args.local_shards > 1
                                    else "single GPU")},
         "roofline": {"bound": "hbm", "kernel": "k_sync_classify", "achieved": achieved, "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                     "traffic_source": traffic_src,
                      "launches": prof["launches"], "avg_launch_ms": avg_ms,
                      "alg_bytes_per_launch": prof["alg_bytes"] / max(1, prof["launches"]),
                      "kernel_time_share": prof["total_ms"] / (dt * 1e3 * world)},

@@ -217,19 +217,22 @@ static int32_t sync_and_collect(swim_engine* e) {
   e->par_slot = 0;  // every staged Params upload has completed
   uint32_t err_all = 0;
   for (Shard& s : e->sh) {
-    uint32_t cnt = 0, err = 0;
-    if (hipMemcpy(&cnt, s.c.ev_cnt, 4, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+    uint32_t cnt[SUBQ], err = 0;
+    if (hipMemcpy(cnt, s.c.ev_cnt, 4 * SUBQ, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
     if (hipMemcpy(&err, s.c.err, 4, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
-    cnt = std::min(cnt, s.c.ev_cap);
-    if (cnt) {
+    bool any = false;
+    for (uint32_t q = 0; q < SUBQ; ++q) {
+      const uint32_t k = std::min(cnt[q], s.c.ev_cap);
+      if (!k) continue;
+      any = true;
       size_t old = e->events.size();
-      e->events.resize(old + cnt);
-      if (hipMemcpy(e->events.data() + old, s.c.ev, sizeof(swim_event) * cnt, hipMemcpyDeviceToHost) != hipSuccess)
+      e->events.resize(old + k);
+      if (hipMemcpy(e->events.data() + old, s.c.ev + (size_t)q * s.c.ev_cap, sizeof(swim_event) * k,
+                    hipMemcpyDeviceToHost) != hipSuccess)
         return SWIM_EDEVICE;
-      e->host_events += cnt;
-      uint32_t zero = 0;
-      if (hipMemcpy(s.c.ev_cnt, &zero, 4, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
+      e->host_events += k;
     }
+    if (any && hipMemset(s.c.ev_cnt, 0, 4 * SUBQ) != hipSuccess) return SWIM_EDEVICE;
     err_all |= err;
     if (e->prof) prof_flush(s);
   }
@@ -492,7 +495,7 @@ static int32_t run_tick(swim_engine* e) {
       if (multi) sync_params(e, sd);
       if (sd.n_rx_msgs)
         k_recv_msgs<<<std::min<uint32_t>(grid_for(sd.n_rx_msgs, 256), 1024), 256, 0, s>>>(sd.d_par, T, sd.n_rx_msgs);
-      k_alloc<<<64, 256, 0, s>>>(sd.b.msg_recv, &sd.k->msg_recv_cnt, sd.b.msg_cnt, sd.b.msg_start, &sd.k->msg_cursor, sd.c.lo);
+      k_alloc<<<std::min<uint32_t>(1024, grid_for(sd.c.nl, 256)), 256, 0, s>>>(sd.d_par, T);
       k_scatter_msgs<<<512, 256, 0, s>>>(sd.d_par, T);
       k_gossip_deliver<<<std::min<uint32_t>(1024, grid_for(sd.c.nl, DLV_BLOCK)), DLV_BLOCK, 0, s>>>(sd.d_par, T);
       run_ins_pipeline(e, sd, 0);
@@ -624,10 +627,10 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.key1 = (uint32_t)(seed >> 32);
   const uint64_t max_timer = (uint64_t)cf.suspicion_mult * (uint64_t)host_ceil_log2((int32_t)n) * e->P;
   c.wheel_mask = next_pow2((uint32_t)max_timer + 2) - 1;
-  c.wheel_cap = std::max<uint32_t>(4096, 2 * std::max(nl, 1u));
-  c.ev_cap = cf.event_capacity ? cf.event_capacity : (1u << 22);
+  c.wheel_cap = SUBQ * std::max<uint32_t>(1024, (2 * std::max(nl, 1u) + SUBQ - 1) / SUBQ);
+  c.ev_cap = std::max<uint32_t>(1024, (cf.event_capacity ? cf.event_capacity : (1u << 22)) / SUBQ);
   c.ins_cap = std::max<uint32_t>(1u << 16, 4 * nl);
-  b.msg_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 256ull * nl));
+  b.msg_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 512ull * nl));
   b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
   b.snap_cap = 64;
   b.chunks = (n + SYNC_CHUNK - 1) / SYNC_CHUNK;
@@ -643,14 +646,15 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&c.remote, nn) && sd.alloc(&c.slab, (size_t)nl * c.gcap) && sd.alloc(&c.coll, (size_t)nl * c.hcap) &&
             sd.alloc(&c.spill, c.spill_cap) && sd.alloc(&c.spill_cnt, 1) &&
             sd.alloc(&c.fd_sync, (size_t)nl * FD_SYNC_MAX) &&
-            sd.alloc(&c.wheel, (size_t)(c.wheel_mask + 1) * c.wheel_cap) && sd.alloc(&c.wheel_cnt, c.wheel_mask + 1) &&
-            sd.alloc(&c.ev, c.ev_cap) && sd.alloc(&c.ev_cnt, 1) && sd.alloc(&c.default_loss, n) &&
+            sd.alloc(&c.wheel, (size_t)(c.wheel_mask + 1) * c.wheel_cap) &&
+            sd.alloc(&c.wheel_cnt, (size_t)(c.wheel_mask + 1) * SUBQ) && sd.alloc(&c.ev, (size_t)c.ev_cap * SUBQ) &&
+            sd.alloc(&c.ev_cnt, SUBQ) && sd.alloc(&c.default_loss, n) &&
             sd.alloc(&c.default_inbound, n) && sd.alloc(&c.group, n) && sd.alloc(&c.links, 1) &&
             sd.alloc(&c.is_seed, n) && sd.alloc(&c.seeds, n) && sd.alloc(&c.ins, c.ins_cap) &&
             sd.alloc(&c.ins_list, nl) && sd.alloc(&c.compact_flag, nl) &&
             sd.alloc(&c.stats, (size_t)ST_COUNT * ST_REPL) && sd.alloc(&c.err, 1) && sd.alloc(&sd.k, 1) &&
             sd.alloc(&sd.x, 1) && sd.alloc(&b.msgs, b.msg_cap) && sd.alloc(&b.msgs_out, b.msg_cap) &&
-            sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.msg_start, nl) && sd.alloc(&b.msg_recv, nl) &&
+            sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.msg_start, nl) &&
             sd.alloc(&b.reqs, b.req_cap) && sd.alloc(&b.reqs_out, b.req_cap) && sd.alloc(&b.req_cnt, nl) &&
             sd.alloc(&b.req_start, nl) && sd.alloc(&b.req_recv, nl) && sd.alloc(&b.acks, b.req_cap) &&
             sd.alloc(&b.acks_out, b.req_cap) && sd.alloc(&b.ack_cnt, nl) && sd.alloc(&b.ack_start, nl) &&
@@ -671,8 +675,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipStream_t s = e->stream;
   hipMemsetAsync(c.coll, 0, sizeof(CollEnt) * (size_t)nl * c.hcap, s);
   hipMemsetAsync(c.spill_cnt, 0, 4, s);
-  hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1), s);
-  hipMemsetAsync(c.ev_cnt, 0, 4, s);
+  hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1) * SUBQ, s);
+  hipMemsetAsync(c.ev_cnt, 0, 4 * SUBQ, s);
   hipMemsetAsync(c.up, 0, n, s);
   hipMemsetAsync(c.up, 1, n_initial, s);
   hipMemsetAsync(c.default_loss, 0, n, s);

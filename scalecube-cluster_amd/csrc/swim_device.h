@@ -128,11 +128,11 @@ struct Ctx {
   uint32_t* spill_cnt;
   uint32_t spill_cap;
   uint32_t* fd_sync;
-  uint64_t* wheel;
-  uint32_t* wheel_cnt;
+  uint64_t* wheel;      // [W][SUBQ][wheel_cap / SUBQ]
+  uint32_t* wheel_cnt;  // [W][SUBQ]
   swim_event* ev;
-  uint32_t* ev_cnt;
-  uint32_t ev_cap;
+  uint32_t* ev_cnt;     // [SUBQ]
+  uint32_t ev_cap;      // per sub-queue
   // network emulator
   uint8_t* default_loss;
   uint8_t* default_inbound;
@@ -411,9 +411,16 @@ __device__ inline uint32_t coll_size(const Ctx& c, const CollEnt* e) {
 __device__ inline void coll_clear(CollEnt* e) { e->meta = COLL_CLEARED; }
 
 // ------------------------------------------------------------------------------- events
+// Appends from thousands of threads in one kernel (a timer storm removes a member at every viewer
+// in one tick) go to SUBQ sub-queues picked by the wave, so no single counter serialises them;
+// order is canonicalised on the host ((tick, viewer, phase, minor) sort).
+constexpr uint32_t SUBQ = 16;
+__device__ __forceinline__ uint32_t subq() { return (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (SUBQ - 1); }
 __device__ inline void emit(const Ctx& c, uint32_t v, uint32_t s, uint32_t type, uint32_t phase, uint32_t minor) {
-  uint32_t i = atomicAdd(c.ev_cnt, 1u);
+  const uint32_t q = subq();
+  uint32_t i = atomicAdd(&c.ev_cnt[q], 1u);
   if (i >= c.ev_cap) { set_err(c, ERR_EVENTS); return; }
+  i += q * c.ev_cap;
   swim_event e;
   e.tick = c.T;
   e.viewer = v;
@@ -502,10 +509,10 @@ __device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
   uint64_t ms = (uint64_t)c.suspicion_mult * (uint64_t)ceil_log2(mem(c, v).table_size) * (uint64_t)c.ping_interval;
   uint64_t deadline = c.T + ms / c.tick_ms;
   *ap = (a & 0xfu) | A_HAS_TIMER | ((uint32_t)(deadline & SWIM_DEADLINE_MASK) << 4);
-  uint32_t b = (uint32_t)(deadline & c.wheel_mask);
-  uint32_t i = atomicAdd(&c.wheel_cnt[b], 1u);
-  if (i >= c.wheel_cap) { set_err(c, ERR_WHEEL); return; }
-  c.wheel[(size_t)b * c.wheel_cap + i] = ((uint64_t)v << 32) | s;
+  const uint32_t b = (uint32_t)(deadline & c.wheel_mask), q = subq(), qcap = c.wheel_cap / SUBQ;
+  const uint32_t i = atomicAdd(&c.wheel_cnt[b * SUBQ + q], 1u);
+  if (i >= qcap) { set_err(c, ERR_WHEEL); return; }
+  c.wheel[(size_t)b * c.wheel_cap + (size_t)q * qcap + i] = ((uint64_t)v << 32) | s;
 }
 
 // ------------------------------------------------------------------------------- metadata fetch

@@ -17,7 +17,7 @@ namespace swimdev {
 
 // per-tick scratch counters, zeroed by one hipMemsetAsync at the start of every tick
 struct Counters {
-  uint32_t msg_total, msg_recv_cnt, msg_cursor;
+  uint32_t msg_total, msg_cursor, pad0;
   uint32_t req_total, req_recv_cnt, req_cursor;
   uint32_t ack_total, ack_recv_cnt, ack_cursor;
   uint32_t ins_total, ins_list_cnt;    // list inserts of the gossip phase
@@ -55,7 +55,6 @@ struct Bufs {
   uint32_t msg_cap;
   uint32_t* msg_cnt;   // per receiver
   uint32_t* msg_start;
-  uint32_t* msg_recv;  // receivers with messages
   SyncReq* reqs;
   SyncReq* reqs_out;
   uint32_t req_cap;
@@ -205,12 +204,20 @@ __global__ void k_start_joins(KP) {
 __global__ void k_timers(KP) {
   const Ctx c = pctx(P, T);
   const uint32_t bucket = (uint32_t)(T & c.wheel_mask);
-  const uint32_t cnt = min(c.wheel_cnt[bucket], c.wheel_cap);
+  const uint32_t qcap = c.wheel_cap / SUBQ;
+  uint32_t qcnt[SUBQ], cnt = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < SUBQ; ++q) {
+    qcnt[q] = min(c.wheel_cnt[bucket * SUBQ + q], qcap);
+    cnt += qcnt[q];
+  }
   const uint64_t* ent = c.wheel + (size_t)bucket * c.wheel_cap;
   const uint32_t tmask = (uint32_t)(c.T & SWIM_DEADLINE_MASK);
   unsigned long long fired = 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
-    uint64_t e = ent[i];
+    uint32_t q = 0, j = i;  // i-th entry of the concatenated sub-queues
+    while (j >= qcnt[q]) j -= qcnt[q++];
+    uint64_t e = ent[(size_t)q * qcap + j];
     uint32_t v = (uint32_t)(e >> 32), s = (uint32_t)e;
     if (!c.up[v]) continue;
     uint32_t* ap = aux_row(c, v) + s;
@@ -384,7 +391,7 @@ __global__ void __launch_bounds__(256) k_fd(KP) {
   const uint32_t bucket = (uint32_t)(T & c.wheel_mask);
   __shared__ uint32_t s_list[256];
   __shared__ uint32_t s_cnt;
-  if (blockIdx.x == 0 && threadIdx.x == 0) c.wheel_cnt[bucket] = 0;  // k_timers drained the bucket
+  if (blockIdx.x == 0 && threadIdx.x < SUBQ) c.wheel_cnt[bucket * SUBQ + threadIdx.x] = 0;  // k_timers drained it
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -430,7 +437,6 @@ __device__ inline void deliver_local_msg(const Ctx& c, const Bufs& b, GMsgFull m
   const uint32_t i = atomicAdd(&b.k->msg_total, 1u);
   if (i >= b.msg_cap) { set_err(c, ERR_MSGS); return; }
   msg.slot = atomicAdd(&b.msg_cnt[msg.to - c.lo], 1u);
-  if (msg.slot == 0) b.msg_recv[atomicAdd(&b.k->msg_recv_cnt, 1u)] = msg.to;
   b.msgs[i] = msg;
 }
 
@@ -445,8 +451,17 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 // spread over the lanes — loss draws and receiver-collector probes of 64 pairs in flight together,
 // one enqueue atomic per (target, pass) — then the order-preserving sweep and the futures.
 constexpr int EMIT_WAVES = 4;
+// message slots are reserved in per-wave chunks (cb, cl: chunk base / slots left, wave-uniform); a
+// pass fills the chunk's remainder and continues in a fresh chunk, so only the wave's last
+// remainder is left over, marked as holes (to = NONE) that k_scatter_msgs skips
+constexpr uint32_t EMIT_CHUNK = 128;
+__device__ inline void emit_mark_holes(const Bufs& b, uint32_t cb, uint32_t cl, uint32_t lane) {
+  for (uint32_t i = lane; i < cl; i += 64)
+    if (cb + i < b.msg_cap) b.msgs[cb + i].to = NONE;
+}
 __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs& b, uint32_t v, uint64_t period,
-                                                        uint32_t glen, uint32_t lane, uint32_t* s_t) {
+                                                        uint32_t glen, uint32_t lane, uint32_t* s_t, uint32_t& cb,
+                                                        uint32_t& cl) {
   MemberDev& m = mem(c, v);
   const uint32_t rlen = m.remote_len;
   const uint32_t F = (uint32_t)c.fanout;
@@ -489,32 +504,52 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     }
     nmsg += send ? 1u : 0u;
     if (!__ballot(mat)) continue;
-    // one enqueue per target present in this pass: lane jj issues target jj's atomics
-    uint32_t base = 0, slot = 0, cnt_mine = 0, pre = 0;
+    // one enqueue per target present in this pass: lane jj issues target jj's receiver atomic; the
+    // message slots of this shard's targets come out of the wave's chunk
+    uint32_t base = 0, slot = 0, cnt_mine = 0, pre = 0, loc_off = 0, loc_tot = 0;
     for (uint32_t jj = 0; jj < nt; ++jj) {
       const uint64_t mk = __ballot(mat && j == jj);
-      if (lane == jj) cnt_mine = (uint32_t)__popcll(mk);
+      const uint32_t cj = (uint32_t)__popcll(mk);
+      if (lane == jj) cnt_mine = cj;
       if (j == jj) pre = lanes_below(mk);
+      if (owned(c, s_t[1 + jj])) {
+        if (lane == jj) loc_off = loc_tot;
+        loc_tot += cj;
+      }
+    }
+    uint32_t nb = 0, want = 0;
+    if (loc_tot > cl) {
+      want = loc_tot - cl > EMIT_CHUNK ? loc_tot - cl : EMIT_CHUNK;
+      if (lane == 0) nb = atomicAdd(&b.k->msg_total, want);
+      nb = __shfl(nb, 0, 64);
     }
     if (lane < nt && cnt_mine) {
       const uint32_t tj = s_t[1 + lane];
       if (owned(c, tj)) {
-        base = atomicAdd(&b.k->msg_total, cnt_mine);
+        base = loc_off;  // index in this pass's local sequence; mapped to a slot below
         slot = atomicAdd(&b.msg_cnt[tj - c.lo], cnt_mine);
-        if (slot == 0) b.msg_recv[atomicAdd(&b.k->msg_recv_cnt, 1u)] = tj;
       } else {
         base = atomicAdd(&b.x->msg[owner(c, tj)], cnt_mine);
       }
     }
     base = __shfl(base, (int)j, 64);
     slot = __shfl(slot, (int)j, 64);
+    const uint32_t seq_i = base + pre;  // local messages: position in the pass's sequence
+    const uint32_t loc_slot = seq_i < cl ? cb + seq_i : nb + (seq_i - cl);
+    if (loc_tot > cl) {
+      cb = nb + (loc_tot - cl);
+      cl = want - (loc_tot - cl);
+    } else {
+      cb += loc_tot;
+      cl -= loc_tot;
+    }
     if (mat) {
       GMsgFull msg;
       msg.to = t; msg.from = v; msg.pos = p; msg.slot = slot + pre;
       msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
       msg.inc = g.inc; msg.pad[0] = msg.pad[1] = msg.pad[2] = 0;
       if (owned(c, t)) {
-        if (base + pre < b.msg_cap) b.msgs[base + pre] = msg; else set_err(c, ERR_MSGS);
+        if (loc_slot < b.msg_cap) b.msgs[loc_slot] = msg; else set_err(c, ERR_MSGS);
       } else {
         const uint32_t d = owner(c, t);
         if (base + pre < b.tx_msg_cap) b.tx_msgs[(size_t)d * b.tx_msg_cap + base + pre] = msg; else set_err(c, ERR_MSGS);
@@ -561,18 +596,27 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
 
 // doSpreadGossip's first steps for every due sender, one thread each: period++ (:143) and, when it
 // holds live gossips (:149-151), a place in the round's sender list
+// (launched with a multiple of 64 threads per block: the list append is one atomic per wave)
 __global__ void k_gossip_round(KP) {
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= c.nl) return;
-  MemberDev& m = c.mem[i];
-  if (!gossip_due(c, c.lo + i, m)) return;
-  const uint64_t period = m.g_period;
-  m.g_period = period + 1;
-  m.period_used = period;
-  if (m.gossip_len == 0) return;  // no target selection, no shuffle draw
-  b.senders[atomicAdd(&b.k->sender_cnt, 1u)] = i;
+  bool busy = false;
+  if (i < c.nl) {
+    MemberDev& m = c.mem[i];
+    if (gossip_due(c, c.lo + i, m)) {
+      const uint64_t period = m.g_period;
+      m.g_period = period + 1;
+      m.period_used = period;
+      busy = m.gossip_len != 0;  // else no target selection, no shuffle draw
+    }
+  }
+  const uint64_t mk = __ballot(busy);
+  if (!mk) return;
+  uint32_t base = 0;
+  if ((threadIdx.x & 63) == 0) base = atomicAdd(&b.k->sender_cnt, (uint32_t)__popcll(mk));
+  base = __shfl(base, 0, 64);
+  if (busy) b.senders[base + lanes_below(mk)] = i;
 }
 
 // the rest of the round for the listed senders: one sender per wave at a time
@@ -583,11 +627,13 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP) {
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t ns = b.k->sender_cnt;
   unsigned long long nmsg = 0;
+  uint32_t cb = 0, cl = 0;
   for (uint32_t k = __builtin_amdgcn_readfirstlane(blockIdx.x * EMIT_WAVES + wv); k < ns; k += gridDim.x * EMIT_WAVES) {
     const uint32_t i = b.senders[k];
     const MemberDev& m = c.mem[i];
-    nmsg += gossip_emit_sender(c, b, c.lo + i, m.g_period - 1, m.gossip_len, lane, s_t[wv]);
+    nmsg += gossip_emit_sender(c, b, c.lo + i, m.g_period - 1, m.gossip_len, lane, s_t[wv], cb, cl);
   }
+  emit_mark_holes(b, cb, cl, lane);
   wave_stat_add(c, ST_GOSSIP_MESSAGES, nmsg);
 }
 
@@ -603,13 +649,22 @@ __global__ void k_recv_msgs(KP, uint32_t nrx) {
   }
 }
 
-// group-by-receiver: region start per receiver, then scatter by (start + arrival slot)
-__global__ void k_alloc(const uint32_t* list, const uint32_t* list_cnt, const uint32_t* cnt, uint32_t* start,
-                        uint32_t* cursor, uint32_t lo) {
-  const uint32_t n = *list_cnt;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    uint32_t r = list[i] - lo;
-    start[r] = atomicAdd(cursor, cnt[r]);
+// group-by-receiver: region start per receiver (a workgroup scan of 256 receivers' counts and one
+// cursor atomic per workgroup), then scatter by (start + arrival slot)
+__global__ void __launch_bounds__(256) k_alloc(KP) {
+  __shared__ uint32_t s_wave[256 / 64 + 1];
+  __shared__ uint32_t s_base;
+  const Bufs b = P->b;
+  const uint32_t nl = P->c.nl;
+  for (uint32_t base = blockIdx.x * 256; base < nl; base += gridDim.x * 256) {
+    const uint32_t r = base + threadIdx.x;
+    const uint32_t k = r < nl ? b.msg_cnt[r] : 0u;
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan<256>(k, s_wave, &total);
+    if (threadIdx.x == 0) s_base = total ? atomicAdd(&b.k->msg_cursor, total) : 0u;
+    __syncthreads();
+    if (k) b.msg_start[r] = s_base + off;
+    __syncthreads();
   }
 }
 
@@ -619,6 +674,7 @@ __global__ void k_scatter_msgs(KP) {
   const uint32_t n = min(b.k->msg_total, b.msg_cap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const GMsgFull m = b.msgs[i];
+    if (m.to == NONE) continue;  // a hole of a wave's slot chunk (k_gossip_emit)
     const uint64_t at = (uint64_t)b.msg_start[m.to - lo] + m.slot;
     if (at < b.msg_cap) b.msgs_out[at] = m;  // beyond: the buffer overflowed (ERR_MSGS is set)
   }
@@ -722,11 +778,11 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) s_nbig = 0;
   __syncthreads();
-  const uint32_t nrecv = b.k->msg_recv_cnt;
   unsigned long long acc = 0;
-  for (uint32_t i = blockIdx.x * DLV_BLOCK + tid; i < nrecv; i += gridDim.x * DLV_BLOCK) {
-    const uint32_t r = b.msg_recv[i];
-    const uint32_t k = b.msg_cnt[r - c.lo];
+  for (uint32_t i = blockIdx.x * DLV_BLOCK + tid; i < c.nl; i += gridDim.x * DLV_BLOCK) {
+    const uint32_t k = b.msg_cnt[i];
+    if (k == 0) continue;
+    const uint32_t r = c.lo + i;
     const uint32_t start = b.msg_start[r - c.lo];
     b.msg_cnt[r - c.lo] = 0;
     if (!c.up[r]) continue;
