@@ -181,7 +181,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "u64",
+        "dtype": "u32",
         "data": "synthetic",
         "config": {"workload": f"config4-lan-{args.workload}: N={n} members (one cluster), LAN defaults (ping 1 s / "
                                f"gossip 200 ms / sync 30 s staggered), 0% loss, "
@@ -197,7 +197,8 @@ def main():
                      "traffic_source": traffic_src,
                      "launches": prof["launches"], "avg_launch_ms": avg_ms,
                      "alg_bytes_per_launch": prof["alg_bytes"] / max(1, prof["launches"]),
-                     "kernel_time_share": prof["total_ms"] / (dt * 1e3 * world)},
+                     # classify runs twice per tick (SYNC, SYNC_ACK); launches are sampled 1 in 7
+                     "kernel_time_share": avg_ms * 2 * e.now()[2] / (dt * 1e3 / args.steps)},
         "stats": {k: stats[k] for k in ("syncs", "sync_records", "gossip_messages", "gossips_created", "pings",
                                          "timers_fired", "events")},
     }
