@@ -130,6 +130,9 @@ def catalog() -> list[Scenario]:
     ]
 
 
+CONFIG2_MEMBERS = list(range(0, 1024, 37)) + [17, 18, 255, 256, 1023]  # rows compared at N = 1,024
+
+
 def config2() -> Scenario:
     """BASELINE config 2: 1,024 members, 0 % loss, kill member 17 at period 10, 150 periods."""
     return Scenario("config2_1024", 1024, 1024, 1500, seed=2, ops=[(100, "kill", 17)], check_every=100)

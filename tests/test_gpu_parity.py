@@ -107,3 +107,28 @@ def test_gpu_sharded_parity_config2_1024(glib, olib):
     sc = dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": 4})
     members = list(range(0, 1024, 37)) + [17, 18, 255, 256, 1023]
     _run_parity(glib, olib, sc, members=members, collectors=False)
+
+
+# ---- committed regression digests (tests/golden/scenario_digests.json, made by the CPU oracle):
+# the GPU engine, unsharded and with 4 in-process shards, reproduces them
+@pytest.mark.parametrize("shards", [1, 4])
+@pytest.mark.parametrize("sc", scenarios.catalog() + [scenarios.config2()], ids=lambda s: s.name)
+def test_gpu_matches_golden_digest(glib, sc, shards):
+    import json
+    import os
+
+    from make_scenario_digests import digest, event_digest
+    golden = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "scenario_digests.json")))
+    want = golden["scenarios"][sc.name]
+    if shards > sc.capacity:
+        pytest.skip("more shards than members")
+    sc2 = dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": shards})
+    e = scenarios.make_engine(glib, sc2)
+    scenarios.run(e, sc2)
+    ev = e.drain_events()
+    big = sc.name == "config2_1024"
+    got_state = digest(e, scenarios.CONFIG2_MEMBERS if big else None, not big)
+    st = e.stats()
+    assert event_digest(ev) == want["events_sha256"] and len(ev) == want["events"]
+    assert {k: int(st[k]) for k in want["stats"]} == want["stats"]
+    assert got_state == want["state_sha256"]
