@@ -120,7 +120,10 @@ typedef struct swim_config {
   int32_t local_shards;       /* swim_create only: > 1 runs the cluster as this many row shards in
                                  one process on `device`, exchanging cross-shard messages with
                                  device copies (the single-GPU test rig of swim_create_shard) */
-  uint32_t reserved[6];
+  int32_t timer_stagger;      /* 1 = each initial member's ping and gossip timers also get a random
+                                 phase (members of a real cluster start at different instants; the
+                                 default 0 aligns them) */
+  uint32_t reserved[5];
 } swim_config;
 
 /* preset: 0 = defaultConfig/defaultLanConfig, 1 = defaultWanConfig, 2 = defaultLocalConfig

@@ -21,6 +21,8 @@
 #define SWIM_STREAM_INIT_PING 1        /* shuffle of the initial ping list, sub32 = i        */
 #define SWIM_STREAM_INIT_REMOTE 2      /* shuffle of the initial gossip remote list          */
 #define SWIM_STREAM_INIT_SYNC_PHASE 3  /* periodic-SYNC phase offset when sync_stagger = 1  */
+#define SWIM_STREAM_INIT_FD_PHASE 4    /* ping-timer phase offset when timer_stagger = 1    */
+#define SWIM_STREAM_INIT_GOSSIP_PHASE 5/* gossip-timer phase offset when timer_stagger = 1  */
 /* failure detector (issuer-keyed: member = issuer) */
 #define SWIM_STREAM_FD_SHUFFLE 10      /* Collections.shuffle(pingMembers), sub32 = i         */
 #define SWIM_STREAM_PING_OUT 11        /* PING issuer -> target outbound loss                 */

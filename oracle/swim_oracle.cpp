@@ -1030,6 +1030,10 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
       mv.remote_index = 0;
       mv.sync_on = true;
       mv.sync_start = c.sync_stagger ? -(int64_t)next_int(e->draw(v, SWIM_STREAM_INIT_SYNC_PHASE, 0, 0, 0), e->S) : 0;
+      if (c.timer_stagger) {  // members of a real cluster start at different instants
+        mv.fd_start = -(int64_t)next_int(e->draw(v, SWIM_STREAM_INIT_FD_PHASE, 0, 0, 0), e->P);
+        mv.g_start = -(int64_t)next_int(e->draw(v, SWIM_STREAM_INIT_GOSSIP_PHASE, 0, 0, 0), e->G);
+      }
     }
   };
   unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));

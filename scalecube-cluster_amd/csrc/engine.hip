@@ -696,7 +696,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.T = 0;
   if (nl) {
     k_init_rows<<<std::min<uint32_t>(nl, 65535), 256, 0, s>>>(c, n_initial);
-    k_init_members<<<grid_for(nl, 64), 64, 0, s>>>(c, n_initial, cf.sync_stagger);
+    k_init_members<<<grid_for(nl, 64), 64, 0, s>>>(c, n_initial, cf.sync_stagger, cf.timer_stagger);
   }
   return SWIM_OK;
 }
@@ -758,7 +758,7 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
     std::memcpy(&id, comm_id, sizeof(id));
     if (nccl_ok(ncclCommInitRank(&e->comm, world, id, rank)) != SWIM_OK) { delete e; return SWIM_EDEVICE; }
   }
-  e->g_residue.assign(e->G, 0);
+  e->g_residue.assign(e->G, cf.timer_stagger ? 1 : 0);  // staggered gossip timers use every residue
   e->g_residue[0] = 1;
   e->is_seed_h.assign(capacity, 0);
   e->joined_h.assign(capacity, 0);

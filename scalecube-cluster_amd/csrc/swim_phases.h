@@ -118,7 +118,7 @@ __global__ void k_init_rows(Ctx c, uint32_t n_initial) {
 }
 
 // initial members: converged state, seeded Fisher-Yates ping / remote lists
-__global__ void k_init_members(Ctx c, uint32_t n_initial, int32_t sync_stagger) {
+__global__ void k_init_members(Ctx c, uint32_t n_initial, int32_t sync_stagger, int32_t timer_stagger) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= c.nl) return;
   const uint32_t v = c.lo + i;
@@ -149,6 +149,10 @@ __global__ void k_init_members(Ctx c, uint32_t n_initial, int32_t sync_stagger) 
     m.remote_idx = 0;
     m.sync_on = 1;
     m.sync_start = sync_stagger ? -(int64_t)next_int(draw_at(c, v, 0, SWIM_STREAM_INIT_SYNC_PHASE, 0, 0), c.S) : 0;
+    if (timer_stagger) {
+      m.fd_start = -(int64_t)next_int(draw_at(c, v, 0, SWIM_STREAM_INIT_FD_PHASE, 0, 0), c.P);
+      m.g_start = -(int64_t)next_int(draw_at(c, v, 0, SWIM_STREAM_INIT_GOSSIP_PHASE, 0, 0), c.G);
+    }
   }
   c.mem[i] = m;
 }

@@ -61,7 +61,8 @@ class swim_config(C.Structure):
         ("event_capacity", C.c_uint32),
         ("device", C.c_int32),
         ("local_shards", C.c_int32),
-        ("reserved", C.c_uint32 * 6),
+        ("timer_stagger", C.c_int32),
+        ("reserved", C.c_uint32 * 5),
     ]
 
 
