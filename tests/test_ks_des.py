@@ -3,7 +3,7 @@ reference-timing DES (north_star; SURVEY.md §8 "KS": two-sample KS, pass at p >
 
 Lockstep runs use `timer_stagger = 1` (independent ping / gossip timer phases per member, as in a
 cluster whose members started at different instants) and a 10 ms tick, the resolution at which the
-lockstep order is a faithful discretisation of the asynchronous reference.  The
+lockstep order is a faithful discretisation of the asynchronous reference ("Distributional parity").  The
 aligned default (every member's timers in phase, 100 ms tick) is the throughput mode; the last CPU
 test pins that it is NOT distributionally equivalent (each gossip hop costs a full gossip interval
 instead of a uniform fraction of one), so nobody reads the aligned mode's latencies as reference
