@@ -293,17 +293,17 @@ int32_t swim_read_collector(swim_engine* e, uint32_t m, uint32_t gossiper, swim_
                             uint32_t cap, uint32_t* len);
 
 /* ---- measurement ---------------------------------------------------------------------------
- * Per-kernel timing of the SYNC classification kernel (k_sync_classify, the dominant HBM stream),
- * measured with HIP events recorded on the engine's own stream around one launch in seven (an event
- * pair drains the stream, so timing every launch would distort the run being measured).  For those
- * sampled launches: `launches`, `total_ms`, `messages` / `records` they processed, and `alg_bytes`:
- * per merged SYNC / SYNC_ACK message the record words of the content row and of the receiver row
- * (2 x N x 4 B) plus 4 B per record routed to the sequential merge.  enable = 0 stops recording; enable = 1
+ * Per-kernel timing of the SYNC classification kernel (k_sync_classify, the dominant HBM stream:
+ * it classifies every SYNC and, from the same loads, the SYNC_ACK answering it), measured with HIP
+ * events bound to one launch in three on the engine's own stream.  For those sampled launches:
+ * `launches`, `total_ms`, `messages` / `records` they processed, and `alg_bytes`: per streamed
+ * message the record words of the content row and of the receiver row (2 x N x 4 B) plus 4 B per
+ * record routed to the sequential merge.  enable = 0 stops recording; enable = 1
  * (re)starts it from zero.  The CPU oracle reports zeros. */
 typedef struct swim_kernel_profile {
   uint64_t launches;
   double total_ms;
-  uint64_t messages;   /* SYNC + SYNC_ACK messages merged */
+  uint64_t messages;   /* SYNC messages whose two rows were streamed */
   uint64_t records;    /* records that changed a table (sequential merge path) */
   uint64_t alg_bytes;
 } swim_kernel_profile;

@@ -14,6 +14,7 @@
 // unsharded engine never synchronises inside a tick; a sharded one synchronises once per exchange
 // (gossip round, SYNC, SYNC_ACK) to learn the per-destination counts.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -33,7 +34,7 @@ constexpr uint32_t kClassifyGrid = 1024;  // 4,096 waves: the resident capacity 
 constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
 constexpr uint32_t kEmitGrid = 2048;      // 8,192 waves, one gossip sender at a time each
 constexpr uint32_t kStopCap = 4096;
-constexpr uint32_t kProfEvery = 7;  // odd: samples alternate between the SYNC and SYNC_ACK launches
+constexpr uint32_t kProfEvery = 3;  // SYNC classify launches between timed ones
 
 uint32_t gcd_u(uint32_t a, uint32_t b) {
   while (b) { uint32_t t = a % b; a = b; b = t; }
@@ -200,16 +201,23 @@ static void prof_flush(Shard& s) {
   s.prof_used = 0;
 }
 
-// HIP events are recorded around one classify launch in kProfEvery: an event pair drains the
-// stream (measured ~6 us bubble each side), so timing every launch would distort the timed region
+// The SYNC classify launch (the HBM stream) is timed by HIP events bound to the dispatch itself
+// (hipExtLaunchKernelGGL: the kernel's own start / completion timestamps, no extra stream packets),
+// one launch in kProfEvery.  The SYNC_ACK launch is a separate kernel (k_ack_classify).
 static void launch_classify(swim_engine* e, Shard& s, int d2) {
-  const bool p = e->prof && (s.prof_seen++ % kProfEvery) == 0 && 2 * (s.prof_used + 1) <= s.prof_ev.size();
-  if (p) hipEventRecord(s.prof_ev[2 * s.prof_used], e->stream);
-  k_sync_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(s.d_par, e->T, d2, p ? s.prof_slots + 2 * s.prof_used : nullptr);
-  if (p) {
-    hipEventRecord(s.prof_ev[2 * s.prof_used + 1], e->stream);
-    s.prof_used++;
+  if (d2) {
+    k_ack_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(s.d_par, e->T);
+    return;
   }
+  const bool p = e->prof && (s.prof_seen++ % kProfEvery) == 0 && 2 * (s.prof_used + 1) <= s.prof_ev.size();
+  if (!p) {
+    k_sync_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(s.d_par, e->T, nullptr);
+    return;
+  }
+  hipExtLaunchKernelGGL(k_sync_classify, dim3(kClassifyGrid), dim3(CLS_BLOCK), 0, e->stream,
+                        s.prof_ev[2 * s.prof_used], s.prof_ev[2 * s.prof_used + 1], 0, s.d_par, e->T,
+                        s.prof_slots + 2 * s.prof_used);
+  s.prof_used++;
 }
 
 static int32_t sync_and_collect(swim_engine* e) {
@@ -510,9 +518,13 @@ static int32_t run_tick(swim_engine* e) {
       if (multi) sync_params(e, sd);
       if (sd.n_rx_reqs)
         k_recv_sync<<<std::min<uint32_t>(grid_for(sd.n_rx_reqs, 256), 256), 256, 0, s>>>(sd.d_par, T, d2, sd.n_rx_reqs);
-      k_sync_prep<<<1, 1024, 0, s>>>(sd.d_par, T, d2);
-      launch_classify(e, sd, d2);
-      k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(sd.d_par, T, d2);
+      // SYNC_ACK: an unsharded engine classifies its acks inside k_sync_apply (every ack is local,
+      // and almost all reuse the SYNC launch's reverse classification); a sharded one streams the
+      // acks that arrived with their rows from other shards
+      const int classified = d2 == 0 || multi;
+      k_sync_prep<<<1, 1024, 0, s>>>(sd.d_par, T, d2, !classified);
+      if (classified) launch_classify(e, sd, d2);
+      k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(sd.d_par, T, d2, classified);
     }
   }
   for (Shard& sd : e->sh) {
@@ -662,6 +674,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&b.snap, (size_t)b.snap_cap * n) && sd.alloc(&b.snap_idx, nl) && sd.alloc(&b.snap_list, b.snap_cap) &&
             sd.alloc(&b.snap_cnt, 1) && sd.alloc(&b.item_chunk, (size_t)b.req_cap * b.chunks) &&
             sd.alloc(&b.item_total, b.req_cap) && sd.alloc(&b.pool, b.pool_cap) &&
+            sd.alloc(&b.rev_chunk, (size_t)b.req_cap * b.chunks) && sd.alloc(&b.rev_total, b.req_cap) &&
+            sd.alloc(&b.row_mod, nl) &&
             sd.alloc(&b.pend, (size_t)kApplyGrid * n) && sd.alloc(&sd.d_par, 1) && sd.alloc(&b.senders, nl);
   if (ok && multi)
     ok = sd.alloc(&b.tx_msgs, (size_t)e->world * b.tx_msg_cap) && sd.alloc(&b.tx_reqs, (size_t)e->world * b.tx_req_cap) &&
@@ -692,6 +706,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(b.req_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.ack_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.snap_idx, 0xff, 4 * (size_t)nl, s);
+  hipMemsetAsync(b.row_mod, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.snap_cnt, 0, 4, s);
   c.T = 0;
   if (nl) {

@@ -95,7 +95,7 @@ struct GMsgFull {
 
 struct SyncReq {  // SYNC (request) or SYNC_ACK
   uint32_t from, to, ordinal, slot;
-  uint32_t flags;    // bit0 initial, bit1 outfail, bit2 delivered
+  uint32_t flags;    // bit0 initial, bit1 outfail, bit2 delivered; bits 8..31 record count (RQ_RECS_SHIFT)
   uint32_t content;  // NONE: `from` is owned here (row / snapshot); else index into the received rows
   uint32_t snap;     // k_sync_prep: snapshot slot of `from`'s row in this sub-phase, or NONE
   uint32_t pad;

@@ -74,6 +74,11 @@ struct Bufs {
   uint64_t* pend;       // per sync-apply workgroup: pending ALIVE admissions
   uint2* item_chunk;    // per (message, chunk): (pool base, complex count)
   uint32_t* item_total; // per message: complex count over all chunks
+  // SYNC_ACK reuse: the SYNC classify also classifies the reverse direction of every
+  // local message (its SYNC_ACK compares the same two rows with the roles swapped)
+  uint2* rev_chunk;     // per (SYNC message, chunk): reverse (pool base, complex count)
+  uint32_t* rev_total;  // per SYNC message: reverse complex count
+  uint32_t* row_mod;    // per owned viewer: tick whose SYNC merge may have changed the row
   uint32_t* senders;    // local indices of this round's senders with live gossips
   uint32_t* pool;       // subjects whose record may change the receiver, chunk-ordered
   uint32_t pool_cap;
@@ -925,7 +930,9 @@ __device__ inline uint32_t select_sync_address(const Ctx& c, uint32_t v) {
   return NONE;
 }
 
-enum : uint32_t { RQ_INITIAL = 1, RQ_OUTFAIL = 2, RQ_DELIVERED = 4 };
+// SyncReq.flags: bits 0..2 below; bits 8..31 the number of records the message carries (the
+// sender's table size when the message is prepared: the count syncMembership iterates, :491-509)
+enum : uint32_t { RQ_INITIAL = 1, RQ_OUTFAIL = 2, RQ_DELIVERED = 4, RQ_RECS_SHIFT = 8 };
 
 // a delivered SYNC / SYNC_ACK joins its receiver's inbox (the receiver is owned by this shard)
 __device__ inline void enqueue_sync(const Ctx& c, SyncReq q, SyncReq* items, uint32_t* total, uint32_t* cnt,
@@ -940,7 +947,8 @@ __device__ inline void enqueue_sync(const Ctx& c, SyncReq q, SyncReq* items, uin
 __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t to, uint32_t ordinal, bool initial) {
   MemberDev& m = mem(c, v);
   SyncReq q;
-  q.from = v; q.to = to; q.ordinal = ordinal; q.slot = 0; q.flags = initial ? RQ_INITIAL : 0;
+  q.from = v; q.to = to; q.ordinal = ordinal; q.slot = 0;
+  q.flags = (initial ? RQ_INITIAL : 0) | (m.table_size << RQ_RECS_SHIFT);
   q.content = NONE; q.snap = NONE; q.pad = 0;
   if (initial) m.init_total++;
   if (out_fail(c, v, to, v, SWIM_STREAM_SYNC_OUT, ordinal, 0)) {

@@ -17,6 +17,12 @@
 //                    admissions whose metadata fetch succeeded; a later message to a receiver whose
 //                    row already changed this sub-phase is re-classified in-workgroup.
 
+#ifndef CLS_MINWAVES
+#define CLS_MINWAVES 4  // waves per SIMD the classify kernels are register-limited to
+#endif
+#ifndef CLS_REV
+#define CLS_REV 1       // SYNC classify also classifies the reverse (SYNC_ACK) direction
+#endif
 constexpr int SYNC_CHUNK = 1024;                 // subjects per classify unit (one wave)
 constexpr int CLS_BLOCK = 256;
 constexpr int CLS_LOADS = SYNC_CHUNK / 256;      // 16-B record loads per lane per row
@@ -113,18 +119,30 @@ __device__ __forceinline__ const uint32_t* sync_content(const Ctx& c, const Bufs
   return si < b.snap_cap ? b.snap + (size_t)si * c.n : rec_row(c, q.from);
 }
 
-__global__ void __launch_bounds__(1024) k_sync_prep(KP, int d2) {
-  const Ctx c = pctx_sync(P, T);
-  const Bufs b = P->b;
+// k_sync_prep: the sub-phase's delivered messages -> one contiguous inbox per receiver in canonical
+// (sender, ordinal) order, snapshot claims for senders that are merged into in the same sub-phase.
+// Messages are staged in LDS (receivers found through an LDS hash, inbox order sorted as LDS index
+// permutations), so the single workgroup makes ~3 dependent rounds of global accesses instead of
+// one per step; sub-phases larger than the LDS stage take the global path.
+constexpr uint32_t PREP_CAP = 2048;    // messages (and receivers) staged in LDS
+constexpr uint32_t PREP_HASH = 4096;   // receiver hash slots (power of two, >= 2 x PREP_CAP)
+constexpr int PREP_BLOCK = 1024;
+
+__device__ __forceinline__ uint32_t prep_slot(uint32_t id) { return (id * 2654435761u) >> 20; }  // 12 bits
+
+__device__ __forceinline__ uint32_t prep_find(const uint32_t* hkey, const uint32_t* hval, uint32_t id) {
+  for (uint32_t h = prep_slot(id);; h = (h + 1) & (PREP_HASH - 1)) {
+    const uint32_t k = hkey[h];
+    if (k == id) return hval[h];
+    if (k == NONE) return NONE;
+  }
+}
+
+__device__ void sync_prep_global(const Ctx& c, const Bufs& b, const SubPhase& p, int d2) {
   __shared__ uint32_t s_cursor;
-  const SubPhase p = sub_phase(b, d2);
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
-  // release the previous sub-phase's snapshot claims
-  const uint32_t prev = min(*b.snap_cnt, b.snap_cap);
-  for (uint32_t i = tid; i < prev; i += nt) b.snap_idx[b.snap_list[i] - c.lo] = NONE;
   if (tid == 0) s_cursor = 0;
   __syncthreads();
-  if (tid == 0) *b.snap_cnt = 0;
   // one contiguous inbox per receiver
   for (uint32_t i = tid; i < p.nrecv; i += nt) {
     const uint32_t r = p.recv[i] - c.lo;
@@ -144,10 +162,11 @@ __global__ void __launch_bounds__(1024) k_sync_prep(KP, int d2) {
   }
   __syncthreads();
   // message content = the sender's table when the message was prepared: a sender that is itself
-  // merged into during this sub-phase gets its row snapshotted by k_sync_classify
+  // merged into during this sub-phase gets its row snapshotted
   const uint32_t ni = s_cursor;
   for (uint32_t i = tid; i < ni; i += nt) {
     b.item_total[i] = 0;
+    if (!d2) b.rev_total[i] = 0;
     if (p.out[i].content != NONE) continue;  // content arrived from another shard: already a copy
     const uint32_t src = p.out[i].from, sl = src - c.lo;
     if (p.cnt[sl] == 0) continue;
@@ -167,27 +186,162 @@ __global__ void __launch_bounds__(1024) k_sync_prep(KP, int d2) {
   }
 }
 
+__device__ void sync_prep_lds(const Ctx& c, const Bufs& b, const SubPhase& p, int d2) {
+  __shared__ SyncReq s_q[PREP_CAP];          // staged messages (64 KiB)
+  __shared__ uint32_t s_perm[PREP_CAP];      // inbox position -> staged message
+  __shared__ uint32_t s_rid[PREP_CAP];       // receiver index -> member
+  __shared__ uint32_t s_start[PREP_CAP + 1]; // receiver index -> message count, then inbox start
+  __shared__ uint32_t s_snap[PREP_CAP];      // receiver index -> snapshot slot of its row
+  __shared__ uint32_t s_hkey[PREP_HASH], s_hval[PREP_HASH];
+  __shared__ uint32_t s_wave[PREP_BLOCK / 64 + 1];
+  __shared__ uint32_t s_nsnap;
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  const uint32_t ni = p.total, nr = p.nrecv;
+  for (uint32_t h = tid; h < PREP_HASH; h += nt) s_hkey[h] = NONE;
+  if (tid == 0) s_nsnap = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < ni; i += nt) s_q[i] = p.items[i];
+  for (uint32_t i = tid; i < nr; i += nt) {
+    const uint32_t id = p.recv[i];
+    s_rid[i] = id;
+    s_start[i] = p.cnt[id - c.lo];
+    s_snap[i] = NONE;
+    for (uint32_t h = prep_slot(id);; h = (h + 1) & (PREP_HASH - 1))
+      if (atomicCAS(&s_hkey[h], NONE, id) == NONE) { s_hval[h] = i; break; }
+  }
+  if (tid >= nr && tid < 2 * PREP_BLOCK) s_start[tid] = 0;  // scan padding
+  if (tid + PREP_BLOCK >= nr && tid + PREP_BLOCK < PREP_CAP) s_start[tid + PREP_BLOCK] = 0;
+  __syncthreads();
+  // inbox starts: exclusive scan of the counts, two receivers per thread
+  const uint32_t c0 = s_start[2 * tid], c1 = s_start[2 * tid + 1];
+  uint32_t total;
+  const uint32_t ex = block_exclusive_scan<PREP_BLOCK>(c0 + c1, s_wave, &total);
+  s_start[2 * tid] = ex;
+  s_start[2 * tid + 1] = ex + c0;
+  if (tid == 0) { s_start[nr] = total; *p.nitems = total; }
+  __syncthreads();
+  for (uint32_t i = tid; i < nr; i += nt) p.start[s_rid[i] - c.lo] = s_start[i];
+  for (uint32_t i = tid; i < ni; i += nt) {
+    const uint32_t ri = prep_find(s_hkey, s_hval, s_q[i].to);
+    s_perm[s_start[ri] + s_q[i].slot] = i;
+  }
+  __syncthreads();
+  // canonical order inside an inbox: (sender, ordinal)
+  for (uint32_t ri = tid; ri < nr; ri += nt) {
+    uint32_t* a = s_perm + s_start[ri];
+    const uint32_t k = s_start[ri + 1] - s_start[ri];
+    for (uint32_t x = 1; x < k; ++x) {
+      const uint32_t v = a[x];
+      const uint32_t vf = s_q[v].from, vo = s_q[v].ordinal;
+      int32_t y = (int32_t)x - 1;
+      while (y >= 0 && (s_q[a[y]].from > vf || (s_q[a[y]].from == vf && s_q[a[y]].ordinal > vo))) {
+        a[y + 1] = a[y];
+        --y;
+      }
+      a[y + 1] = v;
+    }
+  }
+  __syncthreads();
+  // snapshot claims: message content = the sender's table when the message was prepared; a sender
+  // that is itself merged into during this sub-phase gets its row snapshotted
+  for (uint32_t pos = tid; pos < total; pos += nt) {
+    const SyncReq& q = s_q[s_perm[pos]];
+    if (q.content != NONE) continue;  // content arrived from another shard: already a copy
+    const uint32_t rs = prep_find(s_hkey, s_hval, q.from);
+    if (rs == NONE || atomicCAS(&s_snap[rs], NONE, NONE - 1) != NONE) continue;
+    const uint32_t slot = atomicAdd(&s_nsnap, 1u);
+    if (slot >= b.snap_cap) { set_err(c, ERR_SNAP); s_snap[rs] = NONE; continue; }
+    s_snap[rs] = slot;
+    b.snap_list[slot] = q.from;
+    b.snap_idx[q.from - c.lo] = slot;
+  }
+  __syncthreads();
+  for (uint32_t pos = tid; pos < total; pos += nt) {
+    SyncReq q = s_q[s_perm[pos]];
+    uint32_t sn = NONE;
+    if (q.content == NONE) {
+      const uint32_t rs = prep_find(s_hkey, s_hval, q.from);
+      if (rs != NONE && s_snap[rs] < b.snap_cap) sn = s_snap[rs];
+    }
+    q.snap = sn;
+    p.out[pos] = q;
+    b.item_total[pos] = 0;
+    if (!d2) b.rev_total[pos] = 0;
+  }
+  if (tid == 0) *b.snap_cnt = min(s_nsnap, b.snap_cap);
+}
+
+// copy_snaps (SYNC_ACK sub-phase of an unsharded engine, where no classify launch streams the ack
+// rows): copy the claimed rows here, before any SYNC_ACK merge can change them
+__global__ void __launch_bounds__(PREP_BLOCK) k_sync_prep(KP, int d2, int copy_snaps) {
+  const Ctx c = pctx_sync(P, T);
+  const Bufs b = P->b;
+  const SubPhase p = sub_phase(b, d2);
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  // release the previous sub-phase's snapshot claims
+  const uint32_t prev = min(*b.snap_cnt, b.snap_cap);
+  for (uint32_t i = tid; i < prev; i += nt) b.snap_idx[b.snap_list[i] - c.lo] = NONE;
+  __syncthreads();
+  if (tid == 0) *b.snap_cnt = 0;
+  __syncthreads();
+  if (p.total <= PREP_CAP && p.nrecv <= PREP_CAP) sync_prep_lds(c, b, p, d2);
+  else sync_prep_global(c, b, p, d2);
+  if (!copy_snaps) return;
+  __syncthreads();
+  __threadfence_block();
+  const uint32_t ns = min(*b.snap_cnt, b.snap_cap), n = c.n;
+  for (uint32_t k = 0; k < ns; ++k) {
+    const uint32_t* src = rec_row(c, b.snap_list[k]);
+    uint32_t* dst = b.snap + (size_t)k * n;
+    if ((n & 3) == 0) {
+      for (uint32_t x = tid; x < n / 4; x += nt)
+        reinterpret_cast<uint4*>(dst)[x] = reinterpret_cast<const uint4*>(src)[x];
+    } else {
+      for (uint32_t x = tid; x < n; x += nt) dst[x] = src[x];
+    }
+  }
+}
+
 // One (message, chunk) unit per wave: 64 lanes x 16 subjects = SYNC_CHUNK subjects, i.e. four
 // 16-B loads of record words per lane from the content row and four from the receiver row.  Each
 // wave owns a contiguous range of units, so consecutive units share the message header (loaded once
 // per message), and walks it with a one-deep software pipeline: the next unit's rows are in flight
 // while the current one is classified.  Complex subjects are compacted into the pool in subject
 // order with a ballot and a wave scan (no workgroup barriers).
+//
+// SYNC_ACK reuse.  The SYNC_ACK answering a local SYNC s -> r merges r's row into s's row: the same
+// two rows with the roles swapped.  The SYNC launch (d2 = 0) therefore classifies both directions
+// from one load of the pair and keeps the reverse result (rev_chunk / rev_total).  The
+// SYNC_ACK launch reuses it for an ack whose two rows no SYNC merge of this tick touched (row_mod,
+// stamped by k_sync_apply), which is exact: classification is a pure function of the two rows.
 struct ClsHdr {
   const uint32_t* content;
   const uint32_t* rv;
   uint32_t* snapdst;
-  uint32_t i, r;
+  uint32_t i, r, s;
+  uint32_t rev;  // d2 = 0: 1 = also classify the reverse direction (a local SYNC)
+  uint32_t d1;   // d2 = 1: the SYNC whose reverse classification this ack reuses, or NONE
 };
 
-__device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SubPhase& p, uint32_t i, ClsHdr& h) {
-  const SyncReq q = p.out[i];
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// the header is wave-uniform: keep it in scalar registers (the row loads need the VGPRs)
+__device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SubPhase& p, int d2, uint32_t i, ClsHdr& h) {
+  SyncReq q = p.out[i];
+  q.from = uni(q.from); q.to = uni(q.to); q.content = uni(q.content); q.snap = uni(q.snap); q.pad = uni(q.pad);
   const bool remote = q.content != NONE;
   h.content = remote ? b.rx_rows + (size_t)q.content * c.n : rec_row(c, q.from);
   h.rv = rec_row(c, q.to);
   h.snapdst = q.snap < b.snap_cap ? b.snap + (size_t)q.snap * c.n : nullptr;
   h.i = i;
   h.r = q.to;
+  h.s = q.from;
+  h.rev = (CLS_REV && !d2 && !remote) ? 1u : 0u;
+  h.d1 = NONE;
+  if (d2 && q.pad != 0 && !remote) {
+    const uint32_t t = (uint32_t)c.T;
+    if (uni(b.row_mod[q.from - c.lo]) != t && uni(b.row_mod[q.to - c.lo]) != t) h.d1 = q.pad - 1;
+  }
 }
 
 __device__ __forceinline__ void cls_rows(const Ctx& c, const ClsHdr& h, uint32_t ch, uint32_t lane, uint4* a, uint4* o) {
@@ -216,8 +370,60 @@ __device__ __forceinline__ void cls_rows(const Ctx& c, const ClsHdr& h, uint32_t
   }
 }
 
-// prof (profiled launches only): {messages merged, complex records} of this launch
-__global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(KP, int d2, unsigned long long* prof) {
+// wave-uniform: compact the subjects flagged in `flags` (bit 4j+q = subject base + j*256 + 4*lane + q)
+// into the pool in subject order; returns (pool base, count)
+__device__ __forceinline__ uint2 cls_compact(const Ctx& c, const Bufs& b, uint32_t flags, uint32_t base,
+                                             uint32_t lane) {
+  if (!__ballot(flags != 0)) return make_uint2(0, 0);
+  // subject order = (j, lane, q); one wave scan of the four per-j counts
+  uint64_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < CLS_LOADS; ++j) cnt |= (uint64_t)__popc((flags >> (4 * j)) & 0xfu) << (16 * j);
+  uint64_t incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  const uint64_t tot = __shfl(incl, 63, 64);
+  const uint64_t excl = incl - cnt;
+  uint32_t t = 0, jbase[CLS_LOADS];
+#pragma unroll
+  for (int j = 0; j < CLS_LOADS; ++j) { jbase[j] = t; t += (uint32_t)(tot >> (16 * j)) & 0xffffu; }
+  uint32_t pb = 0;
+  if (lane == 0) pb = atomicAdd(&b.k->pool_cursor, t);
+  pb = __shfl(pb, 0, 64);
+  if (pb + t > b.pool_cap) {
+    if (lane == 0) set_err(c, ERR_PEND);
+    return make_uint2(pb, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < CLS_LOADS; ++j) {
+    uint32_t o2 = pb + jbase[j] + ((uint32_t)(excl >> (16 * j)) & 0xffffu);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (flags & (1u << (4 * j + q))) b.pool[o2++] = base + j * 256 + 4 * lane + q;
+  }
+  return make_uint2(pb, t);
+}
+
+__device__ __forceinline__ bool lane_holds(uint32_t subject, uint32_t base, uint32_t lane) {
+  const uint32_t off = subject - base;
+  return off < SYNC_CHUNK && ((off & 255u) >> 2) == lane;
+}
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x += __shfl_down(x, d, 64);
+  return x;
+}
+
+// D2 = 0: the SYNC launch k_sync_classify (streams every message's two rows, both directions);
+// D2 = 1: the SYNC_ACK launch k_ack_classify (reuses the SYNC launch's reverse results, streams only
+// acks whose rows changed).  prof (profiled launches only): {row pairs streamed, complex records}.
+template <int D2>
+__device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint64_t T, unsigned long long* prof) {
+  constexpr int d2 = D2;
   const Ctx c = pctx_sync(P, T);
   const Bufs b = P->b;
   const SubPhase p = sub_phase(b, d2);
@@ -228,25 +434,20 @@ __global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(KP, int d2, unsigne
   const uint32_t nw = gridDim.x * (CLS_BLOCK / 64);
   const uint64_t total = (uint64_t)ni * chunks;
   const uint32_t u0 = (uint32_t)(total * wid / nw), u1 = (uint32_t)(total * (wid + 1) / nw);
-  unsigned long long recs = 0, cplx = 0;
-  __shared__ unsigned long long s_recs[CLS_BLOCK / 64];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    stat_add(c, ST_MERGE_MSGS, ni);
-    if (prof) prof[0] = ni;
-  }
+  uint32_t cplx = 0, streamed = 0;
   if (u0 < u1) {
     ClsHdr hc, hn;
     uint4 a[CLS_LOADS], o[CLS_LOADS], an[CLS_LOADS], on[CLS_LOADS];
-    cls_hdr(c, b, p, u0 / chunks, hc);
-    cls_rows(c, hc, u0 - hc.i * chunks, lane, a, o);
+    cls_hdr(c, b, p, d2, u0 / chunks, hc);
+    if (hc.d1 == NONE || hc.snapdst) cls_rows(c, hc, u0 - hc.i * chunks, lane, a, o);
     hn = hc;
     for (uint32_t u = u0; u < u1; ++u) {
       const uint32_t ch = u - hc.i * chunks;
       const bool more = u + 1 < u1;
       if (more) {
         const uint32_t i2 = (u + 1) / chunks;
-        if (i2 != hn.i) cls_hdr(c, b, p, i2, hn);
-        cls_rows(c, hn, u + 1 - i2 * chunks, lane, an, on);
+        if (i2 != hn.i) cls_hdr(c, b, p, d2, i2, hn);
+        if (hn.d1 == NONE || hn.snapdst) cls_rows(c, hn, u + 1 - i2 * chunks, lane, an, on);
       }
       const uint32_t base = ch * SYNC_CHUNK;
       if (hc.snapdst) {
@@ -260,66 +461,56 @@ __global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(KP, int d2, unsigne
           }
         }
       }
-      uint32_t flags = 0;  // bit 4j+q = subject base + j*256 + 4*lane + q
-      uint32_t diff = 0;
-#pragma unroll
-      for (int j = 0; j < CLS_LOADS; ++j) {
-        diff |= (a[j].x ^ o[j].x) | (a[j].y ^ o[j].y) | (a[j].z ^ o[j].z) | (a[j].w ^ o[j].w);
-        recs += (a[j].x >> 31) + (a[j].y >> 31) + (a[j].z >> 31) + (a[j].w >> 31);
-      }
-      // identical records never change the row (isOverrides(equal) is false and an identical
-      // LEAVING over LEAVING is a no-op) except on the viewer's own subject: the fast path of a
-      // converged cluster, where nearly every lane of nearly every unit compares equal
-      const uint32_t off = hc.r - base;
-      const bool self_here = off < SYNC_CHUNK && ((off & 255u) >> 2) == lane;
-      if (diff != 0 || self_here) {
-#pragma unroll
-        for (int j = 0; j < CLS_LOADS; ++j) {
-          const uint32_t x = base + j * 256 + 4 * lane;
-          const uint32_t av[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
-          const uint32_t ov[4] = {o[j].x, o[j].y, o[j].z, o[j].w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (r_in_table(av[q]) && sync_complex(av[q], ov[q], x + q == hc.r)) flags |= 1u << (4 * j + q);
-        }
-      }
-      uint2 res = make_uint2(0, 0);
-      if (__ballot(flags != 0)) {
-        // rare path: subject order = (j, lane, q); one wave scan of the four per-j counts
-        uint64_t cnt = 0;
-#pragma unroll
-        for (int j = 0; j < CLS_LOADS; ++j) cnt |= (uint64_t)__popc((flags >> (4 * j)) & 0xfu) << (16 * j);
-        uint64_t incl = cnt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const uint64_t y = __shfl_up(incl, d, 64);
-          if (lane >= (uint32_t)d) incl += y;
-        }
-        const uint64_t tot = __shfl(incl, 63, 64);
-        const uint64_t excl = incl - cnt;
-        uint32_t t = 0, jbase[CLS_LOADS];
-#pragma unroll
-        for (int j = 0; j < CLS_LOADS; ++j) { jbase[j] = t; t += (uint32_t)(tot >> (16 * j)) & 0xffffu; }
-        uint32_t pb = 0;
-        if (lane == 0) pb = atomicAdd(&b.k->pool_cursor, t);
-        pb = __shfl(pb, 0, 64);
-        if (pb + t > b.pool_cap) {
-          if (lane == 0) set_err(c, ERR_PEND);
-          t = 0;
-        } else {
-#pragma unroll
-          for (int j = 0; j < CLS_LOADS; ++j) {
-            uint32_t o2 = pb + jbase[j] + ((uint32_t)(excl >> (16 * j)) & 0xffffu);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (flags & (1u << (4 * j + q))) b.pool[o2++] = base + j * 256 + 4 * lane + q;
+      if (hc.d1 != NONE) {
+        // SYNC_ACK whose classification the SYNC launch already made
+        if (lane == 0) {
+          b.item_chunk[(size_t)hc.i * chunks + ch] = b.rev_chunk[(size_t)hc.d1 * chunks + ch];
+          if (ch == 0) {
+            const uint32_t t = b.rev_total[hc.d1];
+            b.item_total[hc.i] = t;
+            cplx += t;
           }
         }
-        res = make_uint2(pb, t);
-        if (lane == 0 && t) atomicAdd(&b.item_total[hc.i], t);
-        cplx += t;
+      } else {
+        if (lane == 0 && ch == 0) ++streamed;
+        uint32_t flags = 0, rflags = 0;
+        uint32_t diff = 0;
+#pragma unroll
+        for (int j = 0; j < CLS_LOADS; ++j)
+          diff |= (a[j].x ^ o[j].x) | (a[j].y ^ o[j].y) | (a[j].z ^ o[j].z) | (a[j].w ^ o[j].w);
+        // identical records never change the row (isOverrides(equal) is false and an identical
+        // LEAVING over LEAVING is a no-op) except on the viewer's own subject: the fast path of a
+        // converged cluster, where nearly every lane of nearly every unit compares equal
+        const bool self_here = lane_holds(hc.r, base, lane);
+        const bool rself_here = hc.rev && lane_holds(hc.s, base, lane);
+        if (diff != 0 || self_here || rself_here) {
+#pragma unroll
+          for (int j = 0; j < CLS_LOADS; ++j) {
+            const uint32_t x = base + j * 256 + 4 * lane;
+            const uint32_t av[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
+            const uint32_t ov[4] = {o[j].x, o[j].y, o[j].z, o[j].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (r_in_table(av[q]) && sync_complex(av[q], ov[q], x + q == hc.r)) flags |= 1u << (4 * j + q);
+              if (hc.rev && r_in_table(ov[q]) && sync_complex(ov[q], av[q], x + q == hc.s))
+                rflags |= 1u << (4 * j + q);
+            }
+          }
+        }
+        const uint2 res = cls_compact(c, b, flags, base, lane);
+        if (lane == 0) {
+          b.item_chunk[(size_t)hc.i * chunks + ch] = res;
+          if (res.y) atomicAdd(&b.item_total[hc.i], res.y);
+        }
+        cplx += res.y;
+        if (hc.rev) {
+          const uint2 rres = cls_compact(c, b, rflags, base, lane);
+          if (lane == 0) {
+            b.rev_chunk[(size_t)hc.i * chunks + ch] = rres;
+            if (rres.y) atomicAdd(&b.rev_total[hc.i], rres.y);
+          }
+        }
       }
-      if (lane == 0) b.item_chunk[(size_t)hc.i * chunks + ch] = res;
       if (more) {
         hc = hn;
 #pragma unroll
@@ -327,21 +518,21 @@ __global__ void __launch_bounds__(CLS_BLOCK) k_sync_classify(KP, int d2, unsigne
       }
     }
   }
-  // one counter update per workgroup (4,096 waves on one replicated counter would serialise)
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) recs += __shfl_down(recs, d, 64);
-  if (lane == 0) s_recs[threadIdx.x >> 6] = recs;
-  if (lane == 0 && cplx) {
-    stat_add(c, ST_MERGE_RECORDS, cplx);
-    if (prof) atomicAdd(prof + 1, cplx);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long t = 0;
-    for (int w = 0; w < CLS_BLOCK / 64; ++w) t += s_recs[w];
-    stat_add(c, ST_SYNC_RECORDS, t);
+  // the message record counts (sync_records) are taken from the headers by k_sync_apply
+  if (lane == 0 && (cplx || streamed)) {
+    if (cplx) stat_add(c, ST_MERGE_RECORDS, cplx);
+    if (streamed) stat_add(c, ST_MERGE_MSGS, streamed);
+    if (prof) {
+      atomicAdd(prof, (unsigned long long)streamed);
+      atomicAdd(prof + 1, (unsigned long long)cplx);
+    }
   }
 }
+
+__global__ void __launch_bounds__(CLS_BLOCK, CLS_MINWAVES) k_sync_classify(KP, unsigned long long* prof) {
+  classify_body<0>(P, T, prof);
+}
+__global__ void __launch_bounds__(CLS_BLOCK, CLS_MINWAVES) k_ack_classify(KP) { classify_body<1>(P, T, nullptr); }
 
 // In-workgroup merge of one message (used when the receiver's row changed earlier in this
 // sub-phase, so the precomputed classification may be stale).  Returns through *s_mod whether any
@@ -381,11 +572,15 @@ __device__ void merge_row_wg(const Ctx& c, uint32_t v, const uint32_t* __restric
 }
 
 // SYNC_ACK from `from` (the SYNC receiver) back to `to` (the SYNC sender)
-__device__ inline void add_ack(const Ctx& c, const Bufs& b, uint32_t to, uint32_t from, uint32_t rank, bool initial) {
+// `d1` = 1 + index of the SYNC being answered when its classify also classified this ack (0 = none)
+__device__ inline void add_ack(const Ctx& c, const Bufs& b, uint32_t to, uint32_t from, uint32_t rank, bool initial,
+                               uint32_t d1) {
   SyncReq a;
-  a.from = from; a.to = to; a.ordinal = rank; a.slot = 0; a.flags = RQ_DELIVERED | (initial ? RQ_INITIAL : 0);
-  a.content = NONE; a.snap = NONE; a.pad = 0;
+  a.from = from; a.to = to; a.ordinal = rank; a.slot = 0;
+  a.flags = RQ_DELIVERED | (initial ? RQ_INITIAL : 0) | (mem(c, from).table_size << RQ_RECS_SHIFT);
+  a.content = NONE; a.snap = NONE; a.pad = d1;
   if (!owned(c, to)) {  // content (this row after the SYNC merges) travels with the ack
+    a.pad = 0;
     const uint32_t d = owner(c, to);
     const uint32_t i = atomicAdd(&b.x->ack[d], 1u);
     if (i >= b.tx_req_cap) { set_err(c, ERR_REQS); return; }
@@ -397,12 +592,16 @@ __device__ inline void add_ack(const Ctx& c, const Bufs& b, uint32_t to, uint32_
 
 // D1 (d2 = 0): onSync at each receiver, then its SYNC_ACKs.  D2 (d2 = 1): the SYNC_ACK merge at
 // the original senders (MembershipProtocolImpl.java:363-415).
-__global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2) {
+// classified = 0 (SYNC_ACK sub-phase of an unsharded engine: no k_ack_classify launch): an ack takes
+// the SYNC launch's reverse classification when its two rows are unchanged since (row_mod), and is
+// classified in-workgroup (merge_row_wg) otherwise.
+__global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int classified) {
   const Ctx c = pctx_sync(P, T);
   const Bufs b = P->b;
   __shared__ uint32_t s_list[APPLY_TILE];
   __shared__ uint32_t s_wave[APPLY_BLOCK / 64 + 1];
   __shared__ uint32_t s_mod;
+  __shared__ unsigned long long s_recs;
   const SubPhase p = sub_phase(b, d2);
   const uint32_t phase = d2 ? SWIM_PHASE_SYNCACK : SWIM_PHASE_SYNC;
   const uint32_t chunks = b.chunks;
@@ -415,6 +614,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2) {
       mem(c, s).ev_minor = 0;
       mem(c, s).fetch_ctr = 0;
       s_mod = 0;
+      s_recs = 0;
     }
     __syncthreads();
     for (uint32_t q = 0; q < k; ++q) {
@@ -423,10 +623,17 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2) {
       const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
       uint32_t npend = 0;
       const uint32_t mod = s_mod;
+      const bool own = d2 && !classified;  // this kernel classifies the ack
+      uint32_t d1 = NONE;
+      if (own && rq.pad != 0 && rq.content == NONE && b.row_mod[rq.from - c.lo] != (uint32_t)c.T &&
+          b.row_mod[s - c.lo] != (uint32_t)c.T)
+        d1 = rq.pad - 1;
       __syncthreads();  // every lane has read s_mod before lane 0 may set it
-      if (mod == 0) {  // precomputed classification is exact: the row is unchanged
-        if (threadIdx.x == 0 && b.item_total[first + q] != 0) {
-          const uint2* ic = b.item_chunk + (size_t)(first + q) * chunks;
+      if (mod == 0 && (!own || d1 != NONE)) {  // precomputed classification is exact: the row is unchanged
+        const uint32_t it = d1 != NONE ? d1 : first + q;
+        const uint32_t tot = d1 != NONE ? b.rev_total[it] : b.item_total[it];
+        if (threadIdx.x == 0 && tot != 0) {
+          const uint2* ic = (d1 != NONE ? b.rev_chunk : b.item_chunk) + (size_t)it * chunks;
           for (uint32_t ch = 0; ch < chunks; ++ch) {
             const uint2 e = ic[ch];
             if (e.y) s_mod = 1;
@@ -444,6 +651,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2) {
       if (threadIdx.x == 0) {
         for (uint32_t j = 0; j < npend; ++j)
           apply_alive(c, s, (uint32_t)(pend[j] >> 32), (int32_t)(uint32_t)pend[j], reason, phase);
+        s_recs += rq.flags >> RQ_RECS_SHIFT;
       }
       __syncthreads();
     }
@@ -453,8 +661,9 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2) {
           const SyncReq rq = p.out[first + q];
           if (out_fail(c, s, rq.from, s, SWIM_STREAM_SYNCACK_OUT, q, 0)) continue;
           if (!in_pass(c, rq.from, s)) continue;
-          add_ack(c, b, rq.from, s, q, (rq.flags & RQ_INITIAL) != 0);
+          add_ack(c, b, rq.from, s, q, (rq.flags & RQ_INITIAL) != 0, CLS_REV && rq.content == NONE ? first + q + 1 : 0);
         }
+        if (s_mod) b.row_mod[s - c.lo] = (uint32_t)c.T;  // invalidates the reverse classifications
       } else {
         // start0's initial-sync completion counts the acks of its INITIAL SYNCs (:270-284)
         uint32_t init = 0;
@@ -463,6 +672,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2) {
         stat_add(c, ST_SYNC_ACKS, k);
       }
       p.cnt[s - c.lo] = 0;
+      stat_add(c, ST_SYNC_RECORDS, s_recs);
     }
     __syncthreads();
   }

@@ -1,0 +1,33 @@
+"""Dev tool: A/B timing of libswimgpu.so builds on the quiet bench workload (not part of the product).
+
+    python tools/variant_bench.py LIB.so [LIB2.so ...]
+
+Loads each build explicitly, runs N = 65,536 quiet periods and prints ms/period and the SYNC
+classify kernel's event-timed average.  Build variants with e.g.
+    hipcc <HIPCC_FLAGS of __graft_entry__> -DCLS_MINWAVES=3 -o scalecube-cluster_amd/lib/variants/x.so ...
+"""
+import ctypes
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "scalecube-cluster_amd"))
+from swimgpu import abi  # noqa: E402
+
+N, WARM, STEPS = 65536, 8, 30
+for path in sys.argv[1:]:
+    lib = abi.bind(ctypes.CDLL(os.path.abspath(path)))
+    cfg = abi.default_config(lib, 0, sync_stagger=1)
+    with abi.Engine(lib, cfg, N, N, 1) as e:
+        e.step(WARM)
+        e.profile_enable(True)
+        t0 = time.perf_counter()
+        e.step(STEPS)
+        dt = time.perf_counter() - t0
+        p = e.profile_merge()
+        st = e.stats()
+    avg = p["total_ms"] / max(1, p["launches"])
+    print(f"{os.path.basename(path):28s} {dt / STEPS * 1e3:7.3f} ms/period  classify {avg * 1e3:6.2f} us "
+          f"{p['alg_bytes'] / max(1e-12, p['total_ms'] / 1e3) / 1e9:7.0f} GB/s  sync_records {st['sync_records']}",
+          flush=True)
