@@ -664,6 +664,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&c.default_inbound, n) && sd.alloc(&c.group, n) && sd.alloc(&c.links, 1) &&
             sd.alloc(&c.is_seed, n) && sd.alloc(&c.seeds, n) && sd.alloc(&c.ins, c.ins_cap) &&
             sd.alloc(&c.ins_list, nl) && sd.alloc(&c.compact_flag, nl) &&
+            sd.alloc(&c.fd_next, nl) && sd.alloc(&c.sync_next, nl) && sd.alloc(&c.mflag, nl) &&
             sd.alloc(&c.stats, (size_t)ST_COUNT * ST_REPL) && sd.alloc(&c.err, 1) && sd.alloc(&sd.k, 1) &&
             sd.alloc(&sd.x, 1) && sd.alloc(&b.msgs, b.msg_cap) && sd.alloc(&b.msgs_out, b.msg_cap) &&
             sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.msg_start, nl) &&

@@ -22,6 +22,7 @@
 namespace swimdev {
 
 constexpr uint32_t NONE = 0xffffffffu;
+enum : uint32_t { MF_FDSYNC = 1, MF_JOIN = 2, MF_LEAVE = 4 };  // Ctx.mflag bits
 constexpr int KIV = 6;         // inline intervals per SequenceIdCollector
 constexpr int FD_SYNC_MAX = 33;  // FD-triggered SYNCs per member per tick (<= 2k+1)
 
@@ -150,6 +151,11 @@ struct Ctx {
   uint32_t* ins_list;      // viewers with ops
   uint32_t* ins_list_cnt;
   uint32_t* compact_flag;  // per viewer: lists hold a REMOVED member (compacted before its next FD step)
+  // compact per-member schedule: lets the per-tick member scans skip idle members
+  // without touching their MemberDev
+  uint32_t* fd_next;    // next tick with FD work (ping due, ack or relay timeout); stale while down
+  uint32_t* sync_next;  // next periodic-SYNC tick (NONE: periodic SYNC off)
+  uint32_t* mflag;      // MF_* work for k_sync_collect / k_end_tick
   unsigned long long* stats;
   uint32_t* err;
 };

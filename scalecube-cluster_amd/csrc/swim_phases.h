@@ -122,6 +122,20 @@ __global__ void k_init_rows(Ctx c, uint32_t n_initial) {
   }
 }
 
+// smallest tick t > after with t > start and (t - start) % period == 0: the next firing of a timer
+// started at `start` (first fire one period after it)
+__device__ inline uint32_t next_due(int64_t start, uint64_t after, uint32_t period) {
+  const int64_t a = (int64_t)after > start ? (int64_t)after : start;
+  return (uint32_t)(start + ((a - start) / (int64_t)period + 1) * (int64_t)period);
+}
+
+__device__ inline uint32_t fd_next_of(const Ctx& c, const MemberDev& m, uint64_t T) {
+  uint32_t t = next_due(m.fd_start, T, c.P);
+  if (m.ack_due > T && m.ack_due < t) t = (uint32_t)m.ack_due;
+  if (m.relay_due > T && m.relay_due < t) t = (uint32_t)m.relay_due;
+  return t;
+}
+
 // initial members: converged state, seeded Fisher-Yates ping / remote lists
 __global__ void k_init_members(Ctx c, uint32_t n_initial, int32_t sync_stagger, int32_t timer_stagger) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -160,6 +174,9 @@ __global__ void k_init_members(Ctx c, uint32_t n_initial, int32_t sync_stagger, 
     }
   }
   c.mem[i] = m;
+  c.fd_next[i] = m.joined ? fd_next_of(c, m, c.T) : NONE;
+  c.sync_next[i] = m.sync_on ? next_due(m.sync_start, c.T, c.S) : NONE;
+  c.mflag[i] = 0;
 }
 
 // ------------------------------------------------------------------------------- block scan helper
@@ -204,6 +221,8 @@ __global__ void k_start_joins(KP) {
   cell_put(c, v, v, B_IN_TABLE | B_IN_MEMBERS);
   m.table_size = 1;
   m.members_size = 1;
+  c.fd_next[i] = fd_next_of(c, m, c.T);
+  c.mflag[i] |= MF_JOIN;
 }
 
 // ------------------------------------------------------------------------------- phase A
@@ -281,6 +300,7 @@ __device__ inline void publish_fd(const Ctx& c, uint32_t v, uint32_t t, uint32_t
   if (status == SWIM_ALIVE) {
     if (m.fd_sync_cnt >= FD_SYNC_MAX) { set_err(c, ERR_FDSYNC); return; }
     c.fd_sync[(size_t)(v - c.lo) * FD_SYNC_MAX + m.fd_sync_cnt++] = t;
+    c.mflag[v - c.lo] |= MF_FDSYNC;
     return;
   }
   update_membership(c, v, t, status, c_inc(cell), R_FD_EVENT, SWIM_PHASE_FD);
@@ -356,8 +376,9 @@ __device__ inline void ping_req(const Ctx& c, uint32_t v, uint32_t t, unsigned l
 __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& nev, unsigned long long& nreq,
                                  unsigned long long& npings) {
   MemberDev& m = mem(c, v);
-  if (!c.up[v]) return;
+  if (!c.up[v]) return;  // a stopped member's timers stop; a join restarts them (fd_next)
   const bool due = (int64_t)c.T > m.fd_start && ((int64_t)c.T - m.fd_start) % c.P == 0;
+  c.fd_next[v - c.lo] = fd_next_of(c, m, c.T);  // ack / relay timeouts set below are > T
   if (!due && m.relay_due != c.T && m.ack_due != c.T) return;
   m.ev_minor = 0;
   if (m.relay_due == c.T) {  // relay timeouts (:200-209)
@@ -390,6 +411,7 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
       }
     }
   }
+  c.fd_next[v - c.lo] = fd_next_of(c, m, c.T);
 }
 
 // 256-thread workgroups, one viewer per thread.  First the workgroup compacts the ping / remote
@@ -417,7 +439,7 @@ __global__ void __launch_bounds__(256) k_fd(KP) {
   if (flagged) c.compact_flag[i] = 0;
   __syncthreads();  // the compacted lengths are visible to every thread
   unsigned long long nev = 0, nreq = 0, npings = 0;
-  if (i < c.nl) fd_member(c, c.lo + i, nev, nreq, npings);
+  if (i < c.nl && c.fd_next[i] == (uint32_t)T) fd_member(c, c.lo + i, nev, nreq, npings);
   wave_stat_add(c, ST_FD_EVENTS, nev);
   wave_stat_add(c, ST_PING_REQS, nreq);
   wave_stat_add(c, ST_PINGS, npings);
@@ -593,6 +615,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     m.gossip_len = w;
     if (any_done) {
       m.leave_done = 1;
+      c.mflag[v - c.lo] |= MF_LEAVE;
       if (c.world > 1) {  // every shard stops sending to v at the end of this tick
         const uint32_t i = atomicAdd(&b.x->stop, 1u);
         if (i < b.tx_stop_cap) b.tx_stops[i] = v; else set_err(c, ERR_MSGS);
@@ -969,11 +992,17 @@ __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t
 
 // doSync (:339-357), FD-triggered SYNCs (:427-442) and start0's initial SYNC to every seed (:250-291)
 __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Bufs& b, uint32_t v) {
+  const uint32_t i = v - c.lo, t32 = (uint32_t)c.T;
+  const bool due = c.sync_next[i] == t32;  // the periodic doSync timer fires (sync_on, phase sync_start)
+  const uint32_t fl = c.mflag[i];
+  if (!due && !(fl & (MF_FDSYNC | MF_JOIN))) return 0;
+  if (due) c.sync_next[i] = t32 + c.S;
+  if (fl & MF_FDSYNC) c.mflag[i] = fl & ~MF_FDSYNC;
   MemberDev& m = mem(c, v);
   if (!c.up[v]) { m.fd_sync_cnt = 0; return 0; }
   uint32_t k = 0;
   unsigned long long nsync = 0;
-  if (m.sync_on && (int64_t)c.T > m.sync_start && ((int64_t)c.T - m.sync_start) % c.S == 0) {
+  if (due) {
     uint32_t t = select_sync_address(c, v);
     if (t != NONE) { add_req(c, b, v, t, k++, false); nsync++; }
   }
@@ -1017,12 +1046,16 @@ __global__ void k_end_tick(KP, uint32_t n_rx_stops) {
   if (x && i < sizeof(Xc) / 4) reinterpret_cast<uint32_t*>(x)[i] = 0;
   if (i < n_rx_stops) c.up[rx_stops[i]] = 0;  // graceful leaves completed on other shards
   if (i >= c.nl) return;
+  const uint32_t fl = c.mflag[i];
+  if (!(fl & (MF_JOIN | MF_LEAVE))) return;
+  c.mflag[i] = fl & ~(MF_JOIN | MF_LEAVE);
   const uint32_t v = c.lo + i;
   MemberDev& m = c.mem[i];
   if (m.join_now) {
     m.sync_on = 1;
     m.sync_start = (int64_t)c.T + (m.init_done == m.init_total ? 0 : (int64_t)c.sync_to_ticks);
     m.join_now = 0;
+    c.sync_next[i] = next_due(m.sync_start, c.T, c.S);
   }
   if (m.leave_done) {
     m.leave_done = 0;

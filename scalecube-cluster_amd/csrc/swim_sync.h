@@ -20,6 +20,9 @@
 #ifndef CLS_MINWAVES
 #define CLS_MINWAVES 4  // waves per SIMD the classify kernels are register-limited to
 #endif
+#ifndef CLS_SKIPZERO
+#define CLS_SKIPZERO 0  // timing experiment only: skip the stores of empty chunk results (NOT exact)
+#endif
 #ifndef CLS_REV
 #define CLS_REV 1       // SYNC classify also classifies the reverse (SYNC_ACK) direction
 #endif
@@ -498,14 +501,14 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
           }
         }
         const uint2 res = cls_compact(c, b, flags, base, lane);
-        if (lane == 0) {
+        if (lane == 0 && (!CLS_SKIPZERO || res.y)) {
           b.item_chunk[(size_t)hc.i * chunks + ch] = res;
           if (res.y) atomicAdd(&b.item_total[hc.i], res.y);
         }
         cplx += res.y;
         if (hc.rev) {
           const uint2 rres = cls_compact(c, b, rflags, base, lane);
-          if (lane == 0) {
+          if (lane == 0 && (!CLS_SKIPZERO || rres.y)) {
             b.rev_chunk[(size_t)hc.i * chunks + ch] = rres;
             if (rres.y) atomicAdd(&b.rev_total[hc.i], rres.y);
           }
