@@ -30,38 +30,82 @@ sys.path.insert(0, os.path.join(REPO, "scalecube-cluster_amd"))
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s)
 KILL_EVERY = 20
 KILL_FIRST = 10
+CHURN_PER_MILLE = 10    # config 3: 1 % of the members killed and as many fresh members joined per period
+CHURN_LOSS = 5          # config 3: 5 % uniform outbound loss
 
 
 WORKLOAD = "quiet"
+LAN = "LAN defaults (ping 1 s / gossip 200 ms / sync 30 s staggered)"
+WORKLOAD_TEXT = {
+    "quiet": "config4-lan-quiet: N={n} members (one cluster), " + LAN + ", 0% loss, no faults",
+    "failures": "config4-lan-failures: N={n} members (one cluster), " + LAN + ", 0% loss, "
+                "one member killed every {every} periods",
+    "churn": "config3-churn: N={n} live members, " + LAN + ", {loss}% uniform outbound loss, {churn} kills + "
+             "{churn} fresh joins via seed 0 per period",
+}
+DEFAULT_MEMBERS = {"quiet": 65536, "failures": 65536, "churn": 16384}
 
 
-def kill_schedule(n, periods_lo, periods_hi):
-    """Members killed at the start of each period in [lo, hi): one every KILL_EVERY periods
-    (workload "failures"; the "quiet" workload kills nobody)."""
-    out = {}
-    if WORKLOAD == "quiet":
-        return out
-    for p in range(periods_lo, periods_hi):
-        if p >= KILL_FIRST and (p - KILL_FIRST) % KILL_EVERY == 0:
-            j = (p - KILL_FIRST) // KILL_EVERY
-            out[p] = (17 + 7919 * j) % n
-    return out
+class Schedule:
+    """The workload's control operations, applied at the start of each period (identical on every
+    rank: the control state they change is replicated).
+      quiet     nothing (BASELINE config 4 at 0 % loss);
+      failures  one member killed every KILL_EVERY periods;
+      churn     BASELINE config 3: 5 % uniform loss, and every period 1 % of the members killed
+                and as many fresh members joined through seed member 0."""
+
+    def __init__(self, workload, n, periods, churn=None, loss=None):
+        import random
+        self.workload, self.n = workload, n
+        self.loss = CHURN_LOSS if loss is None else loss
+        self.churn = (churn if churn is not None else max(1, n * CHURN_PER_MILLE // 1000)) if workload == "churn" else 0
+        self.capacity = n + self.churn * periods
+        self.live = list(range(1, n))  # member 0 is the seed and stays up
+        self.next_id = n
+        self.rng = random.Random(12345)
+
+    def setup(self, e):
+        if self.workload == "churn":
+            e.set_default_loss(self.loss)
+            e.set_seeds([0])
+
+    def ops(self, p):
+        if self.workload == "failures":
+            if p >= KILL_FIRST and (p - KILL_FIRST) % KILL_EVERY == 0:
+                return [("kill", (17 + 7919 * ((p - KILL_FIRST) // KILL_EVERY)) % self.n)]
+            return []
+        if self.workload == "churn":
+            out = []
+            for _ in range(self.churn):
+                out.append(("kill", self.live.pop(self.rng.randrange(len(self.live)))))
+            for _ in range(self.churn):
+                out.append(("join", self.next_id))
+                self.live.append(self.next_id)
+                self.next_id += 1
+            return out
+        return []
+
+    def run(self, e, p0, p1):
+        """Advance e through periods [p0, p1), one step per run of op-free periods."""
+        p = p0
+        while p < p1:
+            for op, m in self.ops(p):
+                getattr(e, op)(m)
+            nxt = p + 1
+            while nxt < p1 and not self._has_ops(nxt):
+                nxt += 1
+            e.step(nxt - p)
+            p = nxt
+
+    def _has_ops(self, p):
+        if self.workload == "failures":
+            return p >= KILL_FIRST and (p - KILL_FIRST) % KILL_EVERY == 0
+        return self.workload == "churn"
 
 
 def make_config(lib, device=0):
     from swimgpu import abi
     return abi.default_config(lib, 0, sync_stagger=1, record_fd_events=0, device=device)
-
-
-def run_periods(e, p0, p1):
-    sched = kill_schedule(e.capacity, p0, p1)
-    p = p0
-    while p < p1:
-        if p in sched:
-            e.kill(sched[p])
-        nxt = min([q for q in sched if q > p] + [p1])
-        e.step(nxt - p)
-        p = nxt
 
 
 def pmc_traffic(kernel, workload):
@@ -87,9 +131,11 @@ def cpu_baseline(n, periods):
     from swimgpu import abi
     lib = oracle.lib()
     cfg = abi.default_config(lib, 0, sync_stagger=1, record_fd_events=0)
-    e = abi.Engine(lib, cfg, n, n, 1)
+    sch = Schedule(WORKLOAD, n, periods)
+    e = abi.Engine(lib, cfg, sch.capacity, n, 1)
+    sch.setup(e)
     t0 = time.perf_counter()
-    run_periods(e, 0, periods)
+    sch.run(e, 0, periods)
     dt = time.perf_counter() - t0
     e.close()
     return {"value": n * periods / dt, "unit": "member-periods/s", "cores": 1, "kind": "port",
@@ -102,11 +148,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--members", type=int, default=65536)
+    ap.add_argument("--members", type=int, default=None, help="default: 65,536 (16,384 for churn)")
     ap.add_argument("--cpu-periods", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=("quiet", "failures"), default="quiet")
+    ap.add_argument("--workload", choices=("quiet", "failures", "churn"), default="quiet")
     ap.add_argument("--gossip-capacity", type=int, default=0)
+    ap.add_argument("--churn", type=int, default=None,
+                    help="churn workload: members killed and joined per period (default 1%% of N, BASELINE config 3)")
+    ap.add_argument("--loss", type=int, default=None, help="churn workload: uniform outbound loss %% (default 5)")
     ap.add_argument("--local-shards", type=int, default=1,
                     help="single-process sharded test rig (cfg.local_shards); measurement of the exchange only")
     args = ap.parse_args()
@@ -126,17 +175,30 @@ def main():
     import swimgpu
     from swimgpu import abi
     lib = swimgpu.load_library()
-    n = args.members
+    n = args.members or DEFAULT_MEMBERS[args.workload]
+    sch = Schedule(args.workload, n, args.warmup + args.steps, args.churn, args.loss)
     cfg = make_config(lib, local_rank)
     cfg.gossip_capacity = args.gossip_capacity
+    if args.workload == "churn":
+        # config-3 churn sizes: a period's joins add every joiner at every viewer (millions of
+        # events); every member holds the gossips of its last ~18 s; a period's kills put a suspicion
+        # timer at every viewer within a few seconds
+        cfg.event_capacity = 1 << 25
+        cfg.gossip_capacity = max(cfg.gossip_capacity, 16384)
+        cfg.timer_capacity = 16 * sch.capacity
+        cfg.message_capacity = min(1 << 28, 4096 * sch.capacity)
+        # a viewer keeps a SequenceIdCollector per gossiper heard until it is removed, and every
+        # member that learns news through SYNC gossips it: in a long churn run that is most members
+        cfg.collector_capacity = 1 << (2 * sch.capacity - 1).bit_length()
     cfg.local_shards = args.local_shards
     se = None
     if world > 1:
         from swimgpu.dist import ShardedEngine
-        se = ShardedEngine(lib, cfg, n, n, 1)
+        se = ShardedEngine(lib, cfg, sch.capacity, n, 1)
         e = se.engine
     else:
-        e = abi.Engine(lib, cfg, n, n, 1)
+        e = abi.Engine(lib, cfg, sch.capacity, n, 1)
+    sch.setup(e)
 
     def barrier():
         if world > 1:
@@ -144,12 +206,12 @@ def main():
         torch.cuda.synchronize()
 
     try:
-        run_periods(e, 0, args.warmup)
+        sch.run(e, 0, args.warmup)
         e.drain_events()
         barrier()
         e.profile_enable(True)
         t0 = time.perf_counter()
-        run_periods(e, args.warmup, args.warmup + args.steps)
+        sch.run(e, args.warmup, args.warmup + args.steps)
         barrier()
         dt = time.perf_counter() - t0
     except abi.SwimError as ex:
@@ -183,10 +245,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
-        "config": {"workload": f"config4-lan-{args.workload}: N={n} members (one cluster), LAN defaults (ping 1 s / "
-                               f"gossip 200 ms / sync 30 s staggered), 0% loss, "
-                               + ("no faults" if args.workload == "quiet"
-                                  else f"one member killed every {KILL_EVERY} periods"),
+        "config": {"workload": WORKLOAD_TEXT[args.workload].format(n=n, churn=sch.churn, every=KILL_EVERY,
+                                                                   loss=sch.loss),
                    "members": n, "tick_ms": 100,
                    "parallelism": (f"rows sharded over {world} GPUs, RCCL send/recv over xGMI" if world > 1 else
                                    f"single GPU, {args.local_shards} in-process shards" if args.local_shards > 1

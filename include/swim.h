@@ -111,7 +111,8 @@ typedef struct swim_config {
   int32_t tick_ms;            /* 0 = gcd of every interval/timeout above */
   int32_t sync_stagger;       /* 1 = each initial member's periodic SYNC gets a random phase */
   int32_t record_fd_events;   /* 1 = FailureDetectorEvents appear in the event stream */
-  uint32_t gossip_capacity;   /* max live GossipStates per member (0 = default 1024) */
+  uint32_t gossip_capacity;   /* max live GossipStates per member (0 = default 1024; a member keeps
+                                 every gossip of the last 2 x (spread + 1) rounds, so churn needs more) */
   uint32_t collector_capacity;/* hash slots for the SequenceIdCollectors a member holds, one per
                                  distinct gossiper heard (power of two; 0 = default 4096; keep the
                                  load well below 1: open addressing) */
@@ -123,7 +124,12 @@ typedef struct swim_config {
   int32_t timer_stagger;      /* 1 = each initial member's ping and gossip timers also get a random
                                  phase (members of a real cluster start at different instants; the
                                  default 0 aligns them) */
-  uint32_t reserved[5];
+  uint32_t timer_capacity;    /* suspicion timers that may fall due in one tick, per row shard
+                                 (0 = default 2 x the shard's rows; churn schedules a timer for every
+                                 killed member at every viewer within a few seconds) */
+  uint32_t message_capacity;  /* GOSSIP_REQ messages one gossip round may materialise, per row shard
+                                 (0 = default 512 x the shard's rows; loss and churn storms need more) */
+  uint32_t reserved[3];
 } swim_config;
 
 /* preset: 0 = defaultConfig/defaultLanConfig, 1 = defaultWanConfig, 2 = defaultLocalConfig

@@ -29,7 +29,8 @@ using namespace swimdev;
 
 namespace {
 
-constexpr uint32_t kDrainEvery = 256;
+constexpr uint32_t kDrainEvery = 256;  // longest interval between event drains (ticks)
+constexpr uint32_t kDrainFirst = 1;    // the interval starts at one tick and adapts to the event rate
 constexpr uint32_t kClassifyGrid = 1024;  // 4,096 waves: the resident capacity at 110 VGPRs (4 waves / SIMD)
 constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
 constexpr uint32_t kEmitGrid = 2048;      // 8,192 waves, one gossip sender at a time each
@@ -129,6 +130,7 @@ struct swim_engine {
   uint32_t par_slot = 0;
   // host mirrors of replicated control state
   std::vector<uint8_t> g_residue;  // gossip timer residues mod G in use
+  uint32_t drain_every = kDrainFirst, since_drain = 0;  // event drain interval (ticks), adaptive
   std::vector<uint32_t> seeds;
   std::vector<uint8_t> is_seed_h, joined_h, join_pending_h;
   std::vector<LinkDev> links_h;
@@ -224,6 +226,7 @@ static int32_t sync_and_collect(swim_engine* e) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return hip_status() ? SWIM_EDEVICE : SWIM_EDEVICE;
   e->par_slot = 0;  // every staged Params upload has completed
   uint32_t err_all = 0;
+  double fill = 0.0;  // fullest event sub-queue since the last drain
   for (Shard& s : e->sh) {
     uint32_t cnt[SUBQ], err = 0;
     if (hipMemcpy(cnt, s.c.ev_cnt, 4 * SUBQ, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
@@ -231,6 +234,7 @@ static int32_t sync_and_collect(swim_engine* e) {
     bool any = false;
     for (uint32_t q = 0; q < SUBQ; ++q) {
       const uint32_t k = std::min(cnt[q], s.c.ev_cap);
+      fill = std::max(fill, (double)cnt[q] / s.c.ev_cap);
       if (!k) continue;
       any = true;
       size_t old = e->events.size();
@@ -244,6 +248,13 @@ static int32_t sync_and_collect(swim_engine* e) {
     err_all |= err;
     if (e->prof) prof_flush(s);
   }
+  // adapt the drain interval so a sub-queue stays well below its capacity between drains (an event
+  // storm — a join burst adds every joiner at every viewer — drains every few ticks, a quiet
+  // cluster every kDrainEvery)
+  if (fill > 0.5) e->drain_every = std::max(1u, e->drain_every / 4);
+  else if (fill > 0.25) e->drain_every = std::max(1u, e->drain_every / 2);
+  else if (fill < 0.05) e->drain_every = std::min(kDrainEvery, e->drain_every * 2);
+  e->since_drain = 0;
   e->err_seen |= err_all;
   return err_all ? SWIM_ECAPACITY : SWIM_OK;
 }
@@ -491,7 +502,6 @@ static int32_t run_tick(swim_engine* e) {
     k_fd<<<gm, 256, 0, s>>>(sd.d_par, T);
     // ---- C: gossip round (emit)
     if (gossip_tick) {
-      if (sd.c.seg_threshold < KIV) k_gossip_seg<<<gm, 256, 0, s>>>(sd.d_par, T);
       k_gossip_round<<<gm, 256, 0, s>>>(sd.d_par, T);
       k_gossip_emit<<<kEmitGrid, 64 * EMIT_WAVES, 0, s>>>(sd.d_par, T);
     }
@@ -620,7 +630,12 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   const uint32_t nl = c.nl;
   c.gcap = cf.gossip_capacity ? cf.gossip_capacity : 1024;
   c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 4096);
-  c.spill_cap = std::max<uint32_t>(1u << 20, 64 * std::max(nl, 1u));
+  // spilled collectors by tier (6 / 62 / 510 / 2,046 intervals); blocks are recycled, so these
+  // bound the collectors spilled at once, not over the run
+  c.spill_cap[0] = std::max<uint32_t>(1u << 18, 64 * std::max(nl, 1u));
+  c.spill_cap[1] = std::max<uint32_t>(1u << 15, 8 * std::max(nl, 1u));
+  c.spill_cap[2] = std::max<uint32_t>(1u << 12, std::max(nl, 1u) / 2);
+  c.spill_cap[3] = std::max<uint32_t>(1u << 10, std::max(nl, 1u) / 16);
   c.P = e->P;
   c.to_ticks = (uint32_t)cf.ping_timeout / e->tick_ms;
   c.relay_ticks = e->P - c.to_ticks;
@@ -639,10 +654,13 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.key1 = (uint32_t)(seed >> 32);
   const uint64_t max_timer = (uint64_t)cf.suspicion_mult * (uint64_t)host_ceil_log2((int32_t)n) * e->P;
   c.wheel_mask = next_pow2((uint32_t)max_timer + 2) - 1;
-  c.wheel_cap = SUBQ * std::max<uint32_t>(1024, (2 * std::max(nl, 1u) + SUBQ - 1) / SUBQ);
+  const uint64_t tcap = cf.timer_capacity ? cf.timer_capacity : 2ull * std::max(nl, 1u);
+  c.wheel_cap = SUBQ * (uint32_t)std::max<uint64_t>(1024, (tcap + SUBQ - 1) / SUBQ);
   c.ev_cap = std::max<uint32_t>(1024, (cf.event_capacity ? cf.event_capacity : (1u << 22)) / SUBQ);
-  c.ins_cap = std::max<uint32_t>(1u << 16, 4 * nl);
-  b.msg_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 512ull * nl));
+  // deferred pingMembers inserts of one phase: a join burst adds every joiner at every viewer
+  c.ins_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 22, 256ull * nl));
+  b.msg_cap = cf.message_capacity ? cf.message_capacity
+                                 : (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 512ull * nl));
   b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
   b.snap_cap = 64;
   b.chunks = (n + SYNC_CHUNK - 1) / SYNC_CHUNK;
@@ -656,7 +674,15 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   const size_t nn = (size_t)nl * n;
   bool ok = sd.alloc(&c.recs, nn) && sd.alloc(&c.aux, nn) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
             sd.alloc(&c.remote, nn) && sd.alloc(&c.slab, (size_t)nl * c.gcap) && sd.alloc(&c.coll, (size_t)nl * c.hcap) &&
-            sd.alloc(&c.spill, c.spill_cap) && sd.alloc(&c.spill_cnt, 1) &&
+            sd.alloc(&c.spill[0], (size_t)c.spill_cap[0] * tier_words(0)) &&
+            sd.alloc(&c.spill[1], (size_t)c.spill_cap[1] * tier_words(1)) &&
+            sd.alloc(&c.spill[2], (size_t)c.spill_cap[2] * tier_words(2)) &&
+            sd.alloc(&c.spill[3], (size_t)c.spill_cap[3] * tier_words(3)) &&
+            sd.alloc(&c.spill_avail[0], c.spill_cap[0]) && sd.alloc(&c.spill_freed[0], c.spill_cap[0]) &&
+            sd.alloc(&c.spill_avail[1], c.spill_cap[1]) && sd.alloc(&c.spill_freed[1], c.spill_cap[1]) &&
+            sd.alloc(&c.spill_avail[2], c.spill_cap[2]) && sd.alloc(&c.spill_freed[2], c.spill_cap[2]) &&
+            sd.alloc(&c.spill_avail[3], c.spill_cap[3]) && sd.alloc(&c.spill_freed[3], c.spill_cap[3]) &&
+            sd.alloc(&c.spill_ctl, NTIER) && sd.alloc(&c.seg_flag, nl) &&
             sd.alloc(&c.fd_sync, (size_t)nl * FD_SYNC_MAX) &&
             sd.alloc(&c.wheel, (size_t)(c.wheel_mask + 1) * c.wheel_cap) &&
             sd.alloc(&c.wheel_cnt, (size_t)(c.wheel_mask + 1) * SUBQ) && sd.alloc(&c.ev, (size_t)c.ev_cap * SUBQ) &&
@@ -689,7 +715,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.x = sd.x;
   hipStream_t s = e->stream;
   hipMemsetAsync(c.coll, 0, sizeof(CollEnt) * (size_t)nl * c.hcap, s);
-  hipMemsetAsync(c.spill_cnt, 0, 4, s);
+  hipMemsetAsync(c.spill_ctl, 0, sizeof(SpillCtl) * NTIER, s);
+  hipMemsetAsync(c.seg_flag, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1) * SUBQ, s);
   hipMemsetAsync(c.ev_cnt, 0, 4 * SUBQ, s);
   hipMemsetAsync(c.up, 0, n, s);
@@ -875,7 +902,7 @@ int32_t swim_step_ticks(swim_engine* e, uint32_t ticks) {
   if (hipSetDevice(e->device) != hipSuccess) return SWIM_EDEVICE;
   for (uint32_t i = 0; i < ticks; ++i) {
     if (int32_t rc = run_tick(e)) return rc;
-    if ((i + 1) % kDrainEvery == 0) {
+    if (++e->since_drain >= e->drain_every) {
       int32_t r = sync_and_collect(e);
       if (r == SWIM_EDEVICE) return r;
     }
@@ -1166,8 +1193,8 @@ int32_t swim_read_gossips(swim_engine* e, uint32_t v, swim_gossip* out, uint32_t
     out[i].inc = g[i].inc;
     out[i].status = g[i].status;
     out[i].infection_period = g[i].inf_period;
-    out[i].infected[0] = g[i].inf0;
-    out[i].infected[1] = g[i].inf1;
+    out[i].infected[0] = g[i].inf[0];
+    out[i].infected[1] = g[i].inf[1];
   }
   return SWIM_OK;
 }
@@ -1185,15 +1212,19 @@ int32_t swim_read_collector(swim_engine* e, uint32_t v, uint32_t gossiper, swim_
   for (const CollEnt& d : tab) {
     if (d.key != gossiper + 1) continue;
     const uint32_t n = d.meta & 7u;
-    CollDev sp{};
-    if (n == COLL_SPILLED &&
-        hipMemcpy(&sp, sd->c.spill + (d.meta >> 8), sizeof(CollDev), hipMemcpyDeviceToHost) != hipSuccess)
-      return SWIM_EDEVICE;
-    const uint32_t cnt = n == COLL_SPILLED ? sp.n : n;
+    std::vector<uint32_t> blk;
+    if (n == COLL_SPILLED) {
+      const int t = (int)((d.meta >> 4) & 3u);
+      blk.resize(tier_words(t));
+      if (hipMemcpy(blk.data(), sd->c.spill[t] + (size_t)(d.meta >> 8) * tier_words(t), 4 * blk.size(),
+                    hipMemcpyDeviceToHost) != hipSuccess)
+        return SWIM_EDEVICE;
+    }
+    const uint32_t cnt = n == COLL_SPILLED ? blk[0] : n;
     if (len) *len = cnt;
     for (uint32_t i = 0; i < cnt && i < cap && out; ++i) {
-      out[i].lo = n == COLL_SPILLED ? sp.lo[i] : d.lo;
-      out[i].hi = n == COLL_SPILLED ? sp.hi[i] : d.hi;
+      out[i].lo = n == COLL_SPILLED ? blk[4 + 2 * i] : d.lo;
+      out[i].hi = n == COLL_SPILLED ? blk[5 + 2 * i] : d.hi;
     }
     break;
   }
@@ -1271,20 +1302,34 @@ int32_t swim_kat_collector(const uint8_t* kinds, const int64_t* values, uint32_t
   int64_t* dv = nullptr;
   int64_t* dr = nullptr;
   CollEnt* de = nullptr;
-  CollDev* dsp = nullptr;
+  uint32_t* dsp = nullptr;  // one block per tier + the tier bookkeeping
   uint32_t* derr = nullptr;
+  // frees are recycled only at a tick end, so every spill of the run gets a fresh block
+  uint32_t kcap[NTIER];
+  size_t words = 0;
+  for (int t = 0; t < NTIER; ++t) {
+    kcap[t] = t < 2 ? n : std::min<uint32_t>(n, 8);
+    words += (size_t)kcap[t] * (tier_words(t) + 2);
+  }
   if (hipMalloc((void**)&dk, n) != hipSuccess || hipMalloc((void**)&dv, 8 * (size_t)n) != hipSuccess ||
       hipMalloc((void**)&dr, 8 * (size_t)n) != hipSuccess || hipMalloc((void**)&de, sizeof(CollEnt)) != hipSuccess ||
-      hipMalloc((void**)&dsp, sizeof(CollDev) * n + 4) != hipSuccess || hipMalloc((void**)&derr, 8) != hipSuccess)
+      hipMalloc((void**)&dsp, 4 * words) != hipSuccess ||
+      hipMalloc((void**)&derr, 4 + sizeof(SpillCtl) * NTIER) != hipSuccess)
     return SWIM_EDEVICE;
   hipMemcpy(dk, kinds, n, hipMemcpyHostToDevice);
   hipMemcpy(dv, values, 8 * (size_t)n, hipMemcpyHostToDevice);
-  hipMemset(derr, 0, 8);
+  hipMemset(derr, 0, 4 + sizeof(SpillCtl) * NTIER);
   Ctx c{};
   c.err = derr;
-  c.spill = dsp;
-  c.spill_cnt = derr + 1;
-  c.spill_cap = n;
+  c.spill_ctl = reinterpret_cast<SpillCtl*>(derr + 1);
+  c.seg_threshold = INT32_MAX;
+  uint32_t* p = dsp;
+  for (int t = 0; t < NTIER; ++t) {
+    c.spill[t] = p; p += (size_t)kcap[t] * tier_words(t);
+    c.spill_avail[t] = p; p += kcap[t];
+    c.spill_freed[t] = p; p += kcap[t];
+    c.spill_cap[t] = kcap[t];
+  }
   k_kat_collector<<<1, 64>>>(c, dk, dv, n, dr, de);
   hipError_t r = hipMemcpy(results, dr, 8 * (size_t)n, hipMemcpyDeviceToHost);
   uint32_t err = 0;

@@ -1,11 +1,12 @@
 // swim_device.h — device data layout and per-viewer protocol logic of the lockstep SWIM engine.
 //
 // Layout: everything is structure-of-arrays in HBM, row-major per viewer.
-//   cells   u64[N][N]   packed view cell per (viewer, subject)  — swim.h cell format
+//   recs    u32[N][N]   view record word per (viewer, subject); aux u32[N][N] the side maps
 //   ping    u32[N][N]   FailureDetectorImpl.pingMembers of each viewer (ArrayList order)
 //   remote  u32[N][N]   GossipProtocolImpl.remoteMembers of each viewer
 //   slab    GossipDev[N][gcap]  live GossipStates, insertion order
-//   coll    CollDev[N][hcap]    SequenceIdCollector per (viewer, gossiper), open addressing
+//   coll    CollEnt[N][hcap]    SequenceIdCollector per (viewer, gossiper), open addressing, one
+//                               interval inline; more spill to size-tiered interval blocks
 //   mem     MemberDev[N]        scalar per-member protocol state
 //
 // The functions below run on ONE thread that owns viewer v for the duration of a phase (the
@@ -23,7 +24,7 @@ namespace swimdev {
 
 constexpr uint32_t NONE = 0xffffffffu;
 enum : uint32_t { MF_FDSYNC = 1, MF_JOIN = 2, MF_LEAVE = 4 };  // Ctx.mflag bits
-constexpr int KIV = 6;         // inline intervals per SequenceIdCollector
+constexpr int NTIER = 4;       // spilled-collector block tiers
 constexpr int FD_SYNC_MAX = 33;  // FD-triggered SYNCs per member per tick (<= 2k+1)
 
 // error bits (stats.capacity_errors / SWIM_ECAPACITY)
@@ -59,26 +60,46 @@ struct alignas(16) MemberDev {
   uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, pad[2];
 };
 
-struct GossipDev {  // GossipState + Gossip + MembershipRecord payload, 32 B
+// GossipState + Gossip + MembershipRecord payload, 48 B.  GossipState.infected gains a member only
+// when the collector accepts the sequence id (onGossipReq :205-212): the first sender, plus one more
+// per re-acceptance after checkGossipSegmentation cleared the collector; GINF entries hold that
+// (ERR_INFECTED beyond, never a silent truncation).
+constexpr int GINF = 6;
+struct GossipDev {
   uint32_t gossiper, subject, seq, inf_period;
   int32_t inc;
   uint32_t status;
-  uint32_t inf0, inf1;  // GossipState.infected (NONE = empty)
+  uint32_t inf[GINF];  // GossipState.infected in insertion order (NONE = empty)
 };
+__device__ __forceinline__ bool gossip_infected(const GossipDev& g, uint32_t m) {
+  bool r = false;
+#pragma unroll
+  for (int k = 0; k < GINF; ++k) r |= g.inf[k] == m;
+  return r;
+}
 
 // SequenceIdCollector (SequenceIdCollector.java) of (viewer, gossiper), 16 B: a collector holds one
 // interval almost always (a gossiper's sequence ids reach a member in order), so the interval is
-// inline and a collector that needs more spills to a 64-B CollDev of up to KIV intervals.
+// inline.  One that needs more (out-of-order arrival, loss) spills to a block of a size tier —
+// 6, 62, 510 or 2,046 closed intervals (64 B .. 16 KiB: a 4-word header {count} + (lo, hi) pairs,
+// ascending) — grows tier by tier, and returns inline when its intervals merge back into one.
+// The reference keeps up to gossipSegmentationThreshold (1,000) intervals before a gossip round
+// clears the collector (checkGossipSegmentation, GossipProtocolImpl.java:217-236); the top tier
+// leaves room for a round's growth beyond that.  Freed blocks are recycled from the next tick on.
 struct CollEnt {
   uint32_t key;   // gossiper + 1; 0 = empty slot
   uint32_t lo, hi;
   uint32_t meta;  // bits 0..2: inline interval count (0 / 1) or COLL_SPILLED; bit 3: cleared;
-                  // bits 8..31: spill index
+                  // bits 4..5: spill tier; bits 8..31: block index in the tier
 };
 constexpr uint32_t COLL_SPILLED = 7u, COLL_CLEARED = 8u;
-struct CollDev {  // spilled SequenceIdCollector: up to KIV closed intervals, ascending
-  uint32_t n, pad[3];
-  uint32_t lo[KIV], hi[KIV];
+__host__ __device__ constexpr uint32_t tier_cap(int t) { return t == 0 ? 6u : t == 1 ? 62u : t == 2 ? 510u : 2046u; }
+__host__ __device__ constexpr uint32_t tier_words(int t) { return 4u + 2u * tier_cap(t); }
+struct SpillCtl {  // one per tier
+  uint32_t bump;    // blocks ever carved from the pool
+  int32_t avail;    // recyclable blocks in `avail` (may dip below 0 during a tick: failed pops)
+  uint32_t freed;   // blocks freed this tick (recyclable from the next)
+  uint32_t pad;
 };
 
 struct LinkDev {  // NetworkEmulator per-link override, sorted by (a, b)
@@ -125,9 +146,12 @@ struct Ctx {
   uint32_t* remote;
   GossipDev* slab;
   CollEnt* coll;       // [nl][hcap] open addressing by gossiper
-  CollDev* spill;      // spilled multi-interval collectors
-  uint32_t* spill_cnt;
-  uint32_t spill_cap;
+  uint32_t* spill[NTIER];        // spilled collectors: tier t holds spill_cap[t] blocks of tier_words(t)
+  uint32_t* spill_avail[NTIER];  // recyclable block indices
+  uint32_t* spill_freed[NTIER];  // block indices freed this tick
+  uint32_t spill_cap[NTIER];
+  SpillCtl* spill_ctl;           // [NTIER]
+  uint32_t* seg_flag;            // per viewer: a collector exceeded gossipSegmentationThreshold
   uint32_t* fd_sync;
   uint64_t* wheel;      // [W][SUBQ][wheel_cap / SUBQ]
   uint32_t* wheel_cnt;  // [W][SUBQ]
@@ -347,83 +371,146 @@ __device__ inline CollEnt* coll_ensure(const Ctx& c, uint32_t v, uint32_t gossip
   set_err(c, ERR_HASH);
   return nullptr;
 }
-// SequenceIdCollector.contains (SequenceIdCollector.java:32-35) on a KIV-interval set
-__device__ inline bool coll_dev_contains(const CollDev* e, uint32_t x) {
-  for (int i = (int)e->n - 1; i >= 0; --i)
-    if (e->lo[i] <= x) return x <= e->hi[i];
-  return false;
+// ---- spilled-collector blocks.  Tier-indexed Ctx members are read through selects, never a runtime
+// array index: indexing an array member of the kernel's register-resident Ctx copy with a runtime
+// value spills the whole Ctx to scratch (measured: 520-660 B/lane in every collector kernel).
+template <typename T>
+__device__ __forceinline__ T tier_sel(const T (&a)[NTIER], int t) {
+  return t == 0 ? a[0] : t == 1 ? a[1] : t == 2 ? a[2] : a[3];
 }
+__device__ __forceinline__ uint32_t tier_words_d(int t) {
+  return t == 0 ? tier_words(0) : t == 1 ? tier_words(1) : t == 2 ? tier_words(2) : tier_words(3);
+}
+__device__ __forceinline__ uint32_t* coll_block(const Ctx& c, uint32_t meta) {
+  const int t = (int)((meta >> 4) & 3u);
+  return tier_sel(c.spill, t) + (size_t)(meta >> 8) * tier_words_d(t);
+}
+__device__ inline uint32_t spill_alloc(const Ctx& c, int t) {
+  const int32_t a = atomicSub(&c.spill_ctl[t].avail, 1);
+  if (a > 0) return tier_sel(c.spill_avail, t)[a - 1];
+  const uint32_t i = atomicAdd(&c.spill_ctl[t].bump, 1u);
+  if (i >= tier_sel(c.spill_cap, t) || i >= (1u << 24)) { set_err(c, ERR_INTERVALS); return NONE; }
+  return i;
+}
+__device__ inline void spill_free(const Ctx& c, uint32_t meta) {
+  const int t = (int)((meta >> 4) & 3u);
+  const uint32_t j = atomicAdd(&c.spill_ctl[t].freed, 1u);
+  if (j < tier_sel(c.spill_cap, t)) tier_sel(c.spill_freed, t)[j] = meta >> 8;
+}
+// greatest i with iv[i].lo <= x, or -1 (TreeMap.floorEntry)
+__device__ inline int coll_floor(const uint2* iv, uint32_t n, uint32_t x) {
+  int lo = 0, hi = (int)n - 1, r = -1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    if (iv[mid].x <= x) { r = mid; lo = mid + 1; } else { hi = mid - 1; }
+  }
+  return r;
+}
+// SequenceIdCollector.contains (SequenceIdCollector.java:32-35)
 __device__ inline bool coll_contains(const Ctx& c, const CollEnt* e, uint32_t x) {
   if (!e) return false;
-  const uint32_t n = e->meta & 7u;
+  const uint32_t meta = e->meta, n = meta & 7u;
   if (n == 1) return e->lo <= x && x <= e->hi;
-  if (n == COLL_SPILLED) return coll_dev_contains(c.spill + (e->meta >> 8), x);
-  return false;
+  if (n != COLL_SPILLED) return false;
+  const uint32_t* blk = coll_block(c, meta);
+  const uint2* iv = reinterpret_cast<const uint2*>(blk + 4);
+  const int f = coll_floor(iv, blk[0], x);
+  return f >= 0 && x <= iv[f].y;
 }
-// SequenceIdCollector.add (SequenceIdCollector.java:43-72) on a KIV-interval set
-__device__ inline bool coll_dev_add(const Ctx& c, CollDev* e, uint32_t x) {
-  int n = (int)e->n, fl = -1;
-  for (int i = n - 1; i >= 0; --i)
-    if (e->lo[i] <= x) { fl = i; break; }
-  if (fl >= 0 && x <= e->hi[fl]) return false;
-  int ce = fl + 1;  // first interval with lo > x (lo == x would have been the floor)
-  bool nf = fl >= 0 && (int64_t)x - 1 == (int64_t)e->hi[fl];
-  bool nc = ce < n && (int64_t)x + 1 == (int64_t)e->lo[ce];
-  if (nf && nc) {
-    e->hi[fl] = e->hi[ce];
-    for (int i = ce; i + 1 < n; ++i) { e->lo[i] = e->lo[i + 1]; e->hi[i] = e->hi[i + 1]; }
-    e->n = n - 1;
-  } else if (nf) {
-    e->hi[fl] = x;
-  } else if (nc) {
-    e->lo[ce] = x;
-  } else {
-    if (n == KIV) { set_err(c, ERR_INTERVALS); return true; }
-    for (int i = n; i > ce; --i) { e->lo[i] = e->lo[i - 1]; e->hi[i] = e->hi[i - 1]; }
-    e->lo[ce] = x;
-    e->hi[ce] = x;
-    e->n = n + 1;
-  }
-  return true;
-}
-__device__ inline bool coll_add(const Ctx& c, CollEnt* e, uint32_t x) {
+// SequenceIdCollector.add (SequenceIdCollector.java:43-72).  `seg` (the viewer's segmentation flag)
+// is raised when the collector ends up with more than c.seg_threshold intervals.
+__device__ inline bool coll_add(const Ctx& c, CollEnt* e, uint32_t x, uint32_t* seg = nullptr) {
   if (!e) return true;
-  const uint32_t n = e->meta & 7u;
-  if (n == COLL_SPILLED) return coll_dev_add(c, c.spill + (e->meta >> 8), x);
-  if (n == 0) {
+  uint32_t meta = e->meta;
+  const uint32_t n0 = meta & 7u;
+  if (n0 == 0) {
     e->lo = e->hi = x;
-    e->meta = (e->meta & ~7u) | 1u;
+    e->meta = (meta & ~7u) | 1u;
     return true;
   }
-  if (e->lo <= x && x <= e->hi) return false;
-  if ((int64_t)x == (int64_t)e->hi + 1) { e->hi = x; return true; }
-  if ((int64_t)x + 1 == (int64_t)e->lo) { e->lo = x; return true; }
-  // a second disjoint interval: spill
-  const uint32_t i = atomicAdd(c.spill_cnt, 1u);
-  if (i >= c.spill_cap || i >= (1u << 24)) { set_err(c, ERR_INTERVALS); return true; }
-  CollDev* d = c.spill + i;
-  d->n = 1;
-  d->lo[0] = e->lo;
-  d->hi[0] = e->hi;
-  e->meta = (e->meta & COLL_CLEARED) | COLL_SPILLED | (i << 8);
-  return coll_dev_add(c, d, x);
+  if (n0 == 1) {
+    if (e->lo <= x && x <= e->hi) return false;
+    if ((int64_t)x == (int64_t)e->hi + 1) { e->hi = x; return true; }
+    if ((int64_t)x + 1 == (int64_t)e->lo) { e->lo = x; return true; }
+    // a second disjoint interval: spill to the smallest tier
+    const uint32_t i = spill_alloc(c, 0);
+    if (i == NONE) return true;
+    uint32_t* blk = c.spill[0] + (size_t)i * tier_words(0);
+    uint2* iv = reinterpret_cast<uint2*>(blk + 4);
+    if (x < e->lo) { iv[0] = make_uint2(x, x); iv[1] = make_uint2(e->lo, e->hi); }
+    else { iv[0] = make_uint2(e->lo, e->hi); iv[1] = make_uint2(x, x); }
+    blk[0] = 2;
+    e->meta = (meta & COLL_CLEARED) | COLL_SPILLED | (i << 8);
+    if (seg && 2 > (uint32_t)c.seg_threshold) *seg = 1;
+    return true;
+  }
+  uint32_t* blk = coll_block(c, meta);
+  uint2* iv = reinterpret_cast<uint2*>(blk + 4);
+  uint32_t n = blk[0];
+  const int fl = coll_floor(iv, n, x);
+  if (fl >= 0 && x <= iv[fl].y) return false;
+  const int ce = fl + 1;  // first interval with lo > x
+  const bool nf = fl >= 0 && (int64_t)x - 1 == (int64_t)iv[fl].y;
+  const bool nc = ce < (int)n && (int64_t)x + 1 == (int64_t)iv[ce].x;
+  if (nf && nc) {
+    iv[fl].y = iv[ce].y;
+    for (uint32_t i = (uint32_t)ce; i + 1 < n; ++i) iv[i] = iv[i + 1];
+    n--;
+  } else if (nf) {
+    iv[fl].y = x;
+  } else if (nc) {
+    iv[ce].x = x;
+  } else {
+    const int t = (int)((meta >> 4) & 3u);
+    if (n == (t == 0 ? tier_cap(0) : t == 1 ? tier_cap(1) : t == 2 ? tier_cap(2) : tier_cap(3))) {  // grow
+      if (t + 1 == NTIER) { set_err(c, ERR_INTERVALS); return true; }
+      const uint32_t i = spill_alloc(c, t + 1);
+      if (i == NONE) return true;
+      uint32_t* nb = tier_sel(c.spill, t + 1) + (size_t)i * tier_words_d(t + 1);
+      uint2* niv = reinterpret_cast<uint2*>(nb + 4);
+      for (uint32_t k = 0; k < n; ++k) niv[k] = iv[k];
+      spill_free(c, meta);
+      meta = (meta & COLL_CLEARED) | COLL_SPILLED | ((uint32_t)(t + 1) << 4) | (i << 8);
+      e->meta = meta;
+      blk = nb;
+      iv = niv;
+    }
+    for (uint32_t i = n; i > (uint32_t)ce; --i) iv[i] = iv[i - 1];
+    iv[ce] = make_uint2(x, x);
+    n++;
+  }
+  if (n == 1) {  // merged back into one interval: inline again
+    e->lo = iv[0].x;
+    e->hi = iv[0].y;
+    spill_free(c, meta);
+    e->meta = (meta & COLL_CLEARED) | 1u;
+    return true;
+  }
+  blk[0] = n;
+  if (seg && n > (uint32_t)c.seg_threshold) *seg = 1;
+  return true;
 }
 // number of intervals (checkGossipSegmentation's size())
 __device__ inline uint32_t coll_size(const Ctx& c, const CollEnt* e) {
   const uint32_t n = e->meta & 7u;
-  return n == COLL_SPILLED ? c.spill[e->meta >> 8].n : n;
+  return n == COLL_SPILLED ? coll_block(c, e->meta)[0] : n;
 }
 // clear() / remove: no intervals, marked cleared (a GossipState may outlive its collector entries)
-__device__ inline void coll_clear(CollEnt* e) { e->meta = COLL_CLEARED; }
+__device__ inline void coll_clear(const Ctx& c, CollEnt* e) {
+  if ((e->meta & 7u) == COLL_SPILLED) spill_free(c, e->meta);
+  e->meta = COLL_CLEARED;
+}
 
 // ------------------------------------------------------------------------------- events
 // Appends from thousands of threads in one kernel (a timer storm removes a member at every viewer
 // in one tick) go to SUBQ sub-queues picked by the wave, so no single counter serialises them;
 // order is canonicalised on the host ((tick, viewer, phase, minor) sort).
 constexpr uint32_t SUBQ = 16;
-__device__ __forceinline__ uint32_t subq() { return (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (SUBQ - 1); }
+// sub-queue of an append for (viewer, subject): hashed, not by the appending wave — one lane may
+// append thousands (a SYNC merge schedules a timer and emits an event per record it changes)
+__device__ __forceinline__ uint32_t subq(uint32_t v, uint32_t s) { return ((v * 0x9E3779B1u) ^ (s * 0x85EBCA77u)) >> 28; }
 __device__ inline void emit(const Ctx& c, uint32_t v, uint32_t s, uint32_t type, uint32_t phase, uint32_t minor) {
-  const uint32_t q = subq();
+  const uint32_t q = subq(v, s);
   uint32_t i = atomicAdd(&c.ev_cnt[q], 1u);
   if (i >= c.ev_cap) { set_err(c, ERR_EVENTS); return; }
   i += q * c.ev_cap;
@@ -468,7 +555,7 @@ __device__ inline void on_added(const Ctx& c, uint32_t v, uint32_t s, uint32_t p
 // Safe under entry-parallel timer processing: only the (v, s) collector entry is written.
 __device__ inline void on_removed(const Ctx& c, uint32_t v, uint32_t s) {
   CollEnt* e = coll_find(c, v, s);
-  if (e) coll_clear(e);
+  if (e) coll_clear(c, e);
   c.compact_flag[v - c.lo] = 1u;
 }
 
@@ -495,13 +582,13 @@ __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject,
   g.status = status;
   g.inc = inc;
   g.inf_period = (uint32_t)m.g_period;
-  g.inf0 = NONE;
-  g.inf1 = NONE;
+#pragma unroll
+  for (int k = 0; k < GINF; ++k) g.inf[k] = NONE;
   slab_of(c, v)[m.gossip_len] = g;
   m.gossip_len++;
   m.g_counter++;
   CollEnt* e = coll_ensure(c, v, v);
-  coll_add(c, e, g.seq);
+  coll_add(c, e, g.seq, &c.seg_flag[v - c.lo]);
   stat_add(c, ST_GOSSIPS_CREATED, 1);
 }
 
@@ -515,7 +602,7 @@ __device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
   uint64_t ms = (uint64_t)c.suspicion_mult * (uint64_t)ceil_log2(mem(c, v).table_size) * (uint64_t)c.ping_interval;
   uint64_t deadline = c.T + ms / c.tick_ms;
   *ap = (a & 0xfu) | A_HAS_TIMER | ((uint32_t)(deadline & SWIM_DEADLINE_MASK) << 4);
-  const uint32_t b = (uint32_t)(deadline & c.wheel_mask), q = subq(), qcap = c.wheel_cap / SUBQ;
+  const uint32_t b = (uint32_t)(deadline & c.wheel_mask), q = subq(v, s), qcap = c.wheel_cap / SUBQ;
   const uint32_t i = atomicAdd(&c.wheel_cnt[b * SUBQ + q], 1u);
   if (i >= qcap) { set_err(c, ERR_WHEEL); return; }
   c.wheel[(size_t)b * c.wheel_cap + (size_t)q * qcap + i] = ((uint64_t)v << 32) | s;

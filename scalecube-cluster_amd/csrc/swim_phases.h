@@ -3,7 +3,7 @@
 // Phase A  k_timers                                   suspicion timeouts
 // Phase B  k_fd                                       list compaction after REMOVED, then ping /
 //                                                     ping-req / ack resolution + FD events
-// Phase C  k_gossip_seg, k_gossip_emit, k_alloc, k_scatter_msgs, k_gossip_deliver
+// Phase C  k_gossip_round (+ segmentation), k_gossip_emit, k_alloc, k_scatter_msgs, k_gossip_deliver
 // Phase D  k_sync_collect, k_sync_prep, k_sync_classify, k_sync_apply (swim_sync.h; SYNC and SYNC_ACK)
 // lists    k_ins_apply                                deferred pingMembers inserts of ADDED events
 // tick end k_end_tick
@@ -452,16 +452,6 @@ __device__ __forceinline__ bool gossip_due(const Ctx& c, uint32_t v, const Membe
 
 // checkGossipSegmentation (GossipProtocolImpl.java:217-236); only launched when the threshold is
 // below the inline interval capacity (otherwise a clear can never trigger).
-__global__ void k_gossip_seg(KP) {
-  const Ctx c = pctx(P, T);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= c.nl) return;
-  const MemberDev& m = c.mem[i];
-  if (!gossip_due(c, c.lo + i, m)) return;
-  CollEnt* base = c.coll + (size_t)i * c.hcap;
-  for (uint32_t j = 0; j < c.hcap; ++j)
-    if (base[j].key && (int32_t)coll_size(c, base + j) > c.seg_threshold) coll_clear(base + j);
-}
 
 // a GOSSIP_REQ for a receiver owned by this shard joins the receiver's inbox
 __device__ inline void deliver_local_msg(const Ctx& c, const Bufs& b, GMsgFull msg) {
@@ -527,7 +517,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     bool send = false, mat = false;
     if (act) {
       g = slab[p];
-      send = (uint64_t)g.inf_period + spread >= period && g.inf0 != t && g.inf1 != t;
+      send = (uint64_t)g.inf_period + spread >= period && !gossip_infected(g, t);
       // delivered copies; a receiver on this shard that already holds the sequence id drops it
       // (its collector only grows until delivery), another shard filters on arrival
       mat = send && c.up[t] && in_pass(c, t, v) && !lost_k(c, out_loss(c, v, t), v, SWIM_STREAM_GOSSIP_OUT, j, p) &&
@@ -640,6 +630,14 @@ __global__ void k_gossip_round(KP) {
       const uint64_t period = m.g_period;
       m.g_period = period + 1;
       m.period_used = period;
+      // checkGossipSegmentation (:217-236): clear collectors holding more than the threshold of
+      // intervals; only viewers whose collector crossed it since their last round look
+      if (c.seg_flag[i]) {
+        c.seg_flag[i] = 0;
+        CollEnt* base = c.coll + (size_t)i * c.hcap;
+        for (uint32_t j = 0; j < c.hcap; ++j)
+          if (base[j].key && (int32_t)coll_size(c, base + j) > c.seg_threshold) coll_clear(c, base + j);
+      }
       busy = m.gossip_len != 0;  // else no target selection, no shuffle draw
     }
   }
@@ -748,7 +746,7 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, Gos
   CollEnt* col = coll_ensure(c, r, g.gossiper);
   if (!col) return false;
   const bool was_cleared = (col->meta & COLL_CLEARED) != 0;
-  if (!coll_add(c, col, g.seq)) return false;
+  if (!coll_add(c, col, g.seq, &c.seg_flag[r - c.lo])) return false;
   int32_t found = -1;
   if (was_cleared) {  // a GossipState can outlive its collector entry only after a clear
     for (uint32_t p = 0; p < m.gossip_len; ++p)
@@ -759,17 +757,19 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, Gos
     GossipDev ns;
     ns.gossiper = g.gossiper; ns.seq = g.seq; ns.subject = g.subject; ns.status = g.status; ns.inc = g.inc;
     ns.inf_period = (uint32_t)m.g_period;
-    ns.inf0 = g.from;
-    ns.inf1 = NONE;
+    ns.inf[0] = g.from;
+#pragma unroll
+    for (int k = 1; k < GINF; ++k) ns.inf[k] = NONE;
     slab[m.gossip_len++] = ns;
     // onMembershipGossip (MembershipProtocolImpl.java:452-459)
     if (update_membership(c, r, g.subject, g.status, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP))
       apply_alive(c, r, g.subject, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP);
   } else {
     GossipDev& st = slab[found];
-    if (st.inf0 != g.from && st.inf1 != g.from) {
-      if (st.inf0 == NONE) st.inf0 = g.from;
-      else if (st.inf1 == NONE) st.inf1 = g.from;
+    if (!gossip_infected(st, g.from)) {
+      int k = 0;
+      while (k < GINF && st.inf[k] != NONE) ++k;
+      if (k < GINF) st.inf[k] = g.from;
       else set_err(c, ERR_INFECTED);
     }
   }
@@ -1041,6 +1041,20 @@ __global__ void k_end_tick(KP, uint32_t n_rx_stops) {
   Xc* x = P->c.world > 1 ? P->b.x : nullptr;
   const uint32_t* rx_stops = P->b.rx_stops;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  // collector blocks freed this tick become allocatable (one workgroup: the counters are read,
+  // then rewritten, by the same threads)
+  if (blockIdx.x == 0) {
+    for (int t = 0; t < NTIER; ++t) {
+      const int32_t a0 = c.spill_ctl[t].avail;
+      const uint32_t a = a0 > 0 ? (uint32_t)a0 : 0u, f = min(c.spill_ctl[t].freed, c.spill_cap[t] - a);
+      for (uint32_t j = threadIdx.x; j < f; j += blockDim.x) c.spill_avail[t][a + j] = c.spill_freed[t][j];
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        c.spill_ctl[t].avail = (int32_t)(a + f);
+        c.spill_ctl[t].freed = 0;
+      }
+    }
+  }
   // every other kernel of the tick has completed: reset the per-tick scratch counters
   if (i < sizeof(Counters) / 4) reinterpret_cast<uint32_t*>(k)[i] = 0;
   if (x && i < sizeof(Xc) / 4) reinterpret_cast<uint32_t*>(x)[i] = 0;
@@ -1072,7 +1086,7 @@ __global__ void k_kat_overrides(const int32_t* cases, uint32_t n, uint8_t* out) 
   out[i] = is_overrides((uint32_t)k[0], k[1], k[2] != 0, (uint32_t)k[3], k[4]) ? 1 : 0;
 }
 
-// SequenceIdCollectorTest through the engine's own collector code (inline entry + spill pool)
+// SequenceIdCollectorTest through the engine's own collector code (inline entry + spill tiers)
 __global__ void k_kat_collector(Ctx c, const uint8_t* kinds, const int64_t* values, uint32_t n, int64_t* res,
                                 CollEnt* e) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -1083,7 +1097,7 @@ __global__ void k_kat_collector(Ctx c, const uint8_t* kinds, const int64_t* valu
       case 0: res[i] = coll_add(c, e, x) ? 1 : 0; break;
       case 1: res[i] = coll_contains(c, e, x) ? 1 : 0; break;
       case 2: res[i] = coll_size(c, e); break;
-      default: coll_clear(e); res[i] = 0; break;
+      default: coll_clear(c, e); res[i] = 0; break;
     }
   }
 }

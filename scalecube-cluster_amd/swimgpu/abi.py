@@ -62,7 +62,9 @@ class swim_config(C.Structure):
         ("device", C.c_int32),
         ("local_shards", C.c_int32),
         ("timer_stagger", C.c_int32),
-        ("reserved", C.c_uint32 * 5),
+        ("timer_capacity", C.c_uint32),
+        ("message_capacity", C.c_uint32),
+        ("reserved", C.c_uint32 * 3),
     ]
 
 

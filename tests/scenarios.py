@@ -123,6 +123,17 @@ def catalog() -> list[Scenario]:
                  ops=[(0, "loss", 2, abi.ALL_MEMBERS)] + [(60 * i, "kill", 2 + 3 * i) for i in range(1, 6)]
                  + [(60 * i + 7, "join", 39 + i) for i in range(1, 9)] + [(333, "leave", 20, 1)],
                  check_every=50),
+        # join burst through one seed under loss: the seed's ALIVE gossips reach members out of order,
+        # so collectors spill into interval blocks (tier growth, merge back inline, block recycling)
+        Scenario("join_burst_144", 144, 64, 260, seed=22, seeds=(0,),
+                 ops=[(0, "loss", 10, abi.ALL_MEMBERS)] + [(5, "join", 64 + i) for i in range(80)],
+                 check_every=20),
+        # the same with gossipSegmentationThreshold = 8: collectors cleared by checkGossipSegmentation, and
+        # gossips re-accepted afterwards (GossipState.infected grows past its first sender)
+        Scenario("join_burst_seg", 144, 64, 260, seed=23, seeds=(0,),
+                 cfg=dict(gossip_segmentation_threshold=8, gossip_capacity=4096),
+                 ops=[(0, "loss", 10, abi.ALL_MEMBERS)] + [(5, "join", 64 + i) for i in range(80)],
+                 check_every=20),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),
                  cfg=dict(sync_interval=5000), ops=[(100, "partition", _partition(32, 16)), (1100, "partition", None)],

@@ -39,6 +39,11 @@ def test_gpu_kat_collector(glib):
     kat.check_collector(glib)
 
 
+def test_gpu_kat_collector_random(glib):
+    """Every spill tier of the device collector (up to ~1,200 intervals), growth and merge-back."""
+    kat.check_collector_random(glib)
+
+
 def test_gpu_kat_philox(glib):
     kat.check_philox(glib)
 

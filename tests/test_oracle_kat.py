@@ -51,6 +51,74 @@ def check_collector(lib):
         assert [g for g, e in zip(got, expected) if e is not None] == [e for e in expected if e is not None], name
 
 
+class TreeMapCollector:
+    """SequenceIdCollector (SequenceIdCollector.java:43-72) restated over a sorted interval list: the
+    model the randomized collector test checks the oracle's and the device's collectors against."""
+
+    def __init__(self):
+        self.iv = []  # [lo, hi] ascending, disjoint, non-adjacent
+
+    def _floor(self, x):
+        lo, hi, r = 0, len(self.iv) - 1, -1
+        while lo <= hi:
+            mid = (lo + hi) // 2
+            if self.iv[mid][0] <= x:
+                r, lo = mid, mid + 1
+            else:
+                hi = mid - 1
+        return r
+
+    def contains(self, x):
+        f = self._floor(x)
+        return f >= 0 and x <= self.iv[f][1]
+
+    def add(self, x):
+        f = self._floor(x)
+        if f >= 0 and x <= self.iv[f][1]:
+            return False
+        c = f + 1
+        nf = f >= 0 and x - 1 == self.iv[f][1]
+        nc = c < len(self.iv) and x + 1 == self.iv[c][0]
+        if nf and nc:
+            self.iv[f][1] = self.iv[c][1]
+            del self.iv[c]
+        elif nf:
+            self.iv[f][1] = x
+        elif nc:
+            self.iv[c][0] = x
+        else:
+            self.iv.insert(c, [x, x])
+        return True
+
+
+def random_collector_ops(seed, n_ops=6000, span=5000):
+    """Random adds / contains / size over [0, span): grows one collector to ~1,200 intervals (every
+    spill tier of the device collector) and merges most of them back; a clear half way.  The
+    model's own answers are checked against the committed reference KATs (check_collector)."""
+    import random
+    rng = random.Random(seed)
+    ops, model, expected = [], TreeMapCollector(), []
+    for i in range(n_ops):
+        if i == n_ops // 2:
+            ops.append(("clear", 0))
+            model.iv = []
+            expected.append(0)
+            continue
+        k = rng.choice((0, 0, 0, 1, 2))
+        x = rng.randrange(span) if i < n_ops // 2 else rng.randrange(span // 2)
+        ops.append((("add", "contains", "size")[k], x))
+        expected.append(int(model.add(x)) if k == 0 else int(model.contains(x)) if k == 1 else len(model.iv))
+    return ops, expected
+
+
+def check_collector_random(lib, seeds=(1, 2)):
+    for seed in seeds:
+        ops, expected = random_collector_ops(seed)
+        got = abi.kat_collector(lib, ops)
+        bad = [i for i, (g, e) in enumerate(zip(got, expected)) if g != e]
+        assert not bad, f"seed {seed}: first mismatch at op {bad[0]}: {ops[bad[0]]} got {got[bad[0]]} want {expected[bad[0]]}"
+
+
 PHILOX_KAT = [  # Random123 kat_vectors: philox4x32 10 <ctr> <key> <expected>
     ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
     ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
@@ -89,6 +157,27 @@ def test_oracle_overrides_truth_table(olib):
 
 def test_oracle_sequence_id_collector(olib):
     check_collector(olib)
+
+
+def test_treemap_model_matches_reference_kats():
+    """The collector model of the randomized test answers every SequenceIdCollectorTest assertion."""
+    for name, (ops, expected) in COLLECTOR_CASES.items():
+        m, got = TreeMapCollector(), []
+        for o in ops:
+            if o[0] == "add":
+                got.append(int(m.add(o[1])))
+            elif o[0] == "contains":
+                got.append(int(m.contains(o[1])))
+            elif o[0] == "size":
+                got.append(len(m.iv))
+            else:
+                m.iv = []
+                got.append(0)
+        assert [g for g, e in zip(got, expected) if e is not None] == [e for e in expected if e is not None], name
+
+
+def test_oracle_collector_random(olib):
+    check_collector_random(olib)
 
 
 def test_oracle_philox_kat(olib):
