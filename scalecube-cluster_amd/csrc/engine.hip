@@ -436,6 +436,7 @@ static Ctx sync_ctx(Shard& sd) {  // list inserts of the SYNC phase use the seco
   Ctx cd = sd.c;
   cd.ins_total = &sd.k->ins_total2;
   cd.ins_list_cnt = &sd.k->ins_list_cnt2;
+  cd.ins_direct = 1;
   return cd;
 }
 
@@ -538,7 +539,6 @@ static int32_t run_tick(swim_engine* e) {
     }
   }
   for (Shard& sd : e->sh) {
-    run_ins_pipeline(e, sd, 1);
     // ---- end of tick (also zeroes the per-tick counters and applies other shards' stops)
     const uint32_t ge = grid_for(std::max<uint32_t>(std::max<uint32_t>(sd.c.nl, sd.n_rx_stops), 64), 256);
     k_end_tick<<<ge, 256, 0, s>>>(sd.d_par, T, sd.n_rx_stops);

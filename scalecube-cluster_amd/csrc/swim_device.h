@@ -172,7 +172,8 @@ struct Ctx {
   InsOp* ins;
   uint32_t* ins_total;
   uint32_t ins_cap;
-  uint32_t* ins_list;      // viewers with ops
+  uint32_t* ins_list;      // viewers with ops (unused when ins_direct: the phase applies its own)
+  uint32_t ins_direct;     // SYNC phase: k_sync_apply applies a viewer's inserts after its merges
   uint32_t* ins_list_cnt;
   uint32_t* compact_flag;  // per viewer: lists hold a REMOVED member (compacted before its next FD step)
   // compact per-member schedule: lets the per-tick member scans skip idle members
@@ -541,7 +542,7 @@ __device__ inline void on_added(const Ctx& c, uint32_t v, uint32_t s, uint32_t p
   c.ins[i] = op;
   if (m.ins_rank++ == 0) {
     m.ins_head = i;
-    c.ins_list[atomicAdd(c.ins_list_cnt, 1u)] = v;
+    if (!c.ins_direct) c.ins_list[atomicAdd(c.ins_list_cnt, 1u)] = v;
   } else {
     c.ins[m.ins_tail].next = i;
   }

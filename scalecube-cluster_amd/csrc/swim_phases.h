@@ -887,45 +887,51 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
 // pingMembers.add(nextInt(size), member) (FailureDetectorImpl.java:334-345), in event order: one
 // workgroup per viewer with inserts walks the viewer's op chain; each insert shifts the tail right
 // by one, tail chunk first.
-__global__ void __launch_bounds__(256) k_ins_apply(KP, int sync_phase) {
-  const Ctx c = sync_phase ? pctx_sync(P, T) : pctx(P, T);
-  __shared__ uint32_t s_idx, s_s, s_next;
-  const uint32_t nv = *c.ins_list_cnt;
-  for (uint32_t i = blockIdx.x; i < nv; i += gridDim.x) {
-    const uint32_t v = c.ins_list[i];
-    MemberDev& m = mem(c, v);
-    const uint32_t k = m.ins_rank;
-    uint32_t* pl = ping_list(c, v);
-    uint32_t cur = m.ins_head;
-    for (uint32_t q = 0; q < k; ++q) {
-      const uint32_t size = m.ping_len;
-      if (threadIdx.x == 0) {
-        const InsOp op = c.ins[cur];
-        s_idx = size > 0 ? next_int(draw(c, v, SWIM_STREAM_PING_INSERT, op.phase, op.minor), size) : 0;
-        s_s = op.s;
-        s_next = op.next;
-      }
+// The deferred pingMembers.add(nextInt(size), s) ops of viewer v, in event order, by the whole
+// workgroup (tail-first parallel shift); every thread of the block must call it.
+__device__ void apply_ins_chain(const Ctx& c, uint32_t v) {
+  __shared__ uint32_t s_idx, s_s, s_next, s_k;
+  MemberDev& m = mem(c, v);
+  if (threadIdx.x == 0) s_k = m.ins_rank;
+  __syncthreads();
+  const uint32_t k = s_k;
+  uint32_t* pl = ping_list(c, v);
+  uint32_t cur = m.ins_head;
+  for (uint32_t q = 0; q < k; ++q) {
+    const uint32_t size = m.ping_len;
+    if (threadIdx.x == 0) {
+      const InsOp op = c.ins[cur];
+      s_idx = size > 0 ? next_int(draw(c, v, SWIM_STREAM_PING_INSERT, op.phase, op.minor), size) : 0;
+      s_s = op.s;
+      s_next = op.next;
+    }
+    __syncthreads();
+    const uint32_t idx = s_idx;
+    for (int64_t hi = (int64_t)size; hi > (int64_t)idx; hi -= blockDim.x) {
+      int64_t lo = hi - (int64_t)blockDim.x < (int64_t)idx ? (int64_t)idx : hi - (int64_t)blockDim.x;
+      int64_t p = lo + threadIdx.x;
+      uint32_t val = 0;
+      if (p < hi) val = pl[p];
       __syncthreads();
-      const uint32_t idx = s_idx;
-      for (int64_t hi = (int64_t)size; hi > (int64_t)idx; hi -= 256) {
-        int64_t lo = hi - 256 < (int64_t)idx ? (int64_t)idx : hi - 256;
-        int64_t p = lo + threadIdx.x;
-        uint32_t val = 0;
-        if (p < hi) val = pl[p];
-        __syncthreads();
-        if (p < hi) pl[p + 1] = val;
-        __syncthreads();
-      }
-      if (threadIdx.x == 0) {
-        pl[idx] = s_s;
-        m.ping_len = size + 1;
-      }
-      cur = s_next;
+      if (p < hi) pl[p + 1] = val;
       __syncthreads();
     }
-    if (threadIdx.x == 0) m.ins_rank = 0;
+    if (threadIdx.x == 0) {
+      pl[idx] = s_s;
+      m.ping_len = size + 1;
+    }
+    cur = s_next;
     __syncthreads();
   }
+  if (threadIdx.x == 0) m.ins_rank = 0;
+  __syncthreads();
+}
+
+// the gossip phase's inserts: one workgroup per viewer with ops
+__global__ void __launch_bounds__(256) k_ins_apply(KP, int sync_phase) {
+  const Ctx c = sync_phase ? pctx_sync(P, T) : pctx(P, T);
+  const uint32_t nv = *c.ins_list_cnt;
+  for (uint32_t i = blockIdx.x; i < nv; i += gridDim.x) apply_ins_chain(c, c.ins_list[i]);
 }
 
 // ------------------------------------------------------------------------------- phase D

@@ -678,5 +678,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       stat_add(c, ST_SYNC_RECORDS, s_recs);
     }
     __syncthreads();
+    // this sub-phase's pingMembers inserts of s (its ADDED events, all made by this workgroup)
+    apply_ins_chain(c, s);
   }
 }
