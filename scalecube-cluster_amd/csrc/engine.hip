@@ -31,7 +31,10 @@ namespace {
 
 constexpr uint32_t kDrainEvery = 256;  // longest interval between event drains (ticks)
 constexpr uint32_t kDrainFirst = 1;    // the interval starts at one tick and adapts to the event rate
-constexpr uint32_t kClassifyGrid = 1024;  // 4,096 waves: the resident capacity at 110 VGPRs (4 waves / SIMD)
+#ifndef CLS_GRID
+#define CLS_GRID 4096
+#endif
+constexpr uint32_t kClassifyGrid = CLS_GRID;  // 16,384 waves: about one (message, chunk) unit each at N = 65,536
 constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
 constexpr uint32_t kEmitGrid = 2048;      // 8,192 waves, one gossip sender at a time each
 constexpr uint32_t kStopCap = 4096;
@@ -500,10 +503,9 @@ static int32_t run_tick(swim_engine* e) {
     // ---- A: suspicion timeouts
     k_timers<<<256, 256, 0, s>>>(sd.d_par, T);
     // ---- B: list compaction of the timer phase's REMOVED + failure detector
-    k_fd<<<gm, 256, 0, s>>>(sd.d_par, T);
-    // ---- C: gossip round (emit)
+    // ---- C: gossip round (period++ and the sender list in k_fd, then emit)
+    k_fd<<<gm, 256, 0, s>>>(sd.d_par, T, gossip_tick ? 1 : 0);
     if (gossip_tick) {
-      k_gossip_round<<<gm, 256, 0, s>>>(sd.d_par, T);
       k_gossip_emit<<<kEmitGrid, 64 * EMIT_WAVES, 0, s>>>(sd.d_par, T);
     }
   }

@@ -3,7 +3,7 @@
 // Phase A  k_timers                                   suspicion timeouts
 // Phase B  k_fd                                       list compaction after REMOVED, then ping /
 //                                                     ping-req / ack resolution + FD events
-// Phase C  k_gossip_round (+ segmentation), k_gossip_emit, k_alloc, k_scatter_msgs, k_gossip_deliver
+// Phase C  round start (+ segmentation) in k_fd, k_gossip_emit, k_alloc, k_scatter_msgs, k_gossip_deliver
 // Phase D  k_sync_collect, k_sync_prep, k_sync_classify, k_sync_apply (swim_sync.h; SYNC and SYNC_ACK)
 // lists    k_ins_apply                                deferred pingMembers inserts of ADDED events
 // tick end k_end_tick
@@ -414,37 +414,6 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
   c.fd_next[v - c.lo] = fd_next_of(c, m, c.T);
 }
 
-// 256-thread workgroups, one viewer per thread.  First the workgroup compacts the ping / remote
-// lists of its viewers that lost a member in this tick's timer phase (a per-viewer dependency, so
-// no separate launch), then every thread runs its viewer's FD step.
-__global__ void __launch_bounds__(256) k_fd(KP) {
-  const Ctx c = pctx(P, T);
-  const uint32_t bucket = (uint32_t)(T & c.wheel_mask);
-  __shared__ uint32_t s_list[256];
-  __shared__ uint32_t s_cnt;
-  if (blockIdx.x == 0 && threadIdx.x < SUBQ) c.wheel_cnt[bucket * SUBQ + threadIdx.x] = 0;  // k_timers drained it
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool flagged = i < c.nl && c.compact_flag[i] != 0;
-  if (flagged) s_list[atomicAdd(&s_cnt, 1u)] = i;
-  __syncthreads();
-  const uint32_t nc = s_cnt;
-  for (uint32_t k = 0; k < nc; ++k) {
-    const uint32_t v = c.lo + s_list[k];
-    MemberDev& m = mem(c, v);
-    compact_list<256>(c, v, ping_list(c, v), m.ping_len);
-    compact_list<256>(c, v, remote_list(c, v), m.remote_len);
-  }
-  if (flagged) c.compact_flag[i] = 0;
-  __syncthreads();  // the compacted lengths are visible to every thread
-  unsigned long long nev = 0, nreq = 0, npings = 0;
-  if (i < c.nl && c.fd_next[i] == (uint32_t)T) fd_member(c, c.lo + i, nev, nreq, npings);
-  wave_stat_add(c, ST_FD_EVENTS, nev);
-  wave_stat_add(c, ST_PING_REQS, nreq);
-  wave_stat_add(c, ST_PINGS, npings);
-}
-
 // ------------------------------------------------------------------------------- phase C
 __device__ __forceinline__ bool gossip_due(const Ctx& c, uint32_t v, const MemberDev& m) {
   return c.up[v] && (int64_t)c.T > m.g_start && ((int64_t)c.T - m.g_start) % c.G == 0;
@@ -616,13 +585,11 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   return nmsg;
 }
 
-// doSpreadGossip's first steps for every due sender, one thread each: period++ (:143) and, when it
-// holds live gossips (:149-151), a place in the round's sender list
-// (launched with a multiple of 64 threads per block: the list append is one atomic per wave)
-__global__ void k_gossip_round(KP) {
-  const Ctx c = pctx(P, T);
-  const Bufs b = P->b;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// doSpreadGossip's first steps for a due sender (one thread each, run by k_fd right after the
+// member's FD step: both touch only the member's own state): period++ (:143) and, when it holds live
+// gossips (:149-151), a place in the round's sender list (called by every lane of a wave: the list
+// append is one atomic per wave)
+__device__ __forceinline__ void gossip_round(const Ctx& c, const Bufs& b, uint32_t i) {
   bool busy = false;
   if (i < c.nl) {
     MemberDev& m = c.mem[i];
@@ -647,6 +614,39 @@ __global__ void k_gossip_round(KP) {
   if ((threadIdx.x & 63) == 0) base = atomicAdd(&b.k->sender_cnt, (uint32_t)__popcll(mk));
   base = __shfl(base, 0, 64);
   if (busy) b.senders[base + lanes_below(mk)] = i;
+}
+
+// Phases B and C's first step.  256-thread workgroups, one viewer per thread.  First the workgroup compacts the ping / remote
+// lists of its viewers that lost a member in this tick's timer phase (a per-viewer dependency, so
+// no separate launch), then every thread runs its viewer's FD step and, on gossip ticks, the
+// first step of its gossip round (k_gossip_emit runs the rest after every FD step is done).
+__global__ void __launch_bounds__(256) k_fd(KP, int gossip) {
+  const Ctx c = pctx(P, T);
+  const uint32_t bucket = (uint32_t)(T & c.wheel_mask);
+  __shared__ uint32_t s_list[256];
+  __shared__ uint32_t s_cnt;
+  if (blockIdx.x == 0 && threadIdx.x < SUBQ) c.wheel_cnt[bucket * SUBQ + threadIdx.x] = 0;  // k_timers drained it
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool flagged = i < c.nl && c.compact_flag[i] != 0;
+  if (flagged) s_list[atomicAdd(&s_cnt, 1u)] = i;
+  __syncthreads();
+  const uint32_t nc = s_cnt;
+  for (uint32_t k = 0; k < nc; ++k) {
+    const uint32_t v = c.lo + s_list[k];
+    MemberDev& m = mem(c, v);
+    compact_list<256>(c, v, ping_list(c, v), m.ping_len);
+    compact_list<256>(c, v, remote_list(c, v), m.remote_len);
+  }
+  if (flagged) c.compact_flag[i] = 0;
+  __syncthreads();  // the compacted lengths are visible to every thread
+  unsigned long long nev = 0, nreq = 0, npings = 0;
+  if (i < c.nl && c.fd_next[i] == (uint32_t)T) fd_member(c, c.lo + i, nev, nreq, npings);
+  if (gossip) gossip_round(c, P->b, i);  // phase C's first step for this member
+  wave_stat_add(c, ST_FD_EVENTS, nev);
+  wave_stat_add(c, ST_PING_REQS, nreq);
+  wave_stat_add(c, ST_PINGS, npings);
 }
 
 // the rest of the round for the listed senders: one sender per wave at a time

@@ -23,6 +23,9 @@
 #ifndef CLS_SKIPZERO
 #define CLS_SKIPZERO 0  // timing experiment only: skip the stores of empty chunk results (NOT exact)
 #endif
+#ifndef CLS_PIPE
+#define CLS_PIPE 0      // 1: prefetch the wave's next unit while classifying the current one
+#endif
 #ifndef CLS_REV
 #define CLS_REV 1       // SYNC classify also classifies the reverse (SYNC_ACK) direction
 #endif
@@ -430,27 +433,31 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
   const Ctx c = pctx_sync(P, T);
   const Bufs b = P->b;
   const SubPhase p = sub_phase(b, d2);
-  const uint32_t ni = *p.nitems;
   const uint32_t chunks = b.chunks, n = c.n;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (CLS_BLOCK / 64) + (threadIdx.x >> 6));
   const uint32_t nw = gridDim.x * (CLS_BLOCK / 64);
-  const uint64_t total = (uint64_t)ni * chunks;
-  const uint32_t u0 = (uint32_t)(total * wid / nw), u1 = (uint32_t)(total * (wid + 1) / nw);
+  // units are dealt grid-stride (wave w: units w, w + nw, ...); the first header is loaded
+  // speculatively, in parallel with the item count, so a wave's first row loads issue two memory
+  // round trips after launch instead of three
+  const uint32_t i0 = wid / chunks;
+  ClsHdr hc, hn;
+  if (i0 < b.req_cap) cls_hdr(c, b, p, d2, i0, hc);
+  const uint32_t ni = *p.nitems;
+  const uint32_t total = ni * chunks;
   uint32_t cplx = 0, streamed = 0;
-  if (u0 < u1) {
-    ClsHdr hc, hn;
+  if (wid < total) {
     uint4 a[CLS_LOADS], o[CLS_LOADS], an[CLS_LOADS], on[CLS_LOADS];
-    cls_hdr(c, b, p, d2, u0 / chunks, hc);
-    if (hc.d1 == NONE || hc.snapdst) cls_rows(c, hc, u0 - hc.i * chunks, lane, a, o);
+    if (hc.d1 == NONE || hc.snapdst) cls_rows(c, hc, wid - hc.i * chunks, lane, a, o);
     hn = hc;
-    for (uint32_t u = u0; u < u1; ++u) {
+    for (uint32_t u = wid; u < total; u += nw) {
       const uint32_t ch = u - hc.i * chunks;
-      const bool more = u + 1 < u1;
-      if (more) {
-        const uint32_t i2 = (u + 1) / chunks;
+      const uint32_t un = u + nw;
+      const bool more = un < total;
+      if (CLS_PIPE && more) {
+        const uint32_t i2 = un / chunks;
         if (i2 != hn.i) cls_hdr(c, b, p, d2, i2, hn);
-        if (hn.d1 == NONE || hn.snapdst) cls_rows(c, hn, u + 1 - i2 * chunks, lane, an, on);
+        if (hn.d1 == NONE || hn.snapdst) cls_rows(c, hn, un - i2 * chunks, lane, an, on);
       }
       const uint32_t base = ch * SYNC_CHUNK;
       if (hc.snapdst) {
@@ -515,9 +522,15 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
         }
       }
       if (more) {
-        hc = hn;
+        if (CLS_PIPE) {
+          hc = hn;
 #pragma unroll
-        for (int j = 0; j < CLS_LOADS; ++j) { a[j] = an[j]; o[j] = on[j]; }
+          for (int j = 0; j < CLS_LOADS; ++j) { a[j] = an[j]; o[j] = on[j]; }
+        } else {
+          const uint32_t i2 = un / chunks;
+          if (i2 != hc.i) cls_hdr(c, b, p, d2, i2, hc);
+          if (hc.d1 == NONE || hc.snapdst) cls_rows(c, hc, un - i2 * chunks, lane, a, o);
+        }
       }
     }
   }
