@@ -124,7 +124,8 @@ typedef struct swim_config {
   int32_t timer_stagger;      /* 1 = each initial member's ping and gossip timers also get a random
                                  phase (members of a real cluster start at different instants; the
                                  default 0 aligns them) */
-  uint32_t timer_capacity;    /* suspicion timers that may fall due in one tick, per row shard
+  uint32_t timer_capacity;    /* suspicion timers that may fall due in one tick, per row shard, split
+                                 evenly over the shard's 256-viewer blocks (at least 1,024 each)
                                  (0 = default 2 x the shard's rows; churn schedules a timer for every
                                  killed member at every viewer within a few seconds) */
   uint32_t message_capacity;  /* GOSSIP_REQ messages one gossip round may materialise, per row shard

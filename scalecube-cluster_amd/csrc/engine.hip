@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <new>
 #include <vector>
 
@@ -119,6 +120,7 @@ struct Shard {
 
 struct swim_engine {
   swim_config cfg{};
+  bool debug_sync = false;  // SWIM_DEBUG_SYNC=1: synchronise after every tick kernel and name a faulting one
   int32_t device = 0;
   uint32_t n = 0, tick_ms = 0, P = 0, G = 0, S = 0, sz = 0;
   uint64_t T = 0;
@@ -479,6 +481,15 @@ static void run_ins_pipeline(swim_engine* e, Shard& sd, int sync_phase) {
   k_ins_apply<<<512, 256, 0, e->stream>>>(sd.d_par, e->T, sync_phase);
 }
 
+// SWIM_DEBUG_SYNC=1: synchronise after each tick kernel so a device fault names its kernel
+#define TICK_CHECK(name)                                                                            \
+  do {                                                                                              \
+    if (e->debug_sync && hipStreamSynchronize(s) != hipSuccess) {                                   \
+      std::fprintf(stderr, "libswimgpu: %s faulted at tick %llu\n", name, (unsigned long long)T);  \
+      return SWIM_EDEVICE;                                                                          \
+    }                                                                                               \
+  } while (0)
+
 // One tick: ~11 kernels per shard (16 on gossip ticks); a sharded engine adds three exchanges.
 static int32_t run_tick(swim_engine* e) {
   e->T += 1;
@@ -495,18 +506,21 @@ static int32_t run_tick(swim_engine* e) {
   if (!e->joins.empty()) {
     for (Shard& sd : e->sh)
       for (uint32_t m : e->joins) hipMemsetAsync(sd.c.up + m, 1, 1, s);
-    for (Shard& sd : e->sh) k_start_joins<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sd.d_par, T);
+    for (Shard& sd : e->sh) {
+      k_start_joins<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sd.d_par, T);
+      TICK_CHECK("k_start_joins");
+    }
     e->joins.clear();
   }
   for (Shard& sd : e->sh) {
     const uint32_t gm = grid_for(sd.c.nl, 256);
-    // ---- A: suspicion timeouts
-    k_timers<<<256, 256, 0, s>>>(sd.d_par, T);
-    // ---- B: list compaction of the timer phase's REMOVED + failure detector
+    // ---- A: suspicion timeouts, B: list compaction of their REMOVED + failure detector
     // ---- C: gossip round (period++ and the sender list in k_fd, then emit)
     k_fd<<<gm, 256, 0, s>>>(sd.d_par, T, gossip_tick ? 1 : 0);
+    TICK_CHECK("k_fd");
     if (gossip_tick) {
       k_gossip_emit<<<kEmitGrid, 64 * EMIT_WAVES, 0, s>>>(sd.d_par, T);
+      TICK_CHECK("k_gossip_emit");
     }
   }
   if (gossip_tick) {
@@ -516,14 +530,22 @@ static int32_t run_tick(swim_engine* e) {
       if (multi) sync_params(e, sd);
       if (sd.n_rx_msgs)
         k_recv_msgs<<<std::min<uint32_t>(grid_for(sd.n_rx_msgs, 256), 1024), 256, 0, s>>>(sd.d_par, T, sd.n_rx_msgs);
+      TICK_CHECK("k_recv_msgs");
       k_alloc<<<std::min<uint32_t>(1024, grid_for(sd.c.nl, 256)), 256, 0, s>>>(sd.d_par, T);
+      TICK_CHECK("k_alloc");
       k_scatter_msgs<<<512, 256, 0, s>>>(sd.d_par, T);
+      TICK_CHECK("k_scatter_msgs");
       k_gossip_deliver<<<std::min<uint32_t>(1024, grid_for(sd.c.nl, DLV_BLOCK)), DLV_BLOCK, 0, s>>>(sd.d_par, T);
+      TICK_CHECK("k_gossip_deliver");
       run_ins_pipeline(e, sd, 0);
+      TICK_CHECK("k_ins_apply");
     }
   }
   // ---- D: SYNC / SYNC_ACK
-  for (Shard& sd : e->sh) k_sync_collect<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sd.d_par, T);
+  for (Shard& sd : e->sh) {
+    k_sync_collect<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sd.d_par, T);
+    TICK_CHECK("k_sync_collect");
+  }
   for (int d2 = 0; d2 < 2; ++d2) {
     if (multi)
       if (int32_t rc = exchange_sync(e, 1 + d2)) return rc;
@@ -531,19 +553,24 @@ static int32_t run_tick(swim_engine* e) {
       if (multi) sync_params(e, sd);
       if (sd.n_rx_reqs)
         k_recv_sync<<<std::min<uint32_t>(grid_for(sd.n_rx_reqs, 256), 256), 256, 0, s>>>(sd.d_par, T, d2, sd.n_rx_reqs);
+      TICK_CHECK("k_recv_sync");
       // SYNC_ACK: an unsharded engine classifies its acks inside k_sync_apply (every ack is local,
       // and almost all reuse the SYNC launch's reverse classification); a sharded one streams the
       // acks that arrived with their rows from other shards
       const int classified = d2 == 0 || multi;
       k_sync_prep<<<1, 1024, 0, s>>>(sd.d_par, T, d2, !classified);
+      TICK_CHECK("k_sync_prep");
       if (classified) launch_classify(e, sd, d2);
+      TICK_CHECK("k_sync_classify");
       k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(sd.d_par, T, d2, classified);
+      TICK_CHECK("k_sync_apply");
     }
   }
   for (Shard& sd : e->sh) {
     // ---- end of tick (also zeroes the per-tick counters and applies other shards' stops)
     const uint32_t ge = grid_for(std::max<uint32_t>(std::max<uint32_t>(sd.c.nl, sd.n_rx_stops), 64), 256);
     k_end_tick<<<ge, 256, 0, s>>>(sd.d_par, T, sd.n_rx_stops);
+    TICK_CHECK("k_end_tick");
   }
   return SWIM_OK;
 }
@@ -657,7 +684,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   const uint64_t max_timer = (uint64_t)cf.suspicion_mult * (uint64_t)host_ceil_log2((int32_t)n) * e->P;
   c.wheel_mask = next_pow2((uint32_t)max_timer + 2) - 1;
   const uint64_t tcap = cf.timer_capacity ? cf.timer_capacity : 2ull * std::max(nl, 1u);
-  c.wheel_cap = SUBQ * (uint32_t)std::max<uint64_t>(1024, (tcap + SUBQ - 1) / SUBQ);
+  c.wheel_nq = std::max(1u, (nl + 255) / 256);  // one queue per k_fd workgroup
+  c.wheel_cap = c.wheel_nq * (uint32_t)std::max<uint64_t>(1024, (tcap + c.wheel_nq - 1) / c.wheel_nq);
   c.ev_cap = std::max<uint32_t>(1024, (cf.event_capacity ? cf.event_capacity : (1u << 22)) / SUBQ);
   // deferred pingMembers inserts of one phase: a join burst adds every joiner at every viewer
   c.ins_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 22, 256ull * nl));
@@ -687,7 +715,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&c.spill_ctl, NTIER) && sd.alloc(&c.seg_flag, nl) &&
             sd.alloc(&c.fd_sync, (size_t)nl * FD_SYNC_MAX) &&
             sd.alloc(&c.wheel, (size_t)(c.wheel_mask + 1) * c.wheel_cap) &&
-            sd.alloc(&c.wheel_cnt, (size_t)(c.wheel_mask + 1) * SUBQ) && sd.alloc(&c.ev, (size_t)c.ev_cap * SUBQ) &&
+            sd.alloc(&c.wheel_cnt, (size_t)(c.wheel_mask + 1) * c.wheel_nq) && sd.alloc(&c.ev, (size_t)c.ev_cap * SUBQ) &&
             sd.alloc(&c.ev_cnt, SUBQ) && sd.alloc(&c.default_loss, n) &&
             sd.alloc(&c.default_inbound, n) && sd.alloc(&c.group, n) && sd.alloc(&c.links, 1) &&
             sd.alloc(&c.is_seed, n) && sd.alloc(&c.seeds, n) && sd.alloc(&c.ins, c.ins_cap) &&
@@ -719,7 +747,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(c.coll, 0, sizeof(CollEnt) * (size_t)nl * c.hcap, s);
   hipMemsetAsync(c.spill_ctl, 0, sizeof(SpillCtl) * NTIER, s);
   hipMemsetAsync(c.seg_flag, 0, 4 * (size_t)nl, s);
-  hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1) * SUBQ, s);
+  hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1) * c.wheel_nq, s);
   hipMemsetAsync(c.ev_cnt, 0, 4 * SUBQ, s);
   hipMemsetAsync(c.up, 0, n, s);
   hipMemsetAsync(c.up, 1, n_initial, s);
@@ -773,6 +801,10 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
   swim_engine* e = new (std::nothrow) swim_engine();
   if (!e) return SWIM_ENOMEM;
   e->cfg = cf;
+  {
+    const char* d = std::getenv("SWIM_DEBUG_SYNC");
+    e->debug_sync = d && d[0] == '1';
+  }
   e->device = cf.device;
   e->n = capacity;
   e->tick_ms = tick;

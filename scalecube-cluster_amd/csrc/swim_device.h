@@ -131,7 +131,7 @@ struct InsOp {  // deferred pingMembers.add(nextInt(size), member) of an ADDED e
 // indexed by viewer (cells, lists, slab, collectors, mem, per-viewer counters) holds owned rows only
 // and is indexed by v - lo; the network emulator, seeds and `up` are replicated.
 struct Ctx {
-  uint32_t n, gcap, hcap, wheel_mask, wheel_cap;
+  uint32_t n, gcap, hcap, wheel_mask, wheel_cap, wheel_nq;
   uint32_t lo, nl, sz, rank, world;
   uint32_t P, to_ticks, relay_ticks, G, S, sync_to_ticks, tick_ms;
   int32_t ping_interval, suspicion_mult, repeat_mult, fanout, ping_req_members, seg_threshold, record_fd;
@@ -153,8 +153,8 @@ struct Ctx {
   SpillCtl* spill_ctl;           // [NTIER]
   uint32_t* seg_flag;            // per viewer: a collector exceeded gossipSegmentationThreshold
   uint32_t* fd_sync;
-  uint64_t* wheel;      // [W][SUBQ][wheel_cap / SUBQ]
-  uint32_t* wheel_cnt;  // [W][SUBQ]
+  uint64_t* wheel;      // [W][wheel_nq][wheel_cap / wheel_nq]: per deadline bucket, per 256-viewer block
+  uint32_t* wheel_cnt;  // [W][wheel_nq]
   swim_event* ev;
   uint32_t* ev_cnt;     // [SUBQ]
   uint32_t ev_cap;      // per sub-queue
@@ -603,8 +603,9 @@ __device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
   uint64_t ms = (uint64_t)c.suspicion_mult * (uint64_t)ceil_log2(mem(c, v).table_size) * (uint64_t)c.ping_interval;
   uint64_t deadline = c.T + ms / c.tick_ms;
   *ap = (a & 0xfu) | A_HAS_TIMER | ((uint32_t)(deadline & SWIM_DEADLINE_MASK) << 4);
-  const uint32_t b = (uint32_t)(deadline & c.wheel_mask), q = subq(v, s), qcap = c.wheel_cap / SUBQ;
-  const uint32_t i = atomicAdd(&c.wheel_cnt[b * SUBQ + q], 1u);
+  // queue of the viewer's 256-viewer block (fired by that block's k_fd workgroup)
+  const uint32_t b = (uint32_t)(deadline & c.wheel_mask), q = (v - c.lo) >> 8, qcap = c.wheel_cap / c.wheel_nq;
+  const uint32_t i = atomicAdd(&c.wheel_cnt[(size_t)b * c.wheel_nq + q], 1u);
   if (i >= qcap) { set_err(c, ERR_WHEEL); return; }
   c.wheel[(size_t)b * c.wheel_cap + (size_t)q * qcap + i] = ((uint64_t)v << 32) | s;
 }

@@ -1,6 +1,6 @@
 // swim_kernels.h — the HIP kernels of one lockstep tick.
 //
-// Phase A  k_timers                                   suspicion timeouts
+// Phase A  k_fd (per 256-viewer block)                suspicion timeouts
 // Phase B  k_fd                                       list compaction after REMOVED, then ping /
 //                                                     ping-req / ack resolution + FD events
 // Phase C  round start (+ segmentation) in k_fd, k_gossip_emit, k_alloc, k_scatter_msgs, k_gossip_deliver
@@ -227,25 +227,21 @@ __global__ void k_start_joins(KP) {
 
 // ------------------------------------------------------------------------------- phase A
 // onSuspicionTimeout (MembershipProtocolImpl.java:825-834) for every due (viewer, subject).
-// Entries of one viewer are independent (each touches only its own cell; counters are atomic),
-// so the bucket is processed entry-parallel; event order is canonicalised by minor = subject.
-__global__ void k_timers(KP) {
-  const Ctx c = pctx(P, T);
+// A timer is queued by deadline bucket and by the 256-viewer block of its viewer, so the k_fd
+// workgroup of that block fires it just before the block's FD steps (a per-viewer dependency: the
+// timer touches only its viewer's state).  Entries of one viewer are independent (each touches only
+// its own cell; counters are atomic), so the queue is processed entry-parallel; event order is
+// canonicalised by minor = subject.
+__device__ inline void timers_block(const Ctx& c, uint64_t T) {
   const uint32_t bucket = (uint32_t)(T & c.wheel_mask);
-  const uint32_t qcap = c.wheel_cap / SUBQ;
-  uint32_t qcnt[SUBQ], cnt = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < SUBQ; ++q) {
-    qcnt[q] = min(c.wheel_cnt[bucket * SUBQ + q], qcap);
-    cnt += qcnt[q];
-  }
-  const uint64_t* ent = c.wheel + (size_t)bucket * c.wheel_cap;
+  const uint32_t qcap = c.wheel_cap / c.wheel_nq;
+  uint32_t* qc = c.wheel_cnt + (size_t)bucket * c.wheel_nq + blockIdx.x;
+  const uint32_t cnt = min(*qc, qcap);
+  const uint64_t* ent = c.wheel + (size_t)bucket * c.wheel_cap + (size_t)blockIdx.x * qcap;
   const uint32_t tmask = (uint32_t)(c.T & SWIM_DEADLINE_MASK);
   unsigned long long fired = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
-    uint32_t q = 0, j = i;  // i-th entry of the concatenated sub-queues
-    while (j >= qcnt[q]) j -= qcnt[q++];
-    uint64_t e = ent[(size_t)q * qcap + j];
+  for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+    uint64_t e = ent[i];
     uint32_t v = (uint32_t)(e >> 32), s = (uint32_t)e;
     if (!c.up[v]) continue;
     uint32_t* ap = aux_row(c, v) + s;
@@ -262,6 +258,8 @@ __global__ void k_timers(KP) {
     if (r_in_table(r)) update_membership(c, v, s, SWIM_DEAD, r_inc(r), R_TIMEOUT, SWIM_PHASE_TIMERS);
   }
   wave_stat_add(c, ST_TIMERS_FIRED, fired);
+  __syncthreads();  // the block's DEAD updates (lists to compact) are visible to every thread
+  if (threadIdx.x == 0 && cnt) *qc = 0;
 }
 
 // REMOVED -> pingMembers.remove / remoteMembers.remove (FailureDetectorImpl.java:323-333,
@@ -616,16 +614,16 @@ __device__ __forceinline__ void gossip_round(const Ctx& c, const Bufs& b, uint32
   if (busy) b.senders[base + lanes_below(mk)] = i;
 }
 
-// Phases B and C's first step.  256-thread workgroups, one viewer per thread.  First the workgroup compacts the ping / remote
-// lists of its viewers that lost a member in this tick's timer phase (a per-viewer dependency, so
+// Phases A, B and C's first step.  256-thread workgroups, one viewer per thread.  The workgroup
+// fires its viewers' due suspicion timers, compacts the ping / remote lists of its viewers that
+// lost a member in the timer phase (a per-viewer dependency, so
 // no separate launch), then every thread runs its viewer's FD step and, on gossip ticks, the
 // first step of its gossip round (k_gossip_emit runs the rest after every FD step is done).
 __global__ void __launch_bounds__(256) k_fd(KP, int gossip) {
   const Ctx c = pctx(P, T);
-  const uint32_t bucket = (uint32_t)(T & c.wheel_mask);
   __shared__ uint32_t s_list[256];
   __shared__ uint32_t s_cnt;
-  if (blockIdx.x == 0 && threadIdx.x < SUBQ) c.wheel_cnt[bucket * SUBQ + threadIdx.x] = 0;  // k_timers drained it
+  timers_block(c, T);  // phase A for this block's viewers
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -332,7 +332,10 @@ struct ClsHdr {
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // the header is wave-uniform: keep it in scalar registers (the row loads need the VGPRs)
-__device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SubPhase& p, int d2, uint32_t i, ClsHdr& h) {
+// (speculative = true: message i may lie beyond the sub-phase's items, so nothing is read through
+// the header's ids; the SYNC_ACK reuse check is left out)
+__device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SubPhase& p, int d2, uint32_t i, ClsHdr& h,
+                                        bool speculative = false) {
   SyncReq q = p.out[i];
   q.from = uni(q.from); q.to = uni(q.to); q.content = uni(q.content); q.snap = uni(q.snap); q.pad = uni(q.pad);
   const bool remote = q.content != NONE;
@@ -344,7 +347,7 @@ __device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SubPh
   h.s = q.from;
   h.rev = (CLS_REV && !d2 && !remote) ? 1u : 0u;
   h.d1 = NONE;
-  if (d2 && q.pad != 0 && !remote) {
+  if (d2 && !speculative && q.pad != 0 && !remote) {
     const uint32_t t = (uint32_t)c.T;
     if (uni(b.row_mod[q.from - c.lo]) != t && uni(b.row_mod[q.to - c.lo]) != t) h.d1 = q.pad - 1;
   }
@@ -442,11 +445,12 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
   // round trips after launch instead of three
   const uint32_t i0 = wid / chunks;
   ClsHdr hc, hn;
-  if (i0 < b.req_cap) cls_hdr(c, b, p, d2, i0, hc);
+  if (i0 < b.req_cap) cls_hdr(c, b, p, d2, i0, hc, true);
   const uint32_t ni = *p.nitems;
   const uint32_t total = ni * chunks;
   uint32_t cplx = 0, streamed = 0;
   if (wid < total) {
+    if (d2) cls_hdr(c, b, p, d2, i0, hc);  // now a valid item: add the SYNC_ACK reuse check
     uint4 a[CLS_LOADS], o[CLS_LOADS], an[CLS_LOADS], on[CLS_LOADS];
     if (hc.d1 == NONE || hc.snapdst) cls_rows(c, hc, wid - hc.i * chunks, lane, a, o);
     hn = hc;
