@@ -216,15 +216,18 @@ def main():
         dt = time.perf_counter() - t0
     except abi.SwimError as ex:
         raise SystemExit(f"{ex}; engine error bits {e.stats()['capacity_errors']:#x}")
-    prof = e.profile_merge()
+    prof, fprof = e.profile_merge(), e.profile_fanout()
     stats = e.stats()
     e.drain_events()
     if se is not None:
         dt = se.max_time(dt)
         stats = se.stats()
-        st = torch.tensor([float(prof["alg_bytes"]), prof["total_ms"], float(prof["launches"])], dtype=torch.float64)
-        dist.all_reduce(st, op=dist.ReduceOp.SUM)
-        prof = {"alg_bytes": st[0].item(), "total_ms": st[1].item(), "launches": int(st[2].item())}
+
+        def reduce(p):
+            st = torch.tensor([float(p["alg_bytes"]), p["total_ms"], float(p["launches"])], dtype=torch.float64)
+            dist.all_reduce(st, op=dist.ReduceOp.SUM)
+            return {"alg_bytes": st[0].item(), "total_ms": st[1].item(), "launches": int(st[2].item())}
+        prof, fprof = reduce(prof), reduce(fprof)
     if stats["capacity_errors"]:
         raise SystemExit(f"capacity error during the benchmark: {stats['capacity_errors']:#x}")
 
@@ -262,6 +265,18 @@ def main():
         "stats": {k: stats[k] for k in ("syncs", "sync_records", "gossip_messages", "gossips_created", "pings",
                                          "timers_fired", "events")},
     }
+    if fprof["alg_bytes"] > 0:
+        # the gossip fanout kernel (north_star: merge AND fanout against the HBM roofline); only
+        # workloads with gossip traffic (failures, churn) give it work
+        f_ms = fprof["total_ms"] / max(1, fprof["launches"])
+        f_ach = fprof["alg_bytes"] / max(1e-12, fprof["total_ms"] / 1e3) / 1e9
+        f_traffic, f_src = pmc_traffic("k_gossip_emit", f"{args.workload}{n // 1024}k")
+        line["roofline_fanout"] = {
+            "bound": "hbm", "kernel": "k_gossip_emit", "achieved": f_ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": f_ach / HBM_PEAK_GBPS, "traffic": f_traffic, "traffic_source": f_src,
+            "launches": fprof["launches"], "avg_launch_ms": f_ms,
+            "alg_bytes_per_launch": fprof["alg_bytes"] / max(1, fprof["launches"]),
+            "alg_bytes_rule": "24 B per materialised GOSSIP_REQ + 32 B per (gossip, sender round) state read"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         e.close()
         line["cpu_baseline"] = cpu_baseline(n, args.cpu_periods)

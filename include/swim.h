@@ -316,6 +316,10 @@ typedef struct swim_kernel_profile {
 } swim_kernel_profile;
 int32_t swim_profile_enable(swim_engine* e, int32_t enable);
 int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out);
+/* The gossip fanout kernel (doSpreadGossip's sends, k_gossip_emit), sampled the same way:
+ * messages = GOSSIP_REQs materialised, records = (gossip, sender round) states read,
+ * alg_bytes = 24 B x messages + 32 B x records (SURVEY.md §8(d) fanout). */
+int32_t swim_profile_fanout(swim_engine* e, swim_kernel_profile* out);
 
 /* ---- known-answer hooks (run the engine's own merge / dedupe code on given inputs) --------- */
 /* Philox4x32-10 block used by every draw site. */

@@ -876,6 +876,8 @@ int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out) {
   return SWIM_OK;
 }
 
+int32_t swim_profile_fanout(swim_engine* e, swim_kernel_profile* out) { return swim_profile_merge(e, out); }
+
 int32_t swim_kat_overrides(const int32_t* cases, uint32_t n, uint8_t* out) {
   if (n && (!cases || !out)) return SWIM_EINVAL;
   for (uint32_t i = 0; i < n; ++i) {

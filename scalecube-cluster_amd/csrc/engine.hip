@@ -67,6 +67,43 @@ uint32_t grid_for(uint32_t n, uint32_t block) { return std::max(1u, (n + block -
 }  // namespace
 
 // One shard: the device state of rows [lo, lo + nl) plus the replicated arrays.
+// One kernel's sampled launch timing: HIP events bound to the dispatch itself (hipExtLaunchKernelGGL:
+// the kernel's own start / completion timestamps, no extra stream packets) on one launch in
+// kProfEvery, plus two per-launch work counters the kernel accumulates into `slots`.
+struct KProf {
+  std::vector<hipEvent_t> ev;
+  uint32_t used = 0;
+  uint64_t seen = 0;  // launches since profiling was enabled
+  unsigned long long* slots = nullptr;  // per sampled launch: {work counter a, work counter b}
+  double ms = 0;
+  unsigned long long a = 0, b = 0;
+  uint64_t launches = 0;
+
+  bool take(bool on) { return on && (seen++ % kProfEvery) == 0 && 2 * (used + 1) <= ev.size(); }
+  void flush() {
+    if (!used) return;
+    std::vector<unsigned long long> h(2 * (size_t)used);
+    hipMemcpy(h.data(), slots, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost);
+    hipMemset(slots, 0, sizeof(unsigned long long) * h.size());
+    for (uint32_t i = 0; i < used; ++i) {
+      float t = 0.f;
+      if (hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]) == hipSuccess) ms += t;
+      a += h[2 * i];
+      b += h[2 * i + 1];
+    }
+    launches += used;
+    used = 0;
+  }
+  void reset() {
+    hipMemset(slots, 0, sizeof(unsigned long long) * ev.size());
+    used = 0;
+    seen = 0;
+    ms = 0;
+    a = b = 0;
+    launches = 0;
+  }
+};
+
 struct Shard {
   Ctx c{};
   Bufs b{};
@@ -86,14 +123,9 @@ struct Shard {
   Params* d_par = nullptr;
   Params up{};
   bool up_valid = false;
-  // swim_profile_*: HIP events around every k_sync_classify launch on the engine's stream
-  std::vector<hipEvent_t> prof_ev;
-  uint32_t prof_used = 0;
-  uint64_t prof_seen = 0;  // classify launches since profiling was enabled
-  unsigned long long* prof_slots = nullptr;  // per sampled launch: {messages, complex records}
-  double prof_ms = 0;
-  unsigned long long prof_msgs = 0, prof_recs = 0;
-  uint64_t prof_launches = 0;
+  // swim_profile_*: HIP events around sampled k_sync_classify (merge) and k_gossip_emit (fanout)
+  // launches on the engine's stream
+  KProf prof_cls, prof_emit;
 
   template <typename T>
   bool alloc(T** p, size_t count) {
@@ -148,7 +180,8 @@ struct swim_engine {
   ~swim_engine() {
     if (stream) hipStreamSynchronize(stream);
     for (Shard& s : sh) {
-      for (hipEvent_t ev : s.prof_ev) hipEventDestroy(ev);
+      for (hipEvent_t ev : s.prof_cls.ev) hipEventDestroy(ev);
+      for (hipEvent_t ev : s.prof_emit.ev) hipEventDestroy(ev);
       for (void* p : s.allocs) hipFree(p);
     }
     if (d_cnt) hipFree(d_cnt);
@@ -193,38 +226,32 @@ static int32_t read_stats(swim_engine* e, unsigned long long* st) {
   return SWIM_OK;
 }
 
-static void prof_flush(Shard& s) {
-  if (!s.prof_used) return;
-  std::vector<unsigned long long> slots(2 * (size_t)s.prof_used);
-  hipMemcpy(slots.data(), s.prof_slots, sizeof(unsigned long long) * slots.size(), hipMemcpyDeviceToHost);
-  hipMemset(s.prof_slots, 0, sizeof(unsigned long long) * slots.size());
-  for (uint32_t i = 0; i < s.prof_used; ++i) {
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, s.prof_ev[2 * i], s.prof_ev[2 * i + 1]) == hipSuccess) s.prof_ms += ms;
-    s.prof_msgs += slots[2 * i];
-    s.prof_recs += slots[2 * i + 1];
-  }
-  s.prof_launches += s.prof_used;
-  s.prof_used = 0;
-}
-
-// The SYNC classify launch (the HBM stream) is timed by HIP events bound to the dispatch itself
-// (hipExtLaunchKernelGGL: the kernel's own start / completion timestamps, no extra stream packets),
-// one launch in kProfEvery.  The SYNC_ACK launch is a separate kernel (k_ack_classify).
+// The SYNC classify launch (the HBM stream) and the gossip fanout launch are sampled by KProf.
+// The SYNC_ACK classify launch is a separate kernel (k_ack_classify).
 static void launch_classify(swim_engine* e, Shard& s, int d2) {
   if (d2) {
     k_ack_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(s.d_par, e->T);
     return;
   }
-  const bool p = e->prof && (s.prof_seen++ % kProfEvery) == 0 && 2 * (s.prof_used + 1) <= s.prof_ev.size();
-  if (!p) {
+  KProf& k = s.prof_cls;
+  if (!k.take(e->prof)) {
     k_sync_classify<<<kClassifyGrid, CLS_BLOCK, 0, e->stream>>>(s.d_par, e->T, nullptr);
     return;
   }
-  hipExtLaunchKernelGGL(k_sync_classify, dim3(kClassifyGrid), dim3(CLS_BLOCK), 0, e->stream,
-                        s.prof_ev[2 * s.prof_used], s.prof_ev[2 * s.prof_used + 1], 0, s.d_par, e->T,
-                        s.prof_slots + 2 * s.prof_used);
-  s.prof_used++;
+  hipExtLaunchKernelGGL(k_sync_classify, dim3(kClassifyGrid), dim3(CLS_BLOCK), 0, e->stream, k.ev[2 * k.used],
+                        k.ev[2 * k.used + 1], 0, s.d_par, e->T, k.slots + 2 * k.used);
+  k.used++;
+}
+
+static void launch_emit(swim_engine* e, Shard& s) {
+  KProf& k = s.prof_emit;
+  if (!k.take(e->prof)) {
+    k_gossip_emit<<<kEmitGrid, 64 * EMIT_WAVES, 0, e->stream>>>(s.d_par, e->T, nullptr);
+    return;
+  }
+  hipExtLaunchKernelGGL(k_gossip_emit, dim3(kEmitGrid), dim3(64 * EMIT_WAVES), 0, e->stream, k.ev[2 * k.used],
+                        k.ev[2 * k.used + 1], 0, s.d_par, e->T, k.slots + 2 * k.used);
+  k.used++;
 }
 
 static int32_t sync_and_collect(swim_engine* e) {
@@ -251,7 +278,10 @@ static int32_t sync_and_collect(swim_engine* e) {
     }
     if (any && hipMemset(s.c.ev_cnt, 0, 4 * SUBQ) != hipSuccess) return SWIM_EDEVICE;
     err_all |= err;
-    if (e->prof) prof_flush(s);
+    if (e->prof) {
+      s.prof_cls.flush();
+      s.prof_emit.flush();
+    }
   }
   // adapt the drain interval so a sub-queue stays well below its capacity between drains (an event
   // storm — a join burst adds every joiner at every viewer — drains every few ticks, a quiet
@@ -519,7 +549,7 @@ static int32_t run_tick(swim_engine* e) {
     k_fd<<<gm, 256, 0, s>>>(sd.d_par, T, gossip_tick ? 1 : 0);
     TICK_CHECK("k_fd");
     if (gossip_tick) {
-      k_gossip_emit<<<kEmitGrid, 64 * EMIT_WAVES, 0, s>>>(sd.d_par, T);
+      launch_emit(e, sd);
       TICK_CHECK("k_gossip_emit");
     }
   }
@@ -1269,18 +1299,15 @@ int32_t swim_profile_enable(swim_engine* e, int32_t enable) {
   if (!e) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
   for (Shard& sd : e->sh) {
-    if (sd.prof_ev.empty()) {
-      sd.prof_ev.resize(4 * kDrainEvery + 4);
-      for (auto& ev : sd.prof_ev)
-        if (hipEventCreate(&ev) != hipSuccess) return SWIM_EDEVICE;
-      if (!sd.alloc(&sd.prof_slots, sd.prof_ev.size())) return SWIM_ENOMEM;
+    for (KProf* k : {&sd.prof_cls, &sd.prof_emit}) {
+      if (k->ev.empty()) {
+        k->ev.resize(4 * kDrainEvery + 4);
+        for (auto& ev : k->ev)
+          if (hipEventCreate(&ev) != hipSuccess) return SWIM_EDEVICE;
+        if (!sd.alloc(&k->slots, k->ev.size())) return SWIM_ENOMEM;
+      }
+      k->reset();
     }
-    hipMemset(sd.prof_slots, 0, sizeof(unsigned long long) * sd.prof_ev.size());
-    sd.prof_used = 0;
-    sd.prof_seen = 0;
-    sd.prof_ms = 0;
-    sd.prof_launches = 0;
-    sd.prof_msgs = sd.prof_recs = 0;
   }
   e->prof = enable != 0;
   return SWIM_OK;
@@ -1291,13 +1318,29 @@ int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
   std::memset(out, 0, sizeof(*out));
   for (Shard& sd : e->sh) {
-    prof_flush(sd);
-    out->launches += sd.prof_launches;
-    out->total_ms += sd.prof_ms;
-    out->messages += sd.prof_msgs;
-    out->records += sd.prof_recs;
+    sd.prof_cls.flush();
+    out->launches += sd.prof_cls.launches;
+    out->total_ms += sd.prof_cls.ms;
+    out->messages += sd.prof_cls.a;
+    out->records += sd.prof_cls.b;
   }
   out->alg_bytes = out->messages * (uint64_t)e->n * 8ull + out->records * 4ull;
+  return SWIM_OK;
+}
+
+int32_t swim_profile_fanout(swim_engine* e, swim_kernel_profile* out) {
+  if (!e || !out) return SWIM_EINVAL;
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  std::memset(out, 0, sizeof(*out));
+  for (Shard& sd : e->sh) {
+    sd.prof_emit.flush();
+    out->launches += sd.prof_emit.launches;
+    out->total_ms += sd.prof_emit.ms;
+    out->messages += sd.prof_emit.a;
+    out->records += sd.prof_emit.b;
+  }
+  // SURVEY.md §8(d) fanout: 24 B per emitted GOSSIP_REQ + 32 B per (gossip, sender round) read
+  out->alg_bytes = out->messages * 24ull + out->records * 32ull;
   return SWIM_OK;
 }
 

@@ -449,7 +449,7 @@ __device__ inline void emit_mark_holes(const Bufs& b, uint32_t cb, uint32_t cl, 
 }
 __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs& b, uint32_t v, uint64_t period,
                                                         uint32_t glen, uint32_t lane, uint32_t* s_t, uint32_t& cb,
-                                                        uint32_t& cl) {
+                                                        uint32_t& cl, unsigned long long& nmat) {
   MemberDev& m = mem(c, v);
   const uint32_t rlen = m.remote_len;
   const uint32_t F = (uint32_t)c.fanout;
@@ -491,7 +491,9 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
             !(owned(c, t) && coll_contains(c, coll_find(c, t, g.gossiper), g.seq));
     }
     nmsg += send ? 1u : 0u;
-    if (!__ballot(mat)) continue;
+    const uint64_t mm = __ballot(mat);
+    if (!mm) continue;
+    nmat += (uint32_t)__popcll(mm);  // wave-uniform
     // one enqueue per target present in this pass: lane jj issues target jj's receiver atomic; the
     // message slots of this shard's targets come out of the wave's chunk
     uint32_t base = 0, slot = 0, cnt_mine = 0, pre = 0, loc_off = 0, loc_tot = 0;
@@ -648,20 +650,27 @@ __global__ void __launch_bounds__(256) k_fd(KP, int gossip) {
 }
 
 // the rest of the round for the listed senders: one sender per wave at a time
-__global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP) {
+// prof (sampled launches only): {GOSSIP_REQs materialised, (gossip, sender round) states read}
+__global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned long long* prof) {
   __shared__ uint32_t s_t[EMIT_WAVES][17];
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t ns = b.k->sender_cnt;
-  unsigned long long nmsg = 0;
+  unsigned long long nmsg = 0, nmat = 0, nstate = 0;
   uint32_t cb = 0, cl = 0;
   for (uint32_t k = __builtin_amdgcn_readfirstlane(blockIdx.x * EMIT_WAVES + wv); k < ns; k += gridDim.x * EMIT_WAVES) {
     const uint32_t i = b.senders[k];
     const MemberDev& m = c.mem[i];
-    nmsg += gossip_emit_sender(c, b, c.lo + i, m.g_period - 1, m.gossip_len, lane, s_t[wv], cb, cl);
+    const uint32_t glen = m.gossip_len;
+    nstate += glen;
+    nmsg += gossip_emit_sender(c, b, c.lo + i, m.g_period - 1, glen, lane, s_t[wv], cb, cl, nmat);
   }
   emit_mark_holes(b, cb, cl, lane);
+  if (prof && lane == 0 && nstate) {
+    atomicAdd(prof, nmat);
+    atomicAdd(prof + 1, nstate);
+  }
   wave_stat_add(c, ST_GOSSIP_MESSAGES, nmsg);
 }
 

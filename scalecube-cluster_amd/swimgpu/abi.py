@@ -188,6 +188,7 @@ PROTOTYPES = {
     "swim_read_collector": (C.c_int32, [_engp, C.c_uint32, C.c_uint32, POINTER(swim_interval), C.c_uint32, _u32p]),
     "swim_profile_enable": (C.c_int32, [_engp, C.c_int32]),
     "swim_profile_merge": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
+    "swim_profile_fanout": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_philox": (C.c_int32, [_u32p, _u32p, _u32p]),
     "swim_kat_overrides": (C.c_int32, [POINTER(C.c_int32), C.c_uint32, POINTER(C.c_uint8)]),
     "swim_kat_collector": (C.c_int32, [POINTER(C.c_uint8), POINTER(C.c_int64), C.c_uint32, POINTER(C.c_int64)]),
@@ -375,6 +376,12 @@ class Engine:
     def profile_merge(self) -> dict:
         p = swim_kernel_profile()
         _check("swim_profile_merge", self.lib.swim_profile_merge(self._h, byref(p)))
+        return {name: getattr(p, name) for name, _ in swim_kernel_profile._fields_}
+
+    def profile_fanout(self) -> dict:
+        """Sampled timing of the gossip fanout kernel (k_gossip_emit), see swim.h."""
+        p = swim_kernel_profile()
+        _check("swim_profile_fanout", self.lib.swim_profile_fanout(self._h, byref(p)))
         return {name: getattr(p, name) for name, _ in swim_kernel_profile._fields_}
 
     def read_collector(self, m: int, gossiper: int) -> list[tuple[int, int]]:
