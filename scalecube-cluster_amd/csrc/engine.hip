@@ -715,6 +715,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.wheel_mask = next_pow2((uint32_t)max_timer + 2) - 1;
   const uint64_t tcap = cf.timer_capacity ? cf.timer_capacity : 2ull * std::max(nl, 1u);
   c.wheel_nq = std::max(1u, (nl + 255) / 256);  // one queue per k_fd workgroup
+  c.gwords = std::max(1u, (nl + 31) / 32);
   c.wheel_cap = c.wheel_nq * (uint32_t)std::max<uint64_t>(1024, (tcap + c.wheel_nq - 1) / c.wheel_nq);
   c.ev_cap = std::max<uint32_t>(1024, (cf.event_capacity ? cf.event_capacity : (1u << 22)) / SUBQ);
   // deferred pingMembers inserts of one phase: a join burst adds every joiner at every viewer
@@ -751,6 +752,9 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&c.is_seed, n) && sd.alloc(&c.seeds, n) && sd.alloc(&c.ins, c.ins_cap) &&
             sd.alloc(&c.ins_list, nl) && sd.alloc(&c.compact_flag, nl) &&
             sd.alloc(&c.fd_next, nl) && sd.alloc(&c.sync_next, nl) && sd.alloc(&c.mflag, nl) &&
+            sd.alloc(&c.gslot, GSLOTS) && sd.alloc(&c.gpend, GSLOTS) &&
+            sd.alloc(&c.gbits, (size_t)GSLOTS * c.gwords) && sd.alloc(&c.clr_tick, std::max(nl, 1u)) &&
+            sd.alloc(&c.gclaim, 2 * GSLOTS) && sd.alloc(&c.gclaim_cnt, 2) &&
             sd.alloc(&c.stats, (size_t)ST_COUNT * ST_REPL) && sd.alloc(&c.err, 1) && sd.alloc(&sd.k, 1) &&
             sd.alloc(&sd.x, 1) && sd.alloc(&b.msgs, b.msg_cap) && sd.alloc(&b.msgs_out, b.msg_cap) &&
             sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.msg_start, nl) &&
@@ -786,6 +790,11 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(c.group, 0, 2 * (size_t)n, s);
   hipMemsetAsync(c.is_seed, 0, n, s);
   hipMemsetAsync(c.compact_flag, 0, 4 * (size_t)nl, s);
+  hipMemsetAsync(c.gslot, 0, sizeof(GSlot) * GSLOTS, s);
+  hipMemsetAsync(c.gpend, 0, sizeof(uint64_t) * GSLOTS, s);
+  hipMemsetAsync(c.gbits, 0, sizeof(uint32_t) * GSLOTS * (size_t)c.gwords, s);
+  hipMemsetAsync(c.clr_tick, 0, sizeof(uint32_t) * std::max(nl, 1u), s);
+  hipMemsetAsync(c.gclaim_cnt, 0, sizeof(uint32_t) * 2, s);
   hipMemsetAsync(c.stats, 0, 8 * (size_t)ST_COUNT * ST_REPL, s);
   hipMemsetAsync(c.err, 0, 4, s);
   hipMemsetAsync(sd.k, 0, sizeof(Counters), s);

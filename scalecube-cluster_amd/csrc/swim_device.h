@@ -127,6 +127,23 @@ struct InsOp {  // deferred pingMembers.add(nextInt(size), member) of an ADDED e
   uint32_t s, phase, minor, next;  // next: the viewer's following op in event order (chain)
 };
 
+// Receipt bitmap slot: gossip (gossiper, seq) hashes to one of GSLOTS slots; the slot's bits are
+// valid for the gossip `key` from tick `tick` on (a slot is (re)claimed only in k_end_tick, when no
+// other kernel runs, and its bits are zeroed then).
+constexpr uint32_t GSLOTS = 8192;
+struct GSlot {
+  uint64_t key;   // (gossiper + 1) << 32 | seq, 0 = unowned
+  uint32_t tick;  // bits set from this tick on are trustworthy
+  uint32_t pad;
+};
+__device__ __forceinline__ uint64_t gkey(uint32_t gossiper, uint32_t seq) {
+  return ((uint64_t)(gossiper + 1) << 32) | seq;
+}
+__device__ __forceinline__ uint32_t gslot_of(uint64_t key) {
+  uint64_t x = key * 0x9E3779B97F4A7C15ull;
+  return (uint32_t)(x >> 51) & (GSLOTS - 1);  // 13 bits
+}
+
 // Row sharding: shard r owns viewers [lo, lo + nl) with lo = r * sz.  Every array
 // indexed by viewer (cells, lists, slab, collectors, mem, per-viewer counters) holds owned rows only
 // and is indexed by v - lo; the network emulator, seeds and `up` are replicated.
@@ -181,6 +198,15 @@ struct Ctx {
   uint32_t* fd_next;    // next tick with FD work (ping due, ack or relay timeout); stale while down
   uint32_t* sync_next;  // next periodic-SYNC tick (NONE: periodic SYNC off)
   uint32_t* mflag;      // MF_* work for k_sync_collect / k_end_tick
+  // receipt bitmaps: a subset of "receiver t's collector holds gossip (gossiper, seq)"
+  // that k_gossip_emit tests before probing the collector table
+  GSlot* gslot;          // [GSLOTS] the gossip owning each bitmap and the tick its bits became valid
+  uint64_t* gpend;       // [GSLOTS] gossip waiting to own the slot at the end of the tick (0 = none)
+  uint32_t* gbits;       // [GSLOTS][gwords] bit t - lo: receiver t accepted the owning gossip
+  uint32_t gwords;
+  uint32_t* clr_tick;    // per viewer: last tick one of its collectors was cleared
+  uint32_t* gclaim;      // [2][GSLOTS] slots to (re)claim at the end of tick T, queue T & 1
+  uint32_t* gclaim_cnt;  // [2]
   unsigned long long* stats;
   uint32_t* err;
 };
@@ -502,6 +528,32 @@ __device__ inline void coll_clear(const Ctx& c, CollEnt* e) {
   e->meta = COLL_CLEARED;
 }
 
+// receipt bitmaps: receiver r (owned) accepted gossip (gossiper, seq) into its collector.  Sets the
+// bit when the slot belongs to the gossip, else asks k_end_tick to hand the slot to it.
+__device__ inline void receipt_mark(const Ctx& c, uint32_t r, uint32_t gossiper, uint32_t seq) {
+  const uint64_t key = gkey(gossiper, seq);
+  const uint32_t sl = gslot_of(key);
+  if (c.gslot[sl].key == key) {
+    const uint32_t i = r - c.lo;
+    atomicOr(&c.gbits[(size_t)sl * c.gwords + (i >> 5)], 1u << (i & 31));
+  } else if (atomicCAS(reinterpret_cast<unsigned long long*>(&c.gpend[sl]), 0ull, (unsigned long long)key) == 0ull) {
+    const uint32_t par = (uint32_t)(c.T & 1);
+    c.gclaim[par * GSLOTS + atomicAdd(&c.gclaim_cnt[par], 1u)] = sl;  // at most one entry per slot
+  }
+}
+// exact: true iff t's collector holds (gossiper, seq); the bitmap answers without the collector
+// probe when its bit is set and trustworthy (set after the slot's claim, and no collector of t was
+// cleared since the claim)
+__device__ inline bool known_received(const Ctx& c, uint32_t t, uint32_t gossiper, uint32_t seq) {
+  const uint64_t key = gkey(gossiper, seq);
+  const uint32_t sl = gslot_of(key);
+  const GSlot g = c.gslot[sl];
+  const uint32_t i = t - c.lo;
+  if (g.key == key && c.clr_tick[i] < g.tick && ((c.gbits[(size_t)sl * c.gwords + (i >> 5)] >> (i & 31)) & 1u))
+    return true;
+  return coll_contains(c, coll_find(c, t, gossiper), seq);
+}
+
 // ------------------------------------------------------------------------------- events
 // Appends from thousands of threads in one kernel (a timer storm removes a member at every viewer
 // in one tick) go to SUBQ sub-queues picked by the wave, so no single counter serialises them;
@@ -556,7 +608,10 @@ __device__ inline void on_added(const Ctx& c, uint32_t v, uint32_t s, uint32_t p
 // Safe under entry-parallel timer processing: only the (v, s) collector entry is written.
 __device__ inline void on_removed(const Ctx& c, uint32_t v, uint32_t s) {
   CollEnt* e = coll_find(c, v, s);
-  if (e) coll_clear(c, e);
+  if (e) {
+    coll_clear(c, e);
+    c.clr_tick[v - c.lo] = (uint32_t)c.T;  // v's receipt bits predating this tick are void
+  }
   c.compact_flag[v - c.lo] = 1u;
 }
 
@@ -589,7 +644,7 @@ __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject,
   m.gossip_len++;
   m.g_counter++;
   CollEnt* e = coll_ensure(c, v, v);
-  coll_add(c, e, g.seq, &c.seg_flag[v - c.lo]);
+  if (coll_add(c, e, g.seq, &c.seg_flag[v - c.lo])) receipt_mark(c, v, v, g.seq);
   stat_add(c, ST_GOSSIPS_CREATED, 1);
 }
 

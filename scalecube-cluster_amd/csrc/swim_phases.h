@@ -488,7 +488,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       // delivered copies; a receiver on this shard that already holds the sequence id drops it
       // (its collector only grows until delivery), another shard filters on arrival
       mat = send && c.up[t] && in_pass(c, t, v) && !lost_k(c, out_loss(c, v, t), v, SWIM_STREAM_GOSSIP_OUT, j, p) &&
-            !(owned(c, t) && coll_contains(c, coll_find(c, t, g.gossiper), g.seq));
+            !(owned(c, t) && known_received(c, t, g.gossiper, g.seq));
     }
     nmsg += send ? 1u : 0u;
     const uint64_t mm = __ballot(mat);
@@ -603,7 +603,10 @@ __device__ __forceinline__ void gossip_round(const Ctx& c, const Bufs& b, uint32
         c.seg_flag[i] = 0;
         CollEnt* base = c.coll + (size_t)i * c.hcap;
         for (uint32_t j = 0; j < c.hcap; ++j)
-          if (base[j].key && (int32_t)coll_size(c, base + j) > c.seg_threshold) coll_clear(c, base + j);
+          if (base[j].key && (int32_t)coll_size(c, base + j) > c.seg_threshold) {
+            coll_clear(c, base + j);
+            c.clr_tick[i] = (uint32_t)c.T;
+          }
       }
       busy = m.gossip_len != 0;  // else no target selection, no shuffle draw
     }
@@ -754,6 +757,7 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, Gos
   if (!col) return false;
   const bool was_cleared = (col->meta & COLL_CLEARED) != 0;
   if (!coll_add(c, col, g.seq, &c.seg_flag[r - c.lo])) return false;
+  receipt_mark(c, r, g.gossiper, g.seq);
   int32_t found = -1;
   if (was_cleared) {  // a GossipState can outlive its collector entry only after a clear
     for (uint32_t p = 0; p < m.gossip_len; ++p)
@@ -1067,6 +1071,23 @@ __global__ void k_end_tick(KP, uint32_t n_rx_stops) {
         c.spill_ctl[t].freed = 0;
       }
     }
+  }
+  // receipt-bitmap slots requested this tick change owner (no other kernel runs now): zeroed bits,
+  // valid from the next tick; the other parity's queue (next tick's) is emptied
+  {
+    const uint32_t par = (uint32_t)(T & 1);
+    const uint32_t nclaim = min(c.gclaim_cnt[par], GSLOTS);
+    for (uint32_t q = blockIdx.x; q < nclaim; q += gridDim.x) {
+      const uint32_t sl = c.gclaim[par * GSLOTS + q];
+      uint32_t* bits = c.gbits + (size_t)sl * c.gwords;
+      for (uint32_t w = threadIdx.x; w < c.gwords; w += blockDim.x) bits[w] = 0;
+      if (threadIdx.x == 0) {
+        c.gslot[sl].key = c.gpend[sl];
+        c.gslot[sl].tick = (uint32_t)T + 1;
+        c.gpend[sl] = 0;
+      }
+    }
+    if (i == 0) c.gclaim_cnt[par ^ 1u] = 0;
   }
   // every other kernel of the tick has completed: reset the per-tick scratch counters
   if (i < sizeof(Counters) / 4) reinterpret_cast<uint32_t*>(k)[i] = 0;
