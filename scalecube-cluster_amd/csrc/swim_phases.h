@@ -474,36 +474,40 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   const uint64_t sweep = 2 * (spread + 1);
   GossipDev* slab = slab_of(c, v);
   unsigned long long nmsg = 0;
-  const uint32_t pairs = nt * glen;
-  for (uint32_t q0 = 0; q0 < pairs; q0 += 64) {
-    const uint32_t q = q0 + lane;
-    const bool act = q < pairs;
-    const uint32_t j = act ? q / glen : 0, p = act ? q - j * glen : 0;
-    const uint32_t t = s_t[1 + j];
+  // lane = slab position: one GossipState read serves all nt targets, whose loss draws and
+  // receiver checks are independent (issued together); messages keep the (target, position) keys
+  for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
+    const uint32_t p = p0 + lane;
     GossipDev g;
-    bool send = false, mat = false;
-    if (act) {
+    bool win = false;
+    if (p < glen) {
       g = slab[p];
-      send = (uint64_t)g.inf_period + spread >= period && !gossip_infected(g, t);
-      // delivered copies; a receiver on this shard that already holds the sequence id drops it
-      // (its collector only grows until delivery), another shard filters on arrival
-      mat = send && c.up[t] && in_pass(c, t, v) && !lost_k(c, out_loss(c, v, t), v, SWIM_STREAM_GOSSIP_OUT, j, p) &&
-            !(owned(c, t) && known_received(c, t, g.gossiper, g.seq));
+      win = (uint64_t)g.inf_period + spread >= period;
     }
-    nmsg += send ? 1u : 0u;
-    const uint64_t mm = __ballot(mat);
-    if (!mm) continue;
-    nmat += (uint32_t)__popcll(mm);  // wave-uniform
-    // one enqueue per target present in this pass: lane jj issues target jj's receiver atomic; the
-    // message slots of this shard's targets come out of the wave's chunk
-    uint32_t base = 0, slot = 0, cnt_mine = 0, pre = 0, loc_off = 0, loc_tot = 0;
-    for (uint32_t jj = 0; jj < nt; ++jj) {
-      const uint64_t mk = __ballot(mat && j == jj);
-      const uint32_t cj = (uint32_t)__popcll(mk);
-      if (lane == jj) cnt_mine = cj;
-      if (j == jj) pre = lanes_below(mk);
-      if (owned(c, s_t[1 + jj])) {
-        if (lane == jj) loc_off = loc_tot;
+    uint32_t matb = 0;  // bit j: a message to target j is materialised
+    if (__ballot(win)) {
+      for (uint32_t j = 0; j < nt; ++j) {
+        const uint32_t t = s_t[1 + j];
+        const bool send = win && !gossip_infected(g, t);
+        nmsg += send ? 1u : 0u;
+        // delivered copies; a receiver on this shard that already holds the sequence id drops it
+        // (its collector only grows until delivery), another shard filters on arrival
+        const bool mat = send && c.up[t] && in_pass(c, t, v) &&
+                         !lost_k(c, out_loss(c, v, t), v, SWIM_STREAM_GOSSIP_OUT, j, p) &&
+                         !(owned(c, t) && known_received(c, t, g.gossiper, g.seq));
+        matb |= (mat ? 1u : 0u) << j;
+      }
+    }
+    if (!__ballot(matb != 0)) continue;
+    // one enqueue per target present in this pass: lane j issues target j's receiver atomic; the
+    // message slots of this shard's targets come out of the wave's chunk, in (target, lane) order
+    uint32_t base = 0, slot = 0, cnt_mine = 0, loc_off = 0, loc_tot = 0;
+    for (uint32_t j = 0; j < nt; ++j) {
+      const uint32_t cj = (uint32_t)__popcll(__ballot((matb >> j) & 1u));
+      nmat += cj;  // wave-uniform
+      if (lane == j) cnt_mine = cj;
+      if (owned(c, s_t[1 + j])) {
+        if (lane == j) loc_off = loc_tot;
         loc_tot += cj;
       }
     }
@@ -522,28 +526,33 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         base = atomicAdd(&b.x->msg[owner(c, tj)], cnt_mine);
       }
     }
-    base = __shfl(base, (int)j, 64);
-    slot = __shfl(slot, (int)j, 64);
-    const uint32_t seq_i = base + pre;  // local messages: position in the pass's sequence
-    const uint32_t loc_slot = seq_i < cl ? cb + seq_i : nb + (seq_i - cl);
+    for (uint32_t j = 0; j < nt; ++j) {
+      const bool mat = (matb >> j) & 1u;
+      const uint64_t mk = __ballot(mat);
+      if (!mk) continue;
+      const uint32_t bj = __shfl(base, (int)j, 64), sj = __shfl(slot, (int)j, 64);
+      if (!mat) continue;
+      const uint32_t pre = lanes_below(mk);
+      const uint32_t t = s_t[1 + j];
+      GMsgFull msg;
+      msg.to = t; msg.from = v; msg.pos = p; msg.slot = sj + pre;
+      msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
+      msg.inc = g.inc; msg.pad[0] = msg.pad[1] = msg.pad[2] = 0;
+      if (owned(c, t)) {
+        const uint32_t seq_i = bj + pre;  // position in the pass's local sequence
+        const uint32_t loc_slot = seq_i < cl ? cb + seq_i : nb + (seq_i - cl);
+        if (loc_slot < b.msg_cap) b.msgs[loc_slot] = msg; else set_err(c, ERR_MSGS);
+      } else {
+        const uint32_t d = owner(c, t);
+        if (bj + pre < b.tx_msg_cap) b.tx_msgs[(size_t)d * b.tx_msg_cap + bj + pre] = msg; else set_err(c, ERR_MSGS);
+      }
+    }
     if (loc_tot > cl) {
       cb = nb + (loc_tot - cl);
       cl = want - (loc_tot - cl);
     } else {
       cb += loc_tot;
       cl -= loc_tot;
-    }
-    if (mat) {
-      GMsgFull msg;
-      msg.to = t; msg.from = v; msg.pos = p; msg.slot = slot + pre;
-      msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
-      msg.inc = g.inc; msg.pad[0] = msg.pad[1] = msg.pad[2] = 0;
-      if (owned(c, t)) {
-        if (loc_slot < b.msg_cap) b.msgs[loc_slot] = msg; else set_err(c, ERR_MSGS);
-      } else {
-        const uint32_t d = owner(c, t);
-        if (base + pre < b.tx_msg_cap) b.tx_msgs[(size_t)d * b.tx_msg_cap + base + pre] = msg; else set_err(c, ERR_MSGS);
-      }
     }
   }
   // sweep (:158-164, :350-358), order preserving: a chunk's survivors land at or below their own
