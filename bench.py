@@ -63,6 +63,7 @@ class Schedule:
         self.live = list(range(1, n))  # member 0 is the seed and stays up
         self.next_id = n
         self.rng = random.Random(12345)
+        self.progress = False  # --progress: a stderr line per step (long churn runs)
 
     def setup(self, e):
         if self.workload == "churn":
@@ -96,6 +97,8 @@ class Schedule:
                 nxt += 1
             e.step(nxt - p)
             p = nxt
+            if self.progress:
+                print(f"bench: period {p}/{p1}", file=sys.stderr, flush=True)
 
     def _has_ops(self, p):
         if self.workload == "failures":
@@ -151,6 +154,7 @@ def main():
     ap.add_argument("--members", type=int, default=None, help="default: 65,536 (16,384 for churn)")
     ap.add_argument("--cpu-periods", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--progress", action="store_true", help="print a stderr line after every period")
     ap.add_argument("--workload", choices=("quiet", "failures", "churn"), default="quiet")
     ap.add_argument("--gossip-capacity", type=int, default=0)
     ap.add_argument("--churn", type=int, default=None,
@@ -177,6 +181,7 @@ def main():
     lib = swimgpu.load_library()
     n = args.members or DEFAULT_MEMBERS[args.workload]
     sch = Schedule(args.workload, n, args.warmup + args.steps, args.churn, args.loss)
+    sch.progress = args.progress
     cfg = make_config(lib, local_rank)
     cfg.gossip_capacity = args.gossip_capacity
     if args.workload == "churn":
@@ -184,12 +189,15 @@ def main():
         # events); every member holds the gossips of its last ~18 s; a period's kills put a suspicion
         # timer at every viewer within a few seconds
         cfg.event_capacity = 1 << 25
-        cfg.gossip_capacity = max(cfg.gossip_capacity, 16384)
-        cfg.timer_capacity = 16 * sch.capacity
+        cfg.gossip_capacity = max(cfg.gossip_capacity, 65536)
         cfg.message_capacity = min(1 << 28, 4096 * sch.capacity)
         # a viewer keeps a SequenceIdCollector per gossiper heard until it is removed, and every
         # member that learns news through SYNC gossips it: in a long churn run that is most members
         cfg.collector_capacity = 1 << (2 * sch.capacity - 1).bit_length()
+        # 5 % loss drops gossips, so collectors fragment (many spilled interval blocks), and every
+        # false suspicion puts a timer at every viewer
+        cfg.interval_capacity = 512
+        cfg.timer_capacity = 64 * sch.capacity
     cfg.local_shards = args.local_shards
     se = None
     if world > 1:

@@ -125,12 +125,15 @@ typedef struct swim_config {
                                  phase (members of a real cluster start at different instants; the
                                  default 0 aligns them) */
   uint32_t timer_capacity;    /* suspicion timers that may fall due in one tick, per row shard, split
-                                 evenly over the shard's 256-viewer blocks (at least 1,024 each)
+                                 over the shard's 256-viewer blocks (2x the even share, at least 1,024 each)
                                  (0 = default 2 x the shard's rows; churn schedules a timer for every
                                  killed member at every viewer within a few seconds) */
   uint32_t message_capacity;  /* GOSSIP_REQ messages one gossip round may materialise, per row shard
                                  (0 = default 512 x the shard's rows; loss and churn storms need more) */
-  uint32_t reserved[3];
+  uint32_t interval_capacity; /* spilled SequenceIdCollector blocks per row in the smallest size tier
+                                 (0 = default 64; the larger tiers scale with it): collectors with
+                                 many gaps (lossy links drop gossips) spill out of their inline entry */
+  uint32_t reserved[2];
 } swim_config;
 
 /* preset: 0 = defaultConfig/defaultLanConfig, 1 = defaultWanConfig, 2 = defaultLocalConfig

@@ -691,10 +691,12 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 4096);
   // spilled collectors by tier (6 / 62 / 510 / 2,046 intervals); blocks are recycled, so these
   // bound the collectors spilled at once, not over the run
-  c.spill_cap[0] = std::max<uint32_t>(1u << 18, 64 * std::max(nl, 1u));
-  c.spill_cap[1] = std::max<uint32_t>(1u << 15, 8 * std::max(nl, 1u));
-  c.spill_cap[2] = std::max<uint32_t>(1u << 12, std::max(nl, 1u) / 2);
-  c.spill_cap[3] = std::max<uint32_t>(1u << 10, std::max(nl, 1u) / 16);
+  const uint64_t icap = cf.interval_capacity ? cf.interval_capacity : 64;  // tier-0 blocks per row
+  const uint64_t rows = std::max(nl, 1u);
+  c.spill_cap[0] = (uint32_t)std::min<uint64_t>(1ull << 31, std::max<uint64_t>(1u << 18, icap * rows));
+  c.spill_cap[1] = (uint32_t)std::min<uint64_t>(1ull << 30, std::max<uint64_t>(1u << 15, icap * rows / 8));
+  c.spill_cap[2] = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1u << 12, icap * rows / 128));
+  c.spill_cap[3] = (uint32_t)std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1u << 10, icap * rows / 1024));
   c.P = e->P;
   c.to_ticks = (uint32_t)cf.ping_timeout / e->tick_ms;
   c.relay_ticks = e->P - c.to_ticks;
@@ -716,7 +718,9 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   const uint64_t tcap = cf.timer_capacity ? cf.timer_capacity : 2ull * std::max(nl, 1u);
   c.wheel_nq = std::max(1u, (nl + 255) / 256);  // one queue per k_fd workgroup
   c.gwords = std::max(1u, (nl + 31) / 32);
-  c.wheel_cap = c.wheel_nq * (uint32_t)std::max<uint64_t>(1024, (tcap + c.wheel_nq - 1) / c.wheel_nq);
+  // per-block queues take 2x their even share: timers cluster on viewers unevenly (a churn tick
+  // schedules ~16 timers at each of 256 viewers of a block)
+  c.wheel_cap = c.wheel_nq * (uint32_t)std::max<uint64_t>(1024, 2 * ((tcap + c.wheel_nq - 1) / c.wheel_nq));
   c.ev_cap = std::max<uint32_t>(1024, (cf.event_capacity ? cf.event_capacity : (1u << 22)) / SUBQ);
   // deferred pingMembers inserts of one phase: a join burst adds every joiner at every viewer
   c.ins_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 22, 256ull * nl));

@@ -802,7 +802,10 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, Gos
 // messages are deferred to the workgroup: one wave bitonic-sorts up to DLV_BIG keys in LDS and its
 // lane 0 processes them; larger inboxes are sorted in place in global memory.
 constexpr int DLV_BLOCK = 256;
-constexpr int DLV_SORT = 24;
+#ifndef DLV_SORT_N
+#define DLV_SORT_N 24
+#endif
+constexpr int DLV_SORT = DLV_SORT_N;
 constexpr int DLV_BIG = 512;
 __device__ inline unsigned long long deliver_sorted(const Ctx& c, uint32_t r, const GMsgFull* a, uint32_t k,
                                                     const uint8_t* ix8, uint32_t ix8_stride, const uint16_t* ix16) {

@@ -64,7 +64,8 @@ class swim_config(C.Structure):
         ("timer_stagger", C.c_int32),
         ("timer_capacity", C.c_uint32),
         ("message_capacity", C.c_uint32),
-        ("reserved", C.c_uint32 * 3),
+        ("interval_capacity", C.c_uint32),
+        ("reserved", C.c_uint32 * 2),
     ]
 
 
