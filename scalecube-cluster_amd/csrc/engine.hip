@@ -404,7 +404,8 @@ static int32_t pack_rows(swim_engine* e, Shard& sd, uint32_t src_idx, int kind, 
   if (!tot) return SWIM_OK;
   if (!sd.grow(&sd.tx_rows, &sd.tx_row_cap, (size_t)tot * e->n)) return SWIM_ENOMEM;
   const SyncReq* tx = kind == 1 ? sd.b.tx_reqs : sd.b.tx_acks;
-  k_pack_rows<<<std::min<uint32_t>(tot, 1024), 256, 0, e->stream>>>(sd.c, tx, sd.b.tx_req_cap, *plan, sd.tx_rows);
+  const uint32_t units = tot * ((e->n + PACK_CHUNK - 1) / PACK_CHUNK);
+  k_pack_rows<<<std::min<uint32_t>(units, 4096), 256, 0, e->stream>>>(sd.c, tx, sd.b.tx_req_cap, *plan, tot, sd.tx_rows);
   return SWIM_OK;
 }
 
