@@ -765,6 +765,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.msg_start, nl) &&
             sd.alloc(&b.reqs, b.req_cap) && sd.alloc(&b.reqs_out, b.req_cap) && sd.alloc(&b.req_cnt, nl) &&
             sd.alloc(&b.req_start, nl) && sd.alloc(&b.req_recv, nl) && sd.alloc(&b.acks, b.req_cap) &&
+            sd.alloc(&b.req_desc, std::max(nl, 1u)) && sd.alloc(&b.ack_desc, std::max(nl, 1u)) &&
             sd.alloc(&b.acks_out, b.req_cap) && sd.alloc(&b.ack_cnt, nl) && sd.alloc(&b.ack_start, nl) &&
             sd.alloc(&b.ack_recv, nl) && 
             sd.alloc(&b.snap, (size_t)b.snap_cap * n) && sd.alloc(&b.snap_idx, nl) && sd.alloc(&b.snap_list, b.snap_cap) &&

@@ -61,11 +61,13 @@ struct Bufs {
   uint32_t* req_cnt;
   uint32_t* req_start;
   uint32_t* req_recv;
+  uint2* req_desc;  // per receiver-list position: (inbox start, message count), written by k_sync_prep
   SyncReq* acks;
   SyncReq* acks_out;
   uint32_t* ack_cnt;
   uint32_t* ack_start;
   uint32_t* ack_recv;
+  uint2* ack_desc;
   uint32_t* snap;       // snapshot record rows
   uint32_t snap_cap;
   uint32_t* snap_idx;   // per member: slot or NONE

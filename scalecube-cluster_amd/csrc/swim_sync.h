@@ -67,6 +67,7 @@ struct SubPhase {  // the SYNC (d2 = 0) or SYNC_ACK (d2 = 1) buffers
   uint32_t nrecv;
   uint32_t* cnt;
   uint32_t* start;
+  uint2* desc;
   SyncReq* out;
   uint32_t* nitems;
 };
@@ -75,10 +76,10 @@ __device__ inline SubPhase sub_phase(const Bufs& b, int d2) {
   SubPhase p;
   if (!d2) {
     p.items = b.reqs; p.total = min(b.k->req_total, b.req_cap); p.recv = b.req_recv; p.nrecv = b.k->req_recv_cnt;
-    p.cnt = b.req_cnt; p.start = b.req_start; p.out = b.reqs_out; p.nitems = &b.k->req_cursor;
+    p.cnt = b.req_cnt; p.start = b.req_start; p.desc = b.req_desc; p.out = b.reqs_out; p.nitems = &b.k->req_cursor;
   } else {
     p.items = b.acks; p.total = min(b.k->ack_total, b.req_cap); p.recv = b.ack_recv; p.nrecv = b.k->ack_recv_cnt;
-    p.cnt = b.ack_cnt; p.start = b.ack_start; p.out = b.acks_out; p.nitems = &b.k->ack_cursor;
+    p.cnt = b.ack_cnt; p.start = b.ack_start; p.desc = b.ack_desc; p.out = b.acks_out; p.nitems = &b.k->ack_cursor;
   }
   return p;
 }
@@ -160,6 +161,7 @@ __device__ void sync_prep_global(const Ctx& c, const Bufs& b, const SubPhase& p,
   for (uint32_t i = tid; i < p.nrecv; i += nt) {
     const uint32_t r = p.recv[i] - c.lo;
     p.start[r] = atomicAdd(&s_cursor, p.cnt[r]);
+    p.desc[i] = make_uint2(p.start[r], p.cnt[r]);
   }
   __syncthreads();
   if (tid == 0) *p.nitems = s_cursor;
@@ -233,7 +235,10 @@ __device__ void sync_prep_lds(const Ctx& c, const Bufs& b, const SubPhase& p, in
   s_start[2 * tid + 1] = ex + c0;
   if (tid == 0) { s_start[nr] = total; *p.nitems = total; }
   __syncthreads();
-  for (uint32_t i = tid; i < nr; i += nt) p.start[s_rid[i] - c.lo] = s_start[i];
+  for (uint32_t i = tid; i < nr; i += nt) {
+    p.start[s_rid[i] - c.lo] = s_start[i];
+    p.desc[i] = make_uint2(s_start[i], s_start[i + 1] - s_start[i]);
+  }
   for (uint32_t i = tid; i < ni; i += nt) {
     const uint32_t ri = prep_find(s_hkey, s_hval, s_q[i].to);
     s_perm[s_start[ri] + s_q[i].slot] = i;
@@ -635,8 +640,8 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
   uint64_t* pend = b.pend + (size_t)blockIdx.x * c.n;
   for (uint32_t i = blockIdx.x; i < p.nrecv; i += gridDim.x) {
     const uint32_t s = p.recv[i];
-    const uint32_t k = p.cnt[s - c.lo];
-    const uint32_t first = p.start[s - c.lo];
+    const uint2 dsc = p.desc[i];  // loaded with the receiver id: no dependent cnt / start lookup
+    const uint32_t first = dsc.x, k = dsc.y;
     if (threadIdx.x == 0) {
       mem(c, s).ev_minor = 0;
       mem(c, s).fetch_ctr = 0;
@@ -646,6 +651,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
     __syncthreads();
     for (uint32_t q = 0; q < k; ++q) {
       const SyncReq rq = p.out[first + q];
+      const uint32_t tot_q = b.item_total[first + q];  // issued with the header (stable since classify)
       const uint32_t* content = sync_content(c, b, rq);
       const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
       uint32_t npend = 0;
@@ -658,7 +664,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       __syncthreads();  // every lane has read s_mod before lane 0 may set it
       if (mod == 0 && (!own || d1 != NONE)) {  // precomputed classification is exact: the row is unchanged
         const uint32_t it = d1 != NONE ? d1 : first + q;
-        const uint32_t tot = d1 != NONE ? b.rev_total[it] : b.item_total[it];
+        const uint32_t tot = d1 != NONE ? b.rev_total[it] : tot_q;
         if (threadIdx.x == 0 && tot != 0) {
           const uint2* ic = (d1 != NONE ? b.rev_chunk : b.item_chunk) + (size_t)it * chunks;
           for (uint32_t ch = 0; ch < chunks; ++ch) {
