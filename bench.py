@@ -98,7 +98,9 @@ class Schedule:
             e.step(nxt - p)
             p = nxt
             if self.progress:
-                print(f"bench: period {p}/{p1}", file=sys.stderr, flush=True)
+                st = e.stats()
+                print(f"bench: period {p}/{p1} t={time.time():.3f} gossips={st['gossips_created']} "
+                      f"msgs={st['gossip_messages']} syncs={st['syncs']}", file=sys.stderr, flush=True)
 
     def _has_ops(self, p):
         if self.workload == "failures":
@@ -190,13 +192,13 @@ def main():
         # timer at every viewer within a few seconds
         cfg.event_capacity = 1 << 25
         cfg.gossip_capacity = max(cfg.gossip_capacity, 65536)
-        cfg.message_capacity = min(1 << 28, 4096 * sch.capacity)
+        cfg.message_capacity = 1 << 28
         # a viewer keeps a SequenceIdCollector per gossiper heard until it is removed, and every
         # member that learns news through SYNC gossips it: in a long churn run that is most members
         cfg.collector_capacity = 1 << (2 * sch.capacity - 1).bit_length()
         # 5 % loss drops gossips, so collectors fragment (many spilled interval blocks), and every
         # false suspicion puts a timer at every viewer
-        cfg.interval_capacity = 512
+        cfg.interval_capacity = 4096
         cfg.timer_capacity = 64 * sch.capacity
     cfg.local_shards = args.local_shards
     se = None
