@@ -547,7 +547,7 @@ static int32_t run_tick(swim_engine* e) {
     const uint32_t gm = grid_for(sd.c.nl, 256);
     // ---- A: suspicion timeouts, B: list compaction of their REMOVED + failure detector
     // ---- C: gossip round (period++ and the sender list in k_fd, then emit)
-    k_fd<<<gm, 256, 0, s>>>(sd.d_par, T, gossip_tick ? 1 : 0);
+    k_fd<<<gm, 256, 0, s>>>(sd.d_par, T, gossip_tick ? 1 : 0, gossip_tick ? 0 : 1);
     TICK_CHECK("k_fd");
     if (gossip_tick) {
       launch_emit(e, sd);
@@ -573,10 +573,11 @@ static int32_t run_tick(swim_engine* e) {
     }
   }
   // ---- D: SYNC / SYNC_ACK
-  for (Shard& sd : e->sh) {
-    k_sync_collect<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sd.d_par, T);
-    TICK_CHECK("k_sync_collect");
-  }
+  if (gossip_tick)  // (other ticks collect inside k_fd)
+    for (Shard& sd : e->sh) {
+      k_sync_collect<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sd.d_par, T);
+      TICK_CHECK("k_sync_collect");
+    }
   for (int d2 = 0; d2 < 2; ++d2) {
     if (multi)
       if (int32_t rc = exchange_sync(e, 1 + d2)) return rc;

@@ -635,7 +635,13 @@ __device__ __forceinline__ void gossip_round(const Ctx& c, const Bufs& b, uint32
 // lost a member in the timer phase (a per-viewer dependency, so
 // no separate launch), then every thread runs its viewer's FD step and, on gossip ticks, the
 // first step of its gossip round (k_gossip_emit runs the rest after every FD step is done).
-__global__ void __launch_bounds__(256) k_fd(KP, int gossip) {
+__device__ inline unsigned long long sync_collect_member(const Ctx& c, const Bufs& b, uint32_t v);
+
+// collect (ticks without a gossip round): the member's SYNC requests of phase D are collected here
+// too, right after its FD step.  Nothing between k_fd and phase D on such a tick touches the state
+// sync_collect_member reads (the member's own lists, schedule, fd_sync queue), so this equals the
+// separate k_sync_collect launch and saves its round trips.
+__global__ void __launch_bounds__(256) k_fd(KP, int gossip, int collect) {
   const Ctx c = pctx(P, T);
   __shared__ uint32_t s_list[256];
   __shared__ uint32_t s_cnt;
@@ -658,6 +664,11 @@ __global__ void __launch_bounds__(256) k_fd(KP, int gossip) {
   unsigned long long nev = 0, nreq = 0, npings = 0;
   if (i < c.nl && c.fd_next[i] == (uint32_t)T) fd_member(c, c.lo + i, nev, nreq, npings);
   if (gossip) gossip_round(c, P->b, i);  // phase C's first step for this member
+  if (collect) {
+    const Ctx cs = pctx_sync(P, T);
+    const unsigned long long nsync = i < c.nl ? sync_collect_member(cs, P->b, c.lo + i) : 0;
+    wave_stat_add(cs, ST_SYNCS, nsync);
+  }
   wave_stat_add(c, ST_FD_EVENTS, nev);
   wave_stat_add(c, ST_PING_REQS, nreq);
   wave_stat_add(c, ST_PINGS, npings);
