@@ -276,10 +276,15 @@ class Engine:
         self.close()
 
     def step(self, periods: int = 1) -> None:
-        _check("swim_step", self.lib.swim_step(self._h, periods))
+        self._check_step("swim_step", self.lib.swim_step(self._h, periods))
 
     def step_ticks(self, ticks: int = 1) -> None:
-        _check("swim_step_ticks", self.lib.swim_step_ticks(self._h, ticks))
+        self._check_step("swim_step_ticks", self.lib.swim_step_ticks(self._h, ticks))
+
+    def _check_step(self, fn: str, rc: int) -> None:
+        if rc == SWIM_ECAPACITY:  # name the structure that overflowed (swim_stats.capacity_errors)
+            raise SwimError(f"{fn} (capacity error bits {self.stats()['capacity_errors']:#x})", rc)
+        _check(fn, rc)
 
     def now(self) -> tuple[int, int, int]:
         t, ms, tpp = C.c_uint64(), C.c_uint32(), C.c_uint32()

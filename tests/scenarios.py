@@ -134,6 +134,15 @@ def catalog() -> list[Scenario]:
                  cfg=dict(gossip_segmentation_threshold=8, gossip_capacity=4096),
                  ops=[(0, "loss", 10, abi.ALL_MEMBERS)] + [(5, "join", 64 + i) for i in range(80)],
                  check_every=20),
+        # BASELINE config 3's rates in miniature: 5 % uniform outbound loss, every period 1 % of the
+        # members (2 of 200) killed and as many fresh members joined through seed 0, for 25 periods,
+        # then 35 quiet periods (the kills' suspicion timers fire, REMOVED)
+        Scenario("config3_rates_200", 250, 200, 600, seed=15, seeds=(0,),
+                 cfg=dict(gossip_capacity=8192, timer_capacity=1 << 16),
+                 ops=[(0, "loss", 5, abi.ALL_MEMBERS)]
+                 + [(10 * p, "kill", (7 + 13 * p + 100 * j) % 200) for p in range(1, 26) for j in range(2)]
+                 + [(10 * p, "join", 200 + 2 * (p - 1) + j) for p in range(1, 26) for j in range(2)],
+                 check_every=50),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),
                  cfg=dict(sync_interval=5000), ops=[(100, "partition", _partition(32, 16)), (1100, "partition", None)],
