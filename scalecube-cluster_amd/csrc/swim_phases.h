@@ -718,6 +718,7 @@ __global__ void __launch_bounds__(256) k_alloc(KP) {
   __shared__ uint32_t s_base;
   const Bufs b = P->b;
   const uint32_t nl = P->c.nl;
+  if (b.k->msg_total == 0) return;  // a round without messages (every msg_cnt is 0)
   for (uint32_t base = blockIdx.x * 256; base < nl; base += gridDim.x * 256) {
     const uint32_t r = base + threadIdx.x;
     const uint32_t k = r < nl ? b.msg_cnt[r] : 0u;
@@ -843,6 +844,7 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
   __shared__ uint16_t s_bix[DLV_BLOCK / 64][DLV_BIG];
   __shared__ uint32_t s_big_r[DLV_BLOCK], s_big_k[DLV_BLOCK], s_big_start[DLV_BLOCK];
   __shared__ uint32_t s_nbig;
+  if (b.k->msg_total == 0) return;  // a round without messages: no receiver has an inbox
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) s_nbig = 0;
   __syncthreads();
