@@ -212,9 +212,13 @@ __device__ void sync_prep_lds(const Ctx& c, const Bufs& b, const SubPhase& p, in
   __shared__ uint32_t s_nsnap;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
   const uint32_t ni = p.total, nr = p.nrecv;
+  // release the previous sub-phase's snapshot claims; their loads overlap the staging loads
+  // (the claims below are made after several barriers; *snap_cnt is rewritten at the end)
+  const uint32_t prev = min(*b.snap_cnt, b.snap_cap);
   for (uint32_t h = tid; h < PREP_HASH; h += nt) s_hkey[h] = NONE;
   if (tid == 0) s_nsnap = 0;
   __syncthreads();
+  const uint32_t rel = tid < prev ? b.snap_list[tid] : NONE;
   for (uint32_t i = tid; i < ni; i += nt) s_q[i] = p.items[i];
   for (uint32_t i = tid; i < nr; i += nt) {
     const uint32_t id = p.recv[i];
@@ -224,6 +228,8 @@ __device__ void sync_prep_lds(const Ctx& c, const Bufs& b, const SubPhase& p, in
     for (uint32_t h = prep_slot(id);; h = (h + 1) & (PREP_HASH - 1))
       if (atomicCAS(&s_hkey[h], NONE, id) == NONE) { s_hval[h] = i; break; }
   }
+  if (rel != NONE) b.snap_idx[rel - c.lo] = NONE;
+  for (uint32_t i = tid + nt; i < prev; i += nt) b.snap_idx[b.snap_list[i] - c.lo] = NONE;  // snap_cap > block
   if (tid >= nr && tid < 2 * PREP_BLOCK) s_start[tid] = 0;  // scan padding
   if (tid + PREP_BLOCK >= nr && tid + PREP_BLOCK < PREP_CAP) s_start[tid + PREP_BLOCK] = 0;
   __syncthreads();
@@ -296,14 +302,17 @@ __global__ void __launch_bounds__(PREP_BLOCK) k_sync_prep(KP, int d2, int copy_s
   const Bufs b = P->b;
   const SubPhase p = sub_phase(b, d2);
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
-  // release the previous sub-phase's snapshot claims
-  const uint32_t prev = min(*b.snap_cnt, b.snap_cap);
-  for (uint32_t i = tid; i < prev; i += nt) b.snap_idx[b.snap_list[i] - c.lo] = NONE;
-  __syncthreads();
-  if (tid == 0) *b.snap_cnt = 0;
-  __syncthreads();
-  if (p.total <= PREP_CAP && p.nrecv <= PREP_CAP) sync_prep_lds(c, b, p, d2);
-  else sync_prep_global(c, b, p, d2);
+  if (p.total <= PREP_CAP && p.nrecv <= PREP_CAP) {
+    sync_prep_lds(c, b, p, d2);  // releases the previous sub-phase's snapshot claims itself
+  } else {
+    // release the previous sub-phase's snapshot claims
+    const uint32_t prev = min(*b.snap_cnt, b.snap_cap);
+    for (uint32_t i = tid; i < prev; i += nt) b.snap_idx[b.snap_list[i] - c.lo] = NONE;
+    __syncthreads();
+    if (tid == 0) *b.snap_cnt = 0;
+    __syncthreads();
+    sync_prep_global(c, b, p, d2);
+  }
   if (!copy_snaps) return;
   __syncthreads();
   __threadfence_block();
