@@ -507,10 +507,6 @@ static void sync_params(swim_engine* e, Shard& sd) {
   sd.up_valid = true;
 }
 
-// deferred pingMembers inserts of the phase's ADDED events
-static void run_ins_pipeline(swim_engine* e, Shard& sd, int sync_phase) {
-  k_ins_apply<<<512, 256, 0, e->stream>>>(sd.d_par, e->T, sync_phase);
-}
 
 // SWIM_DEBUG_SYNC=1: synchronise after each tick kernel so a device fault names its kernel
 #define TICK_CHECK(name)                                                                            \
@@ -567,9 +563,7 @@ static int32_t run_tick(swim_engine* e) {
       k_scatter_msgs<<<512, 256, 0, s>>>(sd.d_par, T);
       TICK_CHECK("k_scatter_msgs");
       k_gossip_deliver<<<std::min<uint32_t>(1024, grid_for(sd.c.nl, DLV_BLOCK)), DLV_BLOCK, 0, s>>>(sd.d_par, T);
-      TICK_CHECK("k_gossip_deliver");
-      run_ins_pipeline(e, sd, 0);
-      TICK_CHECK("k_ins_apply");
+      TICK_CHECK("k_gossip_deliver");  // (also applies the phase's pingMembers inserts)
     }
   }
   // ---- D: SYNC / SYNC_ACK

@@ -5,7 +5,7 @@
 //                                                     ping-req / ack resolution + FD events
 // Phase C  round start (+ segmentation) in k_fd, k_gossip_emit, k_alloc, k_scatter_msgs, k_gossip_deliver
 // Phase D  k_sync_collect, k_sync_prep, k_sync_classify, k_sync_apply (swim_sync.h; SYNC and SYNC_ACK)
-// lists    k_ins_apply                                deferred pingMembers inserts of ADDED events
+// lists    (k_gossip_deliver, k_sync_apply)           deferred pingMembers inserts of ADDED events
 // tick end k_end_tick
 //
 // Every kernel reads its work size from device memory (grid-stride over device counters), so the
@@ -835,6 +835,12 @@ __device__ inline unsigned long long deliver_sorted(const Ctx& c, uint32_t r, co
   return acc;
 }
 
+__device__ void apply_ins_chain(const Ctx& c, uint32_t v);
+
+// Delivery, then the gossip phase's deferred pingMembers inserts of this workgroup's receivers: a
+// viewer's ADDED events of the phase all come from the one thread that delivered to it (on_added),
+// and no delivery reads another viewer's ping list, so a receiver's op chain is complete, and may be
+// applied, as soon as its own workgroup has delivered (no separate k_ins_apply launch).
 __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
@@ -919,6 +925,18 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
     __syncwarp();  // the wave's LDS region is reused by its next receiver
   }
   wave_stat_add(c, ST_GOSSIP_ACCEPTED, acc);
+  __shared__ uint32_t s_ins[DLV_BLOCK];
+  __shared__ uint32_t s_nins;
+  for (uint32_t base = blockIdx.x * DLV_BLOCK; base < c.nl; base += gridDim.x * DLV_BLOCK) {
+    __syncthreads();  // this workgroup's deliveries (and the previous chunk's inserts) are done
+    if (tid == 0) s_nins = 0;
+    __syncthreads();
+    const uint32_t i = base + tid;
+    if (i < c.nl && c.mem[i].ins_rank != 0) s_ins[atomicAdd(&s_nins, 1u)] = c.lo + i;
+    __syncthreads();
+    const uint32_t nv = s_nins;
+    for (uint32_t q = 0; q < nv; ++q) apply_ins_chain(c, s_ins[q]);
+  }
 }
 
 // ------------------------------------------------------------------------------- list inserts
@@ -965,12 +983,6 @@ __device__ void apply_ins_chain(const Ctx& c, uint32_t v) {
   __syncthreads();
 }
 
-// the gossip phase's inserts: one workgroup per viewer with ops
-__global__ void __launch_bounds__(256) k_ins_apply(KP, int sync_phase) {
-  const Ctx c = sync_phase ? pctx_sync(P, T) : pctx(P, T);
-  const uint32_t nv = *c.ins_list_cnt;
-  for (uint32_t i = blockIdx.x; i < nv; i += gridDim.x) apply_ins_chain(c, c.ins_list[i]);
-}
 
 // ------------------------------------------------------------------------------- phase D
 // selectSyncAddress (MembershipProtocolImpl.java:461-472): uniform over seeds U otherMembers by
