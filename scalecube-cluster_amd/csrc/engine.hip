@@ -567,11 +567,7 @@ static int32_t run_tick(swim_engine* e) {
     }
   }
   // ---- D: SYNC / SYNC_ACK
-  if (gossip_tick)  // (other ticks collect inside k_fd)
-    for (Shard& sd : e->sh) {
-      k_sync_collect<<<grid_for(sd.c.nl, 256), 256, 0, s>>>(sd.d_par, T);
-      TICK_CHECK("k_sync_collect");
-    }
+  // (SYNC requests were collected by k_gossip_deliver on gossip ticks, by k_fd on the others)
   for (int d2 = 0; d2 < 2; ++d2) {
     if (multi)
       if (int32_t rc = exchange_sync(e, 1 + d2)) return rc;

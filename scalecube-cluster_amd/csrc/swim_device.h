@@ -197,7 +197,7 @@ struct Ctx {
   // without touching their MemberDev
   uint32_t* fd_next;    // next tick with FD work (ping due, ack or relay timeout); stale while down
   uint32_t* sync_next;  // next periodic-SYNC tick (NONE: periodic SYNC off)
-  uint32_t* mflag;      // MF_* work for k_sync_collect / k_end_tick
+  uint32_t* mflag;      // MF_* work for SYNC collection / k_end_tick
   // receipt bitmaps: a subset of "receiver t's collector holds gossip (gossiper, seq)"
   // that k_gossip_emit tests before probing the collector table
   GSlot* gslot;          // [GSLOTS] the gossip owning each bitmap and the tick its bits became valid

@@ -4,7 +4,7 @@
 // Phase B  k_fd                                       list compaction after REMOVED, then ping /
 //                                                     ping-req / ack resolution + FD events
 // Phase C  round start (+ segmentation) in k_fd, k_gossip_emit, k_alloc, k_scatter_msgs, k_gossip_deliver
-// Phase D  k_sync_collect, k_sync_prep, k_sync_classify, k_sync_apply (swim_sync.h; SYNC and SYNC_ACK)
+// Phase D  SYNC collection (in k_fd / k_gossip_deliver), k_sync_prep, k_sync_classify, k_sync_apply (swim_sync.h; SYNC and SYNC_ACK)
 // lists    (k_gossip_deliver, k_sync_apply)           deferred pingMembers inserts of ADDED events
 // tick end k_end_tick
 //
@@ -836,11 +836,26 @@ __device__ inline unsigned long long deliver_sorted(const Ctx& c, uint32_t r, co
 }
 
 __device__ void apply_ins_chain(const Ctx& c, uint32_t v);
+__device__ inline unsigned long long sync_collect_member(const Ctx& c, const Bufs& b, uint32_t v);
+
+// phase D's SYNC collection for this workgroup's members (same member -> workgroup mapping as the
+// delivery loop), after their deliveries and inserts: nothing else in the gossip phase touches what
+// sync_collect_member reads (the member's own lists, schedule, fd_sync queue)
+__device__ inline void deliver_collect(KP) {
+  const Ctx cs = pctx_sync(P, T);
+  unsigned long long nsync = 0;
+  for (uint32_t base = blockIdx.x * DLV_BLOCK; base < cs.nl; base += gridDim.x * DLV_BLOCK) {
+    const uint32_t i = base + threadIdx.x;
+    if (i < cs.nl) nsync += sync_collect_member(cs, P->b, cs.lo + i);
+  }
+  wave_stat_add(cs, ST_SYNCS, nsync);
+}
 
 // Delivery, then the gossip phase's deferred pingMembers inserts of this workgroup's receivers: a
 // viewer's ADDED events of the phase all come from the one thread that delivered to it (on_added),
 // and no delivery reads another viewer's ping list, so a receiver's op chain is complete, and may be
-// applied, as soon as its own workgroup has delivered (no separate k_ins_apply launch).
+// applied, as soon as its own workgroup has delivered (no separate k_ins_apply launch).  Then the
+// members' SYNC collection (no separate k_sync_collect launch).
 __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
@@ -850,7 +865,10 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
   __shared__ uint16_t s_bix[DLV_BLOCK / 64][DLV_BIG];
   __shared__ uint32_t s_big_r[DLV_BLOCK], s_big_k[DLV_BLOCK], s_big_start[DLV_BLOCK];
   __shared__ uint32_t s_nbig;
-  if (b.k->msg_total == 0) return;  // a round without messages: no receiver has an inbox
+  if (b.k->msg_total == 0) {  // a round without messages: no receiver has an inbox
+    deliver_collect(P, T);
+    return;
+  }
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) s_nbig = 0;
   __syncthreads();
@@ -937,6 +955,8 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
     const uint32_t nv = s_nins;
     for (uint32_t q = 0; q < nv; ++q) apply_ins_chain(c, s_ins[q]);
   }
+  __syncthreads();
+  deliver_collect(P, T);
 }
 
 // ------------------------------------------------------------------------------- list inserts
@@ -1078,13 +1098,6 @@ __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Buf
   return nsync;
 }
 
-__global__ void k_sync_collect(KP) {
-  const Ctx c = pctx_sync(P, T);
-  const Bufs b = P->b;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned long long nsync = i < c.nl ? sync_collect_member(c, b, c.lo + i) : 0;
-  wave_stat_add(c, ST_SYNCS, nsync);
-}
 
 #include "swim_sync.h"
 
