@@ -133,7 +133,10 @@ typedef struct swim_config {
   uint32_t interval_capacity; /* spilled SequenceIdCollector blocks per row in the smallest size tier
                                  (0 = default 64; the larger tiers scale with it): collectors with
                                  many gaps (lossy links drop gossips) spill out of their inline entry */
-  uint32_t reserved[2];
+  uint32_t deliver_wave_min;  /* gossip inboxes above this many messages are delivered by a whole wave
+                                 (0 = default 24, the most the per-thread LDS sort holds; a test knob:
+                                 1 sends every inbox through the wave path) */
+  uint32_t reserved[1];
 } swim_config;
 
 /* preset: 0 = defaultConfig/defaultLanConfig, 1 = defaultWanConfig, 2 = defaultLocalConfig
@@ -303,17 +306,19 @@ int32_t swim_read_collector(swim_engine* e, uint32_t m, uint32_t gossiper, swim_
                             uint32_t cap, uint32_t* len);
 
 /* ---- measurement ---------------------------------------------------------------------------
- * Per-kernel timing of the SYNC classification kernel (k_sync_classify, the dominant HBM stream:
- * it classifies every SYNC and, from the same loads, the SYNC_ACK answering it), measured with HIP
+ * Per-kernel timing of the SYNC classification kernel (k_sync_classify, the SYNC row stream: it
+ * classifies every SYNC and, from the same loads, the SYNC_ACK answering it), measured with HIP
  * events bound to one launch in three on the engine's own stream.  For those sampled launches:
  * `launches`, `total_ms`, `messages` / `records` they processed, and `alg_bytes`: per streamed
- * message the record words of the content row and of the receiver row (2 x N x 4 B) plus 4 B per
- * record routed to the sequential merge.  enable = 0 stops recording; enable = 1
+ * (message, 1,024-subject block) unit the record words of the content row and of the receiver row
+ * (2 x 1,024 x 4 B), 8 B per unit skipped by the exact block witness (its two block counts), plus
+ * 4 B per record routed to the sequential merge.  enable = 0 stops recording; enable = 1
  * (re)starts it from zero.  The CPU oracle reports zeros. */
 typedef struct swim_kernel_profile {
   uint64_t launches;
   double total_ms;
-  uint64_t messages;   /* SYNC messages whose two rows were streamed */
+  uint64_t messages;   /* merge: (SYNC, 1,024-subject block) units whose two rows were streamed;
+                          fanout: GOSSIP_REQs materialised */
   uint64_t records;    /* records that changed a table (sequential merge path) */
   uint64_t alg_bytes;
 } swim_kernel_profile;

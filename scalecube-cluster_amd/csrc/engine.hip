@@ -38,8 +38,10 @@ constexpr uint32_t kDrainFirst = 1;    // the interval starts at one tick and ad
 constexpr uint32_t kClassifyGrid = CLS_GRID;  // 16,384 waves: about one (message, chunk) unit each at N = 65,536
 constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
 constexpr uint32_t kEmitGrid = 2048;      // 8,192 waves, one gossip sender at a time each
+constexpr uint32_t kDeliverGrid = 512;    // 2,048 waves for the big inboxes of a gossip storm
 constexpr uint32_t kStopCap = 4096;
 constexpr uint32_t kProfEvery = 3;  // SYNC classify launches between timed ones
+constexpr uint64_t kRebaseEvery = 16;  // ticks between rebases of the SYNC block witness (k_end_tick)
 
 uint32_t gcd_u(uint32_t a, uint32_t b) {
   while (b) { uint32_t t = a % b; a = b; b = t; }
@@ -69,37 +71,38 @@ uint32_t grid_for(uint32_t n, uint32_t block) { return std::max(1u, (n + block -
 // One shard: the device state of rows [lo, lo + nl) plus the replicated arrays.
 // One kernel's sampled launch timing: HIP events bound to the dispatch itself (hipExtLaunchKernelGGL:
 // the kernel's own start / completion timestamps, no extra stream packets) on one launch in
-// kProfEvery, plus two per-launch work counters the kernel accumulates into `slots`.
+// kProfEvery, plus three per-launch work counters the kernel accumulates into `slots`.
 struct KProf {
   std::vector<hipEvent_t> ev;
   uint32_t used = 0;
   uint64_t seen = 0;  // launches since profiling was enabled
-  unsigned long long* slots = nullptr;  // per sampled launch: {work counter a, work counter b}
+  unsigned long long* slots = nullptr;  // per sampled launch: {work counters a, b, c}
   double ms = 0;
-  unsigned long long a = 0, b = 0;
+  unsigned long long a = 0, b = 0, c = 0;
   uint64_t launches = 0;
 
   bool take(bool on) { return on && (seen++ % kProfEvery) == 0 && 2 * (used + 1) <= ev.size(); }
   void flush() {
     if (!used) return;
-    std::vector<unsigned long long> h(2 * (size_t)used);
+    std::vector<unsigned long long> h(3 * (size_t)used);
     hipMemcpy(h.data(), slots, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost);
     hipMemset(slots, 0, sizeof(unsigned long long) * h.size());
     for (uint32_t i = 0; i < used; ++i) {
       float t = 0.f;
       if (hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]) == hipSuccess) ms += t;
-      a += h[2 * i];
-      b += h[2 * i + 1];
+      a += h[3 * i];
+      b += h[3 * i + 1];
+      c += h[3 * i + 2];
     }
     launches += used;
     used = 0;
   }
   void reset() {
-    hipMemset(slots, 0, sizeof(unsigned long long) * ev.size());
+    hipMemset(slots, 0, sizeof(unsigned long long) * 3 * ev.size());
     used = 0;
     seen = 0;
     ms = 0;
-    a = b = 0;
+    a = b = c = 0;
     launches = 0;
   }
 };
@@ -239,7 +242,7 @@ static void launch_classify(swim_engine* e, Shard& s, int d2) {
     return;
   }
   hipExtLaunchKernelGGL(k_sync_classify, dim3(kClassifyGrid), dim3(CLS_BLOCK), 0, e->stream, k.ev[2 * k.used],
-                        k.ev[2 * k.used + 1], 0, s.d_par, e->T, k.slots + 2 * k.used);
+                        k.ev[2 * k.used + 1], 0, s.d_par, e->T, k.slots + 3 * k.used);
   k.used++;
 }
 
@@ -250,7 +253,7 @@ static void launch_emit(swim_engine* e, Shard& s) {
     return;
   }
   hipExtLaunchKernelGGL(k_gossip_emit, dim3(kEmitGrid), dim3(64 * EMIT_WAVES), 0, e->stream, k.ev[2 * k.used],
-                        k.ev[2 * k.used + 1], 0, s.d_par, e->T, k.slots + 2 * k.used);
+                        k.ev[2 * k.used + 1], 0, s.d_par, e->T, k.slots + 3 * k.used);
   k.used++;
 }
 
@@ -471,8 +474,6 @@ static int32_t exchange_sync(swim_engine* e, int kind) {
 static Ctx sync_ctx(Shard& sd) {  // list inserts of the SYNC phase use the second set of counters
   Ctx cd = sd.c;
   cd.ins_total = &sd.k->ins_total2;
-  cd.ins_list_cnt = &sd.k->ins_list_cnt2;
-  cd.ins_direct = 1;
   return cd;
 }
 
@@ -517,7 +518,7 @@ static void sync_params(swim_engine* e, Shard& sd) {
     }                                                                                               \
   } while (0)
 
-// One tick: ~11 kernels per shard (16 on gossip ticks); a sharded engine adds three exchanges.
+// One tick: 7 kernels per shard (11 on gossip ticks); a sharded engine adds k_recv_* and three exchanges.
 static int32_t run_tick(swim_engine* e) {
   e->T += 1;
   e->host_ticks += 1;
@@ -562,7 +563,8 @@ static int32_t run_tick(swim_engine* e) {
       TICK_CHECK("k_alloc");
       k_scatter_msgs<<<512, 256, 0, s>>>(sd.d_par, T);
       TICK_CHECK("k_scatter_msgs");
-      k_gossip_deliver<<<std::min<uint32_t>(1024, grid_for(sd.c.nl, DLV_BLOCK)), DLV_BLOCK, 0, s>>>(sd.d_par, T);
+      // at least kDeliverGrid workgroups: big inboxes are delivered a wave each, grid-stride
+      k_gossip_deliver<<<std::max<uint32_t>(kDeliverGrid, grid_for(sd.c.nl, DLV_BLOCK)), DLV_BLOCK, 0, s>>>(sd.d_par, T);
       TICK_CHECK("k_gossip_deliver");  // (also applies the phase's pingMembers inserts)
     }
   }
@@ -591,7 +593,7 @@ static int32_t run_tick(swim_engine* e) {
   for (Shard& sd : e->sh) {
     // ---- end of tick (also zeroes the per-tick counters and applies other shards' stops)
     const uint32_t ge = grid_for(std::max<uint32_t>(std::max<uint32_t>(sd.c.nl, sd.n_rx_stops), 64), 256);
-    k_end_tick<<<ge, 256, 0, s>>>(sd.d_par, T, sd.n_rx_stops);
+    k_end_tick<<<ge, REB_BLOCK, 0, s>>>(sd.d_par, T, sd.n_rx_stops, (T % kRebaseEvery) == 0 ? 1 : 0);
     TICK_CHECK("k_end_tick");
   }
   return SWIM_OK;
@@ -719,6 +721,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.msg_cap = cf.message_capacity ? cf.message_capacity
                                  : (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 512ull * nl));
   b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
+  b.wave_min = cf.deliver_wave_min ? std::min<uint32_t>(cf.deliver_wave_min, DLV_SORT) : (uint32_t)DLV_SORT;
   b.snap_cap = 64;
   b.chunks = (n + SYNC_CHUNK - 1) / SYNC_CHUNK;
   b.pool_cap = std::max<uint32_t>(1u << 22, 16 * n);
@@ -729,7 +732,9 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.tx_stop_cap = multi ? kStopCap : 0;
 
   const size_t nn = (size_t)nl * n;
-  bool ok = sd.alloc(&c.recs, nn) && sd.alloc(&c.aux, nn) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
+  c.blocks = (n + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
+  bool ok = sd.alloc(&c.recs, nn) && sd.alloc(&c.aux, nn) && sd.alloc(&c.ref, n) && sd.alloc(&c.dirty, n) &&
+            sd.alloc(&c.bdiff, (size_t)std::max(nl, 1u) * c.blocks) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
             sd.alloc(&c.remote, nn) && sd.alloc(&c.slab, (size_t)nl * c.gcap) && sd.alloc(&c.coll, (size_t)nl * c.hcap) &&
             sd.alloc(&c.spill[0], (size_t)c.spill_cap[0] * tier_words(0)) &&
             sd.alloc(&c.spill[1], (size_t)c.spill_cap[1] * tier_words(1)) &&
@@ -746,14 +751,15 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&c.ev_cnt, SUBQ) && sd.alloc(&c.default_loss, n) &&
             sd.alloc(&c.default_inbound, n) && sd.alloc(&c.group, n) && sd.alloc(&c.links, 1) &&
             sd.alloc(&c.is_seed, n) && sd.alloc(&c.seeds, n) && sd.alloc(&c.ins, c.ins_cap) &&
-            sd.alloc(&c.ins_list, nl) && sd.alloc(&c.compact_flag, nl) &&
+            sd.alloc(&c.ins_inline, (size_t)nl * INS_INLINE) && sd.alloc(&c.compact_flag, nl) &&
             sd.alloc(&c.fd_next, nl) && sd.alloc(&c.sync_next, nl) && sd.alloc(&c.mflag, nl) &&
             sd.alloc(&c.gslot, GSLOTS) && sd.alloc(&c.gpend, GSLOTS) &&
             sd.alloc(&c.gbits, (size_t)GSLOTS * c.gwords) && sd.alloc(&c.clr_tick, std::max(nl, 1u)) &&
             sd.alloc(&c.gclaim, 2 * GSLOTS) && sd.alloc(&c.gclaim_cnt, 2) &&
             sd.alloc(&c.stats, (size_t)ST_COUNT * ST_REPL) && sd.alloc(&c.err, 1) && sd.alloc(&sd.k, 1) &&
             sd.alloc(&sd.x, 1) && sd.alloc(&b.msgs, b.msg_cap) && sd.alloc(&b.msgs_out, b.msg_cap) &&
-            sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.msg_start, nl) &&
+            sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.msg_start, nl) && sd.alloc(&b.big_list, nl) &&
+            sd.alloc(&b.big_tick, nl) && sd.alloc(&b.perm, b.msg_cap) &&
             sd.alloc(&b.reqs, b.req_cap) && sd.alloc(&b.reqs_out, b.req_cap) && sd.alloc(&b.req_cnt, nl) &&
             sd.alloc(&b.req_start, nl) && sd.alloc(&b.req_recv, nl) && sd.alloc(&b.acks, b.req_cap) &&
             sd.alloc(&b.req_desc, std::max(nl, 1u)) && sd.alloc(&b.ack_desc, std::max(nl, 1u)) &&
@@ -771,7 +777,6 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   if (!ok) return SWIM_ENOMEM;
   sd.links_dev_cap = 1;
   c.ins_total = &sd.k->ins_total;
-  c.ins_list_cnt = &sd.k->ins_list_cnt;
   b.k = sd.k;
   b.x = sd.x;
   hipStream_t s = e->stream;
@@ -782,6 +787,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(c.ev_cnt, 0, 4 * SUBQ, s);
   hipMemsetAsync(c.up, 0, n, s);
   hipMemsetAsync(c.up, 1, n_initial, s);
+  hipMemsetAsync(c.ref, 0, 4 * (size_t)n, s);
+  hipMemsetAsync(c.dirty, 0, 4 * (size_t)n, s);
   hipMemsetAsync(c.default_loss, 0, n, s);
   hipMemsetAsync(c.default_inbound, 1, n, s);
   hipMemsetAsync(c.group, 0, 2 * (size_t)n, s);
@@ -797,6 +804,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(sd.k, 0, sizeof(Counters), s);
   hipMemsetAsync(sd.x, 0, sizeof(Xc), s);
   hipMemsetAsync(b.msg_cnt, 0, 4 * (size_t)nl, s);
+  hipMemsetAsync(b.big_tick, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.req_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.ack_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.snap_idx, 0xff, 4 * (size_t)nl, s);
@@ -1310,7 +1318,7 @@ int32_t swim_profile_enable(swim_engine* e, int32_t enable) {
         k->ev.resize(4 * kDrainEvery + 4);
         for (auto& ev : k->ev)
           if (hipEventCreate(&ev) != hipSuccess) return SWIM_EDEVICE;
-        if (!sd.alloc(&k->slots, k->ev.size())) return SWIM_ENOMEM;
+        if (!sd.alloc(&k->slots, 3 * k->ev.size())) return SWIM_ENOMEM;
       }
       k->reset();
     }
@@ -1323,14 +1331,19 @@ int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out) {
   if (!e || !out) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
   std::memset(out, 0, sizeof(*out));
+  uint64_t units = 0;
   for (Shard& sd : e->sh) {
     sd.prof_cls.flush();
     out->launches += sd.prof_cls.launches;
     out->total_ms += sd.prof_cls.ms;
     out->messages += sd.prof_cls.a;
     out->records += sd.prof_cls.b;
+    units += sd.prof_cls.c;
   }
-  out->alg_bytes = out->messages * (uint64_t)e->n * 8ull + out->records * 4ull;
+  const uint64_t skipped = units > out->messages ? units - out->messages : 0;
+  // per streamed unit the record words of both rows over its 1,024 subjects; per unit the block
+  // witness skipped, its two block counts; per complex record its pool entry
+  out->alg_bytes = out->messages * 8ull * SYNC_CHUNK + skipped * 8ull + out->records * 4ull;
   return SWIM_OK;
 }
 

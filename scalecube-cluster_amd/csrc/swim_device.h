@@ -112,7 +112,9 @@ struct GMsgFull {
   uint32_t to, from, pos, slot;
   uint32_t gossiper, seq, subject, status;
   int32_t inc;
-  uint32_t pad[3];
+  uint32_t pseq;  // place among the round's messages of the (from, to) pair, in slab-position order
+  uint32_t dup;   // 1: the receiver's collector already held the sequence id on arrival (a no-op)
+  uint32_t pad;
 };
 
 struct SyncReq {  // SYNC (request) or SYNC_ACK
@@ -126,6 +128,9 @@ struct SyncReq {  // SYNC (request) or SYNC_ACK
 struct InsOp {  // deferred pingMembers.add(nextInt(size), member) of an ADDED event
   uint32_t s, phase, minor, next;  // next: the viewer's following op in event order (chain)
 };
+// a viewer's first INS_INLINE ops of a phase sit in its own slots (read in parallel by the list
+// kernel); later ones chain through the shared op array
+constexpr uint32_t INS_INLINE = 8;
 
 // Receipt bitmap slot: gossip (gossiper, seq) hashes to one of GSLOTS slots; the slot's bits are
 // valid for the gossip `key` from tick `tick` on (a slot is (re)claimed only in k_end_tick, when no
@@ -157,6 +162,15 @@ struct Ctx {
   // the view cell of (viewer, subject) is stored split in two u32 words (layout below)
   uint32_t* recs;  // [nl][n] MembershipRecord: what SYNC carries and the merge filter reads
   uint32_t* aux;   // [nl][n] the viewer-local side maps (members / aliveEmitted / metadata / timer)
+  // exact block witness of the record rows: ref is this shard's reference record per
+  // subject, bdiff[row][blk] the number of subjects of 1,024-subject block blk whose record in the row
+  // differs from ref — two rows with bdiff 0 in a block hold identical records there.  Maintained on
+  // every record write (cell_put); ref follows the rows' majority (k_end_tick's rebase of the subjects
+  // marked dirty).
+  uint32_t* ref;     // [n]
+  uint32_t* bdiff;   // [nl][blocks]
+  uint32_t* dirty;   // [n] 1: some row's record of the subject changed since the last rebase
+  uint32_t blocks;   // ceil(n / 1024)
   MemberDev* mem;
   uint8_t* up;  // replicated: member's transport is running
   uint32_t* ping;
@@ -185,13 +199,12 @@ struct Ctx {
   uint8_t* is_seed;
   uint32_t* seeds;
   uint32_t n_seeds;
-  // deferred list ops
-  InsOp* ins;
+  // deferred list ops: a viewer's ops of one phase are applied by whoever delivered to it, right
+  // after its deliveries / merges (k_gossip_deliver, k_sync_apply)
+  InsOp* ins;              // overflow chain storage, shared by the viewers of the phase
+  InsOp* ins_inline;       // [nl][INS_INLINE] each viewer's first ops of the phase
   uint32_t* ins_total;
   uint32_t ins_cap;
-  uint32_t* ins_list;      // viewers with ops (unused when ins_direct: the phase applies its own)
-  uint32_t ins_direct;     // SYNC phase: k_sync_apply applies a viewer's inserts after its merges
-  uint32_t* ins_list_cnt;
   uint32_t* compact_flag;  // per viewer: lists hold a REMOVED member (compacted before its next FD step)
   // compact per-member schedule: lets the per-tick member scans skip idle members
   // without touching their MemberDev
@@ -285,12 +298,24 @@ __device__ __forceinline__ uint64_t cell_get(const Ctx& c, uint32_t v, uint32_t 
   const size_t i = (size_t)(v - c.lo) * c.n + s;
   return compose_cell(c.recs[i], c.aux[i]);
 }
+constexpr uint32_t BLK_SHIFT = 10;  // 1,024-subject blocks (= the SYNC classify unit)
+// the block witness follows a record change of (v, s): old -> nr (atomic: a row's cells may change
+// from several threads of one kernel, e.g. entry-parallel timers)
+__device__ inline void rec_changed(const Ctx& c, uint32_t v, uint32_t s, uint32_t old, uint32_t nr) {
+  const uint32_t rf = c.ref[s];
+  const int d = (nr != rf ? 1 : 0) - (old != rf ? 1 : 0);
+  if (d) atomicAdd(&c.bdiff[(size_t)(v - c.lo) * c.blocks + (s >> BLK_SHIFT)], (uint32_t)d);
+  c.dirty[s] = 1u;
+}
 __device__ __forceinline__ void cell_put(const Ctx& c, uint32_t v, uint32_t s, uint64_t cell) {
   const size_t i = (size_t)(v - c.lo) * c.n + s;
   const uint32_t inc = (uint32_t)cell;
   if (inc >= REC_INC_MASK) set_err(c, ERR_INC);
-  c.recs[i] = (inc & REC_INC_MASK) | ((uint32_t)((cell >> 32) & 3u) << 29) | ((uint32_t)((cell >> 34) & 1u) << 31);
+  const uint32_t nr = (inc & REC_INC_MASK) | ((uint32_t)((cell >> 32) & 3u) << 29) | ((uint32_t)((cell >> 34) & 1u) << 31);
+  const uint32_t old = c.recs[i];
+  c.recs[i] = nr;
   c.aux[i] = (uint32_t)((cell >> 35) & 0xfu) | ((uint32_t)((cell >> 39) & SWIM_DEADLINE_MASK) << 4);
+  if (nr != old) rec_changed(c, v, s, old, nr);
 }
 __device__ __forceinline__ MemberDev& mem(const Ctx& c, uint32_t v) { return c.mem[v - c.lo]; }
 __device__ __forceinline__ uint32_t* ping_list(const Ctx& c, uint32_t v) { return c.ping + (size_t)(v - c.lo) * c.n; }
@@ -579,26 +604,31 @@ __device__ inline void emit(const Ctx& c, uint32_t v, uint32_t s, uint32_t type,
 }
 
 // FailureDetectorImpl.onMemberEvent (:321-346) + GossipProtocolImpl.onMemberEvent (:238-261) for
-// ADDED: the remote list append is O(1) and done now; the pingMembers insert is deferred to the
-// phase's list kernel, which applies a viewer's inserts in event order.
+// ADDED: the remote list append is O(1) and done now; the pingMembers insert is deferred to the end
+// of the viewer's deliveries in this phase (apply_ins_batch), which applies its inserts in event order.
+// Invariant the early exits of the delivery kernels rely on: ADDED is only published while a viewer
+// processes received messages (gossip delivery, SYNC / SYNC_ACK merges), never by the timer or FD
+// phases (publish_fd never admits ALIVE), so a phase without deliveries has no ops.
 __device__ inline void on_added(const Ctx& c, uint32_t v, uint32_t s, uint32_t phase, uint32_t minor) {
   MemberDev& m = mem(c, v);
   remote_list(c, v)[m.remote_len] = s;
   m.remote_len++;
   // a viewer's ADDED events of one phase come from the one thread that owns it in that phase, so
-  // its ops form a chain in event order with no grouping pass
-  const uint32_t i = atomicAdd(c.ins_total, 1u);
-  if (i >= c.ins_cap) { set_err(c, ERR_INS); return; }
+  // its ops are in event order with no grouping pass
   InsOp op;
   op.s = s; op.phase = phase; op.minor = minor; op.next = NONE;
-  c.ins[i] = op;
-  if (m.ins_rank++ == 0) {
-    m.ins_head = i;
-    if (!c.ins_direct) c.ins_list[atomicAdd(c.ins_list_cnt, 1u)] = v;
+  const uint32_t rank = m.ins_rank;
+  if (rank < INS_INLINE) {
+    c.ins_inline[(size_t)(v - c.lo) * INS_INLINE + rank] = op;
   } else {
-    c.ins[m.ins_tail].next = i;
+    const uint32_t i = atomicAdd(c.ins_total, 1u);
+    if (i >= c.ins_cap) { set_err(c, ERR_INS); return; }
+    c.ins[i] = op;
+    if (rank == INS_INLINE) m.ins_head = i;
+    else c.ins[m.ins_tail].next = i;
+    m.ins_tail = i;
   }
-  m.ins_tail = i;
+  m.ins_rank = rank + 1;
 }
 
 // REMOVED: GossipProtocolImpl drops the member's SequenceIdCollector (:242); both lists drop the

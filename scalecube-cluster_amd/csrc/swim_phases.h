@@ -20,11 +20,12 @@ struct Counters {
   uint32_t msg_total, msg_cursor, pad0;
   uint32_t req_total, req_recv_cnt, req_cursor;
   uint32_t ack_total, ack_recv_cnt, ack_cursor;
-  uint32_t ins_total, ins_list_cnt;    // list inserts of the gossip phase
-  uint32_t ins_total2, ins_list_cnt2;  // list inserts of the SYNC phase
+  uint32_t ins_total, pad1;   // overflow list-insert ops of the gossip phase
+  uint32_t ins_total2, pad2;  // overflow list-insert ops of the SYNC phase
   uint32_t pool_cursor;  // complex-record pool of the SYNC classify kernel
   uint32_t sender_cnt;   // senders of this tick's gossip round with live gossips
-  uint32_t pad[2];
+  uint32_t big_cnt;      // receivers whose inbox takes the wave-parallel delivery path
+  uint32_t pad;
 };
 
 // per-tick message counts by destination shard (sharded engines), zeroed by k_end_tick
@@ -55,6 +56,10 @@ struct Bufs {
   uint32_t msg_cap;
   uint32_t* msg_cnt;   // per receiver
   uint32_t* msg_start;
+  uint32_t* big_list;  // local indices of receivers with big inboxes (k_alloc)
+  uint32_t* big_tick;  // per receiver: tick whose inbox took the wave-parallel path
+  uint32_t wave_min;   // inboxes above this many messages take it (<= DLV_SORT)
+  uint32_t* perm;      // [msg_cap] canonical delivery order of big inboxes (index into the inbox)
   SyncReq* reqs;
   SyncReq* reqs_out;
   uint32_t req_cap;
@@ -112,6 +117,11 @@ __device__ __forceinline__ Ctx pctx_sync(const Params* __restrict__ P, uint64_t 
 // ------------------------------------------------------------------------------- init
 __global__ void k_init_rows(Ctx c, uint32_t n_initial) {
   const uint32_t conv_aux = A_IN_MEMBERS | A_ALIVE_EMITTED | A_HAS_METADATA;
+  // the block witness starts from the converged row: ref = every initial member ALIVE at incarnation 0
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < c.n; s += gridDim.x * blockDim.x) {
+    c.ref[s] = s < n_initial ? REC_IN_TABLE : 0u;
+    c.dirty[s] = 0u;
+  }
   for (uint32_t v = c.lo + blockIdx.x; v < c.lo + c.nl; v += gridDim.x) {
     uint32_t* r = rec_row(c, v);
     uint32_t* a = aux_row(c, v);
@@ -120,6 +130,12 @@ __global__ void k_init_rows(Ctx c, uint32_t n_initial) {
       const bool in = init && s < n_initial;
       r[s] = in ? REC_IN_TABLE : 0u;  // ALIVE, incarnation 0
       a[s] = in ? (s == v ? A_IN_MEMBERS : conv_aux) : 0u;
+    }
+    // an initial row equals ref; a free slot's empty row differs at every initial member
+    for (uint32_t blk = threadIdx.x; blk < c.blocks; blk += blockDim.x) {
+      const uint32_t b0 = blk << BLK_SHIFT, b1 = min(c.n, b0 + (1u << BLK_SHIFT));
+      const uint32_t in_blk = n_initial > b0 ? min(n_initial, b1) - b0 : 0u;
+      c.bdiff[(size_t)(v - c.lo) * c.blocks + blk] = init ? 0u : in_blk;
     }
   }
 }
@@ -476,6 +492,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   const uint64_t sweep = 2 * (spread + 1);
   GossipDev* slab = slab_of(c, v);
   unsigned long long nmsg = 0;
+  uint32_t pseq = 0;  // lane j < nt: messages materialised to target j so far (GMsgFull.pseq)
   // lane = slab position: one GossipState read serves all nt targets, whose loss draws and
   // receiver checks are independent (issued together); messages keep the (target, position) keys
   for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
@@ -532,14 +549,14 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       const bool mat = (matb >> j) & 1u;
       const uint64_t mk = __ballot(mat);
       if (!mk) continue;
-      const uint32_t bj = __shfl(base, (int)j, 64), sj = __shfl(slot, (int)j, 64);
+      const uint32_t bj = __shfl(base, (int)j, 64), sj = __shfl(slot, (int)j, 64), qj = __shfl(pseq, (int)j, 64);
       if (!mat) continue;
       const uint32_t pre = lanes_below(mk);
       const uint32_t t = s_t[1 + j];
       GMsgFull msg;
       msg.to = t; msg.from = v; msg.pos = p; msg.slot = sj + pre;
       msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
-      msg.inc = g.inc; msg.pad[0] = msg.pad[1] = msg.pad[2] = 0;
+      msg.inc = g.inc; msg.pseq = qj + pre; msg.dup = 0; msg.pad = 0;
       if (owned(c, t)) {
         const uint32_t seq_i = bj + pre;  // position in the pass's local sequence
         const uint32_t loc_slot = seq_i < cl ? cb + seq_i : nb + (seq_i - cl);
@@ -549,6 +566,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         if (bj + pre < b.tx_msg_cap) b.tx_msgs[(size_t)d * b.tx_msg_cap + bj + pre] = msg; else set_err(c, ERR_MSGS);
       }
     }
+    pseq += cnt_mine;  // lane j: target j's messages so far this round
     if (loc_tot > cl) {
       cb = nb + (loc_tot - cl);
       cl = want - (loc_tot - cl);
@@ -699,20 +717,29 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned lo
   wave_stat_add(c, ST_GOSSIP_MESSAGES, nmsg);
 }
 
-// GOSSIP_REQs arriving from other shards: drop provable duplicates (the emitter could not see
-// this shard's collectors), then join the local message list exactly as a local send does
+// GOSSIP_REQs arriving from other shards join the local message list exactly as a local send does;
+// provable duplicates (the emitter could not see this shard's collectors) are flagged, and delivery
+// skips them: the collector holds the sequence id, so onGossipReq would return at once
 __global__ void k_recv_msgs(KP, uint32_t nrx) {
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrx; i += gridDim.x * blockDim.x) {
-    const GMsgFull msg = b.rx_msgs[i];
-    if (coll_contains(c, coll_find(c, msg.to, msg.gossiper), msg.seq)) continue;
+    GMsgFull msg = b.rx_msgs[i];
+    // kept (flagged) so that each (sender, receiver) pair's pseq stays dense for deliver_big
+    msg.dup = coll_contains(c, coll_find(c, msg.to, msg.gossiper), msg.seq) ? 1u : 0u;
     deliver_local_msg(c, b, msg);
   }
 }
 
+// inboxes above DLV_SORT messages are delivered by a whole wave (deliver_big)
+#ifndef DLV_SORT_N
+#define DLV_SORT_N 24
+#endif
+constexpr int DLV_SORT = DLV_SORT_N;
+
 // group-by-receiver: region start per receiver (a workgroup scan of 256 receivers' counts and one
-// cursor atomic per workgroup), then scatter by (start + arrival slot)
+// cursor atomic per workgroup), then scatter by (start + arrival slot); receivers with big inboxes
+// are listed (one wave-aggregated atomic) and stamped for the wave-parallel delivery path
 __global__ void __launch_bounds__(256) k_alloc(KP) {
   __shared__ uint32_t s_wave[256 / 64 + 1];
   __shared__ uint32_t s_base;
@@ -727,6 +754,17 @@ __global__ void __launch_bounds__(256) k_alloc(KP) {
     if (threadIdx.x == 0) s_base = total ? atomicAdd(&b.k->msg_cursor, total) : 0u;
     __syncthreads();
     if (k) b.msg_start[r] = s_base + off;
+    const bool big = k > b.wave_min;
+    const uint64_t mk = __ballot(big);
+    if (mk) {
+      uint32_t bb = 0;
+      if ((threadIdx.x & 63) == 0) bb = atomicAdd(&b.k->big_cnt, (uint32_t)__popcll(mk));
+      bb = __shfl(bb, 0, 64);
+      if (big) {
+        b.big_list[bb + lanes_below(mk)] = r;
+        b.big_tick[r] = (uint32_t)T;
+      }
+    }
     __syncthreads();
   }
 }
@@ -745,19 +783,10 @@ __global__ void k_scatter_msgs(KP) {
 
 __device__ __forceinline__ uint64_t msg_key(const GMsgFull& m) { return ((uint64_t)m.from << 32) | m.pos; }
 
-// heap sort of one receiver's messages by (sender, slab position)
+// heap sort of one receiver's messages by (sender, slab position): the big path's fallback for an
+// inbox from more than BIG_MAXD distinct senders
 __device__ inline void sort_msgs(GMsgFull* a, uint32_t n) {
   if (n < 2) return;
-  if (n <= 16) {
-    for (uint32_t i = 1; i < n; ++i) {
-      GMsgFull x = a[i];
-      uint64_t kx = msg_key(x);
-      int32_t j = (int32_t)i - 1;
-      while (j >= 0 && msg_key(a[j]) > kx) { a[j + 1] = a[j]; --j; }
-      a[j + 1] = x;
-    }
-    return;
-  }
   auto sift = [&](uint32_t start, uint32_t end) {
     uint32_t root = start;
     while (2 * root + 1 < end) {
@@ -776,6 +805,7 @@ __device__ inline void sort_msgs(GMsgFull* a, uint32_t n) {
 
 // onGossipReq (GossipProtocolImpl.java:201-215) for one received message, in canonical order
 __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, GossipDev* slab, const GMsgFull& g) {
+  if (g.dup) return false;  // the collector held it on arrival and only grows until now
   CollEnt* col = coll_ensure(c, r, g.gossiper);
   if (!col) return false;
   const bool was_cleared = (col->meta & COLL_CLEARED) != 0;
@@ -810,197 +840,332 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, Gos
   return true;
 }
 
-// One receiver per thread (the onGossipReq chain of a receiver is sequential, so concurrency comes
-// from many receivers): the inbox keys (sender, slab position) are insertion-sorted in an LDS slice
-// laid out [slot][thread] (conflict-free), then processed in that order.  Inboxes above DLV_SORT
-// messages are deferred to the workgroup: one wave bitonic-sorts up to DLV_BIG keys in LDS and its
-// lane 0 processes them; larger inboxes are sorted in place in global memory.
+// ------------------------------------------------------------------------------- list inserts
+// group barrier of apply_ins_batch: the workgroup, or one wave (global and LDS accesses of the wave
+// complete before any lane goes on)
+template <bool WG>
+__device__ __forceinline__ void ins_bar() {
+  if (WG) {
+    __syncthreads();
+  } else {
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// pingMembers.add(nextInt(size), s) (FailureDetectorImpl.java:334-345) for every ADDED event of
+// viewer v in this phase, in event order, in ONE pass over the list: the inserts' final positions are
+// resolved first (insert q shifts every earlier insert at or after its index), then the original
+// elements move right, tail first, by the number of inserted positions before their destination, then
+// the inserted members are written — the list k sequential ArrayList.add calls leave.  NT threads
+// cooperate (a workgroup, WG = true, or one wave); every thread of the group calls it.  sP / sS / sR:
+// NT words of LDS each.
+template <int NT, bool WG>
+__device__ void apply_ins_batch(const Ctx& c, uint32_t v, uint32_t tid, uint32_t* sP, uint32_t* sS, uint32_t* sR) {
+  MemberDev& m = mem(c, v);
+  const uint32_t k = m.ins_rank;
+  if (k == 0) return;
+  uint32_t* pl = ping_list(c, v);
+  const InsOp* inl = c.ins_inline + (size_t)(v - c.lo) * INS_INLINE;
+  uint32_t cur = m.ins_head;  // ops beyond the inline ones (thread 0 walks the chain)
+  uint32_t len = m.ping_len;
+  for (uint32_t q0 = 0; q0 < k; q0 += NT) {
+    const uint32_t kb = min((uint32_t)NT, k - q0);
+    // index of insert q = nextInt(size before it); the draw is keyed by the event (phase, minor)
+    if (tid < kb && q0 + tid < INS_INLINE) {
+      const InsOp op = inl[q0 + tid];
+      sS[tid] = op.s;
+      sP[tid] = next_int(draw(c, v, SWIM_STREAM_PING_INSERT, op.phase, op.minor), len + tid);
+    }
+    if (tid == 0) {
+      for (uint32_t q = max(q0, INS_INLINE); q < q0 + kb; ++q) {
+        const InsOp op = c.ins[cur];
+        sS[q - q0] = op.s;
+        sP[q - q0] = next_int(draw(c, v, SWIM_STREAM_PING_INSERT, op.phase, op.minor), len + (q - q0));
+        cur = op.next;
+      }
+    }
+    ins_bar<WG>();
+    for (uint32_t q = 1; q < kb; ++q) {  // sP[j] -> position of insert j after insert q
+      const uint32_t idx = sP[q];
+      if (tid < q && sP[tid] >= idx) sP[tid] += 1;
+      ins_bar<WG>();
+    }
+    if (tid < kb) {  // final positions ascending (they are distinct)
+      const uint32_t p = sP[tid];
+      uint32_t rk = 0;
+      for (uint32_t j = 0; j < kb; ++j) rk += sP[j] < p ? 1u : 0u;
+      sR[rk] = p;
+    }
+    ins_bar<WG>();
+    // original element i lands at i + #{j : sR[j] - j <= i} (sR[j] - j is non-decreasing)
+    const uint32_t pmin = sR[0];
+    for (int64_t hi = (int64_t)len; hi > (int64_t)pmin; hi -= NT) {
+      const int64_t lo = hi - NT > (int64_t)pmin ? hi - NT : (int64_t)pmin;
+      const int64_t i = lo + tid;
+      uint32_t val = 0, dest = 0;
+      if (i < hi) {
+        val = pl[i];
+        uint32_t a = 0, z = kb;
+        while (a < z) {
+          const uint32_t mid = (a + z) >> 1;
+          if (sR[mid] - mid <= (uint32_t)i) a = mid + 1; else z = mid;
+        }
+        dest = (uint32_t)i + a;
+      }
+      ins_bar<WG>();
+      if (i < hi) pl[dest] = val;
+      ins_bar<WG>();
+    }
+    if (tid < kb) pl[sP[tid]] = sS[tid];
+    len += kb;
+    ins_bar<WG>();
+  }
+  if (tid == 0) {
+    m.ping_len = len;
+    m.ins_rank = 0;
+  }
+  ins_bar<WG>();
+}
+
+// ------------------------------------------------------------------------------- delivery
+// Small inboxes (<= DLV_SORT messages): one receiver per thread, the inbox keys (sender, slab
+// position) insertion-sorted in an LDS slice laid out [slot][thread] (conflict-free), then
+// onGossipReq in that order.  Big inboxes: one wave per receiver (deliver_big).
 constexpr int DLV_BLOCK = 256;
-#ifndef DLV_SORT_N
-#define DLV_SORT_N 24
-#endif
-constexpr int DLV_SORT = DLV_SORT_N;
-constexpr int DLV_BIG = 512;
+constexpr int DLV_WAVES = DLV_BLOCK / 64;
+constexpr uint32_t BIG_MAXD = 128;  // distinct senders a big inbox is ranked over in LDS
+
 __device__ inline unsigned long long deliver_sorted(const Ctx& c, uint32_t r, const GMsgFull* a, uint32_t k,
-                                                    const uint8_t* ix8, uint32_t ix8_stride, const uint16_t* ix16) {
+                                                    const uint8_t* ix8, uint32_t ix8_stride) {
   MemberDev& m = mem(c, r);
   m.ev_minor = 0;
   m.fetch_ctr = 0;
   GossipDev* slab = slab_of(c, r);
   unsigned long long acc = 0;
   for (uint32_t q = 0; q < k; ++q) {
-    const uint32_t at = ix8 ? ix8[q * ix8_stride] : ix16 ? ix16[q] : q;
+    const uint32_t at = ix8 ? ix8[q * ix8_stride] : q;
     if (on_gossip_req(c, r, m, slab, a[at])) acc++;
   }
   return acc;
 }
 
-__device__ void apply_ins_chain(const Ctx& c, uint32_t v);
-__device__ inline unsigned long long sync_collect_member(const Ctx& c, const Bufs& b, uint32_t v);
+struct BigLds {  // per wave
+  uint32_t snd[BIG_MAXD];  // distinct senders (found order, then ascending)
+  uint32_t cnt[BIG_MAXD];  // their message counts, then running inbox bases
+  GMsgFull m[64];          // the messages of the current 64-message step, canonical order
+  uint32_t iP[64], iS[64], iR[64];  // apply_ins_batch scratch
+};
 
-// phase D's SYNC collection for this workgroup's members (same member -> workgroup mapping as the
-// delivery loop), after their deliveries and inserts: nothing else in the gossip phase touches what
-// sync_collect_member reads (the member's own lists, schedule, fd_sync queue)
-__device__ inline void deliver_collect(KP) {
-  const Ctx cs = pctx_sync(P, T);
-  unsigned long long nsync = 0;
-  for (uint32_t base = blockIdx.x * DLV_BLOCK; base < cs.nl; base += gridDim.x * DLV_BLOCK) {
-    const uint32_t i = base + threadIdx.x;
-    if (i < cs.nl) nsync += sync_collect_member(cs, P->b, cs.lo + i);
-  }
-  wave_stat_add(cs, ST_SYNCS, nsync);
+__device__ __forceinline__ void wave_sync() {
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
 }
 
-// Delivery, then the gossip phase's deferred pingMembers inserts of this workgroup's receivers: a
-// viewer's ADDED events of the phase all come from the one thread that delivered to it (on_added),
-// and no delivery reads another viewer's ping list, so a receiver's op chain is complete, and may be
-// applied, as soon as its own workgroup has delivered (no separate k_ins_apply launch).  Then the
-// members' SYNC collection (no separate k_sync_collect launch).
+// slot of sender sf among the nd listed (wave-uniform result), or -1
+__device__ __forceinline__ int big_find(const uint32_t* snd, uint32_t nd, uint32_t sf, uint32_t lane) {
+  for (uint32_t j0 = 0; j0 < nd; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    const uint64_t hit = __ballot(j < nd && snd[j] == sf);
+    if (hit) return (int)(j0 + (uint32_t)__ffsll((unsigned long long)hit) - 1);
+  }
+  return -1;
+}
+
+// One receiver's big inbox, by one wave.  Canonical order is (sender, slab position), and it needs
+// no comparison sort: k_gossip_emit numbers each (sender, receiver) pair's messages of the round in
+// slab-position order (GMsgFull.pseq, dense: every materialised message reaches the inbox, cross-
+// shard duplicates included, flagged), so rank = base of the sender (senders ascending, bases from
+// their message counts) + pseq.  Lane 0 then runs onGossipReq in that
+// order, 64 messages at a time, after every lane has staged its message in LDS and touched the
+// collector probe and view cell that message's step will read (the serial chain then hits L2).
+// Then the receiver's pingMembers inserts of the phase and its SYNC collection.
+__device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Bufs& b, uint32_t i, uint32_t lane,
+                                          BigLds& L, unsigned long long& nsync) {
+  const uint32_t r = c.lo + i;
+  const uint32_t k = b.msg_cnt[i];
+  const uint32_t start = b.msg_start[i];
+  wave_sync();
+  if (lane == 0) b.msg_cnt[i] = 0;
+  unsigned long long acc = 0;
+  if (c.up[r] && k) {
+    if ((uint64_t)start + k > b.msg_cap) {
+      if (lane == 0) set_err(c, ERR_MSGS);
+    } else {
+      GMsgFull* a = b.msgs_out + start;
+      uint32_t* perm = b.perm + start;
+      // pass 1: distinct senders and their message counts
+      uint32_t nd = 0;
+      bool over = false;
+      for (uint32_t q0 = 0; q0 < k && !over; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const uint32_t f = q < k ? a[q].from : NONE;
+        uint64_t todo = __ballot(q < k);
+        while (todo) {
+          const uint32_t sf = __shfl(f, (int)__ffsll((unsigned long long)todo) - 1, 64);
+          const uint64_t same = __ballot(f == sf) & todo;
+          int slot = big_find(L.snd, nd, sf, lane);
+          if (slot < 0) {
+            if (nd == BIG_MAXD) { over = true; break; }
+            slot = (int)nd;
+            if (lane == 0) { L.snd[nd] = sf; L.cnt[nd] = 0; }
+            nd++;
+          }
+          if (lane == 0) L.cnt[slot] += (uint32_t)__popcll(same);
+          wave_sync();
+          todo &= ~same;
+        }
+      }
+      if (over) {  // more distinct senders than the LDS ranking holds: sort the inbox in place
+        if (lane == 0) sort_msgs(a, k);
+        wave_sync();
+        for (uint32_t q = lane; q < k; q += 64) perm[q] = q;
+      } else {
+        // senders ascending, inbox bases = exclusive prefix of their counts in that order
+        uint32_t ms[2], mc[2], mr[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const uint32_t j = lane + 64u * t;
+          ms[t] = j < nd ? L.snd[j] : NONE;
+          mc[t] = j < nd ? L.cnt[j] : 0u;
+          mr[t] = 0;
+          if (j < nd)
+            for (uint32_t x = 0; x < nd; ++x) mr[t] += L.snd[x] < ms[t] ? 1u : 0u;
+        }
+        wave_sync();
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          if (lane + 64u * t < nd) { L.snd[mr[t]] = ms[t]; L.cnt[mr[t]] = mc[t]; }
+        wave_sync();
+        if (lane == 0) {
+          uint32_t acc0 = 0;
+          for (uint32_t x = 0; x < nd; ++x) { const uint32_t t = L.cnt[x]; L.cnt[x] = acc0; acc0 += t; }
+        }
+        wave_sync();
+        // pass 2: rank = base of the sender + the message's pseq (dense per (sender, receiver))
+        for (uint32_t q0 = 0; q0 < k; q0 += 64) {
+          const uint32_t q = q0 + lane;
+          uint32_t f = NONE, ps = 0;
+          if (q < k) {
+            f = a[q].from;
+            ps = a[q].pseq;
+          }
+          uint64_t todo = __ballot(q < k);
+          while (todo) {
+            const uint32_t sf = __shfl(f, (int)__ffsll((unsigned long long)todo) - 1, 64);
+            const uint64_t same = __ballot(f == sf) & todo;
+            const uint32_t at = L.cnt[big_find(L.snd, nd, sf, lane)] + ps;
+            if (((same >> lane) & 1ull) && at < k) perm[at] = q;
+            todo &= ~same;
+          }
+        }
+      }
+      wave_sync();
+      MemberDev& m = mem(c, r);
+      if (lane == 0) {
+        m.ev_minor = 0;
+        m.fetch_ctr = 0;
+      }
+      GossipDev* slab = slab_of(c, r);
+      const size_t row = (size_t)i * c.n;
+      uint32_t sink = 0;
+      for (uint32_t q0 = 0; q0 < k; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        if (q < k) {
+          uint32_t j = perm[q];
+          if (j >= k) {  // a hole: only after a message-buffer overflow (ERR_MSGS is set)
+            set_err(c, ERR_MSGS);
+            j = q;
+          }
+          const GMsgFull g = a[j];
+          L.m[lane] = g;
+          const CollEnt* e = coll_find(c, r, g.gossiper);
+          sink ^= (e ? e->meta : 1u) ^ c.recs[row + g.subject] ^ c.aux[row + g.subject];
+        }
+        wave_sync();
+        if (lane == 0) {
+          const uint32_t nq = min(64u, k - q0);
+          for (uint32_t t = 0; t < nq; ++t)
+            if (on_gossip_req(c, r, m, slab, L.m[t])) acc++;
+        }
+        wave_sync();
+      }
+      if (sink == 0x5bd1e995u && lane == 63) set_err(c, 0u);  // keeps the warming loads; sets no bit
+    }
+  }
+  apply_ins_batch<64, false>(c, r, lane, L.iP, L.iS, L.iR);
+  if (lane == 0) nsync += sync_collect_member(cs, b, r);  // phase D's SYNC collection for r
+  return acc;
+}
+
+// Gossip delivery (phase C) for the round's inboxes, then the pingMembers inserts of every receiver
+// (a viewer's ADDED events of the phase all come from the one thread / wave that delivered to it),
+// then phase D's SYNC collection of every member, each right after its own deliveries and inserts
+// (nothing else in the gossip phase touches what sync_collect_member reads: the member's own lists,
+// schedule and fd_sync queue).  First the big inboxes, a wave each, grid-stride over k_alloc's list;
+// then each workgroup's blocks of 256 members: small inboxes thread per receiver, their inserts by
+// the workgroup, the collection of members whose inbox was not big.
 __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
   const Ctx c = pctx(P, T);
+  const Ctx cs = pctx_sync(P, T);
   const Bufs b = P->b;
   __shared__ uint64_t s_key[DLV_SORT][DLV_BLOCK];
   __shared__ uint8_t s_ix[DLV_SORT][DLV_BLOCK];
-  __shared__ uint64_t s_bkey[DLV_BLOCK / 64][DLV_BIG];
-  __shared__ uint16_t s_bix[DLV_BLOCK / 64][DLV_BIG];
-  __shared__ uint32_t s_big_r[DLV_BLOCK], s_big_k[DLV_BLOCK], s_big_start[DLV_BLOCK];
-  __shared__ uint32_t s_nbig;
-  if (b.k->msg_total == 0) {  // a round without messages: no receiver has an inbox
-    deliver_collect(P, T);
-    return;
-  }
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) s_nbig = 0;
-  __syncthreads();
-  unsigned long long acc = 0;
-  for (uint32_t i = blockIdx.x * DLV_BLOCK + tid; i < c.nl; i += gridDim.x * DLV_BLOCK) {
-    const uint32_t k = b.msg_cnt[i];
-    if (k == 0) continue;
-    const uint32_t r = c.lo + i;
-    const uint32_t start = b.msg_start[r - c.lo];
-    b.msg_cnt[r - c.lo] = 0;
-    if (!c.up[r]) continue;
-    if ((uint64_t)start + k > b.msg_cap) {  // the message buffer overflowed (ERR_MSGS already set)
-      set_err(c, ERR_MSGS);
-      continue;
-    }
-    GMsgFull* a = b.msgs_out + start;
-    if (k <= (uint32_t)DLV_SORT) {
-      for (uint32_t q = 0; q < k; ++q) {
-        const uint64_t kx = ((uint64_t)a[q].from << 32) | a[q].pos;  // keys are unique
-        int32_t j = (int32_t)q - 1;
-        while (j >= 0 && s_key[j][tid] > kx) {
-          s_key[j + 1][tid] = s_key[j][tid];
-          s_ix[j + 1][tid] = s_ix[j][tid];
-          --j;
-        }
-        s_key[j + 1][tid] = kx;
-        s_ix[j + 1][tid] = (uint8_t)q;
-      }
-      acc += deliver_sorted(c, r, a, k, &s_ix[0][tid], DLV_BLOCK, nullptr);
-      continue;
-    }
-    if (k <= (uint32_t)DLV_BIG) {
-      const uint32_t slot = atomicAdd(&s_nbig, 1u);
-      if (slot < DLV_BLOCK) {
-        s_big_r[slot] = r;
-        s_big_k[slot] = k;
-        s_big_start[slot] = start;
-        continue;
-      }
-    }
-    sort_msgs(a, k);
-    acc += deliver_sorted(c, r, a, k, nullptr, 0, nullptr);
-  }
-  __syncthreads();
-  const uint32_t nbig = min(s_nbig, (uint32_t)DLV_BLOCK);
-  uint64_t* key = s_bkey[wv];
-  uint16_t* ix = s_bix[wv];
-  for (uint32_t bi = wv; bi < nbig; bi += DLV_BLOCK / 64) {
-    const uint32_t r = s_big_r[bi], k = s_big_k[bi];
-    const GMsgFull* a = b.msgs_out + s_big_start[bi];
-    uint32_t P = 64;
-    while (P < k) P <<= 1;
-    for (uint32_t q = lane; q < P; q += 64) {
-      key[q] = q < k ? (((uint64_t)a[q].from << 32) | a[q].pos) : ~0ull;
-      ix[q] = (uint16_t)q;
-    }
-    __syncwarp();
-    for (uint32_t size = 2; size <= P; size <<= 1)
-      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-        for (uint32_t t = lane; t < P / 2; t += 64) {
-          const uint32_t lo = 2 * stride * (t / stride) + (t % stride), hi = lo + stride;
-          const bool asc = (lo & size) == 0;
-          const uint64_t kl = key[lo], kh = key[hi];
-          if ((kl > kh) == asc) {
-            key[lo] = kh; key[hi] = kl;
-            const uint16_t tmp = ix[lo]; ix[lo] = ix[hi]; ix[hi] = tmp;
-          }
-        }
-        __syncwarp();
-      }
-    if (lane == 0) acc += deliver_sorted(c, r, a, k, nullptr, 0, ix);
-    __syncwarp();  // the wave's LDS region is reused by its next receiver
-  }
-  wave_stat_add(c, ST_GOSSIP_ACCEPTED, acc);
+  __shared__ BigLds s_big[DLV_WAVES];
   __shared__ uint32_t s_ins[DLV_BLOCK];
   __shared__ uint32_t s_nins;
+  __shared__ uint32_t s_iP[DLV_BLOCK], s_iS[DLV_BLOCK], s_iR[DLV_BLOCK];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t t32 = (uint32_t)T;
+  const bool any = b.k->msg_total != 0;  // else no receiver has an inbox
+  unsigned long long acc = 0, nsync = 0;
+  if (any) {
+    const uint32_t nbig = b.k->big_cnt;
+    for (uint32_t x = __builtin_amdgcn_readfirstlane(blockIdx.x * DLV_WAVES + wv); x < nbig;
+         x += gridDim.x * DLV_WAVES)
+      acc += deliver_big(c, cs, b, b.big_list[x], lane, s_big[wv], nsync);
+  }
   for (uint32_t base = blockIdx.x * DLV_BLOCK; base < c.nl; base += gridDim.x * DLV_BLOCK) {
-    __syncthreads();  // this workgroup's deliveries (and the previous chunk's inserts) are done
     if (tid == 0) s_nins = 0;
     __syncthreads();
     const uint32_t i = base + tid;
-    if (i < c.nl && c.mem[i].ins_rank != 0) s_ins[atomicAdd(&s_nins, 1u)] = c.lo + i;
+    // a big inbox's receiver is owned by its wave for the whole kernel (big_tick is stable; msg_cnt
+    // is not: the wave zeroes it)
+    const bool big = any && i < c.nl && b.big_tick[i] == t32;
+    if (any && i < c.nl && !big) {
+      const uint32_t k = b.msg_cnt[i];
+      const uint32_t r = c.lo + i;
+      if (k != 0) {
+        b.msg_cnt[i] = 0;
+        const uint32_t start = b.msg_start[i];
+        if (!c.up[r]) {
+        } else if ((uint64_t)start + k > b.msg_cap) {  // the buffer overflowed (ERR_MSGS is set)
+          set_err(c, ERR_MSGS);
+        } else {
+          const GMsgFull* a = b.msgs_out + start;
+          for (uint32_t q = 0; q < k; ++q) {
+            const uint64_t kx = msg_key(a[q]);  // keys are unique
+            int32_t j = (int32_t)q - 1;
+            while (j >= 0 && s_key[j][tid] > kx) {
+              s_key[j + 1][tid] = s_key[j][tid];
+              s_ix[j + 1][tid] = s_ix[j][tid];
+              --j;
+            }
+            s_key[j + 1][tid] = kx;
+            s_ix[j + 1][tid] = (uint8_t)q;
+          }
+          acc += deliver_sorted(c, r, a, k, &s_ix[0][tid], DLV_BLOCK);
+          if (c.mem[i].ins_rank) s_ins[atomicAdd(&s_nins, 1u)] = r;
+        }
+      }
+    }
     __syncthreads();
     const uint32_t nv = s_nins;
-    for (uint32_t q = 0; q < nv; ++q) apply_ins_chain(c, s_ins[q]);
+    for (uint32_t q = 0; q < nv; ++q) apply_ins_batch<DLV_BLOCK, true>(c, s_ins[q], tid, s_iP, s_iS, s_iR);
+    if (i < c.nl && !big) nsync += sync_collect_member(cs, b, c.lo + i);
   }
-  __syncthreads();
-  deliver_collect(P, T);
-}
-
-// ------------------------------------------------------------------------------- list inserts
-// pingMembers.add(nextInt(size), member) (FailureDetectorImpl.java:334-345), in event order: one
-// workgroup per viewer with inserts walks the viewer's op chain; each insert shifts the tail right
-// by one, tail chunk first.
-// The deferred pingMembers.add(nextInt(size), s) ops of viewer v, in event order, by the whole
-// workgroup (tail-first parallel shift); every thread of the block must call it.
-__device__ void apply_ins_chain(const Ctx& c, uint32_t v) {
-  __shared__ uint32_t s_idx, s_s, s_next, s_k;
-  MemberDev& m = mem(c, v);
-  if (threadIdx.x == 0) s_k = m.ins_rank;
-  __syncthreads();
-  const uint32_t k = s_k;
-  uint32_t* pl = ping_list(c, v);
-  uint32_t cur = m.ins_head;
-  for (uint32_t q = 0; q < k; ++q) {
-    const uint32_t size = m.ping_len;
-    if (threadIdx.x == 0) {
-      const InsOp op = c.ins[cur];
-      s_idx = size > 0 ? next_int(draw(c, v, SWIM_STREAM_PING_INSERT, op.phase, op.minor), size) : 0;
-      s_s = op.s;
-      s_next = op.next;
-    }
-    __syncthreads();
-    const uint32_t idx = s_idx;
-    for (int64_t hi = (int64_t)size; hi > (int64_t)idx; hi -= blockDim.x) {
-      int64_t lo = hi - (int64_t)blockDim.x < (int64_t)idx ? (int64_t)idx : hi - (int64_t)blockDim.x;
-      int64_t p = lo + threadIdx.x;
-      uint32_t val = 0;
-      if (p < hi) val = pl[p];
-      __syncthreads();
-      if (p < hi) pl[p + 1] = val;
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      pl[idx] = s_s;
-      m.ping_len = size + 1;
-    }
-    cur = s_next;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) m.ins_rank = 0;
-  __syncthreads();
+  wave_stat_add(c, ST_GOSSIP_ACCEPTED, acc);
+  wave_stat_add(cs, ST_SYNCS, nsync);
 }
 
 
@@ -1103,13 +1268,94 @@ __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Buf
 
 
 // ------------------------------------------------------------------------------- end of tick
+// Boyer-Moore majority merge of two (candidate, count) pairs
+__device__ __forceinline__ void bm_merge(uint32_t& c1, uint32_t& n1, uint32_t c2, uint32_t n2) {
+  if (c1 == c2) n1 += n2;
+  else if (n1 >= n2) n1 -= n2;
+  else { c1 = c2; n1 = n2 - n1; }
+}
+
+// Rebase of the block witness (every kRebaseEvery ticks, inside k_end_tick, when no other kernel
+// runs): for each subject whose record changed in some row since the last rebase, ref moves to the
+// majority record of the live owned rows when that record is held by more live rows than the current
+// ref, and every owned row's block count follows exactly (one pass over the column).  Any ref keeps
+// bdiff exact; the majority only keeps it mostly zero.  Every thread of the grid calls it.
+constexpr int REB_BLOCK = 256;
+__device__ void rebase_witness(const Ctx& c) {
+  __shared__ uint32_t s_list[REB_BLOCK], s_n;
+  __shared__ uint32_t s_c[REB_BLOCK / 64], s_k[REB_BLOCK / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (uint32_t s0 = blockIdx.x * REB_BLOCK; s0 < c.n; s0 += gridDim.x * REB_BLOCK) {
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    const uint32_t sj = s0 + tid;
+    if (sj < c.n && c.dirty[sj]) {
+      c.dirty[sj] = 0u;
+      s_list[atomicAdd(&s_n, 1u)] = sj;
+    }
+    __syncthreads();
+    const uint32_t ns = s_n;
+    for (uint32_t q = 0; q < ns; ++q) {
+      const uint32_t s = s_list[q];
+      const uint32_t rf = c.ref[s];
+      const uint32_t* col = c.recs + s;
+      // pass 1: majority candidate of the live rows
+      uint32_t cand = 0, cnt = 0;
+      for (uint32_t v = tid; v < c.nl; v += REB_BLOCK)
+        if (c.up[c.lo + v]) bm_merge(cand, cnt, col[(size_t)v * c.n], 1u);
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) {
+        const uint32_t c2 = __shfl_xor(cand, d, 64), n2 = __shfl_xor(cnt, d, 64);
+        bm_merge(cand, cnt, c2, n2);
+      }
+      if (lane == 0) { s_c[wv] = cand; s_k[wv] = cnt; }
+      __syncthreads();
+      cand = s_c[0];
+      cnt = s_k[0];
+      for (int w = 1; w < REB_BLOCK / 64; ++w) bm_merge(cand, cnt, s_c[w], s_k[w]);
+      __syncthreads();
+      // pass 2: live rows holding the candidate vs holding ref
+      uint32_t hc = 0, hr = 0;
+      if (cand != rf)
+        for (uint32_t v = tid; v < c.nl; v += REB_BLOCK)
+          if (c.up[c.lo + v]) {
+            const uint32_t x = col[(size_t)v * c.n];
+            hc += x == cand ? 1u : 0u;
+            hr += x == rf ? 1u : 0u;
+          }
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) {
+        hc += __shfl_xor(hc, d, 64);
+        hr += __shfl_xor(hr, d, 64);
+      }
+      if (lane == 0) { s_c[wv] = hc; s_k[wv] = hr; }
+      __syncthreads();
+      hc = hr = 0;
+      for (int w = 0; w < REB_BLOCK / 64; ++w) { hc += s_c[w]; hr += s_k[w]; }
+      __syncthreads();
+      if (cand != rf && hc > hr) {
+        // pass 3: every owned row's count of the subject's block follows the new ref
+        const uint32_t blk = s >> BLK_SHIFT;
+        for (uint32_t v = tid; v < c.nl; v += REB_BLOCK) {
+          const uint32_t x = col[(size_t)v * c.n];
+          const int d = (x != cand ? 1 : 0) - (x != rf ? 1 : 0);
+          if (d) atomicAdd(&c.bdiff[(size_t)v * c.blocks + blk], (uint32_t)d);
+        }
+        if (tid == 0) c.ref[s] = cand;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // start0's doFinally (:285-289) for members that joined this tick; graceful leaves complete.
-__global__ void k_end_tick(KP, uint32_t n_rx_stops) {
+__global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, uint32_t n_rx_stops, int rebase) {
   const Ctx c = pctx(P, T);
   Counters* k = P->b.k;
   Xc* x = P->c.world > 1 ? P->b.x : nullptr;
   const uint32_t* rx_stops = P->b.rx_stops;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (rebase) rebase_witness(c);
   // collector blocks freed this tick become allocatable (one workgroup: the counters are read,
   // then rewritten, by the same threads)
   if (blockIdx.x == 0) {

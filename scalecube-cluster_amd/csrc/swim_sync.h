@@ -9,9 +9,10 @@
 //                    snapshot claims for rows that are both read and merged into in this sub-phase
 //   k_sync_classify  the HBM stream: one wave per (message, 1,024-subject chunk), 16 subjects per
 //                    lane as four 16-B loads of record words per row (content row + receiver row =
-//                    8 B per subject), software-pipelined across units; a record is "complex" unless
-//                    updateMembership would provably do nothing; complex subjects of a chunk are
-//                    block-scan compacted into a pool in subject order
+//                    8 B per subject), units whose two rows both equal the reference row there (the
+//                    exact block witness, Ctx.bdiff) skipped without a row load; a record is
+//                    "complex" unless updateMembership would provably do nothing; complex subjects of
+//                    a chunk are wave-scan compacted into a pool in subject order
 //   k_sync_apply     one workgroup per receiver: lane 0 runs the exact sequential updateMembership on
 //                    the complex subjects in (message, chunk, subject) order, then the ALIVE
 //                    admissions whose metadata fetch succeeded; a later message to a receiver whose
@@ -23,11 +24,12 @@
 #ifndef CLS_SKIPZERO
 #define CLS_SKIPZERO 0  // timing experiment only: skip the stores of empty chunk results (NOT exact)
 #endif
-#ifndef CLS_PIPE
-#define CLS_PIPE 0      // 1: prefetch the wave's next unit while classifying the current one
-#endif
 #ifndef CLS_REV
 #define CLS_REV 1       // SYNC classify also classifies the reverse (SYNC_ACK) direction
+#endif
+#ifndef CLS_WITNESS
+#define CLS_WITNESS 1   // 1: units the block witness proves identical are skipped (0: stream all;
+                        // 2, 3: timing experiments only, NOT exact)
 #endif
 constexpr int SYNC_CHUNK = 1024;                 // subjects per classify unit (one wave)
 constexpr int CLS_BLOCK = 256;
@@ -344,6 +346,8 @@ __global__ void __launch_bounds__(PREP_BLOCK) k_sync_prep(KP, int d2, int copy_s
 struct ClsHdr {
   const uint32_t* content;
   const uint32_t* rv;
+  const uint32_t* bdc;  // block witness of the content row (local content only), else nullptr
+  const uint32_t* bdv;  // block witness of the receiver row
   uint32_t* snapdst;
   uint32_t i, r, s;
   uint32_t rev;  // d2 = 0: 1 = also classify the reverse direction (a local SYNC)
@@ -362,6 +366,8 @@ __device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SubPh
   const bool remote = q.content != NONE;
   h.content = remote ? b.rx_rows + (size_t)q.content * c.n : rec_row(c, q.from);
   h.rv = rec_row(c, q.to);
+  h.bdc = remote ? nullptr : c.bdiff + (size_t)(q.from - c.lo) * c.blocks;
+  h.bdv = c.bdiff + (size_t)(q.to - c.lo) * c.blocks;
   h.snapdst = q.snap < b.snap_cap ? b.snap + (size_t)q.snap * c.n : nullptr;
   h.i = i;
   h.r = q.to;
@@ -442,6 +448,14 @@ __device__ __forceinline__ bool lane_holds(uint32_t subject, uint32_t base, uint
   return off < SYNC_CHUNK && ((off & 255u) >> 2) == lane;
 }
 
+// a viewer's own subject x in the unit starting at base is complex even when both records equal ref
+// there (an identical LEAVING re-runs onSelfMemberDetected, sync_complex)
+__device__ __forceinline__ bool self_complex(const Ctx& c, uint32_t x, uint32_t base) {
+  if (x - base >= (uint32_t)SYNC_CHUNK) return false;
+  const uint32_t rf = c.ref[x];
+  return r_in_table(rf) && r_status(rf) == SWIM_LEAVING;
+}
+
 __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) x += __shfl_down(x, d, 64);
@@ -450,7 +464,10 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
 
 // D2 = 0: the SYNC launch k_sync_classify (streams every message's two rows, both directions);
 // D2 = 1: the SYNC_ACK launch k_ack_classify (reuses the SYNC launch's reverse results, streams only
-// acks whose rows changed).  prof (profiled launches only): {row pairs streamed, complex records}.
+// acks whose rows changed).  A unit whose two rows both equal ref throughout the block (block
+// witness counts 0, Ctx.bdiff) holds identical records and is not streamed: its results are empty
+// (the two self subjects excepted, checked on ref).  prof (profiled launches only): {units streamed,
+// complex records, units in the launch}.
 template <int D2>
 __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint64_t T, unsigned long long* prof) {
   constexpr int d2 = D2;
@@ -462,29 +479,33 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
   const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (CLS_BLOCK / 64) + (threadIdx.x >> 6));
   const uint32_t nw = gridDim.x * (CLS_BLOCK / 64);
   // units are dealt grid-stride (wave w: units w, w + nw, ...); the first header is loaded
-  // speculatively, in parallel with the item count, so a wave's first row loads issue two memory
-  // round trips after launch instead of three
+  // speculatively, in parallel with the item count
   const uint32_t i0 = wid / chunks;
-  ClsHdr hc, hn;
+  ClsHdr hc;
   if (i0 < b.req_cap) cls_hdr(c, b, p, d2, i0, hc, true);
   const uint32_t ni = *p.nitems;
   const uint32_t total = ni * chunks;
-  uint32_t cplx = 0, streamed = 0;
+  uint32_t cplx = 0, streamed = 0, skipped = 0;
   if (wid < total) {
     if (d2) cls_hdr(c, b, p, d2, i0, hc);  // now a valid item: add the SYNC_ACK reuse check
-    uint4 a[CLS_LOADS], o[CLS_LOADS], an[CLS_LOADS], on[CLS_LOADS];
-    if (hc.d1 == NONE || hc.snapdst) cls_rows(c, hc, wid - hc.i * chunks, lane, a, o);
-    hn = hc;
     for (uint32_t u = wid; u < total; u += nw) {
-      const uint32_t ch = u - hc.i * chunks;
-      const uint32_t un = u + nw;
-      const bool more = un < total;
-      if (CLS_PIPE && more) {
-        const uint32_t i2 = un / chunks;
-        if (i2 != hn.i) cls_hdr(c, b, p, d2, i2, hn);
-        if (hn.d1 == NONE || hn.snapdst) cls_rows(c, hn, un - i2 * chunks, lane, an, on);
-      }
+      const uint32_t i = u / chunks;
+      if (i != hc.i) cls_hdr(c, b, p, d2, i, hc);
+      const uint32_t ch = u - i * chunks;
       const uint32_t base = ch * SYNC_CHUNK;
+      if (CLS_WITNESS && hc.d1 == NONE && !hc.snapdst && hc.bdc) {
+        const uint32_t dc = CLS_WITNESS == 3 ? 0u : uni(hc.bdc[ch]), dv = CLS_WITNESS == 3 ? 0u : uni(hc.bdv[ch]);
+        if ((dc | dv) == 0 && !self_complex(c, hc.r, base) && !(hc.rev && self_complex(c, hc.s, base))) {
+          if (lane == 0 && CLS_WITNESS != 2) {
+            b.item_chunk[(size_t)hc.i * chunks + ch] = make_uint2(0, 0);
+            if (hc.rev) b.rev_chunk[(size_t)hc.i * chunks + ch] = make_uint2(0, 0);
+          }
+          ++skipped;
+          continue;
+        }
+      }
+      uint4 a[CLS_LOADS], o[CLS_LOADS];
+      if (hc.d1 == NONE || hc.snapdst) cls_rows(c, hc, ch, lane, a, o);
       if (hc.snapdst) {
 #pragma unroll
         for (int j = 0; j < CLS_LOADS; ++j) {
@@ -506,68 +527,60 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
             cplx += t;
           }
         }
-      } else {
-        if (lane == 0 && ch == 0) ++streamed;
-        uint32_t flags = 0, rflags = 0;
-        uint32_t diff = 0;
+        continue;
+      }
+      ++streamed;
+      uint32_t flags = 0, rflags = 0;
+      uint32_t diff = 0;
 #pragma unroll
-        for (int j = 0; j < CLS_LOADS; ++j)
-          diff |= (a[j].x ^ o[j].x) | (a[j].y ^ o[j].y) | (a[j].z ^ o[j].z) | (a[j].w ^ o[j].w);
-        // identical records never change the row (isOverrides(equal) is false and an identical
-        // LEAVING over LEAVING is a no-op) except on the viewer's own subject: the fast path of a
-        // converged cluster, where nearly every lane of nearly every unit compares equal
-        const bool self_here = lane_holds(hc.r, base, lane);
-        const bool rself_here = hc.rev && lane_holds(hc.s, base, lane);
-        if (diff != 0 || self_here || rself_here) {
+      for (int j = 0; j < CLS_LOADS; ++j)
+        diff |= (a[j].x ^ o[j].x) | (a[j].y ^ o[j].y) | (a[j].z ^ o[j].z) | (a[j].w ^ o[j].w);
+      // identical records never change the row (isOverrides(equal) is false and an identical
+      // LEAVING over LEAVING is a no-op) except on the viewer's own subject
+      const bool self_here = lane_holds(hc.r, base, lane);
+      const bool rself_here = hc.rev && lane_holds(hc.s, base, lane);
+      if (diff != 0 || self_here || rself_here) {
 #pragma unroll
-          for (int j = 0; j < CLS_LOADS; ++j) {
-            const uint32_t x = base + j * 256 + 4 * lane;
-            const uint32_t av[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
-            const uint32_t ov[4] = {o[j].x, o[j].y, o[j].z, o[j].w};
+        for (int j = 0; j < CLS_LOADS; ++j) {
+          const uint32_t x = base + j * 256 + 4 * lane;
+          const uint32_t av[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
+          const uint32_t ov[4] = {o[j].x, o[j].y, o[j].z, o[j].w};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              if (r_in_table(av[q]) && sync_complex(av[q], ov[q], x + q == hc.r)) flags |= 1u << (4 * j + q);
-              if (hc.rev && r_in_table(ov[q]) && sync_complex(ov[q], av[q], x + q == hc.s))
-                rflags |= 1u << (4 * j + q);
-            }
-          }
-        }
-        const uint2 res = cls_compact(c, b, flags, base, lane);
-        if (lane == 0 && (!CLS_SKIPZERO || res.y)) {
-          b.item_chunk[(size_t)hc.i * chunks + ch] = res;
-          if (res.y) atomicAdd(&b.item_total[hc.i], res.y);
-        }
-        cplx += res.y;
-        if (hc.rev) {
-          const uint2 rres = cls_compact(c, b, rflags, base, lane);
-          if (lane == 0 && (!CLS_SKIPZERO || rres.y)) {
-            b.rev_chunk[(size_t)hc.i * chunks + ch] = rres;
-            if (rres.y) atomicAdd(&b.rev_total[hc.i], rres.y);
+          for (int q = 0; q < 4; ++q) {
+            if (r_in_table(av[q]) && sync_complex(av[q], ov[q], x + q == hc.r)) flags |= 1u << (4 * j + q);
+            if (hc.rev && r_in_table(ov[q]) && sync_complex(ov[q], av[q], x + q == hc.s))
+              rflags |= 1u << (4 * j + q);
           }
         }
       }
-      if (more) {
-        if (CLS_PIPE) {
-          hc = hn;
-#pragma unroll
-          for (int j = 0; j < CLS_LOADS; ++j) { a[j] = an[j]; o[j] = on[j]; }
-        } else {
-          const uint32_t i2 = un / chunks;
-          if (i2 != hc.i) cls_hdr(c, b, p, d2, i2, hc);
-          if (hc.d1 == NONE || hc.snapdst) cls_rows(c, hc, un - i2 * chunks, lane, a, o);
+      const uint2 res = cls_compact(c, b, flags, base, lane);
+      if (lane == 0 && (!CLS_SKIPZERO || res.y)) {
+        b.item_chunk[(size_t)hc.i * chunks + ch] = res;
+        if (res.y) atomicAdd(&b.item_total[hc.i], res.y);
+      }
+      cplx += res.y;
+      if (hc.rev) {
+        const uint2 rres = cls_compact(c, b, rflags, base, lane);
+        if (lane == 0 && (!CLS_SKIPZERO || rres.y)) {
+          b.rev_chunk[(size_t)hc.i * chunks + ch] = rres;
+          if (rres.y) atomicAdd(&b.rev_total[hc.i], rres.y);
         }
       }
     }
   }
-  // the message record counts (sync_records) are taken from the headers by k_sync_apply
+  // the message record counts (sync_records) are taken from the headers by k_sync_apply; only
+  // non-zero counts are added (thousands of waves skip every unit: one atomic each on the same
+  // address would serialise the launch), the unit total is stored once
+  (void)skipped;
   if (lane == 0 && (cplx || streamed)) {
     if (cplx) stat_add(c, ST_MERGE_RECORDS, cplx);
     if (streamed) stat_add(c, ST_MERGE_MSGS, streamed);
     if (prof) {
-      atomicAdd(prof, (unsigned long long)streamed);
-      atomicAdd(prof + 1, (unsigned long long)cplx);
+      if (streamed) atomicAdd(prof, (unsigned long long)streamed);
+      if (cplx) atomicAdd(prof + 1, (unsigned long long)cplx);
     }
   }
+  if (prof && wid == 0 && lane == 0) prof[2] = total;
 }
 
 __global__ void __launch_bounds__(CLS_BLOCK, CLS_MINWAVES) k_sync_classify(KP, unsigned long long* prof) {
@@ -643,6 +656,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
   __shared__ uint32_t s_wave[APPLY_BLOCK / 64 + 1];
   __shared__ uint32_t s_mod;
   __shared__ unsigned long long s_recs;
+  __shared__ uint32_t s_iP[APPLY_BLOCK], s_iS[APPLY_BLOCK], s_iR[APPLY_BLOCK];
   const SubPhase p = sub_phase(b, d2);
   const uint32_t phase = d2 ? SWIM_PHASE_SYNCACK : SWIM_PHASE_SYNC;
   const uint32_t chunks = b.chunks;
@@ -718,6 +732,6 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
     }
     __syncthreads();
     // this sub-phase's pingMembers inserts of s (its ADDED events, all made by this workgroup)
-    apply_ins_chain(c, s);
+    apply_ins_batch<APPLY_BLOCK, true>(c, s, threadIdx.x, s_iP, s_iS, s_iR);
   }
 }

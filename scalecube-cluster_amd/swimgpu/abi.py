@@ -65,7 +65,8 @@ class swim_config(C.Structure):
         ("timer_capacity", C.c_uint32),
         ("message_capacity", C.c_uint32),
         ("interval_capacity", C.c_uint32),
-        ("reserved", C.c_uint32 * 2),
+        ("deliver_wave_min", C.c_uint32),
+        ("reserved", C.c_uint32 * 1),
     ]
 
 

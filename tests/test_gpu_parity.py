@@ -137,3 +137,10 @@ def test_gpu_matches_golden_digest(glib, sc, shards):
     assert event_digest(ev) == want["events_sha256"] and len(ev) == want["events"]
     assert {k: int(st[k]) for k in want["stats"]} == want["stats"]
     assert got_state == want["state_sha256"]
+
+
+# ---- the wave-parallel delivery path (deliver_big: stable-by-sender canonical ranking, wave-batched
+# pingMembers inserts) for EVERY gossip inbox, not only the big ones of a storm
+@pytest.mark.parametrize("sc", scenarios.catalog(), ids=lambda s: s.name)
+def test_gpu_parity_wave_delivery(glib, olib, sc):
+    _run_parity(glib, olib, dataclasses.replace(sc, cfg={**sc.cfg, "deliver_wave_min": 1}))

@@ -1,8 +1,15 @@
 #!/usr/bin/env bash
-mkdir -p gpurun_out
-for n in 4096 16384; do
-  timeout -k 10 240 python -u bench.py --workload churn --members $n --steps 6 --warmup 2 --progress --no-cpu-baseline > gpurun_out/churn_$n.log 2>&1
-  rc=$?
-  echo "n=$n rc=$rc"; tail -4 gpurun_out/churn_$n.log
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-done
+# config-3 churn probe on the GPU box: per-period progress + rocprofv3 kernel stats at reduced N
+set -uo pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/prof
+n=${N:-4096}
+steps=${STEPS:-8}
+gcap=${GCAP:-524288}
+tag=${TAG:-r02_churn$n}
+timeout -k 10 ${TLIM:-420} rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof/${tag}_stats -o run \
+  -- python3 -u bench.py --workload churn --members $n --steps $steps --warmup 2 --progress --no-cpu-baseline \
+     --gossip-capacity $gcap > gpurun_out/${tag}.log 2>&1
+rc=$?
+echo "n=$n rc=$rc"; tail -3 gpurun_out/${tag}.log
+exit $rc
