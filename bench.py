@@ -15,7 +15,7 @@ the RCCL bootstrap id and brackets the timed region with barriers.
 
 Prints ONE JSON line with `value` (whole-job member-periods/s), the `roofline` object of the
 dominant kernel (k_sync_classify, the SYNC record classification; HIP events on the engine's stream) and the
-`cpu_baseline` (the CPU oracle, 1 thread, bounded sample, rank 0 / N=1 only).
+`cpu_baseline` (the CPU oracle on all of the box's cores and on 1 thread, 10 periods, rank 0 / N=1 only).
 """
 import argparse
 import json
@@ -128,28 +128,48 @@ def pmc_traffic(kernel, workload):
     return k["hbm_bytes_per_launch"], os.path.relpath(paths[-1], REPO)
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(n, periods):
-    """The CPU oracle (oracle/liboracle_swim.so, 1 thread for the timed ticks) on the same N and
-    workload, bounded to `periods` periods from the converged start."""
+    """The CPU oracle (oracle/liboracle_swim.so, the C++ lockstep restatement) on the same N and
+    workload from the converged start, bounded to `periods` periods: once with 1 thread and once
+    multi-threaded over members (std::thread workers over member ranges in every phase; identical
+    results, tests/test_golden.py).  The all-core figure is `value`."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     from swimgpu import abi
     lib = oracle.lib()
-    cfg = abi.default_config(lib, 0, sync_stagger=1, record_fd_events=0)
-    sch = Schedule(WORKLOAD, n, periods)
-    e = abi.Engine(lib, cfg, sch.capacity, n, 1)
-    sch.setup(e)
-    t0 = time.perf_counter()
-    sch.run(e, 0, periods)
-    dt = time.perf_counter() - t0
-    e.close()
+    # the box's CPU share: OMP_NUM_THREADS is set to it there (os.cpu_count() is the whole machine)
+    all_cores = max(1, min(64, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)))
+    legs = {}
+    for threads in (1, all_cores):
+        cfg = abi.default_config(lib, 0, sync_stagger=1, record_fd_events=0)
+        sch = Schedule(WORKLOAD, n, periods)
+        e = abi.Engine(lib, cfg, sch.capacity, n, 1)
+        oracle.set_threads(e, threads)
+        sch.setup(e)
+        t0 = time.perf_counter()
+        sch.run(e, 0, periods)
+        legs[threads] = time.perf_counter() - t0
+        e.close()
     note = ""
     if WORKLOAD != "quiet":  # the GPU's timed periods come later in the same schedule
         note = ("; NOT the GPU's timed work: this workload's per-period volume grows after these first periods "
                 "(kills, gossip storms), so compare member-periods/s of the same periods only")
-    return {"value": n * periods / dt, "unit": "member-periods/s", "cores": 1, "kind": "port",
-            "sample": f"CPU oracle (C++ lockstep restatement, 1 thread), N={n}, LAN defaults, workload {WORKLOAD}, "
-                      f"periods 0..{periods} from the converged start ({dt:.1f} s){note}"}
+    dt1, dtn = legs[1], legs[all_cores]
+    return {"value": n * periods / dtn, "unit": "member-periods/s", "cores": all_cores, "kind": "port",
+            "single_thread_value": n * periods / dt1, "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": f"CPU oracle (C++ lockstep restatement), N={n}, LAN defaults, workload {WORKLOAD}, "
+                      f"periods 0..{periods} from the converged start: {dtn:.1f} s on {all_cores} threads, "
+                      f"{dt1:.1f} s on 1 thread{note}"}
 
 
 def main():
@@ -158,7 +178,7 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--members", type=int, default=None, help="default: 65,536 (16,384 for churn)")
-    ap.add_argument("--cpu-periods", type=int, default=2)
+    ap.add_argument("--cpu-periods", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--progress", action="store_true", help="print a stderr line after every period")
     ap.add_argument("--workload", choices=("quiet", "failures", "churn"), default="quiet")

@@ -37,6 +37,17 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+def set_threads(e: abi.Engine, threads: int) -> None:
+    """Worker threads of the oracle's per-member phase loops (swim_oracle_set_threads, oracle only;
+    0 = hardware concurrency).  Results are identical for every thread count."""
+    fn = e.lib.swim_oracle_set_threads
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    fn.restype = ctypes.c_int32
+    rc = fn(e._h, int(threads))
+    if rc != 0:
+        raise abi.SwimError("swim_oracle_set_threads", rc)
+
+
 def engine(cfg=None, capacity=16, n_initial=None, seed=1, **overrides) -> abi.Engine:
     L = lib()
     if cfg is None:

@@ -145,6 +145,22 @@ struct Member {
   uint64_t g_period = 0, g_counter = 0, period_used = 0;
   std::unordered_map<uint32_t, SeqCollector> collectors;
   std::vector<GossipState> gossips;  // insertion order == canonical order
+  std::unordered_map<uint64_t, uint32_t> gidx;  // gossips.get(gossipId): id -> position (HashMap lookup)
+  static uint64_t gkey(uint32_t gossiper, uint64_t seq) { return ((uint64_t)gossiper << 40) ^ seq; }
+  GossipState* find_gossip(uint32_t gossiper, uint64_t seq) {
+    auto it = gidx.find(gkey(gossiper, seq));
+    if (it == gidx.end()) return nullptr;
+    GossipState& g = gossips[it->second];
+    return (g.gossiper == gossiper && g.seq == seq) ? &g : nullptr;
+  }
+  void add_gossip(const GossipState& g) {
+    gidx[gkey(g.gossiper, g.seq)] = (uint32_t)gossips.size();
+    gossips.push_back(g);
+  }
+  void reindex_gossips() {
+    gidx.clear();
+    for (uint32_t i = 0; i < gossips.size(); ++i) gidx[gkey(gossips[i].gossiper, gossips[i].seq)] = i;
+  }
   std::vector<uint32_t> remote;
   int32_t remote_index = -1;
   // ---- MembershipProtocolImpl: table / members / aliveEmittedSet / metadata / timers live in
@@ -187,6 +203,17 @@ struct PendingAlive {
   Record r1;
 };
 
+// Side effects a worker thread of a parallel phase region collects instead of writing the engine's
+// shared stats / event list / timer queue; merged in thread order after the region (the CPU
+// baseline's multi-threaded mode, swim_oracle_set_threads).  Every other write of a phase touches
+// only the state of the member the worker owns in that phase.
+struct Acc {
+  swim_stats st{};
+  std::vector<swim_event> ev;
+  std::vector<std::pair<uint64_t, std::pair<uint32_t, uint32_t>>> timers;
+};
+thread_local Acc* tl_acc = nullptr;
+
 }  // namespace
 
 struct swim_engine {
@@ -210,6 +237,40 @@ struct swim_engine {
   std::map<uint64_t, std::vector<std::pair<uint32_t, uint32_t>>> timer_queue;
   std::vector<swim_event> events;
   swim_stats st{};
+  uint32_t threads = 1;  // worker threads of the per-member phase loops (1 = the plain sequential loops)
+
+  swim_stats& STT() { return tl_acc ? tl_acc->st : st; }
+
+  // fn(a, b, t) over [lo, hi) split into `threads` contiguous ranges (t = range index), one
+  // std::thread each, then the workers' side effects merged in range order
+  template <class F>
+  void par(uint32_t lo, uint32_t hi, F&& fn) {
+    const uint32_t nt = threads;
+    if (nt <= 1 || hi - lo < 2 * nt) {
+      fn(lo, hi, 0u);
+      return;
+    }
+    std::vector<Acc> acc(nt);
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    for (uint32_t t = 0; t < nt; ++t) {
+      const uint32_t a = lo + (uint32_t)((uint64_t)(hi - lo) * t / nt);
+      const uint32_t b = lo + (uint32_t)((uint64_t)(hi - lo) * (t + 1) / nt);
+      th.emplace_back([&, a, b, t] {
+        tl_acc = &acc[t];
+        fn(a, b, t);
+        tl_acc = nullptr;
+      });
+    }
+    for (auto& x : th) x.join();
+    for (auto& a : acc) {
+      uint64_t* d = reinterpret_cast<uint64_t*>(&st);
+      const uint64_t* x = reinterpret_cast<const uint64_t*>(&a.st);
+      for (size_t i = 0; i < sizeof(swim_stats) / 8; ++i) d[i] += x[i];
+      events.insert(events.end(), a.ev.begin(), a.ev.end());
+      for (auto& tq : a.timers) timer_queue[tq.first].push_back(tq.second);
+    }
+  }
 
   // ------------------------------------------------------------------------- RNG
   uint32_t draw(uint32_t member, uint32_t stream, uint32_t sub24, uint32_t sub32, uint64_t tick) const {
@@ -249,8 +310,8 @@ struct swim_engine {
     e.type = type;
     e.phase = phase;
     e.minor = minor;
-    events.push_back(e);
-    st.events++;
+    if (tl_acc) tl_acc->ev.push_back(e); else events.push_back(e);
+    STT().events++;
   }
   uint32_t next_minor(uint32_t v) { return m[v].ev_minor++; }
 
@@ -290,9 +351,9 @@ struct swim_engine {
     g.seq = mv.g_counter++;
     g.rec = r;
     g.infection_period = mv.g_period;
-    mv.gossips.push_back(g);
+    mv.add_gossip(g);
     mv.collectors[v].add((int64_t)g.seq);
-    st.gossips_created++;
+    STT().gossips_created++;
   }
 
   // ------------------------------------------------------------------------- timers
@@ -303,7 +364,7 @@ struct swim_engine {
     int64_t ms = swim_suspicion_timeout(cfg.suspicion_mult, (int32_t)m[v].table_size, cfg.ping_interval);
     uint64_t deadline = T + (uint64_t)(ms / tick_ms);
     c = c_with_deadline(c | B_HAS_TIMER, deadline);
-    timer_queue[deadline].push_back({v, s});
+    if (tl_acc) tl_acc->timers.push_back({deadline, {v, s}}); else timer_queue[deadline].push_back({v, s});
   }
   // cancelSuspicionTimeoutTask (:797-803)
   void cancel_timer(uint32_t v, uint32_t s) { m[v].row[s] &= ~B_HAS_TIMER; }
@@ -314,9 +375,9 @@ struct swim_engine {
     uint32_t f = m[v].fetch_ctr++;
     uint32_t w1 = draw(v, SWIM_STREAM_FETCH_REQ, phase, f);
     uint32_t w2 = draw(v, SWIM_STREAM_FETCH_RESP, phase, f);
-    st.fetches++;
+    STT().fetches++;
     bool ok = !out_fail(v, s, w1) && in_pass(s, v) && !out_fail(s, v, w2) && in_pass(v, s);
-    if (ok) st.fetch_ok++;
+    if (ok) STT().fetch_ok++;
     return ok;
   }
 
@@ -421,25 +482,29 @@ struct swim_engine {
     timer_queue.erase(it);
     std::sort(due.begin(), due.end());
     due.erase(std::unique(due.begin(), due.end()), due.end());
-    std::vector<PendingAlive> none;
-    for (auto& vs : due) {
-      uint32_t v = vs.first, s = vs.second;
-      if (!m[v].up) continue;
-      uint64_t& c = m[v].row[s];
-      if (!c_has(c, B_HAS_TIMER) || c_deadline(c) != (uint32_t)(T & SWIM_DEADLINE_MASK)) continue;
-      c &= ~B_HAS_TIMER;
-      st.timers_fired++;
-      if (c_has(c, B_IN_TABLE)) {
-        Record dead{s, SWIM_DEAD, c_inc(c)};
-        update_membership(v, dead, SUSPICION_TIMEOUT, SWIM_PHASE_TIMERS, none);
+    // a worker owns the viewers of its range: their due entries are one stretch of the sorted list
+    par(0, n, [&](uint32_t va, uint32_t vb, uint32_t) {
+      std::vector<PendingAlive> none;
+      auto it = std::lower_bound(due.begin(), due.end(), std::make_pair(va, 0u));
+      for (; it != due.end() && it->first < vb; ++it) {
+        uint32_t v = it->first, s = it->second;
+        if (!m[v].up) continue;
+        uint64_t& c = m[v].row[s];
+        if (!c_has(c, B_HAS_TIMER) || c_deadline(c) != (uint32_t)(T & SWIM_DEADLINE_MASK)) continue;
+        c &= ~B_HAS_TIMER;
+        STT().timers_fired++;
+        if (c_has(c, B_IN_TABLE)) {
+          Record dead{s, SWIM_DEAD, c_inc(c)};
+          update_membership(v, dead, SUSPICION_TIMEOUT, SWIM_PHASE_TIMERS, none);
+        }
       }
-    }
+    });
   }
 
   // ------------------------------------------------------------------------- phase B: FD
   // publishPingResult (:377-380) -> MembershipProtocolImpl.onFailureDetectorEvent (:418-449)
   void publish_fd(uint32_t v, uint32_t t, uint32_t status) {
-    st.fd_events++;
+    STT().fd_events++;
     if (cfg.record_fd_events)
       emit(v, t, SWIM_EV_FD_ALIVE + (status == SWIM_ALIVE ? 0 : status == SWIM_SUSPECT ? 1 : 2),
            SWIM_PHASE_FD, next_minor(v));
@@ -515,7 +580,7 @@ struct swim_engine {
       publish_fd(v, t, SWIM_SUSPECT);
       return;
     }
-    st.ping_reqs++;
+    STT().ping_reqs++;
     std::vector<uint32_t> pending;
     for (uint32_t j = 0; j < relays.size(); ++j) {
       if (out_fail(v, relays[j], draw(v, SWIM_STREAM_PINGREQ_OUT, j, 0)))
@@ -555,7 +620,10 @@ struct swim_engine {
   }
 
   void phase_fd() {
-    for (uint32_t v = 0; v < n; ++v) {
+    par(0, n, [&](uint32_t va, uint32_t vb, uint32_t) { phase_fd_range(va, vb); });
+  }
+  void phase_fd_range(uint32_t va, uint32_t vb) {
+    for (uint32_t v = va; v < vb; ++v) {
       Member& mv = m[v];
       if (!mv.up) continue;
       mv.ev_minor = 0;
@@ -573,7 +641,7 @@ struct swim_engine {
         mv.fd_period++;
         uint32_t t = select_ping_member(v);
         if (t == NONE) continue;
-        st.pings++;
+        STT().pings++;
         if (out_fail(v, t, draw(v, SWIM_STREAM_PING_OUT, 0, 0))) {
           ping_req(v, t);  // outbound error -> ping-req right away
         } else if (in_pass(t, v) && !out_fail(t, v, draw(v, SWIM_STREAM_ACK_OUT, 0, 0)) && in_pass(v, t)) {
@@ -611,87 +679,106 @@ struct swim_engine {
     for (uint32_t v = 0; v < n; ++v)
       if (gossip_due(m[v])) due.push_back(v);
     if (due.empty()) return;
+    const uint32_t nd = (uint32_t)due.size();
     // C1: period++ and checkGossipSegmentation (:141-146, :217-236)
-    for (uint32_t v : due) {
-      Member& mv = m[v];
-      mv.period_used = mv.g_period++;
-      for (auto& kv : mv.collectors)
-        if (kv.second.size() > (size_t)cfg.gossip_segmentation_threshold) kv.second.clear();
-    }
-    // C2: spread to selected members, sweep, complete futures (:148-183)
-    std::vector<GMsg> msgs;
-    for (uint32_t v : due) {
-      Member& mv = m[v];
-      if (mv.gossips.empty()) continue;
-      const uint64_t period = mv.period_used;
-      std::vector<uint32_t> targets = select_gossip_members(v);
-      const int32_t size1 = (int32_t)mv.remote.size() + 1;
-      const uint64_t spread = (uint64_t)swim_gossip_periods_to_spread(cfg.gossip_repeat_mult, size1);
-      const uint64_t sweep = (uint64_t)swim_gossip_periods_to_sweep(cfg.gossip_repeat_mult, size1);
-      for (uint32_t j = 0; j < targets.size(); ++j) {
-        uint32_t t = targets[j];
-        for (uint32_t p = 0; p < mv.gossips.size(); ++p) {  // selectGossipsToSend (:311-320)
-          const GossipState& g = mv.gossips[p];
-          if (!(g.infection_period + spread >= period)) continue;
-          if (g.is_infected(t)) continue;
-          st.gossip_messages++;
-          if (out_fail(v, t, draw(v, SWIM_STREAM_GOSSIP_OUT, j, p))) continue;
-          if (!in_pass(t, v)) continue;
-          msgs.push_back(GMsg{t, v, p, g});
+    par(0, nd, [&](uint32_t a, uint32_t b, uint32_t) {
+      for (uint32_t i = a; i < b; ++i) {
+        Member& mv = m[due[i]];
+        mv.period_used = mv.g_period++;
+        for (auto& kv : mv.collectors)
+          if (kv.second.size() > (size_t)cfg.gossip_segmentation_threshold) kv.second.clear();
+      }
+    });
+    // C2: spread to selected members, sweep, complete futures (:148-183).  Messages are bucketed by
+    // the receiver range of the C3 worker that delivers them ([producer][consumer]).
+    const uint32_t nt = std::max(1u, threads);
+    std::vector<uint32_t> rb(nt + 1);
+    for (uint32_t t = 0; t <= nt; ++t) rb[t] = (uint32_t)((uint64_t)n * t / nt);
+    auto consumer = [&](uint32_t to) { return (uint32_t)(std::upper_bound(rb.begin(), rb.end(), to) - rb.begin()) - 1; };
+    std::vector<std::vector<std::vector<GMsg>>> bucket(nt, std::vector<std::vector<GMsg>>(nt));
+    bool any = false;
+    par(0, nd, [&](uint32_t a, uint32_t b, uint32_t t) {
+      for (uint32_t i = a; i < b; ++i) {
+        const uint32_t v = due[i];
+        Member& mv = m[v];
+        if (mv.gossips.empty()) continue;
+        const uint64_t period = mv.period_used;
+        std::vector<uint32_t> targets = select_gossip_members(v);
+        const int32_t size1 = (int32_t)mv.remote.size() + 1;
+        const uint64_t spread = (uint64_t)swim_gossip_periods_to_spread(cfg.gossip_repeat_mult, size1);
+        const uint64_t sweep = (uint64_t)swim_gossip_periods_to_sweep(cfg.gossip_repeat_mult, size1);
+        for (uint32_t j = 0; j < targets.size(); ++j) {
+          uint32_t tg = targets[j];
+          for (uint32_t p = 0; p < mv.gossips.size(); ++p) {  // selectGossipsToSend (:311-320)
+            const GossipState& g = mv.gossips[p];
+            if (!(g.infection_period + spread >= period)) continue;
+            if (g.is_infected(tg)) continue;
+            STT().gossip_messages++;
+            if (out_fail(v, tg, draw(v, SWIM_STREAM_GOSSIP_OUT, j, p))) continue;
+            if (!in_pass(tg, v)) continue;
+            bucket[t][consumer(tg)].push_back(GMsg{tg, v, p, g});
+          }
+        }
+        // sweep (:158-164, :350-358)
+        std::vector<GossipState> keep;
+        keep.reserve(mv.gossips.size());
+        for (auto& g : mv.gossips)
+          if (!(period > g.infection_period + sweep)) keep.push_back(std::move(g));
+        mv.gossips.swap(keep);
+        mv.reindex_gossips();
+        // futures (:167-180, :360-368): only the graceful-leave future has an observer here
+        if (mv.leave_pending) {
+          for (auto& g : mv.gossips)
+            if (period > g.infection_period + spread && g.gossiper == mv.leave_gossiper && g.seq == mv.leave_seq)
+              mv.leave_done = true;
         }
       }
-      // sweep (:158-164, :350-358)
-      std::vector<GossipState> keep;
-      keep.reserve(mv.gossips.size());
-      for (auto& g : mv.gossips)
-        if (!(period > g.infection_period + sweep)) keep.push_back(std::move(g));
-      mv.gossips.swap(keep);
-      // futures (:167-180, :360-368): only the graceful-leave future has an observer here
-      if (mv.leave_pending) {
-        for (auto& g : mv.gossips)
-          if (period > g.infection_period + spread && g.gossiper == mv.leave_gossiper && g.seq == mv.leave_seq)
-            mv.leave_done = true;
-      }
-    }
-    if (msgs.empty()) return;
-    // C3: onGossipReq at every receiver, canonical order (sender, slab position) (:201-215)
-    std::stable_sort(msgs.begin(), msgs.end(), [](const GMsg& a, const GMsg& b) {
-      if (a.to != b.to) return a.to < b.to;
-      if (a.from != b.from) return a.from < b.from;
-      return a.pos < b.pos;
     });
-    uint32_t cur = NONE;
-    std::vector<PendingAlive> pending;
-    for (auto& msg : msgs) {
-      const uint32_t r = msg.to;
-      Member& mr = m[r];
-      if (r != cur) {
-        cur = r;
-        mr.ev_minor = 0;
-        mr.fetch_ctr = 0;
+    for (auto& bp : bucket)
+      for (auto& bc : bp) any |= !bc.empty();
+    if (!any) return;
+    // C3: onGossipReq at every receiver, canonical order (sender, slab position) (:201-215)
+    par(0, n, [&](uint32_t ra, uint32_t rbnd, uint32_t) {
+      std::vector<GMsg> msgs;
+      for (uint32_t d = 0; d < nt; ++d)
+        if (rb[d] >= ra && rb[d + 1] <= rbnd)
+          for (uint32_t pr = 0; pr < nt; ++pr) msgs.insert(msgs.end(), bucket[pr][d].begin(), bucket[pr][d].end());
+      std::sort(msgs.begin(), msgs.end(), [](const GMsg& a, const GMsg& b) {  // keys are unique
+        if (a.to != b.to) return a.to < b.to;
+        if (a.from != b.from) return a.from < b.from;
+        return a.pos < b.pos;
+      });
+      uint32_t cur = NONE;
+      std::vector<PendingAlive> pending;
+      for (auto& msg : msgs) {
+        const uint32_t r = msg.to;
+        Member& mr = m[r];
+        if (r != cur) {
+          cur = r;
+          mr.ev_minor = 0;
+          mr.fetch_ctr = 0;
+        }
+        if (!mr.up) continue;
+        const GossipState& g = msg.g;
+        if (!mr.collectors[g.gossiper].add((int64_t)g.seq)) continue;
+        STT().gossip_accepted++;
+        GossipState* state = mr.find_gossip(g.gossiper, g.seq);  // gossips.get(gossipId) (:206)
+        if (state == nullptr) {
+          GossipState ns;
+          ns.gossiper = g.gossiper;
+          ns.seq = g.seq;
+          ns.rec = g.rec;
+          ns.infection_period = mr.g_period;
+          ns.infected.push_back(msg.from);
+          mr.add_gossip(ns);
+          // onMembershipGossip (:452-459)
+          update_membership(r, g.rec, MEMBERSHIP_GOSSIP, SWIM_PHASE_GOSSIP, pending);
+          flush_pending(r, pending, MEMBERSHIP_GOSSIP, SWIM_PHASE_GOSSIP);
+        } else {
+          state->add_infected(msg.from);
+        }
       }
-      if (!mr.up) continue;
-      const GossipState& g = msg.g;
-      if (!mr.collectors[g.gossiper].add((int64_t)g.seq)) continue;
-      st.gossip_accepted++;
-      GossipState* state = nullptr;
-      for (auto& x : mr.gossips)
-        if (x.gossiper == g.gossiper && x.seq == g.seq) { state = &x; break; }
-      if (state == nullptr) {
-        GossipState ns;
-        ns.gossiper = g.gossiper;
-        ns.seq = g.seq;
-        ns.rec = g.rec;
-        ns.infection_period = mr.g_period;
-        ns.infected.push_back(msg.from);
-        mr.gossips.push_back(ns);
-        // onMembershipGossip (:452-459)
-        update_membership(r, g.rec, MEMBERSHIP_GOSSIP, SWIM_PHASE_GOSSIP, pending);
-        flush_pending(r, pending, MEMBERSHIP_GOSSIP, SWIM_PHASE_GOSSIP);
-      } else {
-        state->add_infected(msg.from);
-      }
-    }
+    });
   }
 
   // ------------------------------------------------------------------------- phase D: SYNC
@@ -719,41 +806,54 @@ struct swim_engine {
     for (uint32_t x = 0; x < n; ++x) {
       uint64_t c = content[x];
       if (!c_has(c, B_IN_TABLE)) continue;
-      st.sync_records++;
+      STT().sync_records++;
       update_membership(v, Record{x, c_status(c), c_inc(c)}, reason, phase, pending);
     }
     flush_pending(v, pending, reason, phase);
   }
 
   void phase_sync() {
+    const uint32_t nt = std::max(1u, threads);
+    std::vector<std::vector<SyncReq>> rq(nt);
+    par(0, n, [&](uint32_t a, uint32_t b, uint32_t t) {
+      for (uint32_t v = a; v < b; ++v) {
+        Member& mv = m[v];
+        if (!mv.up) { mv.fd_sync.clear(); continue; }
+        uint32_t k = 0;
+        if (sync_due(mv)) {  // doSync (:339-357)
+          uint32_t tg = select_sync_address(v);
+          if (tg != NONE) rq[t].push_back(SyncReq{v, tg, k++, false, false, false, false});
+        }
+        for (uint32_t tg : mv.fd_sync) rq[t].push_back(SyncReq{v, tg, k++, false, false, false, false});
+        mv.fd_sync.clear();
+        if (mv.join_now) {  // start0 initial sync to every seed (:250-291)
+          for (uint32_t s : seeds)
+            if (s != v) rq[t].push_back(SyncReq{v, s, k++, true, false, false, false});
+        }
+      }
+    });
     std::vector<SyncReq> reqs;
-    for (uint32_t v = 0; v < n; ++v) {
-      Member& mv = m[v];
-      if (!mv.up) { mv.fd_sync.clear(); continue; }
-      uint32_t k = 0;
-      if (sync_due(mv)) {  // doSync (:339-357)
-        uint32_t t = select_sync_address(v);
-        if (t != NONE) reqs.push_back(SyncReq{v, t, k++, false, false, false, false});
-      }
-      for (uint32_t t : mv.fd_sync) reqs.push_back(SyncReq{v, t, k++, false, false, false, false});
-      mv.fd_sync.clear();
-      if (mv.join_now) {  // start0 initial sync to every seed (:250-291)
-        for (uint32_t s : seeds)
-          if (s != v) reqs.push_back(SyncReq{v, s, k++, true, false, false, false});
-      }
-    }
+    for (auto& x : rq) reqs.insert(reqs.end(), x.begin(), x.end());
     if (reqs.empty()) {
       finish_joins(reqs);
       return;
     }
     // request content: the sender's table when the SYNC is prepared (:485-489)
-    std::map<uint32_t, std::vector<uint64_t>> content;
-    for (auto& q : reqs)
-      if (!content.count(q.from)) content[q.from] = m[q.from].row;
+    std::vector<uint32_t> senders;
+    for (auto& q : reqs) senders.push_back(q.from);
+    std::sort(senders.begin(), senders.end());
+    senders.erase(std::unique(senders.begin(), senders.end()), senders.end());
+    std::vector<std::vector<uint64_t>> rows(senders.size());
+    par(0, (uint32_t)senders.size(), [&](uint32_t a, uint32_t b, uint32_t) {
+      for (uint32_t i = a; i < b; ++i) rows[i] = m[senders[i]].row;
+    });
+    auto content_of = [&](uint32_t s) -> const std::vector<uint64_t>& {
+      return rows[std::lower_bound(senders.begin(), senders.end(), s) - senders.begin()];
+    };
     std::vector<size_t> delivered;
     for (size_t i = 0; i < reqs.size(); ++i) {
       SyncReq& q = reqs[i];
-      st.syncs++;
+      STT().syncs++;
       if (out_fail(q.from, q.to, draw(q.from, SWIM_STREAM_SYNC_OUT, q.ordinal, 0))) { q.outfail = true; continue; }
       if (!in_pass(q.to, q.from)) continue;
       q.delivered = true;
@@ -764,48 +864,61 @@ struct swim_engine {
       if (reqs[a].from != reqs[b].from) return reqs[a].from < reqs[b].from;
       return reqs[a].ordinal < reqs[b].ordinal;
     });
+    // receivers' inboxes: delivered[gs[g] .. gs[g + 1])
+    std::vector<size_t> gs;
+    for (size_t i = 0; i < delivered.size(); ++i)
+      if (i == 0 || reqs[delivered[i]].to != reqs[delivered[i - 1]].to) gs.push_back(i);
+    const uint32_t ng = (uint32_t)gs.size();
+    gs.push_back(delivered.size());
     // D1: onSync at each receiver (:394-415)
-    uint32_t cur = NONE;
-    for (size_t i : delivered) {
-      SyncReq& q = reqs[i];
-      if (q.to != cur) {
-        cur = q.to;
-        m[cur].ev_minor = 0;
-        m[cur].fetch_ctr = 0;
+    par(0, ng, [&](uint32_t a, uint32_t b, uint32_t) {
+      for (uint32_t g = a; g < b; ++g) {
+        const uint32_t r = reqs[delivered[gs[g]]].to;
+        m[r].ev_minor = 0;
+        m[r].fetch_ctr = 0;
+        for (size_t i = gs[g]; i < gs[g + 1]; ++i)
+          sync_membership(r, content_of(reqs[delivered[i]].from), SYNC, SWIM_PHASE_SYNC);
       }
-      sync_membership(q.to, content[q.from], SYNC, SWIM_PHASE_SYNC);
-    }
+    });
     // SYNC_ACK content: the receiver's table once all its requests are merged
-    std::map<uint32_t, std::vector<uint64_t>> ack_content;
-    struct Ack { uint32_t to, from, rank; bool initial; };
+    std::vector<std::vector<uint64_t>> arows(ng);
+    par(0, ng, [&](uint32_t a, uint32_t b, uint32_t) {
+      for (uint32_t g = a; g < b; ++g) arows[g] = m[reqs[delivered[gs[g]]].to].row;
+    });
+    struct Ack { uint32_t to, from, rank, grp; bool initial; };
     std::vector<Ack> acks;
-    cur = NONE;
-    uint32_t rank = 0;
-    for (size_t i : delivered) {
-      SyncReq& q = reqs[i];
-      if (q.to != cur) { cur = q.to; rank = 0; ack_content[cur] = m[cur].row; }
-      uint32_t qr = rank++;
-      if (out_fail(q.to, q.from, draw(q.to, SWIM_STREAM_SYNCACK_OUT, qr, 0))) continue;
-      if (!in_pass(q.from, q.to)) continue;
-      q.acked = true;
-      acks.push_back(Ack{q.from, q.to, qr, q.initial});
+    for (uint32_t g = 0; g < ng; ++g) {
+      for (size_t i = gs[g]; i < gs[g + 1]; ++i) {
+        SyncReq& q = reqs[delivered[i]];
+        const uint32_t qr = (uint32_t)(i - gs[g]);
+        if (out_fail(q.to, q.from, draw(q.to, SWIM_STREAM_SYNCACK_OUT, qr, 0))) continue;
+        if (!in_pass(q.from, q.to)) continue;
+        q.acked = true;
+        acks.push_back(Ack{q.from, q.to, qr, g, q.initial});
+      }
     }
     std::stable_sort(acks.begin(), acks.end(), [](const Ack& a, const Ack& b) {
       if (a.to != b.to) return a.to < b.to;
       if (a.from != b.from) return a.from < b.from;
       return a.rank < b.rank;
     });
+    std::vector<size_t> as;
+    for (size_t i = 0; i < acks.size(); ++i)
+      if (i == 0 || acks[i].to != acks[i - 1].to) as.push_back(i);
+    const uint32_t na = (uint32_t)as.size();
+    as.push_back(acks.size());
     // D2: SYNC_ACK merge at the original sender (:363-391), INITIAL_SYNC for start0's requests
-    cur = NONE;
-    for (auto& a : acks) {
-      if (a.to != cur) {
-        cur = a.to;
-        m[cur].ev_minor = 0;
-        m[cur].fetch_ctr = 0;
+    par(0, na, [&](uint32_t a, uint32_t b, uint32_t) {
+      for (uint32_t g = a; g < b; ++g) {
+        const uint32_t s = acks[as[g]].to;
+        m[s].ev_minor = 0;
+        m[s].fetch_ctr = 0;
+        for (size_t i = as[g]; i < as[g + 1]; ++i) {
+          STT().sync_acks++;
+          sync_membership(s, arows[acks[i].grp], acks[i].initial ? INITIAL_SYNC : SYNC, SWIM_PHASE_SYNCACK);
+        }
       }
-      st.sync_acks++;
-      sync_membership(a.to, ack_content[a.from], a.initial ? INITIAL_SYNC : SYNC, SWIM_PHASE_SYNCACK);
-    }
+    });
     finish_joins(reqs);
   }
 
@@ -1047,6 +1160,14 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
   }
   for (auto& x : th) x.join();
   *out = e;
+  return SWIM_OK;
+}
+
+// Oracle only (not in swim.h): worker threads of the per-member phase loops (the CPU baseline's
+// all-core leg; results are identical for every thread count).  0 = hardware concurrency.
+int32_t swim_oracle_set_threads(swim_engine* e, int32_t threads) {
+  if (!e || threads < 0) return SWIM_EINVAL;
+  e->threads = threads ? (uint32_t)threads : std::max(1u, std::thread::hardware_concurrency());
   return SWIM_OK;
 }
 

@@ -559,10 +559,6 @@ static int32_t run_tick(swim_engine* e) {
       if (sd.n_rx_msgs)
         k_recv_msgs<<<std::min<uint32_t>(grid_for(sd.n_rx_msgs, 256), 1024), 256, 0, s>>>(sd.d_par, T, sd.n_rx_msgs);
       TICK_CHECK("k_recv_msgs");
-      k_alloc<<<std::min<uint32_t>(1024, grid_for(sd.c.nl, 256)), 256, 0, s>>>(sd.d_par, T);
-      TICK_CHECK("k_alloc");
-      k_scatter_msgs<<<512, 256, 0, s>>>(sd.d_par, T);
-      TICK_CHECK("k_scatter_msgs");
       // at least kDeliverGrid workgroups: big inboxes are delivered a wave each, grid-stride
       k_gossip_deliver<<<std::max<uint32_t>(kDeliverGrid, grid_for(sd.c.nl, DLV_BLOCK)), DLV_BLOCK, 0, s>>>(sd.d_par, T);
       TICK_CHECK("k_gossip_deliver");  // (also applies the phase's pingMembers inserts)
@@ -720,6 +716,11 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.ins_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 22, 256ull * nl));
   b.msg_cap = cf.message_capacity ? cf.message_capacity
                                  : (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 512ull * nl));
+  // inbox pages: the message capacity in 64-message pages, plus one partial page per receiver and
+  // slack for racing first touches; a receiver's inbox may span up to pg_max pages (4x its even share)
+  b.pg_cap = (uint32_t)std::min<uint64_t>(1ull << 26, (uint64_t)b.msg_cap / 64 + nl + 4096);
+  b.pg_max = (uint32_t)std::min<uint64_t>(1u << 16, std::max<uint64_t>(4, next_pow2((uint32_t)std::min<uint64_t>(
+                                              1u << 30, 4ull * b.msg_cap / 64 / std::max(nl, 1u)))));
   b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
   b.wave_min = cf.deliver_wave_min ? std::min<uint32_t>(cf.deliver_wave_min, DLV_SORT) : (uint32_t)DLV_SORT;
   b.snap_cap = 64;
@@ -757,9 +758,9 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&c.gbits, (size_t)GSLOTS * c.gwords) && sd.alloc(&c.clr_tick, std::max(nl, 1u)) &&
             sd.alloc(&c.gclaim, 2 * GSLOTS) && sd.alloc(&c.gclaim_cnt, 2) &&
             sd.alloc(&c.stats, (size_t)ST_COUNT * ST_REPL) && sd.alloc(&c.err, 1) && sd.alloc(&sd.k, 1) &&
-            sd.alloc(&sd.x, 1) && sd.alloc(&b.msgs, b.msg_cap) && sd.alloc(&b.msgs_out, b.msg_cap) &&
-            sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.msg_start, nl) && sd.alloc(&b.big_list, nl) &&
-            sd.alloc(&b.big_tick, nl) && sd.alloc(&b.perm, b.msg_cap) &&
+            sd.alloc(&sd.x, 1) && sd.alloc(&b.pg_msgs, (size_t)b.pg_cap * 64) &&
+            sd.alloc(&b.pg_perm, (size_t)b.pg_cap * 64) && sd.alloc(&b.pg_tab, (size_t)std::max(nl, 1u) * b.pg_max) &&
+            sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.big_list, nl) && sd.alloc(&b.big_tick, nl) &&
             sd.alloc(&b.reqs, b.req_cap) && sd.alloc(&b.reqs_out, b.req_cap) && sd.alloc(&b.req_cnt, nl) &&
             sd.alloc(&b.req_start, nl) && sd.alloc(&b.req_recv, nl) && sd.alloc(&b.acks, b.req_cap) &&
             sd.alloc(&b.req_desc, std::max(nl, 1u)) && sd.alloc(&b.ack_desc, std::max(nl, 1u)) &&
@@ -804,6 +805,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(sd.k, 0, sizeof(Counters), s);
   hipMemsetAsync(sd.x, 0, sizeof(Xc), s);
   hipMemsetAsync(b.msg_cnt, 0, 4 * (size_t)nl, s);
+  hipMemsetAsync(b.pg_tab, 0xff, 4 * (size_t)std::max(nl, 1u) * b.pg_max, s);
   hipMemsetAsync(b.big_tick, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.req_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.ack_cnt, 0, 4 * (size_t)nl, s);

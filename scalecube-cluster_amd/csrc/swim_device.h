@@ -32,6 +32,8 @@ enum : uint32_t {
   ERR_SLAB = 1u << 0, ERR_INTERVALS = 1u << 1, ERR_HASH = 1u << 2, ERR_WHEEL = 1u << 3,
   ERR_EVENTS = 1u << 4, ERR_MSGS = 1u << 5, ERR_SNAP = 1u << 6, ERR_INFECTED = 1u << 7,
   ERR_FDSYNC = 1u << 8, ERR_INS = 1u << 9, ERR_REQS = 1u << 10, ERR_PEND = 1u << 11, ERR_INC = 1u << 12,
+  ERR_PAGES = 1u << 13,  // the gossip inbox page pool ran dry
+  ERR_INBOX = 1u << 14,  // one receiver's gossip inbox outgrew its page table
 };
 
 // stats slots (swim_stats order)

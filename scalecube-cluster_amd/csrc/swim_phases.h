@@ -3,7 +3,7 @@
 // Phase A  k_fd (per 256-viewer block)                suspicion timeouts
 // Phase B  k_fd                                       list compaction after REMOVED, then ping /
 //                                                     ping-req / ack resolution + FD events
-// Phase C  round start (+ segmentation) in k_fd, k_gossip_emit, k_alloc, k_scatter_msgs, k_gossip_deliver
+// Phase C  round start (+ segmentation) in k_fd, k_gossip_emit (+ k_recv_msgs), k_gossip_deliver
 // Phase D  SYNC collection (in k_fd / k_gossip_deliver), k_sync_prep, k_sync_classify, k_sync_apply (swim_sync.h; SYNC and SYNC_ACK)
 // lists    (k_gossip_deliver, k_sync_apply)           deferred pingMembers inserts of ADDED events
 // tick end k_end_tick
@@ -17,7 +17,7 @@ namespace swimdev {
 
 // per-tick scratch counters, zeroed by one hipMemsetAsync at the start of every tick
 struct Counters {
-  uint32_t msg_total, msg_cursor, pad0;
+  uint32_t msg_total, pg_cursor, pad0;  // messages materialised this round; inbox pages taken
   uint32_t req_total, req_recv_cnt, req_cursor;
   uint32_t ack_total, ack_recv_cnt, ack_cursor;
   uint32_t ins_total, pad1;   // overflow list-insert ops of the gossip phase
@@ -51,15 +51,16 @@ struct Bufs {
   const SyncReq* rx_reqs;
   const uint32_t* rx_rows;  // record rows of received SYNC / SYNC_ACKs, indexed by SyncReq.content
   const uint32_t* rx_stops;
-  GMsgFull* msgs;      // produced in emit order
-  GMsgFull* msgs_out;  // grouped by receiver
+  // paged gossip inboxes (inbox_page): message k of receiver i's round is pg_msgs[pg_tab[i][k / 64]][k % 64]
+  GMsgFull* pg_msgs;   // [pg_cap][64]
+  uint32_t* pg_perm;   // [pg_cap][64] big inboxes: canonical rank -> inbox position, same paging
+  uint32_t* pg_tab;    // [nl][pg_max] page of each 64-message stretch of the inbox, NONE = none yet
+  uint32_t pg_cap, pg_max;
   uint32_t msg_cap;
   uint32_t* msg_cnt;   // per receiver
-  uint32_t* msg_start;
-  uint32_t* big_list;  // local indices of receivers with big inboxes (k_alloc)
+  uint32_t* big_list;  // local indices of receivers with big inboxes (the writer that crosses wave_min)
   uint32_t* big_tick;  // per receiver: tick whose inbox took the wave-parallel path
   uint32_t wave_min;   // inboxes above this many messages take it (<= DLV_SORT)
-  uint32_t* perm;      // [msg_cap] canonical delivery order of big inboxes (index into the inbox)
   SyncReq* reqs;
   SyncReq* reqs_out;
   uint32_t req_cap;
@@ -438,12 +439,59 @@ __device__ __forceinline__ bool gossip_due(const Ctx& c, uint32_t v, const Membe
 // checkGossipSegmentation (GossipProtocolImpl.java:217-236); only launched when the threshold is
 // below the inline interval capacity (otherwise a clear can never trigger).
 
-// a GOSSIP_REQ for a receiver owned by this shard joins the receiver's inbox
-__device__ inline void deliver_local_msg(const Ctx& c, const Bufs& b, GMsgFull msg) {
-  const uint32_t i = atomicAdd(&b.k->msg_total, 1u);
-  if (i >= b.msg_cap) { set_err(c, ERR_MSGS); return; }
-  msg.slot = atomicAdd(&b.msg_cnt[msg.to - c.lo], 1u);
-  b.msgs[i] = msg;
+// Gossip inboxes are paged: receiver i's k-th message of the round lives in page
+// pg_tab[i][k / 64], slot k % 64; pages come from a per-tick bump pool, so emit and k_recv_msgs write
+// every message straight into its receiver's inbox (no grouping pass) and the deliverer hands the
+// pages back by resetting the receiver's page table.  Exactly one writer allocates each page: the
+// one whose reserved slots include the page's first slot; a writer whose slots start inside a page
+// waits for that page (its first slot was reserved earlier, by a writer that allocates it without
+// waiting).  Writers allocate before they wait, so a wave never waits on one of its own lanes.
+constexpr uint32_t PG_FAILED = 0xfffffffeu;  // the pool ran dry: releases the page's waiters
+__device__ inline uint32_t inbox_page_alloc(const Ctx& c, const Bufs& b, uint32_t i, uint32_t pg) {
+  if (pg >= b.pg_max) { set_err(c, ERR_INBOX); return NONE; }
+  uint32_t np = atomicAdd(&b.k->pg_cursor, 1u);
+  if (np >= b.pg_cap) { set_err(c, ERR_PAGES); np = PG_FAILED; }
+  __atomic_store_n(b.pg_tab + (size_t)i * b.pg_max + pg, np, __ATOMIC_RELAXED);
+  return np == PG_FAILED ? NONE : np;
+}
+__device__ inline uint32_t inbox_page_wait(const Ctx& c, const Bufs& b, uint32_t i, uint32_t pg) {
+  if (pg >= b.pg_max) { set_err(c, ERR_INBOX); return NONE; }
+  const uint32_t* e = b.pg_tab + (size_t)i * b.pg_max + pg;
+  for (uint32_t it = 0; it < (1u << 20); ++it) {
+    const uint32_t v = __atomic_load_n(e, __ATOMIC_RELAXED);
+    if (v != NONE) return v == PG_FAILED ? NONE : v;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  set_err(c, ERR_PAGES);  // bounded: never reached while the page's allocator runs
+  return NONE;
+}
+// the receiver's inbox crossed the per-thread delivery limit: the wave-parallel path takes it
+__device__ __forceinline__ void big_mark(const Bufs& b, uint32_t i, uint64_t T) {
+  b.big_list[atomicAdd(&b.k->big_cnt, 1u)] = i;
+  b.big_tick[i] = (uint32_t)T;
+}
+__device__ __forceinline__ void wave_order() {
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+}
+
+// a GOSSIP_REQ for a receiver owned by this shard joins the receiver's inbox (every lane of the wave
+// calls it: `valid` masks the lanes without a message)
+__device__ inline void deliver_local_msg(const Ctx& c, const Bufs& b, GMsgFull msg, bool valid) {
+  const uint32_t i = msg.to - c.lo;
+  uint32_t s = 0, pid = NONE;
+  if (valid) {
+    s = atomicAdd(&b.msg_cnt[i], 1u);
+    if (s == b.wave_min) big_mark(b, i, c.T);
+    if ((s & 63) == 0) pid = inbox_page_alloc(c, b, i, s >> 6);
+  }
+  wave_order();
+  if (valid && (s & 63) != 0) pid = inbox_page_wait(c, b, i, s >> 6);
+  if (valid && pid != NONE) {
+    msg.slot = s;
+    b.pg_msgs[(size_t)pid * 64 + (s & 63)] = msg;
+    b.k->msg_total = 1u;  // "some inbox is non-empty" (k_gossip_deliver's early exit)
+  }
 }
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
@@ -455,19 +503,12 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 // its period (:143); a sender with live gossips then gets the whole wave: lane 0 selects the
 // targets (:322-343), the (target, slab position) pairs of selectGossipsToSend (:311-320) are
 // spread over the lanes — loss draws and receiver-collector probes of 64 pairs in flight together,
-// one enqueue atomic per (target, pass) — then the order-preserving sweep and the futures.
+// one inbox atomic per (target, pass) — and the same pass over the slab also sweeps it (:158-164,
+// order preserving) and checks the futures.
 constexpr int EMIT_WAVES = 4;
-// message slots are reserved in per-wave chunks (cb, cl: chunk base / slots left, wave-uniform); a
-// pass fills the chunk's remainder and continues in a fresh chunk, so only the wave's last
-// remainder is left over, marked as holes (to = NONE) that k_scatter_msgs skips
-constexpr uint32_t EMIT_CHUNK = 128;
-__device__ inline void emit_mark_holes(const Bufs& b, uint32_t cb, uint32_t cl, uint32_t lane) {
-  for (uint32_t i = lane; i < cl; i += 64)
-    if (cb + i < b.msg_cap) b.msgs[cb + i].to = NONE;
-}
 __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs& b, uint32_t v, uint64_t period,
-                                                        uint32_t glen, uint32_t lane, uint32_t* s_t, uint32_t& cb,
-                                                        uint32_t& cl, unsigned long long& nmat) {
+                                                        uint32_t glen, uint32_t lane, uint32_t* s_t,
+                                                        unsigned long long& nmat) {
   MemberDev& m = mem(c, v);
   const uint32_t rlen = m.remote_len;
   const uint32_t F = (uint32_t)c.fanout;
@@ -490,19 +531,34 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   const uint32_t nt = s_t[0];
   const uint64_t spread = (uint64_t)(c.repeat_mult * ceil_log2(rlen + 1));
   const uint64_t sweep = 2 * (spread + 1);
+  const bool leaving = m.leave_pending != 0;
   GossipDev* slab = slab_of(c, v);
   unsigned long long nmsg = 0;
   uint32_t pseq = 0;  // lane j < nt: messages materialised to target j so far (GMsgFull.pseq)
+  uint32_t w = 0;     // sweep: survivors so far
+  bool done = false;
   // lane = slab position: one GossipState read serves all nt targets, whose loss draws and
   // receiver checks are independent (issued together); messages keep the (target, position) keys
   for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
     const uint32_t p = p0 + lane;
     GossipDev g;
-    bool win = false;
+    bool win = false, keep = false;
     if (p < glen) {
       g = slab[p];
       win = (uint64_t)g.inf_period + spread >= period;
+      keep = !(period > (uint64_t)g.inf_period + sweep);
     }
+    // sweep (:158-164, :350-358): a pass's survivors land at or below their own positions, all of
+    // which the wave has already read
+    const uint64_t kmask = __ballot(keep);
+    if (keep) {
+      slab[w + lanes_below(kmask)] = g;
+      // futures (:167-180): the graceful-leave future stops the member at the end of the tick
+      if (leaving && period > (uint64_t)g.inf_period + spread && g.gossiper == m.leave_gossiper &&
+          g.seq == (uint32_t)m.leave_seq)
+        done = true;
+    }
+    w += (uint32_t)__popcll(kmask);
     uint32_t matb = 0;  // bit j: a message to target j is materialised
     if (__ballot(win)) {
       for (uint32_t j = 0; j < nt; ++j) {
@@ -510,7 +566,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         const bool send = win && !gossip_infected(g, t);
         nmsg += send ? 1u : 0u;
         // delivered copies; a receiver on this shard that already holds the sequence id drops it
-        // (its collector only grows until delivery), another shard filters on arrival
+        // (its collector only grows until delivery), another shard flags it on arrival
         const bool mat = send && c.up[t] && in_pass(c, t, v) &&
                          !lost_k(c, out_loss(c, v, t), v, SWIM_STREAM_GOSSIP_OUT, j, p) &&
                          !(owned(c, t) && known_received(c, t, g.gossiper, g.seq));
@@ -518,85 +574,58 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       }
     }
     if (!__ballot(matb != 0)) continue;
-    // one enqueue per target present in this pass: lane j issues target j's receiver atomic; the
-    // message slots of this shard's targets come out of the wave's chunk, in (target, lane) order
-    uint32_t base = 0, slot = 0, cnt_mine = 0, loc_off = 0, loc_tot = 0;
+    // one inbox reservation per target present in this pass: lane j issues target j's atomic and
+    // makes sure the (at most two) inbox pages of its slot range exist
+    uint32_t cnt_mine = 0;
     for (uint32_t j = 0; j < nt; ++j) {
       const uint32_t cj = (uint32_t)__popcll(__ballot((matb >> j) & 1u));
       nmat += cj;  // wave-uniform
       if (lane == j) cnt_mine = cj;
-      if (owned(c, s_t[1 + j])) {
-        if (lane == j) loc_off = loc_tot;
-        loc_tot += cj;
-      }
     }
-    uint32_t nb = 0, want = 0;
-    if (loc_tot > cl) {
-      want = loc_tot - cl > EMIT_CHUNK ? loc_tot - cl : EMIT_CHUNK;
-      if (lane == 0) nb = atomicAdd(&b.k->msg_total, want);
-      nb = __shfl(nb, 0, 64);
-    }
+    uint32_t base = 0, pid0 = NONE, pid1 = NONE;
+    const bool loc = lane < nt && cnt_mine && owned(c, s_t[1 + lane]);
     if (lane < nt && cnt_mine) {
       const uint32_t tj = s_t[1 + lane];
-      if (owned(c, tj)) {
-        base = loc_off;  // index in this pass's local sequence; mapped to a slot below
-        slot = atomicAdd(&b.msg_cnt[tj - c.lo], cnt_mine);
+      if (loc) {
+        const uint32_t i = tj - c.lo;
+        base = atomicAdd(&b.msg_cnt[i], cnt_mine);
+        if (base <= b.wave_min && base + cnt_mine > b.wave_min) big_mark(b, i, c.T);
+        // pages whose first slot is ours: ours to allocate (first the second page, if any)
+        if (((base + cnt_mine - 1) >> 6) != (base >> 6)) pid1 = inbox_page_alloc(c, b, i, (base >> 6) + 1);
+        if ((base & 63) == 0) pid0 = inbox_page_alloc(c, b, i, base >> 6);
       } else {
         base = atomicAdd(&b.x->msg[owner(c, tj)], cnt_mine);
       }
+    }
+    wave_order();
+    if (loc) {
+      // our slots start inside a page another writer allocates
+      if ((base & 63) != 0) pid0 = inbox_page_wait(c, b, s_t[1 + lane] - c.lo, base >> 6);
+      if (((base + cnt_mine - 1) >> 6) == (base >> 6)) pid1 = pid0;
     }
     for (uint32_t j = 0; j < nt; ++j) {
       const bool mat = (matb >> j) & 1u;
       const uint64_t mk = __ballot(mat);
       if (!mk) continue;
-      const uint32_t bj = __shfl(base, (int)j, 64), sj = __shfl(slot, (int)j, 64), qj = __shfl(pseq, (int)j, 64);
+      const uint32_t bj = __shfl(base, (int)j, 64), qj = __shfl(pseq, (int)j, 64);
+      const uint32_t p0j = __shfl(pid0, (int)j, 64), p1j = __shfl(pid1, (int)j, 64);
       if (!mat) continue;
       const uint32_t pre = lanes_below(mk);
       const uint32_t t = s_t[1 + j];
       GMsgFull msg;
-      msg.to = t; msg.from = v; msg.pos = p; msg.slot = sj + pre;
+      msg.to = t; msg.from = v; msg.pos = p; msg.slot = bj + pre;
       msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
       msg.inc = g.inc; msg.pseq = qj + pre; msg.dup = 0; msg.pad = 0;
       if (owned(c, t)) {
-        const uint32_t seq_i = bj + pre;  // position in the pass's local sequence
-        const uint32_t loc_slot = seq_i < cl ? cb + seq_i : nb + (seq_i - cl);
-        if (loc_slot < b.msg_cap) b.msgs[loc_slot] = msg; else set_err(c, ERR_MSGS);
+        const uint32_t s = bj + pre;
+        const uint32_t pid = (s >> 6) == (bj >> 6) ? p0j : p1j;
+        if (pid != NONE) b.pg_msgs[(size_t)pid * 64 + (s & 63)] = msg;  // else inbox_page set the error bit
       } else {
         const uint32_t d = owner(c, t);
         if (bj + pre < b.tx_msg_cap) b.tx_msgs[(size_t)d * b.tx_msg_cap + bj + pre] = msg; else set_err(c, ERR_MSGS);
       }
     }
     pseq += cnt_mine;  // lane j: target j's messages so far this round
-    if (loc_tot > cl) {
-      cb = nb + (loc_tot - cl);
-      cl = want - (loc_tot - cl);
-    } else {
-      cb += loc_tot;
-      cl -= loc_tot;
-    }
-  }
-  // sweep (:158-164, :350-358), order preserving: a chunk's survivors land at or below their own
-  // positions, all of which the wave has already read
-  uint32_t w = 0;
-  bool done = false;
-  const bool leaving = m.leave_pending != 0;
-  for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
-    const uint32_t p = p0 + lane;
-    GossipDev g;
-    bool keep = false;
-    if (p < glen) {
-      g = slab[p];
-      keep = !(period > (uint64_t)g.inf_period + sweep);
-    }
-    const uint64_t mask = __ballot(keep);
-    if (keep) {
-      slab[w + lanes_below(mask)] = g;
-      // futures (:167-180): the graceful-leave future stops the member at the end of the tick
-      if (leaving && period > (uint64_t)g.inf_period + spread && g.gossiper == m.leave_gossiper &&
-          g.seq == (uint32_t)m.leave_seq)
-        done = true;
-    }
-    w += (uint32_t)__popcll(mask);
   }
   const bool any_done = __ballot(done) != 0;
   if (lane == 0) {
@@ -701,15 +730,14 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned lo
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t ns = b.k->sender_cnt;
   unsigned long long nmsg = 0, nmat = 0, nstate = 0;
-  uint32_t cb = 0, cl = 0;
   for (uint32_t k = __builtin_amdgcn_readfirstlane(blockIdx.x * EMIT_WAVES + wv); k < ns; k += gridDim.x * EMIT_WAVES) {
     const uint32_t i = b.senders[k];
     const MemberDev& m = c.mem[i];
     const uint32_t glen = m.gossip_len;
     nstate += glen;
-    nmsg += gossip_emit_sender(c, b, c.lo + i, m.g_period - 1, glen, lane, s_t[wv], cb, cl, nmat);
+    nmsg += gossip_emit_sender(c, b, c.lo + i, m.g_period - 1, glen, lane, s_t[wv], nmat);
   }
-  emit_mark_holes(b, cb, cl, lane);
+  if (lane == 0 && nmat) atomicAdd(&b.k->msg_total, (uint32_t)nmat);
   if (prof && lane == 0 && nstate) {
     atomicAdd(prof, nmat);
     atomicAdd(prof + 1, nstate);
@@ -723,11 +751,18 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned lo
 __global__ void k_recv_msgs(KP, uint32_t nrx) {
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nrx; i += gridDim.x * blockDim.x) {
-    GMsgFull msg = b.rx_msgs[i];
-    // kept (flagged) so that each (sender, receiver) pair's pseq stays dense for deliver_big
-    msg.dup = coll_contains(c, coll_find(c, msg.to, msg.gossiper), msg.seq) ? 1u : 0u;
-    deliver_local_msg(c, b, msg);
+  // wave-uniform trip count: every lane of a wave takes part in each deliver_local_msg call
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); i0 < nrx; i0 += gridDim.x * blockDim.x) {
+    const uint32_t i = i0 + lane;
+    const bool valid = i < nrx;
+    GMsgFull msg{};
+    if (valid) {
+      msg = b.rx_msgs[i];
+      // kept (flagged) so that each (sender, receiver) pair's pseq stays dense for deliver_big
+      msg.dup = coll_contains(c, coll_find(c, msg.to, msg.gossiper), msg.seq) ? 1u : 0u;
+    }
+    deliver_local_msg(c, b, msg, valid);
   }
 }
 
@@ -737,71 +772,8 @@ __global__ void k_recv_msgs(KP, uint32_t nrx) {
 #endif
 constexpr int DLV_SORT = DLV_SORT_N;
 
-// group-by-receiver: region start per receiver (a workgroup scan of 256 receivers' counts and one
-// cursor atomic per workgroup), then scatter by (start + arrival slot); receivers with big inboxes
-// are listed (one wave-aggregated atomic) and stamped for the wave-parallel delivery path
-__global__ void __launch_bounds__(256) k_alloc(KP) {
-  __shared__ uint32_t s_wave[256 / 64 + 1];
-  __shared__ uint32_t s_base;
-  const Bufs b = P->b;
-  const uint32_t nl = P->c.nl;
-  if (b.k->msg_total == 0) return;  // a round without messages (every msg_cnt is 0)
-  for (uint32_t base = blockIdx.x * 256; base < nl; base += gridDim.x * 256) {
-    const uint32_t r = base + threadIdx.x;
-    const uint32_t k = r < nl ? b.msg_cnt[r] : 0u;
-    uint32_t total;
-    const uint32_t off = block_exclusive_scan<256>(k, s_wave, &total);
-    if (threadIdx.x == 0) s_base = total ? atomicAdd(&b.k->msg_cursor, total) : 0u;
-    __syncthreads();
-    if (k) b.msg_start[r] = s_base + off;
-    const bool big = k > b.wave_min;
-    const uint64_t mk = __ballot(big);
-    if (mk) {
-      uint32_t bb = 0;
-      if ((threadIdx.x & 63) == 0) bb = atomicAdd(&b.k->big_cnt, (uint32_t)__popcll(mk));
-      bb = __shfl(bb, 0, 64);
-      if (big) {
-        b.big_list[bb + lanes_below(mk)] = r;
-        b.big_tick[r] = (uint32_t)T;
-      }
-    }
-    __syncthreads();
-  }
-}
-
-__global__ void k_scatter_msgs(KP) {
-  const Bufs b = P->b;
-  const uint32_t lo = P->c.lo;
-  const uint32_t n = min(b.k->msg_total, b.msg_cap);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const GMsgFull m = b.msgs[i];
-    if (m.to == NONE) continue;  // a hole of a wave's slot chunk (k_gossip_emit)
-    const uint64_t at = (uint64_t)b.msg_start[m.to - lo] + m.slot;
-    if (at < b.msg_cap) b.msgs_out[at] = m;  // beyond: the buffer overflowed (ERR_MSGS is set)
-  }
-}
-
 __device__ __forceinline__ uint64_t msg_key(const GMsgFull& m) { return ((uint64_t)m.from << 32) | m.pos; }
 
-// heap sort of one receiver's messages by (sender, slab position): the big path's fallback for an
-// inbox from more than BIG_MAXD distinct senders
-__device__ inline void sort_msgs(GMsgFull* a, uint32_t n) {
-  if (n < 2) return;
-  auto sift = [&](uint32_t start, uint32_t end) {
-    uint32_t root = start;
-    while (2 * root + 1 < end) {
-      uint32_t ch = 2 * root + 1;
-      if (ch + 1 < end && msg_key(a[ch]) < msg_key(a[ch + 1])) ch++;
-      if (msg_key(a[root]) < msg_key(a[ch])) { GMsgFull t = a[root]; a[root] = a[ch]; a[ch] = t; root = ch; }
-      else return;
-    }
-  };
-  for (int64_t s = (int64_t)n / 2 - 1; s >= 0; --s) sift((uint32_t)s, n);
-  for (uint32_t e = n - 1; e > 0; --e) {
-    GMsgFull t = a[0]; a[0] = a[e]; a[e] = t;
-    sift(0, e);
-  }
-}
 
 // onGossipReq (GossipProtocolImpl.java:201-215) for one received message, in canonical order
 __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, GossipDev* slab, const GMsgFull& g) {
@@ -983,116 +955,140 @@ __device__ __forceinline__ int big_find(const uint32_t* snd, uint32_t nd, uint32
 __device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Bufs& b, uint32_t i, uint32_t lane,
                                           BigLds& L, unsigned long long& nsync) {
   const uint32_t r = c.lo + i;
-  const uint32_t k = b.msg_cnt[i];
-  const uint32_t start = b.msg_start[i];
+  const uint32_t k_all = b.msg_cnt[i];
   wave_sync();
   if (lane == 0) b.msg_cnt[i] = 0;
+  // messages beyond the page table were never written (ERR_MSGS is set)
+  const uint32_t k = min(k_all, b.pg_max * 64u);
+  const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
+  auto msg_at = [&](uint32_t q) -> const GMsgFull& { return b.pg_msgs[(size_t)pt[q >> 6] * 64 + (q & 63)]; };
+  auto perm_at = [&](uint32_t q) -> uint32_t& { return b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)]; };
   unsigned long long acc = 0;
-  if (c.up[r] && k) {
-    if ((uint64_t)start + k > b.msg_cap) {
-      if (lane == 0) set_err(c, ERR_MSGS);
+  bool pages_ok = true;
+  for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) pages_ok &= pt[pg] != NONE;
+  pages_ok = __ballot(!pages_ok) == 0;  // a page the pool could not give (ERR_MSGS is set)
+  if (c.up[r] && k && pages_ok) {
+    // pass 1: distinct senders and their message counts
+    uint32_t nd = 0;
+    bool over = false;
+    for (uint32_t q0 = 0; q0 < k && !over; q0 += 64) {
+      const uint32_t q = q0 + lane;
+      const uint32_t f = q < k ? msg_at(q).from : NONE;
+      uint64_t todo = __ballot(q < k);
+      while (todo) {
+        const uint32_t sf = __shfl(f, (int)__ffsll((unsigned long long)todo) - 1, 64);
+        const uint64_t same = __ballot(f == sf) & todo;
+        int slot = big_find(L.snd, nd, sf, lane);
+        if (slot < 0) {
+          if (nd == BIG_MAXD) { over = true; break; }
+          slot = (int)nd;
+          if (lane == 0) { L.snd[nd] = sf; L.cnt[nd] = 0; }
+          nd++;
+        }
+        if (lane == 0) L.cnt[slot] += (uint32_t)__popcll(same);
+        wave_sync();
+        todo &= ~same;
+      }
+    }
+    if (over) {
+      // more distinct senders than the LDS table holds (needs > BIG_MAXD senders choosing this
+      // receiver in one round): senders one at a time, ascending, by repeated minimum search
+      uint32_t lo_s = 0, rank = 0;
+      for (;;) {
+        uint32_t mn = NONE;
+        for (uint32_t q = lane; q < k; q += 64) {
+          const uint32_t f = msg_at(q).from;
+          if (f >= lo_s && f < mn) mn = f;
+        }
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) mn = min(mn, (uint32_t)__shfl_xor(mn, d, 64));
+        if (mn == NONE) break;
+        uint32_t cnt = 0;
+        for (uint32_t q0 = 0; q0 < k; q0 += 64) {
+          const uint32_t q = q0 + lane;
+          const bool mine = q < k && msg_at(q).from == mn;
+          if (mine && rank + msg_at(q).pseq < k) perm_at(rank + msg_at(q).pseq) = q;
+          cnt += (uint32_t)__popcll(__ballot(mine));
+        }
+        rank += cnt;
+        lo_s = mn + 1;
+      }
     } else {
-      GMsgFull* a = b.msgs_out + start;
-      uint32_t* perm = b.perm + start;
-      // pass 1: distinct senders and their message counts
-      uint32_t nd = 0;
-      bool over = false;
-      for (uint32_t q0 = 0; q0 < k && !over; q0 += 64) {
+      // senders ascending, inbox bases = exclusive prefix of their counts in that order
+      uint32_t ms[2], mc[2], mr[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const uint32_t j = lane + 64u * t;
+        ms[t] = j < nd ? L.snd[j] : NONE;
+        mc[t] = j < nd ? L.cnt[j] : 0u;
+        mr[t] = 0;
+        if (j < nd)
+          for (uint32_t x = 0; x < nd; ++x) mr[t] += L.snd[x] < ms[t] ? 1u : 0u;
+      }
+      wave_sync();
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        if (lane + 64u * t < nd) { L.snd[mr[t]] = ms[t]; L.cnt[mr[t]] = mc[t]; }
+      wave_sync();
+      if (lane == 0) {
+        uint32_t acc0 = 0;
+        for (uint32_t x = 0; x < nd; ++x) { const uint32_t t = L.cnt[x]; L.cnt[x] = acc0; acc0 += t; }
+      }
+      wave_sync();
+      // pass 2: rank = base of the sender + the message's pseq (dense per (sender, receiver))
+      for (uint32_t q0 = 0; q0 < k; q0 += 64) {
         const uint32_t q = q0 + lane;
-        const uint32_t f = q < k ? a[q].from : NONE;
+        uint32_t f = NONE, ps = 0;
+        if (q < k) {
+          const GMsgFull& g = msg_at(q);
+          f = g.from;
+          ps = g.pseq;
+        }
         uint64_t todo = __ballot(q < k);
         while (todo) {
           const uint32_t sf = __shfl(f, (int)__ffsll((unsigned long long)todo) - 1, 64);
           const uint64_t same = __ballot(f == sf) & todo;
-          int slot = big_find(L.snd, nd, sf, lane);
-          if (slot < 0) {
-            if (nd == BIG_MAXD) { over = true; break; }
-            slot = (int)nd;
-            if (lane == 0) { L.snd[nd] = sf; L.cnt[nd] = 0; }
-            nd++;
-          }
-          if (lane == 0) L.cnt[slot] += (uint32_t)__popcll(same);
-          wave_sync();
+          const uint32_t at = L.cnt[big_find(L.snd, nd, sf, lane)] + ps;
+          if (((same >> lane) & 1ull) && at < k) perm_at(at) = q;
           todo &= ~same;
         }
       }
-      if (over) {  // more distinct senders than the LDS ranking holds: sort the inbox in place
-        if (lane == 0) sort_msgs(a, k);
-        wave_sync();
-        for (uint32_t q = lane; q < k; q += 64) perm[q] = q;
-      } else {
-        // senders ascending, inbox bases = exclusive prefix of their counts in that order
-        uint32_t ms[2], mc[2], mr[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const uint32_t j = lane + 64u * t;
-          ms[t] = j < nd ? L.snd[j] : NONE;
-          mc[t] = j < nd ? L.cnt[j] : 0u;
-          mr[t] = 0;
-          if (j < nd)
-            for (uint32_t x = 0; x < nd; ++x) mr[t] += L.snd[x] < ms[t] ? 1u : 0u;
+    }
+    wave_sync();
+    MemberDev& m = mem(c, r);
+    if (lane == 0) {
+      m.ev_minor = 0;
+      m.fetch_ctr = 0;
+    }
+    GossipDev* slab = slab_of(c, r);
+    const size_t row = (size_t)i * c.n;
+    uint32_t sink = 0;
+    for (uint32_t q0 = 0; q0 < k; q0 += 64) {
+      const uint32_t q = q0 + lane;
+      if (q < k) {
+        uint32_t j = perm_at(q);
+        if (j >= k) {  // a hole: only after an inbox overflow (ERR_MSGS is set)
+          set_err(c, ERR_MSGS);
+          j = q;
         }
-        wave_sync();
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          if (lane + 64u * t < nd) { L.snd[mr[t]] = ms[t]; L.cnt[mr[t]] = mc[t]; }
-        wave_sync();
-        if (lane == 0) {
-          uint32_t acc0 = 0;
-          for (uint32_t x = 0; x < nd; ++x) { const uint32_t t = L.cnt[x]; L.cnt[x] = acc0; acc0 += t; }
-        }
-        wave_sync();
-        // pass 2: rank = base of the sender + the message's pseq (dense per (sender, receiver))
-        for (uint32_t q0 = 0; q0 < k; q0 += 64) {
-          const uint32_t q = q0 + lane;
-          uint32_t f = NONE, ps = 0;
-          if (q < k) {
-            f = a[q].from;
-            ps = a[q].pseq;
-          }
-          uint64_t todo = __ballot(q < k);
-          while (todo) {
-            const uint32_t sf = __shfl(f, (int)__ffsll((unsigned long long)todo) - 1, 64);
-            const uint64_t same = __ballot(f == sf) & todo;
-            const uint32_t at = L.cnt[big_find(L.snd, nd, sf, lane)] + ps;
-            if (((same >> lane) & 1ull) && at < k) perm[at] = q;
-            todo &= ~same;
-          }
-        }
+        const GMsgFull g = msg_at(j);
+        L.m[lane] = g;
+        const CollEnt* e = coll_find(c, r, g.gossiper);
+        sink ^= (e ? e->meta : 1u) ^ c.recs[row + g.subject] ^ c.aux[row + g.subject];
       }
       wave_sync();
-      MemberDev& m = mem(c, r);
       if (lane == 0) {
-        m.ev_minor = 0;
-        m.fetch_ctr = 0;
+        const uint32_t nq = min(64u, k - q0);
+        for (uint32_t t = 0; t < nq; ++t)
+          if (on_gossip_req(c, r, m, slab, L.m[t])) acc++;
       }
-      GossipDev* slab = slab_of(c, r);
-      const size_t row = (size_t)i * c.n;
-      uint32_t sink = 0;
-      for (uint32_t q0 = 0; q0 < k; q0 += 64) {
-        const uint32_t q = q0 + lane;
-        if (q < k) {
-          uint32_t j = perm[q];
-          if (j >= k) {  // a hole: only after a message-buffer overflow (ERR_MSGS is set)
-            set_err(c, ERR_MSGS);
-            j = q;
-          }
-          const GMsgFull g = a[j];
-          L.m[lane] = g;
-          const CollEnt* e = coll_find(c, r, g.gossiper);
-          sink ^= (e ? e->meta : 1u) ^ c.recs[row + g.subject] ^ c.aux[row + g.subject];
-        }
-        wave_sync();
-        if (lane == 0) {
-          const uint32_t nq = min(64u, k - q0);
-          for (uint32_t t = 0; t < nq; ++t)
-            if (on_gossip_req(c, r, m, slab, L.m[t])) acc++;
-        }
-        wave_sync();
-      }
-      if (sink == 0x5bd1e995u && lane == 63) set_err(c, 0u);  // keeps the warming loads; sets no bit
+      wave_sync();
     }
+    if (sink == 0x5bd1e995u && lane == 63) set_err(c, 0u);  // keeps the warming loads; sets no bit
   }
+  wave_sync();
+  // the inbox pages go back to the pool (the pool itself restarts every tick)
+  for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) b.pg_tab[(size_t)i * b.pg_max + pg] = NONE;
   apply_ins_batch<64, false>(c, r, lane, L.iP, L.iS, L.iR);
   if (lane == 0) nsync += sync_collect_member(cs, b, r);  // phase D's SYNC collection for r
   return acc;
@@ -1102,7 +1098,7 @@ __device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Buf
 // (a viewer's ADDED events of the phase all come from the one thread / wave that delivered to it),
 // then phase D's SYNC collection of every member, each right after its own deliveries and inserts
 // (nothing else in the gossip phase touches what sync_collect_member reads: the member's own lists,
-// schedule and fd_sync queue).  First the big inboxes, a wave each, grid-stride over k_alloc's list;
+// schedule and fd_sync queue).  First the big inboxes, a wave each, grid-stride over big_list;
 // then each workgroup's blocks of 256 members: small inboxes thread per receiver, their inserts by
 // the workgroup, the collection of members whose inbox was not big.
 __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
@@ -1136,13 +1132,16 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
       const uint32_t k = b.msg_cnt[i];
       const uint32_t r = c.lo + i;
       if (k != 0) {
+        // a small inbox fits its first page (k <= DLV_SORT < 64)
         b.msg_cnt[i] = 0;
-        const uint32_t start = b.msg_start[i];
+        uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
+        const uint32_t pid = *pt;
+        *pt = NONE;
         if (!c.up[r]) {
-        } else if ((uint64_t)start + k > b.msg_cap) {  // the buffer overflowed (ERR_MSGS is set)
+        } else if (pid == NONE) {  // the page pool ran dry (ERR_MSGS is set)
           set_err(c, ERR_MSGS);
         } else {
-          const GMsgFull* a = b.msgs_out + start;
+          const GMsgFull* a = b.pg_msgs + (size_t)pid * 64;
           for (uint32_t q = 0; q < k; ++q) {
             const uint64_t kx = msg_key(a[q]);  // keys are unique
             int32_t j = (int32_t)q - 1;

@@ -40,8 +40,10 @@ def event_digest(ev):
     return hashlib.sha256(cols.tobytes()).hexdigest()
 
 
-def run(sc, members=None, collectors=True):
+def run(sc, members=None, collectors=True, threads=1):
     e = scenarios.make_engine(oracle.lib(), sc)
+    if threads != 1:
+        oracle.set_threads(e, threads)
     scenarios.run(e, sc)
     ev = e.drain_events()
     st = e.stats()

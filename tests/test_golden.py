@@ -37,3 +37,12 @@ def test_oracle_reproduces_scenario_digest(sc):
 def test_oracle_reproduces_config2_digest():
     sc = scenarios.config2()
     assert oracle_run(sc, members=scenarios.CONFIG2_MEMBERS, collectors=False) == DIGESTS[sc.name]
+
+
+# the CPU baseline's multi-threaded oracle (std::thread workers over member ranges in every phase)
+# must reproduce the same digests as the sequential loops
+@pytest.mark.parametrize("name", ["loss5_kills_64", "churn_48", "join_burst_seg", "config3_rates_200",
+                                  "partition_heal_32", "mp_joins_via_seed"])
+def test_threaded_oracle_reproduces_scenario_digest(name):
+    sc = {s.name: s for s in scenarios.catalog()}[name]
+    assert oracle_run(sc, threads=4) == DIGESTS[sc.name]
