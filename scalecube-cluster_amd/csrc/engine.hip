@@ -38,7 +38,7 @@ constexpr uint32_t kDrainFirst = 1;    // the interval starts at one tick and ad
 constexpr uint32_t kClassifyGrid = CLS_GRID;  // 16,384 waves: about one (message, chunk) unit each at N = 65,536
 constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
 constexpr uint32_t kEmitGrid = 2048;      // 8,192 waves, one gossip sender at a time each
-constexpr uint32_t kDeliverGrid = 512;    // 2,048 waves for the big inboxes of a gossip storm
+constexpr uint32_t kDeliverGrid = 256;    // 1,024 waves for the big inboxes of a gossip storm
 constexpr uint32_t kStopCap = 4096;
 constexpr uint32_t kProfEvery = 3;  // SYNC classify launches between timed ones
 constexpr uint64_t kRebaseEvery = 16;  // ticks between rebases of the SYNC block witness (k_end_tick)
@@ -578,8 +578,6 @@ static int32_t run_tick(swim_engine* e) {
       // and almost all reuse the SYNC launch's reverse classification); a sharded one streams the
       // acks that arrived with their rows from other shards
       const int classified = d2 == 0 || multi;
-      k_sync_prep<<<1, 1024, 0, s>>>(sd.d_par, T, d2, !classified);
-      TICK_CHECK("k_sync_prep");
       if (classified) launch_classify(e, sd, d2);
       TICK_CHECK("k_sync_classify");
       k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(sd.d_par, T, d2, classified);
@@ -723,7 +721,9 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
                                               1u << 30, 4ull * b.msg_cap / 64 / std::max(nl, 1u)))));
   b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
   b.wave_min = cf.deliver_wave_min ? std::min<uint32_t>(cf.deliver_wave_min, DLV_SORT) : (uint32_t)DLV_SORT;
-  b.snap_cap = 64;
+  b.snap_cap = 256;
+  b.sy_max = (SY_INBOX - SY_INLINE + 63) / 64;
+  b.sy_pool_cap = b.req_cap / 64 + std::min(nl, b.req_cap) + 64;
   b.chunks = (n + SYNC_CHUNK - 1) / SYNC_CHUNK;
   b.pool_cap = std::max<uint32_t>(1u << 22, 16 * n);
   const bool multi = e->world > 1;
@@ -761,13 +761,16 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&sd.x, 1) && sd.alloc(&b.pg_msgs, (size_t)b.pg_cap * 64) &&
             sd.alloc(&b.pg_perm, (size_t)b.pg_cap * 64) && sd.alloc(&b.pg_tab, (size_t)std::max(nl, 1u) * b.pg_max) &&
             sd.alloc(&b.msg_cnt, nl) && sd.alloc(&b.big_list, nl) && sd.alloc(&b.big_tick, nl) &&
-            sd.alloc(&b.reqs, b.req_cap) && sd.alloc(&b.reqs_out, b.req_cap) && sd.alloc(&b.req_cnt, nl) &&
-            sd.alloc(&b.req_start, nl) && sd.alloc(&b.req_recv, nl) && sd.alloc(&b.acks, b.req_cap) &&
-            sd.alloc(&b.req_desc, std::max(nl, 1u)) && sd.alloc(&b.ack_desc, std::max(nl, 1u)) &&
-            sd.alloc(&b.acks_out, b.req_cap) && sd.alloc(&b.ack_cnt, nl) && sd.alloc(&b.ack_start, nl) &&
+            sd.alloc(&b.reqs, b.req_cap) && sd.alloc(&b.req_cnt, nl) && sd.alloc(&b.req_recv, nl) &&
+            sd.alloc(&b.acks, b.req_cap) && sd.alloc(&b.ack_cnt, nl) &&
+            sd.alloc(&b.rq_inl, (size_t)std::max(nl, 1u) * SY_INLINE) && sd.alloc(&b.ack_inl, (size_t)std::max(nl, 1u) * SY_INLINE) &&
+            sd.alloc(&b.rq_tab, (size_t)std::max(nl, 1u) * b.sy_max) && sd.alloc(&b.rq_pool, (size_t)b.sy_pool_cap * 64) &&
+            sd.alloc(&b.ack_tab, (size_t)std::max(nl, 1u) * b.sy_max) && sd.alloc(&b.ack_pool, (size_t)b.sy_pool_cap * 64) &&
+            sd.alloc(&b.ack_snap, nl) && sd.alloc(&b.sflag, nl) &&
+            sd.alloc(&b.ack_chunk, (size_t)b.req_cap * b.chunks) && sd.alloc(&b.ack_ctot, b.req_cap) &&
             sd.alloc(&b.ack_recv, nl) && 
-            sd.alloc(&b.snap, (size_t)b.snap_cap * n) && sd.alloc(&b.snap_idx, nl) && sd.alloc(&b.snap_list, b.snap_cap) &&
-            sd.alloc(&b.snap_cnt, 1) && sd.alloc(&b.item_chunk, (size_t)b.req_cap * b.chunks) &&
+            sd.alloc(&b.snap, (size_t)b.snap_cap * n) && sd.alloc(&b.snap_idx, nl) &&
+            sd.alloc(&b.snap_list, 2 * (size_t)b.snap_cap) && sd.alloc(&b.snap_cnt, 2) && sd.alloc(&b.item_chunk, (size_t)b.req_cap * b.chunks) &&
             sd.alloc(&b.item_total, b.req_cap) && sd.alloc(&b.pool, b.pool_cap) &&
             sd.alloc(&b.rev_chunk, (size_t)b.req_cap * b.chunks) && sd.alloc(&b.rev_total, b.req_cap) &&
             sd.alloc(&b.row_mod, nl) &&
@@ -810,8 +813,12 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(b.req_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.ack_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.snap_idx, 0xff, 4 * (size_t)nl, s);
+  hipMemsetAsync(b.ack_snap, 0xff, 4 * (size_t)nl, s);
+  hipMemsetAsync(b.sflag, 0, 4 * (size_t)nl, s);
+  hipMemsetAsync(b.rq_tab, 0xff, 4 * (size_t)std::max(nl, 1u) * b.sy_max, s);
+  hipMemsetAsync(b.ack_tab, 0xff, 4 * (size_t)std::max(nl, 1u) * b.sy_max, s);
   hipMemsetAsync(b.row_mod, 0, 4 * (size_t)nl, s);
-  hipMemsetAsync(b.snap_cnt, 0, 4, s);
+  hipMemsetAsync(b.snap_cnt, 0, 8, s);
   c.T = 0;
   if (nl) {
     k_init_rows<<<std::min<uint32_t>(nl, 65535), 256, 0, s>>>(c, n_initial);

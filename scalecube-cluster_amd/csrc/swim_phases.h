@@ -18,8 +18,8 @@ namespace swimdev {
 // per-tick scratch counters, zeroed by one hipMemsetAsync at the start of every tick
 struct Counters {
   uint32_t msg_total, pg_cursor, pad0;  // messages materialised this round; inbox pages taken
-  uint32_t req_total, req_recv_cnt, req_cursor;
-  uint32_t ack_total, ack_recv_cnt, ack_cursor;
+  uint32_t req_total, req_recv_cnt, req_pg;  // SYNC items, receivers, inbox pages taken
+  uint32_t ack_total, ack_recv_cnt, ack_pg;  // the same for SYNC_ACKs
   uint32_t ins_total, pad1;   // overflow list-insert ops of the gossip phase
   uint32_t ins_total2, pad2;  // overflow list-insert ops of the SYNC phase
   uint32_t pool_cursor;  // complex-record pool of the SYNC classify kernel
@@ -61,27 +61,37 @@ struct Bufs {
   uint32_t* big_list;  // local indices of receivers with big inboxes (the writer that crosses wave_min)
   uint32_t* big_tick;  // per receiver: tick whose inbox took the wave-parallel path
   uint32_t wave_min;   // inboxes above this many messages take it (<= DLV_SORT)
+  // SYNC / SYNC_ACK sub-phases (swim_sync.h): items in enqueue order; a receiver's inbox is paged
+  // like the gossip inboxes: its k-th message is item pool[tab[r][k / 64]][k % 64]
   SyncReq* reqs;
-  SyncReq* reqs_out;
   uint32_t req_cap;
-  uint32_t* req_cnt;
-  uint32_t* req_start;
-  uint32_t* req_recv;
-  uint2* req_desc;  // per receiver-list position: (inbox start, message count), written by k_sync_prep
+  uint32_t* req_cnt;    // per receiver
+  uint32_t* req_recv;   // receivers, in order of their first message
+  uint32_t* rq_inl;     // [nl][SY_INLINE] the first messages of each inbox (no page needed)
+  uint32_t* rq_tab;     // [nl][sy_max] pages of the rest: message SY_INLINE + j is page j / 64, slot j % 64
+  uint32_t* rq_pool;    // [sy_pool_cap][64]
   SyncReq* acks;
-  SyncReq* acks_out;
   uint32_t* ack_cnt;
-  uint32_t* ack_start;
   uint32_t* ack_recv;
-  uint2* ack_desc;
-  uint32_t* snap;       // snapshot record rows
+  uint32_t* ack_inl;
+  uint32_t* ack_tab;
+  uint32_t* ack_pool;
+  uint32_t sy_max, sy_pool_cap;
+  // content snapshots (a row that is both read as a message's content and merged into in one
+  // sub-phase): SYNC content claimed during collection (sflag), SYNC_ACK content copied by the
+  // acker's own k_sync_apply workgroup; slots released by k_end_tick
+  uint32_t* snap;       // [snap_cap][n] record rows
   uint32_t snap_cap;
-  uint32_t* snap_idx;   // per member: slot or NONE
-  uint32_t* snap_list;
-  uint32_t* snap_cnt;   // claims made by the last k_sync_prep (persistent across ticks)
+  uint32_t* snap_idx;   // per member: SYNC-content slot or NONE
+  uint32_t* ack_snap;   // per member: SYNC_ACK-content slot or NONE
+  uint32_t* snap_list;  // [2][snap_cap] members holding slots, by tick parity
+  uint32_t* snap_cnt;   // [2] slots taken, by tick parity
+  uint32_t* sflag;      // per member: tick << 3 | SF_* bits of this tick
   uint64_t* pend;       // per sync-apply workgroup: pending ALIVE admissions
-  uint2* item_chunk;    // per (message, chunk): (pool base, complex count)
-  uint32_t* item_total; // per message: complex count over all chunks
+  uint2* item_chunk;    // per (SYNC item, chunk): (pool base, complex count)
+  uint32_t* item_total; // per SYNC item: complex count over all chunks
+  uint2* ack_chunk;     // the same for SYNC_ACK items (classified by k_ack_classify when sharded)
+  uint32_t* ack_ctot;
   // SYNC_ACK reuse: the SYNC classify also classifies the reverse direction of every
   // local message (its SYNC_ACK compares the same two rows with the roles swapped)
   uint2* rev_chunk;     // per (SYNC message, chunk): reverse (pool base, complex count)
@@ -1197,14 +1207,127 @@ __device__ inline uint32_t select_sync_address(const Ctx& c, uint32_t v) {
 // sender's table size when the message is prepared: the count syncMembership iterates, :491-509)
 enum : uint32_t { RQ_INITIAL = 1, RQ_OUTFAIL = 2, RQ_DELIVERED = 4, RQ_RECS_SHIFT = 8 };
 
-// a delivered SYNC / SYNC_ACK joins its receiver's inbox (the receiver is owned by this shard)
-__device__ inline void enqueue_sync(const Ctx& c, SyncReq q, SyncReq* items, uint32_t* total, uint32_t* cnt,
-                                    uint32_t* recv, uint32_t* recv_cnt, uint32_t cap) {
-  q.slot = atomicAdd(&cnt[q.to - c.lo], 1u);
-  if (q.slot == 0) recv[atomicAdd(recv_cnt, 1u)] = q.to;
-  const uint32_t i = atomicAdd(total, 1u);
-  if (i >= cap) { set_err(c, ERR_REQS); return; }
-  items[i] = q;
+// per-member SYNC roles of the tick (Bufs.sflag)
+enum : uint32_t {
+  SF_SENT_LOCAL = 1,  // sent a SYNC delivered to a receiver on this shard (its row is read as content)
+  SF_SENT = 2,        // sent a delivered SYNC (it may be merged into in the SYNC_ACK sub-phase)
+  SF_RECV = 4,        // received a SYNC (its row is merged into in the SYNC sub-phase)
+};
+__device__ inline uint32_t snap_take(const Ctx& c, const Bufs& b, uint32_t i) {
+  const uint32_t par = (uint32_t)(c.T & 1);
+  const uint32_t slot = atomicAdd(&b.snap_cnt[par], 1u);
+  if (slot >= b.snap_cap) { set_err(c, ERR_SNAP); return NONE; }
+  b.snap_list[par * b.snap_cap + slot] = i;
+  return slot;
+}
+// add SF_* bits to member i's roles this tick; the update that completes {SENT, RECV} claims the
+// snapshot slot of i: its row is read as message content while its own merges change it (the SYNC
+// it sent carries its table when the SYNC was prepared, :485-489; the SYNC_ACK it sends carries its
+// table after its SYNC merges).  k_sync_classify fills the slot from the units of the SYNCs i
+// receives (they stream i's row before any merge); k_sync_apply copies i's row again, into a slot
+// of its own for the SYNC_ACK content, only when i's SYNC merges changed it.
+__device__ inline void sflag_set(const Ctx& c, const Bufs& b, uint32_t i, uint32_t bits) {
+  const uint32_t t3 = (uint32_t)c.T << 3;
+  uint32_t old = b.sflag[i];
+  for (;;) {
+    const uint32_t base = (old & ~7u) == t3 ? old : t3;
+    const uint32_t nw = base | bits;
+    if (nw == old) return;
+    const uint32_t prev = atomicCAS(&b.sflag[i], old, nw);
+    if (prev == old) {
+      if ((nw & (SF_SENT | SF_RECV)) == (SF_SENT | SF_RECV) && (base & (SF_SENT | SF_RECV)) != (SF_SENT | SF_RECV)) {
+        const uint32_t slot = snap_take(c, b, i);
+        b.snap_idx[i] = slot;
+        b.ack_snap[i] = slot;
+      }
+      return;
+    }
+    old = prev;
+  }
+}
+__device__ __forceinline__ bool sflag_has(const Ctx& c, const Bufs& b, uint32_t i, uint32_t bits) {
+  const uint32_t f = b.sflag[i];
+  return (f & ~7u) == ((uint32_t)c.T << 3) && (f & bits) == bits;
+}
+
+constexpr uint32_t SY_INLINE = 4;
+struct SyInbox {  // the SYNC (d2 = 0) or SYNC_ACK (d2 = 1) sub-phase's items and inboxes
+  SyncReq* items;
+  uint32_t* total;
+  uint32_t* cnt;
+  uint32_t* recv;
+  uint32_t* recv_cnt;
+  uint32_t* inl;
+  uint32_t* tab;
+  uint32_t* pool;
+  uint32_t* pg;
+};
+__device__ __forceinline__ SyInbox sy_inbox(const Bufs& b, int d2) {
+  SyInbox x;
+  if (!d2) {
+    x.items = b.reqs; x.total = &b.k->req_total; x.cnt = b.req_cnt; x.recv = b.req_recv;
+    x.recv_cnt = &b.k->req_recv_cnt; x.inl = b.rq_inl; x.tab = b.rq_tab; x.pool = b.rq_pool; x.pg = &b.k->req_pg;
+  } else {
+    x.items = b.acks; x.total = &b.k->ack_total; x.cnt = b.ack_cnt; x.recv = b.ack_recv;
+    x.recv_cnt = &b.k->ack_recv_cnt; x.inl = b.ack_inl; x.tab = b.ack_tab; x.pool = b.ack_pool; x.pg = &b.k->ack_pg;
+  }
+  return x;
+}
+// inbox pages of the SYNC sub-phases: allocated by the writer of the page's first slot, awaited by
+// the others (the same discipline as the gossip inboxes, inbox_page_alloc / _wait)
+__device__ inline uint32_t sy_page_alloc(const Ctx& c, const Bufs& b, const SyInbox& x, uint32_t i, uint32_t pg) {
+  if (pg >= b.sy_max) { set_err(c, ERR_REQS); return NONE; }
+  uint32_t np = atomicAdd(x.pg, 1u);
+  if (np >= b.sy_pool_cap) { set_err(c, ERR_REQS); np = PG_FAILED; }
+  __atomic_store_n(x.tab + (size_t)i * b.sy_max + pg, np, __ATOMIC_RELAXED);
+  return np == PG_FAILED ? NONE : np;
+}
+__device__ inline uint32_t sy_page_wait(const Ctx& c, const Bufs& b, const SyInbox& x, uint32_t i, uint32_t pg) {
+  if (pg >= b.sy_max) { set_err(c, ERR_REQS); return NONE; }
+  const uint32_t* e = x.tab + (size_t)i * b.sy_max + pg;
+  for (uint32_t it = 0; it < (1u << 20); ++it) {
+    const uint32_t v = __atomic_load_n(e, __ATOMIC_RELAXED);
+    if (v != NONE) return v == PG_FAILED ? NONE : v;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  set_err(c, ERR_REQS);
+  return NONE;
+}
+
+// a delivered SYNC / SYNC_ACK joins its receiver's inbox (the receiver is owned by this shard).
+// The item's classification counters start at zero here, before any classify launch adds to them.
+__device__ inline void enqueue_sync(const Ctx& c, const Bufs& b, int d2, SyncReq q, bool valid) {
+  const SyInbox x = sy_inbox(b, d2);
+  uint32_t it = NONE, s = 0, pid = NONE, r = 0;
+  if (valid) {
+    it = atomicAdd(x.total, 1u);
+    if (it >= b.req_cap) { set_err(c, ERR_REQS); valid = false; }
+  }
+  if (valid) {
+    r = q.to - c.lo;
+    s = atomicAdd(&x.cnt[r], 1u);
+    q.slot = s;
+    x.items[it] = q;
+    if (!d2) {
+      b.item_total[it] = 0;
+      b.rev_total[it] = 0;
+    } else {
+      b.ack_ctot[it] = 0;
+    }
+    if (s == 0) {
+      x.recv[atomicAdd(x.recv_cnt, 1u)] = q.to;
+      if (!d2) sflag_set(c, b, r, SF_RECV);
+    }
+    if (s < SY_INLINE) {
+      x.inl[(size_t)r * SY_INLINE + s] = it;
+      valid = false;  // placed
+    } else if (((s - SY_INLINE) & 63) == 0) {
+      pid = sy_page_alloc(c, b, x, r, (s - SY_INLINE) >> 6);
+    }
+  }
+  wave_order();
+  if (valid && ((s - SY_INLINE) & 63) != 0) pid = sy_page_wait(c, b, x, r, (s - SY_INLINE) >> 6);
+  if (valid && pid != NONE) x.pool[(size_t)pid * 64 + ((s - SY_INLINE) & 63)] = it;
 }
 
 __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t to, uint32_t ordinal, bool initial) {
@@ -1220,6 +1343,7 @@ __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t
   }
   if (!in_pass(c, to, v)) return;  // inbound-blocked at the receiver: silently dropped
   q.flags |= RQ_DELIVERED;
+  sflag_set(c, b, v - c.lo, owned(c, to) ? SF_SENT | SF_SENT_LOCAL : SF_SENT);
   if (!owned(c, to)) {  // content (this row) travels with the request: k_pack_rows
     const uint32_t d = owner(c, to);
     const uint32_t i = atomicAdd(&b.x->req[d], 1u);
@@ -1227,7 +1351,7 @@ __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t
     b.tx_reqs[(size_t)d * b.tx_req_cap + i] = q;
     return;
   }
-  enqueue_sync(c, q, b.reqs, &b.k->req_total, b.req_cnt, b.req_recv, &b.k->req_recv_cnt, b.req_cap);
+  enqueue_sync(c, b, 0, q, true);
 }
 
 // doSync (:339-357), FD-triggered SYNCs (:427-442) and start0's initial SYNC to every seed (:250-291)
@@ -1355,6 +1479,17 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, uint32_t n_rx_stops,
   const uint32_t* rx_stops = P->b.rx_stops;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (rebase) rebase_witness(c);
+  {  // this tick's content snapshots are released; the next tick's slot counter starts at zero
+    const Bufs& b = P->b;
+    const uint32_t par = (uint32_t)(T & 1);
+    const uint32_t ns = min(b.snap_cnt[par], b.snap_cap);
+    for (uint32_t q = i; q < ns; q += gridDim.x * blockDim.x) {
+      const uint32_t m = b.snap_list[par * b.snap_cap + q];
+      b.snap_idx[m] = NONE;
+      b.ack_snap[m] = NONE;
+    }
+    if (i == 0) b.snap_cnt[par ^ 1u] = 0;
+  }
   // collector blocks freed this tick become allocatable (one workgroup: the counters are read,
   // then rewritten, by the same threads)
   if (blockIdx.x == 0) {

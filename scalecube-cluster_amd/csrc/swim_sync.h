@@ -3,20 +3,24 @@
 //
 // syncMembership (MembershipProtocolImpl.java:491-509) runs updateMembership on every record of a
 // full table; with a 30 s sync interval N/300 members start a SYNC every tick, so the dominant cost
-// of a protocol period is streaming (content row, receiver row) pairs.  It is split in three:
+// of a protocol period is comparing (content row, receiver row) pairs.  Messages enter paged
+// per-receiver inboxes as they are collected (enqueue_sync), so a sub-phase needs no grouping pass:
 //
-//   k_sync_prep      one workgroup: group delivered messages by receiver, canonical inbox order,
-//                    snapshot claims for rows that are both read and merged into in this sub-phase
-//   k_sync_classify  the HBM stream: one wave per (message, 1,024-subject chunk), 16 subjects per
+//   k_sync_classify  the row stream: one wave per (message, 1,024-subject chunk), 16 subjects per
 //                    lane as four 16-B loads of record words per row (content row + receiver row =
 //                    8 B per subject), units whose two rows both equal the reference row there (the
 //                    exact block witness, Ctx.bdiff) skipped without a row load; a record is
 //                    "complex" unless updateMembership would provably do nothing; complex subjects of
-//                    a chunk are wave-scan compacted into a pool in subject order
-//   k_sync_apply     one workgroup per receiver: lane 0 runs the exact sequential updateMembership on
-//                    the complex subjects in (message, chunk, subject) order, then the ALIVE
-//                    admissions whose metadata fetch succeeded; a later message to a receiver whose
-//                    row already changed this sub-phase is re-classified in-workgroup.
+//                    a chunk are wave-scan compacted into a pool in subject order.  The SYNC launch
+//                    also classifies the SYNC_ACK direction of every local message, and copies the
+//                    content rows that need a snapshot (claimed during collection, sflag_set).
+//   k_sync_apply     one workgroup per receiver: its inbox in canonical (sender, ordinal) order (an
+//                    in-LDS rank sort of its few messages), then lane 0 runs the exact sequential
+//                    updateMembership on the complex subjects in (message, chunk, subject) order,
+//                    then the ALIVE admissions whose metadata fetch succeeded; a later message to a
+//                    receiver whose row already changed this sub-phase is re-classified in-workgroup.
+//                    The SYNC launch sends the SYNC_ACKs and snapshots the acker rows that the
+//                    SYNC_ACK sub-phase both reads and merges into.
 
 #ifndef CLS_MINWAVES
 #define CLS_MINWAVES 4  // waves per SIMD the classify kernels are register-limited to
@@ -37,6 +41,7 @@ constexpr int CLS_LOADS = SYNC_CHUNK / 256;      // 16-B record loads per lane p
 constexpr int APPLY_BLOCK = 256;
 constexpr int APPLY_CPT = 8;
 constexpr int APPLY_TILE = APPLY_BLOCK * APPLY_CPT;
+constexpr uint32_t SY_INBOX = 2048;  // messages one receiver's sub-phase inbox holds (sy_max x 64)
 
 // true unless updateMembership(r1 = content record) on the row record r0 provably changes nothing
 __device__ inline bool sync_complex(uint32_t r1, uint32_t r0, bool self) {
@@ -53,48 +58,20 @@ __device__ inline bool sync_complex(uint32_t r1, uint32_t r0, bool self) {
   return true;
 }
 
-__device__ inline void sort_reqs(SyncReq* a, uint32_t n) {
-  for (uint32_t i = 1; i < n; ++i) {
-    SyncReq x = a[i];
-    int32_t j = (int32_t)i - 1;
-    while (j >= 0 && (a[j].from > x.from || (a[j].from == x.from && a[j].ordinal > x.ordinal))) { a[j + 1] = a[j]; --j; }
-    a[j + 1] = x;
-  }
-}
-
-struct SubPhase {  // the SYNC (d2 = 0) or SYNC_ACK (d2 = 1) buffers
-  SyncReq* items;
-  uint32_t total;
-  uint32_t* recv;
-  uint32_t nrecv;
-  uint32_t* cnt;
-  uint32_t* start;
-  uint2* desc;
-  SyncReq* out;
-  uint32_t* nitems;
-};
-
-__device__ inline SubPhase sub_phase(const Bufs& b, int d2) {
-  SubPhase p;
-  if (!d2) {
-    p.items = b.reqs; p.total = min(b.k->req_total, b.req_cap); p.recv = b.req_recv; p.nrecv = b.k->req_recv_cnt;
-    p.cnt = b.req_cnt; p.start = b.req_start; p.desc = b.req_desc; p.out = b.reqs_out; p.nitems = &b.k->req_cursor;
-  } else {
-    p.items = b.acks; p.total = min(b.k->ack_total, b.req_cap); p.recv = b.ack_recv; p.nrecv = b.k->ack_recv_cnt;
-    p.cnt = b.ack_cnt; p.start = b.ack_start; p.desc = b.ack_desc; p.out = b.acks_out; p.nitems = &b.k->ack_cursor;
-  }
-  return p;
-}
-
 // SYNCs / SYNC_ACKs arriving from other shards (content row = rx_rows[k]) join their inboxes
+// (wave-uniform trip count: enqueue_sync's page discipline wants every lane of the wave)
 __global__ void k_recv_sync(KP, int d2, uint32_t nrx) {
   const Ctx c = pctx_sync(P, T);
   const Bufs b = P->b;
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nrx; k += gridDim.x * blockDim.x) {
-    SyncReq q = b.rx_reqs[k];
-    q.content = k;
-    if (!d2) enqueue_sync(c, q, b.reqs, &b.k->req_total, b.req_cnt, b.req_recv, &b.k->req_recv_cnt, b.req_cap);
-    else enqueue_sync(c, q, b.acks, &b.k->ack_total, b.ack_cnt, b.ack_recv, &b.k->ack_recv_cnt, b.req_cap);
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t k0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); k0 < nrx; k0 += gridDim.x * blockDim.x) {
+    const uint32_t k = k0 + lane;
+    SyncReq q{};
+    if (k < nrx) {
+      q = b.rx_reqs[k];
+      q.content = k;
+    }
+    enqueue_sync(c, b, d2, q, k < nrx);
   }
 }
 
@@ -129,206 +106,10 @@ __global__ void __launch_bounds__(256) k_pack_rows(Ctx c, const SyncReq* tx, uin
 }
 
 // the record row a SYNC / SYNC_ACK carries: received copy, snapshot, or the sender's live row
-__device__ __forceinline__ const uint32_t* sync_content(const Ctx& c, const Bufs& b, const SyncReq& q) {
+__device__ __forceinline__ const uint32_t* sync_content(const Ctx& c, const Bufs& b, const SyncReq& q, int d2) {
   if (q.content != NONE) return b.rx_rows + (size_t)q.content * c.n;
-  const uint32_t si = b.snap_idx[q.from - c.lo];
+  const uint32_t si = (d2 ? b.ack_snap : b.snap_idx)[q.from - c.lo];
   return si < b.snap_cap ? b.snap + (size_t)si * c.n : rec_row(c, q.from);
-}
-
-// k_sync_prep: the sub-phase's delivered messages -> one contiguous inbox per receiver in canonical
-// (sender, ordinal) order, snapshot claims for senders that are merged into in the same sub-phase.
-// Messages are staged in LDS (receivers found through an LDS hash, inbox order sorted as LDS index
-// permutations), so the single workgroup makes ~3 dependent rounds of global accesses instead of
-// one per step; sub-phases larger than the LDS stage take the global path.
-constexpr uint32_t PREP_CAP = 2048;    // messages (and receivers) staged in LDS
-constexpr uint32_t PREP_HASH = 4096;   // receiver hash slots (power of two, >= 2 x PREP_CAP)
-constexpr int PREP_BLOCK = 1024;
-
-__device__ __forceinline__ uint32_t prep_slot(uint32_t id) { return (id * 2654435761u) >> 20; }  // 12 bits
-
-__device__ __forceinline__ uint32_t prep_find(const uint32_t* hkey, const uint32_t* hval, uint32_t id) {
-  for (uint32_t h = prep_slot(id);; h = (h + 1) & (PREP_HASH - 1)) {
-    const uint32_t k = hkey[h];
-    if (k == id) return hval[h];
-    if (k == NONE) return NONE;
-  }
-}
-
-__device__ void sync_prep_global(const Ctx& c, const Bufs& b, const SubPhase& p, int d2) {
-  __shared__ uint32_t s_cursor;
-  const uint32_t tid = threadIdx.x, nt = blockDim.x;
-  if (tid == 0) s_cursor = 0;
-  __syncthreads();
-  // one contiguous inbox per receiver
-  for (uint32_t i = tid; i < p.nrecv; i += nt) {
-    const uint32_t r = p.recv[i] - c.lo;
-    p.start[r] = atomicAdd(&s_cursor, p.cnt[r]);
-    p.desc[i] = make_uint2(p.start[r], p.cnt[r]);
-  }
-  __syncthreads();
-  if (tid == 0) *p.nitems = s_cursor;
-  for (uint32_t i = tid; i < p.total; i += nt) {
-    const SyncReq q = p.items[i];
-    p.out[p.start[q.to - c.lo] + q.slot] = q;
-  }
-  __syncthreads();
-  // canonical order inside an inbox: (sender, ordinal)
-  for (uint32_t i = tid; i < p.nrecv; i += nt) {
-    const uint32_t r = p.recv[i] - c.lo;
-    sort_reqs(p.out + p.start[r], p.cnt[r]);
-  }
-  __syncthreads();
-  // message content = the sender's table when the message was prepared: a sender that is itself
-  // merged into during this sub-phase gets its row snapshotted
-  const uint32_t ni = s_cursor;
-  for (uint32_t i = tid; i < ni; i += nt) {
-    b.item_total[i] = 0;
-    if (!d2) b.rev_total[i] = 0;
-    if (p.out[i].content != NONE) continue;  // content arrived from another shard: already a copy
-    const uint32_t src = p.out[i].from, sl = src - c.lo;
-    if (p.cnt[sl] == 0) continue;
-    if (atomicCAS(&b.snap_idx[sl], NONE, NONE - 1) == NONE) {
-      const uint32_t slot = atomicAdd(b.snap_cnt, 1u);
-      if (slot >= b.snap_cap) { set_err(c, ERR_SNAP); b.snap_idx[sl] = NONE; continue; }
-      b.snap_list[slot] = src;
-      b.snap_idx[sl] = slot;
-    }
-  }
-  __syncthreads();
-  __threadfence_block();
-  // every message records its sender's snapshot slot (classify reads it with the header)
-  for (uint32_t i = tid; i < ni; i += nt) {
-    SyncReq& q = p.out[i];
-    q.snap = q.content != NONE ? NONE : b.snap_idx[q.from - c.lo];
-  }
-}
-
-__device__ void sync_prep_lds(const Ctx& c, const Bufs& b, const SubPhase& p, int d2) {
-  __shared__ SyncReq s_q[PREP_CAP];          // staged messages (64 KiB)
-  __shared__ uint32_t s_perm[PREP_CAP];      // inbox position -> staged message
-  __shared__ uint32_t s_rid[PREP_CAP];       // receiver index -> member
-  __shared__ uint32_t s_start[PREP_CAP + 1]; // receiver index -> message count, then inbox start
-  __shared__ uint32_t s_snap[PREP_CAP];      // receiver index -> snapshot slot of its row
-  __shared__ uint32_t s_hkey[PREP_HASH], s_hval[PREP_HASH];
-  __shared__ uint32_t s_wave[PREP_BLOCK / 64 + 1];
-  __shared__ uint32_t s_nsnap;
-  const uint32_t tid = threadIdx.x, nt = blockDim.x;
-  const uint32_t ni = p.total, nr = p.nrecv;
-  // release the previous sub-phase's snapshot claims; their loads overlap the staging loads
-  // (the claims below are made after several barriers; *snap_cnt is rewritten at the end)
-  const uint32_t prev = min(*b.snap_cnt, b.snap_cap);
-  for (uint32_t h = tid; h < PREP_HASH; h += nt) s_hkey[h] = NONE;
-  if (tid == 0) s_nsnap = 0;
-  __syncthreads();
-  const uint32_t rel = tid < prev ? b.snap_list[tid] : NONE;
-  for (uint32_t i = tid; i < ni; i += nt) s_q[i] = p.items[i];
-  for (uint32_t i = tid; i < nr; i += nt) {
-    const uint32_t id = p.recv[i];
-    s_rid[i] = id;
-    s_start[i] = p.cnt[id - c.lo];
-    s_snap[i] = NONE;
-    for (uint32_t h = prep_slot(id);; h = (h + 1) & (PREP_HASH - 1))
-      if (atomicCAS(&s_hkey[h], NONE, id) == NONE) { s_hval[h] = i; break; }
-  }
-  if (rel != NONE) b.snap_idx[rel - c.lo] = NONE;
-  for (uint32_t i = tid + nt; i < prev; i += nt) b.snap_idx[b.snap_list[i] - c.lo] = NONE;  // snap_cap > block
-  if (tid >= nr && tid < 2 * PREP_BLOCK) s_start[tid] = 0;  // scan padding
-  if (tid + PREP_BLOCK >= nr && tid + PREP_BLOCK < PREP_CAP) s_start[tid + PREP_BLOCK] = 0;
-  __syncthreads();
-  // inbox starts: exclusive scan of the counts, two receivers per thread
-  const uint32_t c0 = s_start[2 * tid], c1 = s_start[2 * tid + 1];
-  uint32_t total;
-  const uint32_t ex = block_exclusive_scan<PREP_BLOCK>(c0 + c1, s_wave, &total);
-  s_start[2 * tid] = ex;
-  s_start[2 * tid + 1] = ex + c0;
-  if (tid == 0) { s_start[nr] = total; *p.nitems = total; }
-  __syncthreads();
-  for (uint32_t i = tid; i < nr; i += nt) {
-    p.start[s_rid[i] - c.lo] = s_start[i];
-    p.desc[i] = make_uint2(s_start[i], s_start[i + 1] - s_start[i]);
-  }
-  for (uint32_t i = tid; i < ni; i += nt) {
-    const uint32_t ri = prep_find(s_hkey, s_hval, s_q[i].to);
-    s_perm[s_start[ri] + s_q[i].slot] = i;
-  }
-  __syncthreads();
-  // canonical order inside an inbox: (sender, ordinal)
-  for (uint32_t ri = tid; ri < nr; ri += nt) {
-    uint32_t* a = s_perm + s_start[ri];
-    const uint32_t k = s_start[ri + 1] - s_start[ri];
-    for (uint32_t x = 1; x < k; ++x) {
-      const uint32_t v = a[x];
-      const uint32_t vf = s_q[v].from, vo = s_q[v].ordinal;
-      int32_t y = (int32_t)x - 1;
-      while (y >= 0 && (s_q[a[y]].from > vf || (s_q[a[y]].from == vf && s_q[a[y]].ordinal > vo))) {
-        a[y + 1] = a[y];
-        --y;
-      }
-      a[y + 1] = v;
-    }
-  }
-  __syncthreads();
-  // snapshot claims: message content = the sender's table when the message was prepared; a sender
-  // that is itself merged into during this sub-phase gets its row snapshotted
-  for (uint32_t pos = tid; pos < total; pos += nt) {
-    const SyncReq& q = s_q[s_perm[pos]];
-    if (q.content != NONE) continue;  // content arrived from another shard: already a copy
-    const uint32_t rs = prep_find(s_hkey, s_hval, q.from);
-    if (rs == NONE || atomicCAS(&s_snap[rs], NONE, NONE - 1) != NONE) continue;
-    const uint32_t slot = atomicAdd(&s_nsnap, 1u);
-    if (slot >= b.snap_cap) { set_err(c, ERR_SNAP); s_snap[rs] = NONE; continue; }
-    s_snap[rs] = slot;
-    b.snap_list[slot] = q.from;
-    b.snap_idx[q.from - c.lo] = slot;
-  }
-  __syncthreads();
-  for (uint32_t pos = tid; pos < total; pos += nt) {
-    SyncReq q = s_q[s_perm[pos]];
-    uint32_t sn = NONE;
-    if (q.content == NONE) {
-      const uint32_t rs = prep_find(s_hkey, s_hval, q.from);
-      if (rs != NONE && s_snap[rs] < b.snap_cap) sn = s_snap[rs];
-    }
-    q.snap = sn;
-    p.out[pos] = q;
-    b.item_total[pos] = 0;
-    if (!d2) b.rev_total[pos] = 0;
-  }
-  if (tid == 0) *b.snap_cnt = min(s_nsnap, b.snap_cap);
-}
-
-// copy_snaps (SYNC_ACK sub-phase of an unsharded engine, where no classify launch streams the ack
-// rows): copy the claimed rows here, before any SYNC_ACK merge can change them
-__global__ void __launch_bounds__(PREP_BLOCK) k_sync_prep(KP, int d2, int copy_snaps) {
-  const Ctx c = pctx_sync(P, T);
-  const Bufs b = P->b;
-  const SubPhase p = sub_phase(b, d2);
-  const uint32_t tid = threadIdx.x, nt = blockDim.x;
-  if (p.total <= PREP_CAP && p.nrecv <= PREP_CAP) {
-    sync_prep_lds(c, b, p, d2);  // releases the previous sub-phase's snapshot claims itself
-  } else {
-    // release the previous sub-phase's snapshot claims
-    const uint32_t prev = min(*b.snap_cnt, b.snap_cap);
-    for (uint32_t i = tid; i < prev; i += nt) b.snap_idx[b.snap_list[i] - c.lo] = NONE;
-    __syncthreads();
-    if (tid == 0) *b.snap_cnt = 0;
-    __syncthreads();
-    sync_prep_global(c, b, p, d2);
-  }
-  if (!copy_snaps) return;
-  __syncthreads();
-  __threadfence_block();
-  const uint32_t ns = min(*b.snap_cnt, b.snap_cap), n = c.n;
-  for (uint32_t k = 0; k < ns; ++k) {
-    const uint32_t* src = rec_row(c, b.snap_list[k]);
-    uint32_t* dst = b.snap + (size_t)k * n;
-    if ((n & 3) == 0) {
-      for (uint32_t x = tid; x < n / 4; x += nt)
-        reinterpret_cast<uint4*>(dst)[x] = reinterpret_cast<const uint4*>(src)[x];
-    } else {
-      for (uint32_t x = tid; x < n; x += nt) dst[x] = src[x];
-    }
-  }
 }
 
 // One (message, chunk) unit per wave: 64 lanes x 16 subjects = SYNC_CHUNK subjects, i.e. four
@@ -348,10 +129,9 @@ struct ClsHdr {
   const uint32_t* rv;
   const uint32_t* bdc;  // block witness of the content row (local content only), else nullptr
   const uint32_t* bdv;  // block witness of the receiver row
-  uint32_t* snapdst;
   uint32_t i, r, s;
   uint32_t rev;  // d2 = 0: 1 = also classify the reverse direction (a local SYNC)
-  uint32_t d1;   // d2 = 1: the SYNC whose reverse classification this ack reuses, or NONE
+  uint32_t pad;  // d2 = 1: 1 + the SYNC whose reverse classification this ack may reuse, or 0
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -359,25 +139,19 @@ __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_re
 // the header is wave-uniform: keep it in scalar registers (the row loads need the VGPRs)
 // (speculative = true: message i may lie beyond the sub-phase's items, so nothing is read through
 // the header's ids; the SYNC_ACK reuse check is left out)
-__device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SubPhase& p, int d2, uint32_t i, ClsHdr& h,
-                                        bool speculative = false) {
-  SyncReq q = p.out[i];
-  q.from = uni(q.from); q.to = uni(q.to); q.content = uni(q.content); q.snap = uni(q.snap); q.pad = uni(q.pad);
+__device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SyInbox& p, int d2, uint32_t i, ClsHdr& h) {
+  SyncReq q = p.items[i];
+  q.from = uni(q.from); q.to = uni(q.to); q.content = uni(q.content); q.pad = uni(q.pad);
   const bool remote = q.content != NONE;
   h.content = remote ? b.rx_rows + (size_t)q.content * c.n : rec_row(c, q.from);
   h.rv = rec_row(c, q.to);
   h.bdc = remote ? nullptr : c.bdiff + (size_t)(q.from - c.lo) * c.blocks;
   h.bdv = c.bdiff + (size_t)(q.to - c.lo) * c.blocks;
-  h.snapdst = q.snap < b.snap_cap ? b.snap + (size_t)q.snap * c.n : nullptr;
   h.i = i;
   h.r = q.to;
   h.s = q.from;
   h.rev = (CLS_REV && !d2 && !remote) ? 1u : 0u;
-  h.d1 = NONE;
-  if (d2 && !speculative && q.pad != 0 && !remote) {
-    const uint32_t t = (uint32_t)c.T;
-    if (uni(b.row_mod[q.from - c.lo]) != t && uni(b.row_mod[q.to - c.lo]) != t) h.d1 = q.pad - 1;
-  }
+  h.pad = q.pad;
 }
 
 __device__ __forceinline__ void cls_rows(const Ctx& c, const ClsHdr& h, uint32_t ch, uint32_t lane, uint4* a, uint4* o) {
@@ -448,14 +222,6 @@ __device__ __forceinline__ bool lane_holds(uint32_t subject, uint32_t base, uint
   return off < SYNC_CHUNK && ((off & 255u) >> 2) == lane;
 }
 
-// a viewer's own subject x in the unit starting at base is complex even when both records equal ref
-// there (an identical LEAVING re-runs onSelfMemberDetected, sync_complex)
-__device__ __forceinline__ bool self_complex(const Ctx& c, uint32_t x, uint32_t base) {
-  if (x - base >= (uint32_t)SYNC_CHUNK) return false;
-  const uint32_t rf = c.ref[x];
-  return r_in_table(rf) && r_status(rf) == SWIM_LEAVING;
-}
-
 __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) x += __shfl_down(x, d, 64);
@@ -473,7 +239,9 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
   constexpr int d2 = D2;
   const Ctx c = pctx_sync(P, T);
   const Bufs b = P->b;
-  const SubPhase p = sub_phase(b, d2);
+  const SyInbox p = sy_inbox(b, d2);
+  uint2* const ichunk = d2 ? b.ack_chunk : b.item_chunk;
+  uint32_t* const itot = d2 ? b.ack_ctot : b.item_total;
   const uint32_t chunks = b.chunks, n = c.n;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (CLS_BLOCK / 64) + (threadIdx.x >> 6));
@@ -482,22 +250,45 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
   // speculatively, in parallel with the item count
   const uint32_t i0 = wid / chunks;
   ClsHdr hc;
-  if (i0 < b.req_cap) cls_hdr(c, b, p, d2, i0, hc, true);
-  const uint32_t ni = *p.nitems;
+  if (i0 < b.req_cap) cls_hdr(c, b, p, d2, i0, hc);
+  const uint32_t ni = min(*p.total, b.req_cap);
   const uint32_t total = ni * chunks;
   uint32_t cplx = 0, streamed = 0, skipped = 0;
   if (wid < total) {
-    if (d2) cls_hdr(c, b, p, d2, i0, hc);  // now a valid item: add the SYNC_ACK reuse check
     for (uint32_t u = wid; u < total; u += nw) {
       const uint32_t i = u / chunks;
       if (i != hc.i) cls_hdr(c, b, p, d2, i, hc);
       const uint32_t ch = u - i * chunks;
       const uint32_t base = ch * SYNC_CHUNK;
-      if (CLS_WITNESS && hc.d1 == NONE && !hc.snapdst && hc.bdc) {
-        const uint32_t dc = CLS_WITNESS == 3 ? 0u : uni(hc.bdc[ch]), dv = CLS_WITNESS == 3 ? 0u : uni(hc.bdv[ch]);
-        if ((dc | dv) == 0 && !self_complex(c, hc.r, base) && !(hc.rev && self_complex(c, hc.s, base))) {
+      // one batch of loads that depend only on the header: the receiver's snapshot slot (a SYNC
+      // receiver that also sent a SYNC this tick, sflag_set: this launch copies its row, streamed
+      // here before any merge, into the slot; the SYNC_ACK launch needs none), the SYNC_ACK reuse
+      // stamps, both block counts and the self subjects' ref words
+      const bool local = hc.bdc != nullptr;
+      const bool r_here = hc.r - base < (uint32_t)SYNC_CHUNK, s_here = hc.rev && hc.s - base < (uint32_t)SYNC_CHUNK;
+      uint32_t sn = NONE, rmf = 0, rmt = 0, dc = 1, dv = 1, rfr = 0, rfs = 0;
+      if (!d2) sn = b.snap_idx[hc.r - c.lo];
+      if (d2 && local && hc.pad) {
+        rmf = b.row_mod[hc.s - c.lo];
+        rmt = b.row_mod[hc.r - c.lo];
+      }
+      if (CLS_WITNESS && local) {
+        dc = hc.bdc[ch];
+        dv = hc.bdv[ch];
+      }
+      if (r_here) rfr = c.ref[hc.r];
+      if (s_here) rfs = c.ref[hc.s];
+      sn = uni(sn);
+      uint32_t* const snapdst = sn < b.snap_cap ? b.snap + (size_t)sn * c.n : nullptr;
+      const uint32_t t32 = (uint32_t)c.T;
+      const uint32_t d1 = (d2 && local && hc.pad && uni(rmf) != t32 && uni(rmt) != t32) ? hc.pad - 1 : NONE;
+      // an identical record on a viewer's own subject is complex when it is LEAVING (sync_complex)
+      const auto leaving = [](uint32_t rf) { return r_in_table(rf) && r_status(rf) == SWIM_LEAVING; };
+      if (CLS_WITNESS && d1 == NONE && !snapdst && local) {  // (a snapshot needs the row streamed)
+        if (CLS_WITNESS == 3) dc = dv = 0;
+        if ((uni(dc) | uni(dv)) == 0 && !(r_here && leaving(uni(rfr))) && !(s_here && leaving(uni(rfs)))) {
           if (lane == 0 && CLS_WITNESS != 2) {
-            b.item_chunk[(size_t)hc.i * chunks + ch] = make_uint2(0, 0);
+            ichunk[(size_t)hc.i * chunks + ch] = make_uint2(0, 0);
             if (hc.rev) b.rev_chunk[(size_t)hc.i * chunks + ch] = make_uint2(0, 0);
           }
           ++skipped;
@@ -505,25 +296,25 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
         }
       }
       uint4 a[CLS_LOADS], o[CLS_LOADS];
-      if (hc.d1 == NONE || hc.snapdst) cls_rows(c, hc, ch, lane, a, o);
-      if (hc.snapdst) {
+      if (d1 == NONE || snapdst) cls_rows(c, hc, ch, lane, a, o);
+      if (snapdst) {
 #pragma unroll
         for (int j = 0; j < CLS_LOADS; ++j) {
-          const uint32_t av[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
+          const uint32_t av[4] = {o[j].x, o[j].y, o[j].z, o[j].w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const uint32_t x = base + j * 256 + 4 * lane + q;
-            if (x < n) hc.snapdst[x] = av[q];
+            if (x < n) snapdst[x] = av[q];
           }
         }
       }
-      if (hc.d1 != NONE) {
+      if (d1 != NONE) {
         // SYNC_ACK whose classification the SYNC launch already made
         if (lane == 0) {
-          b.item_chunk[(size_t)hc.i * chunks + ch] = b.rev_chunk[(size_t)hc.d1 * chunks + ch];
+          ichunk[(size_t)hc.i * chunks + ch] = b.rev_chunk[(size_t)d1 * chunks + ch];
           if (ch == 0) {
-            const uint32_t t = b.rev_total[hc.d1];
-            b.item_total[hc.i] = t;
+            const uint32_t t = b.rev_total[d1];
+            itot[hc.i] = t;
             cplx += t;
           }
         }
@@ -555,8 +346,8 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
       }
       const uint2 res = cls_compact(c, b, flags, base, lane);
       if (lane == 0 && (!CLS_SKIPZERO || res.y)) {
-        b.item_chunk[(size_t)hc.i * chunks + ch] = res;
-        if (res.y) atomicAdd(&b.item_total[hc.i], res.y);
+        ichunk[(size_t)hc.i * chunks + ch] = res;
+        if (res.y) atomicAdd(&itot[hc.i], res.y);
       }
       cplx += res.y;
       if (hc.rev) {
@@ -625,23 +416,62 @@ __device__ void merge_row_wg(const Ctx& c, uint32_t v, const uint32_t* __restric
   }
 }
 
-// SYNC_ACK from `from` (the SYNC receiver) back to `to` (the SYNC sender)
-// `d1` = 1 + index of the SYNC being answered when its classify also classified this ack (0 = none)
-__device__ inline void add_ack(const Ctx& c, const Bufs& b, uint32_t to, uint32_t from, uint32_t rank, bool initial,
-                               uint32_t d1) {
-  SyncReq a;
-  a.from = from; a.to = to; a.ordinal = rank; a.slot = 0;
-  a.flags = RQ_DELIVERED | (initial ? RQ_INITIAL : 0) | (mem(c, from).table_size << RQ_RECS_SHIFT);
-  a.content = NONE; a.snap = NONE; a.pad = d1;
-  if (!owned(c, to)) {  // content (this row after the SYNC merges) travels with the ack
-    a.pad = 0;
-    const uint32_t d = owner(c, to);
-    const uint32_t i = atomicAdd(&b.x->ack[d], 1u);
-    if (i >= b.tx_req_cap) { set_err(c, ERR_REQS); return; }
-    b.tx_acks[(size_t)d * b.tx_req_cap + i] = a;
-    return;
+// one record row copied by the workgroup: 16-B accesses, 8 loads in flight per thread before the
+// stores (a row is 4 x N bytes; one load-store round trip per word would take hundreds of us)
+__device__ inline void copy_row(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t n) {
+  if ((n & 3) == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    const uint32_t n4 = n >> 2, step = blockDim.x * 8;
+    for (uint32_t x0 = threadIdx.x; x0 < n4; x0 += step) {
+      uint4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (x0 + j * blockDim.x < n4) v[j] = s4[x0 + j * blockDim.x];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (x0 + j * blockDim.x < n4) d4[x0 + j * blockDim.x] = v[j];
+    }
+  } else {
+    for (uint32_t x = threadIdx.x; x < n; x += blockDim.x) dst[x] = src[x];
   }
-  enqueue_sync(c, a, b.acks, &b.k->ack_total, b.ack_cnt, b.ack_recv, &b.k->ack_recv_cnt, b.req_cap);
+}
+
+// the receiver's inbox in canonical order (sender, ordinal) -> s_it (item indices); its page table
+// is reset for the next sub-phase.  Every thread of the workgroup calls it; returns the count.
+__device__ inline uint32_t load_inbox(const Ctx& c, const Bufs& b, const SyInbox& x, uint32_t r, uint32_t k,
+                                      uint32_t* s_it, uint64_t* s_key, uint32_t* s_raw) {
+  const uint32_t* inl = x.inl + (size_t)r * SY_INLINE;
+  const uint32_t* tab = x.tab + (size_t)r * b.sy_max;
+  if (k == 1) {  // the common inbox: nothing to order
+    if (threadIdx.x == 0) s_it[0] = inl[0];
+    __syncthreads();
+    return 1;
+  }
+  for (uint32_t q = threadIdx.x; q < k; q += blockDim.x) {
+    uint32_t it;
+    if (q < SY_INLINE) {
+      it = inl[q];
+    } else {
+      const uint32_t pid = tab[(q - SY_INLINE) >> 6];
+      it = pid < b.sy_pool_cap ? x.pool[(size_t)pid * 64 + ((q - SY_INLINE) & 63)] : NONE;
+    }
+    s_raw[q] = it;
+    const SyncReq rq = x.items[it < b.req_cap ? it : 0];
+    s_key[q] = it < b.req_cap ? (((uint64_t)rq.from << 32) | rq.ordinal) : ~0ull;  // unique per inbox
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < k; q += blockDim.x) {
+    const uint64_t key = s_key[q];
+    uint32_t rk = 0;
+    for (uint32_t j = 0; j < k; ++j) rk += s_key[j] < key ? 1u : 0u;
+    s_it[rk] = s_raw[q];
+  }
+  if (k > SY_INLINE)
+    for (uint32_t pg = threadIdx.x; pg < (k - SY_INLINE + 63) / 64; pg += blockDim.x)
+      x.tab[(size_t)r * b.sy_max + pg] = NONE;
+  __syncthreads();
+  return k;
 }
 
 // D1 (d2 = 0): onSync at each receiver, then its SYNC_ACKs.  D2 (d2 = 1): the SYNC_ACK merge at
@@ -657,14 +487,23 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
   __shared__ uint32_t s_mod;
   __shared__ unsigned long long s_recs;
   __shared__ uint32_t s_iP[APPLY_BLOCK], s_iS[APPLY_BLOCK], s_iR[APPLY_BLOCK];
-  const SubPhase p = sub_phase(b, d2);
+  __shared__ uint32_t s_it[SY_INBOX], s_raw[SY_INBOX];
+  __shared__ uint64_t s_key[SY_INBOX];
+  const SyInbox x = sy_inbox(b, d2);
+  const uint2* const ichunk = d2 ? b.ack_chunk : b.item_chunk;
+  const uint32_t* const itot = d2 ? b.ack_ctot : b.item_total;
   const uint32_t phase = d2 ? SWIM_PHASE_SYNCACK : SWIM_PHASE_SYNC;
   const uint32_t chunks = b.chunks;
+  const uint32_t nrecv = *x.recv_cnt;
   uint64_t* pend = b.pend + (size_t)blockIdx.x * c.n;
-  for (uint32_t i = blockIdx.x; i < p.nrecv; i += gridDim.x) {
-    const uint32_t s = p.recv[i];
-    const uint2 dsc = p.desc[i];  // loaded with the receiver id: no dependent cnt / start lookup
-    const uint32_t first = dsc.x, k = dsc.y;
+  for (uint32_t ri = blockIdx.x; ri < nrecv; ri += gridDim.x) {
+    const uint32_t s = x.recv[ri];
+    const uint32_t k = min(x.cnt[s - c.lo], SY_INBOX);
+    // s also sent SYNCs this tick (its roles are final since collection): its SYNC_ACKs' content
+    // is this row after the merges below, which its own SYNC_ACK merge may change while another
+    // merge reads it
+    const bool ack_snap = !d2 && sflag_has(c, b, s - c.lo, SF_SENT | SF_RECV);
+    load_inbox(c, b, x, s - c.lo, k, s_it, s_key, s_raw);
     if (threadIdx.x == 0) {
       mem(c, s).ev_minor = 0;
       mem(c, s).fetch_ctr = 0;
@@ -673,9 +512,11 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
     }
     __syncthreads();
     for (uint32_t q = 0; q < k; ++q) {
-      const SyncReq rq = p.out[first + q];
-      const uint32_t tot_q = b.item_total[first + q];  // issued with the header (stable since classify)
-      const uint32_t* content = sync_content(c, b, rq);
+      const uint32_t it = s_it[q];
+      if (it >= b.req_cap) continue;  // a page the pool could not give (ERR_REQS is set); uniform
+      const SyncReq rq = x.items[it];
+      const uint32_t tot_q = itot[it];  // issued with the header (stable since classify)
+      const uint32_t* content = sync_content(c, b, rq, d2);
       const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
       uint32_t npend = 0;
       const uint32_t mod = s_mod;
@@ -686,18 +527,18 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
         d1 = rq.pad - 1;
       __syncthreads();  // every lane has read s_mod before lane 0 may set it
       if (mod == 0 && (!own || d1 != NONE)) {  // precomputed classification is exact: the row is unchanged
-        const uint32_t it = d1 != NONE ? d1 : first + q;
-        const uint32_t tot = d1 != NONE ? b.rev_total[it] : tot_q;
+        const uint32_t at = d1 != NONE ? d1 : it;
+        const uint32_t tot = d1 != NONE ? b.rev_total[at] : tot_q;
         if (threadIdx.x == 0 && tot != 0) {
-          const uint2* ic = (d1 != NONE ? b.rev_chunk : b.item_chunk) + (size_t)it * chunks;
+          const uint2* ic = (d1 != NONE ? b.rev_chunk : ichunk) + (size_t)at * chunks;
           for (uint32_t ch = 0; ch < chunks; ++ch) {
             const uint2 e = ic[ch];
             if (e.y) s_mod = 1;
             for (uint32_t j = 0; j < e.y; ++j) {
-              const uint32_t x = b.pool[e.x + j];
-              const uint32_t a = content[x];
-              if (update_membership(c, s, x, r_status(a), r_inc(a), reason, phase))
-                pend[npend++] = ((uint64_t)x << 32) | (uint32_t)r_inc(a);
+              const uint32_t xs = b.pool[e.x + j];
+              const uint32_t a = content[xs];
+              if (update_membership(c, s, xs, r_status(a), r_inc(a), reason, phase))
+                pend[npend++] = ((uint64_t)xs << 32) | (uint32_t)r_inc(a);
             }
           }
         }
@@ -711,26 +552,58 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       }
       __syncthreads();
     }
+    if (!d2) {
+      // the SYNC_ACKs, one thread per inbox message: the enqueues are independent (the receiver
+      // orders its inbox), the loss draws keyed by the message's rank q
+      const uint32_t tsz = mem(c, s).table_size;
+      for (uint32_t q0 = 0; q0 < k; q0 += blockDim.x) {
+        const uint32_t q = q0 + threadIdx.x;
+        bool valid = false;
+        SyncReq a{};
+        if (q < k && s_it[q] < b.req_cap) {
+          const uint32_t it = s_it[q];
+          const SyncReq rq = x.items[it];
+          if (!out_fail(c, s, rq.from, s, SWIM_STREAM_SYNCACK_OUT, q, 0) && in_pass(c, rq.from, s)) {
+            a.from = s; a.to = rq.from; a.ordinal = q; a.slot = 0;
+            a.flags = RQ_DELIVERED | (rq.flags & RQ_INITIAL) | (tsz << RQ_RECS_SHIFT);
+            a.content = NONE; a.snap = NONE; a.pad = CLS_REV && rq.content == NONE ? it + 1 : 0;
+            valid = true;
+            if (!owned(c, rq.from)) {  // content (this row after the SYNC merges) travels with the ack
+              a.pad = 0;
+              const uint32_t d = owner(c, rq.from);
+              const uint32_t i = atomicAdd(&b.x->ack[d], 1u);
+              if (i < b.tx_req_cap) b.tx_acks[(size_t)d * b.tx_req_cap + i] = a; else set_err(c, ERR_REQS);
+              valid = false;
+            }
+          }
+        }
+        enqueue_sync(c, b, 1, a, valid);
+      }
+    }
     if (threadIdx.x == 0) {
       if (!d2) {
-        for (uint32_t q = 0; q < k; ++q) {
-          const SyncReq rq = p.out[first + q];
-          if (out_fail(c, s, rq.from, s, SWIM_STREAM_SYNCACK_OUT, q, 0)) continue;
-          if (!in_pass(c, rq.from, s)) continue;
-          add_ack(c, b, rq.from, s, q, (rq.flags & RQ_INITIAL) != 0, CLS_REV && rq.content == NONE ? first + q + 1 : 0);
-        }
         if (s_mod) b.row_mod[s - c.lo] = (uint32_t)c.T;  // invalidates the reverse classifications
+        // s holds a snapshot (it also sent SYNCs: its own SYNC_ACK merges may change its row while
+        // another merge reads its SYNC_ACK content): classify filled the slot with the row before
+        // this workgroup's merges; if they changed it, the SYNC_ACK content gets a slot of its own
+        s_list[0] = NONE;
+        if (ack_snap && s_mod) {
+          s_list[0] = snap_take(c, b, s - c.lo);
+          b.ack_snap[s - c.lo] = s_list[0];
+        }
       } else {
         // start0's initial-sync completion counts the acks of its INITIAL SYNCs (:270-284)
         uint32_t init = 0;
-        for (uint32_t q = 0; q < k; ++q) init += (p.out[first + q].flags & RQ_INITIAL) ? 1u : 0u;
+        for (uint32_t q = 0; q < k; ++q)
+          init += (s_it[q] < b.req_cap && (x.items[s_it[q]].flags & RQ_INITIAL)) ? 1u : 0u;
         mem(c, s).init_done += init;
         stat_add(c, ST_SYNC_ACKS, k);
       }
-      p.cnt[s - c.lo] = 0;
+      x.cnt[s - c.lo] = 0;
       stat_add(c, ST_SYNC_RECORDS, s_recs);
     }
     __syncthreads();
+    if (!d2 && s_list[0] < b.snap_cap) copy_row(rec_row(c, s), b.snap + (size_t)s_list[0] * c.n, c.n);
     // this sub-phase's pingMembers inserts of s (its ADDED events, all made by this workgroup)
     apply_ins_batch<APPLY_BLOCK, true>(c, s, threadIdx.x, s_iP, s_iS, s_iR);
   }
