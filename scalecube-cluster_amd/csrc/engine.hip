@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -155,7 +156,8 @@ struct Shard {
 
 struct swim_engine {
   swim_config cfg{};
-  bool debug_sync = false;  // SWIM_DEBUG_SYNC=1: synchronise after every tick kernel and name a faulting one
+  int debug_sync = 0;  // SWIM_DEBUG_SYNC=1: synchronise after every tick kernel and name a faulting one
+  std::chrono::steady_clock::time_point debug_t{};
   int32_t device = 0;
   uint32_t n = 0, tick_ms = 0, P = 0, G = 0, S = 0, sz = 0;
   uint64_t T = 0;
@@ -509,14 +511,23 @@ static void sync_params(swim_engine* e, Shard& sd) {
 }
 
 
-// SWIM_DEBUG_SYNC=1: synchronise after each tick kernel so a device fault names its kernel
+// SWIM_DEBUG_SYNC=1: synchronise after each tick kernel so a device fault names its kernel;
+// SWIM_DEBUG_SYNC=2 also names every kernel that took longer than 20 ms (wall, after the sync)
+static void debug_slow(swim_engine* e, const char* name, uint64_t T);
 #define TICK_CHECK(name)                                                                            \
   do {                                                                                              \
     if (e->debug_sync && hipStreamSynchronize(s) != hipSuccess) {                                   \
       std::fprintf(stderr, "libswimgpu: %s faulted at tick %llu\n", name, (unsigned long long)T);  \
       return SWIM_EDEVICE;                                                                          \
     }                                                                                               \
+    if (e->debug_sync > 1) debug_slow(e, name, T);                                                  \
   } while (0)
+static void debug_slow(swim_engine* e, const char* name, uint64_t T) {
+  const auto now = std::chrono::steady_clock::now();
+  const double ms = std::chrono::duration<double, std::milli>(now - e->debug_t).count();
+  if (ms > 20.0) std::fprintf(stderr, "libswimgpu: %s took %.1f ms at tick %llu\n", name, ms, (unsigned long long)T);
+  e->debug_t = now;
+}
 
 // One tick: 7 kernels per shard (11 on gossip ticks); a sharded engine adds k_recv_* and three exchanges.
 static int32_t run_tick(swim_engine* e) {
@@ -677,7 +688,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   const uint32_t nl = c.nl;
   c.gcap = cf.gossip_capacity ? cf.gossip_capacity : 1024;
   c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 4096);
-  // spilled collectors by tier (6 / 62 / 510 / 2,046 intervals); blocks are recycled, so these
+  // spilled collectors by tier (6 / 62 / 510 / 16,382 intervals); blocks are recycled, so these
   // bound the collectors spilled at once, not over the run
   const uint64_t icap = cf.interval_capacity ? cf.interval_capacity : 64;  // tier-0 blocks per row
   const uint64_t rows = std::max(nl, 1u);
@@ -714,14 +725,18 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.ins_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 22, 256ull * nl));
   b.msg_cap = cf.message_capacity ? cf.message_capacity
                                  : (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 512ull * nl));
-  // inbox pages: the message capacity in 64-message pages, plus one partial page per receiver and
-  // slack for racing first touches; a receiver's inbox may span up to pg_max pages (4x its even share)
-  b.pg_cap = (uint32_t)std::min<uint64_t>(1ull << 26, (uint64_t)b.msg_cap / 64 + nl + 4096);
-  b.pg_max = (uint32_t)std::min<uint64_t>(1u << 16, std::max<uint64_t>(4, next_pow2((uint32_t)std::min<uint64_t>(
-                                              1u << 30, 4ull * b.msg_cap / 64 / std::max(nl, 1u)))));
+  // inbox pages: the message capacity in 64-message pages plus one partial page per receiver; one
+  // receiver's inbox may span pg_max pages: 64x its even share of the capacity, at least 512 pages
+  // (32 Ki messages: a storm's inboxes are uneven), at most the whole pool
+  b.pg_cap = (uint32_t)std::min<uint64_t>(1ull << 26, (uint64_t)b.msg_cap / 64 + nl + 64);
+  b.pg_max = (uint32_t)std::min<uint64_t>(b.pg_cap, std::max<uint64_t>(512, next_pow2((uint32_t)std::min<uint64_t>(
+                                              1u << 30, 64ull * b.msg_cap / 64 / std::max(nl, 1u)))));
+  b.pg_max = std::min<uint32_t>(b.pg_max, 1u << 14);
   b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
   b.wave_min = cf.deliver_wave_min ? std::min<uint32_t>(cf.deliver_wave_min, DLV_SORT) : (uint32_t)DLV_SORT;
-  b.snap_cap = 256;
+  // snapshot rows for members that both send and receive a SYNC in one sub-phase: a few per tick in
+  // steady state, up to every member right after a partition heals; at most 1 GiB of rows
+  b.snap_cap = std::max(1u, std::min(nl, std::max(256u, (uint32_t)((1ull << 28) / std::max(n, 1u)))));
   b.sy_max = (SY_INBOX - SY_INLINE + 63) / 64;
   b.sy_pool_cap = b.req_cap / 64 + std::min(nl, b.req_cap) + 64;
   b.chunks = (n + SYNC_CHUNK - 1) / SYNC_CHUNK;
@@ -856,7 +871,7 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
   e->cfg = cf;
   {
     const char* d = std::getenv("SWIM_DEBUG_SYNC");
-    e->debug_sync = d && d[0] == '1';
+    e->debug_sync = d && (d[0] == '1' || d[0] == '2') ? d[0] - '0' : 0;
   }
   e->device = cf.device;
   e->n = capacity;

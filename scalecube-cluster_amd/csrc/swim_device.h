@@ -34,6 +34,7 @@ enum : uint32_t {
   ERR_FDSYNC = 1u << 8, ERR_INS = 1u << 9, ERR_REQS = 1u << 10, ERR_PEND = 1u << 11, ERR_INC = 1u << 12,
   ERR_PAGES = 1u << 13,  // the gossip inbox page pool ran dry
   ERR_INBOX = 1u << 14,  // one receiver's gossip inbox outgrew its page table
+  ERR_COLL_TOP = 1u << 15,  // a collector outgrew the top spill tier (ERR_INTERVALS: a tier's pool ran dry)
 };
 
 // stats slots (swim_stats order)
@@ -83,7 +84,7 @@ __device__ __forceinline__ bool gossip_infected(const GossipDev& g, uint32_t m) 
 // SequenceIdCollector (SequenceIdCollector.java) of (viewer, gossiper), 16 B: a collector holds one
 // interval almost always (a gossiper's sequence ids reach a member in order), so the interval is
 // inline.  One that needs more (out-of-order arrival, loss) spills to a block of a size tier —
-// 6, 62, 510 or 2,046 closed intervals (64 B .. 16 KiB: a 4-word header {count} + (lo, hi) pairs,
+// 6, 62, 510 or 16,382 closed intervals (64 B .. 128 KiB: a 4-word header {count} + (lo, hi) pairs,
 // ascending) — grows tier by tier, and returns inline when its intervals merge back into one.
 // The reference keeps up to gossipSegmentationThreshold (1,000) intervals before a gossip round
 // clears the collector (checkGossipSegmentation, GossipProtocolImpl.java:217-236); the top tier
@@ -95,7 +96,7 @@ struct CollEnt {
                   // bits 4..5: spill tier; bits 8..31: block index in the tier
 };
 constexpr uint32_t COLL_SPILLED = 7u, COLL_CLEARED = 8u;
-__host__ __device__ constexpr uint32_t tier_cap(int t) { return t == 0 ? 6u : t == 1 ? 62u : t == 2 ? 510u : 2046u; }
+__host__ __device__ constexpr uint32_t tier_cap(int t) { return t == 0 ? 6u : t == 1 ? 62u : t == 2 ? 510u : 16382u; }
 __host__ __device__ constexpr uint32_t tier_words(int t) { return 4u + 2u * tier_cap(t); }
 struct SpillCtl {  // one per tier
   uint32_t bump;    // blocks ever carved from the pool
@@ -517,7 +518,7 @@ __device__ inline bool coll_add(const Ctx& c, CollEnt* e, uint32_t x, uint32_t* 
   } else {
     const int t = (int)((meta >> 4) & 3u);
     if (n == (t == 0 ? tier_cap(0) : t == 1 ? tier_cap(1) : t == 2 ? tier_cap(2) : tier_cap(3))) {  // grow
-      if (t + 1 == NTIER) { set_err(c, ERR_INTERVALS); return true; }
+      if (t + 1 == NTIER) { set_err(c, ERR_COLL_TOP); return true; }
       const uint32_t i = spill_alloc(c, t + 1);
       if (i == NONE) return true;
       uint32_t* nb = tier_sel(c.spill, t + 1) + (size_t)i * tier_words_d(t + 1);

@@ -975,8 +975,9 @@ __device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Buf
   auto perm_at = [&](uint32_t q) -> uint32_t& { return b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)]; };
   unsigned long long acc = 0;
   bool pages_ok = true;
-  for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) pages_ok &= pt[pg] != NONE;
-  pages_ok = __ballot(!pages_ok) == 0;  // a page the pool could not give (ERR_MSGS is set)
+  // a page the pool could not give holds NONE or PG_FAILED (ERR_PAGES / ERR_INBOX are set)
+  for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) pages_ok &= pt[pg] < b.pg_cap;
+  pages_ok = __ballot(!pages_ok) == 0;
   if (c.up[r] && k && pages_ok) {
     // pass 1: distinct senders and their message counts
     uint32_t nd = 0;
@@ -1148,8 +1149,8 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
         const uint32_t pid = *pt;
         *pt = NONE;
         if (!c.up[r]) {
-        } else if (pid == NONE) {  // the page pool ran dry (ERR_MSGS is set)
-          set_err(c, ERR_MSGS);
+        } else if (pid >= b.pg_cap) {  // NONE or PG_FAILED: the page pool ran dry (ERR_PAGES is set)
+          set_err(c, ERR_PAGES);
         } else {
           const GMsgFull* a = b.pg_msgs + (size_t)pid * 64;
           for (uint32_t q = 0; q < k; ++q) {

@@ -22,6 +22,14 @@ sys.path.insert(0, os.path.join(REPO, "scalecube-cluster_amd"))
 sys.path.insert(0, REPO)
 
 
+def converged(e, sample):
+    ok = 0
+    for m in sample:
+        row = e.read_view(m)
+        ok += int((((row >> 34) & 1) == 1).all() and (((row >> 32) & 3) == 0).all())
+    return ok
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("workload", choices=("partition", "churn"))
@@ -29,8 +37,11 @@ def main():
     ap.add_argument("--periods", type=int, default=6)
     ap.add_argument("--hold", type=int, default=None)
     ap.add_argument("--after", type=int, default=40)
+    ap.add_argument("--stop-converged", action="store_true", help="partition: stop once the sample has converged")
     ap.add_argument("--gossip-capacity", type=int, default=1 << 17)
     ap.add_argument("--sample", type=int, default=16)
+    ap.add_argument("--interval-capacity", type=int, default=1024)
+    ap.add_argument("--message-capacity", type=int, default=1 << 28)
     args = ap.parse_args()
     import swimgpu
     from swimgpu import abi
@@ -40,10 +51,12 @@ def main():
     cfg = abi.default_config(lib, 0, sync_stagger=1, record_fd_events=0)
     cfg.gossip_capacity = args.gossip_capacity
     cfg.event_capacity = 1 << 26
-    cfg.message_capacity = 1 << 28
+    cfg.message_capacity = args.message_capacity
     cfg.collector_capacity = 1 << (2 * n - 1).bit_length()
-    cfg.interval_capacity = 1024
-    cfg.timer_capacity = 64 * n
+    cfg.interval_capacity = args.interval_capacity
+    # a partition puts a suspicion timer for every member of the other side at every viewer, falling
+    # due within the few ticks the SUSPECT gossip took to spread
+    cfg.timer_capacity = max(64 * n, n * n // 8)
     sample = [int(x) for x in np.linspace(0, n - 1, args.sample)]
     if args.workload == "churn":
         sch = bench.Schedule("churn", n, args.periods)
@@ -93,6 +106,9 @@ def main():
                           "removed": int((ev["type"] == abi.EV_REMOVED).sum()) if len(ev) else 0,
                           "max_live_gossips": glen}), flush=True)
         prev = st
+        if args.workload == "partition" and args.stop_converged and p + 1 > heal and converged(e, sample) == len(sample):
+            print(json.dumps({"converged_at_period": p + 1}), flush=True)
+            break
     if args.workload == "partition":
         ok = 0
         for m in sample:
