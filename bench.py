@@ -113,6 +113,25 @@ def make_config(lib, device=0):
     return abi.default_config(lib, 0, sync_stagger=1, record_fd_events=0, device=device)
 
 
+def churn_capacities(cfg, capacity):
+    """Config-3 churn sizes (also used by tests/test_gpu_configs.py).  A period's joins add every
+    joiner at every viewer (millions of events); every member holds every gossip of the last
+    periodsToSweep periods, and every member that learns news through SYNC gossips it (DESIGN.md §6:
+    the live gossips per member grow by ~8 x N per period); a period's kills put a suspicion timer
+    at every viewer within a few seconds."""
+    cfg.event_capacity = 1 << 25
+    cfg.gossip_capacity = 1 << 17
+    # one gossip round's GOSSIP_REQs: ~4 x 10^8 in the third period at N = 16,384
+    cfg.message_capacity = 1 << 30 if capacity > 12288 else 1 << 28
+    # a viewer keeps a SequenceIdCollector per gossiper heard until it is removed
+    cfg.collector_capacity = 1 << (2 * capacity - 1).bit_length()
+    # 5 % loss drops gossips, so collectors fragment (many spilled interval blocks), and every
+    # false suspicion puts a timer at every viewer
+    cfg.interval_capacity = 8192
+    cfg.timer_capacity = 64 * capacity
+    return cfg
+
+
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this bench
     (tools/profile.sh -> tools/prof_summary.py -> profiles/<round>_<workload>_pmc.json: separate
@@ -211,19 +230,8 @@ def main():
     cfg = make_config(lib, local_rank)
     cfg.gossip_capacity = args.gossip_capacity
     if args.workload == "churn":
-        # config-3 churn sizes: a period's joins add every joiner at every viewer (millions of
-        # events); every member holds the gossips of its last ~18 s; a period's kills put a suspicion
-        # timer at every viewer within a few seconds
-        cfg.event_capacity = 1 << 25
-        cfg.gossip_capacity = max(cfg.gossip_capacity, 65536)
-        cfg.message_capacity = 1 << 28
-        # a viewer keeps a SequenceIdCollector per gossiper heard until it is removed, and every
-        # member that learns news through SYNC gossips it: in a long churn run that is most members
-        cfg.collector_capacity = 1 << (2 * sch.capacity - 1).bit_length()
-        # 5 % loss drops gossips, so collectors fragment (many spilled interval blocks), and every
-        # false suspicion puts a timer at every viewer
-        cfg.interval_capacity = 4096
-        cfg.timer_capacity = 64 * sch.capacity
+        churn_capacities(cfg, sch.capacity)
+        cfg.gossip_capacity = max(cfg.gossip_capacity, args.gossip_capacity)
     cfg.local_shards = args.local_shards
     se = None
     if world > 1:

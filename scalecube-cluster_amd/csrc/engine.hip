@@ -688,6 +688,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   const uint32_t nl = c.nl;
   c.gcap = cf.gossip_capacity ? cf.gossip_capacity : 1024;
   c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 4096);
+  c.gix_mask = next_pow2(2 * c.gcap) - 1;
   // spilled collectors by tier (6 / 62 / 510 / 16,382 intervals); blocks are recycled, so these
   // bound the collectors spilled at once, not over the run
   const uint64_t icap = cf.interval_capacity ? cf.interval_capacity : 64;  // tier-0 blocks per row
@@ -734,9 +735,10 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.pg_max = std::min<uint32_t>(b.pg_max, 1u << 14);
   b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
   b.wave_min = cf.deliver_wave_min ? std::min<uint32_t>(cf.deliver_wave_min, DLV_SORT) : (uint32_t)DLV_SORT;
-  // snapshot rows for members that both send and receive a SYNC in one sub-phase: a few per tick in
+  // snapshot rows for members that both send and receive a SYNC in one tick (at most two each: the
+  // SYNC content and, when its merges changed the row, the SYNC_ACK content): a few per tick in
   // steady state, up to every member right after a partition heals; at most 1 GiB of rows
-  b.snap_cap = std::max(1u, std::min(nl, std::max(256u, (uint32_t)((1ull << 28) / std::max(n, 1u)))));
+  b.snap_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2ull * nl, std::max<uint64_t>(256, (1ull << 28) / std::max(n, 1u))));
   b.sy_max = (SY_INBOX - SY_INLINE + 63) / 64;
   b.sy_pool_cap = b.req_cap / 64 + std::min(nl, b.req_cap) + 64;
   b.chunks = (n + SYNC_CHUNK - 1) / SYNC_CHUNK;
@@ -751,7 +753,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.blocks = (n + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
   bool ok = sd.alloc(&c.recs, nn) && sd.alloc(&c.aux, nn) && sd.alloc(&c.ref, n) && sd.alloc(&c.dirty, n) &&
             sd.alloc(&c.bdiff, (size_t)std::max(nl, 1u) * c.blocks) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
-            sd.alloc(&c.remote, nn) && sd.alloc(&c.slab, (size_t)nl * c.gcap) && sd.alloc(&c.coll, (size_t)nl * c.hcap) &&
+            sd.alloc(&c.remote, nn) && sd.alloc(&c.slab, (size_t)nl * c.gcap) &&
+            sd.alloc(&c.gix, (size_t)nl * (c.gix_mask + 1)) && sd.alloc(&c.coll, (size_t)nl * c.hcap) &&
             sd.alloc(&c.spill[0], (size_t)c.spill_cap[0] * tier_words(0)) &&
             sd.alloc(&c.spill[1], (size_t)c.spill_cap[1] * tier_words(1)) &&
             sd.alloc(&c.spill[2], (size_t)c.spill_cap[2] * tier_words(2)) &&

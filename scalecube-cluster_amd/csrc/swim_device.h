@@ -5,6 +5,7 @@
 //   ping    u32[N][N]   FailureDetectorImpl.pingMembers of each viewer (ArrayList order)
 //   remote  u32[N][N]   GossipProtocolImpl.remoteMembers of each viewer
 //   slab    GossipDev[N][gcap]  live GossipStates, insertion order
+//   gix     u32[N][2 gcap]      lazily built (gossiper, seq) -> slab serial index (gix_find)
 //   coll    CollEnt[N][hcap]    SequenceIdCollector per (viewer, gossiper), open addressing, one
 //                               interval inline; more spill to size-tiered interval blocks
 //   mem     MemberDev[N]        scalar per-member protocol state
@@ -60,7 +61,8 @@ struct alignas(16) MemberDev {
   uint32_t gossip_len, table_size, members_size, leave_gossiper;
   uint32_t ev_minor, fetch_ctr, fd_sync_cnt, init_total, init_done;
   uint32_t ins_rank, ins_head, ins_tail;  // this phase's deferred pingMembers inserts (op chain)
-  uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, pad[2];
+  uint32_t gix_base, gix_used;  // serial of slab[0]; gix slots taken since the index was (re)built
+  uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, gix_valid, pad;
 };
 
 // GossipState + Gossip + MembershipRecord payload, 48 B.  GossipState.infected gains a member only
@@ -179,6 +181,8 @@ struct Ctx {
   uint32_t* ping;
   uint32_t* remote;
   GossipDev* slab;
+  uint32_t* gix;       // [nl][gix_mask + 1] slab serials by (gossiper, seq), open addressing
+  uint32_t gix_mask;
   CollEnt* coll;       // [nl][hcap] open addressing by gossiper
   uint32_t* spill[NTIER];        // spilled collectors: tier t holds spill_cap[t] blocks of tier_words(t)
   uint32_t* spill_avail[NTIER];  // recyclable block indices
@@ -659,6 +663,57 @@ __device__ __forceinline__ uint32_t next_minor(const Ctx& c, uint32_t v, uint32_
   return phase == SWIM_PHASE_TIMERS ? s : mem(c, v).ev_minor++;
 }
 
+// ------------------------------------------------------------------------------- slab index
+// GossipProtocolImpl.gossips.get(gossipId) (:206) is only needed when the member's collector of the
+// gossiper was cleared (otherwise the collector proves the gossip new), so the index is built the
+// first time a member needs it and kept up from then on.  It maps (gossiper, seq) to the gossip's
+// slab serial (insertion number; slab[p] has serial gix_base + p): the sweep drops a prefix of the
+// slab (infection periods grow along it), which only advances gix_base, and a slot whose serial fell
+// below gix_base is free again.  Rebuilt from the slab when half its slots have been taken.
+__device__ __forceinline__ uint32_t gix_hash(uint32_t g, uint32_t s) { return hash32(g * 0x9e3779b9u ^ s); }
+__device__ __forceinline__ uint32_t* gix_of(const Ctx& c, uint32_t v) {
+  return c.gix + (size_t)(v - c.lo) * (c.gix_mask + 1);
+}
+__device__ inline void gix_put(const Ctx& c, MemberDev& m, uint32_t* ix, uint32_t g, uint32_t s, uint32_t serial) {
+  const uint32_t mask = c.gix_mask;
+  uint32_t h = gix_hash(g, s);
+  for (uint32_t i = 0; i <= mask; ++i, ++h) {
+    const uint32_t e = ix[h & mask];
+    if (e == NONE || e - m.gix_base >= m.gossip_len) {  // empty, or a swept gossip's slot
+      if (e == NONE) m.gix_used++;
+      ix[h & mask] = serial;
+      return;
+    }
+  }
+  m.gix_valid = 0;  // unreachable at <= half load
+}
+// a gossip was appended at slab position gossip_len - 1
+__device__ __forceinline__ void gix_note(const Ctx& c, MemberDev& m, uint32_t v, uint32_t g, uint32_t s) {
+  if (!m.gix_valid) return;
+  if (2 * m.gix_used >= c.gix_mask + 1) { m.gix_valid = 0; return; }
+  gix_put(c, m, gix_of(c, v), g, s, m.gix_base + m.gossip_len - 1);
+}
+// slab position of (g, s), or -1
+__device__ inline int32_t gix_find(const Ctx& c, MemberDev& m, uint32_t v, const GossipDev* slab, uint32_t g,
+                                   uint32_t s) {
+  uint32_t* ix = gix_of(c, v);
+  const uint32_t mask = c.gix_mask;
+  if (!m.gix_valid) {
+    for (uint32_t i = 0; i <= mask; ++i) ix[i] = NONE;
+    m.gix_used = 0;
+    m.gix_valid = 1;
+    for (uint32_t p = 0; p < m.gossip_len; ++p) gix_put(c, m, ix, slab[p].gossiper, slab[p].seq, m.gix_base + p);
+  }
+  uint32_t h = gix_hash(g, s);
+  for (uint32_t i = 0; i <= mask; ++i, ++h) {
+    const uint32_t e = ix[h & mask];
+    if (e == NONE) return -1;
+    const uint32_t p = e - m.gix_base;
+    if (p < m.gossip_len && slab[p].gossiper == g && slab[p].seq == s) return (int32_t)p;
+  }
+  return -1;
+}
+
 // ------------------------------------------------------------------------------- gossip origination
 // spreadMembershipGossip (MembershipProtocolImpl.java:845-860) -> createAndPutGossip (GossipProtocolImpl.java:190-199)
 __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject, uint32_t status, int32_t inc) {
@@ -675,6 +730,7 @@ __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject,
   for (int k = 0; k < GINF; ++k) g.inf[k] = NONE;
   slab_of(c, v)[m.gossip_len] = g;
   m.gossip_len++;
+  gix_note(c, m, v, g.gossiper, g.seq);
   m.g_counter++;
   CollEnt* e = coll_ensure(c, v, v);
   if (coll_add(c, e, g.seq, &c.seg_flag[v - c.lo])) receipt_mark(c, v, v, g.seq);

@@ -546,6 +546,8 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   unsigned long long nmsg = 0;
   uint32_t pseq = 0;  // lane j < nt: messages materialised to target j so far (GMsgFull.pseq)
   uint32_t w = 0;     // sweep: survivors so far
+  uint32_t lead = 0;  // sweep: entries before the first survivor
+  bool seen_keep = false;
   bool done = false;
   // lane = slab position: one GossipState read serves all nt targets, whose loss draws and
   // receiver checks are independent (issued together); messages keep the (target, position) keys
@@ -561,6 +563,10 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     // sweep (:158-164, :350-358): a pass's survivors land at or below their own positions, all of
     // which the wave has already read
     const uint64_t kmask = __ballot(keep);
+    if (!seen_keep) {
+      lead += kmask ? (uint32_t)__ffsll((unsigned long long)kmask) - 1 : min(64u, glen - p0);
+      seen_keep = kmask != 0;
+    }
     if (keep) {
       slab[w + lanes_below(kmask)] = g;
       // futures (:167-180): the graceful-leave future stops the member at the end of the tick
@@ -639,6 +645,9 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   }
   const bool any_done = __ballot(done) != 0;
   if (lane == 0) {
+    // the sweep dropped a prefix (infection periods grow along the slab): the index keeps its serials
+    if (glen - w == lead) m.gix_base += lead;
+    else m.gix_valid = 0;
     m.gossip_len = w;
     if (any_done) {
       m.leave_done = 1;
@@ -793,11 +802,8 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, Gos
   const bool was_cleared = (col->meta & COLL_CLEARED) != 0;
   if (!coll_add(c, col, g.seq, &c.seg_flag[r - c.lo])) return false;
   receipt_mark(c, r, g.gossiper, g.seq);
-  int32_t found = -1;
-  if (was_cleared) {  // a GossipState can outlive its collector entry only after a clear
-    for (uint32_t p = 0; p < m.gossip_len; ++p)
-      if (slab[p].gossiper == g.gossiper && slab[p].seq == g.seq) { found = (int32_t)p; break; }
-  }
+  // a GossipState can outlive its collector entry only after a clear
+  const int32_t found = was_cleared ? gix_find(c, m, r, slab, g.gossiper, g.seq) : -1;
   if (found < 0) {
     if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); return true; }
     GossipDev ns;
@@ -807,6 +813,7 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, Gos
 #pragma unroll
     for (int k = 1; k < GINF; ++k) ns.inf[k] = NONE;
     slab[m.gossip_len++] = ns;
+    gix_note(c, m, r, ns.gossiper, ns.seq);
     // onMembershipGossip (MembershipProtocolImpl.java:452-459)
     if (update_membership(c, r, g.subject, g.status, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP))
       apply_alive(c, r, g.subject, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP);

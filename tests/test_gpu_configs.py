@@ -91,3 +91,126 @@ def test_config4_sharded8_16384_matches_oracle(glib):
     sa, sb = oe.stats(), ge.stats()
     assert not parity.diff_stats(sa, sb), parity.diff_stats(sa, sb)
     assert sb["capacity_errors"] == 0
+
+
+def test_config3_16384_first_periods_match_oracle(glib):
+    """Config 3 at its stated size, N = 16,384: 5 % uniform loss, 164 kills + 164 joins through seed 0
+    per period (bench.py's churn schedule).  The first two periods (the joins' SYNC storm begins)
+    are compared bit-exactly with the threaded oracle — sampled full member state (killed members,
+    joiners, the seed), the event stream and every counter; the GPU then runs the third period alone
+    (the SYNC-originated gossip storm: ~10^9 GOSSIP_REQs per period) with no capacity error and no
+    removal (suspicion timeouts are 70 periods away).  Longer runs do not fit any memory: DESIGN.md §6."""
+    import bench
+    n, exact, total = 16384, 2, 3
+    sch = {k: bench.Schedule("churn", n, total) for k in ("gpu", "oracle")}
+    engines = {}
+    for k, lib in (("gpu", glib), ("oracle", oracle.lib())):
+        cfg = bench.churn_capacities(bench.make_config(lib), sch[k].capacity)
+        cfg.message_capacity = 1 << 30  # the third period's gossip rounds: ~4 x 10^8 messages each
+        engines[k] = abi.Engine(lib, cfg, sch[k].capacity, n, 1)
+        sch[k].setup(engines[k])
+    oracle.set_threads(engines["oracle"], THREADS)
+    ops1 = sch["gpu"].ops(0)
+    killed = [m for op, m in ops1 if op == "kill"][:6]
+    joined = [m for op, m in ops1 if op == "join"][:6]
+    sch["gpu"] = bench.Schedule("churn", n, total)  # ops() consumed the schedule's draws: start over
+    members = [0, 1, 5000, n - 1] + killed + joined + [n + 164 + 3]
+    for p in range(exact):
+        for k in ("gpu", "oracle"):
+            sch[k].run(engines[k], p, p + 1)
+        d = parity.diff_states(parity.state_digest(engines["oracle"], members, False),
+                               parity.state_digest(engines["gpu"], members, False))
+        assert not d, f"diverged in period {p + 1}:\n" + "\n".join(d)
+        ea, eb = engines["oracle"].drain_events(), engines["gpu"].drain_events()
+        assert not parity.diff_events(ea, eb), parity.diff_events(ea, eb)
+        sa, sb = engines["oracle"].stats(), engines["gpu"].stats()
+        assert not parity.diff_stats(sa, sb), parity.diff_stats(sa, sb)
+    engines["oracle"].close()
+    e = engines["gpu"]
+    for p in range(exact, total):
+        sch["gpu"].run(e, p, p + 1)
+        ev = e.drain_events()
+        assert not (ev["type"] == abi.EV_REMOVED).any()
+    st = e.stats()
+    assert st["capacity_errors"] == 0
+    assert st["gossip_messages"] > 10 ** 8
+
+
+def _partition_cfg(lib, n, gossip_capacity):
+    return dict(sync_stagger=1, record_fd_events=0, gossip_capacity=gossip_capacity,
+                timer_capacity=max(64 * n, n * n // 2), collector_capacity=1 << (2 * n - 1).bit_length())
+
+
+@pytest.mark.parametrize("n,hold,after", [(256, 52, 8), (128, 20, 10)])
+def test_config5_partition_heal_matches_oracle(glib, n, hold, after):
+    """Config 5 in miniature, bit-exact for the whole run: a 2-way partition [0, N/2) | [N/2, N) from
+    period 2, seeds {0, N/2}; held past the suspicion timeout (each side REMOVEs the other, then the
+    seeds' SYNCs re-join the halves) or healed while the other side is still SUSPECT (every FD ping
+    across succeeds again: the SYNC storm of refutations).  Full state of every member every 10
+    periods, the event stream and the counters against the threaded oracle."""
+    g = np.zeros(n, dtype=np.uint16)
+    g[n // 2:] = 1
+    heal = 2 + hold
+    sc = scenarios.Scenario(f"partition_{n}_{hold}", n, n, (heal + after) * 10, seed=5, seeds=(0, n // 2),
+                            cfg=_partition_cfg(glib, n, 1 << 17), ops=[(20, "partition", g), (heal * 10, "partition", None)],
+                            check_every=100)
+    ge, oe = scenarios.make_engine(glib, sc), scenarios.make_engine(oracle.lib(), sc)
+    oracle.set_threads(oe, THREADS)
+
+    def check(t):
+        d = parity.diff_states(parity.state_digest(oe, None, False), parity.state_digest(ge, None, False))
+        assert not d, f"diverged by tick {t}:\n" + "\n".join(d)
+
+    scenarios.run(ge, sc)
+    scenarios.run(oe, sc, on_check=None)
+    check(sc.ticks)
+    ea, eb = oe.drain_events(), ge.drain_events()
+    assert not parity.diff_events(ea, eb), parity.diff_events(ea, eb)
+    sa, sb = oe.stats(), ge.stats()
+    assert not parity.diff_stats(sa, sb), parity.diff_stats(sa, sb)
+    assert sb["capacity_errors"] == 0
+
+
+def test_config5_partition_heal_2048_reconverges(glib):
+    """Config 5 at the largest size one MI355X holds for a heal after removal (the
+    partition's SUSPECT gossips alone keep ~80 x N live gossips per member): N = 2,048, partition from
+    period 2, held past the suspicion timeout, healed through seeds {0, N/2}.  Every viewer REMOVEs
+    each member of the other side exactly once while partitioned and nobody of its own side; after
+    the heal every viewer ADDs each of them back exactly once, and within 20 periods every viewer
+    sees all N members ALIVE; no capacity error."""
+    n = 2048
+    cfg = abi.default_config(glib, 0, message_capacity=1 << 28, event_capacity=1 << 26,
+                             **_partition_cfg(glib, n, 1 << 19))
+    e = abi.Engine(glib, cfg, n, n, 5)
+    e.set_seeds([0, n // 2])
+    side = (np.arange(n) >= n // 2).astype(np.int64)
+    # past the suspicion timeout of the last SUSPECT: a side's FD pings find the other side's members
+    # over ~15 periods (one ping per member per period), and the SUSPECT gossip spreads in a few more
+    hold = 5 * _ceil_log2(n) + 30
+    heal = 2 + hold
+    removed = np.zeros((n, n), dtype=np.int16)
+    added = np.zeros((n, n), dtype=np.int16)
+    converged_at = None
+    for p in range(heal + 20):
+        if p == 2:
+            e.set_partition(side.astype(np.uint16))
+        if p == heal:
+            assert (removed.sum(axis=1) == n // 2).all()
+            e.set_partition(None)
+        e.step(1)
+        ev = e.drain_events()
+        for typ, acc in ((abi.EV_REMOVED, removed), (abi.EV_ADDED, added)):
+            x = ev[ev["type"] == typ]
+            np.add.at(acc, (x["viewer"].astype(np.int64), x["subject"].astype(np.int64)), 1)
+        if p >= heal and converged_at is None:
+            if all(((((row := e.read_view(v)) >> 34) & 1) == 1).all() and (((row >> 32) & 3) == 0).all()
+                   for v in range(0, n, 97)):
+                if all(((((row := e.read_view(v)) >> 34) & 1) == 1).all() and (((row >> 32) & 3) == 0).all()
+                       for v in range(n)):
+                    converged_at = p + 1
+                    break
+    assert e.stats()["capacity_errors"] == 0
+    other = side[:, None] != side[None, :]
+    assert (removed[other] == 1).all() and (removed[~other] == 0).all()
+    assert converged_at is not None, "not converged within 20 periods of the heal"
+    assert (added[other] == 1).all() and (added[~other] == 0).all()

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--gossip-capacity", type=int, default=1 << 17)
     ap.add_argument("--sample", type=int, default=16)
     ap.add_argument("--interval-capacity", type=int, default=1024)
+    ap.add_argument("--collectors", action="store_true",
+                    help="per period: collector sizes at member sample[1] (gossipers of its live gossips)")
     ap.add_argument("--message-capacity", type=int, default=1 << 28)
     args = ap.parse_args()
     import swimgpu
@@ -106,6 +108,14 @@ def main():
                           "removed": int((ev["type"] == abi.EV_REMOVED).sum()) if len(ev) else 0,
                           "max_live_gossips": glen}), flush=True)
         prev = st
+        if args.collectors:
+            m = sample[1]
+            gs = e.read_gossips(m)
+            ids, cnt = np.unique(gs["gossiper"], return_counts=True) if len(gs) else ([], [])
+            sizes = sorted(((len(e.read_collector(m, int(g))), int(g), int(c)) for g, c in zip(ids, cnt)),
+                           reverse=True)[:5]
+            print(json.dumps({"member": m, "gossipers": len(ids), "top_collectors(intervals,gossiper,live)": sizes}),
+                  flush=True)
         if args.workload == "partition" and args.stop_converged and p + 1 > heal and converged(e, sample) == len(sample):
             print(json.dumps({"converged_at_period": p + 1}), flush=True)
             break
