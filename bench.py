@@ -157,9 +157,10 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(n, periods):
+def cpu_baseline(n, p0, periods):
     """The CPU oracle (oracle/liboracle_swim.so, the C++ lockstep restatement) on the same N and
-    workload from the converged start, bounded to `periods` periods: once with 1 thread and once
+    workload, over the same periods the GPU timed ([p0, p0 + periods) of the schedule; the periods
+    before p0 run untimed on all cores), bounded to `periods` periods: once with 1 thread and once
     multi-threaded over members (std::thread workers over member ranges in every phase; identical
     results, tests/test_golden.py).  The all-core figure is `value`."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -170,25 +171,25 @@ def cpu_baseline(n, periods):
     all_cores = max(1, min(64, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)))
     legs = {}
     for threads in (1, all_cores):
-        cfg = abi.default_config(lib, 0, sync_stagger=1, record_fd_events=0)
-        sch = Schedule(WORKLOAD, n, periods)
+        cfg = make_config(lib)
+        sch = Schedule(WORKLOAD, n, p0 + periods)
+        if WORKLOAD == "churn":
+            churn_capacities(cfg, sch.capacity)
         e = abi.Engine(lib, cfg, sch.capacity, n, 1)
-        oracle.set_threads(e, threads)
         sch.setup(e)
+        oracle.set_threads(e, all_cores)
+        sch.run(e, 0, p0)
+        oracle.set_threads(e, threads)
         t0 = time.perf_counter()
-        sch.run(e, 0, periods)
+        sch.run(e, p0, p0 + periods)
         legs[threads] = time.perf_counter() - t0
         e.close()
-    note = ""
-    if WORKLOAD != "quiet":  # the GPU's timed periods come later in the same schedule
-        note = ("; NOT the GPU's timed work: this workload's per-period volume grows after these first periods "
-                "(kills, gossip storms), so compare member-periods/s of the same periods only")
     dt1, dtn = legs[1], legs[all_cores]
     return {"value": n * periods / dtn, "unit": "member-periods/s", "cores": all_cores, "kind": "port",
             "single_thread_value": n * periods / dt1, "nproc": os.cpu_count(), "cpu_model": cpu_model(),
             "sample": f"CPU oracle (C++ lockstep restatement), N={n}, LAN defaults, workload {WORKLOAD}, "
-                      f"periods 0..{periods} from the converged start: {dtn:.1f} s on {all_cores} threads, "
-                      f"{dt1:.1f} s on 1 thread{note}"}
+                      f"periods {p0}..{p0 + periods} of the schedule (the GPU's first timed periods; "
+                      f"0..{p0} untimed): {dtn:.1f} s on {all_cores} threads, {dt1:.1f} s on 1 thread"}
 
 
 def main():
@@ -197,7 +198,7 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--members", type=int, default=None, help="default: 65,536 (16,384 for churn)")
-    ap.add_argument("--cpu-periods", type=int, default=10)
+    ap.add_argument("--cpu-periods", type=int, default=0, help="default: 10 (1 for churn)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--progress", action="store_true", help="print a stderr line after every period")
     ap.add_argument("--workload", choices=("quiet", "failures", "churn"), default="quiet")
@@ -321,7 +322,10 @@ def main():
             "alg_bytes_rule": "24 B per materialised GOSSIP_REQ + 32 B per (gossip, sender round) state read"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         e.close()
-        line["cpu_baseline"] = cpu_baseline(n, args.cpu_periods)
+        # churn: the oracle needs minutes per period once the storm builds, so the sample is the
+        # first timed period only
+        cpu_periods = args.cpu_periods or (1 if args.workload == "churn" else 10)
+        line["cpu_baseline"] = cpu_baseline(n, args.warmup, min(cpu_periods, args.steps))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
