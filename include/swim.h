@@ -51,6 +51,16 @@ extern "C" {
 #define SWIM_EV_FD_ALIVE 16
 #define SWIM_EV_FD_SUSPECT 17
 #define SWIM_EV_FD_DEAD 18
+/* user gossips (GossipProtocol.spread / listen, GossipProtocolImpl.java:126-130,201-215,167-180):
+ * GOSSIP: viewer received a new user gossip (listen() emits it); subject = its gossiper, data = payload.
+ * SPREAD_DONE: the spread() Mono of viewer's own gossip completed (the first gossip round with
+ * period > infectionPeriod + periodsToSpread); subject = viewer, data = payload. */
+#define SWIM_EV_GOSSIP 32
+#define SWIM_EV_SPREAD_DONE 33
+/* swim_gossip.status of a user gossip (its subject field holds the payload): USER until the
+ * originator's spread() completes, USER_SPREAD afterwards (copies sent from then on carry it too) */
+#define SWIM_GOSSIP_USER 4
+#define SWIM_GOSSIP_USER_SPREAD 5
 
 /* ---- canonical intra-tick phases ---------------------------------------- */
 #define SWIM_PHASE_TIMERS 1  /* suspicion timeouts      (MembershipProtocolImpl.java:825-834) */
@@ -136,7 +146,8 @@ typedef struct swim_config {
   uint32_t deliver_wave_min;  /* gossip inboxes above this many messages are delivered by a whole wave
                                  (0 = default 24, the most the per-thread LDS sort holds; a test knob:
                                  1 sends every inbox through the wave path) */
-  uint32_t reserved[1];
+  uint32_t delay_capacity;    /* delayed GOSSIP_REQs that may arrive in one tick (0 = default 1,024;
+                                 allocated when a message delay is first set) */
 } swim_config;
 
 /* preset: 0 = defaultConfig/defaultLanConfig, 1 = defaultWanConfig, 2 = defaultLocalConfig
@@ -199,6 +210,11 @@ int32_t swim_leave(swim_engine* e, uint32_t m, int32_t stop_after);
 /* Start a fresh member in free slot m (ClusterImpl.doStart0 + MembershipProtocolImpl.start0
  * :250-291): initial SYNC to every seed during the next tick. */
 int32_t swim_join(swim_engine* e, uint32_t m);
+/* GossipProtocol.spread(Message) (GossipProtocolImpl.java:126-130 -> createAndPutGossip :190-199)
+ * on member m now, between ticks: a user gossip carrying the 32-bit payload (a handle the caller
+ * maps to the message).  Receivers report it with SWIM_EV_GOSSIP, the originator's spread()
+ * completion with SWIM_EV_SPREAD_DONE. */
+int32_t swim_spread(swim_engine* e, uint32_t m, uint32_t payload);
 
 /* ---- network emulator (NetworkEmulator.java) ----------------------------------------------
  * Outbound loss is decided at the sender and fails the send immediately (:167-181); inbound
@@ -208,6 +224,16 @@ int32_t swim_set_default_loss(swim_engine* e, uint32_t m, int32_t loss_percent);
 /* outboundSettings(dst, loss, 0) on src (:69-73); loss_percent < 0 removes the override
  * (unblockOutbound :134-139) */
 int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t loss_percent);
+/* The meanDelay half of setDefaultOutboundSettings(loss, meanDelay) (:80-83) and of
+ * outboundSettings(dst, loss, meanDelay) on src (:69-73); mean_ms < 0 removes the link override.
+ * A message is delivered floor(delay / tick_ms) ticks after it was sent, delay drawn as
+ * evaluateDelay (:359-369) from the Philox hook (swim_delay.h).  Applies to the failure
+ * detector's pings, ping-reqs and acks (a round trip completes when both legs arrived; a late
+ * direct ack joins the ping-req race, :153-210) and to GOSSIP_REQs (delivered in the gossip phase
+ * of their arrival tick, after the arrivals of earlier rounds).  SYNC / SYNC_ACK and metadata
+ * round trips are not delayed.  Single-shard engines only (SWIM_EINVAL otherwise). */
+int32_t swim_set_default_delay(swim_engine* e, uint32_t m, int32_t mean_ms);
+int32_t swim_set_link_delay(swim_engine* e, uint32_t src, uint32_t dst, int32_t mean_ms);
 /* inboundSettings(src, shallPass) on dst (:219-223); shall_pass < 0 removes the override */
 int32_t swim_set_link_inbound(swim_engine* e, uint32_t dst, uint32_t src, int32_t shall_pass);
 /* setDefaultInboundSettings(shallPass) (:230-233); m = UINT32_MAX applies to every member */
@@ -227,7 +253,7 @@ typedef struct swim_event {
   uint32_t type;  /* SWIM_EV_* */
   uint32_t phase; /* SWIM_PHASE_* */
   uint32_t minor; /* order within (tick, viewer, phase) */
-  uint32_t pad;
+  uint32_t data;  /* SWIM_EV_GOSSIP / SWIM_EV_SPREAD_DONE: the payload; 0 otherwise */
 } swim_event;
 /* Events in canonical order (tick, viewer, phase, minor).  *n_out = events copied; events that
  * did not fit stay buffered for the next call. */

@@ -32,9 +32,17 @@
 #define SWIM_STREAM_TRANSIT_PING_OUT 15/* transit PING relay j -> target                      */
 #define SWIM_STREAM_TRANSIT_ACK_OUT 16 /* transit PING_ACK target -> relay j                  */
 #define SWIM_STREAM_RELAY_ACK_OUT 17   /* PING_ACK relay j -> issuer                          */
+/* message delays (swim_delay.h: u53 from words 0 and 1 of the block), member = the issuer */
+#define SWIM_STREAM_PING_DELAY 18      /* PING issuer -> target                               */
+#define SWIM_STREAM_ACK_DELAY 19       /* PING_ACK target -> issuer                           */
+#define SWIM_STREAM_PINGREQ_DELAY 24   /* PING_REQ issuer -> relay j, sub24 = j               */
+#define SWIM_STREAM_TRANSIT_PING_DELAY 25 /* transit PING relay j -> target                   */
+#define SWIM_STREAM_TRANSIT_ACK_DELAY 26  /* transit PING_ACK target -> relay j               */
+#define SWIM_STREAM_RELAY_ACK_DELAY 27 /* PING_ACK relay j -> issuer                          */
 /* gossip (sender-keyed) */
 #define SWIM_STREAM_GOSSIP_SHUFFLE 20  /* Collections.shuffle(remoteMembers), sub32 = i       */
 #define SWIM_STREAM_GOSSIP_OUT 21      /* GOSSIP_REQ outbound loss, sub24 = target j, sub32 = slab position */
+#define SWIM_STREAM_GOSSIP_DELAY 22    /* GOSSIP_REQ delay, member = sender, same sub keys     */
 /* membership */
 #define SWIM_STREAM_SYNC_SELECT 30     /* selectSyncAddress, sub24 = 0 / 1, sub32 = attempt   */
 #define SWIM_STREAM_SYNC_OUT 31        /* SYNC sender -> receiver, sub24 = sender ordinal     */

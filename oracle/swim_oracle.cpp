@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "swim.h"
+#include "swim_delay.h"
 #include "swim_rng.h"
 
 namespace {
@@ -139,8 +140,11 @@ struct Member {
   uint32_t ping_index = 0;
   uint32_t ack_target = NONE;
   uint64_t ack_due = 0;
+  bool ack_ok = false;    // ack_due is the tick the (delayed) ack arrives, not the timeout
+  uint32_t ack_late = 0;  // 1 + ticks after the timeout that a late direct ack arrives (0 = none)
   uint32_t relay_target = NONE, relay_pending = 0;
   uint64_t relay_due = 0;
+  bool relay_ok = false;  // relay_due is the tick the first relayed ack arrives, not the timeout
   // ---- GossipProtocolImpl (:48-55)
   uint64_t g_period = 0, g_counter = 0, period_used = 0;
   std::unordered_map<uint32_t, SeqCollector> collectors;
@@ -231,6 +235,14 @@ struct swim_engine {
   std::vector<uint8_t> default_inbound;
   std::map<LinkKey, int32_t> link_loss;     // (src,dst) -> loss %
   std::map<LinkKey, uint8_t> link_inbound;  // (dst,src) -> shallPass
+  std::vector<int32_t> default_delay;       // OutboundSettings.meanDelay (ms) per member
+  std::map<LinkKey, int32_t> link_delay;    // (src,dst) -> meanDelay (ms)
+  std::map<int32_t, std::vector<uint64_t>> delay_tab;  // meanDelay -> thresholds (swim_delay.h)
+  // GOSSIP_REQs in flight: arrival tick -> messages (sent in an earlier tick's gossip round)
+  struct DelayedMsg {
+    uint32_t to, from, pos;
+    uint64_t sent;
+  };
   bool partition = false;
   std::vector<uint16_t> group;
   // timers: deadline tick -> (viewer, subject)
@@ -300,10 +312,31 @@ struct swim_engine {
   }
   // tryFailOutbound (:167-181) + a stopped destination refusing the connection
   bool out_fail(uint32_t a, uint32_t b, uint32_t w) const { return !m[b].up || lost(out_loss(a, b), w); }
+  // tryDelayOutbound (:190-202) + evaluateDelay (:359-369), in ticks (swim_delay.h); the draw is
+  // keyed (member, stream, sub24, sub32) and taken only when the link has a mean delay
+  int32_t out_delay(uint32_t a, uint32_t b) const {
+    auto it = link_delay.find({a, b});
+    return it != link_delay.end() ? it->second : default_delay[a];
+  }
+  uint32_t delay_ticks(uint32_t a, uint32_t b, uint32_t member, uint32_t stream, uint32_t sub24, uint32_t sub32) {
+    const int32_t mean = out_delay(a, b);
+    if (mean <= 0) return 0;
+    uint32_t c[4] = {member, (uint32_t)T, (stream << 24) | (sub24 & 0xffffffu), sub32}, o[4];
+    philox4x32_10(c, key, o);
+    const uint64_t u53 = ((uint64_t)(o[0] >> 11) << 32) | o[1];
+    return swim_delay_ticks(delay_tab.at(mean).data(), u53);
+  }
+  void ensure_delay_tab(int32_t mean) {
+    if (mean <= 0 || delay_tab.count(mean)) return;
+    std::vector<uint64_t> th(SWIM_DELAY_TICKS_MAX);
+    swim_delay_thresholds(mean, tick_ms, th.data());
+    delay_tab[mean] = std::move(th);
+  }
 
   // ------------------------------------------------------------------------- events
-  void emit(uint32_t v, uint32_t subject, uint32_t type, uint32_t phase, uint32_t minor) {
+  void emit(uint32_t v, uint32_t subject, uint32_t type, uint32_t phase, uint32_t minor, uint32_t data = 0) {
     swim_event e{};
+    e.data = data;
     e.tick = T;
     e.viewer = v;
     e.subject = subject;
@@ -355,6 +388,10 @@ struct swim_engine {
     mv.collectors[v].add((int64_t)g.seq);
     STT().gossips_created++;
   }
+
+  // GossipProtocol.spread(Message) (GossipProtocolImpl.java:126-130): a user gossip, its payload in
+  // the record's member field (status SWIM_GOSSIP_USER)
+  void spread_user(uint32_t v, uint32_t payload) { spread_gossip(v, Record{payload, SWIM_GOSSIP_USER, 0}); }
 
   // ------------------------------------------------------------------------- timers
   // scheduleSuspicionTimeoutTask (:805-823): computeIfAbsent, timeout from the table size now.
@@ -574,7 +611,12 @@ struct swim_engine {
   // doPing's error branch (:153-170) + doPingReq (:173-210).  Every pending relay request shares
   // the ping's correlation id, so the first relayed ack that reaches the issuer completes all of
   // them (TransportImpl.requestResponse :214-238 filters listen() by cid only).
-  void ping_req(uint32_t v, uint32_t t) {
+  // With message delay the first message carrying the cid to arrive decides: the earliest relayed
+  // ack (ties: lowest relay), or a late ack of the direct ping (`late` = 1 + its arrival in ticks
+  // after the ping-req went out, 0 = none; it carries the same cid and arrives after the relay
+  // requests subscribed), and only if the issuer's inbound filter passes its sender
+  // (NetworkEmulatorTransport.requestResponse :65-74); none before pingInterval - pingTimeout: SUSPECT.
+  void ping_req(uint32_t v, uint32_t t, uint32_t late = 0) {
     std::vector<uint32_t> relays = select_ping_req_members(v, t);
     if (relays.empty()) {  // timeLeft <= 0 is excluded by config validation
       publish_fd(v, t, SWIM_SUSPECT);
@@ -589,24 +631,34 @@ struct swim_engine {
         pending.push_back(j);
     }
     if (pending.empty()) return;
-    int64_t arrived = -1;
+    uint32_t best = NONE, first = NONE;  // arrival (ticks after now) and sender of the first ack
     for (uint32_t j : pending) {
       uint32_t r = relays[j];
       if (in_pass(r, v) && !out_fail(r, t, draw(v, SWIM_STREAM_TRANSIT_PING_OUT, j, 0)) &&
           in_pass(t, r) && !out_fail(t, r, draw(v, SWIM_STREAM_TRANSIT_ACK_OUT, j, 0)) &&
           in_pass(r, t) && !out_fail(r, v, draw(v, SWIM_STREAM_RELAY_ACK_OUT, j, 0))) {
-        arrived = j;
-        break;
+        const uint32_t at = delay_ticks(v, r, v, SWIM_STREAM_PINGREQ_DELAY, j, 0) +
+                            delay_ticks(r, t, v, SWIM_STREAM_TRANSIT_PING_DELAY, j, 0) +
+                            delay_ticks(t, r, v, SWIM_STREAM_TRANSIT_ACK_DELAY, j, 0) +
+                            delay_ticks(r, v, v, SWIM_STREAM_RELAY_ACK_DELAY, j, 0);
+        if (at < best) { best = at; first = r; }
       }
     }
-    if (arrived >= 0 && in_pass(v, relays[(size_t)arrived])) {
-      for (size_t i = 0; i < pending.size(); ++i) publish_fd(v, t, SWIM_ALIVE);
+    if (late && late - 1 < best) { best = late - 1; first = t; }
+    Member& mv = m[v];
+    if (first != NONE && best < relay_ticks && in_pass(v, first)) {
+      if (best == 0) {
+        for (size_t i = 0; i < pending.size(); ++i) publish_fd(v, t, SWIM_ALIVE);
+        return;
+      }
+      mv.relay_due = T + best;  // the acks complete every pending relay request then
+      mv.relay_ok = true;
     } else {
-      Member& mv = m[v];
       mv.relay_due = T + relay_ticks;
-      mv.relay_target = t;
-      mv.relay_pending = (uint32_t)pending.size();
+      mv.relay_ok = false;
     }
+    mv.relay_target = t;
+    mv.relay_pending = (uint32_t)pending.size();
   }
 
   bool fd_due(const Member& mv) const {
@@ -627,15 +679,16 @@ struct swim_engine {
       Member& mv = m[v];
       if (!mv.up) continue;
       mv.ev_minor = 0;
-      if (mv.relay_due == T) {  // relay timeouts (:200-209)
+      if (mv.relay_due == T) {  // relayed acks arrive (:190-199) or the relay timeouts (:200-209)
         uint32_t t = mv.relay_target, k = mv.relay_pending;
         mv.relay_due = 0;
-        for (uint32_t i = 0; i < k; ++i) publish_fd(v, t, SWIM_SUSPECT);
+        for (uint32_t i = 0; i < k; ++i) publish_fd(v, t, mv.relay_ok ? SWIM_ALIVE : SWIM_SUSPECT);
       }
-      if (mv.ack_due == T) {  // pingTimeout elapsed (:153-170)
+      if (mv.ack_due == T) {  // the delayed ack arrives, or pingTimeout elapsed (:153-170)
         uint32_t t = mv.ack_target;
         mv.ack_due = 0;
-        ping_req(v, t);
+        if (mv.ack_ok) publish_fd(v, t, SWIM_ALIVE);
+        else ping_req(v, t, mv.ack_late);
       }
       if (fd_due(mv)) {  // doPing (:126-171)
         mv.fd_period++;
@@ -644,11 +697,20 @@ struct swim_engine {
         STT().pings++;
         if (out_fail(v, t, draw(v, SWIM_STREAM_PING_OUT, 0, 0))) {
           ping_req(v, t);  // outbound error -> ping-req right away
-        } else if (in_pass(t, v) && !out_fail(t, v, draw(v, SWIM_STREAM_ACK_OUT, 0, 0)) && in_pass(v, t)) {
-          publish_fd(v, t, SWIM_ALIVE);  // onPing answers DEST_OK (:227-259)
         } else {
-          mv.ack_due = T + to_ticks;
-          mv.ack_target = t;
+          // onPing answers DEST_OK (:227-259); the round trip takes the two messages' delays
+          const bool acked = in_pass(t, v) && !out_fail(t, v, draw(v, SWIM_STREAM_ACK_OUT, 0, 0));
+          const uint32_t rtt = acked ? delay_ticks(v, t, v, SWIM_STREAM_PING_DELAY, 0, 0) +
+                                           delay_ticks(t, v, v, SWIM_STREAM_ACK_DELAY, 0, 0)
+                                     : 0;
+          if (acked && rtt == 0 && in_pass(v, t)) {
+            publish_fd(v, t, SWIM_ALIVE);
+          } else {
+            mv.ack_target = t;
+            mv.ack_ok = acked && rtt < to_ticks && in_pass(v, t);
+            mv.ack_due = T + (mv.ack_ok ? rtt : to_ticks);
+            mv.ack_late = acked && rtt >= to_ticks ? rtt - to_ticks + 1 : 0;
+          }
         }
       }
     }
@@ -658,7 +720,9 @@ struct swim_engine {
   struct GMsg {
     uint32_t to, from, pos;
     GossipState g;
+    uint64_t sent;  // tick of the round that sent it (a delayed message arrives in a later tick)
   };
+  std::map<uint64_t, std::vector<GMsg>> gossip_in_flight;  // arrival tick -> delayed GOSSIP_REQs
 
   // selectGossipMembers (GossipProtocolImpl.java:322-343)
   std::vector<uint32_t> select_gossip_members(uint32_t v) {
@@ -678,7 +742,16 @@ struct swim_engine {
     std::vector<uint32_t> due;
     for (uint32_t v = 0; v < n; ++v)
       if (gossip_due(m[v])) due.push_back(v);
-    if (due.empty()) return;
+    // GOSSIP_REQs delayed by the network emulator that arrive now (tryDelayOutbound :190-202)
+    std::vector<GMsg> arriving;
+    {
+      auto it = gossip_in_flight.find(T);
+      if (it != gossip_in_flight.end()) {
+        arriving.swap(it->second);
+        gossip_in_flight.erase(it);
+      }
+    }
+    if (due.empty() && arriving.empty()) return;
     const uint32_t nd = (uint32_t)due.size();
     // C1: period++ and checkGossipSegmentation (:141-146, :217-236)
     par(0, nd, [&](uint32_t a, uint32_t b, uint32_t) {
@@ -696,6 +769,7 @@ struct swim_engine {
     for (uint32_t t = 0; t <= nt; ++t) rb[t] = (uint32_t)((uint64_t)n * t / nt);
     auto consumer = [&](uint32_t to) { return (uint32_t)(std::upper_bound(rb.begin(), rb.end(), to) - rb.begin()) - 1; };
     std::vector<std::vector<std::vector<GMsg>>> bucket(nt, std::vector<std::vector<GMsg>>(nt));
+    std::vector<std::vector<GMsg>> later(nt);  // delayed sends, by producer
     bool any = false;
     par(0, nd, [&](uint32_t a, uint32_t b, uint32_t t) {
       for (uint32_t i = a; i < b; ++i) {
@@ -716,7 +790,9 @@ struct swim_engine {
             STT().gossip_messages++;
             if (out_fail(v, tg, draw(v, SWIM_STREAM_GOSSIP_OUT, j, p))) continue;
             if (!in_pass(tg, v)) continue;
-            bucket[t][consumer(tg)].push_back(GMsg{tg, v, p, g});
+            const uint32_t k = delay_ticks(v, tg, v, SWIM_STREAM_GOSSIP_DELAY, j, p);
+            if (k) later[t].push_back(GMsg{tg, v, p, g, T + k});
+            else bucket[t][consumer(tg)].push_back(GMsg{tg, v, p, g, T});
           }
         }
         // sweep (:158-164, :350-358)
@@ -726,14 +802,25 @@ struct swim_engine {
           if (!(period > g.infection_period + sweep)) keep.push_back(std::move(g));
         mv.gossips.swap(keep);
         mv.reindex_gossips();
-        // futures (:167-180, :360-368): only the graceful-leave future has an observer here
-        if (mv.leave_pending) {
-          for (auto& g : mv.gossips)
-            if (period > g.infection_period + spread && g.gossiper == mv.leave_gossiper && g.seq == mv.leave_seq)
-              mv.leave_done = true;
+        // futures (:167-180, :360-368): the graceful-leave future, and spread() of user gossips
+        for (auto& g : mv.gossips) {
+          if (!(period > g.infection_period + spread)) continue;
+          if (mv.leave_pending && g.gossiper == mv.leave_gossiper && g.seq == mv.leave_seq) mv.leave_done = true;
+          if (g.rec.status == SWIM_GOSSIP_USER && g.gossiper == v) {
+            g.rec.status = SWIM_GOSSIP_USER_SPREAD;
+            emit(v, v, SWIM_EV_SPREAD_DONE, SWIM_PHASE_GOSSIP, 0x80000000u | (uint32_t)(g.seq & 0x7fffffffu),
+                 g.rec.member);
+          }
         }
       }
     });
+    for (auto& lt : later)
+      for (auto& x : lt) {
+        const uint64_t at = x.sent;
+        x.sent = T;
+        gossip_in_flight[at].push_back(std::move(x));
+      }
+    for (auto& x : arriving) bucket[0][consumer(x.to)].push_back(std::move(x));
     for (auto& bp : bucket)
       for (auto& bc : bp) any |= !bc.empty();
     if (!any) return;
@@ -743,8 +830,10 @@ struct swim_engine {
       for (uint32_t d = 0; d < nt; ++d)
         if (rb[d] >= ra && rb[d + 1] <= rbnd)
           for (uint32_t pr = 0; pr < nt; ++pr) msgs.insert(msgs.end(), bucket[pr][d].begin(), bucket[pr][d].end());
-      std::sort(msgs.begin(), msgs.end(), [](const GMsg& a, const GMsg& b) {  // keys are unique
+      // canonical order: (receiver, sending round, sender, slab position); keys are unique
+      std::sort(msgs.begin(), msgs.end(), [](const GMsg& a, const GMsg& b) {
         if (a.to != b.to) return a.to < b.to;
+        if (a.sent != b.sent) return a.sent < b.sent;
         if (a.from != b.from) return a.from < b.from;
         return a.pos < b.pos;
       });
@@ -771,6 +860,10 @@ struct swim_engine {
           ns.infection_period = mr.g_period;
           ns.infected.push_back(msg.from);
           mr.add_gossip(ns);
+          if (g.rec.status >= SWIM_GOSSIP_USER) {  // sink.next(gossip.message()) (:209): listen()
+            emit(r, g.gossiper, SWIM_EV_GOSSIP, SWIM_PHASE_GOSSIP, next_minor(r), g.rec.member);
+            continue;
+          }
           // onMembershipGossip (:452-459)
           update_membership(r, g.rec, MEMBERSHIP_GOSSIP, SWIM_PHASE_GOSSIP, pending);
           flush_pending(r, pending, MEMBERSHIP_GOSSIP, SWIM_PHASE_GOSSIP);
@@ -1113,6 +1206,7 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
     e->m.resize(capacity);
     e->is_seed.assign(capacity, 0);
     e->default_loss.assign(capacity, 0);
+    e->default_delay.assign(capacity, 0);
     e->default_inbound.assign(capacity, 1);
     e->group.assign(capacity, 0);
     for (auto& mm : e->m) mm.row.assign(capacity, 0);
@@ -1257,6 +1351,13 @@ int32_t swim_leave(swim_engine* e, uint32_t v, int32_t stop_after) {
   return SWIM_OK;
 }
 
+int32_t swim_spread(swim_engine* e, uint32_t v, uint32_t payload) {
+  if (!e || v >= e->n) return SWIM_EINVAL;
+  if (!e->m[v].up) return SWIM_ESTATE;
+  e->spread_user(v, payload);  // GossipProtocolImpl.spread (:126-130)
+  return SWIM_OK;
+}
+
 int32_t swim_join(swim_engine* e, uint32_t v) {
   if (!e || v >= e->n) return SWIM_EINVAL;
   Member& mv = e->m[v];
@@ -1276,6 +1377,26 @@ int32_t swim_set_default_loss(swim_engine* e, uint32_t mm, int32_t pct) {
 int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t pct) {
   if (!e || src >= e->n || dst >= e->n || pct > 100) return SWIM_EINVAL;
   if (pct < 0) e->link_loss.erase({src, dst}); else e->link_loss[{src, dst}] = pct;
+  return SWIM_OK;
+}
+
+int32_t swim_set_default_delay(swim_engine* e, uint32_t mm, int32_t mean_ms) {
+  if (!e || mean_ms < 0) return SWIM_EINVAL;
+  if (mm != 0xffffffffu && mm >= e->n) return SWIM_EINVAL;
+  e->ensure_delay_tab(mean_ms);
+  if (mm == 0xffffffffu) std::fill(e->default_delay.begin(), e->default_delay.end(), mean_ms);
+  else e->default_delay[mm] = mean_ms;
+  return SWIM_OK;
+}
+
+int32_t swim_set_link_delay(swim_engine* e, uint32_t src, uint32_t dst, int32_t mean_ms) {
+  if (!e || src >= e->n || dst >= e->n) return SWIM_EINVAL;
+  if (mean_ms < 0) {
+    e->link_delay.erase({src, dst});
+  } else {
+    e->ensure_delay_tab(mean_ms);
+    e->link_delay[{src, dst}] = mean_ms;
+  }
   return SWIM_OK;
 }
 

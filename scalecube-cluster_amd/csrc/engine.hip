@@ -176,6 +176,7 @@ struct swim_engine {
   std::vector<uint32_t> seeds;
   std::vector<uint8_t> is_seed_h, joined_h, join_pending_h;
   std::vector<LinkDev> links_h;
+  std::vector<int32_t> delay_means;  // NetworkEmulator meanDelay (ms) of each delay table, in table order
   std::vector<uint32_t> joins;  // joins starting at the next tick
   std::vector<swim_event> events;
   uint64_t host_ticks = 0, host_events = 0;
@@ -555,14 +556,21 @@ static int32_t run_tick(swim_engine* e) {
     const uint32_t gm = grid_for(sd.c.nl, 256);
     // ---- A: suspicion timeouts, B: list compaction of their REMOVED + failure detector
     // ---- C: gossip round (period++ and the sender list in k_fd, then emit)
-    k_fd<<<gm, 256, 0, s>>>(sd.d_par, T, gossip_tick ? 1 : 0, gossip_tick ? 0 : 1);
+    // with message delay every tick may deliver GOSSIP_REQs, so the SYNC collection that follows a
+    // member's deliveries moves into k_gossip_deliver on every tick
+    const bool delay = sd.c.delay_on != 0;
+    k_fd<<<gm, 256, 0, s>>>(sd.d_par, T, gossip_tick ? 1 : 0, gossip_tick || delay ? 0 : 1);
     TICK_CHECK("k_fd");
     if (gossip_tick) {
       launch_emit(e, sd);
       TICK_CHECK("k_gossip_emit");
     }
+    if (delay) {
+      k_dq_release<<<(sd.b.dq_bcap + 255) / 256, 256, 0, s>>>(sd.d_par, T);
+      TICK_CHECK("k_dq_release");
+    }
   }
-  if (gossip_tick) {
+  if (gossip_tick || e->sh[0].c.delay_on) {
     if (multi)
       if (int32_t rc = exchange_msgs(e)) return rc;
     for (Shard& sd : e->sh) {
@@ -571,7 +579,7 @@ static int32_t run_tick(swim_engine* e) {
         k_recv_msgs<<<std::min<uint32_t>(grid_for(sd.n_rx_msgs, 256), 1024), 256, 0, s>>>(sd.d_par, T, sd.n_rx_msgs);
       TICK_CHECK("k_recv_msgs");
       // at least kDeliverGrid workgroups: big inboxes are delivered a wave each, grid-stride
-      k_gossip_deliver<<<std::max<uint32_t>(kDeliverGrid, grid_for(sd.c.nl, DLV_BLOCK)), DLV_BLOCK, 0, s>>>(sd.d_par, T);
+      k_gossip_deliver<<<std::max<uint32_t>(kDeliverGrid, grid_for(sd.c.nl, DLV_BLOCK)), DLV_BLOCK, 0, s>>>(sd.d_par, T, 1);
       TICK_CHECK("k_gossip_deliver");  // (also applies the phase's pingMembers inserts)
     }
   }
@@ -626,13 +634,15 @@ static LinkDev* find_link_h(swim_engine* e, uint32_t a, uint32_t b, bool create)
   for (auto& L : e->links_h)
     if (L.a == a && L.b == b) return &L;
   if (!create) return nullptr;
-  e->links_h.push_back(LinkDev{a, b, -1, -1});
+  e->links_h.push_back(LinkDev{a, b, -1, -1, -1});
   return &e->links_h.back();
 }
 
 static void prune_links(swim_engine* e) {
   auto& L = e->links_h;
-  L.erase(std::remove_if(L.begin(), L.end(), [](const LinkDev& x) { return x.out_loss < 0 && x.in_pass < 0; }), L.end());
+  L.erase(std::remove_if(L.begin(), L.end(),
+                         [](const LinkDev& x) { return x.out_loss < 0 && x.in_pass < 0 && x.out_delay == -1; }),
+          L.end());
 }
 
 static int32_t read_member_dev(swim_engine* e, Shard& sd, uint32_t m, MemberDev* out) {
@@ -672,6 +682,11 @@ __global__ void k_leave(Ctx c, uint32_t v, int32_t stop_after) {
     m.leave_gossiper = v;
     m.leave_seq = m.g_counter - 1;
   }
+}
+
+__global__ void k_spread(Ctx c, uint32_t v, uint32_t payload) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  spread_user(c, v, payload);
 }
 
 static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n_initial, uint64_t seed) {
@@ -735,6 +750,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.pg_max = std::min<uint32_t>(b.pg_max, 1u << 14);
   b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
   b.wave_min = cf.deliver_wave_min ? std::min<uint32_t>(cf.deliver_wave_min, DLV_SORT) : (uint32_t)DLV_SORT;
+  b.dq_bcap = 0;  // the delay ring is allocated when a delay is first set (swim_set_*_delay)
   // snapshot rows for members that both send and receive a SYNC in one tick (at most two each: the
   // SYNC content and, when its merges changed the row, the SYNC_ACK content): a few per tick in
   // steady state, up to every member right after a partition heals; at most 1 GiB of rows
@@ -768,6 +784,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&c.wheel, (size_t)(c.wheel_mask + 1) * c.wheel_cap) &&
             sd.alloc(&c.wheel_cnt, (size_t)(c.wheel_mask + 1) * c.wheel_nq) && sd.alloc(&c.ev, (size_t)c.ev_cap * SUBQ) &&
             sd.alloc(&c.ev_cnt, SUBQ) && sd.alloc(&c.default_loss, n) &&
+            sd.alloc(&c.default_delay, n) && sd.alloc(&b.dq_cnt, DQ_BUCKETS) &&
             sd.alloc(&c.default_inbound, n) && sd.alloc(&c.group, n) && sd.alloc(&c.links, 1) &&
             sd.alloc(&c.is_seed, n) && sd.alloc(&c.seeds, n) && sd.alloc(&c.ins, c.ins_cap) &&
             sd.alloc(&c.ins_inline, (size_t)nl * INS_INLINE) && sd.alloc(&c.compact_flag, nl) &&
@@ -812,6 +829,10 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(c.ref, 0, 4 * (size_t)n, s);
   hipMemsetAsync(c.dirty, 0, 4 * (size_t)n, s);
   hipMemsetAsync(c.default_loss, 0, n, s);
+  hipMemsetAsync(c.default_delay, 0xff, 2ull * n, s);  // -1: no delay
+  hipMemsetAsync(b.dq_cnt, 0, 4ull * DQ_BUCKETS, s);
+  c.delay_th = nullptr;
+  c.delay_on = 0;
   hipMemsetAsync(c.default_inbound, 1, n, s);
   hipMemsetAsync(c.group, 0, 2 * (size_t)n, s);
   hipMemsetAsync(c.is_seed, 0, n, s);
@@ -1088,6 +1109,18 @@ int32_t swim_leave(swim_engine* e, uint32_t m, int32_t stop_after) {
   return hip_status();
 }
 
+int32_t swim_spread(swim_engine* e, uint32_t m, uint32_t payload) {
+  if (!e || m >= e->n) return SWIM_EINVAL;
+  uint8_t up = 0;
+  if (read_up(e, m, &up) != SWIM_OK) return SWIM_EDEVICE;
+  if (!up) return SWIM_ESTATE;
+  Shard* sd = e->owner_of(m);
+  if (!sd) return SWIM_OK;  // RCCL: the owning rank runs it
+  sd->c.T = e->T;
+  k_spread<<<1, 64, 0, e->stream>>>(sd->c, m, payload);
+  return hip_status();
+}
+
 int32_t swim_join(swim_engine* e, uint32_t m) {
   if (!e || m >= e->n) return SWIM_EINVAL;
   uint8_t up = 0;
@@ -1118,6 +1151,74 @@ int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t p
     if (L) L->out_loss = -1;
   } else {
     find_link_h(e, src, dst, true)->out_loss = pct;
+  }
+  prune_links(e);
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  return upload_links(e);
+}
+
+// ---- message delay (swim_delay.h): one threshold table per distinct meanDelay, on every shard
+static int32_t delay_table(swim_engine* e, int32_t mean_ms, int32_t* idx) {
+  for (size_t i = 0; i < e->delay_means.size(); ++i)
+    if (e->delay_means[i] == mean_ms) { *idx = (int32_t)i; return SWIM_OK; }
+  if (e->delay_means.size() >= 4096) return SWIM_EINVAL;
+  e->delay_means.push_back(mean_ms);
+  const size_t nt = e->delay_means.size();
+  std::vector<uint64_t> th(nt * SWIM_DELAY_TICKS_MAX);
+  for (size_t i = 0; i < nt; ++i) swim_delay_thresholds(e->delay_means[i], e->tick_ms, th.data() + i * SWIM_DELAY_TICKS_MAX);
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  for (Shard& sd : e->sh) {
+    uint64_t* p = nullptr;
+    if (!sd.alloc(&p, th.size())) return SWIM_ENOMEM;
+    if (hipMemcpy(p, th.data(), 8 * th.size(), hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
+    sd.c.delay_th = p;  // the previous table stays allocated until the engine is destroyed
+  }
+  *idx = (int32_t)(nt - 1);
+  return SWIM_OK;
+}
+// the delay ring and the per-tick release are set up the first time a delay is configured
+static int32_t enable_delay(swim_engine* e) {
+  if (e->world > 1 || e->sh.size() != 1 || e->n > (1u << 20)) return SWIM_EINVAL;  // single shard only
+  Shard& sd = e->sh[0];
+  if (sd.c.delay_on) return SWIM_OK;
+  const uint32_t bcap = e->cfg.delay_capacity ? e->cfg.delay_capacity : 1024;
+  GMsgFull* dq = nullptr;
+  if (!sd.alloc(&dq, (size_t)DQ_BUCKETS * bcap)) return SWIM_ENOMEM;
+  sd.b.dq = dq;
+  sd.b.dq_bcap = bcap;
+  sd.c.delay_on = 1;
+  return SWIM_OK;
+}
+
+int32_t swim_set_default_delay(swim_engine* e, uint32_t m, int32_t mean_ms) {
+  if (!e || mean_ms < 0 || (m != 0xffffffffu && m >= e->n)) return SWIM_EINVAL;
+  int32_t idx = -1;
+  if (mean_ms > 0) {
+    if (int32_t rc = enable_delay(e)) return rc;
+    if (int32_t rc = delay_table(e, mean_ms, &idx)) return rc;
+  }
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  for (Shard& sd : e->sh) {
+    const int16_t v = (int16_t)idx;
+    hipError_t r = m == 0xffffffffu ? hipMemsetD16(reinterpret_cast<hipDeviceptr_t>(sd.c.default_delay), (uint16_t)v, e->n)
+                                    : hipMemcpy(sd.c.default_delay + m, &v, 2, hipMemcpyHostToDevice);
+    if (r != hipSuccess) return SWIM_EDEVICE;
+  }
+  return SWIM_OK;
+}
+
+int32_t swim_set_link_delay(swim_engine* e, uint32_t src, uint32_t dst, int32_t mean_ms) {
+  if (!e || src >= e->n || dst >= e->n) return SWIM_EINVAL;
+  int32_t idx = mean_ms < 0 ? -1 : -2;
+  if (mean_ms > 0) {
+    if (int32_t rc = enable_delay(e)) return rc;
+    if (int32_t rc = delay_table(e, mean_ms, &idx)) return rc;
+  }
+  if (idx == -1) {
+    LinkDev* L = find_link_h(e, src, dst, false);
+    if (L) L->out_delay = -1;
+  } else {
+    find_link_h(e, src, dst, true)->out_delay = idx;
   }
   prune_links(e);
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;

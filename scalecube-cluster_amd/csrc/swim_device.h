@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "../../include/swim.h"
+#include "../../include/swim_delay.h"
 #include "../../include/swim_rng.h"
 
 namespace swimdev {
@@ -36,6 +37,7 @@ enum : uint32_t {
   ERR_PAGES = 1u << 13,  // the gossip inbox page pool ran dry
   ERR_INBOX = 1u << 14,  // one receiver's gossip inbox outgrew its page table
   ERR_COLL_TOP = 1u << 15,  // a collector outgrew the top spill tier (ERR_INTERVALS: a tier's pool ran dry)
+  ERR_DELAY = 1u << 16,     // more delayed GOSSIP_REQs arrive in one tick than a delay bucket holds
 };
 
 // stats slots (swim_stats order)
@@ -62,7 +64,11 @@ struct alignas(16) MemberDev {
   uint32_t ev_minor, fetch_ctr, fd_sync_cnt, init_total, init_done;
   uint32_t ins_rank, ins_head, ins_tail;  // this phase's deferred pingMembers inserts (op chain)
   uint32_t gix_base, gix_used;  // serial of slab[0]; gix slots taken since the index was (re)built
-  uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, gix_valid, pad;
+  uint32_t ack_late;  // 1 + ticks after the ping timeout that a late direct ack arrives (0 = none)
+  uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, gix_valid;
+  uint8_t ack_ok;    // ack_due is the tick the (delayed) ack arrives, not the ping timeout
+  uint8_t relay_ok;  // relay_due is the tick the first relayed ack arrives, not the timeout
+  uint8_t pad[3];
 };
 
 // GossipState + Gossip + MembershipRecord payload, 48 B.  GossipState.infected gains a member only
@@ -109,8 +115,9 @@ struct SpillCtl {  // one per tier
 
 struct LinkDev {  // NetworkEmulator per-link override, sorted by (a, b)
   uint32_t a, b;
-  int32_t out_loss;  // outboundSettings(b) on a; -1 = none
-  int32_t in_pass;   // inboundSettings(b) on a (a receives from b); -1 = none
+  int32_t out_loss;   // outboundSettings(b) on a; -1 = none
+  int32_t in_pass;    // inboundSettings(b) on a (a receives from b); -1 = none
+  int32_t out_delay;  // outboundSettings(b).meanDelay on a as a delay-table index; -1 = none, -2 = 0 ms
 };
 
 struct GMsgFull {
@@ -203,6 +210,11 @@ struct Ctx {
   uint32_t partition;
   LinkDev* links;
   uint32_t n_links;
+  // message delay (swim_delay.h): thresholds per distinct meanDelay, the default table of each
+  // member (-1 = no delay); delay_on: some member or link has a delay
+  const uint64_t* delay_th;  // [tables][SWIM_DELAY_TICKS_MAX]
+  int16_t* default_delay;    // replicated [n]
+  uint32_t delay_on;
   uint8_t* is_seed;
   uint32_t* seeds;
   uint32_t n_seeds;
@@ -381,6 +393,24 @@ __device__ __forceinline__ bool in_pass(const Ctx& c, uint32_t b, uint32_t a) {
     if (L && L->in_pass >= 0) return L->in_pass != 0;
   }
   return c.default_inbound[b] != 0;
+}
+// tryDelayOutbound (NetworkEmulator.java:190-202) + evaluateDelay (:359-369) of a message a -> b, in
+// ticks (swim_delay.h); the draw is keyed (member, stream, sub24, sub32) and taken only when the
+// link has a mean delay
+__device__ inline uint32_t delay_ticks(const Ctx& c, uint32_t a, uint32_t b, uint32_t member, uint32_t stream,
+                                       uint32_t sub24, uint32_t sub32) {
+  if (!c.delay_on) return 0;
+  int32_t tab = c.default_delay[a];
+  if (c.n_links) {
+    const LinkDev* L = find_link(c, a, b);
+    if (L && L->out_delay != -1) tab = L->out_delay;
+  }
+  if (tab < 0) return 0;
+  const uint32_t in[4] = {member, (uint32_t)c.T, (stream << 24) | (sub24 & 0xffffffu), sub32};
+  uint32_t o[4];
+  philox4(in, c.key0, c.key1, o);
+  const uint64_t u53 = ((uint64_t)(o[0] >> 11) << 32) | o[1];
+  return swim_delay_ticks(c.delay_th + (size_t)tab * SWIM_DELAY_TICKS_MAX, u53);
 }
 // lost() with the Philox draw evaluated only when the loss percentage needs it (0 % and 100 %
 // are decided without a draw; draws are keyed, so skipping one shifts nothing)
@@ -594,7 +624,8 @@ constexpr uint32_t SUBQ = 16;
 // sub-queue of an append for (viewer, subject): hashed, not by the appending wave — one lane may
 // append thousands (a SYNC merge schedules a timer and emits an event per record it changes)
 __device__ __forceinline__ uint32_t subq(uint32_t v, uint32_t s) { return ((v * 0x9E3779B1u) ^ (s * 0x85EBCA77u)) >> 28; }
-__device__ inline void emit(const Ctx& c, uint32_t v, uint32_t s, uint32_t type, uint32_t phase, uint32_t minor) {
+__device__ inline void emit(const Ctx& c, uint32_t v, uint32_t s, uint32_t type, uint32_t phase, uint32_t minor,
+                            uint32_t data = 0) {
   const uint32_t q = subq(v, s);
   uint32_t i = atomicAdd(&c.ev_cnt[q], 1u);
   if (i >= c.ev_cap) { set_err(c, ERR_EVENTS); return; }
@@ -606,7 +637,7 @@ __device__ inline void emit(const Ctx& c, uint32_t v, uint32_t s, uint32_t type,
   e.type = type;
   e.phase = phase;
   e.minor = minor;
-  e.pad = 0;
+  e.data = data;
   c.ev[i] = e;
 }
 
@@ -725,6 +756,29 @@ __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject,
   g.subject = subject;
   g.status = status;
   g.inc = inc;
+  g.inf_period = (uint32_t)m.g_period;
+#pragma unroll
+  for (int k = 0; k < GINF; ++k) g.inf[k] = NONE;
+  slab_of(c, v)[m.gossip_len] = g;
+  m.gossip_len++;
+  gix_note(c, m, v, g.gossiper, g.seq);
+  m.g_counter++;
+  CollEnt* e = coll_ensure(c, v, v);
+  if (coll_add(c, e, g.seq, &c.seg_flag[v - c.lo])) receipt_mark(c, v, v, g.seq);
+  stat_add(c, ST_GOSSIPS_CREATED, 1);
+}
+
+// GossipProtocol.spread(Message) (GossipProtocolImpl.java:126-130): a user gossip, its payload in
+// the subject field
+__device__ inline void spread_user(const Ctx& c, uint32_t v, uint32_t payload) {
+  MemberDev& m = mem(c, v);
+  if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); return; }
+  GossipDev g;
+  g.gossiper = v;
+  g.seq = (uint32_t)m.g_counter;
+  g.subject = payload;
+  g.status = SWIM_GOSSIP_USER;
+  g.inc = 0;
   g.inf_period = (uint32_t)m.g_period;
 #pragma unroll
   for (int k = 0; k < GINF; ++k) g.inf[k] = NONE;

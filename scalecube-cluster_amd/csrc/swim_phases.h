@@ -36,6 +36,9 @@ struct Xc {
   uint32_t pad[3];
 };
 
+constexpr uint32_t DQ_BUCKETS = 2048, DQ_MASK = DQ_BUCKETS - 1;  // delay ring (> SWIM_DELAY_TICKS_MAX)
+static_assert(DQ_BUCKETS > SWIM_DELAY_TICKS_MAX, "a delayed message must not land in the current bucket");
+
 struct Bufs {
   Counters* k;
   // cross-shard exchange; an unsharded engine (world == 1) never touches these
@@ -61,6 +64,11 @@ struct Bufs {
   uint32_t* big_list;  // local indices of receivers with big inboxes (the writer that crosses wave_min)
   uint32_t* big_tick;  // per receiver: tick whose inbox took the wave-parallel path
   uint32_t wave_min;   // inboxes above this many messages take it (<= DLV_SORT)
+  // GOSSIP_REQs delayed by the network emulator (swim_delay.h): bucket (arrival tick & DQ_MASK) holds
+  // up to dq_bcap messages, .pad = the sending tick; released into the inboxes by k_dq_release
+  GMsgFull* dq;        // [DQ_BUCKETS][dq_bcap]
+  uint32_t* dq_cnt;    // [DQ_BUCKETS]
+  uint32_t dq_bcap;
   // SYNC / SYNC_ACK sub-phases (swim_sync.h): items in enqueue order; a receiver's inbox is paged
   // like the gossip inboxes: its k-th message is item pool[tab[r][k / 64]][k % 64]
   SyncReq* reqs;
@@ -366,9 +374,12 @@ __device__ inline uint32_t select_relays(const Ctx& c, uint32_t v, uint32_t t, u
 }
 
 // doPing's error branch (:153-170) + doPingReq (:173-210); the relays share the ping's correlation
-// id, so the first relayed ack to reach the issuer completes every pending relay request.
+// id, so the first relayed ack to reach the issuer completes every pending relay request.  With
+// message delay the first message carrying the cid decides: the earliest relayed ack (ties: lowest
+// relay) or a late ack of the direct ping (`late` = 1 + its arrival in ticks after the ping-req went
+// out), if the issuer's inbound filter passes its sender; none before the relay timeout: SUSPECT.
 __device__ inline void ping_req(const Ctx& c, uint32_t v, uint32_t t, unsigned long long& nev,
-                                unsigned long long& nreq) {
+                                unsigned long long& nreq, uint32_t late = 0) {
   uint32_t relays[16];
   uint32_t nr = select_relays(c, v, t, relays);
   if (nr == 0) { publish_fd(c, v, t, SWIM_SUSPECT, nev); return; }
@@ -379,25 +390,36 @@ __device__ inline void ping_req(const Ctx& c, uint32_t v, uint32_t t, unsigned l
     else { pending_mask |= 1u << j; npend++; }
   }
   if (npend == 0) return;
-  int32_t arrived = -1;
+  uint32_t best = NONE, first = NONE;  // arrival (ticks from now) and sender of the first ack
   for (uint32_t j = 0; j < nr; ++j) {
     if (!(pending_mask & (1u << j))) continue;
     uint32_t r = relays[j];
     if (in_pass(c, r, v) && !out_fail(c, r, t, v, SWIM_STREAM_TRANSIT_PING_OUT, j, 0) &&
         in_pass(c, t, r) && !out_fail(c, t, r, v, SWIM_STREAM_TRANSIT_ACK_OUT, j, 0) &&
         in_pass(c, r, t) && !out_fail(c, r, v, v, SWIM_STREAM_RELAY_ACK_OUT, j, 0)) {
-      arrived = (int32_t)j;
-      break;
+      const uint32_t at = delay_ticks(c, v, r, v, SWIM_STREAM_PINGREQ_DELAY, j, 0) +
+                          delay_ticks(c, r, t, v, SWIM_STREAM_TRANSIT_PING_DELAY, j, 0) +
+                          delay_ticks(c, t, r, v, SWIM_STREAM_TRANSIT_ACK_DELAY, j, 0) +
+                          delay_ticks(c, r, v, v, SWIM_STREAM_RELAY_ACK_DELAY, j, 0);
+      if (at < best) { best = at; first = r; }
+      if (!c.delay_on) break;  // every arrival is 0: the lowest relay
     }
   }
-  if (arrived >= 0 && in_pass(c, v, relays[arrived])) {
-    for (uint32_t i = 0; i < npend; ++i) publish_fd(c, v, t, SWIM_ALIVE, nev);
+  if (late && late - 1 < best) { best = late - 1; first = t; }
+  MemberDev& m = mem(c, v);
+  if (first != NONE && best < c.relay_ticks && in_pass(c, v, first)) {
+    if (best == 0) {
+      for (uint32_t i = 0; i < npend; ++i) publish_fd(c, v, t, SWIM_ALIVE, nev);
+      return;
+    }
+    m.relay_due = c.T + best;  // the acks complete every pending relay request then
+    m.relay_ok = 1;
   } else {
-    MemberDev& m = mem(c, v);
     m.relay_due = c.T + c.relay_ticks;
-    m.relay_target = t;
-    m.relay_pending = npend;
+    m.relay_ok = 0;
   }
+  m.relay_target = t;
+  m.relay_pending = npend;
 }
 
 __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& nev, unsigned long long& nreq,
@@ -408,15 +430,16 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
   c.fd_next[v - c.lo] = fd_next_of(c, m, c.T);  // ack / relay timeouts set below are > T
   if (!due && m.relay_due != c.T && m.ack_due != c.T) return;
   m.ev_minor = 0;
-  if (m.relay_due == c.T) {  // relay timeouts (:200-209)
+  if (m.relay_due == c.T) {  // relayed acks arrive (:190-199) or the relay timeouts (:200-209)
     uint32_t t = m.relay_target, k = m.relay_pending;
     m.relay_due = 0;
-    for (uint32_t i = 0; i < k; ++i) publish_fd(c, v, t, SWIM_SUSPECT, nev);
+    for (uint32_t i = 0; i < k; ++i) publish_fd(c, v, t, m.relay_ok ? SWIM_ALIVE : SWIM_SUSPECT, nev);
   }
-  if (m.ack_due == c.T) {  // pingTimeout elapsed
+  if (m.ack_due == c.T) {  // the delayed ack arrives, or pingTimeout elapsed
     uint32_t t = m.ack_target;
     m.ack_due = 0;
-    ping_req(c, v, t, nev, nreq);
+    if (m.ack_ok) publish_fd(c, v, t, SWIM_ALIVE, nev);
+    else ping_req(c, v, t, nev, nreq, m.ack_late);
   }
   if (due) {  // doPing (:126-171), selectPingMember (:352-361)
     m.fd_period++;
@@ -430,11 +453,20 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
       npings++;
       if (out_fail(c, v, t, v, SWIM_STREAM_PING_OUT, 0, 0)) {
         ping_req(c, v, t, nev, nreq);
-      } else if (in_pass(c, t, v) && !out_fail(c, t, v, v, SWIM_STREAM_ACK_OUT, 0, 0) && in_pass(c, v, t)) {
-        publish_fd(c, v, t, SWIM_ALIVE, nev);
       } else {
-        m.ack_due = c.T + c.to_ticks;
-        m.ack_target = t;
+        // onPing answers DEST_OK (:227-259); the round trip takes the two messages' delays
+        const bool acked = in_pass(c, t, v) && !out_fail(c, t, v, v, SWIM_STREAM_ACK_OUT, 0, 0);
+        const uint32_t rtt = acked ? delay_ticks(c, v, t, v, SWIM_STREAM_PING_DELAY, 0, 0) +
+                                         delay_ticks(c, t, v, v, SWIM_STREAM_ACK_DELAY, 0, 0)
+                                   : 0u;
+        if (acked && rtt == 0 && in_pass(c, v, t)) {
+          publish_fd(c, v, t, SWIM_ALIVE, nev);
+        } else {
+          m.ack_target = t;
+          m.ack_ok = acked && rtt < c.to_ticks && in_pass(c, v, t);
+          m.ack_due = c.T + (m.ack_ok ? rtt : c.to_ticks);
+          m.ack_late = acked && rtt >= c.to_ticks ? rtt - c.to_ticks + 1 : 0;
+        }
       }
     }
   }
@@ -568,11 +600,17 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       seen_keep = kmask != 0;
     }
     if (keep) {
-      slab[w + lanes_below(kmask)] = g;
-      // futures (:167-180): the graceful-leave future stops the member at the end of the tick
-      if (leaving && period > (uint64_t)g.inf_period + spread && g.gossiper == m.leave_gossiper &&
-          g.seq == (uint32_t)m.leave_seq)
-        done = true;
+      // futures (:167-180, :360-368): the graceful-leave future stops the member at the end of the
+      // tick; a user gossip's spread() completes (this round's copies were read before the mark)
+      GossipDev gw = g;
+      if (period > (uint64_t)g.inf_period + spread) {
+        if (leaving && g.gossiper == m.leave_gossiper && g.seq == (uint32_t)m.leave_seq) done = true;
+        if (g.status == SWIM_GOSSIP_USER && g.gossiper == v) {
+          gw.status = SWIM_GOSSIP_USER_SPREAD;
+          emit(c, v, v, SWIM_EV_SPREAD_DONE, SWIM_PHASE_GOSSIP, 0x80000000u | (g.seq & 0x7fffffffu), g.subject);
+        }
+      }
+      slab[w + lanes_below(kmask)] = gw;
     }
     w += (uint32_t)__popcll(kmask);
     uint32_t matb = 0;  // bit j: a message to target j is materialised
@@ -583,9 +621,25 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         nmsg += send ? 1u : 0u;
         // delivered copies; a receiver on this shard that already holds the sequence id drops it
         // (its collector only grows until delivery), another shard flags it on arrival
-        const bool mat = send && c.up[t] && in_pass(c, t, v) &&
-                         !lost_k(c, out_loss(c, v, t), v, SWIM_STREAM_GOSSIP_OUT, j, p) &&
-                         !(owned(c, t) && known_received(c, t, g.gossiper, g.seq));
+        bool mat = send && c.up[t] && in_pass(c, t, v) && !lost_k(c, out_loss(c, v, t), v, SWIM_STREAM_GOSSIP_OUT, j, p);
+        // a delayed copy waits in the arrival tick's bucket (delivered whatever the receiver's
+        // collector holds by then: a clear may come in between)
+        const uint32_t k = mat ? delay_ticks(c, v, t, v, SWIM_STREAM_GOSSIP_DELAY, j, p) : 0u;
+        if (k) {
+          mat = false;
+          const uint32_t bk = (uint32_t)(c.T + k) & DQ_MASK;
+          const uint32_t q = atomicAdd(&b.dq_cnt[bk], 1u);
+          if (q < b.dq_bcap) {
+            GMsgFull msg;
+            msg.to = t; msg.from = v; msg.pos = p; msg.slot = 0;
+            msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
+            msg.inc = g.inc; msg.pseq = 0; msg.dup = 0; msg.pad = (uint32_t)c.T;
+            b.dq[(size_t)bk * b.dq_bcap + q] = msg;
+          } else {
+            set_err(c, ERR_DELAY);
+          }
+        }
+        mat = mat && !(owned(c, t) && known_received(c, t, g.gossiper, g.seq));
         matb |= (mat ? 1u : 0u) << j;
       }
     }
@@ -764,6 +818,35 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned lo
   wave_stat_add(c, ST_GOSSIP_MESSAGES, nmsg);
 }
 
+// GOSSIP_REQs delayed by the network emulator that arrive in tick T join the inboxes (one launch of
+// ceil(cnt / 256) workgroups; emit never writes the bucket of the current tick, and k_end_tick empties
+// it).  Each (receiver, sending tick, sender) group gets pseq dense in slab-position order, as emit
+// gives a round's fresh messages, so the deliverer ranks them by their snd_key.
+__global__ void __launch_bounds__(256) k_dq_release(KP) {
+  const Ctx c = pctx(P, T);
+  const Bufs b = P->b;
+  const uint32_t bk = (uint32_t)T & DQ_MASK;
+  const uint32_t cnt = min(b.dq_cnt[bk], b.dq_bcap);
+  const GMsgFull* q = b.dq + (size_t)bk * b.dq_bcap;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); i0 < cnt; i0 += gridDim.x * blockDim.x) {
+    const uint32_t i = i0 + lane;
+    const bool valid = i < cnt;
+    GMsgFull msg{};
+    if (valid) {
+      msg = q[i];
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < cnt; ++j) {
+        const GMsgFull& o = q[j];
+        rank += (o.to == msg.to && o.pad == msg.pad && o.from == msg.from && o.pos < msg.pos) ? 1u : 0u;
+      }
+      msg.pseq = rank;
+      msg.pad = (uint32_t)T - msg.pad;  // age: snd_key orders earlier rounds first
+    }
+    deliver_local_msg(c, b, msg, valid);  // every lane of the wave takes part
+  }
+}
+
 // GOSSIP_REQs arriving from other shards join the local message list exactly as a local send does;
 // provable duplicates (the emitter could not see this shard's collectors) are flagged, and delivery
 // skips them: the collector holds the sequence id, so onGossipReq would return at once
@@ -791,7 +874,14 @@ __global__ void k_recv_msgs(KP, uint32_t nrx) {
 #endif
 constexpr int DLV_SORT = DLV_SORT_N;
 
-__device__ __forceinline__ uint64_t msg_key(const GMsgFull& m) { return ((uint64_t)m.from << 32) | m.pos; }
+// canonical sender key: earlier sending rounds first (a released delayed message's pad holds its age
+// in ticks, DQ: n <= 2^20 when delays are on), then the sender
+__device__ __forceinline__ uint32_t snd_key(const Ctx& c, const GMsgFull& g) {
+  return c.delay_on ? ((4095u - min(g.pad, 4095u)) << 20) | g.from : g.from;
+}
+__device__ __forceinline__ uint64_t msg_key(const Ctx& c, const GMsgFull& m) {
+  return ((uint64_t)snd_key(c, m) << 32) | m.pos;
+}
 
 
 // onGossipReq (GossipProtocolImpl.java:201-215) for one received message, in canonical order
@@ -814,8 +904,10 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, Gos
     for (int k = 1; k < GINF; ++k) ns.inf[k] = NONE;
     slab[m.gossip_len++] = ns;
     gix_note(c, m, r, ns.gossiper, ns.seq);
+    if (g.status >= SWIM_GOSSIP_USER)  // sink.next(gossip.message()) (:209): listen() subscribers
+      emit(c, r, g.gossiper, SWIM_EV_GOSSIP, SWIM_PHASE_GOSSIP, m.ev_minor++, g.subject);
     // onMembershipGossip (MembershipProtocolImpl.java:452-459)
-    if (update_membership(c, r, g.subject, g.status, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP))
+    else if (update_membership(c, r, g.subject, g.status, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP))
       apply_alive(c, r, g.subject, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP);
   } else {
     GossipDev& st = slab[found];
@@ -969,7 +1061,7 @@ __device__ __forceinline__ int big_find(const uint32_t* snd, uint32_t nd, uint32
 // order, 64 messages at a time, after every lane has staged its message in LDS and touched the
 // collector probe and view cell that message's step will read (the serial chain then hits L2).
 // Then the receiver's pingMembers inserts of the phase and its SYNC collection.
-__device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Bufs& b, uint32_t i, uint32_t lane,
+__device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Bufs& b, uint32_t i, uint32_t lane, int collect,
                                           BigLds& L, unsigned long long& nsync) {
   const uint32_t r = c.lo + i;
   const uint32_t k_all = b.msg_cnt[i];
@@ -991,7 +1083,7 @@ __device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Buf
     bool over = false;
     for (uint32_t q0 = 0; q0 < k && !over; q0 += 64) {
       const uint32_t q = q0 + lane;
-      const uint32_t f = q < k ? msg_at(q).from : NONE;
+      const uint32_t f = q < k ? snd_key(c, msg_at(q)) : NONE;
       uint64_t todo = __ballot(q < k);
       while (todo) {
         const uint32_t sf = __shfl(f, (int)__ffsll((unsigned long long)todo) - 1, 64);
@@ -1015,7 +1107,7 @@ __device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Buf
       for (;;) {
         uint32_t mn = NONE;
         for (uint32_t q = lane; q < k; q += 64) {
-          const uint32_t f = msg_at(q).from;
+          const uint32_t f = snd_key(c, msg_at(q));
           if (f >= lo_s && f < mn) mn = f;
         }
 #pragma unroll
@@ -1024,7 +1116,7 @@ __device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Buf
         uint32_t cnt = 0;
         for (uint32_t q0 = 0; q0 < k; q0 += 64) {
           const uint32_t q = q0 + lane;
-          const bool mine = q < k && msg_at(q).from == mn;
+          const bool mine = q < k && snd_key(c, msg_at(q)) == mn;
           if (mine && rank + msg_at(q).pseq < k) perm_at(rank + msg_at(q).pseq) = q;
           cnt += (uint32_t)__popcll(__ballot(mine));
         }
@@ -1059,7 +1151,7 @@ __device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Buf
         uint32_t f = NONE, ps = 0;
         if (q < k) {
           const GMsgFull& g = msg_at(q);
-          f = g.from;
+          f = snd_key(c, g);
           ps = g.pseq;
         }
         uint64_t todo = __ballot(q < k);
@@ -1092,7 +1184,8 @@ __device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Buf
         const GMsgFull g = msg_at(j);
         L.m[lane] = g;
         const CollEnt* e = coll_find(c, r, g.gossiper);
-        sink ^= (e ? e->meta : 1u) ^ c.recs[row + g.subject] ^ c.aux[row + g.subject];
+        if (g.status < SWIM_GOSSIP_USER) sink ^= c.recs[row + g.subject] ^ c.aux[row + g.subject];
+        sink ^= e ? e->meta : 1u;
       }
       wave_sync();
       if (lane == 0) {
@@ -1108,7 +1201,7 @@ __device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Buf
   // the inbox pages go back to the pool (the pool itself restarts every tick)
   for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) b.pg_tab[(size_t)i * b.pg_max + pg] = NONE;
   apply_ins_batch<64, false>(c, r, lane, L.iP, L.iS, L.iR);
-  if (lane == 0) nsync += sync_collect_member(cs, b, r);  // phase D's SYNC collection for r
+  if (lane == 0 && collect) nsync += sync_collect_member(cs, b, r);  // phase D's SYNC collection for r
   return acc;
 }
 
@@ -1119,7 +1212,7 @@ __device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Buf
 // schedule and fd_sync queue).  First the big inboxes, a wave each, grid-stride over big_list;
 // then each workgroup's blocks of 256 members: small inboxes thread per receiver, their inserts by
 // the workgroup, the collection of members whose inbox was not big.
-__global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
+__global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect) {
   const Ctx c = pctx(P, T);
   const Ctx cs = pctx_sync(P, T);
   const Bufs b = P->b;
@@ -1137,7 +1230,7 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
     const uint32_t nbig = b.k->big_cnt;
     for (uint32_t x = __builtin_amdgcn_readfirstlane(blockIdx.x * DLV_WAVES + wv); x < nbig;
          x += gridDim.x * DLV_WAVES)
-      acc += deliver_big(c, cs, b, b.big_list[x], lane, s_big[wv], nsync);
+      acc += deliver_big(c, cs, b, b.big_list[x], lane, collect, s_big[wv], nsync);
   }
   for (uint32_t base = blockIdx.x * DLV_BLOCK; base < c.nl; base += gridDim.x * DLV_BLOCK) {
     if (tid == 0) s_nins = 0;
@@ -1161,7 +1254,7 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
         } else {
           const GMsgFull* a = b.pg_msgs + (size_t)pid * 64;
           for (uint32_t q = 0; q < k; ++q) {
-            const uint64_t kx = msg_key(a[q]);  // keys are unique
+            const uint64_t kx = msg_key(c, a[q]);  // keys are unique
             int32_t j = (int32_t)q - 1;
             while (j >= 0 && s_key[j][tid] > kx) {
               s_key[j + 1][tid] = s_key[j][tid];
@@ -1179,7 +1272,7 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP) {
     __syncthreads();
     const uint32_t nv = s_nins;
     for (uint32_t q = 0; q < nv; ++q) apply_ins_batch<DLV_BLOCK, true>(c, s_ins[q], tid, s_iP, s_iS, s_iR);
-    if (i < c.nl && !big) nsync += sync_collect_member(cs, b, c.lo + i);
+    if (collect && i < c.nl && !big) nsync += sync_collect_member(cs, b, c.lo + i);
   }
   wave_stat_add(c, ST_GOSSIP_ACCEPTED, acc);
   wave_stat_add(cs, ST_SYNCS, nsync);
@@ -1497,6 +1590,7 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, uint32_t n_rx_stops,
       b.ack_snap[m] = NONE;
     }
     if (i == 0) b.snap_cnt[par ^ 1u] = 0;
+    if (i == 0 && c.delay_on) b.dq_cnt[(uint32_t)T & DQ_MASK] = 0;  // this tick's delayed arrivals are delivered
   }
   // collector blocks freed this tick become allocatable (one workgroup: the counters are read,
   // then rewritten, by the same threads)

@@ -28,6 +28,8 @@ _ERRORS = {
 
 ALIVE, SUSPECT, LEAVING, DEAD = 0, 1, 2, 3
 EV_ADDED, EV_REMOVED, EV_LEAVING, EV_UPDATED = 0, 1, 2, 3
+EV_GOSSIP, EV_SPREAD_DONE = 32, 33  # user gossips (swim_spread)
+GOSSIP_USER, GOSSIP_USER_SPREAD = 4, 5  # swim_gossip.status of a user gossip
 EV_FD_ALIVE, EV_FD_SUSPECT, EV_FD_DEAD = 16, 17, 18
 PHASE_TIMERS, PHASE_FD, PHASE_GOSSIP, PHASE_SYNC, PHASE_SYNCACK, PHASE_CONTROL = 1, 2, 3, 4, 5, 6
 ALL_MEMBERS = 0xFFFFFFFF
@@ -66,7 +68,7 @@ class swim_config(C.Structure):
         ("message_capacity", C.c_uint32),
         ("interval_capacity", C.c_uint32),
         ("deliver_wave_min", C.c_uint32),
-        ("reserved", C.c_uint32 * 1),
+        ("delay_capacity", C.c_uint32),
     ]
 
 
@@ -78,13 +80,13 @@ class swim_event(C.Structure):
         ("type", C.c_uint32),
         ("phase", C.c_uint32),
         ("minor", C.c_uint32),
-        ("pad", C.c_uint32),
+        ("data", C.c_uint32),
     ]
 
 
 EVENT_DTYPE = np.dtype(
     [("tick", "<u8"), ("viewer", "<u4"), ("subject", "<u4"), ("type", "<u4"), ("phase", "<u4"),
-     ("minor", "<u4"), ("pad", "<u4")])
+     ("minor", "<u4"), ("data", "<u4")])
 
 
 class swim_stats(C.Structure):
@@ -174,9 +176,12 @@ PROTOTYPES = {
     "swim_set_seeds": (C.c_int32, [_engp, _u32p, C.c_uint32]),
     "swim_kill": (C.c_int32, [_engp, C.c_uint32]),
     "swim_leave": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
+    "swim_spread": (C.c_int32, [_engp, C.c_uint32, C.c_uint32]),
     "swim_join": (C.c_int32, [_engp, C.c_uint32]),
     "swim_set_default_loss": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
     "swim_set_link_loss": (C.c_int32, [_engp, C.c_uint32, C.c_uint32, C.c_int32]),
+    "swim_set_default_delay": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
+    "swim_set_link_delay": (C.c_int32, [_engp, C.c_uint32, C.c_uint32, C.c_int32]),
     "swim_set_link_inbound": (C.c_int32, [_engp, C.c_uint32, C.c_uint32, C.c_int32]),
     "swim_set_default_inbound": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
     "swim_set_partition": (C.c_int32, [_engp, POINTER(C.c_uint16)]),
@@ -303,6 +308,10 @@ class Engine:
     def leave(self, m: int, stop_after: bool = True) -> None:
         _check("swim_leave", self.lib.swim_leave(self._h, m, 1 if stop_after else 0))
 
+    def spread(self, m: int, payload: int) -> None:
+        """GossipProtocol.spread: a user gossip with a 32-bit payload handle from member m, now."""
+        _check("swim_spread", self.lib.swim_spread(self._h, m, payload))
+
     def join(self, m: int) -> None:
         _check("swim_join", self.lib.swim_join(self._h, m))
 
@@ -311,6 +320,12 @@ class Engine:
 
     def set_link_loss(self, src: int, dst: int, loss_percent: int) -> None:
         _check("swim_set_link_loss", self.lib.swim_set_link_loss(self._h, src, dst, loss_percent))
+
+    def set_default_delay(self, mean_ms: int, m: int = ALL_MEMBERS) -> None:
+        _check("swim_set_default_delay", self.lib.swim_set_default_delay(self._h, m, mean_ms))
+
+    def set_link_delay(self, src: int, dst: int, mean_ms: int) -> None:
+        _check("swim_set_link_delay", self.lib.swim_set_link_delay(self._h, src, dst, mean_ms))
 
     def set_link_inbound(self, dst: int, src: int, shall_pass: int) -> None:
         _check("swim_set_link_inbound", self.lib.swim_set_link_inbound(self._h, dst, src, shall_pass))

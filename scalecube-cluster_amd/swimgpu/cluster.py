@@ -320,44 +320,87 @@ class FailureDetectorView:
         return self._c._take(self._m, fd=True)
 
 
-class NetworkEmulator:
-    """NetworkEmulator of one member (NetworkEmulator.java).  Delays are not modelled in this round:
-    a non-zero mean delay raises NotImplementedError rather than being silently ignored."""
+class GossipMessage:
+    """A user gossip as listen() delivers it (transport-api Message: the data the spreader passed)."""
+
+    def __init__(self, data, gossiper: int):
+        self.data = data
+        self.gossiper = gossiper
+
+    def __repr__(self):
+        return f"GossipMessage(data={self.data!r}, gossiper={self.gossiper})"
+
+
+class SpreadFuture:
+    """The Mono<String> GossipProtocol.spread returns: completes once the gossip has been spread for
+    periodsToSpread rounds (GossipProtocolImpl.java:167-180)."""
+
+    def __init__(self):
+        self.done = False
+        self.completed_ms = None
+
+
+class GossipProtocolView:
+    """GossipProtocol (GossipProtocol.java:12-29) of one virtual member: spread() / listen()."""
 
     def __init__(self, cluster: "SimulatedCluster", m: int):
         self._c, self._m = cluster, m
 
-    @staticmethod
-    def _no_delay(mean_delay):
-        if mean_delay:
-            raise NotImplementedError("NetworkEmulator mean delay is not modelled by the lockstep engine yet")
+    def spread(self, data) -> SpreadFuture:  # GossipProtocolImpl.spread (:126-130)
+        pid = self._c._payload_id(data)
+        fut = SpreadFuture()
+        self._c._futures[(self._m, pid)] = fut
+        self._c.engine.spread(self._m, pid)
+        return fut
+
+    def listen(self) -> list[GossipMessage]:  # the new gossips this member received since the last call
+        self._c._pump()
+        out = self._c._gossip_queues[self._m]
+        self._c._gossip_queues[self._m] = []
+        return out
+
+
+class NetworkEmulator:
+    """NetworkEmulator of one member (NetworkEmulator.java): outbound loss and mean delay per
+    destination or by default, inbound pass/block per source or by default.  Delays are quantised to
+    engine ticks (include/swim_delay.h)."""
+
+    def __init__(self, cluster: "SimulatedCluster", m: int):
+        self._c, self._m = cluster, m
 
     def outbound_settings(self, destination: int, loss_percent: int, mean_delay: int = 0):  # :69-73
-        self._no_delay(mean_delay)
+        self._c._note_link(self._m, destination)
         self._c.engine.set_link_loss(self._m, destination, loss_percent)
+        self._c.engine.set_link_delay(self._m, destination, mean_delay)
 
     def set_default_outbound_settings(self, loss_percent: int, mean_delay: int = 0):  # :80-83
-        self._no_delay(mean_delay)
         self._c.engine.set_default_loss(loss_percent, self._m)
+        self._c.engine.set_default_delay(mean_delay, self._m)
 
     def block_all_outbound(self):  # :86-90
         for d in self._c._links_from(self._m):
             self._c.engine.set_link_loss(self._m, d, -1)
+            self._c.engine.set_link_delay(self._m, d, -1)
         self._c.engine.set_default_loss(100, self._m)
+        self._c.engine.set_default_delay(0, self._m)
 
     def unblock_all_outbound(self):  # :93-97
         for d in self._c._links_from(self._m):
             self._c.engine.set_link_loss(self._m, d, -1)
+            self._c.engine.set_link_delay(self._m, d, -1)
         self._c.engine.set_default_loss(0, self._m)
+        self._c.engine.set_default_delay(0, self._m)
 
     def block_outbound(self, *destinations):  # :110-121
         for d in _flatten(destinations):
             self._c._note_link(self._m, d)
             self._c.engine.set_link_loss(self._m, d, 100)
+            self._c.engine.set_link_delay(self._m, d, 0)
 
     def unblock_outbound(self, *destinations):  # :128-139
         for d in _flatten(destinations):
             self._c.engine.set_link_loss(self._m, d, -1)
+            self._c.engine.set_link_delay(self._m, d, -1)
 
     def inbound_settings(self, destination: int, shall_pass: bool):  # :219-223
         self._c.engine.set_link_inbound(self._m, destination, 1 if shall_pass else 0)
@@ -426,6 +469,9 @@ class SimulatedCluster:
         self._fd_queues = defaultdict(list)
         self._links = defaultdict(set)
         self._inlinks = defaultdict(set)
+        self._gossip_queues = defaultdict(list)
+        self._payloads = []      # payload handle -> the spread data
+        self._futures = {}       # (member, payload handle) -> SpreadFuture
         _, self.tick_ms, self.ticks_per_period = engine.now()
         seeds = list(self.config.membership_config.seed_members)
         if seeds:
@@ -477,6 +523,9 @@ class SimulatedCluster:
     def failure_detector(self, m: int) -> FailureDetectorView:
         return FailureDetectorView(self, m)
 
+    def gossip(self, m: int) -> GossipProtocolView:
+        return GossipProtocolView(self, m)
+
     def network_emulator(self, m: int) -> NetworkEmulator:
         return NetworkEmulator(self, m)
 
@@ -503,11 +552,23 @@ class SimulatedCluster:
         self._inlinks[a].clear()
         return s
 
+    def _payload_id(self, data) -> int:
+        self._payloads.append(data)
+        return len(self._payloads) - 1
+
     def _pump(self):
         ev = self.engine.drain_events()
         for e in ev:
             t = int(e["type"])
-            if t in _FD_EV:
+            if t == abi.EV_GOSSIP:
+                self._gossip_queues[int(e["viewer"])].append(
+                    GossipMessage(self._payloads[int(e["data"])], int(e["subject"])))
+            elif t == abi.EV_SPREAD_DONE:
+                fut = self._futures.pop((int(e["viewer"]), int(e["data"])), None)
+                if fut is not None:
+                    fut.done = True
+                    fut.completed_ms = int(e["tick"]) * self.tick_ms
+            elif t in _FD_EV:
                 self._fd_queues[int(e["viewer"])].append(FailureDetectorEvent(Member(int(e["subject"])), _FD_EV[t]))
             else:
                 self._queues[int(e["viewer"])].append(

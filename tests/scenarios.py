@@ -24,6 +24,7 @@ class Scenario:
     seeds: tuple = ()
     ops: list = dataclasses.field(default_factory=list)  # (tick, op, args...) applied before tick+1
     check_every: int = 10
+    shardable: bool = True  # False: uses a single-shard-only feature (message delay)
 
 
 def apply_op(e: abi.Engine, op, args):
@@ -41,6 +42,12 @@ def apply_op(e: abi.Engine, op, args):
         e.set_link_inbound(*args)
     elif op == "default_in":
         e.set_default_inbound(*args)
+    elif op == "default_delay":
+        e.set_default_delay(*args)
+    elif op == "link_delay":
+        e.set_link_delay(*args)
+    elif op == "spread":
+        e.spread(*args)
     elif op == "partition":
         e.set_partition(None if args[0] is None else np.asarray(args[0], dtype=np.uint16))
     else:
@@ -143,6 +150,24 @@ def catalog() -> list[Scenario]:
                  + [(10 * p, "kill", (7 + 13 * p + 100 * j) % 200) for p in range(1, 26) for j in range(2)]
                  + [(10 * p, "join", 200 + 2 * (p - 1) + j) for p in range(1, 26) for j in range(2)],
                  check_every=50),
+        # user gossips (GossipProtocol.spread / listen) under 25 % loss: GossipProtocolTest's N=10 row
+        # (:47-63), three gossips from three members, one while another is still spreading
+        Scenario("user_gossip_10_loss25", 10, 10, 160, seed=16,
+                 ops=[(0, "loss", 25, abi.ALL_MEMBERS), (5, "spread", 0, 101), (5, "spread", 3, 102),
+                      (12, "spread", 7, 103)], check_every=20),
+        # GossipDelayTest (:33-69): members 0 and 1 delay every message by 3 s on average, member 2 by
+        # 100 ms; member 0 spreads three gossips (failure detector and SYNC pushed past the window)
+        Scenario("gossip_delay_3", 3, 3, 190, seed=17, cfg=dict(ping_interval=3_600_000, sync_interval=3_600_000),
+                 ops=[(0, "default_delay", 3000, 0), (0, "default_delay", 3000, 1), (0, "default_delay", 100, 2),
+                      (1, "spread", 0, 1), (1, "spread", 0, 2), (1, "spread", 0, 3)],
+                 check_every=20, shardable=False),
+        # the whole stack under delay: a 150 ms mean delay on every message (round trips beyond the
+        # 500 ms ping timeout, late direct acks racing the relays, gossips arriving on non-gossip
+        # ticks), a slow link, 5 % loss, a kill, a user gossip
+        Scenario("delay_fd_gossip_12", 12, 12, 700, seed=18,
+                 ops=[(0, "default_delay", 150, abi.ALL_MEMBERS), (0, "loss", 5, abi.ALL_MEMBERS),
+                      (0, "link_delay", 2, 5, 2500), (50, "spread", 4, 77), (120, "kill", 9)],
+                 check_every=50, shardable=False),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),
                  cfg=dict(sync_interval=5000), ops=[(100, "partition", _partition(32, 16)), (1100, "partition", None)],

@@ -104,6 +104,8 @@ def test_gpu_parity_config2_1024(glib, olib):
 @pytest.mark.parametrize("shards", [2, 3])
 @pytest.mark.parametrize("sc", scenarios.catalog(), ids=lambda s: s.name)
 def test_gpu_sharded_parity_scenario(glib, olib, sc, shards):
+    if not sc.shardable:
+        pytest.skip("message delay is single-shard only")
     _run_parity(glib, olib, dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": shards}))
 
 
@@ -127,6 +129,8 @@ def test_gpu_matches_golden_digest(glib, sc, shards):
     want = golden["scenarios"][sc.name]
     if shards > sc.capacity:
         pytest.skip("more shards than members")
+    if shards > 1 and not sc.shardable:
+        pytest.skip("message delay is single-shard only")
     sc2 = dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": shards})
     e = scenarios.make_engine(glib, sc2)
     scenarios.run(e, sc2)

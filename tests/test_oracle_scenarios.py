@@ -9,7 +9,7 @@ import pytest
 
 import oracle
 from swimgpu import abi
-from swimgpu.cluster import ClusterConfig, MembershipEvent, MemberStatus, SimulatedCluster
+from swimgpu.cluster import ClusterConfig, ClusterMath, MembershipEvent, MemberStatus, SimulatedCluster
 
 Type = MembershipEvent.Type
 
@@ -277,3 +277,105 @@ def test_config2_1024_single_failure_converges():
     assert all(len(removed[v]) == 1 and removed[v][0].member.id == 17 for v in range(1024) if v != 17)
     t_rem = [removed[v][0].timestamp / 1000 for v in range(1024) if v != 17]
     assert min(t_rem) >= 10 + 55 and max(t_rem) <= 10 + 55 + 20
+
+
+# ------------------------------------------------------------------------------ GossipProtocolTest
+# testGossipProtocol (:107-199) over the experiment rows (:47-63) whose mean delay (2 ms) is below
+# one 100 ms tick; the default outbound loss on every member; one gossip from member 0.
+@pytest.mark.parametrize("n,loss", [(2, 0), (3, 0), (5, 0), (10, 0), (10, 10), (10, 25), (10, 50), (50, 0),
+                                    (50, 10)])
+def test_gossip_protocol_experiment(n, loss):
+    c = make(ClusterConfig.default_config(), n, seed=3)
+    for m in range(n):
+        c.network_emulator(m).set_default_outbound_settings(loss, 0)
+    gcfg = c.config.gossip_config
+    timeout_ms = ClusterMath.gossip_timeout_to_sweep(gcfg.gossip_repeat_mult, n, gcfg.gossip_interval)
+    data = "test gossip - 7"
+    fut = c.gossip(0).spread(data)
+    t0 = c.now_ms
+    receivers, dissemination = {}, None
+
+    def pump():
+        nonlocal dissemination
+        for m in range(n):
+            for g in c.gossip(m).listen():
+                if g.data == data:
+                    receivers[m] = receivers.get(m, 0) + 1
+        if dissemination is None and len(receivers) == n - 1:
+            dissemination = c.now_ms - t0
+
+    while c.now_ms - t0 < 2 * timeout_ms and dissemination is None:  # latch.await(2 * gossipTimeout)
+        c.step_ticks(1)
+        pump()
+    assert len(receivers) == n - 1 and 0 not in receivers, "Not all members received gossip"
+    assert dissemination < timeout_ms, f"Too long dissemination time {dissemination}ms (timeout {timeout_ms}ms)"
+    # awaitFullCompletion: the gossip's whole lifetime plus three gossip intervals
+    c.await_seconds((timeout_ms - dissemination + 3 * gcfg.gossip_interval) / 1000)
+    pump()
+    assert all(k == 1 for k in receivers.values()), "Delivered gossip twice to same member"
+    assert fut.done  # spread()'s Mono completed at the originator
+
+
+def gossip_only_config():
+    """GossipProtocolTest / GossipDelayTest run GossipProtocolImpl alone over a static member list
+    (initGossipProtocol :274-295): the failure detector and SYNC are pushed past the test window."""
+    return (ClusterConfig.default_config()
+            .failure_detector(ping_interval=3_600_000, ping_timeout=500)
+            .membership(sync_interval=3_600_000))
+
+
+# GossipProtocolTest rows with a 100 ms mean delay (:47-63): delays quantised to the 100 ms tick
+@pytest.mark.parametrize("n,loss,delay", [(10, 25, 100), (50, 10, 100), (10, 0, 300)])
+def test_gossip_protocol_experiment_delayed(n, loss, delay):
+    c = make(gossip_only_config(), n, seed=5)
+    for m in range(n):
+        c.network_emulator(m).set_default_outbound_settings(loss, delay)
+    gcfg = c.config.gossip_config
+    timeout_ms = ClusterMath.gossip_timeout_to_sweep(gcfg.gossip_repeat_mult, n, gcfg.gossip_interval)
+    data = "delayed gossip"
+    fut = c.gossip(0).spread(data)
+    t0 = c.now_ms
+    receivers, dissemination = {}, None
+    while c.now_ms - t0 < 2 * timeout_ms:
+        c.step_ticks(1)
+        for m in range(n):
+            for g in c.gossip(m).listen():
+                if g.data == data:
+                    receivers[m] = receivers.get(m, 0) + 1
+        if dissemination is None and len(receivers) == n - 1:
+            dissemination = c.now_ms - t0
+    assert len(receivers) == n - 1 and 0 not in receivers, "Not all members received gossip"
+    assert dissemination < timeout_ms
+    assert all(k == 1 for k in receivers.values()), "Delivered gossip twice to same member"
+    assert fut.done
+
+
+# GossipDelayTest.testMessageDelayMoreThanGossipSweepTime (:33-69): members 0 and 1 delay every
+# outbound message by 3,000 ms on average, member 2 by 100 ms; member 0 spreads three gossips
+def test_gossip_delay_more_than_sweep_time():
+    c = make(gossip_only_config(), 3, seed=9)
+    for m, d in ((0, 3000), (1, 3000), (2, 100)):
+        c.network_emulator(m).set_default_outbound_settings(0, d)
+    for i in range(3):
+        c.gossip(0).spread(f"message: {i}")
+    gcfg = c.config.gossip_config
+    sweep_ms = ClusterMath.gossip_timeout_to_sweep(gcfg.gossip_repeat_mult, 3, gcfg.gossip_interval)
+    counts = [0, 0, 0]
+    ticks = 2 * (sweep_ms + 6000) // c.tick_ms
+    for _ in range(ticks):
+        c.step_ticks(1)
+        for m in range(3):
+            counts[m] += len(c.gossip(m).listen())
+    assert counts == [0, 3, 3]
+
+
+# FailureDetectorTest-style: a slow link (mean delay well above the ping timeout) makes the direct
+# ping time out, yet the member stays trusted through the relays; a fast one answers directly
+def test_fd_delay_trusted_through_relays():
+    c = make(fd_config(), 4, seed=11)
+    c.network_emulator(0).outbound_settings(1, 0, 2000)  # 0 -> 1 slow
+    c.await_seconds(10)
+    fd = c.failure_detector(0).listen()
+    statuses = {ev.status for ev in fd if ev.member.id == 1}
+    assert MemberStatus.ALIVE in statuses
+    assert trusted(c, 0) == [0, 1, 2, 3]
