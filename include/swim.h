@@ -216,6 +216,16 @@ int32_t swim_join(swim_engine* e, uint32_t m);
  * completion with SWIM_EV_SPREAD_DONE. */
 int32_t swim_spread(swim_engine* e, uint32_t m, uint32_t payload);
 
+/* ClusterImpl.updateMetadata (:497-500): member m's metadata changes (its version + 1) and
+ * MembershipProtocolImpl.updateIncarnation (:214-226) puts ALIVE inc+1 and spreads it; a viewer
+ * that then admits the record fetches the new metadata and publishes UPDATED (:780-781). */
+int32_t swim_update_metadata(swim_engine* e, uint32_t m);
+/* MembershipConfig.namespace of every member as a group id (ns_of_member[capacity] < n_ns) and the
+ * n_ns x n_ns matrix related[a * n_ns + b] = areNamespacesRelated(a, b) (:511-536): updateMembership
+ * skips records of members in unrelated namespaces (:575-586).  n_ns = 0 restores one namespace.
+ * SWIM_ESTATE if two initially joined members are unrelated (the converged start holds both). */
+int32_t swim_set_namespaces(swim_engine* e, const uint16_t* ns_of_member, uint32_t n_ns, const uint8_t* related);
+
 /* ---- network emulator (NetworkEmulator.java) ----------------------------------------------
  * Outbound loss is decided at the sender and fails the send immediately (:167-181); inbound
  * blocking silently drops at the receiver (NetworkEmulatorTransport.java:69-83). */

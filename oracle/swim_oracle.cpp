@@ -235,6 +235,15 @@ struct swim_engine {
   std::vector<uint8_t> default_inbound;
   std::map<LinkKey, int32_t> link_loss;     // (src,dst) -> loss %
   std::map<LinkKey, uint8_t> link_inbound;  // (dst,src) -> shallPass
+  // MembershipConfig.namespace of each member as a group id, and which groups are related
+  // (areNamespacesRelated :511-536); n_ns = 0: one namespace
+  std::vector<uint16_t> ns;
+  std::vector<uint8_t> ns_rel;
+  uint32_t n_ns = 0;
+  // metadata: version of each member's metadata (ClusterImpl.updateMetadata :497-500 bumps it) and,
+  // once a metadata update happened, the version each viewer's MetadataStore holds per subject
+  std::vector<uint32_t> meta_ver;
+  std::vector<std::vector<uint32_t>> meta_seen;
   std::vector<int32_t> default_delay;       // OutboundSettings.meanDelay (ms) per member
   std::map<LinkKey, int32_t> link_delay;    // (src,dst) -> meanDelay (ms)
   std::map<int32_t, std::vector<uint64_t>> delay_tab;  // meanDelay -> thresholds (swim_delay.h)
@@ -426,7 +435,8 @@ struct swim_engine {
     Member& mv = m[v];
     const uint32_t s = r1.member;
     uint64_t& c = mv.row[s];
-    // (namespace filter :575-586: every simulated member shares one namespace)
+    // namespace filter (:575-586)
+    if (n_ns && !ns_rel[(size_t)ns[v] * n_ns + ns[s]]) return;
     const bool present = c_has(c, B_IN_TABLE);
     Record r0v{s, c_status(c), c_inc(c)};
     const Record* r0 = present ? &r0v : nullptr;
@@ -493,15 +503,24 @@ struct swim_engine {
     cancel_timer(v, s);
     if (reason != MEMBERSHIP_GOSSIP && reason != INITIAL_SYNC) spread_gossip(v, r1);
     uint64_t& c = mv.row[s];
-    c |= B_HAS_METADATA;  // metadataStore.updateMetadata
+    // metadataStore.updateMetadata(member, metadata1) returns metadata0 (null when none is stored);
+    // metadata1 is the subject's metadata now (the fetch answers within the tick)
+    const bool had_meta = c_has(c, B_HAS_METADATA);
+    bool same_meta = had_meta;
+    if (!meta_seen.empty()) {
+      same_meta = had_meta && meta_seen[v][s] == meta_ver[s];
+      meta_seen[v][s] = meta_ver[s];
+    }
+    c |= B_HAS_METADATA;
     const bool exists = c_has(c, B_IN_MEMBERS);
     if (!c_has(c, B_IN_TABLE)) mv.table_size++;
     if (!exists) mv.members_size++;
     c = c_with_record(c | B_IN_TABLE | B_IN_MEMBERS, SWIM_ALIVE, r1.inc);
     if (!exists) {
-      // metadata never changes in the simulation, so an existing member yields no UPDATED
       publish_event(v, s, SWIM_EV_ADDED, phase, ev_minor_for(v, phase, s));
       c |= B_ALIVE_EMITTED;
+    } else if (!same_meta) {  // !metadata1.equals(metadata0) (:780-781)
+      publish_event(v, s, SWIM_EV_UPDATED, phase, ev_minor_for(v, phase, s));
     }
   }
 
@@ -1207,6 +1226,7 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
     e->is_seed.assign(capacity, 0);
     e->default_loss.assign(capacity, 0);
     e->default_delay.assign(capacity, 0);
+    e->meta_ver.assign(capacity, 0);
     e->default_inbound.assign(capacity, 1);
     e->group.assign(capacity, 0);
     for (auto& mm : e->m) mm.row.assign(capacity, 0);
@@ -1377,6 +1397,42 @@ int32_t swim_set_default_loss(swim_engine* e, uint32_t mm, int32_t pct) {
 int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t pct) {
   if (!e || src >= e->n || dst >= e->n || pct > 100) return SWIM_EINVAL;
   if (pct < 0) e->link_loss.erase({src, dst}); else e->link_loss[{src, dst}] = pct;
+  return SWIM_OK;
+}
+
+int32_t swim_set_namespaces(swim_engine* e, const uint16_t* ns_of_member, uint32_t n_ns, const uint8_t* related) {
+  if (!e) return SWIM_EINVAL;
+  if (n_ns == 0 || !ns_of_member) {
+    e->n_ns = 0;
+    return SWIM_OK;
+  }
+  if (!related || n_ns > 4096) return SWIM_EINVAL;
+  for (uint32_t i = 0; i < e->n; ++i)
+    if (ns_of_member[i] >= n_ns) return SWIM_EINVAL;
+  // the converged start holds every initial member in every initial member's table
+  std::vector<uint8_t> used(n_ns, 0);
+  for (uint32_t a = 0; a < e->n; ++a)
+    if (e->m[a].joined) used[ns_of_member[a]] = 1;
+  for (uint32_t x = 0; x < n_ns; ++x)
+    for (uint32_t y = 0; y < n_ns; ++y)
+      if (used[x] && used[y] && !related[(size_t)x * n_ns + y]) return SWIM_ESTATE;
+  e->ns.assign(ns_of_member, ns_of_member + e->n);
+  e->ns_rel.assign(related, related + (size_t)n_ns * n_ns);
+  e->n_ns = n_ns;
+  return SWIM_OK;
+}
+
+int32_t swim_update_metadata(swim_engine* e, uint32_t v) {
+  if (!e || v >= e->n) return SWIM_EINVAL;
+  Member& mv = e->m[v];
+  if (!mv.up) return SWIM_ESTATE;
+  if (e->meta_seen.empty()) e->meta_seen.assign(e->n, std::vector<uint32_t>(e->n, 0));
+  e->meta_ver[v]++;  // metadataStore.updateMetadata(metadata) (ClusterImpl.java:497-500)
+  // updateIncarnation (MembershipProtocolImpl.java:214-226): ALIVE inc+1, spread
+  uint64_t& c = mv.row[v];
+  Record r{v, SWIM_ALIVE, c_inc(c) + 1};
+  c = c_with_record(c, r.status, r.inc);
+  e->spread_gossip(v, r);
   return SWIM_OK;
 }
 

@@ -684,6 +684,17 @@ __global__ void k_leave(Ctx c, uint32_t v, int32_t stop_after) {
   }
 }
 
+// ClusterImpl.updateMetadata (:497-500) + updateIncarnation (MembershipProtocolImpl.java:214-226)
+__global__ void k_update_meta(Ctx c, uint32_t v, int owner) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  c.meta_ver[v]++;
+  if (!owner) return;
+  const uint64_t cell = cell_get(c, v, v);
+  const int32_t inc = c_inc(cell) + 1;
+  cell_put(c, v, v, c_with_record(cell, SWIM_ALIVE, inc));
+  spread_gossip(c, v, v, SWIM_ALIVE, inc);
+}
+
 __global__ void k_spread(Ctx c, uint32_t v, uint32_t payload) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   spread_user(c, v, payload);
@@ -784,7 +795,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&c.wheel, (size_t)(c.wheel_mask + 1) * c.wheel_cap) &&
             sd.alloc(&c.wheel_cnt, (size_t)(c.wheel_mask + 1) * c.wheel_nq) && sd.alloc(&c.ev, (size_t)c.ev_cap * SUBQ) &&
             sd.alloc(&c.ev_cnt, SUBQ) && sd.alloc(&c.default_loss, n) &&
-            sd.alloc(&c.default_delay, n) && sd.alloc(&b.dq_cnt, DQ_BUCKETS) &&
+            sd.alloc(&c.default_delay, n) && sd.alloc(&b.dq_cnt, DQ_BUCKETS) && sd.alloc(&c.meta_ver, n) &&
             sd.alloc(&c.default_inbound, n) && sd.alloc(&c.group, n) && sd.alloc(&c.links, 1) &&
             sd.alloc(&c.is_seed, n) && sd.alloc(&c.seeds, n) && sd.alloc(&c.ins, c.ins_cap) &&
             sd.alloc(&c.ins_inline, (size_t)nl * INS_INLINE) && sd.alloc(&c.compact_flag, nl) &&
@@ -833,6 +844,11 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(b.dq_cnt, 0, 4ull * DQ_BUCKETS, s);
   c.delay_th = nullptr;
   c.delay_on = 0;
+  hipMemsetAsync(c.meta_ver, 0, 4ull * n, s);
+  c.meta_seen = nullptr;
+  c.ns = nullptr;
+  c.ns_rel = nullptr;
+  c.n_ns = 0;
   hipMemsetAsync(c.default_inbound, 1, n, s);
   hipMemsetAsync(c.group, 0, 2 * (size_t)n, s);
   hipMemsetAsync(c.is_seed, 0, n, s);
@@ -1107,6 +1123,54 @@ int32_t swim_leave(swim_engine* e, uint32_t m, int32_t stop_after) {
   k_leave<<<1, 64, 0, e->stream>>>(sd->c, m, stop_after);
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
   return hip_status();
+}
+
+int32_t swim_update_metadata(swim_engine* e, uint32_t m) {
+  if (!e || m >= e->n) return SWIM_EINVAL;
+  uint8_t up = 0;
+  if (read_up(e, m, &up) != SWIM_OK) return SWIM_EDEVICE;
+  if (!up) return SWIM_ESTATE;
+  for (Shard& sd : e->sh) {
+    if (!sd.c.meta_seen) {  // every store still holds version 0 of everything
+      uint32_t* p = nullptr;
+      if (!sd.alloc(&p, (size_t)std::max(sd.c.nl, 1u) * e->n)) return SWIM_ENOMEM;
+      if (hipMemsetAsync(p, 0, 4ull * std::max(sd.c.nl, 1u) * e->n, e->stream) != hipSuccess) return SWIM_EDEVICE;
+      sd.c.meta_seen = p;
+    }
+    sd.c.T = e->T;
+    k_update_meta<<<1, 64, 0, e->stream>>>(sd.c, m, e->owner_of(m) == &sd ? 1 : 0);
+  }
+  return hip_status();
+}
+
+int32_t swim_set_namespaces(swim_engine* e, const uint16_t* ns_of_member, uint32_t n_ns, const uint8_t* related) {
+  if (!e) return SWIM_EINVAL;
+  if (n_ns == 0 || !ns_of_member) {
+    for (Shard& sd : e->sh) sd.c.n_ns = 0;
+    return SWIM_OK;
+  }
+  if (!related || n_ns > 4096) return SWIM_EINVAL;
+  for (uint32_t i = 0; i < e->n; ++i)
+    if (ns_of_member[i] >= n_ns) return SWIM_EINVAL;
+  std::vector<uint8_t> used(n_ns, 0);  // the converged start holds every initial member everywhere
+  for (uint32_t a = 0; a < e->n; ++a)
+    if (e->joined_h[a]) used[ns_of_member[a]] = 1;
+  for (uint32_t x = 0; x < n_ns; ++x)
+    for (uint32_t y = 0; y < n_ns; ++y)
+      if (used[x] && used[y] && !related[(size_t)x * n_ns + y]) return SWIM_ESTATE;
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  for (Shard& sd : e->sh) {
+    uint16_t* ns = nullptr;
+    uint8_t* rel = nullptr;
+    if (!sd.alloc(&ns, e->n) || !sd.alloc(&rel, (size_t)n_ns * n_ns)) return SWIM_ENOMEM;
+    if (hipMemcpy(ns, ns_of_member, 2ull * e->n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(rel, related, (size_t)n_ns * n_ns, hipMemcpyHostToDevice) != hipSuccess)
+      return SWIM_EDEVICE;
+    sd.c.ns = ns;
+    sd.c.ns_rel = rel;
+    sd.c.n_ns = n_ns;
+  }
+  return SWIM_OK;
 }
 
 int32_t swim_spread(swim_engine* e, uint32_t m, uint32_t payload) {

@@ -212,6 +212,15 @@ struct Ctx {
   uint32_t n_links;
   // message delay (swim_delay.h): thresholds per distinct meanDelay, the default table of each
   // member (-1 = no delay); delay_on: some member or link has a delay
+  // namespaces (areNamespacesRelated, MembershipProtocolImpl.java:511-536): group of each member,
+  // relation matrix of the groups; n_ns = 0: one namespace
+  const uint16_t* ns;
+  const uint8_t* ns_rel;
+  uint32_t n_ns;
+  // metadata version of each member (replicated; ClusterImpl.updateMetadata bumps it) and, once a
+  // metadata update happened, the version each owned viewer's MetadataStore holds per subject
+  uint32_t* meta_ver;
+  uint32_t* meta_seen;  // [nl][n] or nullptr
   const uint64_t* delay_th;  // [tables][SWIM_DELAY_TICKS_MAX]
   int16_t* default_delay;    // replicated [n]
   uint32_t delay_on;
@@ -824,6 +833,7 @@ __device__ inline bool fetch_ok(const Ctx& c, uint32_t v, uint32_t s, uint32_t p
 // metadata fetch succeeded: the caller applies it (apply_alive) at its flush point.
 __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, uint32_t st1, int32_t inc1,
                                          int reason, uint32_t phase) {
+  if (c.n_ns && !c.ns_rel[(size_t)c.ns[v] * c.n_ns + c.ns[s]]) return false;  // namespace filter (:575-586)
   MemberDev& m = mem(c, v);
   uint64_t cell = cell_get(c, v, s);
   const bool present = c_has(cell, B_IN_TABLE);
@@ -889,7 +899,17 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
 __device__ inline void apply_alive(const Ctx& c, uint32_t v, uint32_t s, int32_t inc1, int reason, uint32_t phase) {
   MemberDev& m = mem(c, v);
   // cancelSuspicionTimeoutTask
-  uint64_t cell = (cell_get(c, v, s) & ~B_HAS_TIMER) | B_HAS_METADATA;
+  uint64_t cell = cell_get(c, v, s) & ~B_HAS_TIMER;
+  // metadataStore.updateMetadata(member, metadata1) returns metadata0 (null when none is stored);
+  // metadata1 is the subject's metadata now (the fetch answers within the tick)
+  bool same_meta = c_has(cell, B_HAS_METADATA);
+  if (c.meta_seen) {
+    uint32_t& seen = c.meta_seen[(size_t)(v - c.lo) * c.n + s];
+    const uint32_t ver = c.meta_ver[s];
+    same_meta = same_meta && seen == ver;
+    seen = ver;
+  }
+  cell |= B_HAS_METADATA;
   if (reason != R_GOSSIP && reason != R_INITIAL_SYNC) spread_gossip(c, v, s, SWIM_ALIVE, inc1);
   const bool exists = c_has(cell, B_IN_MEMBERS);
   if (!c_has(cell, B_IN_TABLE)) m.table_size++;
@@ -898,6 +918,8 @@ __device__ inline void apply_alive(const Ctx& c, uint32_t v, uint32_t s, int32_t
   if (!exists) cell |= B_ALIVE_EMITTED;
   cell_put(c, v, s, cell);
   if (!exists) publish_event(c, v, s, SWIM_EV_ADDED, phase, next_minor(c, v, phase, s));
+  else if (!same_meta)  // !metadata1.equals(metadata0) (:780-781)
+    publish_event(c, v, s, SWIM_EV_UPDATED, phase, next_minor(c, v, phase, s));
 }
 
 // Collections.shuffle: for (i = size; i > 1; i--) swap(i-1, nextInt(i))

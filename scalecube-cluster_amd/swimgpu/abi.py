@@ -177,6 +177,8 @@ PROTOTYPES = {
     "swim_kill": (C.c_int32, [_engp, C.c_uint32]),
     "swim_leave": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
     "swim_spread": (C.c_int32, [_engp, C.c_uint32, C.c_uint32]),
+    "swim_update_metadata": (C.c_int32, [_engp, C.c_uint32]),
+    "swim_set_namespaces": (C.c_int32, [_engp, C.c_void_p, C.c_uint32, C.c_void_p]),
     "swim_join": (C.c_int32, [_engp, C.c_uint32]),
     "swim_set_default_loss": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
     "swim_set_link_loss": (C.c_int32, [_engp, C.c_uint32, C.c_uint32, C.c_int32]),
@@ -311,6 +313,19 @@ class Engine:
     def spread(self, m: int, payload: int) -> None:
         """GossipProtocol.spread: a user gossip with a 32-bit payload handle from member m, now."""
         _check("swim_spread", self.lib.swim_spread(self._h, m, payload))
+
+    def update_metadata(self, m: int) -> None:
+        """ClusterImpl.updateMetadata: m's metadata changes, ALIVE inc+1 is gossiped."""
+        _check("swim_update_metadata", self.lib.swim_update_metadata(self._h, m))
+
+    def set_namespaces(self, ns_of_member, related) -> None:
+        """Namespace group per member (uint16[capacity]) + the groups' relation matrix; None: one namespace."""
+        if ns_of_member is None:
+            _check("swim_set_namespaces", self.lib.swim_set_namespaces(self._h, None, 0, None))
+            return
+        g = np.ascontiguousarray(ns_of_member, dtype=np.uint16)
+        r = np.ascontiguousarray(related, dtype=np.uint8)
+        _check("swim_set_namespaces", self.lib.swim_set_namespaces(self._h, g.ctypes.data, int(r.shape[0]), r.ctypes.data))
 
     def join(self, m: int) -> None:
         _check("swim_join", self.lib.swim_join(self._h, m))

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import dataclasses
 import enum
+import re
 import math
 from collections import defaultdict
 
@@ -320,6 +321,27 @@ class FailureDetectorView:
         return self._c._take(self._m, fd=True)
 
 
+_NAMESPACE_PATTERN = re.compile(r"(\w+[\w\-./]*\w)+", re.ASCII)  # ClusterImpl.java:60, matches()
+
+
+def validate_namespace(namespace: str) -> None:
+    """ClusterImpl.validateConfiguration (:350-353)."""
+    if not _NAMESPACE_PATTERN.fullmatch(namespace or ""):
+        raise ValueError("Invalid cluster config: membership.namespace format is invalid")
+
+
+def namespaces_related(ns1: str, ns2: str) -> bool:
+    """MembershipProtocolImpl.areNamespacesRelated (:511-536) over java.nio Path name components."""
+    a = [x for x in ns1.split("/") if x]
+    b = [x for x in ns2.split("/") if x]
+    if a == b:
+        return True
+    if len(a) == len(b):
+        return False
+    shorter, longer = (a, b) if len(a) < len(b) else (b, a)
+    return longer[:len(shorter)] == shorter
+
+
 class GossipMessage:
     """A user gossip as listen() delivers it (transport-api Message: the data the spreader passed)."""
 
@@ -528,6 +550,20 @@ class SimulatedCluster:
 
     def network_emulator(self, m: int) -> NetworkEmulator:
         return NetworkEmulator(self, m)
+
+    def update_metadata(self, m: int):
+        """ClusterImpl.updateMetadata (:497-500) of member m (a new metadata version)."""
+        self.engine.update_metadata(m)
+
+    def set_namespaces(self, namespaces):
+        """MembershipConfig.namespace of every member (capacity strings), validated as the reference
+        does; members of unrelated namespaces never enter each other's tables."""
+        names = sorted(set(namespaces))
+        for x in names:
+            validate_namespace(x)
+        gid = {x: i for i, x in enumerate(names)}
+        rel = np.array([[namespaces_related(x, y) for y in names] for x in names], dtype=np.uint8)
+        self.engine.set_namespaces(np.array([gid[x] for x in namespaces], dtype=np.uint16), rel)
 
     def partition(self, groups):
         self.engine.set_partition(groups)

@@ -42,6 +42,14 @@ def apply_op(e: abi.Engine, op, args):
         e.set_link_inbound(*args)
     elif op == "default_in":
         e.set_default_inbound(*args)
+    elif op == "update_meta":
+        e.update_metadata(*args)
+    elif op == "namespaces":
+        from swimgpu.cluster import namespaces_related
+        names = sorted(set(args[0]))
+        gid = {x: i for i, x in enumerate(names)}
+        rel = np.array([[namespaces_related(x, y) for y in names] for x in names], dtype=np.uint8)
+        e.set_namespaces(np.array([gid[x] for x in args[0]], dtype=np.uint16), rel)
     elif op == "default_delay":
         e.set_default_delay(*args)
     elif op == "link_delay":
@@ -168,6 +176,20 @@ def catalog() -> list[Scenario]:
                  ops=[(0, "default_delay", 150, abi.ALL_MEMBERS), (0, "loss", 5, abi.ALL_MEMBERS),
                       (0, "link_delay", 2, 5, 2500), (50, "spread", 4, 77), (120, "kill", 9)],
                  check_every=50, shardable=False),
+        # ClusterTest.testUpdateMetadata (:179-247): members join through seed 0, member 1 updates its
+        # metadata twice (updateIncarnation: ALIVE inc+1 gossiped; every viewer fetches -> UPDATED)
+        Scenario("update_metadata_12", 12, 2, 300, seed=19, seeds=(0,), cfg=mp_test,
+                 ops=[(2, "join", 2 + i) for i in range(10)] + [(60, "update_meta", 1), (140, "update_meta", 1),
+                                                               (141, "kill", 7)],
+                 check_every=20),
+        # ClusterNamespacesTest.testSimpleNamespacesHierarchy (:149-196) + testSeparateNonEmptyNamespaces
+        # (:84-143) on one engine: "develop" sees everyone below it, siblings stay apart, "root" and
+        # "root2" never meet; members start one by one through seeds
+        Scenario("namespaces_9", 9, 1, 240, seed=20, seeds=(0, 1, 2, 5, 6, 7), cfg=mp_test,
+                 ops=[(0, "namespaces", ["develop", "develop/develop", "develop/develop", "develop/develop-2",
+                                         "develop/develop-2", "root", "root", "root2", "root2"])]
+                 + [(2 + 3 * i, "join", 1 + i) for i in range(8)],
+                 check_every=20),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),
                  cfg=dict(sync_interval=5000), ops=[(100, "partition", _partition(32, 16)), (1100, "partition", None)],

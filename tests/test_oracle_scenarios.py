@@ -379,3 +379,79 @@ def test_fd_delay_trusted_through_relays():
     statuses = {ev.status for ev in fd if ev.member.id == 1}
     assert MemberStatus.ALIVE in statuses
     assert trusted(c, 0) == [0, 1, 2, 3]
+
+
+# ------------------------------------------------------------------------------ ClusterNamespacesTest
+@pytest.mark.parametrize("ns", ["", "  ", "/abc", "a /b /c", "a\nb\nc", ".abc", "abc.", "a-/b-/c-", "a+/b+/c+",
+                                "abc/", "abc/*", "abc/.", "./abc", "a./b./c."])
+def test_invalid_namespace_format(ns):  # testInvalidNamespaceFormat (:20-56)
+    from swimgpu.cluster import validate_namespace
+    with pytest.raises(ValueError, match="membership.namespace format is invalid"):
+        validate_namespace(ns)
+
+
+def _namespace_cluster(namespaces, seeds):
+    """Members start one by one (startAwait) through the seeds; member 0 is up from the start."""
+    n = len(namespaces)
+    lib = oracle.lib()
+    cfg = mp_config(n).to_abi(lib)
+    e = abi.Engine(lib, cfg, n, 1, 1)
+    e.set_seeds(list(seeds))
+    c = SimulatedCluster.from_engine(e, mp_config(n).membership(seed_members=tuple(seeds)))
+    c.set_namespaces(namespaces)
+    for m in range(1, n):
+        c.join(m)
+        c.step_ticks(3)
+    c.await_seconds(2)
+    return c
+
+
+def others(c, m):
+    return sorted(x.id for x in c.membership(m).other_members())
+
+
+def test_separate_empty_namespaces():  # :58-81
+    c = _namespace_cluster(["root", "root1", "root2"], seeds=(0,))
+    assert others(c, 0) == others(c, 1) == others(c, 2) == []
+
+
+def test_separate_non_empty_namespaces():  # :84-143
+    c = _namespace_cluster(["root", "root", "root", "root2", "root2", "root2"], seeds=(0, 1, 2, 3, 4))
+    assert (others(c, 0), others(c, 1), others(c, 2)) == ([1, 2], [0, 2], [0, 1])
+    assert (others(c, 3), others(c, 4), others(c, 5)) == ([4, 5], [3, 5], [3, 4])
+
+
+def test_simple_namespaces_hierarchy():  # :146-196
+    c = _namespace_cluster(["develop", "develop/develop", "develop/develop", "develop/develop-2",
+                            "develop/develop-2"], seeds=(0, 1, 2, 3))
+    assert others(c, 0) == [1, 2, 3, 4]
+    assert (others(c, 1), others(c, 2)) == ([0, 2], [0, 1])
+    assert (others(c, 3), others(c, 4)) == ([0, 4], [0, 3])
+
+
+def test_isolated_parent_namespaces():  # :199-250
+    c = _namespace_cluster(["a/1", "a/1/c", "a/1/c", "a/111", "a/111/c", "a/111/c"], seeds=(0, 1, 2, 3, 4))
+    assert (others(c, 0), others(c, 1), others(c, 2)) == ([1, 2], [0, 2], [0, 1])
+    assert (others(c, 3), others(c, 4), others(c, 5)) == ([4, 5], [3, 5], [3, 4])
+
+
+# ------------------------------------------------------------------------------ ClusterTest
+def test_update_metadata():  # testUpdateMetadata (:179-247): every member sees the new metadata
+    n = 12
+    lib = oracle.lib()
+    e = abi.Engine(lib, ClusterConfig.default_config().to_abi(lib), n, 2, 1)
+    e.set_seeds([0])
+    c = SimulatedCluster.from_engine(e, ClusterConfig.default_config().membership(seed_members=(0,)))
+    for m in range(2, n):
+        c.join(m)
+    c.await_seconds(3)
+    for m in range(n):
+        c.membership(m).listen()
+    c.update_metadata(1)
+    c.await_seconds(3)
+    for m in range(n):
+        ev = c.membership(m).listen()
+        upd = [x for x in ev if x.type == Type.UPDATED]
+        assert ([x.member.id for x in upd] == [1]) == (m != 1), (m, ev)
+        assert not [x for x in ev if x.type != Type.UPDATED]
+    assert c.membership(1).incarnation() == 1  # updateIncarnation: ALIVE inc 0 -> 1
