@@ -157,6 +157,46 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def side_run(lib, workload, n, warmup, steps, device=0, **knobs):
+    """A secondary single-GPU measurement on its own engine (the headline engine is closed first):
+    `warmup` untimed periods, then `steps` timed ones.  Returns (seconds, merge profile, fanout
+    profile, stats)."""
+    import torch
+    from swimgpu import abi
+    sch = Schedule(workload, n, warmup + steps)
+    cfg = make_config(lib, device)
+    for k, v in knobs.items():
+        setattr(cfg, k, v)
+    e = abi.Engine(lib, cfg, sch.capacity, n, 1)
+    try:
+        sch.setup(e)
+        sch.run(e, 0, warmup)
+        e.drain_events()
+        torch.cuda.synchronize()
+        e.profile_enable(True)
+        t0 = time.perf_counter()
+        sch.run(e, warmup, warmup + steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        out = (dt, e.profile_merge(), e.profile_fanout(), e.stats())
+        e.drain_events()
+    finally:
+        e.close()
+    return out
+
+
+def fanout_roofline(fprof, window):
+    f_ms = fprof["total_ms"] / max(1, fprof["launches"])
+    f_ach = fprof["alg_bytes"] / max(1e-12, fprof["total_ms"] / 1e3) / 1e9
+    f_traffic, f_src = pmc_traffic("k_gossip_emit", "failures64k")
+    return {"bound": "hbm", "kernel": "k_gossip_emit", "achieved": f_ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": f_ach / HBM_PEAK_GBPS, "traffic": f_traffic, "traffic_source": f_src,
+            "launches": fprof["launches"], "avg_launch_ms": f_ms,
+            "alg_bytes_per_launch": fprof["alg_bytes"] / max(1, fprof["launches"]),
+            "alg_bytes_rule": "24 B per materialised GOSSIP_REQ + 32 B per (gossip, sender round) state read",
+            "window": window}
+
+
 def cpu_baseline(n, p0, periods):
     """The CPU oracle (oracle/liboracle_swim.so, the C++ lockstep restatement) on the same N and
     workload, over the same periods the GPU timed ([p0, p0 + periods) of the schedule; the periods
@@ -200,6 +240,10 @@ def main():
     ap.add_argument("--members", type=int, default=None, help="default: 65,536 (16,384 for churn)")
     ap.add_argument("--cpu-periods", type=int, default=0, help="default: 10 (1 for churn)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="quiet workload: skip the fanout-roofline (failures window) and KS-mode side runs")
+    ap.add_argument("--fanout-steps", type=int, default=6)
+    ap.add_argument("--ks-steps", type=int, default=5)
     ap.add_argument("--progress", action="store_true", help="print a stderr line after every period")
     ap.add_argument("--workload", choices=("quiet", "failures", "churn"), default="quiet")
     ap.add_argument("--gossip-capacity", type=int, default=0)
@@ -311,15 +355,24 @@ def main():
     if fprof["alg_bytes"] > 0:
         # the gossip fanout kernel (north_star: merge AND fanout against the HBM roofline); only
         # workloads with gossip traffic (failures, churn) give it work
-        f_ms = fprof["total_ms"] / max(1, fprof["launches"])
-        f_ach = fprof["alg_bytes"] / max(1e-12, fprof["total_ms"] / 1e3) / 1e9
-        f_traffic, f_src = pmc_traffic("k_gossip_emit", f"{args.workload}{n // 1024}k")
-        line["roofline_fanout"] = {
-            "bound": "hbm", "kernel": "k_gossip_emit", "achieved": f_ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": f_ach / HBM_PEAK_GBPS, "traffic": f_traffic, "traffic_source": f_src,
-            "launches": fprof["launches"], "avg_launch_ms": f_ms,
-            "alg_bytes_per_launch": fprof["alg_bytes"] / max(1, fprof["launches"]),
-            "alg_bytes_rule": "24 B per materialised GOSSIP_REQ + 32 B per (gossip, sender round) state read"}
+        line["roofline_fanout"] = fanout_roofline(fprof, f"the timed window ({args.workload})")
+    if world == 1 and args.workload == "quiet" and not args.no_extras and args.local_shards == 1:
+        e.close()
+        # the quiet headline sends no gossip: the fanout kernel is measured on the failures workload
+        # over a window that starts with its first kill (period 10: FD detection, the SUSPECT storm
+        # through all N members, then the gossip's remaining rounds)
+        fw, fs = KILL_FIRST, args.fanout_steps
+        f_dt, _, f_fprof, f_st = side_run(lib, "failures", n, fw, fs, local_rank)
+        line["roofline_fanout"] = fanout_roofline(
+            f_fprof, f"config4-lan-failures N={n}: periods {fw}..{fw + fs} (member killed at period {fw}), "
+                     f"{n * fs / f_dt:.3g} member-periods/s, {f_st['gossip_messages']} GOSSIP_REQs sent")
+        # the timing mode whose latency distributions pass the KS test against the reference-timing
+        # DES (tests/test_ks_des.py: independent timer phases, 10 ms ticks); same quiet workload
+        k_dt, _, _, _ = side_run(lib, "quiet", n, 2, args.ks_steps, local_rank, timer_stagger=1, tick_ms=10)
+        line["ks_mode"] = {"value": n * args.ks_steps / k_dt, "unit": "member-periods/s",
+                           "ms_per_step": k_dt / args.ks_steps * 1e3, "steps": args.ks_steps,
+                           "config": "same workload, timer_stagger=1, tick_ms=10 (100 ticks per period)",
+                           "ks": "tests/test_ks_des.py::test_ks_gpu_vs_des (N=64 and 1,024, 200 seeds, p >= 0.01)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         e.close()
         # churn: the oracle needs minutes per period once the storm builds, so the sample is the

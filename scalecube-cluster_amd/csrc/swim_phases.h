@@ -1034,7 +1034,6 @@ __device__ inline unsigned long long deliver_sorted(const Ctx& c, uint32_t r, co
 struct BigLds {  // per wave
   uint32_t snd[BIG_MAXD];  // distinct senders (found order, then ascending)
   uint32_t cnt[BIG_MAXD];  // their message counts, then running inbox bases
-  GMsgFull m[64];          // the messages of the current 64-message step, canonical order
   uint32_t iP[64], iS[64], iR[64];  // apply_ins_batch scratch
 };
 
@@ -1053,155 +1052,165 @@ __device__ __forceinline__ int big_find(const uint32_t* snd, uint32_t nd, uint32
   return -1;
 }
 
-// One receiver's big inbox, by one wave.  Canonical order is (sender, slab position), and it needs
-// no comparison sort: k_gossip_emit numbers each (sender, receiver) pair's messages of the round in
+// Big inboxes, up to 64 per wave.  Canonical order is (sender, slab position), and it needs no
+// comparison sort: k_gossip_emit numbers each (sender, receiver) pair's messages of the round in
 // slab-position order (GMsgFull.pseq, dense: every materialised message reaches the inbox, cross-
-// shard duplicates included, flagged), so rank = base of the sender (senders ascending, bases from
-// their message counts) + pseq.  Lane 0 then runs onGossipReq in that
-// order, 64 messages at a time, after every lane has staged its message in LDS and touched the
-// collector probe and view cell that message's step will read (the serial chain then hits L2).
-// Then the receiver's pingMembers inserts of the phase and its SYNC collection.
-__device__ unsigned long long deliver_big(const Ctx& c, const Ctx& cs, const Bufs& b, uint32_t i, uint32_t lane, int collect,
-                                          BigLds& L, unsigned long long& nsync) {
-  const uint32_t r = c.lo + i;
-  const uint32_t k_all = b.msg_cnt[i];
-  wave_sync();
-  if (lane == 0) b.msg_cnt[i] = 0;
-  // messages beyond the page table were never written (ERR_MSGS is set)
-  const uint32_t k = min(k_all, b.pg_max * 64u);
+// shard duplicates included, flagged), so rank = base of the sender (senders ascending by snd_key,
+// bases from their message counts) + pseq.  The wave ranks its receivers one after the other (all
+// lanes on one inbox), then lane j runs receiver j's onGossipReq chain in rank order — the chains
+// of the batch run side by side, each touching only its own receiver's state — then, receiver by
+// receiver, the inbox pages go back, the pingMembers inserts of the phase run and the SYNC
+// collection follows.
+__device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L) {
   const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
   auto msg_at = [&](uint32_t q) -> const GMsgFull& { return b.pg_msgs[(size_t)pt[q >> 6] * 64 + (q & 63)]; };
   auto perm_at = [&](uint32_t q) -> uint32_t& { return b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)]; };
-  unsigned long long acc = 0;
-  bool pages_ok = true;
-  // a page the pool could not give holds NONE or PG_FAILED (ERR_PAGES / ERR_INBOX are set)
-  for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) pages_ok &= pt[pg] < b.pg_cap;
-  pages_ok = __ballot(!pages_ok) == 0;
-  if (c.up[r] && k && pages_ok) {
-    // pass 1: distinct senders and their message counts
-    uint32_t nd = 0;
-    bool over = false;
-    for (uint32_t q0 = 0; q0 < k && !over; q0 += 64) {
+  // pass 1: distinct senders and their message counts
+  uint32_t nd = 0;
+  bool over = false;
+  for (uint32_t q0 = 0; q0 < k && !over; q0 += 64) {
+    const uint32_t q = q0 + lane;
+    const uint32_t f = q < k ? snd_key(c, msg_at(q)) : NONE;
+    uint64_t todo = __ballot(q < k);
+    while (todo) {
+      const uint32_t sf = __shfl(f, (int)__ffsll((unsigned long long)todo) - 1, 64);
+      const uint64_t same = __ballot(f == sf) & todo;
+      int slot = big_find(L.snd, nd, sf, lane);
+      if (slot < 0) {
+        if (nd == BIG_MAXD) { over = true; break; }
+        slot = (int)nd;
+        if (lane == 0) { L.snd[nd] = sf; L.cnt[nd] = 0; }
+        nd++;
+      }
+      if (lane == 0) L.cnt[slot] += (uint32_t)__popcll(same);
+      wave_sync();
+      todo &= ~same;
+    }
+  }
+  if (over) {
+    // more distinct senders than the LDS table holds (needs > BIG_MAXD senders choosing this
+    // receiver in one round): senders one at a time, ascending, by repeated minimum search
+    uint32_t lo_s = 0, rank = 0;
+    for (;;) {
+      uint32_t mn = NONE;
+      for (uint32_t q = lane; q < k; q += 64) {
+        const uint32_t f = snd_key(c, msg_at(q));
+        if (f >= lo_s && f < mn) mn = f;
+      }
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) mn = min(mn, (uint32_t)__shfl_xor(mn, d, 64));
+      if (mn == NONE) break;
+      uint32_t cnt = 0;
+      for (uint32_t q0 = 0; q0 < k; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const bool mine = q < k && snd_key(c, msg_at(q)) == mn;
+        if (mine && rank + msg_at(q).pseq < k) perm_at(rank + msg_at(q).pseq) = q;
+        cnt += (uint32_t)__popcll(__ballot(mine));
+      }
+      rank += cnt;
+      lo_s = mn + 1;
+    }
+  } else {
+    // senders ascending, inbox bases = exclusive prefix of their counts in that order
+    uint32_t ms[2], mc[2], mr[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t j = lane + 64u * t;
+      ms[t] = j < nd ? L.snd[j] : NONE;
+      mc[t] = j < nd ? L.cnt[j] : 0u;
+      mr[t] = 0;
+      if (j < nd)
+        for (uint32_t x = 0; x < nd; ++x) mr[t] += L.snd[x] < ms[t] ? 1u : 0u;
+    }
+    wave_sync();
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      if (lane + 64u * t < nd) { L.snd[mr[t]] = ms[t]; L.cnt[mr[t]] = mc[t]; }
+    wave_sync();
+    if (lane == 0) {
+      uint32_t acc0 = 0;
+      for (uint32_t x = 0; x < nd; ++x) { const uint32_t t = L.cnt[x]; L.cnt[x] = acc0; acc0 += t; }
+    }
+    wave_sync();
+    // pass 2: rank = base of the sender + the message's pseq (dense per (sender, receiver))
+    for (uint32_t q0 = 0; q0 < k; q0 += 64) {
       const uint32_t q = q0 + lane;
-      const uint32_t f = q < k ? snd_key(c, msg_at(q)) : NONE;
+      uint32_t f = NONE, ps = 0;
+      if (q < k) {
+        const GMsgFull& g = msg_at(q);
+        f = snd_key(c, g);
+        ps = g.pseq;
+      }
       uint64_t todo = __ballot(q < k);
       while (todo) {
         const uint32_t sf = __shfl(f, (int)__ffsll((unsigned long long)todo) - 1, 64);
         const uint64_t same = __ballot(f == sf) & todo;
-        int slot = big_find(L.snd, nd, sf, lane);
-        if (slot < 0) {
-          if (nd == BIG_MAXD) { over = true; break; }
-          slot = (int)nd;
-          if (lane == 0) { L.snd[nd] = sf; L.cnt[nd] = 0; }
-          nd++;
-        }
-        if (lane == 0) L.cnt[slot] += (uint32_t)__popcll(same);
-        wave_sync();
+        const uint32_t at = L.cnt[big_find(L.snd, nd, sf, lane)] + ps;
+        if (((same >> lane) & 1ull) && at < k) perm_at(at) = q;
         todo &= ~same;
       }
     }
-    if (over) {
-      // more distinct senders than the LDS table holds (needs > BIG_MAXD senders choosing this
-      // receiver in one round): senders one at a time, ascending, by repeated minimum search
-      uint32_t lo_s = 0, rank = 0;
-      for (;;) {
-        uint32_t mn = NONE;
-        for (uint32_t q = lane; q < k; q += 64) {
-          const uint32_t f = snd_key(c, msg_at(q));
-          if (f >= lo_s && f < mn) mn = f;
-        }
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) mn = min(mn, (uint32_t)__shfl_xor(mn, d, 64));
-        if (mn == NONE) break;
-        uint32_t cnt = 0;
-        for (uint32_t q0 = 0; q0 < k; q0 += 64) {
-          const uint32_t q = q0 + lane;
-          const bool mine = q < k && snd_key(c, msg_at(q)) == mn;
-          if (mine && rank + msg_at(q).pseq < k) perm_at(rank + msg_at(q).pseq) = q;
-          cnt += (uint32_t)__popcll(__ballot(mine));
-        }
-        rank += cnt;
-        lo_s = mn + 1;
-      }
-    } else {
-      // senders ascending, inbox bases = exclusive prefix of their counts in that order
-      uint32_t ms[2], mc[2], mr[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const uint32_t j = lane + 64u * t;
-        ms[t] = j < nd ? L.snd[j] : NONE;
-        mc[t] = j < nd ? L.cnt[j] : 0u;
-        mr[t] = 0;
-        if (j < nd)
-          for (uint32_t x = 0; x < nd; ++x) mr[t] += L.snd[x] < ms[t] ? 1u : 0u;
-      }
-      wave_sync();
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-        if (lane + 64u * t < nd) { L.snd[mr[t]] = ms[t]; L.cnt[mr[t]] = mc[t]; }
-      wave_sync();
-      if (lane == 0) {
-        uint32_t acc0 = 0;
-        for (uint32_t x = 0; x < nd; ++x) { const uint32_t t = L.cnt[x]; L.cnt[x] = acc0; acc0 += t; }
-      }
-      wave_sync();
-      // pass 2: rank = base of the sender + the message's pseq (dense per (sender, receiver))
-      for (uint32_t q0 = 0; q0 < k; q0 += 64) {
-        const uint32_t q = q0 + lane;
-        uint32_t f = NONE, ps = 0;
-        if (q < k) {
-          const GMsgFull& g = msg_at(q);
-          f = snd_key(c, g);
-          ps = g.pseq;
-        }
-        uint64_t todo = __ballot(q < k);
-        while (todo) {
-          const uint32_t sf = __shfl(f, (int)__ffsll((unsigned long long)todo) - 1, 64);
-          const uint64_t same = __ballot(f == sf) & todo;
-          const uint32_t at = L.cnt[big_find(L.snd, nd, sf, lane)] + ps;
-          if (((same >> lane) & 1ull) && at < k) perm_at(at) = q;
-          todo &= ~same;
-        }
-      }
-    }
-    wave_sync();
-    MemberDev& m = mem(c, r);
-    if (lane == 0) {
-      m.ev_minor = 0;
-      m.fetch_ctr = 0;
-    }
-    GossipDev* slab = slab_of(c, r);
-    const size_t row = (size_t)i * c.n;
-    uint32_t sink = 0;
-    for (uint32_t q0 = 0; q0 < k; q0 += 64) {
-      const uint32_t q = q0 + lane;
-      if (q < k) {
-        uint32_t j = perm_at(q);
-        if (j >= k) {  // a hole: only after an inbox overflow (ERR_MSGS is set)
-          set_err(c, ERR_MSGS);
-          j = q;
-        }
-        const GMsgFull g = msg_at(j);
-        L.m[lane] = g;
-        const CollEnt* e = coll_find(c, r, g.gossiper);
-        if (g.status < SWIM_GOSSIP_USER) sink ^= c.recs[row + g.subject] ^ c.aux[row + g.subject];
-        sink ^= e ? e->meta : 1u;
-      }
-      wave_sync();
-      if (lane == 0) {
-        const uint32_t nq = min(64u, k - q0);
-        for (uint32_t t = 0; t < nq; ++t)
-          if (on_gossip_req(c, r, m, slab, L.m[t])) acc++;
-      }
-      wave_sync();
-    }
-    if (sink == 0x5bd1e995u && lane == 63) set_err(c, 0u);  // keeps the warming loads; sets no bit
   }
   wave_sync();
-  // the inbox pages go back to the pool (the pool itself restarts every tick)
-  for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) b.pg_tab[(size_t)i * b.pg_max + pg] = NONE;
-  apply_ins_batch<64, false>(c, r, lane, L.iP, L.iS, L.iR);
-  if (lane == 0 && collect) nsync += sync_collect_member(cs, b, r);  // phase D's SYNC collection for r
+  return k;
+}
+
+__device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, const Bufs& b, const uint32_t* list,
+                                                uint32_t nb, uint32_t lane, int collect, BigLds& L,
+                                                unsigned long long& nsync) {
+  // 1. rank every inbox of the batch; lane j keeps receiver j's message count (0: nothing to
+  //    deliver) and the count of inbox pages to hand back
+  uint32_t my_k = 0, my_pages = 0;
+  for (uint32_t j = 0; j < nb; ++j) {
+    const uint32_t i = list[j];
+    const uint32_t r = c.lo + i;
+    const uint32_t k_all = b.msg_cnt[i];
+    wave_sync();
+    if (lane == 0) b.msg_cnt[i] = 0;
+    // messages beyond the page table were never written (ERR_INBOX is set)
+    const uint32_t k = min(k_all, b.pg_max * 64u);
+    const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
+    bool pages_ok = true;
+    // a page the pool could not give holds NONE or PG_FAILED (ERR_PAGES / ERR_INBOX are set)
+    for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) pages_ok &= pt[pg] < b.pg_cap;
+    pages_ok = __ballot(!pages_ok) == 0;
+    const bool go = c.up[r] && k && pages_ok;
+    if (go) rank_big_inbox(c, b, i, k, lane, L);
+    if (lane == j) {
+      my_k = go ? k : 0;
+      my_pages = (k + 63) / 64;
+    }
+  }
+  wave_sync();
+  // 2. the onGossipReq chains, lane j for receiver j
+  unsigned long long acc = 0;
+  if (lane < nb && my_k) {
+    const uint32_t i = list[lane], r = c.lo + i;
+    const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
+    MemberDev& m = mem(c, r);
+    m.ev_minor = 0;
+    m.fetch_ctr = 0;
+    GossipDev* slab = slab_of(c, r);
+    for (uint32_t q = 0; q < my_k; ++q) {
+      uint32_t jq = b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)];
+      if (jq >= my_k) {  // a hole: only after an inbox overflow (ERR_MSGS is set)
+        set_err(c, ERR_MSGS);
+        jq = q;
+      }
+      const GMsgFull g = b.pg_msgs[(size_t)pt[jq >> 6] * 64 + (jq & 63)];
+      if (on_gossip_req(c, r, m, slab, g)) acc++;
+    }
+  }
+  wave_sync();
+  // 3. per receiver: the inbox pages go back to the pool (the pool itself restarts every tick),
+  //    the phase's pingMembers inserts, phase D's SYNC collection
+  for (uint32_t j = 0; j < nb; ++j) {
+    const uint32_t i = list[j], r = c.lo + i;
+    const uint32_t np = __shfl(my_pages, (int)j, 64);
+    for (uint32_t pg = lane; pg < np; pg += 64) b.pg_tab[(size_t)i * b.pg_max + pg] = NONE;
+    apply_ins_batch<64, false>(c, r, lane, L.iP, L.iS, L.iR);
+    if (lane == 0 && collect) nsync += sync_collect_member(cs, b, r);
+  }
   return acc;
 }
 
@@ -1226,11 +1235,11 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect) {
   const uint32_t t32 = (uint32_t)T;
   const bool any = b.k->msg_total != 0;  // else no receiver has an inbox
   unsigned long long acc = 0, nsync = 0;
-  if (any) {
+  if (any) {  // big inboxes, 64 per wave and batch
     const uint32_t nbig = b.k->big_cnt;
-    for (uint32_t x = __builtin_amdgcn_readfirstlane(blockIdx.x * DLV_WAVES + wv); x < nbig;
-         x += gridDim.x * DLV_WAVES)
-      acc += deliver_big(c, cs, b, b.big_list[x], lane, collect, s_big[wv], nsync);
+    for (uint32_t x = __builtin_amdgcn_readfirstlane((blockIdx.x * DLV_WAVES + wv) * 64u); x < nbig;
+         x += gridDim.x * DLV_WAVES * 64u)
+      acc += deliver_big_batch(c, cs, b, b.big_list + x, min(64u, nbig - x), lane, collect, s_big[wv], nsync);
   }
   for (uint32_t base = blockIdx.x * DLV_BLOCK; base < c.nl; base += gridDim.x * DLV_BLOCK) {
     if (tid == 0) s_nins = 0;

@@ -12,8 +12,8 @@ wl=${WORKLOAD:-quiet}
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof/${tag}_stats -o run \
-  -- python3 bench.py --workload "$wl" --steps "$steps" --warmup "$warm" --no-cpu-baseline > gpurun_out/prof/${tag}_stats.log 2>&1
+  -- python3 bench.py --workload "$wl" --steps "$steps" --warmup "$warm" --no-cpu-baseline --no-extras > gpurun_out/prof/${tag}_stats.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d gpurun_out/prof/${tag}_fetch -o run \
-  -- python3 bench.py --workload "$wl" --steps "${PMC_STEPS:-4}" --warmup "$warm" --no-cpu-baseline > gpurun_out/prof/${tag}_fetch.log 2>&1
+  -- python3 bench.py --workload "$wl" --steps "${PMC_STEPS:-4}" --warmup "$warm" --no-cpu-baseline --no-extras > gpurun_out/prof/${tag}_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d gpurun_out/prof/${tag}_write -o run \
-  -- python3 bench.py --workload "$wl" --steps "${PMC_STEPS:-4}" --warmup "$warm" --no-cpu-baseline > gpurun_out/prof/${tag}_write.log 2>&1
+  -- python3 bench.py --workload "$wl" --steps "${PMC_STEPS:-4}" --warmup "$warm" --no-cpu-baseline --no-extras > gpurun_out/prof/${tag}_write.log 2>&1
