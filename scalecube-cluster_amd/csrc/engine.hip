@@ -39,7 +39,7 @@ constexpr uint32_t kDrainFirst = 1;    // the interval starts at one tick and ad
 constexpr uint32_t kClassifyGrid = CLS_GRID;  // 16,384 waves: about one (message, chunk) unit each at N = 65,536
 constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
 constexpr uint32_t kEmitGrid = 2048;      // 8,192 waves, one gossip sender at a time each
-constexpr uint32_t kDeliverGrid = 256;    // 1,024 waves for the big inboxes of a gossip storm
+constexpr uint32_t kDeliverGrid = 512;    // 2,048 waves (two workgroups per CU) for the big inboxes of a storm
 constexpr uint32_t kStopCap = 4096;
 constexpr uint32_t kProfEvery = 3;  // SYNC classify launches between timed ones
 constexpr uint64_t kRebaseEvery = 16;  // ticks between rebases of the SYNC block witness (k_end_tick)
