@@ -455,3 +455,31 @@ def test_update_metadata():  # testUpdateMetadata (:179-247): every member sees 
         assert ([x.member.id for x in upd] == [1]) == (m != 1), (m, ev)
         assert not [x for x in ev if x.type != Type.UPDATED]
     assert c.membership(1).incarnation() == 1  # updateIncarnation: ALIVE inc 0 -> 1
+
+
+def test_mp_restart_stopped_members():  # MembershipProtocolTest.testRestartStoppedMembers (:564-640)
+    """C and D stop, are suspected, then REMOVED after the suspicion timeout; restarted instances
+    (new ids at new addresses: free slots 4 and 5, seeded with the original four addresses) join and
+    every live member trusts exactly {A, B, new C, new D}."""
+    lib = oracle.lib()
+    conf = mp_config(4)
+    e = abi.Engine(lib, conf.to_abi(lib, record_fd_events=1), 6, 4, 9)
+    c = SimulatedCluster.from_engine(e, conf)
+    c.await_seconds(1)
+    assert trusted(c, 0) == [0, 1, 2, 3]
+    c.membership(0).listen(), c.membership(1).listen()
+    c.kill(2)
+    c.kill(3)
+    c.await_seconds(1)
+    assert trusted(c, 0) == [0, 1] and suspected(c, 0) == [2, 3]
+    assert trusted(c, 1) == [0, 1] and suspected(c, 1) == [2, 3]
+    c.await_suspicion(4)
+    for m in (0, 1):
+        assert trusted(c, m) == [0, 1] and suspected(c, m) == []
+        removed = sorted(x.member.id for x in c.membership(m).listen() if x.type == Type.REMOVED)
+        assert removed == [2, 3]
+    c.join(4)
+    c.join(5)
+    c.await_seconds(3)
+    for m, want in ((4, [0, 1, 4, 5]), (5, [0, 1, 4, 5]), (0, [0, 1, 4, 5]), (1, [0, 1, 4, 5])):
+        assert trusted(c, m) == want and suspected(c, m) == [], m
