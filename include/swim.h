@@ -210,6 +210,17 @@ int32_t swim_leave(swim_engine* e, uint32_t m, int32_t stop_after);
 /* Start a fresh member in free slot m (ClusterImpl.doStart0 + MembershipProtocolImpl.start0
  * :250-291): initial SYNC to every seed during the next tick. */
 int32_t swim_join(swim_engine* e, uint32_t m);
+/* swim_join, with member m's transport bound to the address of member addr_of, whose transport is
+ * stopped: a restart on the same port (MembershipProtocolTest.testRestartStoppedMembersOnSameAddresses
+ * :654-711).  From m's start on, every message sent to addr_of's address reaches m:
+ *   - its onPing answers DEST_GONE (FailureDetectorImpl.onPing :227-259), which the pinger's
+ *     computeMemberStatus turns into DEAD (:382-404), directly or through a relay (:291-315);
+ *   - a GET_METADATA request for addr_of goes unanswered (MetadataStoreImpl.onMetadataRequest :209);
+ *   - gossips and SYNCs to addr_of are delivered to m;
+ * and m ignores records of other members at its own address (MembershipProtocolImpl.updateMembership
+ * :605-610) and drops that address from its seeds (cleanUpSeedMembers :171-190).
+ * SWIM_ESTATE if the address is in use (its holder is up or about to start). */
+int32_t swim_join_at(swim_engine* e, uint32_t m, uint32_t addr_of);
 /* GossipProtocol.spread(Message) (GossipProtocolImpl.java:126-130 -> createAndPutGossip :190-199)
  * on member m now, between ticks: a user gossip carrying the 32-bit payload (a handle the caller
  * maps to the message).  Receivers report it with SWIM_EV_GOSSIP, the originator's spread()

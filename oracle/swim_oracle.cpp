@@ -141,10 +141,13 @@ struct Member {
   uint32_t ack_target = NONE;
   uint64_t ack_due = 0;
   bool ack_ok = false;    // ack_due is the tick the (delayed) ack arrives, not the timeout
+  bool ack_gone = false;  // that ack says DEST_GONE (another member answers at the target's address)
   uint32_t ack_late = 0;  // 1 + ticks after the timeout that a late direct ack arrives (0 = none)
   uint32_t relay_target = NONE, relay_pending = 0;
   uint64_t relay_due = 0;
   bool relay_ok = false;  // relay_due is the tick the first relayed ack arrives, not the timeout
+  bool relay_gone = false;  // that ack says DEST_GONE
+  uint32_t join_addr = NONE;  // swim_join_at: the member whose address this joiner binds
   // ---- GossipProtocolImpl (:48-55)
   uint64_t g_period = 0, g_counter = 0, period_used = 0;
   std::unordered_map<uint32_t, SeqCollector> collectors;
@@ -230,6 +233,10 @@ struct swim_engine {
   std::vector<Member> m;
   std::vector<uint32_t> seeds;
   std::vector<uint8_t> is_seed;
+  // addresses (swim_join_at): addr[x] = the address member x was started on (a slot number),
+  // route[x] = the member whose transport listens on x's address now; both empty while every member
+  // is on its own address
+  std::vector<uint32_t> addr, route;
   // network emulator
   std::vector<int32_t> default_loss;
   std::vector<uint8_t> default_inbound;
@@ -304,6 +311,22 @@ struct swim_engine {
     return draw(member, stream, sub24, sub32, T);
   }
   static bool lost(int32_t pct, uint32_t w) { return pct > 0 && (pct >= 100 || (int32_t)next_int(w, 100) < pct); }
+
+  // ------------------------------------------------------------------------- addresses
+  // the member a message sent to x's address reaches (Transport.send / requestResponse by Address)
+  uint32_t dst(uint32_t x) const { return route.empty() ? x : route[x]; }
+  // member m starts listening on the address of member a (whose transport is stopped)
+  void bind_address(uint32_t m_, uint32_t a) {
+    if (route.empty()) {
+      route.resize(n);
+      addr.resize(n);
+      for (uint32_t x = 0; x < n; ++x) route[x] = addr[x] = x;
+    }
+    const uint32_t A = addr[a];
+    addr[m_] = A;
+    for (uint32_t x = 0; x < n; ++x)
+      if (addr[x] == A) route[x] = m_;
+  }
 
   // ------------------------------------------------------------------------- NetworkEmulator
   // OutboundSettings resolution (NetworkEmulator.java:59-61), partition shorthand first.
@@ -422,7 +445,9 @@ struct swim_engine {
     uint32_t w1 = draw(v, SWIM_STREAM_FETCH_REQ, phase, f);
     uint32_t w2 = draw(v, SWIM_STREAM_FETCH_RESP, phase, f);
     STT().fetches++;
-    bool ok = !out_fail(v, s, w1) && in_pass(s, v) && !out_fail(s, v, w2) && in_pass(v, s);
+    // the request goes to s's address; another member listening there does not answer (:209)
+    const uint32_t d = dst(s);
+    bool ok = d == s && !out_fail(v, d, w1) && in_pass(d, v) && !out_fail(d, v, w2) && in_pass(v, d);
     if (ok) STT().fetch_ok++;
     return ok;
   }
@@ -450,6 +475,7 @@ struct swim_engine {
       spread_gossip(v, r2);
       return;
     }
+    if (dst(s) == v) return;  // another member at the local address (:605-610)
     if (r1.status == SWIM_LEAVING) {  // onLeavingDetected (:710-733)
       if (!present) { mv.table_size++; }
       c = c_with_record(c | B_IN_TABLE, SWIM_LEAVING, r1.inc);
@@ -635,7 +661,10 @@ struct swim_engine {
   // after the ping-req went out, 0 = none; it carries the same cid and arrives after the relay
   // requests subscribed), and only if the issuer's inbound filter passes its sender
   // (NetworkEmulatorTransport.requestResponse :65-74); none before pingInterval - pingTimeout: SUSPECT.
-  void ping_req(uint32_t v, uint32_t t, uint32_t late = 0) {
+  // Every message goes to an address (dst): a relay's transit ping reaches whoever listens at t's
+  // address, and that member's onPing answers DEST_GONE when it is not t (:227-259), which every
+  // ack carries back (onTransitPingAck :291-315) and computeMemberStatus turns into DEAD (:382-404).
+  void ping_req(uint32_t v, uint32_t t, uint32_t late = 0, bool late_gone = false) {
     std::vector<uint32_t> relays = select_ping_req_members(v, t);
     if (relays.empty()) {  // timeLeft <= 0 is excluded by config validation
       publish_fd(v, t, SWIM_SUSPECT);
@@ -643,35 +672,39 @@ struct swim_engine {
     }
     STT().ping_reqs++;
     std::vector<uint32_t> pending;
+    const uint32_t d = dst(t);
+    const bool gone = d != t;
     for (uint32_t j = 0; j < relays.size(); ++j) {
-      if (out_fail(v, relays[j], draw(v, SWIM_STREAM_PINGREQ_OUT, j, 0)))
+      if (out_fail(v, dst(relays[j]), draw(v, SWIM_STREAM_PINGREQ_OUT, j, 0)))
         publish_fd(v, t, SWIM_SUSPECT);  // immediate outbound error
       else
         pending.push_back(j);
     }
     if (pending.empty()) return;
     uint32_t best = NONE, first = NONE;  // arrival (ticks after now) and sender of the first ack
+    bool first_gone = gone;
     for (uint32_t j : pending) {
-      uint32_t r = relays[j];
-      if (in_pass(r, v) && !out_fail(r, t, draw(v, SWIM_STREAM_TRANSIT_PING_OUT, j, 0)) &&
-          in_pass(t, r) && !out_fail(t, r, draw(v, SWIM_STREAM_TRANSIT_ACK_OUT, j, 0)) &&
-          in_pass(r, t) && !out_fail(r, v, draw(v, SWIM_STREAM_RELAY_ACK_OUT, j, 0))) {
+      uint32_t r = dst(relays[j]);
+      if (in_pass(r, v) && !out_fail(r, d, draw(v, SWIM_STREAM_TRANSIT_PING_OUT, j, 0)) &&
+          in_pass(d, r) && !out_fail(d, r, draw(v, SWIM_STREAM_TRANSIT_ACK_OUT, j, 0)) &&
+          in_pass(r, d) && !out_fail(r, v, draw(v, SWIM_STREAM_RELAY_ACK_OUT, j, 0))) {
         const uint32_t at = delay_ticks(v, r, v, SWIM_STREAM_PINGREQ_DELAY, j, 0) +
-                            delay_ticks(r, t, v, SWIM_STREAM_TRANSIT_PING_DELAY, j, 0) +
-                            delay_ticks(t, r, v, SWIM_STREAM_TRANSIT_ACK_DELAY, j, 0) +
+                            delay_ticks(r, d, v, SWIM_STREAM_TRANSIT_PING_DELAY, j, 0) +
+                            delay_ticks(d, r, v, SWIM_STREAM_TRANSIT_ACK_DELAY, j, 0) +
                             delay_ticks(r, v, v, SWIM_STREAM_RELAY_ACK_DELAY, j, 0);
         if (at < best) { best = at; first = r; }
       }
     }
-    if (late && late - 1 < best) { best = late - 1; first = t; }
+    if (late && late - 1 < best) { best = late - 1; first = d; first_gone = late_gone; }
     Member& mv = m[v];
     if (first != NONE && best < relay_ticks && in_pass(v, first)) {
       if (best == 0) {
-        for (size_t i = 0; i < pending.size(); ++i) publish_fd(v, t, SWIM_ALIVE);
+        for (size_t i = 0; i < pending.size(); ++i) publish_fd(v, t, first_gone ? SWIM_DEAD : SWIM_ALIVE);
         return;
       }
       mv.relay_due = T + best;  // the acks complete every pending relay request then
       mv.relay_ok = true;
+      mv.relay_gone = first_gone;
     } else {
       mv.relay_due = T + relay_ticks;
       mv.relay_ok = false;
@@ -701,32 +734,36 @@ struct swim_engine {
       if (mv.relay_due == T) {  // relayed acks arrive (:190-199) or the relay timeouts (:200-209)
         uint32_t t = mv.relay_target, k = mv.relay_pending;
         mv.relay_due = 0;
-        for (uint32_t i = 0; i < k; ++i) publish_fd(v, t, mv.relay_ok ? SWIM_ALIVE : SWIM_SUSPECT);
+        const uint32_t ok_status = mv.relay_gone ? SWIM_DEAD : SWIM_ALIVE;
+        for (uint32_t i = 0; i < k; ++i) publish_fd(v, t, mv.relay_ok ? ok_status : SWIM_SUSPECT);
       }
       if (mv.ack_due == T) {  // the delayed ack arrives, or pingTimeout elapsed (:153-170)
         uint32_t t = mv.ack_target;
         mv.ack_due = 0;
-        if (mv.ack_ok) publish_fd(v, t, SWIM_ALIVE);
-        else ping_req(v, t, mv.ack_late);
+        if (mv.ack_ok) publish_fd(v, t, mv.ack_gone ? SWIM_DEAD : SWIM_ALIVE);
+        else ping_req(v, t, mv.ack_late, mv.ack_gone);
       }
       if (fd_due(mv)) {  // doPing (:126-171)
         mv.fd_period++;
         uint32_t t = select_ping_member(v);
         if (t == NONE) continue;
         STT().pings++;
-        if (out_fail(v, t, draw(v, SWIM_STREAM_PING_OUT, 0, 0))) {
+        const uint32_t d = dst(t);  // whoever listens at t's address now
+        if (out_fail(v, d, draw(v, SWIM_STREAM_PING_OUT, 0, 0))) {
           ping_req(v, t);  // outbound error -> ping-req right away
         } else {
-          // onPing answers DEST_OK (:227-259); the round trip takes the two messages' delays
-          const bool acked = in_pass(t, v) && !out_fail(t, v, draw(v, SWIM_STREAM_ACK_OUT, 0, 0));
-          const uint32_t rtt = acked ? delay_ticks(v, t, v, SWIM_STREAM_PING_DELAY, 0, 0) +
-                                           delay_ticks(t, v, v, SWIM_STREAM_ACK_DELAY, 0, 0)
+          // onPing answers DEST_OK, or DEST_GONE from another member at t's address (:227-259) ->
+          // computeMemberStatus ALIVE / DEAD (:382-404); the round trip takes both messages' delays
+          const bool acked = in_pass(d, v) && !out_fail(d, v, draw(v, SWIM_STREAM_ACK_OUT, 0, 0));
+          const uint32_t rtt = acked ? delay_ticks(v, d, v, SWIM_STREAM_PING_DELAY, 0, 0) +
+                                           delay_ticks(d, v, v, SWIM_STREAM_ACK_DELAY, 0, 0)
                                      : 0;
-          if (acked && rtt == 0 && in_pass(v, t)) {
-            publish_fd(v, t, SWIM_ALIVE);
+          mv.ack_gone = d != t;
+          if (acked && rtt == 0 && in_pass(v, d)) {
+            publish_fd(v, t, mv.ack_gone ? SWIM_DEAD : SWIM_ALIVE);
           } else {
             mv.ack_target = t;
-            mv.ack_ok = acked && rtt < to_ticks && in_pass(v, t);
+            mv.ack_ok = acked && rtt < to_ticks && in_pass(v, d);
             mv.ack_due = T + (mv.ack_ok ? rtt : to_ticks);
             mv.ack_late = acked && rtt >= to_ticks ? rtt - to_ticks + 1 : 0;
           }
@@ -801,17 +838,17 @@ struct swim_engine {
         const uint64_t spread = (uint64_t)swim_gossip_periods_to_spread(cfg.gossip_repeat_mult, size1);
         const uint64_t sweep = (uint64_t)swim_gossip_periods_to_sweep(cfg.gossip_repeat_mult, size1);
         for (uint32_t j = 0; j < targets.size(); ++j) {
-          uint32_t tg = targets[j];
+          const uint32_t tg = targets[j], rc = dst(tg);  // sent to tg's address, received by rc
           for (uint32_t p = 0; p < mv.gossips.size(); ++p) {  // selectGossipsToSend (:311-320)
             const GossipState& g = mv.gossips[p];
             if (!(g.infection_period + spread >= period)) continue;
             if (g.is_infected(tg)) continue;
             STT().gossip_messages++;
-            if (out_fail(v, tg, draw(v, SWIM_STREAM_GOSSIP_OUT, j, p))) continue;
-            if (!in_pass(tg, v)) continue;
-            const uint32_t k = delay_ticks(v, tg, v, SWIM_STREAM_GOSSIP_DELAY, j, p);
-            if (k) later[t].push_back(GMsg{tg, v, p, g, T + k});
-            else bucket[t][consumer(tg)].push_back(GMsg{tg, v, p, g, T});
+            if (out_fail(v, rc, draw(v, SWIM_STREAM_GOSSIP_OUT, j, p))) continue;
+            if (!in_pass(rc, v)) continue;
+            const uint32_t k = delay_ticks(v, rc, v, SWIM_STREAM_GOSSIP_DELAY, j, p);
+            if (k) later[t].push_back(GMsg{rc, v, p, g, T + k});
+            else bucket[t][consumer(rc)].push_back(GMsg{rc, v, p, g, T});
           }
         }
         // sweep (:158-164, :350-358)
@@ -897,11 +934,14 @@ struct swim_engine {
   // selectSyncAddress (:461-472): uniform over seeds U otherMembers, by seeded rejection sampling.
   uint32_t select_sync_address(uint32_t v) {
     const Member& mv = m[v];
+    // seed addresses exclude the local one (cleanUpSeedMembers :171-190)
     uint32_t count = mv.members_size - 1;
     for (uint32_t s : seeds)
-      if (s != v && !c_has(mv.row[s], B_IN_MEMBERS)) count++;
+      if (s != v && dst(s) != v && !c_has(mv.row[s], B_IN_MEMBERS)) count++;
     if (count == 0) return NONE;
-    auto in_set = [&](uint32_t x) { return x != v && (c_has(mv.row[x], B_IN_MEMBERS) || is_seed[x]); };
+    auto in_set = [&](uint32_t x) {
+      return x != v && (c_has(mv.row[x], B_IN_MEMBERS) || (is_seed[x] && dst(x) != v));
+    };
     for (uint32_t i = 0; i < SWIM_SYNC_SELECT_ATTEMPTS; ++i) {
       uint32_t x = next_int(draw(v, SWIM_STREAM_SYNC_SELECT, 0, i), n);
       if (in_set(x)) return x;
@@ -934,13 +974,13 @@ struct swim_engine {
         uint32_t k = 0;
         if (sync_due(mv)) {  // doSync (:339-357)
           uint32_t tg = select_sync_address(v);
-          if (tg != NONE) rq[t].push_back(SyncReq{v, tg, k++, false, false, false, false});
+          if (tg != NONE) rq[t].push_back(SyncReq{v, dst(tg), k++, false, false, false, false});
         }
-        for (uint32_t tg : mv.fd_sync) rq[t].push_back(SyncReq{v, tg, k++, false, false, false, false});
+        for (uint32_t tg : mv.fd_sync) rq[t].push_back(SyncReq{v, dst(tg), k++, false, false, false, false});
         mv.fd_sync.clear();
-        if (mv.join_now) {  // start0 initial sync to every seed (:250-291)
+        if (mv.join_now) {  // start0 initial sync to every seed (:250-291) but its own address
           for (uint32_t s : seeds)
-            if (s != v) rq[t].push_back(SyncReq{v, s, k++, true, false, false, false});
+            if (s != v && dst(s) != v) rq[t].push_back(SyncReq{v, dst(s), k++, true, false, false, false});
         }
       }
     });
@@ -1055,6 +1095,8 @@ struct swim_engine {
       Member& mv = m[v];
       if (!mv.join_pending) continue;
       mv.join_pending = false;
+      if (mv.join_addr != NONE) bind_address(v, mv.join_addr);  // the new transport binds the address
+      mv.join_addr = NONE;
       mv.up = true;
       mv.joined = true;
       mv.join_now = true;
@@ -1383,6 +1425,18 @@ int32_t swim_join(swim_engine* e, uint32_t v) {
   Member& mv = e->m[v];
   if (mv.joined || mv.up || mv.join_pending) return SWIM_ESTATE;
   mv.join_pending = true;
+  return SWIM_OK;
+}
+
+int32_t swim_join_at(swim_engine* e, uint32_t v, uint32_t addr_of) {
+  if (!e || v >= e->n || addr_of >= e->n || addr_of == v) return SWIM_EINVAL;
+  const uint32_t holder = e->dst(addr_of);
+  if (e->m[holder].up || e->m[holder].join_pending) return SWIM_ESTATE;  // the address is in use
+  for (uint32_t x = 0; x < e->n; ++x)
+    if (x != v && e->m[x].join_pending && e->m[x].join_addr != NONE && e->dst(e->m[x].join_addr) == holder)
+      return SWIM_ESTATE;
+  if (int32_t rc = swim_join(e, v)) return rc;
+  e->m[v].join_addr = addr_of;
   return SWIM_OK;
 }
 

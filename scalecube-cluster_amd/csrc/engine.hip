@@ -178,6 +178,12 @@ struct swim_engine {
   std::vector<LinkDev> links_h;
   std::vector<int32_t> delay_means;  // NetworkEmulator meanDelay (ms) of each delay table, in table order
   std::vector<uint32_t> joins;  // joins starting at the next tick
+  // addresses (swim_join_at): addr_h[x] = the address member x was started on, route_h[x] = the
+  // member listening on it now (both empty while every member is on its own address); binds: the
+  // (joiner, member whose address it takes) pairs starting at the next tick
+  std::vector<uint32_t> addr_h, route_h;
+  std::vector<std::pair<uint32_t, uint32_t>> binds;
+  uint32_t route_of(uint32_t x) const { return route_h.empty() ? x : route_h[x]; }
   std::vector<swim_event> events;
   uint64_t host_ticks = 0, host_events = 0;
   uint32_t err_seen = 0;
@@ -531,10 +537,40 @@ static void debug_slow(swim_engine* e, const char* name, uint64_t T) {
 }
 
 // One tick: 7 kernels per shard (11 on gossip ticks); a sharded engine adds k_recv_* and three exchanges.
+// joiners of this tick that take another member's address start listening on it: route_h is
+// recomputed and copied to every shard's replicated Ctx.route (allocated at the first bind)
+static int32_t apply_binds(swim_engine* e) {
+  if (e->route_h.empty()) {
+    e->route_h.resize(e->n);
+    e->addr_h.resize(e->n);
+    for (uint32_t x = 0; x < e->n; ++x) e->route_h[x] = e->addr_h[x] = x;
+  }
+  for (auto& bd : e->binds) {
+    const uint32_t A = e->addr_h[bd.second];
+    e->addr_h[bd.first] = A;
+    for (uint32_t x = 0; x < e->n; ++x)
+      if (e->addr_h[x] == A) e->route_h[x] = bd.first;
+  }
+  e->binds.clear();
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  for (Shard& sd : e->sh) {
+    if (!sd.c.route) {
+      uint32_t* r = nullptr;
+      if (!sd.alloc(&r, e->n)) return SWIM_ENOMEM;
+      sd.c.route = r;
+    }
+    if (hipMemcpy((void*)sd.c.route, e->route_h.data(), 4 * (size_t)e->n, hipMemcpyHostToDevice) != hipSuccess)
+      return SWIM_EDEVICE;
+  }
+  return SWIM_OK;
+}
+
 static int32_t run_tick(swim_engine* e) {
   e->T += 1;
   e->host_ticks += 1;
   hipStream_t s = e->stream;
+  if (!e->binds.empty())
+    if (int32_t rc = apply_binds(e)) return rc;
   const uint64_t T = e->T;
   const bool multi = e->world > 1;
   const bool gossip_tick = e->g_residue[e->T % e->G] != 0;
@@ -1199,6 +1235,19 @@ int32_t swim_join(swim_engine* e, uint32_t m) {
   e->joined_h[m] = 1;
   e->joins.push_back(m);
   e->g_residue[(e->T + 1) % e->G] = 1;  // the joiner's gossip timer phase
+  return SWIM_OK;
+}
+
+int32_t swim_join_at(swim_engine* e, uint32_t m, uint32_t addr_of) {
+  if (!e || m >= e->n || addr_of >= e->n || addr_of == m) return SWIM_EINVAL;
+  const uint32_t holder = e->route_of(addr_of);
+  uint8_t up = 0;
+  if (read_up(e, holder, &up) != SWIM_OK) return SWIM_EDEVICE;
+  if (up || std::find(e->joins.begin(), e->joins.end(), holder) != e->joins.end()) return SWIM_ESTATE;
+  for (auto& bd : e->binds)
+    if (e->route_of(bd.second) == holder) return SWIM_ESTATE;  // the address is taken at the next tick
+  if (int32_t rc = swim_join(e, m)) return rc;
+  e->binds.push_back({m, addr_of});
   return SWIM_OK;
 }
 

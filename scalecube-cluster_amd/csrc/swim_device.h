@@ -68,7 +68,8 @@ struct alignas(16) MemberDev {
   uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, gix_valid;
   uint8_t ack_ok;    // ack_due is the tick the (delayed) ack arrives, not the ping timeout
   uint8_t relay_ok;  // relay_due is the tick the first relayed ack arrives, not the timeout
-  uint8_t pad[3];
+  uint8_t ack_gone, relay_gone;  // that ack says DEST_GONE (another member listens at the target's address)
+  uint8_t pad[1];
 };
 
 // GossipState + Gossip + MembershipRecord payload, 48 B.  GossipState.infected gains a member only
@@ -185,6 +186,9 @@ struct Ctx {
   uint32_t blocks;   // ceil(n / 1024)
   MemberDev* mem;
   uint8_t* up;  // replicated: member's transport is running
+  // replicated (swim_join_at): route[x] = the member listening on member x's address now; nullptr
+  // while every member listens on its own address
+  const uint32_t* route;
   uint32_t* ping;
   uint32_t* remote;
   GossipDev* slab;
@@ -431,6 +435,9 @@ __device__ __forceinline__ bool lost_k(const Ctx& c, int32_t pct, uint32_t membe
 }
 // tryFailOutbound (NetworkEmulator.java:167-181) + a stopped destination refusing the connection;
 // the draw is keyed (member, stream, sub24, sub32)
+// the member a message sent to x's address reaches (Transport.send / requestResponse by Address)
+__device__ __forceinline__ uint32_t dst(const Ctx& c, uint32_t x) { return c.route ? c.route[x] : x; }
+
 __device__ __forceinline__ bool out_fail(const Ctx& c, uint32_t a, uint32_t b, uint32_t member, uint32_t stream,
                                          uint32_t sub24, uint32_t sub32) {
   return !c.up[b] || lost_k(c, out_loss(c, a, b), member, stream, sub24, sub32);
@@ -822,8 +829,10 @@ __device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
 __device__ inline bool fetch_ok(const Ctx& c, uint32_t v, uint32_t s, uint32_t phase) {
   uint32_t f = mem(c, v).fetch_ctr++;
   stat_add(c, ST_FETCHES, 1);
-  bool ok = !out_fail(c, v, s, v, SWIM_STREAM_FETCH_REQ, phase, f) && in_pass(c, s, v) &&
-            !out_fail(c, s, v, v, SWIM_STREAM_FETCH_RESP, phase, f) && in_pass(c, v, s);
+  // the request goes to s's address; another member listening there does not answer (:209)
+  const uint32_t d = dst(c, s);
+  bool ok = d == s && !out_fail(c, v, d, v, SWIM_STREAM_FETCH_REQ, phase, f) && in_pass(c, d, v) &&
+            !out_fail(c, d, v, v, SWIM_STREAM_FETCH_RESP, phase, f) && in_pass(c, v, d);
   if (ok) stat_add(c, ST_FETCH_OK, 1);
   return ok;
 }
@@ -848,6 +857,7 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
     spread_gossip(c, v, v, st0, cur + 1);
     return false;
   }
+  if (dst(c, s) == v) return false;  // another member at the local address (:605-610)
   if (st1 == SWIM_LEAVING) {  // onLeavingDetected (:710-733)
     if (!present) m.table_size++;
     cell = c_with_record(cell | B_IN_TABLE, SWIM_LEAVING, inc1);

@@ -378,42 +378,48 @@ __device__ inline uint32_t select_relays(const Ctx& c, uint32_t v, uint32_t t, u
 // message delay the first message carrying the cid decides: the earliest relayed ack (ties: lowest
 // relay) or a late ack of the direct ping (`late` = 1 + its arrival in ticks after the ping-req went
 // out), if the issuer's inbound filter passes its sender; none before the relay timeout: SUSPECT.
+// Every message goes to an address (dst): a relay's transit ping reaches whoever listens at t's
+// address, whose onPing answers DEST_GONE when it is not t (:227-259); every ack carries that back
+// (onTransitPingAck :291-315) and computeMemberStatus turns it into DEAD (:382-404).
 __device__ inline void ping_req(const Ctx& c, uint32_t v, uint32_t t, unsigned long long& nev,
-                                unsigned long long& nreq, uint32_t late = 0) {
+                                unsigned long long& nreq, uint32_t late = 0, bool late_gone = false) {
   uint32_t relays[16];
   uint32_t nr = select_relays(c, v, t, relays);
   if (nr == 0) { publish_fd(c, v, t, SWIM_SUSPECT, nev); return; }
   nreq++;
+  const uint32_t d = dst(c, t);
   uint32_t pending_mask = 0, npend = 0;
   for (uint32_t j = 0; j < nr; ++j) {
-    if (out_fail(c, v, relays[j], v, SWIM_STREAM_PINGREQ_OUT, j, 0)) publish_fd(c, v, t, SWIM_SUSPECT, nev);
+    if (out_fail(c, v, dst(c, relays[j]), v, SWIM_STREAM_PINGREQ_OUT, j, 0)) publish_fd(c, v, t, SWIM_SUSPECT, nev);
     else { pending_mask |= 1u << j; npend++; }
   }
   if (npend == 0) return;
   uint32_t best = NONE, first = NONE;  // arrival (ticks from now) and sender of the first ack
+  bool first_gone = d != t;
   for (uint32_t j = 0; j < nr; ++j) {
     if (!(pending_mask & (1u << j))) continue;
-    uint32_t r = relays[j];
-    if (in_pass(c, r, v) && !out_fail(c, r, t, v, SWIM_STREAM_TRANSIT_PING_OUT, j, 0) &&
-        in_pass(c, t, r) && !out_fail(c, t, r, v, SWIM_STREAM_TRANSIT_ACK_OUT, j, 0) &&
-        in_pass(c, r, t) && !out_fail(c, r, v, v, SWIM_STREAM_RELAY_ACK_OUT, j, 0)) {
+    uint32_t r = dst(c, relays[j]);
+    if (in_pass(c, r, v) && !out_fail(c, r, d, v, SWIM_STREAM_TRANSIT_PING_OUT, j, 0) &&
+        in_pass(c, d, r) && !out_fail(c, d, r, v, SWIM_STREAM_TRANSIT_ACK_OUT, j, 0) &&
+        in_pass(c, r, d) && !out_fail(c, r, v, v, SWIM_STREAM_RELAY_ACK_OUT, j, 0)) {
       const uint32_t at = delay_ticks(c, v, r, v, SWIM_STREAM_PINGREQ_DELAY, j, 0) +
-                          delay_ticks(c, r, t, v, SWIM_STREAM_TRANSIT_PING_DELAY, j, 0) +
-                          delay_ticks(c, t, r, v, SWIM_STREAM_TRANSIT_ACK_DELAY, j, 0) +
+                          delay_ticks(c, r, d, v, SWIM_STREAM_TRANSIT_PING_DELAY, j, 0) +
+                          delay_ticks(c, d, r, v, SWIM_STREAM_TRANSIT_ACK_DELAY, j, 0) +
                           delay_ticks(c, r, v, v, SWIM_STREAM_RELAY_ACK_DELAY, j, 0);
       if (at < best) { best = at; first = r; }
       if (!c.delay_on) break;  // every arrival is 0: the lowest relay
     }
   }
-  if (late && late - 1 < best) { best = late - 1; first = t; }
+  if (late && late - 1 < best) { best = late - 1; first = d; first_gone = late_gone; }
   MemberDev& m = mem(c, v);
   if (first != NONE && best < c.relay_ticks && in_pass(c, v, first)) {
     if (best == 0) {
-      for (uint32_t i = 0; i < npend; ++i) publish_fd(c, v, t, SWIM_ALIVE, nev);
+      for (uint32_t i = 0; i < npend; ++i) publish_fd(c, v, t, first_gone ? SWIM_DEAD : SWIM_ALIVE, nev);
       return;
     }
     m.relay_due = c.T + best;  // the acks complete every pending relay request then
     m.relay_ok = 1;
+    m.relay_gone = first_gone ? 1 : 0;
   } else {
     m.relay_due = c.T + c.relay_ticks;
     m.relay_ok = 0;
@@ -433,13 +439,14 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
   if (m.relay_due == c.T) {  // relayed acks arrive (:190-199) or the relay timeouts (:200-209)
     uint32_t t = m.relay_target, k = m.relay_pending;
     m.relay_due = 0;
-    for (uint32_t i = 0; i < k; ++i) publish_fd(c, v, t, m.relay_ok ? SWIM_ALIVE : SWIM_SUSPECT, nev);
+    const uint32_t ok_status = m.relay_gone ? SWIM_DEAD : SWIM_ALIVE;
+    for (uint32_t i = 0; i < k; ++i) publish_fd(c, v, t, m.relay_ok ? ok_status : SWIM_SUSPECT, nev);
   }
   if (m.ack_due == c.T) {  // the delayed ack arrives, or pingTimeout elapsed
     uint32_t t = m.ack_target;
     m.ack_due = 0;
-    if (m.ack_ok) publish_fd(c, v, t, SWIM_ALIVE, nev);
-    else ping_req(c, v, t, nev, nreq, m.ack_late);
+    if (m.ack_ok) publish_fd(c, v, t, m.ack_gone ? SWIM_DEAD : SWIM_ALIVE, nev);
+    else ping_req(c, v, t, nev, nreq, m.ack_late, m.ack_gone != 0);
   }
   if (due) {  // doPing (:126-171), selectPingMember (:352-361)
     m.fd_period++;
@@ -451,19 +458,22 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
       }
       uint32_t t = pl[m.ping_cursor++];
       npings++;
-      if (out_fail(c, v, t, v, SWIM_STREAM_PING_OUT, 0, 0)) {
+      const uint32_t d = dst(c, t);  // whoever listens at t's address now
+      if (out_fail(c, v, d, v, SWIM_STREAM_PING_OUT, 0, 0)) {
         ping_req(c, v, t, nev, nreq);
       } else {
-        // onPing answers DEST_OK (:227-259); the round trip takes the two messages' delays
-        const bool acked = in_pass(c, t, v) && !out_fail(c, t, v, v, SWIM_STREAM_ACK_OUT, 0, 0);
-        const uint32_t rtt = acked ? delay_ticks(c, v, t, v, SWIM_STREAM_PING_DELAY, 0, 0) +
-                                         delay_ticks(c, t, v, v, SWIM_STREAM_ACK_DELAY, 0, 0)
+        // onPing answers DEST_OK, or DEST_GONE from another member at t's address (:227-259) ->
+        // computeMemberStatus ALIVE / DEAD (:382-404); the round trip takes both messages' delays
+        const bool acked = in_pass(c, d, v) && !out_fail(c, d, v, v, SWIM_STREAM_ACK_OUT, 0, 0);
+        const uint32_t rtt = acked ? delay_ticks(c, v, d, v, SWIM_STREAM_PING_DELAY, 0, 0) +
+                                         delay_ticks(c, d, v, v, SWIM_STREAM_ACK_DELAY, 0, 0)
                                    : 0u;
-        if (acked && rtt == 0 && in_pass(c, v, t)) {
-          publish_fd(c, v, t, SWIM_ALIVE, nev);
+        m.ack_gone = d != t ? 1 : 0;
+        if (acked && rtt == 0 && in_pass(c, v, d)) {
+          publish_fd(c, v, t, d != t ? SWIM_DEAD : SWIM_ALIVE, nev);
         } else {
           m.ack_target = t;
-          m.ack_ok = acked && rtt < c.to_ticks && in_pass(c, v, t);
+          m.ack_ok = acked && rtt < c.to_ticks && in_pass(c, v, d);
           m.ack_due = c.T + (m.ack_ok ? rtt : c.to_ticks);
           m.ack_late = acked && rtt >= c.to_ticks ? rtt - c.to_ticks + 1 : 0;
         }
@@ -568,6 +578,11 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       m.remote_idx += (int32_t)F;
     }
     s_t[0] = nt;
+    // s_t[1 + j]: the member that receives what is sent to target j's address; s_t[17 + j]: target j
+    for (uint32_t j = 0; j < nt; ++j) {
+      s_t[17 + j] = s_t[1 + j];
+      s_t[1 + j] = dst(c, s_t[1 + j]);
+    }
   }
   __syncwarp();
   const uint32_t nt = s_t[0];
@@ -617,7 +632,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     if (__ballot(win)) {
       for (uint32_t j = 0; j < nt; ++j) {
         const uint32_t t = s_t[1 + j];
-        const bool send = win && !gossip_infected(g, t);
+        const bool send = win && !gossip_infected(g, s_t[17 + j]);
         nmsg += send ? 1u : 0u;
         // delivered copies; a receiver on this shard that already holds the sequence id drops it
         // (its collector only grows until delivery), another shard flags it on arrival
@@ -797,7 +812,7 @@ __global__ void __launch_bounds__(256) k_fd(KP, int gossip, int collect) {
 // the rest of the round for the listed senders: one sender per wave at a time
 // prof (sampled launches only): {GOSSIP_REQs materialised, (gossip, sender round) states read}
 __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned long long* prof) {
-  __shared__ uint32_t s_t[EMIT_WAVES][17];
+  __shared__ uint32_t s_t[EMIT_WAVES][33];
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1308,19 +1323,20 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect) {
 __device__ inline uint32_t select_sync_address(const Ctx& c, uint32_t v) {
   const MemberDev& m = mem(c, v);
   const uint32_t* a = aux_row(c, v);
+  // seed addresses exclude the local one (cleanUpSeedMembers :171-190)
   uint32_t count = m.members_size - 1;
   for (uint32_t i = 0; i < c.n_seeds; ++i) {
     uint32_t s = c.seeds[i];
-    if (s != v && !(a[s] & A_IN_MEMBERS)) count++;
+    if (s != v && dst(c, s) != v && !(a[s] & A_IN_MEMBERS)) count++;
   }
   if (count == 0) return NONE;
   for (uint32_t i = 0; i < SWIM_SYNC_SELECT_ATTEMPTS; ++i) {
     uint32_t x = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 0, i), c.n);
-    if (x != v && ((a[x] & A_IN_MEMBERS) || c.is_seed[x])) return x;
+    if (x != v && ((a[x] & A_IN_MEMBERS) || (c.is_seed[x] && dst(c, x) != v))) return x;
   }
   uint32_t k = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 1, 0), count);
   for (uint32_t x = 0; x < c.n; ++x)
-    if (x != v && ((a[x] & A_IN_MEMBERS) || c.is_seed[x])) {
+    if (x != v && ((a[x] & A_IN_MEMBERS) || (c.is_seed[x] && dst(c, x) != v))) {
       if (k == 0) return x;
       --k;
     }
@@ -1492,10 +1508,10 @@ __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Buf
   unsigned long long nsync = 0;
   if (due) {
     uint32_t t = select_sync_address(c, v);
-    if (t != NONE) { add_req(c, b, v, t, k++, false); nsync++; }
+    if (t != NONE) { add_req(c, b, v, dst(c, t), k++, false); nsync++; }
   }
   for (uint32_t i = 0; i < m.fd_sync_cnt; ++i) {
-    add_req(c, b, v, c.fd_sync[(size_t)(v - c.lo) * FD_SYNC_MAX + i], k++, false);
+    add_req(c, b, v, dst(c, c.fd_sync[(size_t)(v - c.lo) * FD_SYNC_MAX + i]), k++, false);
     nsync++;
   }
   m.fd_sync_cnt = 0;
@@ -1504,7 +1520,7 @@ __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Buf
     m.init_done = 0;
     for (uint32_t i = 0; i < c.n_seeds; ++i) {
       uint32_t s = c.seeds[i];
-      if (s != v) { add_req(c, b, v, s, k++, true); nsync++; }
+      if (s != v && dst(c, s) != v) { add_req(c, b, v, dst(c, s), k++, true); nsync++; }
     }
   }
   return nsync;

@@ -180,6 +180,7 @@ PROTOTYPES = {
     "swim_update_metadata": (C.c_int32, [_engp, C.c_uint32]),
     "swim_set_namespaces": (C.c_int32, [_engp, C.c_void_p, C.c_uint32, C.c_void_p]),
     "swim_join": (C.c_int32, [_engp, C.c_uint32]),
+    "swim_join_at": (C.c_int32, [_engp, C.c_uint32, C.c_uint32]),
     "swim_set_default_loss": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
     "swim_set_link_loss": (C.c_int32, [_engp, C.c_uint32, C.c_uint32, C.c_int32]),
     "swim_set_default_delay": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
@@ -329,6 +330,10 @@ class Engine:
 
     def join(self, m: int) -> None:
         _check("swim_join", self.lib.swim_join(self._h, m))
+
+    def join_at(self, m: int, addr_of: int) -> None:
+        """Start member m on the address of stopped member addr_of (a restart on the same port)."""
+        _check("swim_join_at", self.lib.swim_join_at(self._h, m, addr_of))
 
     def set_default_loss(self, loss_percent: int, m: int = ALL_MEMBERS) -> None:
         _check("swim_set_default_loss", self.lib.swim_set_default_loss(self._h, m, loss_percent))

@@ -535,8 +535,13 @@ class SimulatedCluster:
         """MembershipProtocolImpl.leaveCluster (:233-242) without stopping the member."""
         self.engine.leave(m, False)
 
-    def join(self, m: int):
-        self.engine.join(m)
+    def join(self, m: int, same_address_as: int = None):
+        """Start member m; with same_address_as, on that stopped member's address (a restart on the
+        same port, MembershipProtocolTest.testRestartStoppedMembersOnSameAddresses :654-711)."""
+        if same_address_as is None:
+            self.engine.join(m)
+        else:
+            self.engine.join_at(m, same_address_as)
 
     # -- views
     def membership(self, m: int) -> MembershipView:

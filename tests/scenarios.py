@@ -34,6 +34,8 @@ def apply_op(e: abi.Engine, op, args):
         e.leave(*args)
     elif op == "join":
         e.join(*args)
+    elif op == "join_at":
+        e.join_at(*args)
     elif op == "loss":
         e.set_default_loss(*args)
     elif op == "link_loss":
@@ -190,6 +192,24 @@ def catalog() -> list[Scenario]:
                                          "develop/develop-2", "root", "root", "root2", "root2"])]
                  + [(2 + 3 * i, "join", 1 + i) for i in range(8)],
                  check_every=20),
+        # MembershipProtocolTest.testRestartStoppedMembersOnSameAddresses (:643-711): C and D stop, new
+        # instances start on their ports; pings to the old ids answer DEST_GONE -> DEAD -> REMOVED
+        Scenario("mp_restart_same_address", 6, 4, 60, seed=24, cfg=mp_test, seeds=(0, 1, 2, 3),
+                 ops=[(10, "kill", 2), (10, "kill", 3), (20, "join_at", 4, 2), (20, "join_at", 5, 3)]),
+        # restarts on the same address under 5 % loss (DEST_GONE through ping-req relays, unanswered
+        # metadata requests): a seed restarted, a member restarted twice, a plain kill and join
+        Scenario("restart_same_address_40", 40, 32, 600, seed=25, seeds=(0, 5),
+                 ops=[(0, "loss", 5, abi.ALL_MEMBERS), (30, "kill", 5), (30, "kill", 9), (45, "join_at", 32, 5),
+                      (60, "join_at", 33, 9), (100, "kill", 12), (110, "join", 35), (200, "kill", 33),
+                      (215, "join_at", 34, 9)],
+                 check_every=50),
+        # the same under a 150 ms mean message delay (a DEST_GONE ack arriving late, after the ping
+        # timeout, joins the ping-req race)
+        Scenario("restart_same_address_delay", 40, 32, 600, seed=26, seeds=(0, 5),
+                 ops=[(0, "loss", 5, abi.ALL_MEMBERS), (0, "default_delay", 150, abi.ALL_MEMBERS), (30, "kill", 5),
+                      (30, "kill", 9), (45, "join_at", 32, 5), (60, "join_at", 33, 9), (200, "kill", 33),
+                      (215, "join_at", 34, 9)],
+                 check_every=50, shardable=False),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),
                  cfg=dict(sync_interval=5000), ops=[(100, "partition", _partition(32, 16)), (1100, "partition", None)],

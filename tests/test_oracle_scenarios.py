@@ -483,3 +483,47 @@ def test_mp_restart_stopped_members():  # MembershipProtocolTest.testRestartStop
     c.await_seconds(3)
     for m, want in ((4, [0, 1, 4, 5]), (5, [0, 1, 4, 5]), (0, [0, 1, 4, 5]), (1, [0, 1, 4, 5])):
         assert trusted(c, m) == want and suspected(c, m) == [], m
+
+
+def restart_on_same_addresses(lib, seed=9):
+    """MembershipProtocolTest.testRestartStoppedMembersOnSameAddresses (:643-711): C and D stop and
+    are suspected; new instances (fresh ids: free slots 4 and 5) start on C's and D's ports."""
+    conf = mp_config(4)
+    e = abi.Engine(lib, conf.to_abi(lib, record_fd_events=1), 6, 4, seed)
+    c = SimulatedCluster.from_engine(e, conf)
+    c.await_seconds(1)
+    for m, want in ((0, [0, 1, 2, 3]), (1, [0, 1, 2, 3]), (2, [0, 1, 2, 3]), (3, [0, 1, 2, 3])):
+        assert trusted(c, m) == want, m
+    c.membership(0).listen(), c.membership(1).listen()
+    c.failure_detector(0).listen(), c.failure_detector(1).listen()
+    c.kill(2)
+    c.kill(3)
+    c.await_seconds(1)
+    for m in (0, 1):
+        assert trusted(c, m) == [0, 1] and suspected(c, m) == [2, 3], m
+    c.join(4, same_address_as=2)
+    c.join(5, same_address_as=3)
+    return c
+
+
+def test_mp_restart_stopped_members_on_same_addresses():
+    c = restart_on_same_addresses(oracle.lib())
+    t_restart = c.now_ms
+    c.await_seconds(3)
+    # new C -> A, B, new D; new D -> A, B, new C; A, B -> B / A, new C, new D; nobody suspected
+    for m, want in ((4, [0, 1, 4, 5]), (5, [0, 1, 4, 5]), (0, [0, 1, 4, 5]), (1, [0, 1, 4, 5])):
+        assert trusted(c, m) == want and suspected(c, m) == [], m
+    for m in (0, 1):
+        ev = c.membership(m).listen()
+        assert sorted(x.member.id for x in ev if x.type == Type.REMOVED) == [2, 3]
+        # old C / D are removed through DEST_GONE: a ping to their address reaches the new member,
+        # which answers DEST_GONE (FailureDetectorImpl.onPing :227-259) -> FD DEAD (:382-404) ->
+        # REMOVED well before their suspicion timeouts (ClusterMath.suspicionTimeout: 3 s here)
+        fd = c.failure_detector(m).listen()
+        dead = {x.member.id for x in fd if x.status == MemberStatus.DEAD}
+        assert dead == {2, 3}, (m, fd)
+        removed_ms = [x.timestamp for x in ev if x.type == Type.REMOVED]
+        assert max(removed_ms) - t_restart < 1500, removed_ms
+    # the restarted members never admit the old records at their own addresses (:605-610)
+    assert 2 not in [x.id for x in c.membership(4).members()]
+    assert 3 not in [x.id for x in c.membership(5).members()]
