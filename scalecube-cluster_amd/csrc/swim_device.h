@@ -687,8 +687,9 @@ __device__ inline void on_added(const Ctx& c, uint32_t v, uint32_t s, uint32_t p
 
 // REMOVED: GossipProtocolImpl drops the member's SequenceIdCollector (:242); both lists drop the
 // member before the viewer's next FD step (k_fd; they hold exactly the viewer's other `members`).
-// REMOVED only arises in the timer phase (DEAD is never gossiped or synced, and the FD publishes no
-// DEAD without DEST_GONE), and nothing reads the lists between the timers and the FD step.
+// REMOVED arises in the timer phase (DEAD is never gossiped or synced), where nothing reads the lists
+// before the FD step, and in the FD step on a DEST_GONE ack, which removes the member from both lists
+// itself (publish_fd).
 // Safe under entry-parallel timer processing: only the (v, s) collector entry is written.
 __device__ inline void on_removed(const Ctx& c, uint32_t v, uint32_t s) {
   CollEnt* e = coll_find(c, v, s);

@@ -321,6 +321,15 @@ __device__ void compact_list(const Ctx& c, uint32_t v, uint32_t* list, uint32_t&
   __syncthreads();
 }
 
+// ArrayList.remove(Object): the first x, later elements shift down one place
+__device__ inline void list_remove(uint32_t* list, uint32_t& len, uint32_t x) {
+  uint32_t j = 0;
+  while (j < len && list[j] != x) ++j;
+  if (j == len) return;
+  for (; j + 1 < len; ++j) list[j] = list[j + 1];
+  len--;
+}
+
 // ------------------------------------------------------------------------------- phase B
 // publishPingResult (FailureDetectorImpl.java:377-380) -> onFailureDetectorEvent (:418-449)
 __device__ inline void publish_fd(const Ctx& c, uint32_t v, uint32_t t, uint32_t status, unsigned long long& nev) {
@@ -339,6 +348,14 @@ __device__ inline void publish_fd(const Ctx& c, uint32_t v, uint32_t t, uint32_t
     return;
   }
   update_membership(c, v, t, status, c_inc(cell), R_FD_EVENT, SWIM_PHASE_FD);
+  if (status == SWIM_DEAD && !(aux_row(c, v)[t] & A_IN_MEMBERS)) {
+    // a DEST_GONE ack removed t inside the FD step: pingMembers / remoteMembers.remove(t) now
+    // (FailureDetectorImpl.java:323-333, GossipProtocolImpl.java:240-251), before the member's
+    // doPing picks its target; the serial shift is ArrayList.remove (rare: one per restart seen)
+    MemberDev& m = mem(c, v);
+    list_remove(ping_list(c, v), m.ping_len, t);
+    list_remove(remote_list(c, v), m.remote_len, t);
+  }
 }
 
 // selectPingReqMembers (:363-375) as a forward partial Fisher-Yates over pingMembers \ {target}
@@ -578,11 +595,19 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       m.remote_idx += (int32_t)F;
     }
     s_t[0] = nt;
-    // s_t[1 + j]: the member that receives what is sent to target j's address; s_t[17 + j]: target j
+    // s_t[1 + j]: the member that receives what is sent to target j's address; s_t[17 + j]: target j;
+    // s_t[33 + j]: the first target with the same receiver (an old member and the member restarted
+    // on its address are both targets); s_t[49]: some target shares its receiver
+    uint32_t alias = 0;
     for (uint32_t j = 0; j < nt; ++j) {
       s_t[17 + j] = s_t[1 + j];
       s_t[1 + j] = dst(c, s_t[1 + j]);
+      uint32_t j0 = 0;
+      while (s_t[1 + j0] != s_t[1 + j]) ++j0;
+      s_t[33 + j] = j0;
+      alias |= j0 != j ? 1u : 0u;
     }
+    s_t[49] = alias;
   }
   __syncwarp();
   const uint32_t nt = s_t[0];
@@ -656,6 +681,16 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         }
         mat = mat && !(owned(c, t) && known_received(c, t, g.gossiper, g.seq));
         matb |= (mat ? 1u : 0u) << j;
+      }
+      if (s_t[49]) {
+        // two targets at one address: their copies of this gossip are the same message to the same
+        // receiver in the same round, and after the first the collector holds the sequence id
+        // (onGossipReq :205 returns), so one copy is materialised, under the first such target,
+        // which keeps the pair's pseq dense
+        for (uint32_t j = 1; j < nt; ++j) {
+          const uint32_t j0 = s_t[33 + j];
+          if (j0 != j && ((matb >> j) & 1u)) matb = (matb & ~(1u << j)) | (1u << j0);
+        }
       }
     }
     if (!__ballot(matb != 0)) continue;
@@ -812,7 +847,7 @@ __global__ void __launch_bounds__(256) k_fd(KP, int gossip, int collect) {
 // the rest of the round for the listed senders: one sender per wave at a time
 // prof (sampled launches only): {GOSSIP_REQs materialised, (gossip, sender round) states read}
 __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned long long* prof) {
-  __shared__ uint32_t s_t[EMIT_WAVES][33];
+  __shared__ uint32_t s_t[EMIT_WAVES][50];
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -853,7 +888,10 @@ __global__ void __launch_bounds__(256) k_dq_release(KP) {
       uint32_t rank = 0;
       for (uint32_t j = 0; j < cnt; ++j) {
         const GMsgFull& o = q[j];
-        rank += (o.to == msg.to && o.pad == msg.pad && o.from == msg.from && o.pos < msg.pos) ? 1u : 0u;
+        // copies with equal keys (one gossip sent to two targets at one address) are identical
+        // messages: ranked in bucket order
+        rank += (o.to == msg.to && o.pad == msg.pad && o.from == msg.from &&
+                 (o.pos < msg.pos || (o.pos == msg.pos && j < i))) ? 1u : 0u;
       }
       msg.pseq = rank;
       msg.pad = (uint32_t)T - msg.pad;  // age: snd_key orders earlier rounds first

@@ -205,7 +205,7 @@ def catalog() -> list[Scenario]:
                  check_every=50),
         # the same under a 150 ms mean message delay (a DEST_GONE ack arriving late, after the ping
         # timeout, joins the ping-req race)
-        Scenario("restart_same_address_delay", 40, 32, 600, seed=26, seeds=(0, 5),
+        Scenario("restart_same_address_delay", 40, 32, 600, seed=26, seeds=(0, 5), cfg=dict(delay_capacity=16384),
                  ops=[(0, "loss", 5, abi.ALL_MEMBERS), (0, "default_delay", 150, abi.ALL_MEMBERS), (30, "kill", 5),
                       (30, "kill", 9), (45, "join_at", 32, 5), (60, "join_at", 33, 9), (200, "kill", 33),
                       (215, "join_at", 34, 9)],
