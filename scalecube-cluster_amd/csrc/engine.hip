@@ -114,14 +114,13 @@ struct Shard {
   Counters* k = nullptr;
   Xc* x = nullptr;
   std::vector<void*> allocs;
-  // received cross-shard traffic (grown on demand; sizes are known on the host before each copy)
-  GMsgFull* rx_msgs = nullptr;
-  SyncReq* rx_reqs = nullptr;
-  uint32_t* rx_rows = nullptr;
-  uint32_t* rx_stops = nullptr;
-  uint32_t* tx_rows = nullptr;
-  size_t rx_msg_cap = 0, rx_req_cap = 0, rx_row_cap = 0, tx_row_cap = 0, rx_stop_cap = 0;
-  uint32_t n_rx_msgs = 0, n_rx_reqs = 0, n_rx_stops = 0;
+  // cross-shard exchange: the producer-side buffers (tx_msgs, tx_reqs, tx_acks,
+  // tx_stops, tx_rows) live in one allocation, `xreg`, whose IPC handle the other ranks open;
+  // `peers` (device) says where this shard reads what the others produced for it
+  void* xreg = nullptr;
+  size_t xreg_bytes = 0;
+  Peers* peers = nullptr;
+  std::vector<void*> ipc_open;  // peers' regions mapped here (RCCL)
   uint32_t links_dev_cap = 0;
   // device-resident launch parameters (swim_phases.h Params) and the last uploaded image
   Params* d_par = nullptr;
@@ -166,8 +165,7 @@ struct swim_engine {
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
   std::vector<Shard> sh;  // local shards, in shard order
-  uint32_t* d_cnt = nullptr;  // RCCL: received per-peer counts
-  uint32_t* h_cnt = nullptr;  // pinned host mirror
+  uint32_t* d_cnt = nullptr;  // RCCL: the capacity-error allreduce of swim_step_ticks
   Params* h_par = nullptr;    // pinned staging ring for Params uploads
   uint32_t par_slot = 0;
   // host mirrors of replicated control state
@@ -194,10 +192,11 @@ struct swim_engine {
     for (Shard& s : sh) {
       for (hipEvent_t ev : s.prof_cls.ev) hipEventDestroy(ev);
       for (hipEvent_t ev : s.prof_emit.ev) hipEventDestroy(ev);
+      for (void* p : s.ipc_open) hipIpcCloseMemHandle(p);
       for (void* p : s.allocs) hipFree(p);
+      if (s.xreg) hipFree(s.xreg);
     }
     if (d_cnt) hipFree(d_cnt);
-    if (h_cnt) hipHostFree(h_cnt);
     if (h_par) hipHostFree(h_par);
     if (comm) ncclCommDestroy(comm);
     if (stream) hipStreamDestroy(stream);
@@ -307,176 +306,25 @@ static int32_t sync_and_collect(swim_engine* e) {
 }
 
 // ------------------------------------------------------------------------------- exchange
-// Per-destination counts of every local shard's outgoing traffic (and, with RCCL, the counts every
-// peer sends here).  `kind`: 0 gossip messages + stops, 1 SYNC, 2 SYNC_ACK.
-struct Counts {
-  uint32_t tx[MAXW][MAXW];  // [src][dst] (RCCL: only row `rank` is valid)
-  uint32_t rx[MAXW];        // RCCL: count arriving from each peer
-  uint32_t stop_tx[MAXW];   // [src]
-  uint32_t stop_rx[MAXW];   // RCCL: stop count of each peer
-};
+// Per exchange (E1 GOSSIP_REQs + stops, E2 SYNCs, E3 SYNC_ACKs) every shard learns, on the device,
+// how many items each other shard produced for it, then pulls them from the producers' buffers with
+// kernels that read those counts themselves: no host synchronisation and no copies
+// sized by the host.  RCCL: one ncclAllToAll of the per-destination counts (+ one ncclAllGather of
+// the stop counts on E1), which is also the barrier after which the producers' buffers are complete;
+// a local group: k_gather_counts reads the peer shards' counters.
+constexpr uint32_t kRecvGrid = 1024, kPackGrid = 2048;
 
-static int32_t read_counts(swim_engine* e, int kind, Counts* ct) {
-  std::memset(ct, 0, sizeof(*ct));
-  const uint32_t W = (uint32_t)e->world;
+static int32_t exchange_counts(swim_engine* e, uint32_t kind) {
   hipStream_t s = e->stream;
   if (e->rccl) {
     Shard& sd = e->sh[0];
-    uint32_t* send = kind == 0 ? sd.x->msg : kind == 1 ? sd.x->req : sd.x->ack;
+    uint32_t* send = kind == XK_MSG ? sd.x->msg : kind == XK_REQ ? sd.x->req : sd.x->ack;
     if (ncclGroupStart() != ncclSuccess) return SWIM_EDEVICE;
-    ncclAllToAll(send, e->d_cnt, 1, ncclUint32, e->comm, s);
-    if (kind == 0) ncclAllGather(&sd.x->stop, e->d_cnt + MAXW, 1, ncclUint32, e->comm, s);
-    if (nccl_ok(ncclGroupEnd()) != SWIM_OK) return SWIM_EDEVICE;
-    hipMemcpyAsync(e->h_cnt, e->d_cnt, sizeof(uint32_t) * 2 * MAXW, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(e->h_cnt + 2 * MAXW, sd.x, sizeof(Xc), hipMemcpyDeviceToHost, s);
-    if (hipStreamSynchronize(s) != hipSuccess) return SWIM_EDEVICE;
-    const Xc* hx = reinterpret_cast<const Xc*>(e->h_cnt + 2 * MAXW);
-    const uint32_t* own = kind == 0 ? hx->msg : kind == 1 ? hx->req : hx->ack;
-    const uint32_t cap = kind == 0 ? sd.b.tx_msg_cap : sd.b.tx_req_cap;
-    for (uint32_t d = 0; d < W; ++d) {
-      ct->tx[e->rank][d] = std::min(own[d], cap);
-      ct->rx[d] = std::min(e->h_cnt[d], cap);
-      ct->stop_rx[d] = kind == 0 ? std::min(e->h_cnt[MAXW + d], kStopCap) : 0;
-    }
-    ct->stop_tx[e->rank] = kind == 0 ? std::min(hx->stop, kStopCap) : 0;
-    return SWIM_OK;
+    ncclAllToAll(send, sd.b.rx_cnt + kind * MAXW, 1, ncclUint32, e->comm, s);
+    if (kind == XK_MSG) ncclAllGather(&sd.x->stop, sd.b.rx_cnt + XK_STOP * MAXW, 1, ncclUint32, e->comm, s);
+    return nccl_ok(ncclGroupEnd());
   }
-  std::vector<Xc> hx(W);
-  for (uint32_t r = 0; r < W; ++r) hipMemcpyAsync(&hx[r], e->sh[r].x, sizeof(Xc), hipMemcpyDeviceToHost, s);
-  if (hipStreamSynchronize(s) != hipSuccess) return SWIM_EDEVICE;
-  for (uint32_t r = 0; r < W; ++r) {
-    const uint32_t* own = kind == 0 ? hx[r].msg : kind == 1 ? hx[r].req : hx[r].ack;
-    const uint32_t cap = kind == 0 ? e->sh[r].b.tx_msg_cap : e->sh[r].b.tx_req_cap;
-    for (uint32_t d = 0; d < W; ++d) ct->tx[r][d] = std::min(own[d], cap);
-    ct->stop_tx[r] = kind == 0 ? std::min(hx[r].stop, kStopCap) : 0;
-  }
-  return SWIM_OK;
-}
-
-// E1: GOSSIP_REQs for receivers on other shards + completed graceful leaves (broadcast)
-static int32_t exchange_msgs(swim_engine* e) {
-  Counts ct;
-  if (int32_t rc = read_counts(e, 0, &ct)) return rc;
-  const uint32_t W = (uint32_t)e->world;
-  hipStream_t s = e->stream;
-  if (e->rccl) {
-    Shard& sd = e->sh[0];
-    const uint32_t me = (uint32_t)e->rank;
-    size_t nm = 0, ns = 0;
-    for (uint32_t p = 0; p < W; ++p) if (p != me) { nm += ct.rx[p]; ns += ct.stop_rx[p]; }
-    if (!sd.grow(&sd.rx_msgs, &sd.rx_msg_cap, nm) || !sd.grow(&sd.rx_stops, &sd.rx_stop_cap, ns)) return SWIM_ENOMEM;
-    if (ncclGroupStart() != ncclSuccess) return SWIM_EDEVICE;
-    size_t om = 0, os = 0;
-    for (uint32_t p = 0; p < W; ++p) {
-      if (p == me) continue;
-      if (ct.tx[me][p]) ncclSend(sd.b.tx_msgs + (size_t)p * sd.b.tx_msg_cap, ct.tx[me][p] * sizeof(GMsgFull), ncclUint8, p, e->comm, s);
-      if (ct.stop_tx[me]) ncclSend(sd.b.tx_stops, ct.stop_tx[me] * 4, ncclUint8, p, e->comm, s);
-      if (ct.rx[p]) ncclRecv(sd.rx_msgs + om, ct.rx[p] * sizeof(GMsgFull), ncclUint8, p, e->comm, s);
-      if (ct.stop_rx[p]) ncclRecv(sd.rx_stops + os, ct.stop_rx[p] * 4, ncclUint8, p, e->comm, s);
-      om += ct.rx[p];
-      os += ct.stop_rx[p];
-    }
-    if (nccl_ok(ncclGroupEnd()) != SWIM_OK) return SWIM_EDEVICE;
-    sd.n_rx_msgs = (uint32_t)om;
-    sd.n_rx_stops = (uint32_t)os;
-    return SWIM_OK;
-  }
-  for (uint32_t d = 0; d < W; ++d) {
-    Shard& dst = e->sh[d];
-    size_t nm = 0, ns = 0;
-    for (uint32_t r = 0; r < W; ++r) if (r != d) { nm += ct.tx[r][d]; ns += ct.stop_tx[r]; }
-    if (!dst.grow(&dst.rx_msgs, &dst.rx_msg_cap, nm) || !dst.grow(&dst.rx_stops, &dst.rx_stop_cap, ns)) return SWIM_ENOMEM;
-    size_t om = 0, os = 0;
-    for (uint32_t r = 0; r < W; ++r) {
-      if (r == d) continue;
-      Shard& src = e->sh[r];
-      if (ct.tx[r][d])
-        hipMemcpyAsync(dst.rx_msgs + om, src.b.tx_msgs + (size_t)d * src.b.tx_msg_cap, ct.tx[r][d] * sizeof(GMsgFull),
-                       hipMemcpyDeviceToDevice, s);
-      if (ct.stop_tx[r])
-        hipMemcpyAsync(dst.rx_stops + os, src.b.tx_stops, ct.stop_tx[r] * 4, hipMemcpyDeviceToDevice, s);
-      om += ct.tx[r][d];
-      os += ct.stop_tx[r];
-    }
-    dst.n_rx_msgs = (uint32_t)om;
-    dst.n_rx_stops = (uint32_t)os;
-  }
-  return SWIM_OK;
-}
-
-// pack the content rows of shard `sd`'s outgoing SYNC (kind 1) / SYNC_ACK (kind 2) per destination
-static int32_t pack_rows(swim_engine* e, Shard& sd, uint32_t src_idx, int kind, const Counts& ct, PackPlan* plan) {
-  std::memset(plan, 0, sizeof(*plan));
-  uint32_t tot = 0;
-  for (uint32_t d = 0; d < (uint32_t)e->world; ++d) {
-    plan->cnt[d] = d == src_idx ? 0 : ct.tx[src_idx][d];
-    plan->off[d] = tot;
-    tot += plan->cnt[d];
-  }
-  if (!tot) return SWIM_OK;
-  if (!sd.grow(&sd.tx_rows, &sd.tx_row_cap, (size_t)tot * e->n)) return SWIM_ENOMEM;
-  const SyncReq* tx = kind == 1 ? sd.b.tx_reqs : sd.b.tx_acks;
-  const uint32_t units = tot * ((e->n + PACK_CHUNK - 1) / PACK_CHUNK);
-  k_pack_rows<<<std::min<uint32_t>(units, 4096), 256, 0, e->stream>>>(sd.c, tx, sd.b.tx_req_cap, *plan, tot, sd.tx_rows);
-  return SWIM_OK;
-}
-
-// E2 / E3: SYNC (kind 1) or SYNC_ACK (kind 2) headers + content rows for receivers on other shards
-static int32_t exchange_sync(swim_engine* e, int kind) {
-  Counts ct;
-  if (int32_t rc = read_counts(e, kind, &ct)) return rc;
-  const uint32_t W = (uint32_t)e->world;
-  const size_t row_bytes = (size_t)e->n * 4;  // a SYNC carries the record words of a row
-  hipStream_t s = e->stream;
-  if (e->rccl) {
-    Shard& sd = e->sh[0];
-    const uint32_t me = (uint32_t)e->rank;
-    PackPlan plan;
-    if (int32_t rc = pack_rows(e, sd, me, kind, ct, &plan)) return rc;
-    size_t nr = 0;
-    for (uint32_t p = 0; p < W; ++p) if (p != me) nr += ct.rx[p];
-    if (!sd.grow(&sd.rx_reqs, &sd.rx_req_cap, nr) || !sd.grow(&sd.rx_rows, &sd.rx_row_cap, nr * e->n)) return SWIM_ENOMEM;
-    const SyncReq* tx = kind == 1 ? sd.b.tx_reqs : sd.b.tx_acks;
-    if (ncclGroupStart() != ncclSuccess) return SWIM_EDEVICE;
-    size_t o = 0;
-    for (uint32_t p = 0; p < W; ++p) {
-      if (p == me) continue;
-      if (plan.cnt[p]) {
-        ncclSend(tx + (size_t)p * sd.b.tx_req_cap, plan.cnt[p] * sizeof(SyncReq), ncclUint8, p, e->comm, s);
-        ncclSend(sd.tx_rows + (size_t)plan.off[p] * e->n, plan.cnt[p] * row_bytes, ncclUint8, p, e->comm, s);
-      }
-      if (ct.rx[p]) {
-        ncclRecv(sd.rx_reqs + o, ct.rx[p] * sizeof(SyncReq), ncclUint8, p, e->comm, s);
-        ncclRecv(sd.rx_rows + o * e->n, ct.rx[p] * row_bytes, ncclUint8, p, e->comm, s);
-      }
-      o += ct.rx[p];
-    }
-    if (nccl_ok(ncclGroupEnd()) != SWIM_OK) return SWIM_EDEVICE;
-    sd.n_rx_reqs = (uint32_t)o;
-    return SWIM_OK;
-  }
-  std::vector<PackPlan> plans(W);
-  for (uint32_t r = 0; r < W; ++r)
-    if (int32_t rc = pack_rows(e, e->sh[r], r, kind, ct, &plans[r])) return rc;
-  for (uint32_t d = 0; d < W; ++d) {
-    Shard& dst = e->sh[d];
-    size_t nr = 0;
-    for (uint32_t r = 0; r < W; ++r) if (r != d) nr += ct.tx[r][d];
-    if (!dst.grow(&dst.rx_reqs, &dst.rx_req_cap, nr) || !dst.grow(&dst.rx_rows, &dst.rx_row_cap, nr * e->n))
-      return SWIM_ENOMEM;
-    size_t o = 0;
-    for (uint32_t r = 0; r < W; ++r) {
-      if (r == d || !ct.tx[r][d]) continue;
-      Shard& src = e->sh[r];
-      const SyncReq* tx = kind == 1 ? src.b.tx_reqs : src.b.tx_acks;
-      hipMemcpyAsync(dst.rx_reqs + o, tx + (size_t)d * src.b.tx_req_cap, ct.tx[r][d] * sizeof(SyncReq),
-                     hipMemcpyDeviceToDevice, s);
-      hipMemcpyAsync(dst.rx_rows + o * e->n, src.tx_rows + (size_t)plans[r].off[d] * e->n, ct.tx[r][d] * row_bytes,
-                     hipMemcpyDeviceToDevice, s);
-      o += ct.tx[r][d];
-    }
-    dst.n_rx_reqs = (uint32_t)o;
-  }
+  for (Shard& sd : e->sh) k_gather_counts<<<1, 64, 0, s>>>(sd.d_par, e->T, (int)kind);
   return SWIM_OK;
 }
 
@@ -486,19 +334,11 @@ static Ctx sync_ctx(Shard& sd) {  // list inserts of the SYNC phase use the seco
   return cd;
 }
 
-static void bind_rx(Shard& sd) {
-  sd.b.rx_msgs = sd.rx_msgs;
-  sd.b.rx_reqs = sd.rx_reqs;
-  sd.b.rx_rows = sd.rx_rows;
-  sd.b.rx_stops = sd.rx_stops;
-}
-
 // Upload the shard's launch parameters when any field differs from the image the device holds.
 // Uploads go through a pinned staging ring on the engine's stream, so they are ordered with the
 // kernels; the ring wraps only after a stream synchronisation.
 constexpr uint32_t kParRing = 64;
 static void sync_params(swim_engine* e, Shard& sd) {
-  bind_rx(sd);
   Params p;
   std::memset(&p, 0, sizeof p);
   p.c = sd.c;
@@ -576,7 +416,6 @@ static int32_t run_tick(swim_engine* e) {
   const bool gossip_tick = e->g_residue[e->T % e->G] != 0;
   for (Shard& sd : e->sh) {
     sd.c.T = e->T;
-    sd.n_rx_msgs = sd.n_rx_reqs = sd.n_rx_stops = 0;
     sync_params(e, sd);
   }
   if (!e->joins.empty()) {
@@ -608,12 +447,12 @@ static int32_t run_tick(swim_engine* e) {
   }
   if (gossip_tick || e->sh[0].c.delay_on) {
     if (multi)
-      if (int32_t rc = exchange_msgs(e)) return rc;
+      if (int32_t rc = exchange_counts(e, XK_MSG)) return rc;
     for (Shard& sd : e->sh) {
-      if (multi) sync_params(e, sd);
-      if (sd.n_rx_msgs)
-        k_recv_msgs<<<std::min<uint32_t>(grid_for(sd.n_rx_msgs, 256), 1024), 256, 0, s>>>(sd.d_par, T, sd.n_rx_msgs);
-      TICK_CHECK("k_recv_msgs");
+      if (multi) {
+        k_recv_msgs<<<kRecvGrid, 256, 0, s>>>(sd.d_par, T);
+        TICK_CHECK("k_recv_msgs");
+      }
       // at least kDeliverGrid workgroups: big inboxes are delivered a wave each, grid-stride
       k_gossip_deliver<<<std::max<uint32_t>(kDeliverGrid, grid_for(sd.c.nl, DLV_BLOCK)), DLV_BLOCK, 0, s>>>(sd.d_par, T, 1);
       TICK_CHECK("k_gossip_deliver");  // (also applies the phase's pingMembers inserts)
@@ -622,13 +461,22 @@ static int32_t run_tick(swim_engine* e) {
   // ---- D: SYNC / SYNC_ACK
   // (SYNC requests were collected by k_gossip_deliver on gossip ticks, by k_fd on the others)
   for (int d2 = 0; d2 < 2; ++d2) {
-    if (multi)
-      if (int32_t rc = exchange_sync(e, 1 + d2)) return rc;
+    if (multi) {
+      for (Shard& sd : e->sh) {
+        k_pack_rows<<<kPackGrid, 256, 0, s>>>(sd.d_par, T, d2);
+        TICK_CHECK("k_pack_rows");
+      }
+      if (int32_t rc = exchange_counts(e, d2 ? XK_ACK : XK_REQ)) return rc;
+    }
     for (Shard& sd : e->sh) {
-      if (multi) sync_params(e, sd);
-      if (sd.n_rx_reqs)
-        k_recv_sync<<<std::min<uint32_t>(grid_for(sd.n_rx_reqs, 256), 256), 256, 0, s>>>(sd.d_par, T, d2, sd.n_rx_reqs);
-      TICK_CHECK("k_recv_sync");
+      if (multi) {
+        k_recv_sync<<<256, 256, 0, s>>>(sd.d_par, T, d2);
+        TICK_CHECK("k_recv_sync");
+        if (e->rccl) {
+          k_pull_rows<<<kPackGrid, 256, 0, s>>>(sd.d_par, T, d2);
+          TICK_CHECK("k_pull_rows");
+        }
+      }
       // SYNC_ACK: an unsharded engine classifies its acks inside k_sync_apply (every ack is local,
       // and almost all reuse the SYNC launch's reverse classification); a sharded one streams the
       // acks that arrived with their rows from other shards
@@ -641,8 +489,8 @@ static int32_t run_tick(swim_engine* e) {
   }
   for (Shard& sd : e->sh) {
     // ---- end of tick (also zeroes the per-tick counters and applies other shards' stops)
-    const uint32_t ge = grid_for(std::max<uint32_t>(std::max<uint32_t>(sd.c.nl, sd.n_rx_stops), 64), 256);
-    k_end_tick<<<ge, REB_BLOCK, 0, s>>>(sd.d_par, T, sd.n_rx_stops, (T % kRebaseEvery) == 0 ? 1 : 0);
+    const uint32_t ge = grid_for(std::max<uint32_t>(sd.c.nl, 64), 256);
+    k_end_tick<<<ge, REB_BLOCK, 0, s>>>(sd.d_par, T, (T % kRebaseEvery) == 0 ? 1 : 0);
     TICK_CHECK("k_end_tick");
   }
   return SWIM_OK;
@@ -811,6 +659,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.tx_msg_cap = multi ? (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 256ull * e->sz)) : 0;
   b.tx_req_cap = multi ? b.req_cap : 0;
   b.tx_stop_cap = multi ? kStopCap : 0;
+  // content rows one shard may send in one SYNC (or SYNC_ACK) exchange: 256 MiB of rows, 64..4,096
+  b.row_cap = multi ? std::min<uint32_t>(4096, std::max<uint32_t>(64, (1u << 26) / std::max(n, 1u))) : 0;
 
   const size_t nn = (size_t)nl * n;
   c.blocks = (n + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
@@ -857,9 +707,33 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&b.rev_chunk, (size_t)b.req_cap * b.chunks) && sd.alloc(&b.rev_total, b.req_cap) &&
             sd.alloc(&b.row_mod, nl) &&
             sd.alloc(&b.pend, (size_t)kApplyGrid * n) && sd.alloc(&sd.d_par, 1) && sd.alloc(&b.senders, nl);
-  if (ok && multi)
-    ok = sd.alloc(&b.tx_msgs, (size_t)e->world * b.tx_msg_cap) && sd.alloc(&b.tx_reqs, (size_t)e->world * b.tx_req_cap) &&
-         sd.alloc(&b.tx_acks, (size_t)e->world * b.tx_req_cap) && sd.alloc(&b.tx_stops, b.tx_stop_cap);
+  if (ok && multi) {
+    // the producer side of the exchange, one region (one IPC handle); with RCCL it is uncached, so
+    // the producers' stores reach HBM, where the peers' system-scope loads over xGMI read them
+    const size_t W = (size_t)e->world, rows = (size_t)b.row_cap * n * 4;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    const size_t o_msgs = take(W * b.tx_msg_cap * sizeof(GMsgFull)), o_reqs = take(W * b.tx_req_cap * sizeof(SyncReq)),
+                 o_acks = take(W * b.tx_req_cap * sizeof(SyncReq)), o_stops = take(4ull * b.tx_stop_cap),
+                 o_rows0 = take(rows), o_rows1 = take(rows);
+    sd.xreg_bytes = off;
+    hipError_t r = hipErrorUnknown;
+    if (e->rccl) r = hipExtMallocWithFlags(&sd.xreg, off, hipDeviceMallocUncached);
+    if (r != hipSuccess) r = hipMalloc(&sd.xreg, off);
+    ok = r == hipSuccess;
+    if (ok) {
+      char* base = static_cast<char*>(sd.xreg);
+      b.tx_msgs = reinterpret_cast<GMsgFull*>(base + o_msgs);
+      b.tx_reqs = reinterpret_cast<SyncReq*>(base + o_reqs);
+      b.tx_acks = reinterpret_cast<SyncReq*>(base + o_acks);
+      b.tx_stops = reinterpret_cast<uint32_t*>(base + o_stops);
+      b.tx_rows[0] = reinterpret_cast<uint32_t*>(base + o_rows0);
+      b.tx_rows[1] = reinterpret_cast<uint32_t*>(base + o_rows1);
+      ok = sd.alloc(&b.rx_cnt, 4 * MAXW) && sd.alloc(&b.rx_stops, W * b.tx_stop_cap) && sd.alloc(&b.rx_stop_n, 1) &&
+           sd.alloc(&sd.peers, 1);
+      b.peers = sd.peers;
+    }
+  }
   if (!ok) return SWIM_ENOMEM;
   sd.links_dev_cap = 1;
   c.ins_total = &sd.k->ins_total;
@@ -898,6 +772,10 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(c.err, 0, 4, s);
   hipMemsetAsync(sd.k, 0, sizeof(Counters), s);
   hipMemsetAsync(sd.x, 0, sizeof(Xc), s);
+  if (multi) {
+    hipMemsetAsync(b.rx_cnt, 0, 4 * MAXW * sizeof(uint32_t), s);
+    hipMemsetAsync(b.rx_stop_n, 0, sizeof(uint32_t), s);
+  }
   hipMemsetAsync(b.msg_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.pg_tab, 0xff, 4 * (size_t)std::max(nl, 1u) * b.pg_max, s);
   hipMemsetAsync(b.big_tick, 0, 4 * (size_t)nl, s);
@@ -916,6 +794,73 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
     k_init_members<<<grid_for(nl, 64), 64, 0, s>>>(c, n_initial, cf.sync_stagger, cf.timer_stagger);
   }
   return SWIM_OK;
+}
+
+// offsets of the producer buffers inside a shard's exchange region (identical on every rank)
+static size_t xoff(const Shard& sd, const void* p) {
+  return (size_t)(static_cast<const char*>(p) - static_cast<const char*>(sd.xreg));
+}
+
+// A local group: every shard reads the other shards' buffers directly.
+static int32_t setup_peers_local(swim_engine* e) {
+  for (Shard& sd : e->sh) {
+    Peers ph{};
+    for (uint32_t p = 0; p < (uint32_t)e->world; ++p) {
+      const Bufs& pb = e->sh[p].b;
+      ph.msgs[p] = pb.tx_msgs;
+      ph.hdr[0][p] = pb.tx_reqs;
+      ph.hdr[1][p] = pb.tx_acks;
+      ph.stops[p] = pb.tx_stops;
+      for (int k = 0; k < 2; ++k) ph.rows[k][p] = ph.rows_in[k][p] = pb.tx_rows[k];
+      ph.x[p] = e->sh[p].x;
+    }
+    if (hipMemcpy(sd.peers, &ph, sizeof ph, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
+  }
+  return SWIM_OK;
+}
+
+// RCCL: every rank maps the other ranks' exchange regions (IPC handles gathered with ncclAllGather)
+// and pulls what they produced for it into rx_rows over xGMI (k_pull_rows).
+static int32_t setup_peers_rccl(swim_engine* e) {
+  Shard& sd = e->sh[0];
+  const uint32_t W = (uint32_t)e->world, me = (uint32_t)e->rank;
+  hipIpcMemHandle_t mine;
+  if (hipIpcGetMemHandle(&mine, sd.xreg) != hipSuccess) return SWIM_EDEVICE;
+  uint8_t* d_h = nullptr;
+  if (hipMalloc((void**)&d_h, sizeof(hipIpcMemHandle_t) * (W + 1)) != hipSuccess) return SWIM_ENOMEM;
+  std::vector<hipIpcMemHandle_t> all(W);
+  int32_t rc = SWIM_OK;
+  if (hipMemcpy(d_h + sizeof(hipIpcMemHandle_t) * W, &mine, sizeof mine, hipMemcpyHostToDevice) != hipSuccess ||
+      nccl_ok(ncclAllGather(d_h + sizeof(hipIpcMemHandle_t) * W, d_h, sizeof(hipIpcMemHandle_t), ncclUint8, e->comm,
+                            e->stream)) != SWIM_OK ||
+      hipStreamSynchronize(e->stream) != hipSuccess ||
+      hipMemcpy(all.data(), d_h, sizeof(hipIpcMemHandle_t) * W, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = SWIM_EDEVICE;
+  hipFree(d_h);
+  if (rc) return rc;
+  Peers ph{};
+  for (int k = 0; k < 2; ++k) {
+    if (!sd.alloc(&ph.rx_rows[k], (size_t)W * sd.b.row_cap * e->n)) return SWIM_ENOMEM;
+  }
+  for (uint32_t p = 0; p < W; ++p) {
+    char* base = static_cast<char*>(sd.xreg);
+    if (p != me) {
+      void* q = nullptr;
+      if (hipIpcOpenMemHandle(&q, all[p], hipIpcMemLazyEnablePeerAccess) != hipSuccess) return SWIM_EDEVICE;
+      sd.ipc_open.push_back(q);
+      base = static_cast<char*>(q);
+    }
+    ph.msgs[p] = reinterpret_cast<const GMsgFull*>(base + xoff(sd, sd.b.tx_msgs));
+    ph.hdr[0][p] = reinterpret_cast<const SyncReq*>(base + xoff(sd, sd.b.tx_reqs));
+    ph.hdr[1][p] = reinterpret_cast<const SyncReq*>(base + xoff(sd, sd.b.tx_acks));
+    ph.stops[p] = reinterpret_cast<const uint32_t*>(base + xoff(sd, sd.b.tx_stops));
+    for (int k = 0; k < 2; ++k) {
+      ph.rows[k][p] = reinterpret_cast<const uint32_t*>(base + xoff(sd, sd.b.tx_rows[k]));
+      ph.rows_in[k][p] = ph.rx_rows[k] + (size_t)p * sd.b.row_cap * e->n;
+    }
+    ph.x[p] = nullptr;
+  }
+  return hipMemcpy(sd.peers, &ph, sizeof ph, hipMemcpyHostToDevice) == hipSuccess ? SWIM_OK : SWIM_EDEVICE;
 }
 
 static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t n_initial, uint64_t seed, int32_t rank,
@@ -967,8 +912,7 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
   }
   if (hipHostMalloc((void**)&e->h_par, sizeof(Params) * kParRing) != hipSuccess) { delete e; return SWIM_ENOMEM; }
   if (world > 1) {
-    if (hipMalloc((void**)&e->d_cnt, sizeof(uint32_t) * 2 * MAXW) != hipSuccess ||
-        hipHostMalloc((void**)&e->h_cnt, sizeof(uint32_t) * 2 * MAXW + sizeof(Xc)) != hipSuccess) {
+    if (hipMalloc((void**)&e->d_cnt, sizeof(uint32_t) * 2) != hipSuccess) {
       delete e;
       return SWIM_ENOMEM;
     }
@@ -978,6 +922,10 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
     ncclUniqueId id;
     std::memcpy(&id, comm_id, sizeof(id));
     if (nccl_ok(ncclCommInitRank(&e->comm, world, id, rank)) != SWIM_OK) { delete e; return SWIM_EDEVICE; }
+  }
+  if (world > 1) {
+    const int32_t rc = rccl ? setup_peers_rccl(e) : setup_peers_local(e);
+    if (rc != SWIM_OK) { delete e; return rc; }
   }
   e->g_residue.assign(e->G, cf.timer_stagger ? 1 : 0);  // staggered gossip timers use every residue
   e->g_residue[0] = 1;

@@ -36,6 +36,24 @@ struct Xc {
   uint32_t pad[3];
 };
 
+// Where this shard reads what the other shards produced for it.  Device pointers: a
+// local group's peers are the other shards in this process; with RCCL they are the peers' exchange
+// buffers mapped over xGMI (hipIpcOpenMemHandle), read with system-scope loads after the exchange's
+// count collective, which no rank leaves before every rank's producers have finished.
+struct Peers {
+  const GMsgFull* msgs[MAXW];        // peer p's tx_msgs ([world][tx_msg_cap])
+  const SyncReq* hdr[2][MAXW];       // peer p's tx_reqs / tx_acks ([world][tx_req_cap])
+  const uint32_t* stops[MAXW];       // peer p's tx_stops
+  const uint32_t* rows[2][MAXW];     // peer p's packed SYNC / SYNC_ACK content rows ([row_cap][n])
+  const uint32_t* rows_in[2][MAXW];  // where content rows from p are read: p's rows (local group) or
+                                     // this shard's pulled copy (RCCL)
+  uint32_t* rx_rows[2];              // RCCL: the pulled copies, [world][row_cap][n]
+  const Xc* x[MAXW];                 // local group: peer counters (RCCL: the counts arrive in rx_cnt)
+};
+// rx_cnt[kind][p]: what peer p produced for this shard this tick (kind 0 GOSSIP_REQs, 1 SYNCs,
+// 2 SYNC_ACKs) and, kind 3, its completed graceful leaves (broadcast)
+enum : uint32_t { XK_MSG = 0, XK_REQ = 1, XK_ACK = 2, XK_STOP = 3 };
+
 constexpr uint32_t DQ_BUCKETS = 2048, DQ_MASK = DQ_BUCKETS - 1;  // delay ring (> SWIM_DELAY_TICKS_MAX)
 static_assert(DQ_BUCKETS > SWIM_DELAY_TICKS_MAX, "a delayed message must not land in the current bucket");
 
@@ -50,10 +68,12 @@ struct Bufs {
   uint32_t tx_req_cap;
   uint32_t* tx_stops; // members whose graceful leave completed this tick (broadcast)
   uint32_t tx_stop_cap;
-  const GMsgFull* rx_msgs;
-  const SyncReq* rx_reqs;
-  const uint32_t* rx_rows;  // record rows of received SYNC / SYNC_ACKs, indexed by SyncReq.content
-  const uint32_t* rx_stops;
+  uint32_t* tx_rows[2];  // [row_cap][n] content rows of the outgoing SYNCs / SYNC_ACKs (k_pack_rows)
+  uint32_t row_cap;
+  const Peers* peers;
+  uint32_t* rx_cnt;      // [4][MAXW] (XK_*)
+  uint32_t* rx_stops;    // [world * tx_stop_cap] other shards' completed leaves, applied by k_end_tick
+  uint32_t* rx_stop_n;   // how many (zeroed by k_fd, set by k_recv_msgs)
   // paged gossip inboxes (inbox_page): message k of receiver i's round is pg_msgs[pg_tab[i][k / 64]][k % 64]
   GMsgFull* pg_msgs;   // [pg_cap][64]
   uint32_t* pg_perm;   // [pg_cap][64] big inboxes: canonical rank -> inbox position, same paging
@@ -815,6 +835,7 @@ __global__ void __launch_bounds__(256) k_fd(KP, int gossip, int collect) {
   const Ctx c = pctx(P, T);
   __shared__ uint32_t s_list[256];
   __shared__ uint32_t s_cnt;
+  if (c.world > 1 && blockIdx.x == 0 && threadIdx.x == 0) *P->b.rx_stop_n = 0;  // no leaves received yet
   timers_block(c, T);  // phase A for this block's viewers
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
@@ -900,20 +921,90 @@ __global__ void __launch_bounds__(256) k_dq_release(KP) {
   }
 }
 
-// GOSSIP_REQs arriving from other shards join the local message list exactly as a local send does;
-// provable duplicates (the emitter could not see this shard's collectors) are flagged, and delivery
-// skips them: the collector holds the sequence id, so onGossipReq would return at once
-__global__ void k_recv_msgs(KP, uint32_t nrx) {
+// ------------------------------------------------------------------------------- exchange
+// A system-scope load: coherent with another GPU's finished stores (exchange buffers over xGMI; in a
+// local group it is an ordinary load of this device's memory that bypasses nothing it needs).
+template <typename T>
+__device__ __forceinline__ T ld_peer(const T* p) {
+  static_assert(sizeof(T) % 8 == 0, "8-byte granules");
+  T v;
+  const uint64_t* s = reinterpret_cast<const uint64_t*>(p);
+  uint64_t* d = reinterpret_cast<uint64_t*>(&v);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 8); ++i) d[i] = __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return v;
+}
+__device__ __forceinline__ uint32_t ld_peer_u32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// What each peer produced for this shard this tick, clamped to the exchange capacity, and its total.
+struct PeerCounts {
+  uint32_t n[MAXW];
+  uint32_t total;
+};
+__device__ __forceinline__ PeerCounts peer_counts(const Ctx& c, const Bufs& b, uint32_t kind, uint32_t cap) {
+  PeerCounts pc;
+  pc.total = 0;
+  for (uint32_t p = 0; p < (uint32_t)MAXW; ++p) {
+    const uint32_t k = p < c.world && p != c.rank ? min(b.rx_cnt[kind * MAXW + p], cap) : 0u;
+    pc.n[p] = k;
+    pc.total += k;
+  }
+  return pc;
+}
+// flat index i < pc.total -> (peer, index among that peer's items)
+__device__ __forceinline__ uint32_t peer_of(const PeerCounts& pc, uint32_t& i) {
+  uint32_t p = 0;
+  while (i >= pc.n[p]) { i -= pc.n[p]; ++p; }
+  return p;
+}
+
+// Local group only: the counts each peer shard produced for this one (what ncclAllToAll /
+// ncclAllGather deliver to a rank), read from the peers' counters.
+__global__ void k_gather_counts(KP, int kind) {
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
+  const uint32_t p = threadIdx.x;
+  if (p >= (uint32_t)MAXW) return;
+  uint32_t n = 0, stop = 0;
+  if (p < c.world && p != c.rank) {
+    const Xc& x = *b.peers->x[p];
+    n = kind == XK_MSG ? x.msg[c.rank] : kind == XK_REQ ? x.req[c.rank] : x.ack[c.rank];
+    stop = x.stop;
+  }
+  b.rx_cnt[kind * MAXW + p] = n;
+  if (kind == XK_MSG) b.rx_cnt[XK_STOP * MAXW + p] = stop;
+}
+
+// E1: GOSSIP_REQs other shards produced for receivers owned here join the inboxes exactly as a local
+// send does (read straight from the producers' tx buffers); provable duplicates (the emitter could
+// not see this shard's collectors) are flagged, and delivery skips them: the collector holds the
+// sequence id, so onGossipReq would return at once.  Workgroup 0 also takes the peers' completed
+// graceful leaves (k_end_tick applies them).  The work size is read on the device: a fixed grid.
+__global__ void k_recv_msgs(KP) {
+  const Ctx c = pctx(P, T);
+  const Bufs b = P->b;
+  const Peers* pr = b.peers;
+  if (blockIdx.x == 0) {
+    const PeerCounts ps = peer_counts(c, b, XK_STOP, b.tx_stop_cap);
+    uint32_t o = 0;
+    for (uint32_t p = 0; p < c.world; ++p) {
+      for (uint32_t j = threadIdx.x; j < ps.n[p]; j += blockDim.x) b.rx_stops[o + j] = ld_peer_u32(pr->stops[p] + j);
+      o += ps.n[p];
+    }
+    if (threadIdx.x == 0) *b.rx_stop_n = o;
+  }
+  const PeerCounts pc = peer_counts(c, b, XK_MSG, b.tx_msg_cap);
   // wave-uniform trip count: every lane of a wave takes part in each deliver_local_msg call
   const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); i0 < nrx; i0 += gridDim.x * blockDim.x) {
-    const uint32_t i = i0 + lane;
-    const bool valid = i < nrx;
+  for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); i0 < pc.total; i0 += gridDim.x * blockDim.x) {
+    uint32_t i = i0 + lane;
+    const bool valid = i < pc.total;
     GMsgFull msg{};
     if (valid) {
-      msg = b.rx_msgs[i];
+      const uint32_t p = peer_of(pc, i);
+      msg = ld_peer(pr->msgs[p] + (size_t)c.rank * b.tx_msg_cap + i);
       // kept (flagged) so that each (sender, receiver) pair's pseq stays dense for deliver_big
       msg.dup = coll_contains(c, coll_find(c, msg.to, msg.gossiper), msg.seq) ? 1u : 0u;
     }
@@ -1650,11 +1741,10 @@ __device__ void rebase_witness(const Ctx& c) {
 }
 
 // start0's doFinally (:285-289) for members that joined this tick; graceful leaves complete.
-__global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, uint32_t n_rx_stops, int rebase) {
+__global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
   const Ctx c = pctx(P, T);
   Counters* k = P->b.k;
   Xc* x = P->c.world > 1 ? P->b.x : nullptr;
-  const uint32_t* rx_stops = P->b.rx_stops;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (rebase) rebase_witness(c);
   {  // this tick's content snapshots are released; the next tick's slot counter starts at zero
@@ -1703,7 +1793,10 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, uint32_t n_rx_stops,
   // every other kernel of the tick has completed: reset the per-tick scratch counters
   if (i < sizeof(Counters) / 4) reinterpret_cast<uint32_t*>(k)[i] = 0;
   if (x && i < sizeof(Xc) / 4) reinterpret_cast<uint32_t*>(x)[i] = 0;
-  if (i < n_rx_stops) c.up[rx_stops[i]] = 0;  // graceful leaves completed on other shards
+  if (x) {  // graceful leaves completed on other shards (k_recv_msgs took them)
+    const uint32_t ns = *P->b.rx_stop_n;
+    for (uint32_t q = i; q < ns; q += gridDim.x * blockDim.x) c.up[P->b.rx_stops[q]] = 0;
+  }
   if (i >= c.nl) return;
   const uint32_t fl = c.mflag[i];
   if (!(fl & (MF_JOIN | MF_LEAVE))) return;

@@ -58,42 +58,36 @@ __device__ inline bool sync_complex(uint32_t r1, uint32_t r0, bool self) {
   return true;
 }
 
-// SYNCs / SYNC_ACKs arriving from other shards (content row = rx_rows[k]) join their inboxes
-// (wave-uniform trip count: enqueue_sync's page discipline wants every lane of the wave)
-__global__ void k_recv_sync(KP, int d2, uint32_t nrx) {
-  const Ctx c = pctx_sync(P, T);
-  const Bufs b = P->b;
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t k0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); k0 < nrx; k0 += gridDim.x * blockDim.x) {
-    const uint32_t k = k0 + lane;
-    SyncReq q{};
-    if (k < nrx) {
-      q = b.rx_reqs[k];
-      q.content = k;
-    }
-    enqueue_sync(c, b, d2, q, k < nrx);
-  }
-}
-
-// content rows of this shard's outgoing SYNC / SYNC_ACKs, packed per destination in tx order (the
-// sender's table when the message is prepared, prepareSyncDataMsg :485-489)
-struct PackPlan {
-  uint32_t cnt[MAXW];
-  uint32_t off[MAXW];  // first packed row of destination d
-};
-// Packed rows are copied in 16-KiB chunks, one workgroup per (row, chunk): a handful of 256-KiB
-// rows per exchange would otherwise leave most CUs idle (one workgroup per row ran at ~2 GB/s).
+// E2 / E3.  The content rows of this shard's outgoing SYNCs (d2 = 0) / SYNC_ACKs (d2 = 1) — the
+// sender's table when the message is prepared (prepareSyncDataMsg :485-489) — are packed per
+// destination in tx order into tx_rows[d2]; each header learns its row (SyncReq.content), which is
+// how the receiver finds it.  Offsets come from this shard's own counters: no host round trip.
+// Rows are copied in 16-KiB chunks, one workgroup per (row, chunk): a handful of 256-KiB rows per
+// exchange would otherwise leave most CUs idle.
 constexpr uint32_t PACK_CHUNK = 4096;  // record words per unit
-__global__ void __launch_bounds__(256) k_pack_rows(Ctx c, const SyncReq* tx, uint32_t tx_cap, PackPlan plan,
-                                                   uint32_t tot, uint32_t* out) {
+__global__ void __launch_bounds__(256) k_pack_rows(KP, int d2) {
+  const Ctx c = pctx(P, T);
+  const Bufs b = P->b;
+  SyncReq* tx = d2 ? b.tx_acks : b.tx_reqs;
+  const uint32_t* cnt = d2 ? b.x->ack : b.x->req;
+  uint32_t n[MAXW], total = 0;
+  for (uint32_t d = 0; d < (uint32_t)MAXW; ++d) {
+    n[d] = d < c.world && d != c.rank ? min(cnt[d], b.tx_req_cap) : 0u;
+    total += n[d];
+  }
+  if (total > b.row_cap && blockIdx.x == 0 && threadIdx.x == 0) set_err(c, ERR_REQS);
   const uint32_t per_row = (c.n + PACK_CHUNK - 1) / PACK_CHUNK;
-  for (uint32_t u = blockIdx.x; u < tot * per_row; u += gridDim.x) {
+  uint32_t* out = b.tx_rows[d2];
+  for (uint32_t u = blockIdx.x; u < total * per_row; u += gridDim.x) {
     const uint32_t row = u / per_row, ch = u - row * per_row;
-    uint32_t d = 0;  // destination of packed row `row` (plan.off is the running sum of plan.cnt)
-    while (d + 1 < c.world && row >= plan.off[d] + plan.cnt[d]) ++d;
-    const SyncReq q = tx[(size_t)d * tx_cap + (row - plan.off[d])];
+    uint32_t k = row, d = 0;
+    while (k >= n[d]) { k -= n[d]; ++d; }
+    SyncReq* q = tx + (size_t)d * b.tx_req_cap + k;
+    const bool fits = row < b.row_cap;
+    if (ch == 0 && threadIdx.x == 0) q->content = fits ? row : NONE;
+    if (!fits) continue;
     const uint32_t x0 = ch * PACK_CHUNK, len = min(PACK_CHUNK, c.n - x0);
-    const uint32_t* src = rec_row(c, q.from) + x0;
+    const uint32_t* src = rec_row(c, q->from) + x0;
     uint32_t* dst = out + (size_t)row * c.n + x0;
     if (c.n & 3) {  // rows are only 4-B aligned
       for (uint32_t x = threadIdx.x; x < len; x += blockDim.x) dst[x] = src[x];
@@ -105,9 +99,68 @@ __global__ void __launch_bounds__(256) k_pack_rows(Ctx c, const SyncReq* tx, uin
   }
 }
 
+// SYNCs / SYNC_ACKs other shards sent to receivers owned here join their inboxes; a message's
+// content row is row `content` of the sender's shard p: SyncReq.content = p * row_cap + content
+// (wave-uniform trip count: enqueue_sync's page discipline wants every lane of the wave)
+__global__ void k_recv_sync(KP, int d2) {
+  const Ctx c = pctx_sync(P, T);
+  const Bufs b = P->b;
+  const PeerCounts pc = peer_counts(c, b, d2 ? XK_ACK : XK_REQ, b.tx_req_cap);
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t k0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); k0 < pc.total; k0 += gridDim.x * blockDim.x) {
+    uint32_t k = k0 + lane;
+    SyncReq q{};
+    bool valid = k < pc.total;
+    if (valid) {
+      const uint32_t p = peer_of(pc, k);
+      q = ld_peer(b.peers->hdr[d2][p] + (size_t)c.rank * b.tx_req_cap + k);
+      valid = q.content != NONE;  // its row did not fit the sender's tx_rows (ERR_REQS is set there)
+      q.content = p * b.row_cap + q.content;
+    }
+    enqueue_sync(c, b, d2, q, valid);
+  }
+}
+
+// RCCL only: the content rows other ranks packed for this one, pulled over xGMI into rx_rows[d2]
+// (row p * row_cap + content), one workgroup per (row, chunk)
+__global__ void __launch_bounds__(256) k_pull_rows(KP, int d2) {
+  const Ctx c = pctx(P, T);
+  const Bufs b = P->b;
+  const Peers* pr = b.peers;
+  const PeerCounts pc = peer_counts(c, b, d2 ? XK_ACK : XK_REQ, b.tx_req_cap);
+  const uint32_t per_row = (c.n + PACK_CHUNK - 1) / PACK_CHUNK;
+  for (uint32_t u = blockIdx.x; u < pc.total * per_row; u += gridDim.x) {
+    uint32_t k = u / per_row;
+    const uint32_t ch = u - k * per_row;
+    const uint32_t p = peer_of(pc, k);
+    const uint32_t row = ld_peer_u32(&pr->hdr[d2][p][(size_t)c.rank * b.tx_req_cap + k].content);
+    if (row >= b.row_cap) continue;
+    const uint32_t x0 = ch * PACK_CHUNK, len = min(PACK_CHUNK, c.n - x0);
+    const uint32_t* src = pr->rows[d2][p] + (size_t)row * c.n + x0;
+    uint32_t* dst = pr->rx_rows[d2] + ((size_t)p * b.row_cap + row) * c.n + x0;
+    if (c.n & 1) {  // rows are only 4-B aligned
+      for (uint32_t x = threadIdx.x; x < len; x += blockDim.x) dst[x] = ld_peer_u32(src + x);
+    } else {
+      const uint64_t* s8 = reinterpret_cast<const uint64_t*>(src);
+      uint64_t* d8 = reinterpret_cast<uint64_t*>(dst);
+      for (uint32_t x = threadIdx.x; x < len / 2; x += blockDim.x) d8[x] = ld_peer(s8 + x);
+    }
+  }
+}
+
+// where a received message's content row is: row `content % row_cap` of shard content / row_cap.
+// Also evaluated for the speculative header of no message (classify's look-ahead), whose content
+// is arbitrary: only arithmetic on such a pointer, which is never read, so no load may fault.
+__device__ __forceinline__ const uint32_t* remote_row(const Ctx& c, const Bufs& b, int d2, uint32_t content) {
+  if (!b.peers) return c.recs;  // unsharded: nothing arrives from other shards
+  const uint32_t p = content / b.row_cap;
+  if (p >= (uint32_t)MAXW) return c.recs;
+  return b.peers->rows_in[d2][p] + (size_t)(content - p * b.row_cap) * c.n;
+}
+
 // the record row a SYNC / SYNC_ACK carries: received copy, snapshot, or the sender's live row
 __device__ __forceinline__ const uint32_t* sync_content(const Ctx& c, const Bufs& b, const SyncReq& q, int d2) {
-  if (q.content != NONE) return b.rx_rows + (size_t)q.content * c.n;
+  if (q.content != NONE) return remote_row(c, b, d2, q.content);
   const uint32_t si = (d2 ? b.ack_snap : b.snap_idx)[q.from - c.lo];
   return si < b.snap_cap ? b.snap + (size_t)si * c.n : rec_row(c, q.from);
 }
@@ -143,7 +196,7 @@ __device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SyInb
   SyncReq q = p.items[i];
   q.from = uni(q.from); q.to = uni(q.to); q.content = uni(q.content); q.pad = uni(q.pad);
   const bool remote = q.content != NONE;
-  h.content = remote ? b.rx_rows + (size_t)q.content * c.n : rec_row(c, q.from);
+  h.content = remote ? remote_row(c, b, d2, q.content) : rec_row(c, q.from);
   h.rv = rec_row(c, q.to);
   h.bdc = remote ? nullptr : c.bdiff + (size_t)(q.from - c.lo) * c.blocks;
   h.bdv = c.bdiff + (size_t)(q.to - c.lo) * c.blocks;
