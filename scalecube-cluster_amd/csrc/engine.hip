@@ -584,6 +584,34 @@ __global__ void k_spread(Ctx c, uint32_t v, uint32_t payload) {
   spread_user(c, v, payload);
 }
 
+// The producer side of a shard's exchange, one region (one IPC handle): tx_msgs, tx_reqs, tx_acks,
+// tx_stops, tx_rows[2], at offsets that are the same on every rank.  With RCCL it is uncached, so the
+// producers' stores land in HBM, where the peers' system-scope loads over xGMI read them.
+static int32_t alloc_xreg(swim_engine* e, Shard& sd, bool uncached) {
+  Bufs& b = sd.b;
+  const size_t W = (size_t)e->world, rows = (size_t)b.row_cap * e->n * 4;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+  const size_t o_msgs = take(W * b.tx_msg_cap * sizeof(GMsgFull)), o_reqs = take(W * b.tx_req_cap * sizeof(SyncReq)),
+               o_acks = take(W * b.tx_req_cap * sizeof(SyncReq)), o_stops = take(4ull * b.tx_stop_cap),
+               o_rows0 = take(rows), o_rows1 = take(rows);
+  if (sd.xreg) hipFree(sd.xreg);
+  sd.xreg = nullptr;
+  sd.xreg_bytes = off;
+  hipError_t r = hipErrorUnknown;
+  if (uncached) r = hipExtMallocWithFlags(&sd.xreg, off, hipDeviceMallocUncached);
+  if (r != hipSuccess) r = hipMalloc(&sd.xreg, off);
+  if (r != hipSuccess) return SWIM_ENOMEM;
+  char* base = static_cast<char*>(sd.xreg);
+  b.tx_msgs = reinterpret_cast<GMsgFull*>(base + o_msgs);
+  b.tx_reqs = reinterpret_cast<SyncReq*>(base + o_reqs);
+  b.tx_acks = reinterpret_cast<SyncReq*>(base + o_acks);
+  b.tx_stops = reinterpret_cast<uint32_t*>(base + o_stops);
+  b.tx_rows[0] = reinterpret_cast<uint32_t*>(base + o_rows0);
+  b.tx_rows[1] = reinterpret_cast<uint32_t*>(base + o_rows1);
+  return SWIM_OK;
+}
+
 static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n_initial, uint64_t seed) {
   const swim_config& cf = e->cfg;
   Ctx& c = sd.c;
@@ -708,31 +736,9 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&b.row_mod, nl) &&
             sd.alloc(&b.pend, (size_t)kApplyGrid * n) && sd.alloc(&sd.d_par, 1) && sd.alloc(&b.senders, nl);
   if (ok && multi) {
-    // the producer side of the exchange, one region (one IPC handle); with RCCL it is uncached, so
-    // the producers' stores reach HBM, where the peers' system-scope loads over xGMI read them
-    const size_t W = (size_t)e->world, rows = (size_t)b.row_cap * n * 4;
-    size_t off = 0;
-    auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const size_t o_msgs = take(W * b.tx_msg_cap * sizeof(GMsgFull)), o_reqs = take(W * b.tx_req_cap * sizeof(SyncReq)),
-                 o_acks = take(W * b.tx_req_cap * sizeof(SyncReq)), o_stops = take(4ull * b.tx_stop_cap),
-                 o_rows0 = take(rows), o_rows1 = take(rows);
-    sd.xreg_bytes = off;
-    hipError_t r = hipErrorUnknown;
-    if (e->rccl) r = hipExtMallocWithFlags(&sd.xreg, off, hipDeviceMallocUncached);
-    if (r != hipSuccess) r = hipMalloc(&sd.xreg, off);
-    ok = r == hipSuccess;
-    if (ok) {
-      char* base = static_cast<char*>(sd.xreg);
-      b.tx_msgs = reinterpret_cast<GMsgFull*>(base + o_msgs);
-      b.tx_reqs = reinterpret_cast<SyncReq*>(base + o_reqs);
-      b.tx_acks = reinterpret_cast<SyncReq*>(base + o_acks);
-      b.tx_stops = reinterpret_cast<uint32_t*>(base + o_stops);
-      b.tx_rows[0] = reinterpret_cast<uint32_t*>(base + o_rows0);
-      b.tx_rows[1] = reinterpret_cast<uint32_t*>(base + o_rows1);
-      ok = sd.alloc(&b.rx_cnt, 4 * MAXW) && sd.alloc(&b.rx_stops, W * b.tx_stop_cap) && sd.alloc(&b.rx_stop_n, 1) &&
-           sd.alloc(&sd.peers, 1);
-      b.peers = sd.peers;
-    }
+    ok = alloc_xreg(e, sd, e->rccl) == SWIM_OK && sd.alloc(&b.rx_cnt, 4 * MAXW) &&
+         sd.alloc(&b.rx_stops, (size_t)e->world * b.tx_stop_cap) && sd.alloc(&b.rx_stop_n, 1) && sd.alloc(&sd.peers, 1);
+    b.peers = sd.peers;
   }
   if (!ok) return SWIM_ENOMEM;
   sd.links_dev_cap = 1;
@@ -825,7 +831,12 @@ static int32_t setup_peers_rccl(swim_engine* e) {
   Shard& sd = e->sh[0];
   const uint32_t W = (uint32_t)e->world, me = (uint32_t)e->rank;
   hipIpcMemHandle_t mine;
-  if (hipIpcGetMemHandle(&mine, sd.xreg) != hipSuccess) return SWIM_EDEVICE;
+  if (hipIpcGetMemHandle(&mine, sd.xreg) != hipSuccess) {
+    // no handle for an uncached allocation: an ordinary one (the consumers' loads are system-scope)
+    if (alloc_xreg(e, sd, false) != SWIM_OK) return SWIM_ENOMEM;
+    if (hipIpcGetMemHandle(&mine, sd.xreg) != hipSuccess) return SWIM_EDEVICE;
+    std::fprintf(stderr, "libswimgpu: rank %d: exchange region is cached (no IPC handle for uncached memory)\n", e->rank);
+  }
   uint8_t* d_h = nullptr;
   if (hipMalloc((void**)&d_h, sizeof(hipIpcMemHandle_t) * (W + 1)) != hipSuccess) return SWIM_ENOMEM;
   std::vector<hipIpcMemHandle_t> all(W);

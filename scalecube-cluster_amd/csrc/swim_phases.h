@@ -938,25 +938,22 @@ __device__ __forceinline__ uint32_t ld_peer_u32(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// What each peer produced for this shard this tick, clamped to the exchange capacity, and its total.
-struct PeerCounts {
-  uint32_t n[MAXW];
-  uint32_t total;
-};
-__device__ __forceinline__ PeerCounts peer_counts(const Ctx& c, const Bufs& b, uint32_t kind, uint32_t cap) {
-  PeerCounts pc;
-  pc.total = 0;
-  for (uint32_t p = 0; p < (uint32_t)MAXW; ++p) {
-    const uint32_t k = p < c.world && p != c.rank ? min(b.rx_cnt[kind * MAXW + p], cap) : 0u;
-    pc.n[p] = k;
-    pc.total += k;
+// What each peer produced for this shard this tick, clamped to the exchange capacity, loaded by the
+// workgroup into LDS (a register array indexed by peer would live in scratch); returns the total.
+__device__ __forceinline__ uint32_t peer_counts(const Ctx& c, const Bufs& b, uint32_t kind, uint32_t cap, uint32_t* s_n) {
+  if (threadIdx.x < (uint32_t)MAXW) {
+    const uint32_t p = threadIdx.x;
+    s_n[p] = p < c.world && p != c.rank ? min(b.rx_cnt[kind * MAXW + p], cap) : 0u;
   }
-  return pc;
+  __syncthreads();
+  uint32_t total = 0;
+  for (uint32_t p = 0; p < (uint32_t)MAXW; ++p) total += s_n[p];
+  return total;
 }
-// flat index i < pc.total -> (peer, index among that peer's items)
-__device__ __forceinline__ uint32_t peer_of(const PeerCounts& pc, uint32_t& i) {
+// flat index i < total -> (peer, index among that peer's items)
+__device__ __forceinline__ uint32_t peer_of(const uint32_t* s_n, uint32_t& i) {
   uint32_t p = 0;
-  while (i >= pc.n[p]) { i -= pc.n[p]; ++p; }
+  while (i >= s_n[p]) { i -= s_n[p]; ++p; }
   return p;
 }
 
@@ -986,24 +983,25 @@ __global__ void k_recv_msgs(KP) {
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
   const Peers* pr = b.peers;
+  __shared__ uint32_t s_n[MAXW], s_st[MAXW];
   if (blockIdx.x == 0) {
-    const PeerCounts ps = peer_counts(c, b, XK_STOP, b.tx_stop_cap);
+    peer_counts(c, b, XK_STOP, b.tx_stop_cap, s_st);
     uint32_t o = 0;
     for (uint32_t p = 0; p < c.world; ++p) {
-      for (uint32_t j = threadIdx.x; j < ps.n[p]; j += blockDim.x) b.rx_stops[o + j] = ld_peer_u32(pr->stops[p] + j);
-      o += ps.n[p];
+      for (uint32_t j = threadIdx.x; j < s_st[p]; j += blockDim.x) b.rx_stops[o + j] = ld_peer_u32(pr->stops[p] + j);
+      o += s_st[p];
     }
     if (threadIdx.x == 0) *b.rx_stop_n = o;
   }
-  const PeerCounts pc = peer_counts(c, b, XK_MSG, b.tx_msg_cap);
+  const uint32_t total = peer_counts(c, b, XK_MSG, b.tx_msg_cap, s_n);
   // wave-uniform trip count: every lane of a wave takes part in each deliver_local_msg call
   const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); i0 < pc.total; i0 += gridDim.x * blockDim.x) {
+  for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); i0 < total; i0 += gridDim.x * blockDim.x) {
     uint32_t i = i0 + lane;
-    const bool valid = i < pc.total;
+    const bool valid = i < total;
     GMsgFull msg{};
     if (valid) {
-      const uint32_t p = peer_of(pc, i);
+      const uint32_t p = peer_of(s_n, i);
       msg = ld_peer(pr->msgs[p] + (size_t)c.rank * b.tx_msg_cap + i);
       // kept (flagged) so that each (sender, receiver) pair's pseq stays dense for deliver_big
       msg.dup = coll_contains(c, coll_find(c, msg.to, msg.gossiper), msg.seq) ? 1u : 0u;

@@ -62,34 +62,40 @@ __device__ inline bool sync_complex(uint32_t r1, uint32_t r0, bool self) {
 // sender's table when the message is prepared (prepareSyncDataMsg :485-489) — are packed per
 // destination in tx order into tx_rows[d2]; each header learns its row (SyncReq.content), which is
 // how the receiver finds it.  Offsets come from this shard's own counters: no host round trip.
-// Rows are copied in 16-KiB chunks, one workgroup per (row, chunk): a handful of 256-KiB rows per
+// Rows are copied in 4-KiB chunks, one workgroup per (row, chunk): a handful of 256-KiB rows per
 // exchange would otherwise leave most CUs idle.
-constexpr uint32_t PACK_CHUNK = 4096;  // record words per unit
+constexpr uint32_t PACK_CHUNK = 1024;  // record words per unit (4 KiB: a dozen rows still spread over ~1,000 workgroups)
 __global__ void __launch_bounds__(256) k_pack_rows(KP, int d2) {
-  const Ctx c = pctx(P, T);
-  const Bufs b = P->b;
-  SyncReq* tx = d2 ? b.tx_acks : b.tx_reqs;
-  const uint32_t* cnt = d2 ? b.x->ack : b.x->req;
-  uint32_t n[MAXW], total = 0;
-  for (uint32_t d = 0; d < (uint32_t)MAXW; ++d) {
-    n[d] = d < c.world && d != c.rank ? min(cnt[d], b.tx_req_cap) : 0u;
-    total += n[d];
+  // (the counts live in LDS and the few Ctx fields are read directly: a dynamically indexed count
+  // array or a Ctx copy would live in scratch)
+  const Bufs& b = P->b;
+  const uint32_t n = P->c.n, lo = P->c.lo, world = P->c.world, rank = P->c.rank;
+  const uint32_t* recs = P->c.recs;
+  __shared__ uint32_t s_n[MAXW];
+  if (threadIdx.x < (uint32_t)MAXW) {
+    const uint32_t d = threadIdx.x;
+    const uint32_t* cnt = d2 ? b.x->ack : b.x->req;
+    s_n[d] = d < world && d != rank ? min(cnt[d], b.tx_req_cap) : 0u;
   }
-  if (total > b.row_cap && blockIdx.x == 0 && threadIdx.x == 0) set_err(c, ERR_REQS);
-  const uint32_t per_row = (c.n + PACK_CHUNK - 1) / PACK_CHUNK;
+  __syncthreads();
+  uint32_t total = 0;
+  for (uint32_t d = 0; d < (uint32_t)MAXW; ++d) total += s_n[d];
+  if (total > b.row_cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(P->c.err, ERR_REQS);
+  SyncReq* tx = d2 ? b.tx_acks : b.tx_reqs;
   uint32_t* out = b.tx_rows[d2];
+  const uint32_t per_row = (n + PACK_CHUNK - 1) / PACK_CHUNK;
   for (uint32_t u = blockIdx.x; u < total * per_row; u += gridDim.x) {
     const uint32_t row = u / per_row, ch = u - row * per_row;
     uint32_t k = row, d = 0;
-    while (k >= n[d]) { k -= n[d]; ++d; }
+    while (k >= s_n[d]) { k -= s_n[d]; ++d; }
     SyncReq* q = tx + (size_t)d * b.tx_req_cap + k;
     const bool fits = row < b.row_cap;
     if (ch == 0 && threadIdx.x == 0) q->content = fits ? row : NONE;
     if (!fits) continue;
-    const uint32_t x0 = ch * PACK_CHUNK, len = min(PACK_CHUNK, c.n - x0);
-    const uint32_t* src = rec_row(c, q->from) + x0;
-    uint32_t* dst = out + (size_t)row * c.n + x0;
-    if (c.n & 3) {  // rows are only 4-B aligned
+    const uint32_t x0 = ch * PACK_CHUNK, len = min(PACK_CHUNK, n - x0);
+    const uint32_t* src = recs + (size_t)(q->from - lo) * n + x0;
+    uint32_t* dst = out + (size_t)row * n + x0;
+    if (n & 3) {  // rows are only 4-B aligned
       for (uint32_t x = threadIdx.x; x < len; x += blockDim.x) dst[x] = src[x];
     } else {
       const uint4* s4 = reinterpret_cast<const uint4*>(src);
@@ -105,14 +111,15 @@ __global__ void __launch_bounds__(256) k_pack_rows(KP, int d2) {
 __global__ void k_recv_sync(KP, int d2) {
   const Ctx c = pctx_sync(P, T);
   const Bufs b = P->b;
-  const PeerCounts pc = peer_counts(c, b, d2 ? XK_ACK : XK_REQ, b.tx_req_cap);
+  __shared__ uint32_t s_n[MAXW];
+  const uint32_t total = peer_counts(c, b, d2 ? XK_ACK : XK_REQ, b.tx_req_cap, s_n);
   const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t k0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); k0 < pc.total; k0 += gridDim.x * blockDim.x) {
+  for (uint32_t k0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); k0 < total; k0 += gridDim.x * blockDim.x) {
     uint32_t k = k0 + lane;
     SyncReq q{};
-    bool valid = k < pc.total;
+    bool valid = k < total;
     if (valid) {
-      const uint32_t p = peer_of(pc, k);
+      const uint32_t p = peer_of(s_n, k);
       q = ld_peer(b.peers->hdr[d2][p] + (size_t)c.rank * b.tx_req_cap + k);
       valid = q.content != NONE;  // its row did not fit the sender's tx_rows (ERR_REQS is set there)
       q.content = p * b.row_cap + q.content;
@@ -127,12 +134,13 @@ __global__ void __launch_bounds__(256) k_pull_rows(KP, int d2) {
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
   const Peers* pr = b.peers;
-  const PeerCounts pc = peer_counts(c, b, d2 ? XK_ACK : XK_REQ, b.tx_req_cap);
+  __shared__ uint32_t s_n[MAXW];
+  const uint32_t total = peer_counts(c, b, d2 ? XK_ACK : XK_REQ, b.tx_req_cap, s_n);
   const uint32_t per_row = (c.n + PACK_CHUNK - 1) / PACK_CHUNK;
-  for (uint32_t u = blockIdx.x; u < pc.total * per_row; u += gridDim.x) {
+  for (uint32_t u = blockIdx.x; u < total * per_row; u += gridDim.x) {
     uint32_t k = u / per_row;
     const uint32_t ch = u - k * per_row;
-    const uint32_t p = peer_of(pc, k);
+    const uint32_t p = peer_of(s_n, k);
     const uint32_t row = ld_peer_u32(&pr->hdr[d2][p][(size_t)c.rank * b.tx_req_cap + k].content);
     if (row >= b.row_cap) continue;
     const uint32_t x0 = ch * PACK_CHUNK, len = min(PACK_CHUNK, c.n - x0);
