@@ -188,7 +188,15 @@ def side_run(lib, workload, n, warmup, steps, device=0, **knobs):
 def fanout_roofline(fprof, window):
     f_ms = fprof["total_ms"] / max(1, fprof["launches"])
     f_ach = fprof["alg_bytes"] / max(1e-12, fprof["total_ms"] / 1e3) / 1e9
-    f_traffic, f_src = pmc_traffic("k_gossip_emit", "failures64k")
+    # traffic: the same window's PMC passes (tools/window_prof.sh + tools/window_summary.py: the last
+    # 30 launches = this side run's 6 timed periods), else the whole-run summary
+    import glob
+    wins = sorted(glob.glob(os.path.join(REPO, "profiles", "*_failures64k_window_emit_pmc.json")))
+    if wins:
+        doc = json.load(open(wins[-1]))
+        f_traffic, f_src = doc["hbm_bytes_per_launch"], os.path.relpath(wins[-1], REPO)
+    else:
+        f_traffic, f_src = pmc_traffic("k_gossip_emit", "failures64k")
     return {"bound": "hbm", "kernel": "k_gossip_emit", "achieved": f_ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": f_ach / HBM_PEAK_GBPS, "traffic": f_traffic, "traffic_source": f_src,
             "launches": fprof["launches"], "avg_launch_ms": f_ms,

@@ -121,14 +121,29 @@ struct LinkDev {  // NetworkEmulator per-link override, sorted by (a, b)
   int32_t out_delay;  // outboundSettings(b).meanDelay on a as a delay-table index; -1 = none, -2 = 0 ms
 };
 
-struct GMsgFull {
-  uint32_t to, from, pos, slot;
-  uint32_t gossiper, seq, subject, status;
-  int32_t inc;
-  uint32_t pseq;  // place among the round's messages of the (from, to) pair, in slab-position order
-  uint32_t dup;   // 1: the receiver's collector already held the sequence id on arrival (a no-op)
-  uint32_t pad;
+// A GOSSIP_REQ in flight: 32 B, two 16-B stores by the sender, two 16-B loads by the receiver.
+struct alignas(16) GMsgFull {
+  uint32_t to;       // the receiver, until the message is in its inbox; there: its age in ticks
+                     // (a message the network emulator delayed, 0 otherwise)
+  uint32_t from;     // the sender (GossipRequest.from)
+  uint32_t gossiper, seq, subject;  // Gossip id and the record (or user payload handle) it carries
+  uint32_t inc_st;   // incarnation (bits 0..28) | status << 29
+  uint32_t pos_dup;  // the sender's slab position (bits 0..30) | dup << 31: the receiver's collector
+                     // already held the sequence id on arrival (a no-op)
+  uint32_t pseq;     // place among the round's messages of the (from, to) pair in slab-position order;
+                     // in the delay ring: the sending tick, until k_dq_release ranks it
+  __device__ __forceinline__ int32_t inc() const { return (int32_t)(inc_st & 0x1fffffffu); }
+  __device__ __forceinline__ uint32_t status() const { return inc_st >> 29; }
+  __device__ __forceinline__ uint32_t pos() const { return pos_dup & 0x7fffffffu; }
+  __device__ __forceinline__ bool dup() const { return (pos_dup >> 31) != 0; }
+  __device__ __forceinline__ void set_gossip(uint32_t g, uint32_t q, uint32_t subj, uint32_t st, int32_t inc) {
+    gossiper = g;
+    seq = q;
+    subject = subj;
+    inc_st = ((uint32_t)inc & 0x1fffffffu) | (st << 29);
+  }
 };
+static_assert(sizeof(GMsgFull) == 32, "a GOSSIP_REQ is two 16-B words");
 
 struct SyncReq {  // SYNC (request) or SYNC_ACK
   uint32_t from, to, ordinal, slot;

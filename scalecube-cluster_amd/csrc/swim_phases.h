@@ -565,9 +565,10 @@ __device__ __forceinline__ void wave_order() {
 }
 
 // a GOSSIP_REQ for a receiver owned by this shard joins the receiver's inbox (every lane of the wave
-// calls it: `valid` masks the lanes without a message)
-__device__ inline void deliver_local_msg(const Ctx& c, const Bufs& b, GMsgFull msg, bool valid) {
+// calls it: `valid` masks the lanes without a message); in the inbox, `to` holds the message's age
+__device__ inline void deliver_local_msg(const Ctx& c, const Bufs& b, GMsgFull msg, bool valid, uint32_t age) {
   const uint32_t i = msg.to - c.lo;
+  msg.to = age;
   uint32_t s = 0, pid = NONE;
   if (valid) {
     s = atomicAdd(&b.msg_cnt[i], 1u);
@@ -577,7 +578,6 @@ __device__ inline void deliver_local_msg(const Ctx& c, const Bufs& b, GMsgFull m
   wave_order();
   if (valid && (s & 63) != 0) pid = inbox_page_wait(c, b, i, s >> 6);
   if (valid && pid != NONE) {
-    msg.slot = s;
     b.pg_msgs[(size_t)pid * 64 + (s & 63)] = msg;
     b.k->msg_total = 1u;  // "some inbox is non-empty" (k_gossip_deliver's early exit)
   }
@@ -631,6 +631,17 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   }
   __syncwarp();
   const uint32_t nt = s_t[0];
+  // what depends on the target only, once per round instead of once per (target, gossip): whether
+  // it is up and its inbound filter passes v (s_t[50 + j]), v's outbound loss towards it
+  // (s_t[66 + j]), the tick its collectors were last cleared (s_t[82 + j]; receipt bits older than
+  // that are void)
+  if (lane < nt) {
+    const uint32_t t = s_t[1 + lane];
+    s_t[50 + lane] = (c.up[t] && in_pass(c, t, v)) ? 1u : 0u;
+    s_t[66 + lane] = (uint32_t)out_loss(c, v, t);
+    s_t[82 + lane] = owned(c, t) ? c.clr_tick[t - c.lo] : 0xffffffffu;
+  }
+  wave_order();
   const uint64_t spread = (uint64_t)(c.repeat_mult * ceil_log2(rlen + 1));
   const uint64_t sweep = 2 * (spread + 1);
   const bool leaving = m.leave_pending != 0;
@@ -662,26 +673,43 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     if (keep) {
       // futures (:167-180, :360-368): the graceful-leave future stops the member at the end of the
       // tick; a user gossip's spread() completes (this round's copies were read before the mark)
-      GossipDev gw = g;
+      bool changed = false;
       if (period > (uint64_t)g.inf_period + spread) {
         if (leaving && g.gossiper == m.leave_gossiper && g.seq == (uint32_t)m.leave_seq) done = true;
         if (g.status == SWIM_GOSSIP_USER && g.gossiper == v) {
-          gw.status = SWIM_GOSSIP_USER_SPREAD;
+          changed = true;
           emit(c, v, v, SWIM_EV_SPREAD_DONE, SWIM_PHASE_GOSSIP, 0x80000000u | (g.seq & 0x7fffffffu), g.subject);
         }
       }
-      slab[w + lanes_below(kmask)] = gw;
+      // only entries that move (a swept prefix before them) or changed are written back: in a
+      // round that sweeps nothing the slab is read, never rewritten
+      const uint32_t to = w + lanes_below(kmask);
+      if (to != p || changed) {
+        GossipDev gw = g;
+        if (changed) gw.status = SWIM_GOSSIP_USER_SPREAD;
+        slab[to] = gw;
+      }
     }
     w += (uint32_t)__popcll(kmask);
     uint32_t matb = 0;  // bit j: a message to target j is materialised
     if (__ballot(win)) {
+      // the gossip's receipt-bitmap slot serves every target (known_received, one load per gossip)
+      uint64_t key = 0;
+      uint32_t sl = 0;
+      GSlot gs{};
+      if (win) {
+        key = gkey(g.gossiper, g.seq);
+        sl = gslot_of(key);
+        gs = c.gslot[sl];
+      }
+      const bool gs_ok = win && gs.key == key;
       for (uint32_t j = 0; j < nt; ++j) {
         const uint32_t t = s_t[1 + j];
         const bool send = win && !gossip_infected(g, s_t[17 + j]);
         nmsg += send ? 1u : 0u;
         // delivered copies; a receiver on this shard that already holds the sequence id drops it
         // (its collector only grows until delivery), another shard flags it on arrival
-        bool mat = send && c.up[t] && in_pass(c, t, v) && !lost_k(c, out_loss(c, v, t), v, SWIM_STREAM_GOSSIP_OUT, j, p);
+        bool mat = send && s_t[50 + j] && !lost_k(c, (int32_t)s_t[66 + j], v, SWIM_STREAM_GOSSIP_OUT, j, p);
         // a delayed copy waits in the arrival tick's bucket (delivered whatever the receiver's
         // collector holds by then: a clear may come in between)
         const uint32_t k = mat ? delay_ticks(c, v, t, v, SWIM_STREAM_GOSSIP_DELAY, j, p) : 0u;
@@ -691,15 +719,20 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
           const uint32_t q = atomicAdd(&b.dq_cnt[bk], 1u);
           if (q < b.dq_bcap) {
             GMsgFull msg;
-            msg.to = t; msg.from = v; msg.pos = p; msg.slot = 0;
-            msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
-            msg.inc = g.inc; msg.pseq = 0; msg.dup = 0; msg.pad = (uint32_t)c.T;
+            msg.to = t; msg.from = v; msg.pos_dup = p; msg.pseq = (uint32_t)c.T;  // (the sending tick)
+            msg.set_gossip(g.gossiper, g.seq, g.subject, g.status, g.inc);
             b.dq[(size_t)bk * b.dq_bcap + q] = msg;
           } else {
             set_err(c, ERR_DELAY);
           }
         }
-        mat = mat && !(owned(c, t) && known_received(c, t, g.gossiper, g.seq));
+        if (mat && owned(c, t)) {  // known_received, with the slot and the clear tick hoisted
+          const uint32_t i = t - c.lo;
+          bool known = gs_ok && s_t[82 + j] < gs.tick &&
+                       ((c.gbits[(size_t)sl * c.gwords + (i >> 5)] >> (i & 31)) & 1u);
+          if (!known) known = coll_contains(c, coll_find(c, t, g.gossiper), g.seq);
+          mat = !known;
+        }
         matb |= (mat ? 1u : 0u) << j;
       }
       if (s_t[49]) {
@@ -753,9 +786,9 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       const uint32_t pre = lanes_below(mk);
       const uint32_t t = s_t[1 + j];
       GMsgFull msg;
-      msg.to = t; msg.from = v; msg.pos = p; msg.slot = bj + pre;
-      msg.gossiper = g.gossiper; msg.seq = g.seq; msg.subject = g.subject; msg.status = g.status;
-      msg.inc = g.inc; msg.pseq = qj + pre; msg.dup = 0; msg.pad = 0;
+      msg.to = owned(c, t) ? 0u : t;  // in the inbox: age 0; for another shard: the receiver
+      msg.from = v; msg.pos_dup = p; msg.pseq = qj + pre;
+      msg.set_gossip(g.gossiper, g.seq, g.subject, g.status, g.inc);
       if (owned(c, t)) {
         const uint32_t s = bj + pre;
         const uint32_t pid = (s >> 6) == (bj >> 6) ? p0j : p1j;
@@ -868,7 +901,7 @@ __global__ void __launch_bounds__(256) k_fd(KP, int gossip, int collect) {
 // the rest of the round for the listed senders: one sender per wave at a time
 // prof (sampled launches only): {GOSSIP_REQs materialised, (gossip, sender round) states read}
 __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned long long* prof) {
-  __shared__ uint32_t s_t[EMIT_WAVES][50];
+  __shared__ uint32_t s_t[EMIT_WAVES][98];
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -904,6 +937,7 @@ __global__ void __launch_bounds__(256) k_dq_release(KP) {
     const uint32_t i = i0 + lane;
     const bool valid = i < cnt;
     GMsgFull msg{};
+    uint32_t age = 0;
     if (valid) {
       msg = q[i];
       uint32_t rank = 0;
@@ -911,13 +945,13 @@ __global__ void __launch_bounds__(256) k_dq_release(KP) {
         const GMsgFull& o = q[j];
         // copies with equal keys (one gossip sent to two targets at one address) are identical
         // messages: ranked in bucket order
-        rank += (o.to == msg.to && o.pad == msg.pad && o.from == msg.from &&
-                 (o.pos < msg.pos || (o.pos == msg.pos && j < i))) ? 1u : 0u;
+        rank += (o.to == msg.to && o.pseq == msg.pseq && o.from == msg.from &&
+                 (o.pos() < msg.pos() || (o.pos() == msg.pos() && j < i))) ? 1u : 0u;
       }
+      age = (uint32_t)T - msg.pseq;  // snd_key orders earlier rounds first
       msg.pseq = rank;
-      msg.pad = (uint32_t)T - msg.pad;  // age: snd_key orders earlier rounds first
     }
-    deliver_local_msg(c, b, msg, valid);  // every lane of the wave takes part
+    deliver_local_msg(c, b, msg, valid, age);  // every lane of the wave takes part
   }
 }
 
@@ -1004,9 +1038,9 @@ __global__ void k_recv_msgs(KP) {
       const uint32_t p = peer_of(s_n, i);
       msg = ld_peer(pr->msgs[p] + (size_t)c.rank * b.tx_msg_cap + i);
       // kept (flagged) so that each (sender, receiver) pair's pseq stays dense for deliver_big
-      msg.dup = coll_contains(c, coll_find(c, msg.to, msg.gossiper), msg.seq) ? 1u : 0u;
+      if (coll_contains(c, coll_find(c, msg.to, msg.gossiper), msg.seq)) msg.pos_dup |= 0x80000000u;
     }
-    deliver_local_msg(c, b, msg, valid);
+    deliver_local_msg(c, b, msg, valid, 0u);
   }
 }
 
@@ -1019,16 +1053,16 @@ constexpr int DLV_SORT = DLV_SORT_N;
 // canonical sender key: earlier sending rounds first (a released delayed message's pad holds its age
 // in ticks, DQ: n <= 2^20 when delays are on), then the sender
 __device__ __forceinline__ uint32_t snd_key(const Ctx& c, const GMsgFull& g) {
-  return c.delay_on ? ((4095u - min(g.pad, 4095u)) << 20) | g.from : g.from;
+  return c.delay_on ? ((4095u - min(g.to, 4095u)) << 20) | g.from : g.from;
 }
 __device__ __forceinline__ uint64_t msg_key(const Ctx& c, const GMsgFull& m) {
-  return ((uint64_t)snd_key(c, m) << 32) | m.pos;
+  return ((uint64_t)snd_key(c, m) << 32) | m.pos();
 }
 
 
 // onGossipReq (GossipProtocolImpl.java:201-215) for one received message, in canonical order
 __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, GossipDev* slab, const GMsgFull& g) {
-  if (g.dup) return false;  // the collector held it on arrival and only grows until now
+  if (g.dup()) return false;  // the collector held it on arrival and only grows until now
   CollEnt* col = coll_ensure(c, r, g.gossiper);
   if (!col) return false;
   const bool was_cleared = (col->meta & COLL_CLEARED) != 0;
@@ -1039,18 +1073,18 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, Gos
   if (found < 0) {
     if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); return true; }
     GossipDev ns;
-    ns.gossiper = g.gossiper; ns.seq = g.seq; ns.subject = g.subject; ns.status = g.status; ns.inc = g.inc;
+    ns.gossiper = g.gossiper; ns.seq = g.seq; ns.subject = g.subject; ns.status = g.status(); ns.inc = g.inc();
     ns.inf_period = (uint32_t)m.g_period;
     ns.inf[0] = g.from;
 #pragma unroll
     for (int k = 1; k < GINF; ++k) ns.inf[k] = NONE;
     slab[m.gossip_len++] = ns;
     gix_note(c, m, r, ns.gossiper, ns.seq);
-    if (g.status >= SWIM_GOSSIP_USER)  // sink.next(gossip.message()) (:209): listen() subscribers
+    if (g.status() >= SWIM_GOSSIP_USER)  // sink.next(gossip.message()) (:209): listen() subscribers
       emit(c, r, g.gossiper, SWIM_EV_GOSSIP, SWIM_PHASE_GOSSIP, m.ev_minor++, g.subject);
     // onMembershipGossip (MembershipProtocolImpl.java:452-459)
-    else if (update_membership(c, r, g.subject, g.status, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP))
-      apply_alive(c, r, g.subject, g.inc, R_GOSSIP, SWIM_PHASE_GOSSIP);
+    else if (update_membership(c, r, g.subject, g.status(), g.inc(), R_GOSSIP, SWIM_PHASE_GOSSIP))
+      apply_alive(c, r, g.subject, g.inc(), R_GOSSIP, SWIM_PHASE_GOSSIP);
   } else {
     GossipDev& st = slab[found];
     if (!gossip_infected(st, g.from)) {
