@@ -201,6 +201,8 @@ def fanout_roofline(fprof, window):
             "frac": f_ach / HBM_PEAK_GBPS, "traffic": f_traffic, "traffic_source": f_src,
             "launches": fprof["launches"], "avg_launch_ms": f_ms,
             "alg_bytes_per_launch": fprof["alg_bytes"] / max(1, fprof["launches"]),
+            "messages_per_launch": fprof["messages"] / max(1, fprof["launches"]),
+            "states_per_launch": fprof["records"] / max(1, fprof["launches"]),
             "alg_bytes_rule": "24 B per materialised GOSSIP_REQ + 32 B per (gossip, sender round) state read",
             "window": window}
 
