@@ -156,6 +156,7 @@ struct Shard {
 struct swim_engine {
   swim_config cfg{};
   int debug_sync = 0;  // SWIM_DEBUG_SYNC=1: synchronise after every tick kernel and name a faulting one
+  bool pull_rows = false;  // content rows pulled into local copies (RCCL; SWIM_EXCHANGE_PULL=1 in a local group)
   std::chrono::steady_clock::time_point debug_t{};
   int32_t device = 0;
   uint32_t n = 0, tick_ms = 0, P = 0, G = 0, S = 0, sz = 0;
@@ -472,7 +473,7 @@ static int32_t run_tick(swim_engine* e) {
       if (multi) {
         k_recv_sync<<<256, 256, 0, s>>>(sd.d_par, T, d2);
         TICK_CHECK("k_recv_sync");
-        if (e->rccl) {
+        if (e->pull_rows) {
           k_pull_rows<<<kPackGrid, 256, 0, s>>>(sd.d_par, T, d2);
           TICK_CHECK("k_pull_rows");
         }
@@ -807,17 +808,25 @@ static size_t xoff(const Shard& sd, const void* p) {
   return (size_t)(static_cast<const char*>(p) - static_cast<const char*>(sd.xreg));
 }
 
-// A local group: every shard reads the other shards' buffers directly.
+// A local group: every shard reads the other shards' buffers directly.  With SWIM_EXCHANGE_PULL=1
+// the content rows take the RCCL route instead — pulled by k_pull_rows into per-shard copies — so
+// the single-GPU parity tests cover that kernel and its system-scope loads too.
 static int32_t setup_peers_local(swim_engine* e) {
   for (Shard& sd : e->sh) {
     Peers ph{};
+    if (e->pull_rows)
+      for (int k = 0; k < 2; ++k)
+        if (!sd.alloc(&ph.rx_rows[k], (size_t)e->world * sd.b.row_cap * e->n)) return SWIM_ENOMEM;
     for (uint32_t p = 0; p < (uint32_t)e->world; ++p) {
       const Bufs& pb = e->sh[p].b;
       ph.msgs[p] = pb.tx_msgs;
       ph.hdr[0][p] = pb.tx_reqs;
       ph.hdr[1][p] = pb.tx_acks;
       ph.stops[p] = pb.tx_stops;
-      for (int k = 0; k < 2; ++k) ph.rows[k][p] = ph.rows_in[k][p] = pb.tx_rows[k];
+      for (int k = 0; k < 2; ++k) {
+        ph.rows[k][p] = pb.tx_rows[k];
+        ph.rows_in[k][p] = e->pull_rows ? ph.rx_rows[k] + (size_t)p * sd.b.row_cap * e->n : pb.tx_rows[k];
+      }
       ph.x[p] = e->sh[p].x;
     }
     if (hipMemcpy(sd.peers, &ph, sizeof ph, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
@@ -914,6 +923,10 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
   e->rank = rank;
   e->world = world;
   e->rccl = rccl;
+  {
+    const char* p = std::getenv("SWIM_EXCHANGE_PULL");
+    e->pull_rows = rccl || (p && p[0] == '1');
+  }
   e->sz = (capacity + (uint32_t)world - 1) / (uint32_t)world;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return SWIM_EDEVICE; }
   e->sh.resize(rccl ? 1 : (size_t)world);

@@ -109,6 +109,19 @@ def test_gpu_sharded_parity_scenario(glib, olib, sc, shards):
     _run_parity(glib, olib, dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": shards}))
 
 
+# the RCCL route of the content rows (k_pull_rows: pulled with system-scope loads into per-shard
+# copies, then classified from there) in the single-GPU rig (SWIM_EXCHANGE_PULL=1)
+PULL_SCENARIOS = ("mp_joins_via_seed", "churn_48", "config3_rates_200", "partition_heal_32", "restart_same_address_40")
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+@pytest.mark.parametrize("name", PULL_SCENARIOS)
+def test_gpu_sharded_pull_parity_scenario(glib, olib, name, shards, monkeypatch):
+    sc = {s.name: s for s in scenarios.catalog()}[name]
+    monkeypatch.setenv("SWIM_EXCHANGE_PULL", "1")
+    _run_parity(glib, olib, dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": shards}))
+
+
 def test_gpu_sharded_parity_config2_1024(glib, olib):
     sc = scenarios.config2()
     sc = dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": 4})
