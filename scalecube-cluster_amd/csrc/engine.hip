@@ -695,7 +695,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.blocks = (n + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
   bool ok = sd.alloc(&c.recs, nn) && sd.alloc(&c.aux, nn) && sd.alloc(&c.ref, n) && sd.alloc(&c.dirty, n) &&
             sd.alloc(&c.bdiff, (size_t)std::max(nl, 1u) * c.blocks) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
-            sd.alloc(&c.remote, nn) && sd.alloc(&c.slab, (size_t)nl * c.gcap) &&
+            sd.alloc(&c.remote, nn) && sd.alloc(&c.slab_hot, (size_t)nl * c.gcap) && sd.alloc(&c.slab_cold, (size_t)nl * c.gcap) &&
             sd.alloc(&c.gix, (size_t)nl * (c.gix_mask + 1)) && sd.alloc(&c.coll, (size_t)nl * c.hcap) &&
             sd.alloc(&c.spill[0], (size_t)c.spill_cap[0] * tier_words(0)) &&
             sd.alloc(&c.spill[1], (size_t)c.spill_cap[1] * tier_words(1)) &&
@@ -1473,19 +1473,21 @@ int32_t swim_read_gossips(swim_engine* e, uint32_t v, swim_gossip* out, uint32_t
   if (len) *len = m.gossip_len;
   uint32_t k = std::min(cap, m.gossip_len);
   if (!out || !k) return SWIM_OK;
-  std::vector<GossipDev> g(k);
-  if (hipMemcpy(g.data(), sd->c.slab + (size_t)(v - sd->c.lo) * sd->c.gcap, sizeof(GossipDev) * k,
-                hipMemcpyDeviceToHost) != hipSuccess)
+  std::vector<GossipHot> gh(k);
+  std::vector<GossipCold> gc(k);
+  const size_t o = (size_t)(v - sd->c.lo) * sd->c.gcap;
+  if (hipMemcpy(gh.data(), sd->c.slab_hot + o, sizeof(GossipHot) * k, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(gc.data(), sd->c.slab_cold + o, sizeof(GossipCold) * k, hipMemcpyDeviceToHost) != hipSuccess)
     return SWIM_EDEVICE;
-  for (uint32_t i = 0; i < k; ++i) {
-    out[i].gossiper = g[i].gossiper;
-    out[i].subject = g[i].subject;
-    out[i].seq = g[i].seq;
-    out[i].inc = g[i].inc;
-    out[i].status = g[i].status;
-    out[i].infection_period = g[i].inf_period;
-    out[i].infected[0] = g[i].inf[0];
-    out[i].infected[1] = g[i].inf[1];
+  for (uint32_t i = 0; i < k; ++i) {  // (the SlabRef layout, swim_device.h)
+    out[i].gossiper = gh[i].gossiper;
+    out[i].subject = gc[i].subject;
+    out[i].seq = gh[i].seq;
+    out[i].inc = gc[i].inc;
+    out[i].status = (gh[i].per_st >> PER_BITS) & 7u;
+    out[i].infection_period = gh[i].per_st & PER_MASK;
+    out[i].infected[0] = gh[i].inf0;
+    out[i].infected[1] = gc[i].inf[0];
   }
   return SWIM_OK;
 }

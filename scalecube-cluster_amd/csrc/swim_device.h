@@ -90,6 +90,60 @@ __device__ __forceinline__ bool gossip_infected(const GossipDev& g, uint32_t m) 
   return r;
 }
 
+// The slab stores a GossipDev in two parts at the same position: 16 hot bytes — all that a gossip
+// round reads for every live gossip (window, sweep, futures, first infected member, receipt key) —
+// and 32 cold bytes read only for the gossips a round actually sends, moves or marks.
+constexpr uint32_t PER_BITS = 28, PER_MASK = (1u << PER_BITS) - 1;  // infection period: 2^28 rounds
+struct alignas(16) GossipHot {
+  uint32_t gossiper, seq;
+  uint32_t per_st;  // infection period (bits 0..27) | status << 28 (3 bits) | more << 31: inf[1..] in use
+  uint32_t inf0;    // GossipState.infected's first member (the first sender), NONE = empty
+  __device__ __forceinline__ uint32_t inf_period() const { return per_st & PER_MASK; }
+  __device__ __forceinline__ uint32_t status() const { return (per_st >> PER_BITS) & 7u; }
+  __device__ __forceinline__ bool more() const { return (per_st >> 31) != 0; }
+};
+struct alignas(16) GossipCold {
+  uint32_t subject;
+  int32_t inc;
+  uint32_t inf[GINF - 1];  // GossipState.infected after the first, NONE = empty
+  uint32_t pad;
+};
+static_assert(sizeof(GossipHot) == 16 && sizeof(GossipCold) == 32, "48 B per GossipState");
+struct SlabRef {
+  GossipHot* hot;
+  GossipCold* cold;
+  __device__ __forceinline__ GossipDev get(uint32_t p) const {
+    const GossipHot h = hot[p];
+    const GossipCold k = cold[p];
+    GossipDev g;
+    g.gossiper = h.gossiper;
+    g.seq = h.seq;
+    g.inf_period = h.inf_period();
+    g.status = h.status();
+    g.subject = k.subject;
+    g.inc = k.inc;
+    g.inf[0] = h.inf0;
+#pragma unroll
+    for (int i = 1; i < GINF; ++i) g.inf[i] = k.inf[i - 1];
+    return g;
+  }
+  __device__ __forceinline__ void put(uint32_t p, const GossipDev& g) const {
+    GossipHot h;
+    h.gossiper = g.gossiper;
+    h.seq = g.seq;
+    h.per_st = (g.inf_period & PER_MASK) | (g.status << PER_BITS) | (g.inf[1] != NONE ? 1u << 31 : 0u);
+    h.inf0 = g.inf[0];
+    GossipCold k;
+    k.subject = g.subject;
+    k.inc = g.inc;
+#pragma unroll
+    for (int i = 1; i < GINF; ++i) k.inf[i - 1] = g.inf[i];
+    k.pad = 0;
+    hot[p] = h;
+    cold[p] = k;
+  }
+};
+
 // SequenceIdCollector (SequenceIdCollector.java) of (viewer, gossiper), 16 B: a collector holds one
 // interval almost always (a gossiper's sequence ids reach a member in order), so the interval is
 // inline.  One that needs more (out-of-order arrival, loss) spills to a block of a size tier —
@@ -206,7 +260,8 @@ struct Ctx {
   const uint32_t* route;
   uint32_t* ping;
   uint32_t* remote;
-  GossipDev* slab;
+  GossipHot* slab_hot;   // [nl][gcap] (SlabRef)
+  GossipCold* slab_cold;  // [nl][gcap]
   uint32_t* gix;       // [nl][gix_mask + 1] slab serials by (gossiper, seq), open addressing
   uint32_t gix_mask;
   CollEnt* coll;       // [nl][hcap] open addressing by gossiper
@@ -367,7 +422,10 @@ __device__ __forceinline__ void cell_put(const Ctx& c, uint32_t v, uint32_t s, u
 __device__ __forceinline__ MemberDev& mem(const Ctx& c, uint32_t v) { return c.mem[v - c.lo]; }
 __device__ __forceinline__ uint32_t* ping_list(const Ctx& c, uint32_t v) { return c.ping + (size_t)(v - c.lo) * c.n; }
 __device__ __forceinline__ uint32_t* remote_list(const Ctx& c, uint32_t v) { return c.remote + (size_t)(v - c.lo) * c.n; }
-__device__ __forceinline__ GossipDev* slab_of(const Ctx& c, uint32_t v) { return c.slab + (size_t)(v - c.lo) * c.gcap; }
+__device__ __forceinline__ SlabRef slab_of(const Ctx& c, uint32_t v) {
+  const size_t o = (size_t)(v - c.lo) * c.gcap;
+  return SlabRef{c.slab_hot + o, c.slab_cold + o};
+}
 __device__ __forceinline__ bool owned(const Ctx& c, uint32_t v) { return v - c.lo < c.nl; }
 __device__ __forceinline__ uint32_t owner(const Ctx& c, uint32_t v) { return v / c.sz; }
 
@@ -757,7 +815,7 @@ __device__ __forceinline__ void gix_note(const Ctx& c, MemberDev& m, uint32_t v,
   gix_put(c, m, gix_of(c, v), g, s, m.gix_base + m.gossip_len - 1);
 }
 // slab position of (g, s), or -1
-__device__ inline int32_t gix_find(const Ctx& c, MemberDev& m, uint32_t v, const GossipDev* slab, uint32_t g,
+__device__ inline int32_t gix_find(const Ctx& c, MemberDev& m, uint32_t v, const SlabRef& slab, uint32_t g,
                                    uint32_t s) {
   uint32_t* ix = gix_of(c, v);
   const uint32_t mask = c.gix_mask;
@@ -765,14 +823,14 @@ __device__ inline int32_t gix_find(const Ctx& c, MemberDev& m, uint32_t v, const
     for (uint32_t i = 0; i <= mask; ++i) ix[i] = NONE;
     m.gix_used = 0;
     m.gix_valid = 1;
-    for (uint32_t p = 0; p < m.gossip_len; ++p) gix_put(c, m, ix, slab[p].gossiper, slab[p].seq, m.gix_base + p);
+    for (uint32_t p = 0; p < m.gossip_len; ++p) gix_put(c, m, ix, slab.hot[p].gossiper, slab.hot[p].seq, m.gix_base + p);
   }
   uint32_t h = gix_hash(g, s);
   for (uint32_t i = 0; i <= mask; ++i, ++h) {
     const uint32_t e = ix[h & mask];
     if (e == NONE) return -1;
     const uint32_t p = e - m.gix_base;
-    if (p < m.gossip_len && slab[p].gossiper == g && slab[p].seq == s) return (int32_t)p;
+    if (p < m.gossip_len && slab.hot[p].gossiper == g && slab.hot[p].seq == s) return (int32_t)p;
   }
   return -1;
 }
@@ -791,7 +849,8 @@ __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject,
   g.inf_period = (uint32_t)m.g_period;
 #pragma unroll
   for (int k = 0; k < GINF; ++k) g.inf[k] = NONE;
-  slab_of(c, v)[m.gossip_len] = g;
+  if (m.g_period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
+  slab_of(c, v).put(m.gossip_len, g);
   m.gossip_len++;
   gix_note(c, m, v, g.gossiper, g.seq);
   m.g_counter++;
@@ -814,7 +873,8 @@ __device__ inline void spread_user(const Ctx& c, uint32_t v, uint32_t payload) {
   g.inf_period = (uint32_t)m.g_period;
 #pragma unroll
   for (int k = 0; k < GINF; ++k) g.inf[k] = NONE;
-  slab_of(c, v)[m.gossip_len] = g;
+  if (m.g_period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
+  slab_of(c, v).put(m.gossip_len, g);
   m.gossip_len++;
   gix_note(c, m, v, g.gossiper, g.seq);
   m.g_counter++;

@@ -645,7 +645,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   const uint64_t spread = (uint64_t)(c.repeat_mult * ceil_log2(rlen + 1));
   const uint64_t sweep = 2 * (spread + 1);
   const bool leaving = m.leave_pending != 0;
-  GossipDev* slab = slab_of(c, v);
+  const SlabRef slab = slab_of(c, v);
   unsigned long long nmsg = 0;
   uint32_t pseq = 0;  // lane j < nt: messages materialised to target j so far (GMsgFull.pseq)
   uint32_t w = 0;     // sweep: survivors so far
@@ -653,15 +653,17 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   bool seen_keep = false;
   bool done = false;
   // lane = slab position: one GossipState read serves all nt targets, whose loss draws and
-  // receiver checks are independent (issued together); messages keep the (target, position) keys
+  // receiver checks are independent (issued together); messages keep the (target, position) keys.
+  // A pass reads the 16 hot bytes of each state; the 32 cold ones only where a message is
+  // materialised, the first-infected check is not enough, or the entry moves.
   for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
     const uint32_t p = p0 + lane;
-    GossipDev g;
+    GossipHot h{};
     bool win = false, keep = false;
     if (p < glen) {
-      g = slab[p];
-      win = (uint64_t)g.inf_period + spread >= period;
-      keep = !(period > (uint64_t)g.inf_period + sweep);
+      h = slab.hot[p];
+      win = (uint64_t)h.inf_period() + spread >= period;
+      keep = !(period > (uint64_t)h.inf_period() + sweep);
     }
     // sweep (:158-164, :350-358): a pass's survivors land at or below their own positions, all of
     // which the wave has already read
@@ -670,42 +672,50 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       lead += kmask ? (uint32_t)__ffsll((unsigned long long)kmask) - 1 : min(64u, glen - p0);
       seen_keep = kmask != 0;
     }
-    if (keep) {
-      // futures (:167-180, :360-368): the graceful-leave future stops the member at the end of the
-      // tick; a user gossip's spread() completes (this round's copies were read before the mark)
-      bool changed = false;
-      if (period > (uint64_t)g.inf_period + spread) {
-        if (leaving && g.gossiper == m.leave_gossiper && g.seq == (uint32_t)m.leave_seq) done = true;
-        if (g.status == SWIM_GOSSIP_USER && g.gossiper == v) {
-          changed = true;
-          emit(c, v, v, SWIM_EV_SPREAD_DONE, SWIM_PHASE_GOSSIP, 0x80000000u | (g.seq & 0x7fffffffu), g.subject);
-        }
-      }
-      // only entries that move (a swept prefix before them) or changed are written back: in a
-      // round that sweeps nothing the slab is read, never rewritten
-      const uint32_t to = w + lanes_below(kmask);
-      if (to != p || changed) {
-        GossipDev gw = g;
-        if (changed) gw.status = SWIM_GOSSIP_USER_SPREAD;
-        slab[to] = gw;
+    // futures (:167-180, :360-368): the graceful-leave future stops the member at the end of the
+    // tick; a user gossip's spread() completes (this round's copies carry the status read above)
+    bool changed = false;
+    if (keep && period > (uint64_t)h.inf_period() + spread) {
+      if (leaving && h.gossiper == m.leave_gossiper && h.seq == (uint32_t)m.leave_seq) done = true;
+      if (h.status() == SWIM_GOSSIP_USER && h.gossiper == v) {
+        changed = true;
+        emit(c, v, v, SWIM_EV_SPREAD_DONE, SWIM_PHASE_GOSSIP, 0x80000000u | (h.seq & 0x7fffffffu), slab.cold[p].subject);
       }
     }
+    const uint32_t to = w + lanes_below(kmask);
     w += (uint32_t)__popcll(kmask);
     uint32_t matb = 0;  // bit j: a message to target j is materialised
+    uint32_t subj = 0;
+    int32_t inc = 0;
+    bool have_cold = false;
+    auto load_cold = [&]() {
+      if (!have_cold) {
+        const GossipCold k = slab.cold[p];
+        subj = k.subject;
+        inc = k.inc;
+        have_cold = true;
+      }
+    };
     if (__ballot(win)) {
       // the gossip's receipt-bitmap slot serves every target (known_received, one load per gossip)
       uint64_t key = 0;
       uint32_t sl = 0;
       GSlot gs{};
       if (win) {
-        key = gkey(g.gossiper, g.seq);
+        key = gkey(h.gossiper, h.seq);
         sl = gslot_of(key);
         gs = c.gslot[sl];
       }
       const bool gs_ok = win && gs.key == key;
       for (uint32_t j = 0; j < nt; ++j) {
-        const uint32_t t = s_t[1 + j];
-        const bool send = win && !gossip_infected(g, s_t[17 + j]);
+        const uint32_t t = s_t[1 + j], tm = s_t[17 + j];
+        bool infected = h.inf0 == tm;
+        if (win && !infected && h.more()) {  // GossipState.infected beyond its first member
+          const GossipCold k = slab.cold[p];
+#pragma unroll
+          for (int q = 0; q < GINF - 1; ++q) infected |= k.inf[q] == tm;
+        }
+        const bool send = win && !infected;
         nmsg += send ? 1u : 0u;
         // delivered copies; a receiver on this shard that already holds the sequence id drops it
         // (its collector only grows until delivery), another shard flags it on arrival
@@ -715,12 +725,13 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         const uint32_t k = mat ? delay_ticks(c, v, t, v, SWIM_STREAM_GOSSIP_DELAY, j, p) : 0u;
         if (k) {
           mat = false;
+          load_cold();
           const uint32_t bk = (uint32_t)(c.T + k) & DQ_MASK;
           const uint32_t q = atomicAdd(&b.dq_cnt[bk], 1u);
           if (q < b.dq_bcap) {
             GMsgFull msg;
             msg.to = t; msg.from = v; msg.pos_dup = p; msg.pseq = (uint32_t)c.T;  // (the sending tick)
-            msg.set_gossip(g.gossiper, g.seq, g.subject, g.status, g.inc);
+            msg.set_gossip(h.gossiper, h.seq, subj, h.status(), inc);
             b.dq[(size_t)bk * b.dq_bcap + q] = msg;
           } else {
             set_err(c, ERR_DELAY);
@@ -730,7 +741,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
           const uint32_t i = t - c.lo;
           bool known = gs_ok && s_t[82 + j] < gs.tick &&
                        ((c.gbits[(size_t)sl * c.gwords + (i >> 5)] >> (i & 31)) & 1u);
-          if (!known) known = coll_contains(c, coll_find(c, t, g.gossiper), g.seq);
+          if (!known) known = coll_contains(c, coll_find(c, t, h.gossiper), h.seq);
           mat = !known;
         }
         matb |= (mat ? 1u : 0u) << j;
@@ -746,59 +757,74 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         }
       }
     }
-    if (!__ballot(matb != 0)) continue;
-    // one inbox reservation per target present in this pass: lane j issues target j's atomic and
-    // makes sure the (at most two) inbox pages of its slot range exist
-    uint32_t cnt_mine = 0;
-    for (uint32_t j = 0; j < nt; ++j) {
-      const uint32_t cj = (uint32_t)__popcll(__ballot((matb >> j) & 1u));
-      nmat += cj;  // wave-uniform
-      if (lane == j) cnt_mine = cj;
-    }
-    uint32_t base = 0, pid0 = NONE, pid1 = NONE;
-    const bool loc = lane < nt && cnt_mine && owned(c, s_t[1 + lane]);
-    if (lane < nt && cnt_mine) {
-      const uint32_t tj = s_t[1 + lane];
+    if (__ballot(matb != 0)) {
+      if (matb) load_cold();
+      // one inbox reservation per target present in this pass: lane j issues target j's atomic and
+      // makes sure the (at most two) inbox pages of its slot range exist
+      uint32_t cnt_mine = 0;
+      for (uint32_t j = 0; j < nt; ++j) {
+        const uint32_t cj = (uint32_t)__popcll(__ballot((matb >> j) & 1u));
+        nmat += cj;  // wave-uniform
+        if (lane == j) cnt_mine = cj;
+      }
+      uint32_t base = 0, pid0 = NONE, pid1 = NONE;
+      const bool loc = lane < nt && cnt_mine && owned(c, s_t[1 + lane]);
+      if (lane < nt && cnt_mine) {
+        const uint32_t tj = s_t[1 + lane];
+        if (loc) {
+          const uint32_t i = tj - c.lo;
+          base = atomicAdd(&b.msg_cnt[i], cnt_mine);
+          if (base <= b.wave_min && base + cnt_mine > b.wave_min) big_mark(b, i, c.T);
+          // pages whose first slot is ours: ours to allocate (first the second page, if any)
+          if (((base + cnt_mine - 1) >> 6) != (base >> 6)) pid1 = inbox_page_alloc(c, b, i, (base >> 6) + 1);
+          if ((base & 63) == 0) pid0 = inbox_page_alloc(c, b, i, base >> 6);
+        } else {
+          base = atomicAdd(&b.x->msg[owner(c, tj)], cnt_mine);
+        }
+      }
+      wave_order();
       if (loc) {
-        const uint32_t i = tj - c.lo;
-        base = atomicAdd(&b.msg_cnt[i], cnt_mine);
-        if (base <= b.wave_min && base + cnt_mine > b.wave_min) big_mark(b, i, c.T);
-        // pages whose first slot is ours: ours to allocate (first the second page, if any)
-        if (((base + cnt_mine - 1) >> 6) != (base >> 6)) pid1 = inbox_page_alloc(c, b, i, (base >> 6) + 1);
-        if ((base & 63) == 0) pid0 = inbox_page_alloc(c, b, i, base >> 6);
-      } else {
-        base = atomicAdd(&b.x->msg[owner(c, tj)], cnt_mine);
+        // our slots start inside a page another writer allocates
+        if ((base & 63) != 0) pid0 = inbox_page_wait(c, b, s_t[1 + lane] - c.lo, base >> 6);
+        if (((base + cnt_mine - 1) >> 6) == (base >> 6)) pid1 = pid0;
       }
+      for (uint32_t j = 0; j < nt; ++j) {
+        const bool mat = (matb >> j) & 1u;
+        const uint64_t mk = __ballot(mat);
+        if (!mk) continue;
+        const uint32_t bj = __shfl(base, (int)j, 64), qj = __shfl(pseq, (int)j, 64);
+        const uint32_t p0j = __shfl(pid0, (int)j, 64), p1j = __shfl(pid1, (int)j, 64);
+        if (!mat) continue;
+        const uint32_t pre = lanes_below(mk);
+        const uint32_t t = s_t[1 + j];
+        GMsgFull msg;
+        msg.to = owned(c, t) ? 0u : t;  // in the inbox: age 0; for another shard: the receiver
+        msg.from = v; msg.pos_dup = p; msg.pseq = qj + pre;
+        msg.set_gossip(h.gossiper, h.seq, subj, h.status(), inc);
+        if (owned(c, t)) {
+          const uint32_t s = bj + pre;
+          const uint32_t pid = (s >> 6) == (bj >> 6) ? p0j : p1j;
+          if (pid != NONE) b.pg_msgs[(size_t)pid * 64 + (s & 63)] = msg;  // else inbox_page set the error bit
+        } else {
+          const uint32_t d = owner(c, t);
+          if (bj + pre < b.tx_msg_cap) b.tx_msgs[(size_t)d * b.tx_msg_cap + bj + pre] = msg; else set_err(c, ERR_MSGS);
+        }
+      }
+      pseq += cnt_mine;  // lane j: target j's messages so far this round
     }
+    // the sweep's write-back, last in the pass (every lane's reads of this pass are done): only
+    // entries that move (a swept prefix before them) or changed; a round that sweeps nothing
+    // rewrites nothing.  Every moving lane loads its cold part before any lane stores.
+    const bool wb = keep && (to != p || changed);
+    GossipCold kc{};
+    if (wb && to != p) kc = slab.cold[p];
     wave_order();
-    if (loc) {
-      // our slots start inside a page another writer allocates
-      if ((base & 63) != 0) pid0 = inbox_page_wait(c, b, s_t[1 + lane] - c.lo, base >> 6);
-      if (((base + cnt_mine - 1) >> 6) == (base >> 6)) pid1 = pid0;
+    if (wb) {
+      GossipHot hw = h;
+      if (changed) hw.per_st = (hw.per_st & ~(7u << PER_BITS)) | (SWIM_GOSSIP_USER_SPREAD << PER_BITS);
+      slab.hot[to] = hw;
+      if (to != p) slab.cold[to] = kc;
     }
-    for (uint32_t j = 0; j < nt; ++j) {
-      const bool mat = (matb >> j) & 1u;
-      const uint64_t mk = __ballot(mat);
-      if (!mk) continue;
-      const uint32_t bj = __shfl(base, (int)j, 64), qj = __shfl(pseq, (int)j, 64);
-      const uint32_t p0j = __shfl(pid0, (int)j, 64), p1j = __shfl(pid1, (int)j, 64);
-      if (!mat) continue;
-      const uint32_t pre = lanes_below(mk);
-      const uint32_t t = s_t[1 + j];
-      GMsgFull msg;
-      msg.to = owned(c, t) ? 0u : t;  // in the inbox: age 0; for another shard: the receiver
-      msg.from = v; msg.pos_dup = p; msg.pseq = qj + pre;
-      msg.set_gossip(g.gossiper, g.seq, g.subject, g.status, g.inc);
-      if (owned(c, t)) {
-        const uint32_t s = bj + pre;
-        const uint32_t pid = (s >> 6) == (bj >> 6) ? p0j : p1j;
-        if (pid != NONE) b.pg_msgs[(size_t)pid * 64 + (s & 63)] = msg;  // else inbox_page set the error bit
-      } else {
-        const uint32_t d = owner(c, t);
-        if (bj + pre < b.tx_msg_cap) b.tx_msgs[(size_t)d * b.tx_msg_cap + bj + pre] = msg; else set_err(c, ERR_MSGS);
-      }
-    }
-    pseq += cnt_mine;  // lane j: target j's messages so far this round
   }
   const bool any_done = __ballot(done) != 0;
   if (lane == 0) {
@@ -1061,7 +1087,7 @@ __device__ __forceinline__ uint64_t msg_key(const Ctx& c, const GMsgFull& m) {
 
 
 // onGossipReq (GossipProtocolImpl.java:201-215) for one received message, in canonical order
-__device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, GossipDev* slab, const GMsgFull& g) {
+__device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, const SlabRef& slab, const GMsgFull& g) {
   if (g.dup()) return false;  // the collector held it on arrival and only grows until now
   CollEnt* col = coll_ensure(c, r, g.gossiper);
   if (!col) return false;
@@ -1078,7 +1104,8 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, Gos
     ns.inf[0] = g.from;
 #pragma unroll
     for (int k = 1; k < GINF; ++k) ns.inf[k] = NONE;
-    slab[m.gossip_len++] = ns;
+    if (m.g_period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
+    slab.put(m.gossip_len++, ns);
     gix_note(c, m, r, ns.gossiper, ns.seq);
     if (g.status() >= SWIM_GOSSIP_USER)  // sink.next(gossip.message()) (:209): listen() subscribers
       emit(c, r, g.gossiper, SWIM_EV_GOSSIP, SWIM_PHASE_GOSSIP, m.ev_minor++, g.subject);
@@ -1086,12 +1113,16 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, Gos
     else if (update_membership(c, r, g.subject, g.status(), g.inc(), R_GOSSIP, SWIM_PHASE_GOSSIP))
       apply_alive(c, r, g.subject, g.inc(), R_GOSSIP, SWIM_PHASE_GOSSIP);
   } else {
-    GossipDev& st = slab[found];
+    GossipDev st = slab.get((uint32_t)found);
     if (!gossip_infected(st, g.from)) {
       int k = 0;
       while (k < GINF && st.inf[k] != NONE) ++k;
-      if (k < GINF) st.inf[k] = g.from;
-      else set_err(c, ERR_INFECTED);
+      if (k < GINF) {
+        st.inf[k] = g.from;
+        slab.put((uint32_t)found, st);
+      } else {
+        set_err(c, ERR_INFECTED);
+      }
     }
   }
   return true;
@@ -1198,7 +1229,7 @@ __device__ inline unsigned long long deliver_sorted(const Ctx& c, uint32_t r, co
   MemberDev& m = mem(c, r);
   m.ev_minor = 0;
   m.fetch_ctr = 0;
-  GossipDev* slab = slab_of(c, r);
+  const SlabRef slab = slab_of(c, r);
   unsigned long long acc = 0;
   for (uint32_t q = 0; q < k; ++q) {
     const uint32_t at = ix8 ? ix8[q * ix8_stride] : q;
@@ -1366,7 +1397,7 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     MemberDev& m = mem(c, r);
     m.ev_minor = 0;
     m.fetch_ctr = 0;
-    GossipDev* slab = slab_of(c, r);
+    const SlabRef slab = slab_of(c, r);
     // the next message (and its collector slot) is fetched while the current one is processed: the
     // chain's own dependent round trips are the cost of a big inbox
     auto fetch = [&](uint32_t q) -> GMsgFull {
