@@ -656,12 +656,16 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   // receiver checks are independent (issued together); messages keep the (target, position) keys.
   // A pass reads the 16 hot bytes of each state; the 32 cold ones only where a message is
   // materialised, the first-infected check is not enough, or the entry moves.
+  // the next pass's hot bytes are loaded while this pass runs (the sweep writes only positions at
+  // or below the current pass's)
+  GossipHot hn{};
+  if (lane < glen) hn = slab.hot[lane];
   for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
     const uint32_t p = p0 + lane;
-    GossipHot h{};
+    const GossipHot h = hn;
+    if (p + 64 < glen) hn = slab.hot[p + 64];
     bool win = false, keep = false;
     if (p < glen) {
-      h = slab.hot[p];
       win = (uint64_t)h.inf_period() + spread >= period;
       keep = !(period > (uint64_t)h.inf_period() + sweep);
     }
@@ -707,6 +711,14 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         gs = c.gslot[sl];
       }
       const bool gs_ok = win && gs.key == key;
+      // the first four targets' receipt words are loaded beside the slot (their addresses need only
+      // the slot index, not its contents): one round trip where the check needs two
+      auto rword = [&](uint32_t jj) -> uint32_t {
+        const uint32_t t = s_t[1 + min(jj, nt - 1)];
+        const uint32_t i = owned(c, t) ? t - c.lo : 0u;
+        return (win && jj < nt) ? c.gbits[(size_t)sl * c.gwords + (i >> 5)] : 0u;
+      };
+      const uint32_t wb0 = rword(0), wb1 = rword(1), wb2 = rword(2), wb3 = rword(3);
       for (uint32_t j = 0; j < nt; ++j) {
         const uint32_t t = s_t[1 + j], tm = s_t[17 + j];
         bool infected = h.inf0 == tm;
@@ -739,8 +751,9 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         }
         if (mat && owned(c, t)) {  // known_received, with the slot and the clear tick hoisted
           const uint32_t i = t - c.lo;
-          bool known = gs_ok && s_t[82 + j] < gs.tick &&
-                       ((c.gbits[(size_t)sl * c.gwords + (i >> 5)] >> (i & 31)) & 1u);
+          const uint32_t word = j == 0 ? wb0 : j == 1 ? wb1 : j == 2 ? wb2 : j == 3 ? wb3
+                                                 : c.gbits[(size_t)sl * c.gwords + (i >> 5)];
+          bool known = gs_ok && s_t[82 + j] < gs.tick && ((word >> (i & 31)) & 1u);
           if (!known) known = coll_contains(c, coll_find(c, t, h.gossiper), h.seq);
           mat = !known;
         }
