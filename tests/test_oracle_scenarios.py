@@ -1,4 +1,4 @@
-"""The reference's own scenario tests, restated on the lockstep oracle (virtual time).
+"""The reference's own scenario tests, restated on the lockstep oracle and on the GPU engine (virtual time).
 
 Each test mirrors one JUnit test: same topology, same fault schedule, same test configuration, and
 the same final-state assertions (trusted / suspected sets, event sequences, FD event statuses).
@@ -12,6 +12,17 @@ from swimgpu import abi
 from swimgpu.cluster import ClusterConfig, ClusterMath, MembershipEvent, MemberStatus, SimulatedCluster
 
 Type = MembershipEvent.Type
+
+
+# Every restatement runs on the CPU oracle and, marked gpu, on libswimgpu.so itself: the reference's
+# own assertions are then checked on the MI355X engine directly, not only through oracle parity.
+@pytest.fixture(autouse=True, params=["oracle", pytest.param("gpu", marks=pytest.mark.gpu)])
+def backend(request, monkeypatch):
+    if request.param == "gpu":
+        from swimgpu import load_library
+        glib = load_library()
+        monkeypatch.setattr(oracle, "lib", lambda: glib)
+    return request.param
 
 # MembershipProtocolTest.testConfig (:1111-1121)
 PING_INTERVAL = 200
