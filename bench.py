@@ -185,18 +185,18 @@ def side_run(lib, workload, n, warmup, steps, device=0, **knobs):
     return out
 
 
-def fanout_roofline(fprof, window):
+def fanout_roofline(fprof, window, same_window_pmc):
     f_ms = fprof["total_ms"] / max(1, fprof["launches"])
     f_ach = fprof["alg_bytes"] / max(1e-12, fprof["total_ms"] / 1e3) / 1e9
     # traffic: the same window's PMC passes (tools/window_prof.sh + tools/window_summary.py: the last
     # 30 launches = this side run's 6 timed periods), else the whole-run summary
+    # (only when this run IS that window: the failures workload, periods 30-36)
     import glob
     wins = sorted(glob.glob(os.path.join(REPO, "profiles", "*_failures64k_window_emit_pmc.json")))
-    if wins:
+    f_traffic, f_src = None, None
+    if wins and same_window_pmc:
         doc = json.load(open(wins[-1]))
         f_traffic, f_src = doc["hbm_bytes_per_launch"], os.path.relpath(wins[-1], REPO)
-    else:
-        f_traffic, f_src = pmc_traffic("k_gossip_emit", "failures64k")
     return {"bound": "hbm", "kernel": "k_gossip_emit", "achieved": f_ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": f_ach / HBM_PEAK_GBPS, "traffic": f_traffic, "traffic_source": f_src,
             "launches": fprof["launches"], "avg_launch_ms": f_ms,
@@ -365,7 +365,8 @@ def main():
     if fprof["alg_bytes"] > 0:
         # the gossip fanout kernel (north_star: merge AND fanout against the HBM roofline); only
         # workloads with gossip traffic (failures, churn) give it work
-        line["roofline_fanout"] = fanout_roofline(fprof, f"the timed window ({args.workload})")
+        same = args.workload == "failures" and args.warmup == KILL_FIRST + KILL_EVERY and args.steps == 6 and n == 65536
+        line["roofline_fanout"] = fanout_roofline(fprof, f"the timed window ({args.workload})", same)
     if world == 1 and args.workload == "quiet" and not args.no_extras and args.local_shards == 1:
         e.close()
         # the quiet headline sends no gossip: the fanout kernel is measured on the failures workload
@@ -377,7 +378,8 @@ def main():
         f_dt, _, f_fprof, f_st = side_run(lib, "failures", n, fw, fs, local_rank)
         line["roofline_fanout"] = fanout_roofline(
             f_fprof, f"config4-lan-failures N={n}: periods {fw}..{fw + fs} (member killed at period {fw}), "
-                     f"{n * fs / f_dt:.3g} member-periods/s, {f_st['gossip_messages']} GOSSIP_REQs sent")
+                     f"{n * fs / f_dt:.3g} member-periods/s, {f_st['gossip_messages']} GOSSIP_REQs sent",
+            fs == 6 and n == 65536)
         # the timing mode whose latency distributions pass the KS test against the reference-timing
         # DES (tests/test_ks_des.py: independent timer phases, 10 ms ticks); same quiet workload
         k_dt, _, _, _ = side_run(lib, "quiet", n, 2, args.ks_steps, local_rank, timer_stagger=1, tick_ms=10)
