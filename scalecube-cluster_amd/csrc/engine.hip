@@ -3,16 +3,17 @@
 // A swim_engine simulates one cluster of N members whose view rows are sharded by viewer
 // (DESIGN.md §7).  It holds the shards it runs in this process:
 //   * unsharded (world = 1): one shard owning every row — the single-GPU engine;
-//   * local group (cfg.local_shards = G > 1): all G shards in this process on one device, exchanging
-//     cross-shard messages with device-to-device copies (the bit-exact test rig of the sharded path);
-//   * RCCL (swim_create_shard): one shard per process / GPU, exchanging with ncclSend / ncclRecv
-//     over xGMI.
-// Both multi-shard modes run the same exchange plan (counts per destination shard -> packed content
-// rows -> segments concatenated in source-shard order); only the copy primitive differs.
+//   * local group (cfg.local_shards = G > 1): all G shards in this process on one device (the
+//     bit-exact test rig of the sharded path);
+//   * RCCL (swim_create_shard): one shard per process / GPU, the other ranks' exchange regions
+//     mapped over xGMI.
+// Both multi-shard modes run the same device-side exchange: producers write into their own region,
+// each shard learns on the device what every peer produced for it (ncclAllToAll of the counts, or
+// k_gather_counts in a local group), and fixed-grid kernels pull the items (k_recv_msgs,
+// k_recv_sync, k_pull_rows).
 //
-// Per tick every shard runs the kernel sequence of swim_phases.h on the engine's stream.  An
-// unsharded engine never synchronises inside a tick; a sharded one synchronises once per exchange
-// (gossip round, SYNC, SYNC_ACK) to learn the per-destination counts.
+// Per tick every shard runs the kernel sequence of swim_phases.h on the engine's stream; no engine
+// synchronises with the host inside a tick.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <rccl/rccl.h>

@@ -692,18 +692,6 @@ __device__ inline void receipt_mark(const Ctx& c, uint32_t r, uint32_t gossiper,
     c.gclaim[par * GSLOTS + atomicAdd(&c.gclaim_cnt[par], 1u)] = sl;  // at most one entry per slot
   }
 }
-// exact: true iff t's collector holds (gossiper, seq); the bitmap answers without the collector
-// probe when its bit is set and trustworthy (set after the slot's claim, and no collector of t was
-// cleared since the claim)
-__device__ inline bool known_received(const Ctx& c, uint32_t t, uint32_t gossiper, uint32_t seq) {
-  const uint64_t key = gkey(gossiper, seq);
-  const uint32_t sl = gslot_of(key);
-  const GSlot g = c.gslot[sl];
-  const uint32_t i = t - c.lo;
-  if (g.key == key && c.clr_tick[i] < g.tick && ((c.gbits[(size_t)sl * c.gwords + (i >> 5)] >> (i & 31)) & 1u))
-    return true;
-  return coll_contains(c, coll_find(c, t, gossiper), seq);
-}
 
 // ------------------------------------------------------------------------------- events
 // Appends from thousands of threads in one kernel (a timer storm removes a member at every viewer

@@ -701,7 +701,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       }
     };
     if (__ballot(win)) {
-      // the gossip's receipt-bitmap slot serves every target (known_received, one load per gossip)
+      // the gossip's receipt-bitmap slot serves every target (one load per gossip)
       uint64_t key = 0;
       uint32_t sl = 0;
       GSlot gs{};
@@ -749,7 +749,10 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
             set_err(c, ERR_DELAY);
           }
         }
-        if (mat && owned(c, t)) {  // known_received, with the slot and the clear tick hoisted
+        if (mat && owned(c, t)) {
+          // exact: does t's collector hold (gossiper, seq)?  The receipt bit answers without the
+          // collector probe when it is set and trustworthy (set after the slot's claim, and no
+          // collector of t was cleared since the claim)
           const uint32_t i = t - c.lo;
           const uint32_t word = j == 0 ? wb0 : j == 1 ? wb1 : j == 2 ? wb2 : j == 3 ? wb3
                                                  : c.gbits[(size_t)sl * c.gwords + (i >> 5)];
