@@ -39,7 +39,12 @@ constexpr uint32_t kDrainFirst = 1;    // the interval starts at one tick and ad
 #endif
 constexpr uint32_t kClassifyGrid = CLS_GRID;  // 16,384 waves: about one (message, chunk) unit each at N = 65,536
 constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
-constexpr uint32_t kEmitGrid = 2048;      // 8,192 waves, one gossip sender at a time each
+#ifndef EMIT_GRID
+#define EMIT_GRID 1024
+#endif
+// 4,096 waves, one gossip sender at a time each: all resident at the kernel's occupancy (4 waves per
+// SIMD); 2,048 workgroups (two rounds of waves) measured 7 % slower in a storm, 512 8 % slower
+constexpr uint32_t kEmitGrid = EMIT_GRID;
 constexpr uint32_t kDeliverGrid = 512;    // 2,048 waves (two workgroups per CU) for the big inboxes of a storm
 constexpr uint32_t kStopCap = 4096;
 constexpr uint32_t kProfEvery = 3;  // SYNC classify launches between timed ones
