@@ -35,11 +35,9 @@ namespace {
 constexpr uint32_t kDrainEvery = 256;  // longest interval between event drains (ticks)
 constexpr uint32_t kDrainFirst = 1;    // the interval starts at one tick and adapts to the event rate
 #ifndef CLS_GRID
-#define CLS_GRID 2048
+#define CLS_GRID 4096
 #endif
-// 8,192 waves, grid-stride over (message, chunk) units (4,096 workgroups measured 1 % slower on the
-// quiet tick, where most units are witness-skipped)
-constexpr uint32_t kClassifyGrid = CLS_GRID;
+constexpr uint32_t kClassifyGrid = CLS_GRID;  // 16,384 waves: about one (message, chunk) unit each at N = 65,536
 constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
 #ifndef EMIT_GRID
 #define EMIT_GRID 1024
