@@ -296,8 +296,26 @@ typedef struct swim_stats {
   uint64_t timers_fired;
   uint64_t events;
   uint64_t capacity_errors;
-  uint64_t reserved[9];
+  /* gossips_created split by the reference call site that originated each gossip (SWIM_ORIG_*) */
+  uint64_t gossips_by_reason[7];
+  uint64_t reserved[2];
 } swim_stats;
+/* Gossip origination reasons (the callers of spreadMembershipGossip / GossipProtocol.spread in
+ * MembershipProtocolImpl.java; MEMBERSHIP_GOSSIP and INITIAL_SYNC never originate, :836-843):
+ *   FD       SUSPECT from a FailureDetector event          (updateMembership :621-628, reason FD)
+ *   SYNC     SUSPECT or admitted ALIVE learned from a SYNC / SYNC_ACK   (:621-628, :648-656)
+ *   REFUTE   ALIVE/LEAVING inc+1 about oneself              (onSelfMemberDetected :686-708)
+ *   LEAVING  a received LEAVING record re-spread            (onLeavingDetected :710-733)
+ *   LEAVE    own graceful leave                             (leaveCluster :233-242)
+ *   METADATA own metadata update                            (updateIncarnation :214-226)
+ *   USER     GossipProtocol.spread                          (GossipProtocolImpl.java:126-130) */
+#define SWIM_ORIG_FD 0
+#define SWIM_ORIG_SYNC 1
+#define SWIM_ORIG_REFUTE 2
+#define SWIM_ORIG_LEAVING 3
+#define SWIM_ORIG_LEAVE 4
+#define SWIM_ORIG_METADATA 5
+#define SWIM_ORIG_USER 6
 int32_t swim_get_stats(swim_engine* e, swim_stats* out);
 
 /* ---- full-state readback for parity tests (not needed by a Java host) --------------------- */

@@ -27,6 +27,7 @@ import java.util.HashMap;
 import java.util.List;
 import java.util.Map;
 import java.util.Optional;
+import java.util.TreeSet;
 import java.util.concurrent.Callable;
 import reactor.core.publisher.DirectProcessor;
 import reactor.core.publisher.FluxSink;
@@ -62,6 +63,10 @@ public final class SimulatedCluster implements AutoCloseable {
   private final MemorySegment row;
   private final int[] addressSlot;
   private final long[] metadataVersion;
+  // per member: the destinations / sources it holds NetworkEmulator link overrides for, so that
+  // blockAll* / unblockAll* can clear them (outboundSettings.clear(), NetworkEmulator.java:88-99,238-249)
+  private final Map<Integer, TreeSet<Integer>> outLinks = new HashMap<>();
+  private final Map<Integer, TreeSet<Integer>> inLinks = new HashMap<>();
 
   private final List<DirectProcessor<MembershipEvent>> membership = new ArrayList<>();
   private final List<FluxSink<MembershipEvent>> membershipSinks = new ArrayList<>();
@@ -283,6 +288,25 @@ public final class SimulatedCluster implements AutoCloseable {
 
   // ------------------------------------------------------------------ plumbing
   MemorySegment engine() { return engine; }
+
+  void noteOutLink(int member, int destination) {
+    outLinks.computeIfAbsent(member, k -> new TreeSet<>()).add(destination);
+  }
+
+  void noteInLink(int member, int source) {
+    inLinks.computeIfAbsent(member, k -> new TreeSet<>()).add(source);
+  }
+
+  /** the member's link overrides, ascending; forgotten (the caller removes them from the engine) */
+  int[] takeOutLinks(int member) {
+    TreeSet<Integer> s = outLinks.remove(member);
+    return s == null ? new int[0] : s.stream().mapToInt(Integer::intValue).toArray();
+  }
+
+  int[] takeInLinks(int member) {
+    TreeSet<Integer> s = inLinks.remove(member);
+    return s == null ? new int[0] : s.stream().mapToInt(Integer::intValue).toArray();
+  }
 
   void run(Runnable r) {
     onScheduler(() -> {

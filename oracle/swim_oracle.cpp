@@ -409,7 +409,8 @@ struct swim_engine {
   // ------------------------------------------------------------------------- gossip origination
   // spreadMembershipGossip (MembershipProtocolImpl.java:845-860) -> GossipProtocolImpl.spread ->
   // createAndPutGossip (GossipProtocolImpl.java:190-199)
-  void spread_gossip(uint32_t v, const Record& r) {
+  // `why`: the call site (SWIM_ORIG_*), counted in swim_stats.gossips_by_reason
+  void spread_gossip(uint32_t v, const Record& r, uint32_t why) {
     Member& mv = m[v];
     GossipState g;
     g.gossiper = v;
@@ -419,11 +420,16 @@ struct swim_engine {
     mv.add_gossip(g);
     mv.collectors[v].add((int64_t)g.seq);
     STT().gossips_created++;
+    STT().gossips_by_reason[why]++;
   }
+  // the SWIM_ORIG_* reason of a spreadMembershipGossipUnlessGossiped call (:836-843)
+  static uint32_t orig_of(Reason r) { return r == FD_EVENT ? SWIM_ORIG_FD : SWIM_ORIG_SYNC; }
 
   // GossipProtocol.spread(Message) (GossipProtocolImpl.java:126-130): a user gossip, its payload in
   // the record's member field (status SWIM_GOSSIP_USER)
-  void spread_user(uint32_t v, uint32_t payload) { spread_gossip(v, Record{payload, SWIM_GOSSIP_USER, 0}); }
+  void spread_user(uint32_t v, uint32_t payload) {
+    spread_gossip(v, Record{payload, SWIM_GOSSIP_USER, 0}, SWIM_ORIG_USER);
+  }
 
   // ------------------------------------------------------------------------- timers
   // scheduleSuspicionTimeoutTask (:805-823): computeIfAbsent, timeout from the table size now.
@@ -472,7 +478,7 @@ struct swim_engine {
       int32_t cur = std::max(r0v.inc, r1.inc);
       Record r2{v, r0v.status, cur + 1};
       c = c_with_record(c, r2.status, r2.inc);
-      spread_gossip(v, r2);
+      spread_gossip(v, r2, SWIM_ORIG_REFUTE);
       return;
     }
     if (dst(s) == v) return;  // another member at the local address (:605-610)
@@ -485,7 +491,7 @@ struct swim_engine {
       }
       if (!present || r0v.status != SWIM_LEAVING) {
         schedule_timer(v, s);
-        spread_gossip(v, r1);
+        spread_gossip(v, r1, SWIM_ORIG_LEAVING);
       }
       return;
     }
@@ -504,7 +510,7 @@ struct swim_engine {
         c = c_with_record(c | B_IN_TABLE, SWIM_SUSPECT, r1.inc);
       }
       schedule_timer(v, s);
-      if (reason != MEMBERSHIP_GOSSIP && reason != INITIAL_SYNC) spread_gossip(v, r1);
+      if (reason != MEMBERSHIP_GOSSIP && reason != INITIAL_SYNC) spread_gossip(v, r1, orig_of(reason));
       return;
     }
     // ALIVE (:630-660)
@@ -527,7 +533,7 @@ struct swim_engine {
     Member& mv = m[v];
     const uint32_t s = r1.member;
     cancel_timer(v, s);
-    if (reason != MEMBERSHIP_GOSSIP && reason != INITIAL_SYNC) spread_gossip(v, r1);
+    if (reason != MEMBERSHIP_GOSSIP && reason != INITIAL_SYNC) spread_gossip(v, r1, orig_of(reason));
     uint64_t& c = mv.row[s];
     // metadataStore.updateMetadata(member, metadata1) returns metadata0 (null when none is stored);
     // metadata1 is the subject's metadata now (the fetch answers within the tick)
@@ -1404,7 +1410,7 @@ int32_t swim_leave(swim_engine* e, uint32_t v, int32_t stop_after) {
   uint64_t& c = mv.row[v];
   Record r{v, SWIM_LEAVING, c_inc(c) + 1};
   c = c_with_record(c, r.status, r.inc);
-  e->spread_gossip(v, r);
+  e->spread_gossip(v, r, SWIM_ORIG_LEAVE);
   if (stop_after) {
     mv.leave_pending = true;
     mv.leave_gossiper = v;
@@ -1486,7 +1492,7 @@ int32_t swim_update_metadata(swim_engine* e, uint32_t v) {
   uint64_t& c = mv.row[v];
   Record r{v, SWIM_ALIVE, c_inc(c) + 1};
   c = c_with_record(c, r.status, r.inc);
-  e->spread_gossip(v, r);
+  e->spread_gossip(v, r, SWIM_ORIG_METADATA);
   return SWIM_OK;
 }
 

@@ -567,7 +567,7 @@ __global__ void k_leave(Ctx c, uint32_t v, int32_t stop_after) {
   const uint64_t cell = cell_get(c, v, v);
   const int32_t inc = c_inc(cell) + 1;
   cell_put(c, v, v, c_with_record(cell, SWIM_LEAVING, inc));
-  spread_gossip(c, v, v, SWIM_LEAVING, inc);
+  spread_gossip(c, v, v, SWIM_LEAVING, inc, SWIM_ORIG_LEAVE);
   if (stop_after) {
     m.leave_pending = 1;
     m.leave_gossiper = v;
@@ -583,7 +583,7 @@ __global__ void k_update_meta(Ctx c, uint32_t v, int owner) {
   const uint64_t cell = cell_get(c, v, v);
   const int32_t inc = c_inc(cell) + 1;
   cell_put(c, v, v, c_with_record(cell, SWIM_ALIVE, inc));
-  spread_gossip(c, v, v, SWIM_ALIVE, inc);
+  spread_gossip(c, v, v, SWIM_ALIVE, inc, SWIM_ORIG_METADATA);
 }
 
 __global__ void k_spread(Ctx c, uint32_t v, uint32_t payload) {
@@ -1401,6 +1401,7 @@ int32_t swim_get_stats(swim_engine* e, swim_stats* out) {
   out->timers_fired = st[ST_TIMERS_FIRED];
   out->events = e->host_events;
   out->capacity_errors = e->err_seen;
+  for (int r = 0; r < 7; ++r) out->gossips_by_reason[r] = st[ST_ORIG0 + r];
   return SWIM_OK;
 }
 

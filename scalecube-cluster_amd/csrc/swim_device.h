@@ -45,7 +45,9 @@ enum { ST_TICKS, ST_PINGS, ST_PING_REQS, ST_FD_EVENTS, ST_GOSSIPS_CREATED, ST_GO
        ST_GOSSIP_ACCEPTED, ST_SYNCS, ST_SYNC_ACKS, ST_SYNC_RECORDS, ST_FETCHES, ST_FETCH_OK,
        ST_TIMERS_FIRED, ST_EVENTS, ST_CAPACITY_ERRORS,
        ST_MERGE_MSGS, ST_MERGE_RECORDS,  // swim_profile_merge accounting
-       ST_COUNT = 24 };
+       ST_ORIG0,  // 7 slots: gossips_created by SWIM_ORIG_* reason (swim_stats.gossips_by_reason)
+       ST_COUNT = ST_ORIG0 + 7 };
+static_assert(ST_COUNT == 24, "stats slots");
 
 enum Reason { R_FD_EVENT, R_GOSSIP, R_SYNC, R_INITIAL_SYNC, R_TIMEOUT };
 
@@ -825,7 +827,9 @@ __device__ inline int32_t gix_find(const Ctx& c, MemberDev& m, uint32_t v, const
 
 // ------------------------------------------------------------------------------- gossip origination
 // spreadMembershipGossip (MembershipProtocolImpl.java:845-860) -> createAndPutGossip (GossipProtocolImpl.java:190-199)
-__device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject, uint32_t status, int32_t inc) {
+// `why`: the call site (SWIM_ORIG_*), counted in swim_stats.gossips_by_reason
+__device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject, uint32_t status, int32_t inc,
+                                     uint32_t why) {
   MemberDev& m = mem(c, v);
   if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); return; }
   GossipDev g;
@@ -845,7 +849,10 @@ __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject,
   CollEnt* e = coll_ensure(c, v, v);
   if (coll_add(c, e, g.seq, &c.seg_flag[v - c.lo])) receipt_mark(c, v, v, g.seq);
   stat_add(c, ST_GOSSIPS_CREATED, 1);
+  stat_add(c, ST_ORIG0 + (int)why, 1);
 }
+// the SWIM_ORIG_* reason of a spreadMembershipGossipUnlessGossiped call (:836-843)
+__device__ __forceinline__ uint32_t orig_of(int reason) { return reason == R_FD_EVENT ? SWIM_ORIG_FD : SWIM_ORIG_SYNC; }
 
 // GossipProtocol.spread(Message) (GossipProtocolImpl.java:126-130): a user gossip, its payload in
 // the subject field
@@ -869,6 +876,7 @@ __device__ inline void spread_user(const Ctx& c, uint32_t v, uint32_t payload) {
   CollEnt* e = coll_ensure(c, v, v);
   if (coll_add(c, e, g.seq, &c.seg_flag[v - c.lo])) receipt_mark(c, v, v, g.seq);
   stat_add(c, ST_GOSSIPS_CREATED, 1);
+  stat_add(c, ST_ORIG0 + SWIM_ORIG_USER, 1);
 }
 
 // ------------------------------------------------------------------------------- timers
@@ -918,7 +926,7 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
   if (s == v) {  // onSelfMemberDetected (:686-708)
     int32_t cur = inc0 > inc1 ? inc0 : inc1;
     cell_put(c, v, s, c_with_record(cell, st0, cur + 1));
-    spread_gossip(c, v, v, st0, cur + 1);
+    spread_gossip(c, v, v, st0, cur + 1, SWIM_ORIG_REFUTE);
     return false;
   }
   if (dst(c, s) == v) return false;  // another member at the local address (:605-610)
@@ -930,7 +938,7 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
       publish_event(c, v, s, SWIM_EV_LEAVING, phase, next_minor(c, v, phase, s));
     if (!present || st0 != SWIM_LEAVING) {
       schedule_timer(c, v, s);
-      spread_gossip(c, v, s, SWIM_LEAVING, inc1);
+      spread_gossip(c, v, s, SWIM_LEAVING, inc1, SWIM_ORIG_LEAVING);
     }
     return false;
   }
@@ -949,7 +957,7 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
       cell_put(c, v, s, c_with_record(cell | B_IN_TABLE, SWIM_SUSPECT, inc1));
     }
     schedule_timer(c, v, s);
-    if (reason != R_GOSSIP && reason != R_INITIAL_SYNC) spread_gossip(c, v, s, SWIM_SUSPECT, inc1);
+    if (reason != R_GOSSIP && reason != R_INITIAL_SYNC) spread_gossip(c, v, s, SWIM_SUSPECT, inc1, orig_of(reason));
     return false;
   }
   // ALIVE (:630-660)
@@ -984,7 +992,7 @@ __device__ inline void apply_alive(const Ctx& c, uint32_t v, uint32_t s, int32_t
     seen = ver;
   }
   cell |= B_HAS_METADATA;
-  if (reason != R_GOSSIP && reason != R_INITIAL_SYNC) spread_gossip(c, v, s, SWIM_ALIVE, inc1);
+  if (reason != R_GOSSIP && reason != R_INITIAL_SYNC) spread_gossip(c, v, s, SWIM_ALIVE, inc1, orig_of(reason));
   const bool exists = c_has(cell, B_IN_MEMBERS);
   if (!c_has(cell, B_IN_TABLE)) m.table_size++;
   if (!exists) m.members_size++;

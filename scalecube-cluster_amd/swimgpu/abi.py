@@ -93,7 +93,11 @@ class swim_stats(C.Structure):
     _fields_ = [(name, C.c_uint64) for name in (
         "ticks", "pings", "ping_reqs", "fd_events", "gossips_created", "gossip_messages",
         "gossip_accepted", "syncs", "sync_acks", "sync_records", "fetches", "fetch_ok",
-        "timers_fired", "events", "capacity_errors")] + [("reserved", C.c_uint64 * 9)]
+        "timers_fired", "events", "capacity_errors")] + [
+        ("gossips_by_reason", C.c_uint64 * 7), ("reserved", C.c_uint64 * 2)]
+
+# swim_stats.gossips_by_reason indices (SWIM_ORIG_*, swim.h)
+ORIG_REASONS = ("fd", "sync", "refute", "leaving", "leave", "metadata", "user")
 
 
 class swim_member_state(C.Structure):
@@ -382,7 +386,11 @@ class Engine:
     def stats(self) -> dict:
         s = swim_stats()
         _check("swim_get_stats", self.lib.swim_get_stats(self._h, byref(s)))
-        return {name: getattr(s, name) for name, _ in swim_stats._fields_ if name != "reserved"}
+        out = {name: getattr(s, name) for name, _ in swim_stats._fields_
+               if name not in ("reserved", "gossips_by_reason")}
+        # gossips_created split by origination reason: orig_fd, orig_sync, ... (SWIM_ORIG_*)
+        out.update({f"orig_{r}": int(s.gossips_by_reason[i]) for i, r in enumerate(ORIG_REASONS)})
+        return out
 
     def read_member(self, m: int) -> dict:
         s = swim_member_state()

@@ -424,7 +424,8 @@ class NetworkEmulator:
             self._c.engine.set_link_loss(self._m, d, -1)
             self._c.engine.set_link_delay(self._m, d, -1)
 
-    def inbound_settings(self, destination: int, shall_pass: bool):  # :219-223
+    def inbound_settings(self, destination: int, shall_pass: bool):  # :221-225
+        self._c._note_inlink(self._m, destination)
         self._c.engine.set_link_inbound(self._m, destination, 1 if shall_pass else 0)
 
     def set_default_inbound_settings(self, shall_pass: bool):  # :230-233
@@ -583,13 +584,13 @@ class SimulatedCluster:
     def _note_inlink(self, a, b):
         self._inlinks[a].add(b)
 
-    def _links_from(self, a):
-        s = set(self._links[a])
+    def _links_from(self, a):  # ascending, as SimulatedCluster.takeOutLinks (TreeSet)
+        s = sorted(self._links[a])
         self._links[a].clear()
         return s
 
     def _inlinks_to(self, a):
-        s = set(self._inlinks[a])
+        s = sorted(self._inlinks[a])
         self._inlinks[a].clear()
         return s
 

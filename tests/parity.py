@@ -11,7 +11,8 @@ MEMBER_FIELDS = ("up", "joined", "leave_pending", "join_pending", "remote_idx", 
                  "relay_target", "relay_pending", "relay_due", "leave_gossiper", "leave_seq")
 
 STAT_FIELDS = ("pings", "ping_reqs", "fd_events", "gossips_created", "gossip_messages", "gossip_accepted",
-               "syncs", "sync_acks", "sync_records", "fetches", "fetch_ok", "timers_fired", "events")
+               "syncs", "sync_acks", "sync_records", "fetches", "fetch_ok", "timers_fired", "events") + tuple(
+                   f"orig_{r}" for r in abi.ORIG_REASONS)
 
 
 def state_digest(e: abi.Engine, members=None, collectors=True) -> dict:

@@ -46,3 +46,10 @@ def test_oracle_reproduces_config2_digest():
 def test_threaded_oracle_reproduces_scenario_digest(name):
     sc = {s.name: s for s in scenarios.catalog()}[name]
     assert oracle_run(sc, threads=4) == DIGESTS[sc.name]
+
+
+def test_origination_reasons_partition_gossips_created():
+    """swim_stats.gossips_by_reason (SWIM_ORIG_*) splits gossips_created by call site, exactly."""
+    for name, d in DIGESTS.items():
+        st = d["stats"]
+        assert sum(v for k, v in st.items() if k.startswith("orig_")) == st["gossips_created"], name
