@@ -129,6 +129,9 @@ def churn_capacities(cfg, capacity):
     # false suspicion puts a timer at every viewer
     cfg.interval_capacity = 8192
     cfg.timer_capacity = 64 * capacity
+    # pending at once: a period's kills (and false suspicions) at every viewer, for the suspicion
+    # timeout (5 x ceil_log2(N) periods): ~2.2 x 10^8 at N = 16,384
+    cfg.timer_pool_capacity = 1 << 28 if capacity > 12288 else 1 << 27
     return cfg
 
 
@@ -160,7 +163,7 @@ def cpu_model() -> str:
 def side_run(lib, workload, n, warmup, steps, device=0, **knobs):
     """A secondary single-GPU measurement on its own engine (the headline engine is closed first):
     `warmup` untimed periods, then `steps` timed ones.  Returns (seconds, merge profile, fanout
-    profile, stats)."""
+    profile, stats, deliver profile)."""
     import torch
     from swimgpu import abi
     sch = Schedule(workload, n, warmup + steps)
@@ -178,7 +181,7 @@ def side_run(lib, workload, n, warmup, steps, device=0, **knobs):
         sch.run(e, warmup, warmup + steps)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        out = (dt, e.profile_merge(), e.profile_fanout(), e.stats())
+        out = (dt, e.profile_merge(), e.profile_fanout(), e.stats(), e.profile_deliver())
         e.drain_events()
     finally:
         e.close()
@@ -205,6 +208,63 @@ def fanout_roofline(fprof, window, same_window_pmc):
             "states_per_launch": fprof["records"] / max(1, fprof["launches"]),
             "alg_bytes_rule": "24 B per materialised GOSSIP_REQ + 32 B per (gossip, sender round) state read",
             "window": window}
+
+
+def deliver_roofline(dprof, window, same_window_pmc):
+    """k_gossip_deliver (onGossipReq for every inbox) over the same window as the fanout roofline:
+    SURVEY.md §8(d) merge bytes, 24 B per delivered GOSSIP_REQ + 24 B (dedupe + view RMW) per message
+    that runs the collector check (swim_profile_deliver)."""
+    d_ms = dprof["total_ms"] / max(1, dprof["launches"])
+    d_ach = dprof["alg_bytes"] / max(1e-12, dprof["total_ms"] / 1e3) / 1e9
+    import glob
+    wins = sorted(glob.glob(os.path.join(REPO, "profiles", "*_failures64k_window_deliver_pmc.json")))
+    traffic, src = None, None
+    if wins and same_window_pmc:
+        doc = json.load(open(wins[-1]))
+        traffic, src = doc["hbm_bytes_per_launch"], os.path.relpath(wins[-1], REPO)
+    return {"bound": "hbm", "kernel": "k_gossip_deliver", "achieved": d_ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": d_ach / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": src,
+            "launches": dprof["launches"], "avg_launch_ms": d_ms,
+            "alg_bytes_per_launch": dprof["alg_bytes"] / max(1, dprof["launches"]),
+            "messages_per_launch": dprof["messages"] / max(1, dprof["launches"]),
+            "accepted_per_launch": dprof["records"] / max(1, dprof["launches"]),
+            "alg_bytes_rule": "24 B per delivered GOSSIP_REQ + 24 B (8 B dedupe RMW + 16 B view RMW) per message "
+                              "not flagged as a provable duplicate",
+            "window": window}
+
+
+def step_roofline(stats, prof, fprof, dprof, ticks, gossip_ticks, dt, steps, workload, n):
+    """The whole step against the HBM roofline (the quiet step is a chain of latency-bound launches,
+    no single kernel owns it): SURVEY.md §8(d)'s algorithmic bytes of everything the step did in the
+    timed window — ping phase 21 B per ping, events 16 B each, timers 4 B per fired timer, and the
+    sampled SYNC classify / fanout / delivery launches' per-launch bytes (swim_profile_*) times the
+    window's launches of each — over the timed wall time.  `traffic`: the HBM bytes per tick of every
+    kernel (the committed rocprofv3 PMC passes of this workload) times the window's ticks."""
+    per = lambda p: p["alg_bytes"] / max(1, p["launches"])
+    parts = {"fd_pings": 21.0 * stats["pings"], "events": 16.0 * stats["events"],
+             "timers": 4.0 * stats["timers_fired"], "sync_classify": per(prof) * ticks,
+             "fanout": per(fprof) * gossip_ticks, "deliver": per(dprof) * gossip_ticks}
+    total = sum(parts.values())
+    ach = total / dt / 1e9
+    import glob
+    traffic, src = None, None
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}{n // 1024}k_pmc.json")))
+    kst = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}{n // 1024}k_kernel_stats.csv")))
+    if paths and kst and os.path.basename(paths[-1]).split("_")[0] == os.path.basename(kst[-1]).split("_")[0]:
+        import csv
+        doc = json.load(open(paths[-1]))
+        calls = {r["kernel"]: int(r["calls"]) for r in csv.DictReader(open(kst[-1]))}
+        ticks_prof = max(1, calls.get("k_end_tick", 1))
+        per_tick = sum(v.get("hbm_bytes_per_launch", 0.0) * calls.get(k, 0) for k, v in doc["kernels"].items()) / ticks_prof
+        traffic, src = per_tick * ticks / steps, os.path.relpath(paths[-1], REPO)
+    return {"bound": "hbm", "scope": "step (one protocol period, every kernel)", "achieved": ach,
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,
+            "traffic": traffic, "traffic_unit": "HBM bytes per step (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, all kernels)",
+            "traffic_source": src, "alg_bytes_per_step": total / steps,
+            "alg_bytes_per_member_period": total / steps / n,
+            "alg_bytes_parts_per_step": {k: v / steps for k, v in parts.items()},
+            "rule": "SURVEY.md §8(d): ping 21 B, event 16 B, timer 4 B, SYNC classify / fanout / delivery per "
+                    "their swim_profile_* rules"}
 
 
 def cpu_baseline(n, p0, periods):
@@ -313,8 +373,9 @@ def main():
         dt = time.perf_counter() - t0
     except abi.SwimError as ex:
         raise SystemExit(f"{ex}; engine error bits {e.stats()['capacity_errors']:#x}")
-    prof, fprof = e.profile_merge(), e.profile_fanout()
+    prof, fprof, dprof = e.profile_merge(), e.profile_fanout(), e.profile_deliver()
     stats = e.stats()
+    tpp = e.now()[2]
     e.drain_events()
     if se is not None:
         dt = se.max_time(dt)
@@ -324,7 +385,7 @@ def main():
             st = torch.tensor([float(p["alg_bytes"]), p["total_ms"], float(p["launches"])], dtype=torch.float64)
             dist.all_reduce(st, op=dist.ReduceOp.SUM)
             return {"alg_bytes": st[0].item(), "total_ms": st[1].item(), "launches": int(st[2].item())}
-        prof, fprof = reduce(prof), reduce(fprof)
+        prof, fprof, dprof = reduce(prof), reduce(fprof), reduce(dprof)
     if stats["capacity_errors"]:
         raise SystemExit(f"capacity error during the benchmark: {stats['capacity_errors']:#x}")
 
@@ -351,7 +412,8 @@ def main():
                    "parallelism": (f"rows sharded over {world} GPUs, RCCL send/recv over xGMI" if world > 1 else
                                    f"single GPU, {args.local_shards} in-process shards" if args.local_shards > 1
                                    else "single GPU")},
-        "roofline": {"bound": "hbm", "kernel": "k_sync_classify", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+        "roofline": None,
+        "roofline_merge": {"bound": "hbm", "kernel": "k_sync_classify", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_src,
@@ -362,11 +424,16 @@ def main():
         "stats": {k: stats[k] for k in ("syncs", "sync_records", "gossip_messages", "gossips_created", "pings",
                                          "timers_fired", "events")},
     }
+    ticks = args.steps * tpp
+    gossip_ticks = ticks // max(1, cfg.gossip_interval // e.now()[1])  # ticks with a gossip round
+    line["roofline"] = step_roofline(stats, prof, fprof, dprof, ticks, gossip_ticks, dt, args.steps,
+                                     args.workload, n)
     if fprof["alg_bytes"] > 0:
         # the gossip fanout kernel (north_star: merge AND fanout against the HBM roofline); only
         # workloads with gossip traffic (failures, churn) give it work
         same = args.workload == "failures" and args.warmup == KILL_FIRST + KILL_EVERY and args.steps == 6 and n == 65536
         line["roofline_fanout"] = fanout_roofline(fprof, f"the timed window ({args.workload})", same)
+        line["roofline_deliver"] = deliver_roofline(dprof, f"the timed window ({args.workload})", same)
     if world == 1 and args.workload == "quiet" and not args.no_extras and args.local_shards == 1:
         e.close()
         # the quiet headline sends no gossip: the fanout kernel is measured on the failures workload
@@ -375,14 +442,14 @@ def main():
         # every member's first selectGossipMembers shuffle of its 65,535-entry remote list (once per
         # member, then every N / fanout rounds), which is not the steady state.
         fw, fs = KILL_FIRST + KILL_EVERY, args.fanout_steps
-        f_dt, _, f_fprof, f_st = side_run(lib, "failures", n, fw, fs, local_rank)
-        line["roofline_fanout"] = fanout_roofline(
-            f_fprof, f"config4-lan-failures N={n}: periods {fw}..{fw + fs} (member killed at period {fw}), "
-                     f"{n * fs / f_dt:.3g} member-periods/s, {f_st['gossip_messages']} GOSSIP_REQs sent",
-            fs == 6 and n == 65536)
+        f_dt, _, f_fprof, f_st, f_dprof = side_run(lib, "failures", n, fw, fs, local_rank)
+        window = (f"config4-lan-failures N={n}: periods {fw}..{fw + fs} (member killed at period {fw}), "
+                  f"{n * fs / f_dt:.3g} member-periods/s, {f_st['gossip_messages']} GOSSIP_REQs sent")
+        line["roofline_fanout"] = fanout_roofline(f_fprof, window, fs == 6 and n == 65536)
+        line["roofline_deliver"] = deliver_roofline(f_dprof, window, fs == 6 and n == 65536)
         # the timing mode whose latency distributions pass the KS test against the reference-timing
         # DES (tests/test_ks_des.py: independent timer phases, 10 ms ticks); same quiet workload
-        k_dt, _, _, _ = side_run(lib, "quiet", n, 2, args.ks_steps, local_rank, timer_stagger=1, tick_ms=10)
+        k_dt, _, _, _, _ = side_run(lib, "quiet", n, 2, args.ks_steps, local_rank, timer_stagger=1, tick_ms=10)
         line["ks_mode"] = {"value": n * args.ks_steps / k_dt, "unit": "member-periods/s",
                            "ms_per_step": k_dt / args.ks_steps * 1e3, "steps": args.ks_steps,
                            "config": "same workload, timer_stagger=1, tick_ms=10 (100 ticks per period)",

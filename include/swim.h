@@ -135,7 +135,7 @@ typedef struct swim_config {
                                  phase (members of a real cluster start at different instants; the
                                  default 0 aligns them) */
   uint32_t timer_capacity;    /* suspicion timers that may fall due in one tick, per row shard, split
-                                 over the shard's 256-viewer blocks (2x the even share, at least 1,024 each)
+                                 over the shard's 256-viewer blocks (2x the even share, at least 4,096 each)
                                  (0 = default 2 x the shard's rows; churn schedules a timer for every
                                  killed member at every viewer within a few seconds) */
   uint32_t message_capacity;  /* GOSSIP_REQ messages one gossip round may materialise, per row shard
@@ -148,6 +148,9 @@ typedef struct swim_config {
                                  1 sends every inbox through the wave path) */
   uint32_t delay_capacity;    /* delayed GOSSIP_REQs that may arrive in one tick (0 = default 1,024;
                                  allocated when a message delay is first set) */
+  uint32_t timer_pool_capacity; /* suspicion timers pending at once, per row shard, over all deadlines
+                                 (0 = default: the wheel's deadline buckets x timer_capacity, capped
+                                 at 2^27; a 2-way partition holds N/2 timers at every viewer) */
 } swim_config;
 
 /* preset: 0 = defaultConfig/defaultLanConfig, 1 = defaultWanConfig, 2 = defaultLocalConfig
@@ -252,7 +255,9 @@ int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t l
  * detector's pings, ping-reqs and acks (a round trip completes when both legs arrived; a late
  * direct ack joins the ping-req race, :153-210) and to GOSSIP_REQs (delivered in the gossip phase
  * of their arrival tick, after the arrivals of earlier rounds).  SYNC / SYNC_ACK and metadata
- * round trips are not delayed.  Single-shard engines only (SWIM_EINVAL otherwise). */
+ * round trips are not delayed.  Single-shard engines only (SWIM_EINVAL otherwise).
+ * A mean above SWIM_DELAY_MEAN_MAX_TICKS (64) ticks is refused with SWIM_EINVAL: the quantised
+ * delay is capped at SWIM_DELAY_TICKS_MAX ticks and would truncate draws (swim_delay.h). */
 int32_t swim_set_default_delay(swim_engine* e, uint32_t m, int32_t mean_ms);
 int32_t swim_set_link_delay(swim_engine* e, uint32_t src, uint32_t dst, int32_t mean_ms);
 /* inboundSettings(src, shallPass) on dst (:219-223); shall_pass < 0 removes the override */
@@ -393,6 +398,11 @@ int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out);
  * messages = GOSSIP_REQs materialised, records = (gossip, sender round) states read,
  * alg_bytes = 24 B x messages + 32 B x records (SURVEY.md §8(d) fanout). */
 int32_t swim_profile_fanout(swim_engine* e, swim_kernel_profile* out);
+/* The gossip delivery kernel (onGossipReq for every inbox, k_gossip_deliver), sampled the same way:
+ * messages = GOSSIP_REQs delivered, records = those accepted (new GossipStates), alg_bytes =
+ * 24 B x messages + 24 B (8 B dedupe RMW + 16 B view RMW) x messages not flagged as provable
+ * duplicates by the sender (SURVEY.md §8(d) merge). */
+int32_t swim_profile_deliver(swim_engine* e, swim_kernel_profile* out);
 
 /* ---- known-answer hooks (run the engine's own merge / dedupe code on given inputs) --------- */
 /* Philox4x32-10 block used by every draw site. */

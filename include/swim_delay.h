@@ -14,8 +14,10 @@
  * integers.  The thresholds are computed once per distinct meanDelay on the host, by this one
  * function, in the GPU engine and in the CPU oracle alike (same libm at run time), so both engines
  * quantise every draw identically; the device and the oracle only compare integers.  Delays are
- * capped at SWIM_DELAY_TICKS_MAX ticks (for meanDelay / tick_ms <= 30 the cap is reached with
- * probability < 2^-90).
+ * capped at SWIM_DELAY_TICKS_MAX ticks; a draw reaches the cap with probability
+ * exp(-SWIM_DELAY_TICKS_MAX * tick_ms / meanDelay), so both engines refuse (SWIM_EINVAL) a mean
+ * above SWIM_DELAY_MEAN_MAX_TICKS ticks (swim_delay_mean_ok): at the limit that probability is
+ * e^-32 = 1.3e-14 per draw (at the reference's GossipDelayTest 3 s over 100 ms ticks, e^-68).
  */
 #ifndef SWIM_DELAY_H
 #define SWIM_DELAY_H
@@ -24,6 +26,13 @@
 #include <stdint.h>
 
 #define SWIM_DELAY_TICKS_MAX 2047u /* < the 2,048 arrival buckets of the GPU's delay ring */
+
+#define SWIM_DELAY_MEAN_MAX_TICKS 64u /* SWIM_DELAY_TICKS_MAX / 64 = 32 means: cap probability e^-32 */
+
+/* a meanDelay the tick-quantised delay can represent without truncating draws (mean_ms > 0) */
+static inline int swim_delay_mean_ok(int32_t mean_ms, uint32_t tick_ms) {
+  return mean_ms > 0 && (uint64_t)mean_ms <= (uint64_t)SWIM_DELAY_MEAN_MAX_TICKS * tick_ms;
+}
 
 static inline void swim_delay_thresholds(int32_t mean_ms, uint32_t tick_ms, uint64_t* th /* [SWIM_DELAY_TICKS_MAX] */) {
   for (uint32_t j = 1; j <= SWIM_DELAY_TICKS_MAX; ++j) {

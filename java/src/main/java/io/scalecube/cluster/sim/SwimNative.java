@@ -85,7 +85,8 @@ public final class SwimNative {
           JAVA_INT.withName("message_capacity"),
           JAVA_INT.withName("interval_capacity"),
           JAVA_INT.withName("deliver_wave_min"),
-          JAVA_INT.withName("delay_capacity"));
+          JAVA_INT.withName("delay_capacity"),
+          JAVA_INT.withName("timer_pool_capacity"));
 
   /** swim_event: (tick, viewer, subject, type, phase, minor, data), canonical order. */
   public static final StructLayout EVENT =

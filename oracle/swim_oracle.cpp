@@ -1150,6 +1150,7 @@ int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out) {
 }
 
 int32_t swim_profile_fanout(swim_engine* e, swim_kernel_profile* out) { return swim_profile_merge(e, out); }
+int32_t swim_profile_deliver(swim_engine* e, swim_kernel_profile* out) { return swim_profile_merge(e, out); }
 
 int32_t swim_kat_overrides(const int32_t* cases, uint32_t n, uint8_t* out) {
   if (n && (!cases || !out)) return SWIM_EINVAL;
@@ -1499,6 +1500,7 @@ int32_t swim_update_metadata(swim_engine* e, uint32_t v) {
 int32_t swim_set_default_delay(swim_engine* e, uint32_t mm, int32_t mean_ms) {
   if (!e || mean_ms < 0) return SWIM_EINVAL;
   if (mm != 0xffffffffu && mm >= e->n) return SWIM_EINVAL;
+  if (mean_ms > 0 && !swim_delay_mean_ok(mean_ms, e->tick_ms)) return SWIM_EINVAL;  // swim_delay.h cap
   e->ensure_delay_tab(mean_ms);
   if (mm == 0xffffffffu) std::fill(e->default_delay.begin(), e->default_delay.end(), mean_ms);
   else e->default_delay[mm] = mean_ms;
@@ -1510,6 +1512,7 @@ int32_t swim_set_link_delay(swim_engine* e, uint32_t src, uint32_t dst, int32_t 
   if (mean_ms < 0) {
     e->link_delay.erase({src, dst});
   } else {
+    if (mean_ms > 0 && !swim_delay_mean_ok(mean_ms, e->tick_ms)) return SWIM_EINVAL;  // swim_delay.h cap
     e->ensure_delay_tab(mean_ms);
     e->link_delay[{src, dst}] = mean_ms;
   }

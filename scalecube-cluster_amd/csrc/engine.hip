@@ -128,13 +128,15 @@ struct Shard {
   Peers* peers = nullptr;
   std::vector<void*> ipc_open;  // peers' regions mapped here (RCCL)
   uint32_t links_dev_cap = 0;
+  uint64_t* delay_buf = nullptr;  // the delay threshold tables (Ctx.delay_th)
+  size_t delay_cap = 0;           // words allocated
   // device-resident launch parameters (swim_phases.h Params) and the last uploaded image
   Params* d_par = nullptr;
   Params up{};
   bool up_valid = false;
   // swim_profile_*: HIP events around sampled k_sync_classify (merge) and k_gossip_emit (fanout)
   // launches on the engine's stream
-  KProf prof_cls, prof_emit;
+  KProf prof_cls, prof_emit, prof_dlv;
 
   template <typename T>
   bool alloc(T** p, size_t count) {
@@ -142,12 +144,14 @@ struct Shard {
     allocs.push_back((void*)*p);
     return true;
   }
+  // (keep: the first *cap elements are copied into the new allocation; the caller has drained the stream)
   template <typename T>
-  bool grow(T** p, size_t* cap, size_t need) {
+  bool grow(T** p, size_t* cap, size_t need, bool keep = false) {
     if (need <= *cap) return true;
     size_t nc = std::max<size_t>(need, *cap * 2);
     T* q = nullptr;
     if (dalloc(&q, nc) != hipSuccess) return false;
+    if (keep && *p && *cap && hipMemcpy(q, *p, sizeof(T) * *cap, hipMemcpyDeviceToDevice) != hipSuccess) return false;
     if (*p) {
       allocs.erase(std::remove(allocs.begin(), allocs.end(), (void*)*p), allocs.end());
       hipFree(*p);
@@ -199,6 +203,7 @@ struct swim_engine {
     for (Shard& s : sh) {
       for (hipEvent_t ev : s.prof_cls.ev) hipEventDestroy(ev);
       for (hipEvent_t ev : s.prof_emit.ev) hipEventDestroy(ev);
+      for (hipEvent_t ev : s.prof_dlv.ev) hipEventDestroy(ev);
       for (void* p : s.ipc_open) hipIpcCloseMemHandle(p);
       for (void* p : s.allocs) hipFree(p);
       if (s.xreg) hipFree(s.xreg);
@@ -272,6 +277,19 @@ static void launch_emit(swim_engine* e, Shard& s) {
   k.used++;
 }
 
+static void launch_deliver(swim_engine* e, Shard& s) {
+  // at least kDeliverGrid workgroups: big inboxes are delivered a wave each, grid-stride
+  const uint32_t grid = std::max<uint32_t>(kDeliverGrid, grid_for(s.c.nl, DLV_BLOCK));
+  KProf& k = s.prof_dlv;
+  if (!k.take(e->prof)) {
+    k_gossip_deliver<<<grid, DLV_BLOCK, 0, e->stream>>>(s.d_par, e->T, 1, nullptr);
+    return;
+  }
+  hipExtLaunchKernelGGL(k_gossip_deliver, dim3(grid), dim3(DLV_BLOCK), 0, e->stream, k.ev[2 * k.used],
+                        k.ev[2 * k.used + 1], 0, s.d_par, e->T, 1, k.slots + 3 * k.used);
+  k.used++;
+}
+
 static int32_t sync_and_collect(swim_engine* e) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return hip_status() ? SWIM_EDEVICE : SWIM_EDEVICE;
   e->par_slot = 0;  // every staged Params upload has completed
@@ -299,6 +317,7 @@ static int32_t sync_and_collect(swim_engine* e) {
     if (e->prof) {
       s.prof_cls.flush();
       s.prof_emit.flush();
+      s.prof_dlv.flush();
     }
   }
   // adapt the drain interval so a sub-queue stays well below its capacity between drains (an event
@@ -425,6 +444,19 @@ static int32_t run_tick(swim_engine* e) {
     sd.c.T = e->T;
     sync_params(e, sd);
   }
+  if (e->debug_sync && multi) {  // the exchange pointers of a sharded tick are set
+    for (Shard& sd : e->sh) k_debug_exchange<<<1, 64, 0, s>>>(sd.d_par, T);
+    if (hipStreamSynchronize(s) != hipSuccess) return SWIM_EDEVICE;
+    for (Shard& sd : e->sh) {
+      uint32_t err = 0;
+      if (hipMemcpy(&err, sd.c.err, 4, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+      if (err & ERR_XPTR) {
+        std::fprintf(stderr, "libswimgpu: shard %u: null exchange pointer at tick %llu\n", sd.c.rank,
+                     (unsigned long long)T);
+        return SWIM_EDEVICE;
+      }
+    }
+  }
   if (!e->joins.empty()) {
     for (Shard& sd : e->sh)
       for (uint32_t m : e->joins) hipMemsetAsync(sd.c.up + m, 1, 1, s);
@@ -460,8 +492,7 @@ static int32_t run_tick(swim_engine* e) {
         k_recv_msgs<<<kRecvGrid, 256, 0, s>>>(sd.d_par, T);
         TICK_CHECK("k_recv_msgs");
       }
-      // at least kDeliverGrid workgroups: big inboxes are delivered a wave each, grid-stride
-      k_gossip_deliver<<<std::max<uint32_t>(kDeliverGrid, grid_for(sd.c.nl, DLV_BLOCK)), DLV_BLOCK, 0, s>>>(sd.d_par, T, 1);
+      launch_deliver(e, sd);
       TICK_CHECK("k_gossip_deliver");  // (also applies the phase's pingMembers inserts)
     }
   }
@@ -663,9 +694,21 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   const uint64_t tcap = cf.timer_capacity ? cf.timer_capacity : 2ull * std::max(nl, 1u);
   c.wheel_nq = std::max(1u, (nl + 255) / 256);  // one queue per k_fd workgroup
   c.gwords = std::max(1u, (nl + 31) / 32);
-  // per-block queues take 2x their even share: timers cluster on viewers unevenly (a churn tick
-  // schedules ~16 timers at each of 256 viewers of a block)
-  c.wheel_cap = c.wheel_nq * (uint32_t)std::max<uint64_t>(1024, 2 * ((tcap + c.wheel_nq - 1) / c.wheel_nq));
+  // paged wheel (swim_device.h): one (bucket, queue) may take 2x its block's even share of the
+  // per-tick capacity (timers cluster on viewers unevenly: a churn tick schedules ~16 timers at each
+  // of 256 viewers of a block), at most every (viewer, subject) pair of the block; its page table has
+  // ~1,024 pages (the page grows from 64 to 4,096 entries with that bound); the pool holds
+  // timer_pool_capacity entries in whole pages plus one partial page per (bucket, queue)
+  {
+    const uint64_t W = (uint64_t)c.wheel_mask + 1, nq = c.wheel_nq;
+    const uint64_t per_q = std::min<uint64_t>(256ull * n, std::max<uint64_t>(4096, 2 * ((tcap + nq - 1) / nq)));
+    uint32_t sh = 6;
+    while (sh < 12 && (per_q >> sh) > 1024) ++sh;
+    c.wheel_pshift = sh;
+    c.wheel_ptmax = (uint32_t)((per_q + (1ull << sh) - 1) >> sh);
+    const uint64_t pool = cf.timer_pool_capacity ? cf.timer_pool_capacity : std::min<uint64_t>(1ull << 27, W * tcap);
+    c.wheel_pages = (uint32_t)std::min<uint64_t>(1ull << 30, ((pool + (1ull << sh) - 1) >> sh) + W * nq + 64);
+  }
   c.ev_cap = std::max<uint32_t>(1024, (cf.event_capacity ? cf.event_capacity : (1u << 22)) / SUBQ);
   // deferred pingMembers inserts of one phase: a join burst adds every joiner at every viewer
   c.ins_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 22, 256ull * nl));
@@ -713,8 +756,11 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&c.spill_avail[3], c.spill_cap[3]) && sd.alloc(&c.spill_freed[3], c.spill_cap[3]) &&
             sd.alloc(&c.spill_ctl, NTIER) && sd.alloc(&c.seg_flag, nl) &&
             sd.alloc(&c.fd_sync, (size_t)nl * FD_SYNC_MAX) &&
-            sd.alloc(&c.wheel, (size_t)(c.wheel_mask + 1) * c.wheel_cap) &&
-            sd.alloc(&c.wheel_cnt, (size_t)(c.wheel_mask + 1) * c.wheel_nq) && sd.alloc(&c.ev, (size_t)c.ev_cap * SUBQ) &&
+            sd.alloc(&c.wheel, (size_t)c.wheel_pages << c.wheel_pshift) &&
+            sd.alloc(&c.wheel_cnt, (size_t)(c.wheel_mask + 1) * c.wheel_nq) &&
+            sd.alloc(&c.wheel_pt, (size_t)(c.wheel_mask + 1) * c.wheel_nq * c.wheel_ptmax) &&
+            sd.alloc(&c.wheel_avail, c.wheel_pages) && sd.alloc(&c.wheel_freed, c.wheel_pages) &&
+            sd.alloc(&c.wheel_ctl, 1) && sd.alloc(&c.ev, (size_t)c.ev_cap * SUBQ) &&
             sd.alloc(&c.ev_cnt, SUBQ) && sd.alloc(&c.default_loss, n) &&
             sd.alloc(&c.default_delay, n) && sd.alloc(&b.dq_cnt, DQ_BUCKETS) && sd.alloc(&c.meta_ver, n) &&
             sd.alloc(&c.default_inbound, n) && sd.alloc(&c.group, n) && sd.alloc(&c.links, 1) &&
@@ -757,6 +803,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(c.spill_ctl, 0, sizeof(SpillCtl) * NTIER, s);
   hipMemsetAsync(c.seg_flag, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1) * c.wheel_nq, s);
+  hipMemsetAsync(c.wheel_pt, 0xff, sizeof(uint32_t) * (c.wheel_mask + 1) * c.wheel_nq * c.wheel_ptmax, s);
+  hipMemsetAsync(c.wheel_ctl, 0, sizeof(SpillCtl), s);
   hipMemsetAsync(c.ev_cnt, 0, 4 * SUBQ, s);
   hipMemsetAsync(c.up, 0, n, s);
   hipMemsetAsync(c.up, 1, n_initial, s);
@@ -1248,22 +1296,27 @@ int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t p
   return upload_links(e);
 }
 
-// ---- message delay (swim_delay.h): one threshold table per distinct meanDelay, on every shard
+// ---- message delay (swim_delay.h): one threshold table per distinct meanDelay, on every shard.
+// The tables live in one device array that grows by doubling (the previous one is freed after the
+// stream drained), and only the new table is written.  A mean above SWIM_DELAY_MEAN_MAX_TICKS ticks
+// is refused: beyond it the SWIM_DELAY_TICKS_MAX cap would truncate draws with non-negligible
+// probability (swim_delay_mean_ok, shared with the oracle).
 static int32_t delay_table(swim_engine* e, int32_t mean_ms, int32_t* idx) {
   for (size_t i = 0; i < e->delay_means.size(); ++i)
     if (e->delay_means[i] == mean_ms) { *idx = (int32_t)i; return SWIM_OK; }
-  if (e->delay_means.size() >= 4096) return SWIM_EINVAL;
-  e->delay_means.push_back(mean_ms);
-  const size_t nt = e->delay_means.size();
-  std::vector<uint64_t> th(nt * SWIM_DELAY_TICKS_MAX);
-  for (size_t i = 0; i < nt; ++i) swim_delay_thresholds(e->delay_means[i], e->tick_ms, th.data() + i * SWIM_DELAY_TICKS_MAX);
+  if (e->delay_means.size() >= 4096 || !swim_delay_mean_ok(mean_ms, e->tick_ms)) return SWIM_EINVAL;
+  std::vector<uint64_t> th(SWIM_DELAY_TICKS_MAX);
+  swim_delay_thresholds(mean_ms, e->tick_ms, th.data());
+  const size_t nt = e->delay_means.size() + 1;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
   for (Shard& sd : e->sh) {
-    uint64_t* p = nullptr;
-    if (!sd.alloc(&p, th.size())) return SWIM_ENOMEM;
-    if (hipMemcpy(p, th.data(), 8 * th.size(), hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
-    sd.c.delay_th = p;  // the previous table stays allocated until the engine is destroyed
+    if (!sd.grow(&sd.delay_buf, &sd.delay_cap, nt * SWIM_DELAY_TICKS_MAX, /*keep=*/true)) return SWIM_ENOMEM;
+    sd.c.delay_th = sd.delay_buf;
+    if (hipMemcpy(sd.delay_buf + (nt - 1) * SWIM_DELAY_TICKS_MAX, th.data(), 8 * th.size(), hipMemcpyHostToDevice) !=
+        hipSuccess)
+      return SWIM_EDEVICE;
   }
+  e->delay_means.push_back(mean_ms);
   *idx = (int32_t)(nt - 1);
   return SWIM_OK;
 }
@@ -1535,7 +1588,7 @@ int32_t swim_profile_enable(swim_engine* e, int32_t enable) {
   if (!e) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
   for (Shard& sd : e->sh) {
-    for (KProf* k : {&sd.prof_cls, &sd.prof_emit}) {
+    for (KProf* k : {&sd.prof_cls, &sd.prof_emit, &sd.prof_dlv}) {
       if (k->ev.empty()) {
         k->ev.resize(4 * kDrainEvery + 4);
         for (auto& ev : k->ev)
@@ -1582,6 +1635,25 @@ int32_t swim_profile_fanout(swim_engine* e, swim_kernel_profile* out) {
   }
   // SURVEY.md §8(d) fanout: 24 B per emitted GOSSIP_REQ + 32 B per (gossip, sender round) read
   out->alg_bytes = out->messages * 24ull + out->records * 32ull;
+  return SWIM_OK;
+}
+
+int32_t swim_profile_deliver(swim_engine* e, swim_kernel_profile* out) {
+  if (!e || !out) return SWIM_EINVAL;
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  std::memset(out, 0, sizeof(*out));
+  uint64_t fresh = 0;
+  for (Shard& sd : e->sh) {
+    sd.prof_dlv.flush();
+    out->launches += sd.prof_dlv.launches;
+    out->total_ms += sd.prof_dlv.ms;
+    out->messages += sd.prof_dlv.a;
+    fresh += sd.prof_dlv.b;
+    out->records += sd.prof_dlv.c;
+  }
+  // SURVEY.md §8(d) merge: 24 B per delivered GOSSIP_REQ read, + 8 B dedupe RMW + 16 B view RMW per
+  // message that runs onGossipReq's collector check (those emit flagged as provable duplicates do not)
+  out->alg_bytes = out->messages * 24ull + fresh * 24ull;
   return SWIM_OK;
 }
 

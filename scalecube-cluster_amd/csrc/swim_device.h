@@ -38,6 +38,7 @@ enum : uint32_t {
   ERR_INBOX = 1u << 14,  // one receiver's gossip inbox outgrew its page table
   ERR_COLL_TOP = 1u << 15,  // a collector outgrew the top spill tier (ERR_INTERVALS: a tier's pool ran dry)
   ERR_DELAY = 1u << 16,     // more delayed GOSSIP_REQs arrive in one tick than a delay bucket holds
+  ERR_XPTR = 1u << 17,      // SWIM_DEBUG_SYNC: a sharded tick would dereference a null exchange pointer
 };
 
 // stats slots (swim_stats order)
@@ -237,7 +238,7 @@ __device__ __forceinline__ uint32_t gslot_of(uint64_t key) {
 // indexed by viewer (cells, lists, slab, collectors, mem, per-viewer counters) holds owned rows only
 // and is indexed by v - lo; the network emulator, seeds and `up` are replicated.
 struct Ctx {
-  uint32_t n, gcap, hcap, wheel_mask, wheel_cap, wheel_nq;
+  uint32_t n, gcap, hcap, wheel_mask, wheel_nq;
   uint32_t lo, nl, sz, rank, world;
   uint32_t P, to_ticks, relay_ticks, G, S, sync_to_ticks, tick_ms;
   int32_t ping_interval, suspicion_mult, repeat_mult, fanout, ping_req_members, seg_threshold, record_fd;
@@ -274,8 +275,19 @@ struct Ctx {
   SpillCtl* spill_ctl;           // [NTIER]
   uint32_t* seg_flag;            // per viewer: a collector exceeded gossipSegmentationThreshold
   uint32_t* fd_sync;
-  uint64_t* wheel;      // [W][wheel_nq][wheel_cap / wheel_nq]: per deadline bucket, per 256-viewer block
+  // suspicion-timer wheel: one queue per (deadline bucket, 256-viewer block), paged.  Queue q of
+  // bucket b holds wheel_cnt[b][q] entries (viewer << 32 | subject); entry i lives in page
+  // wheel_pt[b][q][i >> wheel_pshift], slot i & page mask.  Pages come from a shared pool (bump +
+  // recycled: pages of a bucket fired this tick are reusable from the next), so the wheel holds
+  // timer_capacity entries in all buckets together, however they cluster in time (a partition
+  // schedules N/2 timers at every viewer within a few ticks).
+  uint64_t* wheel;      // [wheel_pages][1 << wheel_pshift]
   uint32_t* wheel_cnt;  // [W][wheel_nq]
+  uint32_t* wheel_pt;   // [W][wheel_nq][wheel_ptmax] page ids (NONE = not allocated yet)
+  uint32_t* wheel_avail;  // recyclable page ids
+  uint32_t* wheel_freed;  // page ids freed this tick
+  SpillCtl* wheel_ctl;    // {bump, avail, freed}
+  uint32_t wheel_pages, wheel_ptmax, wheel_pshift;  // page: 64 .. 4,096 entries (host-sized)
   swim_event* ev;
   uint32_t* ev_cnt;     // [SUBQ]
   uint32_t ev_cap;      // per sub-queue
@@ -880,6 +892,18 @@ __device__ inline void spread_user(const Ctx& c, uint32_t v, uint32_t payload) {
 }
 
 // ------------------------------------------------------------------------------- timers
+constexpr uint32_t WHEEL_FAILED = 0xfffffffeu;  // the page pool ran dry: releases the page's waiters
+__device__ __forceinline__ uint32_t b_of_deadline(const Ctx& c, uint64_t deadline) {
+  return (uint32_t)(deadline & c.wheel_mask);
+}
+// a page from the recycled list, else a fresh one from the pool (WHEEL_FAILED when dry)
+__device__ inline uint32_t wheel_page_alloc(const Ctx& c) {
+  const int32_t a = atomicSub(&c.wheel_ctl->avail, 1);
+  if (a > 0) return c.wheel_avail[a - 1];
+  const uint32_t i = atomicAdd(&c.wheel_ctl->bump, 1u);
+  return i < c.wheel_pages ? i : WHEEL_FAILED;
+}
+
 // scheduleSuspicionTimeoutTask (MembershipProtocolImpl.java:805-823)
 __device__ __forceinline__ int32_t ceil_log2(uint32_t x) { return x ? 32 - __clz(x) : 0; }
 __device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
@@ -890,10 +914,30 @@ __device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
   uint64_t deadline = c.T + ms / c.tick_ms;
   *ap = (a & 0xfu) | A_HAS_TIMER | ((uint32_t)(deadline & SWIM_DEADLINE_MASK) << 4);
   // queue of the viewer's 256-viewer block (fired by that block's k_fd workgroup)
-  const uint32_t b = (uint32_t)(deadline & c.wheel_mask), q = (v - c.lo) >> 8, qcap = c.wheel_cap / c.wheel_nq;
-  const uint32_t i = atomicAdd(&c.wheel_cnt[(size_t)b * c.wheel_nq + q], 1u);
-  if (i >= qcap) { set_err(c, ERR_WHEEL); return; }
-  c.wheel[(size_t)b * c.wheel_cap + (size_t)q * qcap + i] = ((uint64_t)v << 32) | s;
+  const uint32_t q = (size_t)b_of_deadline(c, deadline) * c.wheel_nq + ((v - c.lo) >> 8);
+  const uint32_t i = atomicAdd(&c.wheel_cnt[q], 1u);
+  const uint32_t pg = i >> c.wheel_pshift, slot = i & ((1u << c.wheel_pshift) - 1);
+  if (pg >= c.wheel_ptmax) { set_err(c, ERR_WHEEL); return; }
+  uint32_t* pt = c.wheel_pt + (size_t)q * c.wheel_ptmax + pg;
+  // the writer of a page's first slot allocates it, the others wait for it; every lane of the wave
+  // that reserved a slot here allocates before any lane waits, so a wave never waits on itself
+  // (a lane that reserved an earlier slot elsewhere completed its own call before this one)
+  const bool first = slot == 0;
+  uint32_t pid = NONE;
+  if (first) {
+    pid = wheel_page_alloc(c);
+    __atomic_store_n(pt, pid, __ATOMIC_RELAXED);
+  }
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+  if (!first)
+    for (uint32_t it = 0; it < (1u << 22); ++it) {
+      pid = __atomic_load_n(pt, __ATOMIC_RELAXED);
+      if (pid != NONE) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  if (pid >= c.wheel_pages) { set_err(c, ERR_WHEEL); return; }  // pool dry (PG_FAILED) or timed out
+  c.wheel[((size_t)pid << c.wheel_pshift) + slot] = ((uint64_t)v << 32) | s;
 }
 
 // ------------------------------------------------------------------------------- metadata fetch

@@ -114,7 +114,7 @@ struct Bufs {
   uint32_t* ack_snap;   // per member: SYNC_ACK-content slot or NONE
   uint32_t* snap_list;  // [2][snap_cap] members holding slots, by tick parity
   uint32_t* snap_cnt;   // [2] slots taken, by tick parity
-  uint32_t* sflag;      // per member: tick << 3 | SF_* bits of this tick
+  uint32_t* sflag;      // per member: tick << SF_BITS | SF_* bits of this tick
   uint64_t* pend;       // per sync-apply workgroup: pending ALIVE admissions
   uint2* item_chunk;    // per (SYNC item, chunk): (pool base, complex count)
   uint32_t* item_total; // per SYNC item: complex count over all chunks
@@ -291,14 +291,17 @@ __global__ void k_start_joins(KP) {
 // canonicalised by minor = subject.
 __device__ inline void timers_block(const Ctx& c, uint64_t T) {
   const uint32_t bucket = (uint32_t)(T & c.wheel_mask);
-  const uint32_t qcap = c.wheel_cap / c.wheel_nq;
-  uint32_t* qc = c.wheel_cnt + (size_t)bucket * c.wheel_nq + blockIdx.x;
-  const uint32_t cnt = min(*qc, qcap);
-  const uint64_t* ent = c.wheel + (size_t)bucket * c.wheel_cap + (size_t)blockIdx.x * qcap;
+  const size_t q = (size_t)bucket * c.wheel_nq + blockIdx.x;
+  uint32_t* qc = c.wheel_cnt + q;
+  const uint32_t cnt = min(*qc, c.wheel_ptmax << c.wheel_pshift);
+  const uint32_t pmask = (1u << c.wheel_pshift) - 1;
+  uint32_t* pt = c.wheel_pt + q * c.wheel_ptmax;
   const uint32_t tmask = (uint32_t)(c.T & SWIM_DEADLINE_MASK);
   unsigned long long fired = 0;
   for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-    uint64_t e = ent[i];
+    const uint32_t pid = pt[i >> c.wheel_pshift];
+    if (pid >= c.wheel_pages) continue;  // never allocated (ERR_WHEEL is set)
+    uint64_t e = c.wheel[((size_t)pid << c.wheel_pshift) + (i & pmask)];
     uint32_t v = (uint32_t)(e >> 32), s = (uint32_t)e;
     if (!c.up[v]) continue;
     uint32_t* ap = aux_row(c, v) + s;
@@ -316,7 +319,15 @@ __device__ inline void timers_block(const Ctx& c, uint64_t T) {
   }
   wave_stat_add(c, ST_TIMERS_FIRED, fired);
   __syncthreads();  // the block's DEAD updates (lists to compact) are visible to every thread
-  if (threadIdx.x == 0 && cnt) *qc = 0;
+  if (cnt) {  // the queue's pages are reusable from the next tick (k_end_tick)
+    const uint32_t np = (cnt + pmask) >> c.wheel_pshift;
+    for (uint32_t g = threadIdx.x; g < np; g += blockDim.x) {
+      const uint32_t pid = pt[g];
+      pt[g] = NONE;
+      if (pid < c.wheel_pages) c.wheel_freed[atomicAdd(&c.wheel_ctl->freed, 1u)] = pid;
+    }
+    if (threadIdx.x == 0) *qc = 0;
+  }
 }
 
 // REMOVED -> pingMembers.remove / remoteMembers.remove (FailureDetectorImpl.java:323-333,
@@ -583,6 +594,11 @@ __device__ inline void deliver_local_msg(const Ctx& c, const Bufs& b, GMsgFull m
   }
 }
 
+__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {  // lane 0 gets the wave's sum
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x += __shfl_down(x, d, 64);
+  return x;
+}
 __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
@@ -900,6 +916,7 @@ __device__ __forceinline__ void gossip_round(const Ctx& c, const Bufs& b, uint32
 // lost a member in the timer phase (a per-viewer dependency, so
 // no separate launch), then every thread runs its viewer's FD step and, on gossip ticks, the
 // first step of its gossip round (k_gossip_emit runs the rest after every FD step is done).
+__device__ inline unsigned long long sync_collect_pre(const Ctx& c, const Bufs& b, uint32_t v, uint32_t sn, uint32_t fl);
 __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Bufs& b, uint32_t v);
 
 // collect (ticks without a gossip round): the member's SYNC requests of phase D are collected here
@@ -911,10 +928,18 @@ __global__ void __launch_bounds__(256) k_fd(KP, int gossip, int collect) {
   __shared__ uint32_t s_list[256];
   __shared__ uint32_t s_cnt;
   if (c.world > 1 && blockIdx.x == 0 && threadIdx.x == 0) *P->b.rx_stop_n = 0;  // no leaves received yet
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  // the member's schedule words, loaded alongside the timer queue's count (phase A changes none of
+  // them; the FD step may set MF_FDSYNC, so mflag is reloaded after it)
+  const uint32_t fdn = i < c.nl ? c.fd_next[i] : NONE;
+  uint32_t sn = NONE, mfl = 0;
+  if (collect && i < c.nl) {
+    sn = c.sync_next[i];
+    mfl = c.mflag[i];
+  }
   timers_block(c, T);  // phase A for this block's viewers
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool flagged = i < c.nl && c.compact_flag[i] != 0;
   if (flagged) s_list[atomicAdd(&s_cnt, 1u)] = i;
   __syncthreads();
@@ -928,16 +953,32 @@ __global__ void __launch_bounds__(256) k_fd(KP, int gossip, int collect) {
   if (flagged) c.compact_flag[i] = 0;
   __syncthreads();  // the compacted lengths are visible to every thread
   unsigned long long nev = 0, nreq = 0, npings = 0;
-  if (i < c.nl && c.fd_next[i] == (uint32_t)T) fd_member(c, c.lo + i, nev, nreq, npings);
+  if (i < c.nl && fdn == (uint32_t)T) {
+    fd_member(c, c.lo + i, nev, nreq, npings);
+    if (collect) mfl = c.mflag[i];
+  }
   if (gossip) gossip_round(c, P->b, i);  // phase C's first step for this member
   if (collect) {
     const Ctx cs = pctx_sync(P, T);
-    const unsigned long long nsync = i < c.nl ? sync_collect_member(cs, P->b, c.lo + i) : 0;
+    const unsigned long long nsync = i < c.nl ? sync_collect_pre(cs, P->b, c.lo + i, sn, mfl) : 0;
     wave_stat_add(cs, ST_SYNCS, nsync);
   }
   wave_stat_add(c, ST_FD_EVENTS, nev);
   wave_stat_add(c, ST_PING_REQS, nreq);
   wave_stat_add(c, ST_PINGS, npings);
+}
+
+// SWIM_DEBUG_SYNC: every exchange pointer a sharded tick dereferences (k_fd's rx_stop_n reset,
+// k_recv_*, k_pack_rows, k_pull_rows, k_end_tick's counter reset and stop application, add_req's and
+// emit's tx_* appends) is non-null when world > 1; an unsharded engine must never reach them (every
+// use is guarded by world > 1 or by the owned() test, which is always true then)
+__global__ void k_debug_exchange(KP) {
+  const Ctx c = pctx(P, T);
+  const Bufs& b = P->b;
+  if (threadIdx.x != 0 || blockIdx.x != 0 || c.world <= 1) return;
+  const bool ok = b.x && b.tx_msgs && b.tx_reqs && b.tx_acks && b.tx_stops && b.tx_rows[0] && b.tx_rows[1] &&
+                  b.peers && b.rx_cnt && b.rx_stops && b.rx_stop_n;
+  if (!ok) atomicOr(c.err, ERR_XPTR);
 }
 
 // the rest of the round for the listed senders: one sender per wave at a time
@@ -1240,8 +1281,9 @@ constexpr int DLV_BLOCK = 256;
 constexpr int DLV_WAVES = DLV_BLOCK / 64;
 constexpr uint32_t BIG_MAXD = 128;  // distinct senders a big inbox is ranked over in LDS
 
+// (nfresh: messages not flagged as provable duplicates, i.e. that ran the collector check)
 __device__ inline unsigned long long deliver_sorted(const Ctx& c, uint32_t r, const GMsgFull* a, uint32_t k,
-                                                    const uint8_t* ix8, uint32_t ix8_stride) {
+                                                    const uint8_t* ix8, uint32_t ix8_stride, uint32_t& nfresh) {
   MemberDev& m = mem(c, r);
   m.ev_minor = 0;
   m.fetch_ctr = 0;
@@ -1249,7 +1291,9 @@ __device__ inline unsigned long long deliver_sorted(const Ctx& c, uint32_t r, co
   unsigned long long acc = 0;
   for (uint32_t q = 0; q < k; ++q) {
     const uint32_t at = ix8 ? ix8[q * ix8_stride] : q;
-    if (on_gossip_req(c, r, m, slab, a[at])) acc++;
+    const GMsgFull g = a[at];
+    nfresh += g.dup() ? 0u : 1u;
+    if (on_gossip_req(c, r, m, slab, g)) acc++;
   }
   return acc;
 }
@@ -1380,7 +1424,7 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
 
 __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, const Bufs& b, const uint32_t* list,
                                                 uint32_t nb, uint32_t lane, int collect, BigLds& L,
-                                                unsigned long long& nsync) {
+                                                unsigned long long& nsync, uint32_t& nmsg, uint32_t& nfresh) {
   // 1. rank every inbox of the batch; lane j keeps receiver j's message count (0: nothing to
   //    deliver) and the count of inbox pages to hand back
   uint32_t my_k = 0, my_pages = 0;
@@ -1427,12 +1471,14 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     const CollEnt* cbase = c.coll + (size_t)i * c.hcap;
     uint32_t sink = 0;
     GMsgFull next = fetch(0);
+    nmsg += my_k;
     for (uint32_t q = 0; q < my_k; ++q) {
       const GMsgFull g = next;
       if (q + 1 < my_k) {
         next = fetch(q + 1);
         sink ^= cbase[hash32(next.gossiper) & (c.hcap - 1)].key;  // warms the slot coll_find probes first
       }
+      nfresh += g.dup() ? 0u : 1u;
       if (on_gossip_req(c, r, m, slab, g)) acc++;
     }
     if (sink == 0x5bd1e995u && my_k == 0x7fffffffu) set_err(c, 0u);  // keeps the warming loads; sets no bit
@@ -1457,7 +1503,8 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
 // schedule and fd_sync queue).  First the big inboxes, a wave each, grid-stride over big_list;
 // then each workgroup's blocks of 256 members: small inboxes thread per receiver, their inserts by
 // the workgroup, the collection of members whose inbox was not big.
-__global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect) {
+// prof (sampled launches only): {inbox messages delivered, of which not provable duplicates, accepted}
+__global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect, unsigned long long* prof) {
   const Ctx c = pctx(P, T);
   const Ctx cs = pctx_sync(P, T);
   const Bufs b = P->b;
@@ -1471,12 +1518,14 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect) {
   const uint32_t t32 = (uint32_t)T;
   const bool any = b.k->msg_total != 0;  // else no receiver has an inbox
   unsigned long long acc = 0, nsync = 0;
+  uint32_t nmsg = 0, nfresh = 0;
   if (any) {  // big inboxes in batches of up to 64 per wave, spread over every wave of the grid
     const uint32_t nbig = b.k->big_cnt;
     const uint32_t nw = gridDim.x * DLV_WAVES;
     const uint32_t bsz = min(64u, max(1u, (nbig + nw - 1) / nw));
     for (uint32_t x = __builtin_amdgcn_readfirstlane((blockIdx.x * DLV_WAVES + wv) * bsz); x < nbig; x += nw * bsz)
-      acc += deliver_big_batch(c, cs, b, b.big_list + x, min(bsz, nbig - x), lane, collect, s_big[wv], nsync);
+      acc += deliver_big_batch(c, cs, b, b.big_list + x, min(bsz, nbig - x), lane, collect, s_big[wv], nsync, nmsg,
+                               nfresh);
   }
   for (uint32_t base = blockIdx.x * DLV_BLOCK; base < c.nl; base += gridDim.x * DLV_BLOCK) {
     if (tid == 0) s_nins = 0;
@@ -1510,7 +1559,8 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect) {
             s_key[j + 1][tid] = kx;
             s_ix[j + 1][tid] = (uint8_t)q;
           }
-          acc += deliver_sorted(c, r, a, k, &s_ix[0][tid], DLV_BLOCK);
+          nmsg += k;
+          acc += deliver_sorted(c, r, a, k, &s_ix[0][tid], DLV_BLOCK, nfresh);
           if (c.mem[i].ins_rank) s_ins[atomicAdd(&s_nins, 1u)] = r;
         }
       }
@@ -1522,6 +1572,14 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect) {
   }
   wave_stat_add(c, ST_GOSSIP_ACCEPTED, acc);
   wave_stat_add(cs, ST_SYNCS, nsync);
+  if (prof) {
+    const unsigned long long a0 = wave_sum(nmsg), a1 = wave_sum(nfresh), a2 = wave_sum(acc);
+    if ((tid & 63) == 0 && (a0 | a1 | a2)) {
+      atomicAdd(prof, a0);
+      atomicAdd(prof + 1, a1);
+      atomicAdd(prof + 2, a2);
+    }
+  }
 }
 
 
@@ -1560,7 +1618,9 @@ enum : uint32_t {
   SF_SENT_LOCAL = 1,  // sent a SYNC delivered to a receiver on this shard (its row is read as content)
   SF_SENT = 2,        // sent a delivered SYNC (it may be merged into in the SYNC_ACK sub-phase)
   SF_RECV = 4,        // received a SYNC (its row is merged into in the SYNC sub-phase)
+  SF_MULTI = 8,       // sent two or more SYNCs: more than one SYNC_ACK may come back
 };
+constexpr uint32_t SF_BITS = 4, SF_MASK = (1u << SF_BITS) - 1;  // sflag = tick << SF_BITS | SF_*
 __device__ inline uint32_t snap_take(const Ctx& c, const Bufs& b, uint32_t i) {
   const uint32_t par = (uint32_t)(c.T & 1);
   const uint32_t slot = atomicAdd(&b.snap_cnt[par], 1u);
@@ -1575,10 +1635,10 @@ __device__ inline uint32_t snap_take(const Ctx& c, const Bufs& b, uint32_t i) {
 // receives (they stream i's row before any merge); k_sync_apply copies i's row again, into a slot
 // of its own for the SYNC_ACK content, only when i's SYNC merges changed it.
 __device__ inline void sflag_set(const Ctx& c, const Bufs& b, uint32_t i, uint32_t bits) {
-  const uint32_t t3 = (uint32_t)c.T << 3;
+  const uint32_t t3 = (uint32_t)c.T << SF_BITS;
   uint32_t old = b.sflag[i];
   for (;;) {
-    const uint32_t base = (old & ~7u) == t3 ? old : t3;
+    const uint32_t base = (old & ~SF_MASK) == t3 ? old : t3;
     const uint32_t nw = base | bits;
     if (nw == old) return;
     const uint32_t prev = atomicCAS(&b.sflag[i], old, nw);
@@ -1595,7 +1655,7 @@ __device__ inline void sflag_set(const Ctx& c, const Bufs& b, uint32_t i, uint32
 }
 __device__ __forceinline__ bool sflag_has(const Ctx& c, const Bufs& b, uint32_t i, uint32_t bits) {
   const uint32_t f = b.sflag[i];
-  return (f & ~7u) == ((uint32_t)c.T << 3) && (f & bits) == bits;
+  return (f & ~SF_MASK) == ((uint32_t)c.T << SF_BITS) && (f & bits) == bits;
 }
 
 constexpr uint32_t SY_INLINE = 4;
@@ -1703,10 +1763,10 @@ __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t
 }
 
 // doSync (:339-357), FD-triggered SYNCs (:427-442) and start0's initial SYNC to every seed (:250-291)
-__device__ inline unsigned long long sync_collect_member(const Ctx& c, const Bufs& b, uint32_t v) {
+// (sn, fl: the member's sync_next and mflag words, loaded by the caller)
+__device__ inline unsigned long long sync_collect_pre(const Ctx& c, const Bufs& b, uint32_t v, uint32_t sn, uint32_t fl) {
   const uint32_t i = v - c.lo, t32 = (uint32_t)c.T;
-  const bool due = c.sync_next[i] == t32;  // the periodic doSync timer fires (sync_on, phase sync_start)
-  const uint32_t fl = c.mflag[i];
+  const bool due = sn == t32;  // the periodic doSync timer fires (sync_on, phase sync_start)
   if (!due && !(fl & (MF_FDSYNC | MF_JOIN))) return 0;
   if (due) c.sync_next[i] = t32 + c.S;
   if (fl & MF_FDSYNC) c.mflag[i] = fl & ~MF_FDSYNC;
@@ -1731,7 +1791,11 @@ __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Buf
       if (s != v && dst(c, s) != v) { add_req(c, b, v, dst(c, s), k++, true); nsync++; }
     }
   }
+  if (k > 1) sflag_set(c, b, i, SF_MULTI);  // (k_sync_apply's lone-SYNC_ACK shortcut needs k = 1)
   return nsync;
+}
+__device__ inline unsigned long long sync_collect_member(const Ctx& c, const Bufs& b, uint32_t v) {
+  return sync_collect_pre(c, b, v, c.sync_next[v - c.lo], c.mflag[v - c.lo]);
 }
 
 
@@ -1850,6 +1914,17 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
         c.spill_ctl[t].avail = (int32_t)(a + f);
         c.spill_ctl[t].freed = 0;
       }
+    }
+  }
+  // timer-wheel pages freed this tick become allocatable (workgroup 1, as above)
+  if (blockIdx.x == (gridDim.x > 1 ? 1u : 0u)) {
+    const int32_t a0 = c.wheel_ctl->avail;
+    const uint32_t a = a0 > 0 ? (uint32_t)a0 : 0u, f = min(c.wheel_ctl->freed, c.wheel_pages - a);
+    for (uint32_t j = threadIdx.x; j < f; j += blockDim.x) c.wheel_avail[a + j] = c.wheel_freed[j];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      c.wheel_ctl->avail = (int32_t)(a + f);
+      c.wheel_ctl->freed = 0;
     }
   }
   // receipt-bitmap slots requested this tick change owner (no other kernel runs now): zeroed bits,

@@ -283,11 +283,6 @@ __device__ __forceinline__ bool lane_holds(uint32_t subject, uint32_t base, uint
   return off < SYNC_CHUNK && ((off & 255u) >> 2) == lane;
 }
 
-__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) x += __shfl_down(x, d, 64);
-  return x;
-}
 
 // D2 = 0: the SYNC launch k_sync_classify (streams every message's two rows, both directions);
 // D2 = 1: the SYNC_ACK launch k_ack_classify (reuses the SYNC launch's reverse results, streams only
@@ -590,16 +585,27 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       if (mod == 0 && (!own || d1 != NONE)) {  // precomputed classification is exact: the row is unchanged
         const uint32_t at = d1 != NONE ? d1 : it;
         const uint32_t tot = d1 != NONE ? b.rev_total[at] : tot_q;
-        if (threadIdx.x == 0 && tot != 0) {
+        if (threadIdx.x < 64 && tot != 0) {
+          // wave 0 reads the chunk results 64 at a time; lane 0 applies the non-empty chunks' complex
+          // records in (chunk, subject) order
+          const uint32_t lane = threadIdx.x;
           const uint2* ic = (d1 != NONE ? b.rev_chunk : ichunk) + (size_t)at * chunks;
-          for (uint32_t ch = 0; ch < chunks; ++ch) {
-            const uint2 e = ic[ch];
-            if (e.y) s_mod = 1;
-            for (uint32_t j = 0; j < e.y; ++j) {
-              const uint32_t xs = b.pool[e.x + j];
-              const uint32_t a = content[xs];
-              if (update_membership(c, s, xs, r_status(a), r_inc(a), reason, phase))
-                pend[npend++] = ((uint64_t)xs << 32) | (uint32_t)r_inc(a);
+          for (uint32_t c0 = 0; c0 < chunks; c0 += 64) {
+            const uint2 e = c0 + lane < chunks ? ic[c0 + lane] : make_uint2(0, 0);
+            uint64_t nz = __ballot(e.y != 0);
+            while (nz) {
+              const int j = __ffsll((unsigned long long)nz) - 1;
+              nz &= nz - 1;
+              const uint32_t base = __shfl(e.x, j, 64), cnt = __shfl(e.y, j, 64);
+              if (lane == 0) {
+                s_mod = 1;
+                for (uint32_t q2 = 0; q2 < cnt; ++q2) {
+                  const uint32_t xs = b.pool[base + q2];
+                  const uint32_t a = content[xs];
+                  if (update_membership(c, s, xs, r_status(a), r_inc(a), reason, phase))
+                    pend[npend++] = ((uint64_t)xs << 32) | (uint32_t)r_inc(a);
+                }
+              }
             }
           }
         }
@@ -629,7 +635,24 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
             a.flags = RQ_DELIVERED | (rq.flags & RQ_INITIAL) | (tsz << RQ_RECS_SHIFT);
             a.content = NONE; a.snap = NONE; a.pad = CLS_REV && rq.content == NONE ? it + 1 : 0;
             valid = true;
-            if (!owned(c, rq.from)) {  // content (this row after the SYNC merges) travels with the ack
+            // the lone SYNC_ACK shortcut: the ack is the only one its receiver gets this tick (it sent
+            // one SYNC and received none, so its row is unchanged since classify), this row did not
+            // change in the SYNC merges, and the reverse classification of the pair found no record
+            // that could change the receiver: its merge is a no-op, so the SYNC_ACK sub-phase's
+            // bookkeeping for it (onSyncAck :385-391: the phase's minor / fetch counters restart, an
+            // INITIAL ack completes a join step, the counters) is done here and nothing is enqueued
+            if (CLS_REV && rq.content == NONE && s_mod == 0 && owned(c, rq.from) &&
+                !sflag_has(c, b, rq.from - c.lo, SF_RECV) && !sflag_has(c, b, rq.from - c.lo, SF_MULTI) &&
+                b.rev_total[it] == 0) {
+              MemberDev& mf = mem(c, rq.from);
+              mf.ev_minor = 0;
+              mf.fetch_ctr = 0;
+              if (rq.flags & RQ_INITIAL) mf.init_done += 1;
+              stat_add(c, ST_SYNC_ACKS, 1);
+              stat_add(c, ST_SYNC_RECORDS, tsz);
+              valid = false;
+            }
+            if (valid && !owned(c, rq.from)) {  // content (this row after the SYNC merges) travels with the ack
               a.pad = 0;
               const uint32_t d = owner(c, rq.from);
               const uint32_t i = atomicAdd(&b.x->ack[d], 1u);

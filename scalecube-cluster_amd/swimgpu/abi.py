@@ -69,6 +69,7 @@ class swim_config(C.Structure):
         ("interval_capacity", C.c_uint32),
         ("deliver_wave_min", C.c_uint32),
         ("delay_capacity", C.c_uint32),
+        ("timer_pool_capacity", C.c_uint32),
     ]
 
 
@@ -203,6 +204,7 @@ PROTOTYPES = {
     "swim_profile_enable": (C.c_int32, [_engp, C.c_int32]),
     "swim_profile_merge": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_profile_fanout": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
+    "swim_profile_deliver": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_philox": (C.c_int32, [_u32p, _u32p, _u32p]),
     "swim_kat_overrides": (C.c_int32, [POINTER(C.c_int32), C.c_uint32, POINTER(C.c_uint8)]),
     "swim_kat_collector": (C.c_int32, [POINTER(C.c_uint8), POINTER(C.c_int64), C.c_uint32, POINTER(C.c_int64)]),
@@ -432,6 +434,12 @@ class Engine:
         """Sampled timing of the gossip fanout kernel (k_gossip_emit), see swim.h."""
         p = swim_kernel_profile()
         _check("swim_profile_fanout", self.lib.swim_profile_fanout(self._h, byref(p)))
+        return {name: getattr(p, name) for name, _ in swim_kernel_profile._fields_}
+
+    def profile_deliver(self) -> dict:
+        """Sampled timing of the gossip delivery kernel (k_gossip_deliver), see swim.h."""
+        p = swim_kernel_profile()
+        _check("swim_profile_deliver", self.lib.swim_profile_deliver(self._h, byref(p)))
         return {name: getattr(p, name) for name, _ in swim_kernel_profile._fields_}
 
     def read_collector(self, m: int, gossiper: int) -> list[tuple[int, int]]:

@@ -12,4 +12,16 @@ sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libswimgpu.so on cuda:0)")
-    config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "slow: long-running test (GPU ones run only with SWIM_GPU_SLOW=1)")
+
+
+def pytest_collection_modifyitems(config, items):
+    """GPU tests marked slow (BASELINE configs at their stated sizes, minutes each) keep the default
+    `-m gpu` suite inside the driver's time limit; they run with SWIM_GPU_SLOW=1 (tools/gpu_slow.sh),
+    and their logs are committed under profiles/."""
+    if os.environ.get("SWIM_GPU_SLOW") == "1":
+        return
+    skip = pytest.mark.skip(reason="long GPU run: set SWIM_GPU_SLOW=1 (tools/gpu_slow.sh)")
+    for it in items:
+        if "gpu" in it.keywords and "slow" in it.keywords:
+            it.add_marker(skip)

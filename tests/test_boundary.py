@@ -57,3 +57,25 @@ def test_create_without_device_reports_edevice():
     with pytest.raises(abi.SwimError) as ei:
         abi.Engine(lib, abi.default_config(lib, 0), 8, 8, 1)
     assert ei.value.code == abi.SWIM_EDEVICE
+
+
+def test_delay_mean_beyond_cap_is_refused():
+    """delays are capped at SWIM_DELAY_TICKS_MAX ticks, so a mean the cap would truncate
+    (above 64 ticks) is refused by the oracle (and, identically, by swim_delay_mean_ok in the GPU
+    engine) instead of silently truncating draws."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
+    import oracle
+    lib = oracle.lib()
+    cfg = abi.default_config(lib)  # LAN: 100 ms ticks
+    e = abi.Engine(lib, cfg, 8, 8, seed=1)
+    tick = cfg.tick_ms or 100  # 0: gcd of the intervals (LAN: 100 ms)
+    assert tick == 100
+    e.set_default_delay(64 * tick)        # at the limit: accepted
+    e.set_link_delay(1, 2, 64 * tick)
+    with pytest.raises(abi.SwimError) as ei:
+        e.set_default_delay(64 * tick + 1)
+    assert ei.value.code == abi.SWIM_EINVAL
+    with pytest.raises(abi.SwimError):
+        e.set_link_delay(1, 2, 64 * tick + 1)
+    e.set_link_delay(1, 2, -1)            # removing an override needs no table

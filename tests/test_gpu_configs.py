@@ -137,8 +137,11 @@ def test_config3_16384_first_periods_match_oracle(glib):
 
 
 def _partition_cfg(lib, n, gossip_capacity):
+    # a partition puts a suspicion timer for every member of the other side at every viewer (N^2 / 2
+    # pending), falling due within the few ticks the SUSPECT gossip took to spread
     return dict(sync_stagger=1, record_fd_events=0, gossip_capacity=gossip_capacity,
-                timer_capacity=max(64 * n, n * n // 2), collector_capacity=1 << (2 * n - 1).bit_length())
+                timer_capacity=max(64 * n, n * n // 2), timer_pool_capacity=n * n // 2 + 64 * n,
+                collector_capacity=1 << (2 * n - 1).bit_length())
 
 
 @pytest.mark.parametrize("n,hold,after", [(256, 52, 8), (128, 20, 10)])
@@ -214,3 +217,123 @@ def test_config5_partition_heal_2048_reconverges(glib):
     assert (removed[other] == 1).all() and (removed[~other] == 0).all()
     assert converged_at is not None, "not converged within 20 periods of the heal"
     assert (added[other] == 1).all() and (added[~other] == 0).all()
+
+
+def _period_log(name):
+    """per-period JSON lines of a long config run, under gpurun_out/ when it exists (GPU box)"""
+    import json
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    f = open(os.path.join(d, f"{name}.jsonl"), "w") if os.path.isdir(d) else None
+
+    def log(**kw):
+        if f:
+            f.write(json.dumps(kw) + "\n")
+            f.flush()
+    return log
+
+
+def _reason_delta(st, prev):
+    return {r: st[f"orig_{r}"] - prev[f"orig_{r}"] for r in abi.ORIG_REASONS if st[f"orig_{r}"] != prev[f"orig_{r}"]}
+
+
+@pytest.mark.slow
+def test_config5_partition_16384_removes_other_side(glib):
+    """BASELINE config 5's partition phase at N = 16,384 on one MI355X (the pre-heal half; its N^2
+    state fits one GPU, the heal's gossip volume does not: DESIGN.md §6): seeds {0, N/2}, a 2-way
+    partition [0, N/2) | [N/2, N) from period 2, held past the suspicion timeout.  Every viewer
+    REMOVEs each member of the other side exactly once and nobody of its own side; no capacity
+    error; the phase's gossips are SUSPECTs originated by the failure detectors (or re-gossiped by a
+    member that learned one through a same-side SYNC first) and nobody refutes (no gossip crosses
+    the cut): swim_stats.gossips_by_reason."""
+    n = 16384
+    cfg = abi.default_config(glib, 0, message_capacity=1 << 28, event_capacity=1 << 27,
+                             **_partition_cfg(glib, n, 1 << 17))
+    e = abi.Engine(glib, cfg, n, n, 5)
+    e.set_seeds([0, n // 2])
+    side = (np.arange(n) >= n // 2).astype(np.int64)
+    timeout_periods = 5 * _ceil_log2(n)
+    hold = timeout_periods + 30
+    log = _period_log("config5_partition_16384")
+    keys = []
+    prev = e.stats()
+    for p in range(2 + hold):
+        if p == 2:
+            e.set_partition(side.astype(np.uint16))
+        e.step(1)
+        ev = e.drain_events(1 << 27)
+        rem = ev[ev["type"] == abi.EV_REMOVED]
+        keys.append(rem["viewer"].astype(np.int64) * n + rem["subject"].astype(np.int64))
+        assert not (ev["type"] == abi.EV_ADDED).any()
+        st = e.stats()
+        log(period=p + 1, gossips=st["gossips_created"] - prev["gossips_created"], by_reason=_reason_delta(st, prev),
+            msgs=st["gossip_messages"] - prev["gossip_messages"], removed=len(rem),
+            timers_fired=st["timers_fired"] - prev["timers_fired"], capacity_errors=st["capacity_errors"])
+        prev = st
+        assert st["capacity_errors"] == 0, f"capacity error in period {p + 1}"
+    keys = np.concatenate(keys)
+    v, s = keys // n, keys % n
+    assert (side[v] != side[s]).all(), "a member of the viewer's own side was removed"
+    assert len(np.unique(keys)) == len(keys), "a member was removed twice by one viewer"
+    assert len(keys) == n * (n // 2), f"{n * (n // 2) - len(keys)} (viewer, other-side member) pairs not removed"
+    st = e.stats()
+    assert st["orig_fd"] > 0 and st["orig_refute"] == 0
+    assert st["orig_fd"] + st["orig_sync"] == st["gossips_created"]
+
+
+@pytest.mark.slow
+def test_config5_heal_4096_reconverges_and_sync_originates_the_storm(glib):
+    """Config 5's heal at N = 4,096 (twice the round-2 size): partition from period 2, held past the
+    suspicion timeout (each side REMOVEs the other), healed through seeds {0, N/2}.  Every viewer
+    REMOVEs each member of the other side exactly once and ADDs it back exactly once; all views are
+    all-ALIVE within 20 periods of the heal; no capacity error.  The gossips originated after the
+    heal come from the SYNC branch of updateMembership (spreadMembershipGossipUnlessGossiped,
+    MembershipProtocolImpl.java:627,652,836-843): a member that learns the other side through a
+    SYNC / SYNC_ACK re-gossips every record it learned — swim_stats.gossips_by_reason['sync']
+    carries (almost) all of them, which is the O(N^2) gossip volume DESIGN.md §6 cites."""
+    n = 4096
+    cfg = abi.default_config(glib, 0, message_capacity=1 << 28, event_capacity=1 << 26,
+                             **_partition_cfg(glib, n, 720_000))
+    e = abi.Engine(glib, cfg, n, n, 5)
+    e.set_seeds([0, n // 2])
+    side = (np.arange(n) >= n // 2).astype(np.int64)
+    hold = 5 * _ceil_log2(n) + 30
+    heal = 2 + hold
+    log = _period_log("config5_heal_4096")
+    removed = np.zeros((n, n), dtype=np.int16)
+    added = np.zeros((n, n), dtype=np.int16)
+    converged_at = None
+    prev = e.stats()
+    at_heal = None
+    for p in range(heal + 20):
+        if p == 2:
+            e.set_partition(side.astype(np.uint16))
+        if p == heal:
+            assert (removed.sum(axis=1) == n // 2).all()
+            e.set_partition(None)
+            at_heal = e.stats()
+        e.step(1)
+        ev = e.drain_events(1 << 26)
+        for typ, acc in ((abi.EV_REMOVED, removed), (abi.EV_ADDED, added)):
+            x = ev[ev["type"] == typ]
+            np.add.at(acc, (x["viewer"].astype(np.int64), x["subject"].astype(np.int64)), 1)
+        st = e.stats()
+        glen = max(e.read_member(m)["gossip_len"] for m in range(0, n, 257))
+        log(period=p + 1, gossips=st["gossips_created"] - prev["gossips_created"], by_reason=_reason_delta(st, prev),
+            msgs=st["gossip_messages"] - prev["gossip_messages"], syncs=st["syncs"] - prev["syncs"],
+            events=len(ev), max_live_gossips_sampled=glen, capacity_errors=st["capacity_errors"])
+        prev = st
+        assert st["capacity_errors"] == 0, f"capacity error in period {p + 1}"
+        if p >= heal and converged_at is None:
+            if all(((((row := e.read_view(v)) >> 34) & 1) == 1).all() and (((row >> 32) & 3) == 0).all()
+                   for v in range(n)):
+                converged_at = p + 1
+                break
+    other = side[:, None] != side[None, :]
+    assert (removed[other] == 1).all() and (removed[~other] == 0).all()
+    assert converged_at is not None, "not converged within 20 periods of the heal"
+    assert (added[other] == 1).all() and (added[~other] == 0).all()
+    st = e.stats()
+    healed = {r: st[f"orig_{r}"] - at_heal[f"orig_{r}"] for r in abi.ORIG_REASONS}
+    total = sum(healed.values())
+    log(heal_gossips_by_reason=healed, converged_at=converged_at)
+    assert healed["sync"] >= 0.9 * total, healed

@@ -101,8 +101,24 @@ def test_gpu_parity_config2_1024(glib, olib):
 # GOSSIP_REQ / SYNC / SYNC_ACK traffic exactly as the RCCL ranks do (cfg.local_shards), compared with
 # the UNSHARDED oracle: sharding must not change a single bit.  3 shards over 4 members leaves the
 # last shard empty; over 3 members every shard owns one row.
-@pytest.mark.parametrize("shards", [2, 3])
-@pytest.mark.parametrize("sc", scenarios.catalog(), ids=lambda s: s.name)
+# the longest scenario (config3_rates_200, ~70 s a run) runs unsharded, with 3 shards and through
+# the pull route with 3 shards in the default suite; its other variants are marked slow (run with
+# SWIM_GPU_SLOW=1, tools/gpu_slow.sh) to keep `-m gpu` inside the driver's time limit
+SLOW_SCENARIOS = ("config3_rates_200",)
+
+
+def _cases(shard_list=None):
+    out = []
+    for sc in scenarios.catalog():
+        for sh in (shard_list or [None]):
+            slow = sc.name in SLOW_SCENARIOS and sh != 3
+            args = (sc,) if sh is None else (sc, sh)
+            out.append(pytest.param(*args, id=sc.name if sh is None else f"{sc.name}-{sh}",
+                                    marks=[pytest.mark.slow] if slow else []))
+    return out
+
+
+@pytest.mark.parametrize("sc,shards", _cases([2, 3]))
 def test_gpu_sharded_parity_scenario(glib, olib, sc, shards):
     if not sc.shardable:
         pytest.skip("message delay is single-shard only")
@@ -114,8 +130,9 @@ def test_gpu_sharded_parity_scenario(glib, olib, sc, shards):
 PULL_SCENARIOS = ("mp_joins_via_seed", "churn_48", "config3_rates_200", "partition_heal_32", "restart_same_address_40")
 
 
-@pytest.mark.parametrize("shards", [2, 3])
-@pytest.mark.parametrize("name", PULL_SCENARIOS)
+@pytest.mark.parametrize("name,shards", [
+    pytest.param(nm, sh, id=f"{nm}-{sh}", marks=[pytest.mark.slow] if nm in SLOW_SCENARIOS and sh != 3 else [])
+    for nm in PULL_SCENARIOS for sh in (2, 3)])
 def test_gpu_sharded_pull_parity_scenario(glib, olib, name, shards, monkeypatch):
     sc = {s.name: s for s in scenarios.catalog()}[name]
     monkeypatch.setenv("SWIM_EXCHANGE_PULL", "1")
@@ -158,6 +175,7 @@ def test_gpu_matches_golden_digest(glib, sc, shards):
 
 # ---- the wave-parallel delivery path (deliver_big: stable-by-sender canonical ranking, wave-batched
 # pingMembers inserts) for EVERY gossip inbox, not only the big ones of a storm
-@pytest.mark.parametrize("sc", scenarios.catalog(), ids=lambda s: s.name)
+@pytest.mark.parametrize("sc", [pytest.param(sc, id=sc.name, marks=[pytest.mark.slow] if sc.name in SLOW_SCENARIOS else [])
+                                for sc in scenarios.catalog()])
 def test_gpu_parity_wave_delivery(glib, olib, sc):
     _run_parity(glib, olib, dataclasses.replace(sc, cfg={**sc.cfg, "deliver_wave_min": 1}))

@@ -58,12 +58,14 @@ def main():
     cfg.interval_capacity = args.interval_capacity
     # a partition puts a suspicion timer for every member of the other side at every viewer, falling
     # due within the few ticks the SUSPECT gossip took to spread
-    cfg.timer_capacity = max(64 * n, n * n // 8)
+    cfg.timer_capacity = max(64 * n, n * n // 2)
+    cfg.timer_pool_capacity = n * n // 2 + 64 * n  # N/2 pending timers at every viewer
     sample = [int(x) for x in np.linspace(0, n - 1, args.sample)]
     if args.workload == "churn":
         sch = bench.Schedule("churn", n, args.periods)
         cfg.collector_capacity = 1 << (2 * sch.capacity - 1).bit_length()
         cfg.timer_capacity = 64 * sch.capacity
+        cfg.timer_pool_capacity = 1 << 28 if sch.capacity > 12288 else 1 << 27
         e = abi.Engine(lib, cfg, sch.capacity, n, 1)
         sch.setup(e)
         plan = [(p, sch.ops(p)) for p in range(args.periods)]
@@ -103,6 +105,8 @@ def main():
         glen = max(e.read_member(m)["gossip_len"] for m in sample)
         print(json.dumps({"period": p + 1, "s": round(time.time() - t1, 3),
                           "gossips": st["gossips_created"] - prev["gossips_created"],
+                          "by_reason": {r: st[f"orig_{r}"] - prev[f"orig_{r}"] for r in abi.ORIG_REASONS
+                                        if st[f"orig_{r}"] != prev[f"orig_{r}"]},
                           "msgs": st["gossip_messages"] - prev["gossip_messages"],
                           "syncs": st["syncs"] - prev["syncs"], "events": len(ev),
                           "removed": int((ev["type"] == abi.EV_REMOVED).sum()) if len(ev) else 0,
@@ -126,8 +130,10 @@ def main():
             st = (row >> 32) & 3
             intab = (row >> 34) & 1
             ok += int(intab.all() and (st == 0).all())
+        st = e.stats()
         print(json.dumps({"converged_sampled": ok, "sampled": len(sample), "wall_s": round(time.time() - t0, 1),
-                          "events_total": ev_total}), flush=True)
+                          "events_total": ev_total, "capacity_errors": st["capacity_errors"],
+                          "gossips_by_reason": {r: st[f"orig_{r}"] for r in abi.ORIG_REASONS}}), flush=True)
     return 0
 
 
