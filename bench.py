@@ -255,7 +255,9 @@ def step_roofline(stats, prof, fprof, dprof, ticks, gossip_ticks, dt, steps, wor
         doc = json.load(open(paths[-1]))
         calls = {r["kernel"]: int(r["calls"]) for r in csv.DictReader(open(kst[-1]))}
         ticks_prof = max(1, calls.get("k_end_tick", 1))
-        per_tick = sum(v.get("hbm_bytes_per_launch", 0.0) * calls.get(k, 0) for k, v in doc["kernels"].items()) / ticks_prof
+        tick_kernel = lambda k: k.startswith("k_") and not k.startswith(("k_init", "k_kat"))  # not setup / copies
+        per_tick = sum(v.get("hbm_bytes_per_launch", 0.0) * calls.get(k, 0) for k, v in doc["kernels"].items()
+                       if tick_kernel(k)) / ticks_prof
         traffic, src = per_tick * ticks / steps, os.path.relpath(paths[-1], REPO)
     return {"bound": "hbm", "scope": "step (one protocol period, every kernel)", "achieved": ach,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,

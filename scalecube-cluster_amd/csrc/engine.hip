@@ -45,7 +45,10 @@ constexpr uint32_t kApplyGrid = 256;      // grid-stride over receivers
 // 4,096 waves, one gossip sender at a time each: all resident at the kernel's occupancy (4 waves per
 // SIMD); 2,048 workgroups (two rounds of waves) measured 7 % slower in a storm, 512 8 % slower
 constexpr uint32_t kEmitGrid = EMIT_GRID;
-constexpr uint32_t kDeliverGrid = 512;    // 2,048 waves (two workgroups per CU) for the big inboxes of a storm
+#ifndef DLV_GRID
+#define DLV_GRID 512
+#endif
+constexpr uint32_t kDeliverGrid = DLV_GRID;  // 2,048 waves (two workgroups per CU) for the big inboxes of a storm
 constexpr uint32_t kStopCap = 4096;
 constexpr uint32_t kProfEvery = 3;  // SYNC classify launches between timed ones
 constexpr uint64_t kRebaseEvery = 16;  // ticks between rebases of the SYNC block witness (k_end_tick)

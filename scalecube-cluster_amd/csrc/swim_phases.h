@@ -1634,9 +1634,9 @@ __device__ inline uint32_t snap_take(const Ctx& c, const Bufs& b, uint32_t i) {
 // table after its SYNC merges).  k_sync_classify fills the slot from the units of the SYNCs i
 // receives (they stream i's row before any merge); k_sync_apply copies i's row again, into a slot
 // of its own for the SYNC_ACK content, only when i's SYNC merges changed it.
-__device__ inline void sflag_set(const Ctx& c, const Bufs& b, uint32_t i, uint32_t bits) {
+// (old: the caller's guess of the word, loaded early; a stale guess only costs a CAS retry)
+__device__ inline void sflag_set_from(const Ctx& c, const Bufs& b, uint32_t i, uint32_t bits, uint32_t old) {
   const uint32_t t3 = (uint32_t)c.T << SF_BITS;
-  uint32_t old = b.sflag[i];
   for (;;) {
     const uint32_t base = (old & ~SF_MASK) == t3 ? old : t3;
     const uint32_t nw = base | bits;
@@ -1652,6 +1652,9 @@ __device__ inline void sflag_set(const Ctx& c, const Bufs& b, uint32_t i, uint32
     }
     old = prev;
   }
+}
+__device__ __forceinline__ void sflag_set(const Ctx& c, const Bufs& b, uint32_t i, uint32_t bits) {
+  sflag_set_from(c, b, i, bits, b.sflag[i]);
 }
 __device__ __forceinline__ bool sflag_has(const Ctx& c, const Bufs& b, uint32_t i, uint32_t bits) {
   const uint32_t f = b.sflag[i];
@@ -1704,27 +1707,32 @@ __device__ inline uint32_t sy_page_wait(const Ctx& c, const Bufs& b, const SyInb
 
 // a delivered SYNC / SYNC_ACK joins its receiver's inbox (the receiver is owned by this shard).
 // The item's classification counters start at zero here, before any classify launch adds to them.
-__device__ inline void enqueue_sync(const Ctx& c, const Bufs& b, int d2, SyncReq q, bool valid) {
+// (rsf: a guess of the receiver's sflag word, see sflag_set_from)
+__device__ inline void enqueue_sync(const Ctx& c, const Bufs& b, int d2, SyncReq q, bool valid, uint32_t rsf) {
   const SyInbox x = sy_inbox(b, d2);
   uint32_t it = NONE, s = 0, pid = NONE, r = 0;
   if (valid) {
-    it = atomicAdd(x.total, 1u);
-    if (it >= b.req_cap) { set_err(c, ERR_REQS); valid = false; }
-  }
-  if (valid) {
+    // the item and the inbox slot are taken together (two independent atomics in flight at once); an
+    // item beyond the capacity (ERR_REQS) still takes its slot, as NONE, which readers skip
     r = q.to - c.lo;
+    it = atomicAdd(x.total, 1u);
     s = atomicAdd(&x.cnt[r], 1u);
-    q.slot = s;
-    x.items[it] = q;
-    if (!d2) {
-      b.item_total[it] = 0;
-      b.rev_total[it] = 0;
+    if (it >= b.req_cap) {
+      set_err(c, ERR_REQS);
+      it = NONE;
     } else {
-      b.ack_ctot[it] = 0;
+      q.slot = s;
+      x.items[it] = q;
+      if (!d2) {
+        b.item_total[it] = 0;
+        b.rev_total[it] = 0;
+      } else {
+        b.ack_ctot[it] = 0;
+      }
     }
     if (s == 0) {
       x.recv[atomicAdd(x.recv_cnt, 1u)] = q.to;
-      if (!d2) sflag_set(c, b, r, SF_RECV);
+      if (!d2) sflag_set_from(c, b, r, SF_RECV, rsf);
     }
     if (s < SY_INLINE) {
       x.inl[(size_t)r * SY_INLINE + s] = it;
@@ -1736,6 +1744,9 @@ __device__ inline void enqueue_sync(const Ctx& c, const Bufs& b, int d2, SyncReq
   wave_order();
   if (valid && ((s - SY_INLINE) & 63) != 0) pid = sy_page_wait(c, b, x, r, (s - SY_INLINE) >> 6);
   if (valid && pid != NONE) x.pool[(size_t)pid * 64 + ((s - SY_INLINE) & 63)] = it;
+}
+__device__ __forceinline__ void enqueue_sync(const Ctx& c, const Bufs& b, int d2, SyncReq q, bool valid) {
+  enqueue_sync(c, b, d2, q, valid, valid && !d2 ? b.sflag[q.to - c.lo] : 0u);
 }
 
 __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t to, uint32_t ordinal, bool initial) {
@@ -1764,10 +1775,57 @@ __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t
 
 // doSync (:339-357), FD-triggered SYNCs (:427-442) and start0's initial SYNC to every seed (:250-291)
 // (sn, fl: the member's sync_next and mflag words, loaded by the caller)
+// The common case, a periodic doSync and nothing else, with no per-link settings, partition or
+// address routing: selectSyncAddress's first draw almost always names a member, so everything the
+// SYNC needs — the candidate's membership and seed words, the sender's up / table size / loss, the
+// candidate's up / inbound filter and both members' sflag words — is loaded in ONE batch before any
+// decision, and the item / inbox counters are taken together: the collection costs a few dependent
+// round trips instead of a dozen.  Same draws, same decisions, same results as the general path
+// (when the first draw does not name a member, select_sync_address takes over from scratch).
+__device__ inline unsigned long long sync_collect_fast(const Ctx& c, const Bufs& b, uint32_t v) {
+  const uint32_t i = v - c.lo, t32 = (uint32_t)c.T;
+  c.sync_next[i] = t32 + c.S;
+  const uint32_t x0 = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 0, 0), c.n);
+  MemberDev& m = mem(c, v);
+  // ---- one batch of independent loads
+  const uint8_t upv = c.up[v], upx = c.up[x0], seedx = c.is_seed[x0], inbx = c.default_inbound[x0];
+  const uint8_t lossv = c.default_loss[v];
+  const uint32_t ax = aux_row(c, v)[x0], tsz = m.table_size;
+  const uint32_t sfv = b.sflag[i];
+  const bool x_local = owned(c, x0);
+  const uint32_t sfx = x_local ? b.sflag[x0 - c.lo] : 0u;
+  if (!upv) return 0;  // (fd_sync_cnt is already 0: no MF_FDSYNC)
+  uint32_t t = x0;
+  if (!(x0 != v && ((ax & A_IN_MEMBERS) || seedx))) {
+    t = select_sync_address(c, v);
+    if (t == NONE) return 0;
+  }
+  SyncReq q;
+  q.from = v; q.to = t; q.ordinal = 0; q.slot = 0;
+  q.flags = tsz << RQ_RECS_SHIFT;
+  q.content = NONE; q.snap = NONE; q.pad = 0;
+  const bool up_t = t == x0 ? upx != 0 : c.up[t] != 0;
+  if (!up_t || lost_k(c, lossv, v, SWIM_STREAM_SYNC_OUT, 0, 0)) return 1;  // tryFailOutbound
+  if (!(t == x0 ? inbx : c.default_inbound[t])) return 1;                   // inbound-blocked: dropped
+  q.flags |= RQ_DELIVERED;
+  const bool local = owned(c, t);
+  sflag_set_from(c, b, i, local ? SF_SENT | SF_SENT_LOCAL : SF_SENT, sfv);
+  if (!local) {  // content (this row) travels with the request: k_pack_rows
+    const uint32_t d = owner(c, t);
+    const uint32_t k = atomicAdd(&b.x->req[d], 1u);
+    if (k >= b.tx_req_cap) { set_err(c, ERR_REQS); return 1; }
+    b.tx_reqs[(size_t)d * b.tx_req_cap + k] = q;
+    return 1;
+  }
+  enqueue_sync(c, b, 0, q, true, t == x0 ? sfx : b.sflag[t - c.lo]);
+  return 1;
+}
+
 __device__ inline unsigned long long sync_collect_pre(const Ctx& c, const Bufs& b, uint32_t v, uint32_t sn, uint32_t fl) {
   const uint32_t i = v - c.lo, t32 = (uint32_t)c.T;
   const bool due = sn == t32;  // the periodic doSync timer fires (sync_on, phase sync_start)
   if (!due && !(fl & (MF_FDSYNC | MF_JOIN))) return 0;
+  if (due && !(fl & (MF_FDSYNC | MF_JOIN)) && !c.n_links && !c.partition && !c.route) return sync_collect_fast(c, b, v);
   if (due) c.sync_next[i] = t32 + c.S;
   if (fl & MF_FDSYNC) c.mflag[i] = fl & ~MF_FDSYNC;
   MemberDev& m = mem(c, v);
@@ -1902,22 +1960,21 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
     if (i == 0) b.snap_cnt[par ^ 1u] = 0;
     if (i == 0 && c.delay_on) b.dq_cnt[(uint32_t)T & DQ_MASK] = 0;  // this tick's delayed arrivals are delivered
   }
-  // collector blocks freed this tick become allocatable (one workgroup: the counters are read,
-  // then rewritten, by the same threads)
-  if (blockIdx.x == 0) {
-    for (int t = 0; t < NTIER; ++t) {
-      const int32_t a0 = c.spill_ctl[t].avail;
-      const uint32_t a = a0 > 0 ? (uint32_t)a0 : 0u, f = min(c.spill_ctl[t].freed, c.spill_cap[t] - a);
-      for (uint32_t j = threadIdx.x; j < f; j += blockDim.x) c.spill_avail[t][a + j] = c.spill_freed[t][j];
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        c.spill_ctl[t].avail = (int32_t)(a + f);
-        c.spill_ctl[t].freed = 0;
-      }
+  // collector blocks freed this tick become allocatable: tier t by workgroup t (the counters are
+  // read, then rewritten, by the same threads), all tiers by workgroup 0 in a grid of fewer than 5
+  for (int t = 0; t < NTIER; ++t) {
+    if (blockIdx.x != (gridDim.x > NTIER ? (uint32_t)t : 0u)) continue;
+    const int32_t a0 = c.spill_ctl[t].avail;
+    const uint32_t a = a0 > 0 ? (uint32_t)a0 : 0u, f = min(c.spill_ctl[t].freed, c.spill_cap[t] - a);
+    for (uint32_t j = threadIdx.x; j < f; j += blockDim.x) c.spill_avail[t][a + j] = c.spill_freed[t][j];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      c.spill_ctl[t].avail = (int32_t)(a + f);
+      c.spill_ctl[t].freed = 0;
     }
   }
-  // timer-wheel pages freed this tick become allocatable (workgroup 1, as above)
-  if (blockIdx.x == (gridDim.x > 1 ? 1u : 0u)) {
+  // timer-wheel pages freed this tick become allocatable (workgroup NTIER, as above)
+  if (blockIdx.x == (gridDim.x > NTIER ? (uint32_t)NTIER : 0u)) {
     const int32_t a0 = c.wheel_ctl->avail;
     const uint32_t a = a0 > 0 ? (uint32_t)a0 : 0u, f = min(c.wheel_ctl->freed, c.wheel_pages - a);
     for (uint32_t j = threadIdx.x; j < f; j += blockDim.x) c.wheel_avail[a + j] = c.wheel_freed[j];

@@ -292,7 +292,7 @@ def test_config5_heal_4096_reconverges_and_sync_originates_the_storm(glib):
     carries (almost) all of them, which is the O(N^2) gossip volume DESIGN.md §6 cites."""
     n = 4096
     cfg = abi.default_config(glib, 0, message_capacity=1 << 28, event_capacity=1 << 26,
-                             **_partition_cfg(glib, n, 720_000))
+                             **_partition_cfg(glib, n, 800_000))
     e = abi.Engine(glib, cfg, n, n, 5)
     e.set_seeds([0, n // 2])
     side = (np.arange(n) >= n // 2).astype(np.int64)
