@@ -782,7 +782,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&b.rq_inl, (size_t)std::max(nl, 1u) * SY_INLINE) && sd.alloc(&b.ack_inl, (size_t)std::max(nl, 1u) * SY_INLINE) &&
             sd.alloc(&b.rq_tab, (size_t)std::max(nl, 1u) * b.sy_max) && sd.alloc(&b.rq_pool, (size_t)b.sy_pool_cap * 64) &&
             sd.alloc(&b.ack_tab, (size_t)std::max(nl, 1u) * b.sy_max) && sd.alloc(&b.ack_pool, (size_t)b.sy_pool_cap * 64) &&
-            sd.alloc(&b.ack_snap, nl) && sd.alloc(&b.sflag, nl) &&
+            sd.alloc(&b.ack_snap, nl) && sd.alloc(&b.snap_ready, nl) && sd.alloc(&b.sflag, nl) &&
             sd.alloc(&b.ack_chunk, (size_t)b.req_cap * b.chunks) && sd.alloc(&b.ack_ctot, b.req_cap) &&
             sd.alloc(&b.ack_recv, nl) && 
             sd.alloc(&b.snap, (size_t)b.snap_cap * n) && sd.alloc(&b.snap_idx, nl) &&
@@ -847,6 +847,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(b.ack_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.snap_idx, 0xff, 4 * (size_t)nl, s);
   hipMemsetAsync(b.ack_snap, 0xff, 4 * (size_t)nl, s);
+  hipMemsetAsync(b.snap_ready, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.sflag, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.rq_tab, 0xff, 4 * (size_t)std::max(nl, 1u) * b.sy_max, s);
   hipMemsetAsync(b.ack_tab, 0xff, 4 * (size_t)std::max(nl, 1u) * b.sy_max, s);

@@ -45,7 +45,7 @@ enum : uint32_t {
 enum { ST_TICKS, ST_PINGS, ST_PING_REQS, ST_FD_EVENTS, ST_GOSSIPS_CREATED, ST_GOSSIP_MESSAGES,
        ST_GOSSIP_ACCEPTED, ST_SYNCS, ST_SYNC_ACKS, ST_SYNC_RECORDS, ST_FETCHES, ST_FETCH_OK,
        ST_TIMERS_FIRED, ST_EVENTS, ST_CAPACITY_ERRORS,
-       ST_MERGE_MSGS, ST_MERGE_RECORDS,  // swim_profile_merge accounting
+       ST_MERGE_MSGS, ST_MERGE_RECORDS,  // (unused slots, kept for the stats layout)
        ST_ORIG0,  // 7 slots: gossips_created by SWIM_ORIG_* reason (swim_stats.gossips_by_reason)
        ST_COUNT = ST_ORIG0 + 7 };
 static_assert(ST_COUNT == 24, "stats slots");

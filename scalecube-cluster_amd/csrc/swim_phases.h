@@ -111,7 +111,8 @@ struct Bufs {
   uint32_t* snap;       // [snap_cap][n] record rows
   uint32_t snap_cap;
   uint32_t* snap_idx;   // per member: SYNC-content slot or NONE
-  uint32_t* ack_snap;   // per member: SYNC_ACK-content slot or NONE
+  uint32_t* ack_snap;   // per member: SYNC_ACK-content slot or NONE (the same slot as snap_idx)
+  uint32_t* snap_ready; // per member: tick << 2 | 1 (2): the slot holds its SYNC (SYNC_ACK) content
   uint32_t* snap_list;  // [2][snap_cap] members holding slots, by tick parity
   uint32_t* snap_cnt;   // [2] slots taken, by tick parity
   uint32_t* sflag;      // per member: tick << SF_BITS | SF_* bits of this tick

@@ -25,6 +25,9 @@
 #ifndef CLS_MINWAVES
 #define CLS_MINWAVES 4  // waves per SIMD the classify kernels are register-limited to
 #endif
+#ifndef ACK_NORECV_EXPERIMENT
+#define ACK_NORECV_EXPERIMENT 0  // timing experiment only (NOT exact): lone-ack shortcut ignores SF_RECV
+#endif
 #ifndef CLS_SKIPZERO
 #define CLS_SKIPZERO 0  // timing experiment only: skip the stores of empty chunk results (NOT exact)
 #endif
@@ -164,13 +167,6 @@ __device__ __forceinline__ const uint32_t* remote_row(const Ctx& c, const Bufs& 
   const uint32_t p = content / b.row_cap;
   if (p >= (uint32_t)MAXW) return c.recs;
   return b.peers->rows_in[d2][p] + (size_t)(content - p * b.row_cap) * c.n;
-}
-
-// the record row a SYNC / SYNC_ACK carries: received copy, snapshot, or the sender's live row
-__device__ __forceinline__ const uint32_t* sync_content(const Ctx& c, const Bufs& b, const SyncReq& q, int d2) {
-  if (q.content != NONE) return remote_row(c, b, d2, q.content);
-  const uint32_t si = (d2 ? b.ack_snap : b.snap_idx)[q.from - c.lo];
-  return si < b.snap_cap ? b.snap + (size_t)si * c.n : rec_row(c, q.from);
 }
 
 // One (message, chunk) unit per wave: 64 lanes x 16 subjects = SYNC_CHUNK subjects, i.e. four
@@ -322,8 +318,7 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
       // stamps, both block counts and the self subjects' ref words
       const bool local = hc.bdc != nullptr;
       const bool r_here = hc.r - base < (uint32_t)SYNC_CHUNK, s_here = hc.rev && hc.s - base < (uint32_t)SYNC_CHUNK;
-      uint32_t sn = NONE, rmf = 0, rmt = 0, dc = 1, dv = 1, rfr = 0, rfs = 0;
-      if (!d2) sn = b.snap_idx[hc.r - c.lo];
+      uint32_t rmf = 0, rmt = 0, dc = 1, dv = 1, rfr = 0, rfs = 0;
       if (d2 && local && hc.pad) {
         rmf = b.row_mod[hc.s - c.lo];
         rmt = b.row_mod[hc.r - c.lo];
@@ -334,13 +329,11 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
       }
       if (r_here) rfr = c.ref[hc.r];
       if (s_here) rfs = c.ref[hc.s];
-      sn = uni(sn);
-      uint32_t* const snapdst = sn < b.snap_cap ? b.snap + (size_t)sn * c.n : nullptr;
       const uint32_t t32 = (uint32_t)c.T;
       const uint32_t d1 = (d2 && local && hc.pad && uni(rmf) != t32 && uni(rmt) != t32) ? hc.pad - 1 : NONE;
       // an identical record on a viewer's own subject is complex when it is LEAVING (sync_complex)
       const auto leaving = [](uint32_t rf) { return r_in_table(rf) && r_status(rf) == SWIM_LEAVING; };
-      if (CLS_WITNESS && d1 == NONE && !snapdst && local) {  // (a snapshot needs the row streamed)
+      if (CLS_WITNESS && d1 == NONE && local) {
         if (CLS_WITNESS == 3) dc = dv = 0;
         if ((uni(dc) | uni(dv)) == 0 && !(r_here && leaving(uni(rfr))) && !(s_here && leaving(uni(rfs)))) {
           if (lane == 0 && CLS_WITNESS != 2) {
@@ -352,18 +345,7 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
         }
       }
       uint4 a[CLS_LOADS], o[CLS_LOADS];
-      if (d1 == NONE || snapdst) cls_rows(c, hc, ch, lane, a, o);
-      if (snapdst) {
-#pragma unroll
-        for (int j = 0; j < CLS_LOADS; ++j) {
-          const uint32_t av[4] = {o[j].x, o[j].y, o[j].z, o[j].w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint32_t x = base + j * 256 + 4 * lane + q;
-            if (x < n) snapdst[x] = av[q];
-          }
-        }
-      }
+      if (d1 == NONE) cls_rows(c, hc, ch, lane, a, o);
       if (d1 != NONE) {
         // SYNC_ACK whose classification the SYNC launch already made
         if (lane == 0) {
@@ -415,17 +397,13 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
       }
     }
   }
-  // the message record counts (sync_records) are taken from the headers by k_sync_apply; only
-  // non-zero counts are added (thousands of waves skip every unit: one atomic each on the same
-  // address would serialise the launch), the unit total is stored once
+  // the message record counts (sync_records) are taken from the headers by k_sync_apply; the work
+  // counters are kept only on profiled launches (same-address atomics from every streaming wave
+  // would serialise the launch), the unit total is stored once
   (void)skipped;
-  if (lane == 0 && (cplx || streamed)) {
-    if (cplx) stat_add(c, ST_MERGE_RECORDS, cplx);
-    if (streamed) stat_add(c, ST_MERGE_MSGS, streamed);
-    if (prof) {
-      if (streamed) atomicAdd(prof, (unsigned long long)streamed);
-      if (cplx) atomicAdd(prof + 1, (unsigned long long)cplx);
-    }
+  if (prof && lane == 0 && (cplx || streamed)) {
+    if (streamed) atomicAdd(prof, (unsigned long long)streamed);
+    if (cplx) atomicAdd(prof + 1, (unsigned long long)cplx);
   }
   if (prof && wid == 0 && lane == 0) prof[2] = total;
 }
@@ -435,22 +413,70 @@ __global__ void __launch_bounds__(CLS_BLOCK, CLS_MINWAVES) k_sync_classify(KP, u
 }
 __global__ void __launch_bounds__(CLS_BLOCK, CLS_MINWAVES) k_ack_classify(KP) { classify_body<1>(P, T, nullptr); }
 
+// ---- message content under concurrent merges (lazy snapshots).  A SYNC carries its sender's row
+// as it was before the SYNC merges (prepareSyncDataMsg :485-489), a SYNC_ACK its acker's row as it
+// was before the SYNC_ACK merges.  A member whose row is read as such content by another receiver's
+// workgroup while its own workgroup merges into it (it both sent and received this tick: sflag
+// SENT | RECV, which claimed a snapshot slot at collection) copies its row into the slot just
+// before its FIRST change of the sub-phase and then publishes snap_ready = tick << 2 | phase bit;
+// a row that no merge changes is never copied (every quiet tick).  A reader takes the slot once it
+// is published, else the live row — and re-checks the flag after the read: a value read while the
+// flag was still unpublished predates every change (the writer changes nothing before publishing).
+struct Content {
+  const uint32_t* live;
+  const uint32_t* snap;   // the sender's slot, or nullptr when no merge can change the live row now
+  const uint32_t* ready;  // its snap_ready word
+  uint32_t want;
+};
+__device__ __forceinline__ uint32_t snap_want(const Ctx& c, int d2) { return ((uint32_t)c.T << 2) | (d2 ? 2u : 1u); }
+__device__ __forceinline__ bool snap_published(const Content& k) {
+  return __hip_atomic_load(k.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == k.want;
+}
+__device__ inline uint32_t content_at(const Content& k, uint32_t x) {
+  if (!k.snap) return k.live[x];
+  if (snap_published(k)) return k.snap[x];
+  const uint32_t v = k.live[x];
+  __threadfence();  // the value is in before the flag is read again
+  return snap_published(k) ? k.snap[x] : v;
+}
+// the content of message q (received rows, the sender's slot or its live row)
+__device__ __forceinline__ Content msg_content(const Ctx& c, const Bufs& b, const SyncReq& q, int d2) {
+  if (q.content != NONE) return Content{remote_row(c, b, d2, q.content), nullptr, nullptr, 0};
+  const uint32_t i = q.from - c.lo;
+  const uint32_t si = (d2 ? b.ack_snap : b.snap_idx)[i];
+  if (si >= b.snap_cap) return Content{rec_row(c, q.from), nullptr, nullptr, 0};
+  return Content{rec_row(c, q.from), b.snap + (size_t)si * c.n, b.snap_ready + i, snap_want(c, d2)};
+}
+
 // In-workgroup merge of one message (used when the receiver's row changed earlier in this
 // sub-phase, so the precomputed classification may be stale).  Returns through *s_mod whether any
 // record could change the row.
-__device__ void merge_row_wg(const Ctx& c, uint32_t v, const uint32_t* __restrict__ content, int reason,
+__device__ void merge_row_wg(const Ctx& c, uint32_t v, const Content& kc, int reason,
                              uint32_t phase, uint64_t* pend, uint32_t& npend, uint32_t* s_list, uint32_t* s_wave,
                              uint32_t* s_mod) {
   const uint32_t* __restrict__ rv = rec_row(c, v);
   const uint32_t n = c.n;
+  __shared__ uint32_t s_pub;
+  const uint32_t* content = kc.snap && snap_published(kc) ? kc.snap : kc.live;
   for (uint32_t base = 0; base < n; base += APPLY_TILE) {
     const uint32_t x0 = base + threadIdx.x * APPLY_CPT;
     uint32_t flags = 0;
-    for (int k = 0; k < APPLY_CPT; ++k) {
-      const uint32_t x = x0 + k;
-      if (x >= n) break;
-      const uint32_t a = content[x];
-      if (r_in_table(a) && sync_complex(a, rv[x], x == v)) flags |= 1u << k;
+    for (int pass = 0; pass < 2; ++pass) {
+      flags = 0;
+      for (int k = 0; k < APPLY_CPT; ++k) {
+        const uint32_t x = x0 + k;
+        if (x >= n) break;
+        const uint32_t a = content[x];
+        if (r_in_table(a) && sync_complex(a, rv[x], x == v)) flags |= 1u << k;
+      }
+      if (!kc.snap || content == kc.snap) break;
+      // read from the live row: valid unless the sender published its copy meanwhile
+      __threadfence();
+      __syncthreads();
+      if (threadIdx.x == 0) s_pub = snap_published(kc) ? 1u : 0u;
+      __syncthreads();
+      if (!s_pub) break;
+      content = kc.snap;  // (uniform) the tile again, from the copy
     }
     uint32_t total;
     const uint32_t off = block_exclusive_scan<APPLY_BLOCK>((uint32_t)__popc(flags), s_wave, &total);
@@ -463,7 +489,7 @@ __device__ void merge_row_wg(const Ctx& c, uint32_t v, const uint32_t* __restric
       *s_mod = 1;
       for (uint32_t i = 0; i < total; ++i) {
         const uint32_t x = s_list[i];
-        const uint32_t a = content[x];
+        const uint32_t a = content == kc.snap ? kc.snap[x] : content_at(kc, x);
         if (update_membership(c, v, x, r_status(a), r_inc(a), reason, phase))
           pend[npend++] = ((uint64_t)x << 32) | (uint32_t)r_inc(a);
       }
@@ -555,10 +581,11 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
   for (uint32_t ri = blockIdx.x; ri < nrecv; ri += gridDim.x) {
     const uint32_t s = x.recv[ri];
     const uint32_t k = min(x.cnt[s - c.lo], SY_INBOX);
-    // s also sent SYNCs this tick (its roles are final since collection): its SYNC_ACKs' content
-    // is this row after the merges below, which its own SYNC_ACK merge may change while another
-    // merge reads it
-    const bool ack_snap = !d2 && sflag_has(c, b, s - c.lo, SF_SENT | SF_RECV);
+    // s both sent and received this tick (its roles are final since collection): other receivers
+    // read this row as content while this workgroup merges into it, so it is copied into its slot
+    // before the first change (lazy snapshot, Content above)
+    const uint32_t slot = (d2 ? b.ack_snap : b.snap_idx)[s - c.lo];
+    bool copied = slot >= b.snap_cap;  // (no slot: nobody reads this row as content now)
     load_inbox(c, b, x, s - c.lo, k, s_it, s_key, s_raw);
     if (threadIdx.x == 0) {
       mem(c, s).ev_minor = 0;
@@ -572,7 +599,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       if (it >= b.req_cap) continue;  // a page the pool could not give (ERR_REQS is set); uniform
       const SyncReq rq = x.items[it];
       const uint32_t tot_q = itot[it];  // issued with the header (stable since classify)
-      const uint32_t* content = sync_content(c, b, rq, d2);
+      const Content kc = msg_content(c, b, rq, d2);
       const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
       uint32_t npend = 0;
       const uint32_t mod = s_mod;
@@ -581,10 +608,22 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       if (own && rq.pad != 0 && rq.content == NONE && b.row_mod[rq.from - c.lo] != (uint32_t)c.T &&
           b.row_mod[s - c.lo] != (uint32_t)c.T)
         d1 = rq.pad - 1;
+      const bool pre = mod == 0 && (!own || d1 != NONE);  // precomputed classification is exact
+      const uint32_t at = d1 != NONE ? d1 : it;
+      const uint32_t tot = pre ? (d1 != NONE ? b.rev_total[at] : tot_q) : 0u;
       __syncthreads();  // every lane has read s_mod before lane 0 may set it
-      if (mod == 0 && (!own || d1 != NONE)) {  // precomputed classification is exact: the row is unchanged
-        const uint32_t at = d1 != NONE ? d1 : it;
-        const uint32_t tot = d1 != NONE ? b.rev_total[at] : tot_q;
+      if (!copied && (!pre || tot != 0)) {  // this message may change the row: the lazy snapshot first
+        copy_row(rec_row(c, s), b.snap + (size_t)slot * c.n, c.n);
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          __hip_atomic_store(b.snap_ready + (s - c.lo), snap_want(c, d2), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          __threadfence();  // published before any change of the row
+        }
+        __syncthreads();
+        copied = true;
+      }
+      if (pre) {  // the row is unchanged since classify
         if (threadIdx.x < 64 && tot != 0) {
           // wave 0 reads the chunk results 64 at a time; lane 0 applies the non-empty chunks' complex
           // records in (chunk, subject) order
@@ -601,7 +640,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
                 s_mod = 1;
                 for (uint32_t q2 = 0; q2 < cnt; ++q2) {
                   const uint32_t xs = b.pool[base + q2];
-                  const uint32_t a = content[xs];
+                  const uint32_t a = content_at(kc, xs);
                   if (update_membership(c, s, xs, r_status(a), r_inc(a), reason, phase))
                     pend[npend++] = ((uint64_t)xs << 32) | (uint32_t)r_inc(a);
                 }
@@ -610,7 +649,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
           }
         }
       } else {
-        merge_row_wg(c, s, content, reason, phase, pend, npend, s_list, s_wave, &s_mod);
+        merge_row_wg(c, s, kc, reason, phase, pend, npend, s_list, s_wave, &s_mod);
       }
       if (threadIdx.x == 0) {
         for (uint32_t j = 0; j < npend; ++j)
@@ -642,7 +681,8 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
             // bookkeeping for it (onSyncAck :385-391: the phase's minor / fetch counters restart, an
             // INITIAL ack completes a join step, the counters) is done here and nothing is enqueued
             if (CLS_REV && rq.content == NONE && s_mod == 0 && owned(c, rq.from) &&
-                !sflag_has(c, b, rq.from - c.lo, SF_RECV) && !sflag_has(c, b, rq.from - c.lo, SF_MULTI) &&
+                (ACK_NORECV_EXPERIMENT || !sflag_has(c, b, rq.from - c.lo, SF_RECV)) &&
+                !sflag_has(c, b, rq.from - c.lo, SF_MULTI) &&
                 b.rev_total[it] == 0) {
               MemberDev& mf = mem(c, rq.from);
               mf.ev_minor = 0;
@@ -667,14 +707,6 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
     if (threadIdx.x == 0) {
       if (!d2) {
         if (s_mod) b.row_mod[s - c.lo] = (uint32_t)c.T;  // invalidates the reverse classifications
-        // s holds a snapshot (it also sent SYNCs: its own SYNC_ACK merges may change its row while
-        // another merge reads its SYNC_ACK content): classify filled the slot with the row before
-        // this workgroup's merges; if they changed it, the SYNC_ACK content gets a slot of its own
-        s_list[0] = NONE;
-        if (ack_snap && s_mod) {
-          s_list[0] = snap_take(c, b, s - c.lo);
-          b.ack_snap[s - c.lo] = s_list[0];
-        }
       } else {
         // start0's initial-sync completion counts the acks of its INITIAL SYNCs (:270-284)
         uint32_t init = 0;
@@ -687,7 +719,6 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       stat_add(c, ST_SYNC_RECORDS, s_recs);
     }
     __syncthreads();
-    if (!d2 && s_list[0] < b.snap_cap) copy_row(rec_row(c, s), b.snap + (size_t)s_list[0] * c.n, c.n);
     // this sub-phase's pingMembers inserts of s (its ADDED events, all made by this workgroup)
     apply_ins_batch<APPLY_BLOCK, true>(c, s, threadIdx.x, s_iP, s_iS, s_iR);
   }
