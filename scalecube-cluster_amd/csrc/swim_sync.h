@@ -457,7 +457,12 @@ __device__ void merge_row_wg(const Ctx& c, uint32_t v, const Content& kc, int re
   const uint32_t* __restrict__ rv = rec_row(c, v);
   const uint32_t n = c.n;
   __shared__ uint32_t s_pub;
-  const uint32_t* content = kc.snap && snap_published(kc) ? kc.snap : kc.live;
+  // one decision for the whole workgroup (threads reading the flag separately could disagree, and
+  // the tile loop below branches around barriers on it)
+  if (threadIdx.x == 0) s_pub = kc.snap && snap_published(kc) ? 1u : 0u;
+  __syncthreads();
+  const uint32_t* content = s_pub ? kc.snap : kc.live;
+  __syncthreads();  // (s_pub is reused below)
   for (uint32_t base = 0; base < n; base += APPLY_TILE) {
     const uint32_t x0 = base + threadIdx.x * APPLY_CPT;
     uint32_t flags = 0;
@@ -521,12 +526,13 @@ __device__ inline void copy_row(const uint32_t* __restrict__ src, uint32_t* __re
 
 // the receiver's inbox in canonical order (sender, ordinal) -> s_it (item indices); its page table
 // is reset for the next sub-phase.  Every thread of the workgroup calls it; returns the count.
+// (inl0: the inbox's first inline slot, loaded by the caller with the receiver's other words)
 __device__ inline uint32_t load_inbox(const Ctx& c, const Bufs& b, const SyInbox& x, uint32_t r, uint32_t k,
-                                      uint32_t* s_it, uint64_t* s_key, uint32_t* s_raw) {
+                                      uint32_t* s_it, uint64_t* s_key, uint32_t* s_raw, uint32_t inl0) {
   const uint32_t* inl = x.inl + (size_t)r * SY_INLINE;
   const uint32_t* tab = x.tab + (size_t)r * b.sy_max;
   if (k == 1) {  // the common inbox: nothing to order
-    if (threadIdx.x == 0) s_it[0] = inl[0];
+    if (threadIdx.x == 0) s_it[0] = inl0;
     __syncthreads();
     return 1;
   }
@@ -576,17 +582,25 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
   const uint32_t* const itot = d2 ? b.ack_ctot : b.item_total;
   const uint32_t phase = d2 ? SWIM_PHASE_SYNCACK : SWIM_PHASE_SYNC;
   const uint32_t chunks = b.chunks;
+  // the receiver list's entry is loaded beside its count (entries past the count are stale and
+  // only read, never used)
+  uint32_t s_spec = blockIdx.x < c.nl ? x.recv[blockIdx.x] : 0u;
   const uint32_t nrecv = *x.recv_cnt;
   uint64_t* pend = b.pend + (size_t)blockIdx.x * c.n;
   for (uint32_t ri = blockIdx.x; ri < nrecv; ri += gridDim.x) {
-    const uint32_t s = x.recv[ri];
-    const uint32_t k = min(x.cnt[s - c.lo], SY_INBOX);
+    const uint32_t s = s_spec;
+    if (ri + gridDim.x < c.nl) s_spec = x.recv[ri + gridDim.x];
+    // every word that depends on the receiver alone, in one batch
+    const uint32_t li = s - c.lo;
+    const uint32_t k = min(x.cnt[li], SY_INBOX);
+    const uint32_t inl0 = x.inl[(size_t)li * SY_INLINE];
+    const uint32_t tsz0 = mem(c, s).table_size, ins0 = mem(c, s).ins_rank;
     // s both sent and received this tick (its roles are final since collection): other receivers
     // read this row as content while this workgroup merges into it, so it is copied into its slot
     // before the first change (lazy snapshot, Content above)
-    const uint32_t slot = (d2 ? b.ack_snap : b.snap_idx)[s - c.lo];
+    const uint32_t slot = (d2 ? b.ack_snap : b.snap_idx)[li];
     bool copied = slot >= b.snap_cap;  // (no slot: nobody reads this row as content now)
-    load_inbox(c, b, x, s - c.lo, k, s_it, s_key, s_raw);
+    load_inbox(c, b, x, li, k, s_it, s_key, s_raw, inl0);
     if (threadIdx.x == 0) {
       mem(c, s).ev_minor = 0;
       mem(c, s).fetch_ctr = 0;
@@ -599,7 +613,6 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       if (it >= b.req_cap) continue;  // a page the pool could not give (ERR_REQS is set); uniform
       const SyncReq rq = x.items[it];
       const uint32_t tot_q = itot[it];  // issued with the header (stable since classify)
-      const Content kc = msg_content(c, b, rq, d2);
       const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
       uint32_t npend = 0;
       const uint32_t mod = s_mod;
@@ -625,6 +638,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       }
       if (pre) {  // the row is unchanged since classify
         if (threadIdx.x < 64 && tot != 0) {
+          const Content kc = msg_content(c, b, rq, d2);
           // wave 0 reads the chunk results 64 at a time; lane 0 applies the non-empty chunks' complex
           // records in (chunk, subject) order
           const uint32_t lane = threadIdx.x;
@@ -649,7 +663,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
           }
         }
       } else {
-        merge_row_wg(c, s, kc, reason, phase, pend, npend, s_list, s_wave, &s_mod);
+        merge_row_wg(c, s, msg_content(c, b, rq, d2), reason, phase, pend, npend, s_list, s_wave, &s_mod);
       }
       if (threadIdx.x == 0) {
         for (uint32_t j = 0; j < npend; ++j)
@@ -661,7 +675,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
     if (!d2) {
       // the SYNC_ACKs, one thread per inbox message: the enqueues are independent (the receiver
       // orders its inbox), the loss draws keyed by the message's rank q
-      const uint32_t tsz = mem(c, s).table_size;
+      const uint32_t tsz = s_mod ? mem(c, s).table_size : tsz0;  // (merges may have changed it)
       for (uint32_t q0 = 0; q0 < k; q0 += blockDim.x) {
         const uint32_t q = q0 + threadIdx.x;
         bool valid = false;
@@ -719,7 +733,8 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       stat_add(c, ST_SYNC_RECORDS, s_recs);
     }
     __syncthreads();
-    // this sub-phase's pingMembers inserts of s (its ADDED events, all made by this workgroup)
-    apply_ins_batch<APPLY_BLOCK, true>(c, s, threadIdx.x, s_iP, s_iS, s_iR);
+    // this sub-phase's pingMembers inserts of s (its ADDED events, all made by this workgroup; none
+    // when no merge changed the row and none were pending)
+    if (s_mod || ins0) apply_ins_batch<APPLY_BLOCK, true>(c, s, threadIdx.x, s_iP, s_iS, s_iR);
   }
 }
