@@ -394,7 +394,10 @@ def main():
     value = n * args.steps / dt  # one cluster of n members, sharded over `world` GPUs
     avg_ms = prof["total_ms"] / max(1, prof["launches"])
     achieved = prof["alg_bytes"] / max(1e-12, prof["total_ms"] / 1e3) / 1e9
-    traffic, traffic_src = pmc_traffic("k_sync_classify", f"{args.workload}{n // 1024}k")
+    # unsharded: the SYNC classification runs inside the SYNC launch of k_sync_apply (fused, no
+    # classify launch); sharded: k_sync_classify streams the rows that arrived from other shards
+    merge_kernel = "k_sync_apply" if world == 1 and args.local_shards == 1 else "k_sync_classify"
+    traffic, traffic_src = pmc_traffic(merge_kernel, f"{args.workload}{n // 1024}k")
     line = {
         "metric": "simulated member-protocol-periods/sec at N=65,536; achieved HBM GB/s",
         "value": value,
@@ -415,13 +418,16 @@ def main():
                                    f"single GPU, {args.local_shards} in-process shards" if args.local_shards > 1
                                    else "single GPU")},
         "roofline": None,
-        "roofline_merge": {"bound": "hbm", "kernel": "k_sync_classify", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+        "roofline_merge": {"bound": "hbm", "kernel": merge_kernel + (" (SYNC launch, classification fused)"
+                                                                     if merge_kernel == "k_sync_apply" else ""),
+                     "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                     "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                     "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE; k_sync_apply: its SYNC "
+                                     "and SYNC_ACK launches averaged)",
                      "traffic_source": traffic_src,
                      "launches": prof["launches"], "avg_launch_ms": avg_ms,
                      "alg_bytes_per_launch": prof["alg_bytes"] / max(1, prof["launches"]),
-                     # one SYNC classify launch per tick (the SYNC_ACK launch reuses its results); 1 in 3 timed
+                     # one SYNC merge launch per tick (the SYNC_ACK launch reuses its results); 1 in 3 timed
                      "kernel_time_share": avg_ms * e.now()[2] / (dt * 1e3 / args.steps)},
         "stats": {k: stats[k] for k in ("syncs", "sync_records", "gossip_messages", "gossips_created", "pings",
                                          "timers_fired", "events")},

@@ -280,6 +280,18 @@ static void launch_emit(swim_engine* e, Shard& s) {
   k.used++;
 }
 
+// the fused SYNC apply (unsharded) carries the merge profile that k_sync_classify carries otherwise
+static void launch_apply(swim_engine* e, Shard& s, int d2, int classified, int fused) {
+  KProf& k = s.prof_cls;
+  if (!fused || !k.take(e->prof)) {
+    k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, e->stream>>>(s.d_par, e->T, d2, classified, fused, nullptr);
+    return;
+  }
+  hipExtLaunchKernelGGL(k_sync_apply, dim3(kApplyGrid), dim3(APPLY_BLOCK), 0, e->stream, k.ev[2 * k.used],
+                        k.ev[2 * k.used + 1], 0, s.d_par, e->T, d2, classified, fused, k.slots + 3 * k.used);
+  k.used++;
+}
+
 static void launch_deliver(swim_engine* e, Shard& s) {
   // at least kDeliverGrid workgroups: big inboxes are delivered a wave each, grid-stride
   const uint32_t grid = std::max<uint32_t>(kDeliverGrid, grid_for(s.c.nl, DLV_BLOCK));
@@ -518,13 +530,16 @@ static int32_t run_tick(swim_engine* e) {
           TICK_CHECK("k_pull_rows");
         }
       }
-      // SYNC_ACK: an unsharded engine classifies its acks inside k_sync_apply (every ack is local,
-      // and almost all reuse the SYNC launch's reverse classification); a sharded one streams the
-      // acks that arrived with their rows from other shards
-      const int classified = d2 == 0 || multi;
+      // SYNC: an unsharded engine classifies every SYNC inside k_sync_apply with the block witness
+      // (fused, no classify launch), a sharded one streams the rows that arrived from other shards
+      // in k_sync_classify.  SYNC_ACK: an unsharded engine classifies its acks inside k_sync_apply
+      // (every ack is local, and almost all reuse the SYNC merge's reverse classification); a sharded
+      // one streams the acks that arrived with their rows from other shards
+      const int fused = !multi && d2 == 0;
+      const int classified = (d2 == 0 && !fused) || multi;
       if (classified) launch_classify(e, sd, d2);
       TICK_CHECK("k_sync_classify");
-      k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, s>>>(sd.d_par, T, d2, classified);
+      launch_apply(e, sd, d2, classified, fused);
       TICK_CHECK("k_sync_apply");
     }
   }
@@ -785,7 +800,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&b.ack_snap, nl) && sd.alloc(&b.snap_ready, nl) && sd.alloc(&b.sflag, nl) &&
             sd.alloc(&b.ack_chunk, (size_t)b.req_cap * b.chunks) && sd.alloc(&b.ack_ctot, b.req_cap) &&
             sd.alloc(&b.ack_recv, nl) && 
-            sd.alloc(&b.snap, (size_t)b.snap_cap * n) && sd.alloc(&b.snap_idx, nl) &&
+            sd.alloc(&b.snap, (size_t)b.snap_cap * (n + c.blocks)) && sd.alloc(&b.snap_idx, nl) &&
             sd.alloc(&b.snap_list, 2 * (size_t)b.snap_cap) && sd.alloc(&b.snap_cnt, 2) && sd.alloc(&b.item_chunk, (size_t)b.req_cap * b.chunks) &&
             sd.alloc(&b.item_total, b.req_cap) && sd.alloc(&b.pool, b.pool_cap) &&
             sd.alloc(&b.rev_chunk, (size_t)b.req_cap * b.chunks) && sd.alloc(&b.rev_total, b.req_cap) &&

@@ -429,6 +429,10 @@ struct Content {
   uint32_t want;
 };
 __device__ __forceinline__ uint32_t snap_want(const Ctx& c, int d2) { return ((uint32_t)c.T << 2) | (d2 ? 2u : 1u); }
+// a slot holds the row (n words) and, after it, the row's block-witness counts (blocks words)
+__device__ __forceinline__ uint32_t* snap_slot(const Ctx& c, const Bufs& b, uint32_t slot) {
+  return b.snap + (size_t)slot * (c.n + c.blocks);
+}
 __device__ __forceinline__ bool snap_published(const Content& k) {
   return __hip_atomic_load(k.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == k.want;
 }
@@ -445,7 +449,24 @@ __device__ __forceinline__ Content msg_content(const Ctx& c, const Bufs& b, cons
   const uint32_t i = q.from - c.lo;
   const uint32_t si = (d2 ? b.ack_snap : b.snap_idx)[i];
   if (si >= b.snap_cap) return Content{rec_row(c, q.from), nullptr, nullptr, 0};
-  return Content{rec_row(c, q.from), b.snap + (size_t)si * c.n, b.snap_ready + i, snap_want(c, d2)};
+  return Content{rec_row(c, q.from), snap_slot(c, b, si), b.snap_ready + i, snap_want(c, d2)};
+}
+
+// the copy of row s (and its witness counts) into its slot before its first change in sub-phase d2,
+// then the publication (every thread of the workgroup calls it)
+__device__ inline void copy_row(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t n);
+__device__ inline void lazy_snapshot(const Ctx& c, const Bufs& b, uint32_t s, uint32_t slot, int d2) {
+  uint32_t* dst = snap_slot(c, b, slot);
+  copy_row(rec_row(c, s), dst, c.n);
+  const uint32_t* bd = c.bdiff + (size_t)(s - c.lo) * c.blocks;
+  for (uint32_t k = threadIdx.x; k < c.blocks; k += blockDim.x) dst[c.n + k] = bd[k];
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(b.snap_ready + (s - c.lo), snap_want(c, d2), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();  // published before any change of the row
+  }
+  __syncthreads();
 }
 
 // In-workgroup merge of one message (used when the receiver's row changed earlier in this
@@ -524,6 +545,148 @@ __device__ inline void copy_row(const uint32_t* __restrict__ src, uint32_t* __re
   }
 }
 
+// ---- the unsharded SYNC merge, classified in the receiver's workgroup (no classify launch).
+// One message s -> r: (1) the block witness of both rows, chunk per thread — a 1,024-subject block
+// where both rows equal the reference record (counts 0) holds identical records and is skipped
+// unless it holds r's own subject as LEAVING (or, for the reverse direction, s's); (2) every other
+// block streamed by the workgroup, 4 subjects per thread, both directions from one load: the forward
+// complex records compacted in subject order and applied by thread 0 at once (each update touches
+// only its own subject's cell, so classifying block j+1 after applying block j is exact), the
+// reverse ones (the SYNC_ACK answering this SYNC merges r's row into s's: the same two rows) into the
+// pool as rev_chunk / rev_total for the SYNC_ACK sub-phase and the lone-ack shortcut.  The content
+// row is s's live row or its lazy snapshot (Content): the choice is made once for the workgroup and
+// re-validated after every read of the live row.  s_need: LDS bitmask of the blocks to stream.
+// prof: {blocks streamed, complex records, blocks}.
+constexpr uint32_t NEED_WORDS = 512;  // (1 << 24 members) / 1,024 / 32
+__device__ void sync_msg_wg(const Ctx& c, const Bufs& b, uint32_t r, uint32_t it, const SyncReq& rq, bool do_rev,
+                            int reason, uint32_t phase, uint64_t* pend, uint32_t& npend, uint32_t* s_list,
+                            uint32_t* s_wave, uint32_t* s_mod, uint32_t* s_need, uint32_t slot, bool& copied,
+                            unsigned long long* prof) {
+  __shared__ uint32_t s_pub3, s_rtot;
+  const uint32_t n = c.n, chunks = b.chunks, tid = threadIdx.x, s = rq.from;
+  const Content kc = msg_content(c, b, rq, 0);
+  if (tid == 0) {
+    s_pub3 = kc.snap && snap_published(kc) ? 1u : 0u;
+    s_rtot = 0;
+  }
+  for (uint32_t w = tid; w < (chunks + 31) / 32; w += blockDim.x) s_need[w] = 0;
+  __syncthreads();
+  bool from_snap = s_pub3 != 0;
+  const uint32_t* rv = rec_row(c, r);
+  const uint32_t* bdv = c.bdiff + (size_t)(r - c.lo) * c.blocks;
+  const auto leaving = [](uint32_t rf) { return r_in_table(rf) && r_status(rf) == SWIM_LEAVING; };
+  const uint32_t rfr = c.ref[r], rfs = c.ref[s];
+  uint2* const rch = b.rev_chunk + (size_t)it * chunks;
+  // (1) witness, chunk per thread
+  for (int pass = 0; pass < 2; ++pass) {
+    const uint32_t* bdc = from_snap ? kc.snap + n : c.bdiff + (size_t)(s - c.lo) * c.blocks;
+    for (uint32_t ch = tid; ch < chunks; ch += blockDim.x) {
+      const uint32_t base = ch * SYNC_CHUNK;
+      const bool need = (bdc[ch] | bdv[ch]) != 0 || (r - base < (uint32_t)SYNC_CHUNK && leaving(rfr)) ||
+                        (do_rev && s - base < (uint32_t)SYNC_CHUNK && leaving(rfs));
+      if (need) atomicOr(&s_need[ch >> 5], 1u << (ch & 31));
+      else if (do_rev) rch[ch] = make_uint2(0, 0);
+    }
+    if (!kc.snap || from_snap) break;
+    __threadfence();  // the witness words are in before the flag is read again
+    __syncthreads();
+    if (tid == 0) s_pub3 = snap_published(kc) ? 1u : 0u;
+    __syncthreads();
+    if (!s_pub3) break;
+    from_snap = true;  // s published its copy meanwhile: the witness again, from the copy
+    for (uint32_t w = tid; w < (chunks + 31) / 32; w += blockDim.x) s_need[w] = 0;
+    __syncthreads();
+  }
+  __syncthreads();
+  // (2) the blocks to stream, in subject order
+  uint32_t streamed = 0, cplx = 0;
+  for (uint32_t w = 0; w < (chunks + 31) / 32; ++w) {
+    uint32_t bits = s_need[w];
+    while (bits) {
+      const uint32_t ch = w * 32 + (uint32_t)__ffs(bits) - 1;
+      bits &= bits - 1;
+      ++streamed;
+      const uint32_t base = ch * SYNC_CHUNK, x0 = base + 4 * tid;
+      uint32_t flags = 0, rflags = 0;
+      for (int pass = 0; pass < 2; ++pass) {
+        const uint32_t* cr = from_snap ? kc.snap : kc.live;
+        flags = rflags = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t x = x0 + q;
+          if (x >= n || x0 >= base + SYNC_CHUNK) break;
+          const uint32_t av = cr[x], ov = rv[x];
+          if (r_in_table(av) && sync_complex(av, ov, x == r)) flags |= 1u << q;
+          if (do_rev && r_in_table(ov) && sync_complex(ov, av, x == s)) rflags |= 1u << q;
+        }
+        if (!kc.snap || from_snap) break;
+        __threadfence();
+        __syncthreads();
+        if (tid == 0) s_pub3 = snap_published(kc) ? 1u : 0u;
+        __syncthreads();
+        if (!s_pub3) break;
+        from_snap = true;
+      }
+      // forward: compact in subject order, then thread 0 applies
+      uint32_t total;
+      const uint32_t off = block_exclusive_scan<APPLY_BLOCK>((uint32_t)__popc(flags), s_wave, &total);
+      if (total) {
+        uint32_t o = off;
+        for (int q = 0; q < 4; ++q)
+          if (flags & (1u << q)) s_list[o++] = x0 + q;
+        if (!copied) {  // the first change of this row in the sub-phase: the lazy snapshot first
+          lazy_snapshot(c, b, r, slot, 0);
+          copied = true;
+        }
+        __syncthreads();
+        if (tid == 0) {
+          *s_mod = 1;
+          for (uint32_t i = 0; i < total; ++i) {
+            const uint32_t x = s_list[i];
+            const uint32_t a = from_snap ? kc.snap[x] : content_at(kc, x);
+            if (update_membership(c, r, x, r_status(a), r_inc(a), reason, phase))
+              pend[npend++] = ((uint64_t)x << 32) | (uint32_t)r_inc(a);
+          }
+        }
+        __syncthreads();
+        cplx += total;
+      }
+      if (do_rev) {  // reverse: the subjects into the pool, in subject order
+        uint32_t rt;
+        const uint32_t roff = block_exclusive_scan<APPLY_BLOCK>((uint32_t)__popc(rflags), s_wave, &rt);
+        if (tid == 0) {
+          uint32_t pb = 0;
+          if (rt) {
+            pb = atomicAdd(&b.k->pool_cursor, rt);
+            if (pb + rt > b.pool_cap) { set_err(c, ERR_PEND); rt = 0; }
+          }
+          s_list[0] = pb;
+          s_list[1] = rt;
+          rch[ch] = make_uint2(pb, rt);
+          s_rtot += rt;
+        }
+        __syncthreads();
+        const uint32_t pb = s_list[0], ok = s_list[1];
+        if (ok) {
+          uint32_t o = pb + roff;
+          for (int q = 0; q < 4; ++q)
+            if (rflags & (1u << q)) b.pool[o++] = x0 + q;
+        }
+        __syncthreads();
+      }
+    }
+  }
+  if (tid == 0) {
+    if (do_rev) b.rev_total[it] = s_rtot;
+    if (prof) {
+      atomicAdd(prof, (unsigned long long)streamed);
+      if (cplx) atomicAdd(prof + 1, (unsigned long long)cplx);
+      atomicAdd(prof + 2, (unsigned long long)chunks);
+    }
+  }
+  __syncthreads();
+}
+
 // the receiver's inbox in canonical order (sender, ordinal) -> s_it (item indices); its page table
 // is reset for the next sub-phase.  Every thread of the workgroup calls it; returns the count.
 // (inl0: the inbox's first inline slot, loaded by the caller with the receiver's other words)
@@ -567,9 +730,13 @@ __device__ inline uint32_t load_inbox(const Ctx& c, const Bufs& b, const SyInbox
 // classified = 0 (SYNC_ACK sub-phase of an unsharded engine: no k_ack_classify launch): an ack takes
 // the SYNC launch's reverse classification when its two rows are unchanged since (row_mod), and is
 // classified in-workgroup (merge_row_wg) otherwise.
-__global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int classified) {
+// fused = 1 (unsharded SYNC sub-phase): no k_sync_classify launch, every message is classified in
+// the receiver's workgroup with the block witness (sync_msg_wg); prof as k_sync_classify's.
+__global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int classified, int fused,
+                                                            unsigned long long* prof) {
   const Ctx c = pctx_sync(P, T);
   const Bufs b = P->b;
+  __shared__ uint32_t s_need[NEED_WORDS];
   __shared__ uint32_t s_list[APPLY_TILE];
   __shared__ uint32_t s_wave[APPLY_BLOCK / 64 + 1];
   __shared__ uint32_t s_mod;
@@ -612,7 +779,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       const uint32_t it = s_it[q];
       if (it >= b.req_cap) continue;  // a page the pool could not give (ERR_REQS is set); uniform
       const SyncReq rq = x.items[it];
-      const uint32_t tot_q = itot[it];  // issued with the header (stable since classify)
+      const uint32_t tot_q = fused ? 0u : itot[it];  // issued with the header (stable since classify)
       const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
       uint32_t npend = 0;
       const uint32_t mod = s_mod;
@@ -621,22 +788,19 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       if (own && rq.pad != 0 && rq.content == NONE && b.row_mod[rq.from - c.lo] != (uint32_t)c.T &&
           b.row_mod[s - c.lo] != (uint32_t)c.T)
         d1 = rq.pad - 1;
-      const bool pre = mod == 0 && (!own || d1 != NONE);  // precomputed classification is exact
+      const bool pre = !fused && mod == 0 && (!own || d1 != NONE);  // precomputed classification is exact
       const uint32_t at = d1 != NONE ? d1 : it;
       const uint32_t tot = pre ? (d1 != NONE ? b.rev_total[at] : tot_q) : 0u;
       __syncthreads();  // every lane has read s_mod before lane 0 may set it
-      if (!copied && (!pre || tot != 0)) {  // this message may change the row: the lazy snapshot first
-        copy_row(rec_row(c, s), b.snap + (size_t)slot * c.n, c.n);
-        __threadfence();
-        __syncthreads();
-        if (threadIdx.x == 0) {
-          __hip_atomic_store(b.snap_ready + (s - c.lo), snap_want(c, d2), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-          __threadfence();  // published before any change of the row
-        }
-        __syncthreads();
+      if (fused) {  // unsharded SYNC sub-phase: the in-workgroup witness merge (no classify launch)
+        sync_msg_wg(c, b, s, it, rq, CLS_REV && mod == 0, reason, phase, pend, npend, s_list, s_wave, &s_mod,
+                    s_need, slot, copied, prof);
+      } else if (!copied && (!pre || tot != 0)) {  // this message may change the row: the lazy snapshot first
+        lazy_snapshot(c, b, s, slot, d2);
         copied = true;
       }
-      if (pre) {  // the row is unchanged since classify
+      if (fused) {
+      } else if (pre) {  // the row is unchanged since classify
         if (threadIdx.x < 64 && tot != 0) {
           const Content kc = msg_content(c, b, rq, d2);
           // wave 0 reads the chunk results 64 at a time; lane 0 applies the non-empty chunks' complex
