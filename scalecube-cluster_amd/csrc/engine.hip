@@ -594,6 +594,10 @@ static int32_t write_member_dev(Shard& sd, uint32_t m, const MemberDev& in) {
   return hipMemcpy(sd.c.mem + (m - sd.c.lo), &in, sizeof(MemberDev), hipMemcpyHostToDevice) == hipSuccess ? SWIM_OK
                                                                                                          : SWIM_EDEVICE;
 }
+static int32_t read_gsched(Shard& sd, uint32_t m, GossipSched* out) {
+  return hipMemcpy(out, sd.c.gs + (m - sd.c.lo), sizeof(GossipSched), hipMemcpyDeviceToHost) == hipSuccess ? SWIM_OK
+                                                                                                          : SWIM_EDEVICE;
+}
 static int32_t read_up(swim_engine* e, uint32_t m, uint8_t* up) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
   return hipMemcpy(up, e->sh[0].c.up + m, 1, hipMemcpyDeviceToHost) == hipSuccess ? SWIM_OK : SWIM_EDEVICE;
@@ -785,6 +789,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&c.is_seed, n) && sd.alloc(&c.seeds, n) && sd.alloc(&c.ins, c.ins_cap) &&
             sd.alloc(&c.ins_inline, (size_t)nl * INS_INLINE) && sd.alloc(&c.compact_flag, nl) &&
             sd.alloc(&c.fd_next, nl) && sd.alloc(&c.sync_next, nl) && sd.alloc(&c.mflag, nl) &&
+            sd.alloc(&c.gs, std::max(nl, 1u)) &&
             sd.alloc(&c.gslot, GSLOTS) && sd.alloc(&c.gpend, GSLOTS) &&
             sd.alloc(&c.gbits, (size_t)GSLOTS * c.gwords) && sd.alloc(&c.clr_tick, std::max(nl, 1u)) &&
             sd.alloc(&c.gclaim, 2 * GSLOTS) && sd.alloc(&c.gclaim_cnt, 2) &&
@@ -1482,7 +1487,8 @@ int32_t swim_read_member(swim_engine* e, uint32_t v, swim_member_state* o) {
   Shard* sd = e->owner_of(v);
   if (!sd) return SWIM_EINVAL;
   MemberDev m;
-  if (read_member_dev(e, *sd, v, &m) != SWIM_OK) return SWIM_EDEVICE;
+  GossipSched gs;
+  if (read_member_dev(e, *sd, v, &m) != SWIM_OK || read_gsched(*sd, v, &gs) != SWIM_OK) return SWIM_EDEVICE;
   uint8_t up = 0;
   if (read_up(e, v, &up) != SWIM_OK) return SWIM_EDEVICE;
   std::memset(o, 0, sizeof(*o));
@@ -1495,8 +1501,8 @@ int32_t swim_read_member(swim_engine* e, uint32_t v, swim_member_state* o) {
   o->ping_cursor = m.ping_cursor;
   o->ping_len = m.ping_len;
   o->remote_len = m.remote_len;
-  o->gossip_len = m.gossip_len;
-  o->gossip_period = m.g_period;
+  o->gossip_len = gs.len;
+  o->gossip_period = gs.period;
   o->gossip_counter = m.g_counter;
   o->table_size = m.table_size;
   o->members_size = m.members_size;
@@ -1547,10 +1553,10 @@ int32_t swim_read_gossips(swim_engine* e, uint32_t v, swim_gossip* out, uint32_t
   if (!e || v >= e->n) return SWIM_EINVAL;
   Shard* sd = e->owner_of(v);
   if (!sd) return SWIM_EINVAL;
-  MemberDev m;
-  if (read_member_dev(e, *sd, v, &m) != SWIM_OK) return SWIM_EDEVICE;
-  if (len) *len = m.gossip_len;
-  uint32_t k = std::min(cap, m.gossip_len);
+  GossipSched gs;
+  if (hipStreamSynchronize(e->stream) != hipSuccess || read_gsched(*sd, v, &gs) != SWIM_OK) return SWIM_EDEVICE;
+  if (len) *len = gs.len;
+  uint32_t k = std::min(cap, gs.len);
   if (!out || !k) return SWIM_OK;
   std::vector<GossipHot> gh(k);
   std::vector<GossipCold> gc(k);

@@ -57,13 +57,23 @@ constexpr uint64_t B_IN_TABLE = 1ull << 34, B_IN_MEMBERS = 1ull << 35, B_ALIVE_E
 
 // Per-member scalar state of an OWNED member (index v - Ctx.lo).  Whether a member's transport
 // is up is replicated on every shard (Ctx.up), because every sender reads it.
+// The per-member words every gossip tick touches for every member (doSpreadGossip's period++ and
+// the live-gossip test), kept out of MemberDev so that a round costs one coalesced 16-B word per
+// member instead of two MemberDev cache lines.
+struct alignas(16) GossipSched {
+  uint32_t next;    // tick of the next gossip round (schedule phase g_start, period G; kept while down)
+  uint32_t period;  // GossipProtocolImpl.currentPeriod (< 2^28: ERR_INC)
+  uint32_t len;     // live gossips in the member's slab (GossipProtocolImpl.gossips.size())
+  uint32_t pad;
+};
+
 struct alignas(16) MemberDev {
-  uint64_t fd_period, ack_due, relay_due, g_period, g_counter, period_used, leave_seq;
+  uint64_t fd_period, ack_due, relay_due, g_counter, leave_seq;
   int64_t fd_start, g_start, sync_start;
   uint32_t ping_cursor, ping_len, ack_target, relay_target, relay_pending;
   uint32_t remote_len;
   int32_t remote_idx;
-  uint32_t gossip_len, table_size, members_size, leave_gossiper;
+  uint32_t table_size, members_size, leave_gossiper;
   uint32_t ev_minor, fetch_ctr, fd_sync_cnt, init_total, init_done;
   uint32_t ins_rank, ins_head, ins_tail;  // this phase's deferred pingMembers inserts (op chain)
   uint32_t gix_base, gix_used;  // serial of slab[0]; gix slots taken since the index was (re)built
@@ -327,6 +337,7 @@ struct Ctx {
   uint32_t* fd_next;    // next tick with FD work (ping due, ack or relay timeout); stale while down
   uint32_t* sync_next;  // next periodic-SYNC tick (NONE: periodic SYNC off)
   uint32_t* mflag;      // MF_* work for SYNC collection / k_end_tick
+  GossipSched* gs;      // per member: gossip round schedule, period and slab length (one 16-B word)
   // receipt bitmaps: a subset of "receiver t's collector holds gossip (gossiper, seq)"
   // that k_gossip_emit tests before probing the collector table
   GSlot* gslot;          // [GSLOTS] the gossip owning each bitmap and the tick its bits became valid
@@ -434,6 +445,7 @@ __device__ __forceinline__ void cell_put(const Ctx& c, uint32_t v, uint32_t s, u
   if (nr != old) rec_changed(c, v, s, old, nr);
 }
 __device__ __forceinline__ MemberDev& mem(const Ctx& c, uint32_t v) { return c.mem[v - c.lo]; }
+__device__ __forceinline__ GossipSched& gsched(const Ctx& c, uint32_t v) { return c.gs[v - c.lo]; }
 __device__ __forceinline__ uint32_t* ping_list(const Ctx& c, uint32_t v) { return c.ping + (size_t)(v - c.lo) * c.n; }
 __device__ __forceinline__ uint32_t* remote_list(const Ctx& c, uint32_t v) { return c.remote + (size_t)(v - c.lo) * c.n; }
 __device__ __forceinline__ SlabRef slab_of(const Ctx& c, uint32_t v) {
@@ -797,12 +809,12 @@ __device__ __forceinline__ uint32_t gix_hash(uint32_t g, uint32_t s) { return ha
 __device__ __forceinline__ uint32_t* gix_of(const Ctx& c, uint32_t v) {
   return c.gix + (size_t)(v - c.lo) * (c.gix_mask + 1);
 }
-__device__ inline void gix_put(const Ctx& c, MemberDev& m, uint32_t* ix, uint32_t g, uint32_t s, uint32_t serial) {
+__device__ inline void gix_put(const Ctx& c, MemberDev& m, uint32_t len, uint32_t* ix, uint32_t g, uint32_t s, uint32_t serial) {
   const uint32_t mask = c.gix_mask;
   uint32_t h = gix_hash(g, s);
   for (uint32_t i = 0; i <= mask; ++i, ++h) {
     const uint32_t e = ix[h & mask];
-    if (e == NONE || e - m.gix_base >= m.gossip_len) {  // empty, or a swept gossip's slot
+    if (e == NONE || e - m.gix_base >= len) {  // empty, or a swept gossip's slot
       if (e == NONE) m.gix_used++;
       ix[h & mask] = serial;
       return;
@@ -814,25 +826,27 @@ __device__ inline void gix_put(const Ctx& c, MemberDev& m, uint32_t* ix, uint32_
 __device__ __forceinline__ void gix_note(const Ctx& c, MemberDev& m, uint32_t v, uint32_t g, uint32_t s) {
   if (!m.gix_valid) return;
   if (2 * m.gix_used >= c.gix_mask + 1) { m.gix_valid = 0; return; }
-  gix_put(c, m, gix_of(c, v), g, s, m.gix_base + m.gossip_len - 1);
+  const uint32_t len = gsched(c, v).len;
+  gix_put(c, m, len, gix_of(c, v), g, s, m.gix_base + len - 1);
 }
 // slab position of (g, s), or -1
 __device__ inline int32_t gix_find(const Ctx& c, MemberDev& m, uint32_t v, const SlabRef& slab, uint32_t g,
                                    uint32_t s) {
   uint32_t* ix = gix_of(c, v);
   const uint32_t mask = c.gix_mask;
+  const uint32_t len = gsched(c, v).len;
   if (!m.gix_valid) {
     for (uint32_t i = 0; i <= mask; ++i) ix[i] = NONE;
     m.gix_used = 0;
     m.gix_valid = 1;
-    for (uint32_t p = 0; p < m.gossip_len; ++p) gix_put(c, m, ix, slab.hot[p].gossiper, slab.hot[p].seq, m.gix_base + p);
+    for (uint32_t p = 0; p < len; ++p) gix_put(c, m, len, ix, slab.hot[p].gossiper, slab.hot[p].seq, m.gix_base + p);
   }
   uint32_t h = gix_hash(g, s);
   for (uint32_t i = 0; i <= mask; ++i, ++h) {
     const uint32_t e = ix[h & mask];
     if (e == NONE) return -1;
     const uint32_t p = e - m.gix_base;
-    if (p < m.gossip_len && slab.hot[p].gossiper == g && slab.hot[p].seq == s) return (int32_t)p;
+    if (p < len && slab.hot[p].gossiper == g && slab.hot[p].seq == s) return (int32_t)p;
   }
   return -1;
 }
@@ -843,19 +857,20 @@ __device__ inline int32_t gix_find(const Ctx& c, MemberDev& m, uint32_t v, const
 __device__ inline void spread_gossip(const Ctx& c, uint32_t v, uint32_t subject, uint32_t status, int32_t inc,
                                      uint32_t why) {
   MemberDev& m = mem(c, v);
-  if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); return; }
+  GossipSched& gs = gsched(c, v);
+  if (gs.len >= c.gcap) { set_err(c, ERR_SLAB); return; }
   GossipDev g;
   g.gossiper = v;
   g.seq = (uint32_t)m.g_counter;
   g.subject = subject;
   g.status = status;
   g.inc = inc;
-  g.inf_period = (uint32_t)m.g_period;
+  g.inf_period = gs.period;
 #pragma unroll
   for (int k = 0; k < GINF; ++k) g.inf[k] = NONE;
-  if (m.g_period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
-  slab_of(c, v).put(m.gossip_len, g);
-  m.gossip_len++;
+  if (gs.period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
+  slab_of(c, v).put(gs.len, g);
+  gs.len++;
   gix_note(c, m, v, g.gossiper, g.seq);
   m.g_counter++;
   CollEnt* e = coll_ensure(c, v, v);
@@ -870,19 +885,20 @@ __device__ __forceinline__ uint32_t orig_of(int reason) { return reason == R_FD_
 // the subject field
 __device__ inline void spread_user(const Ctx& c, uint32_t v, uint32_t payload) {
   MemberDev& m = mem(c, v);
-  if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); return; }
+  GossipSched& gs = gsched(c, v);
+  if (gs.len >= c.gcap) { set_err(c, ERR_SLAB); return; }
   GossipDev g;
   g.gossiper = v;
   g.seq = (uint32_t)m.g_counter;
   g.subject = payload;
   g.status = SWIM_GOSSIP_USER;
   g.inc = 0;
-  g.inf_period = (uint32_t)m.g_period;
+  g.inf_period = gs.period;
 #pragma unroll
   for (int k = 0; k < GINF; ++k) g.inf[k] = NONE;
-  if (m.g_period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
-  slab_of(c, v).put(m.gossip_len, g);
-  m.gossip_len++;
+  if (gs.period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
+  slab_of(c, v).put(gs.len, g);
+  gs.len++;
   gix_note(c, m, v, g.gossiper, g.seq);
   m.g_counter++;
   CollEnt* e = coll_ensure(c, v, v);

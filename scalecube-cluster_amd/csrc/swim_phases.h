@@ -232,6 +232,7 @@ __global__ void k_init_members(Ctx c, uint32_t n_initial, int32_t sync_stagger, 
     }
   }
   c.mem[i] = m;
+  c.gs[i] = GossipSched{next_due(m.g_start, c.T, c.G), 0u, 0u, 0u};
   c.fd_next[i] = m.joined ? fd_next_of(c, m, c.T) : NONE;
   c.sync_next[i] = m.sync_on ? next_due(m.sync_start, c.T, c.S) : NONE;
   c.mflag[i] = 0;
@@ -276,6 +277,7 @@ __global__ void k_start_joins(KP) {
   m.join_now = 1;
   m.fd_start = (int64_t)c.T;
   m.g_start = (int64_t)c.T;
+  c.gs[i].next = (uint32_t)c.T + c.G;
   cell_put(c, v, v, B_IN_TABLE | B_IN_MEMBERS);
   m.table_size = 1;
   m.members_size = 1;
@@ -533,9 +535,6 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
 }
 
 // ------------------------------------------------------------------------------- phase C
-__device__ __forceinline__ bool gossip_due(const Ctx& c, uint32_t v, const MemberDev& m) {
-  return c.up[v] && (int64_t)c.T > m.g_start && ((int64_t)c.T - m.g_start) % c.G == 0;
-}
 
 // checkGossipSegmentation (GossipProtocolImpl.java:217-236); only launched when the threshold is
 // below the inline interval capacity (otherwise a clear can never trigger).
@@ -864,7 +863,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     // the sweep dropped a prefix (infection periods grow along the slab): the index keeps its serials
     if (glen - w == lead) m.gix_base += lead;
     else m.gix_valid = 0;
-    m.gossip_len = w;
+    gsched(c, v).len = w;
     if (any_done) {
       m.leave_done = 1;
       c.mflag[v - c.lo] |= MF_LEAVE;
@@ -885,23 +884,27 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
 __device__ __forceinline__ void gossip_round(const Ctx& c, const Bufs& b, uint32_t i) {
   bool busy = false;
   if (i < c.nl) {
-    MemberDev& m = c.mem[i];
-    if (gossip_due(c, c.lo + i, m)) {
-      const uint64_t period = m.g_period;
-      m.g_period = period + 1;
-      m.period_used = period;
-      // checkGossipSegmentation (:217-236): clear collectors holding more than the threshold of
-      // intervals; only viewers whose collector crossed it since their last round look
-      if (c.seg_flag[i]) {
-        c.seg_flag[i] = 0;
-        CollEnt* base = c.coll + (size_t)i * c.hcap;
-        for (uint32_t j = 0; j < c.hcap; ++j)
-          if (base[j].key && (int32_t)coll_size(c, base + j) > c.seg_threshold) {
-            coll_clear(c, base + j);
-            c.clr_tick[i] = (uint32_t)c.T;
-          }
+    GossipSched gs = c.gs[i];  // one 16-B word per member
+    const uint32_t t32 = (uint32_t)c.T;
+    if (gs.next == t32) {  // the spreadGossip timer fires (phase g_start, period G; it runs while down too)
+      gs.next = t32 + c.G;
+      if (c.up[c.lo + i]) {
+        gs.period++;  // period++ (:143); emit runs the round as period - 1
+        // checkGossipSegmentation (:217-236): clear collectors holding more than the threshold of
+        // intervals; only viewers whose collector crossed it since their last round look
+        if (c.seg_flag[i]) {
+          c.seg_flag[i] = 0;
+          CollEnt* base = c.coll + (size_t)i * c.hcap;
+          for (uint32_t j = 0; j < c.hcap; ++j)
+            if (base[j].key && (int32_t)coll_size(c, base + j) > c.seg_threshold) {
+              coll_clear(c, base + j);
+              c.clr_tick[i] = (uint32_t)c.T;
+            }
+        }
+        busy = gs.len != 0;  // else no target selection, no shuffle draw
       }
-      busy = m.gossip_len != 0;  // else no target selection, no shuffle draw
+      c.gs[i].next = gs.next;
+      c.gs[i].period = gs.period;
     }
   }
   const uint64_t mk = __ballot(busy);
@@ -993,10 +996,9 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned lo
   unsigned long long nmsg = 0, nmat = 0, nstate = 0;
   for (uint32_t k = __builtin_amdgcn_readfirstlane(blockIdx.x * EMIT_WAVES + wv); k < ns; k += gridDim.x * EMIT_WAVES) {
     const uint32_t i = b.senders[k];
-    const MemberDev& m = c.mem[i];
-    const uint32_t glen = m.gossip_len;
-    nstate += glen;
-    nmsg += gossip_emit_sender(c, b, c.lo + i, m.g_period - 1, glen, lane, s_t[wv], nmat);
+    const GossipSched gs = c.gs[i];
+    nstate += gs.len;
+    nmsg += gossip_emit_sender(c, b, c.lo + i, gs.period - 1, gs.len, lane, s_t[wv], nmat);
   }
   if (lane == 0 && nmat) atomicAdd(&b.k->msg_total, (uint32_t)nmat);
   if (prof && lane == 0 && nstate) {
@@ -1155,15 +1157,16 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, con
   // a GossipState can outlive its collector entry only after a clear
   const int32_t found = was_cleared ? gix_find(c, m, r, slab, g.gossiper, g.seq) : -1;
   if (found < 0) {
-    if (m.gossip_len >= c.gcap) { set_err(c, ERR_SLAB); return true; }
+    GossipSched& gs = gsched(c, r);
+    if (gs.len >= c.gcap) { set_err(c, ERR_SLAB); return true; }
     GossipDev ns;
     ns.gossiper = g.gossiper; ns.seq = g.seq; ns.subject = g.subject; ns.status = g.status(); ns.inc = g.inc();
-    ns.inf_period = (uint32_t)m.g_period;
+    ns.inf_period = gs.period;
     ns.inf[0] = g.from;
 #pragma unroll
     for (int k = 1; k < GINF; ++k) ns.inf[k] = NONE;
-    if (m.g_period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
-    slab.put(m.gossip_len++, ns);
+    if (gs.period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
+    slab.put(gs.len++, ns);
     gix_note(c, m, r, ns.gossiper, ns.seq);
     if (g.status() >= SWIM_GOSSIP_USER)  // sink.next(gossip.message()) (:209): listen() subscribers
       emit(c, r, g.gossiper, SWIM_EV_GOSSIP, SWIM_PHASE_GOSSIP, m.ev_minor++, g.subject);
