@@ -47,8 +47,12 @@
 #define SWIM_STREAM_SYNC_SELECT 30     /* selectSyncAddress, sub24 = 0 / 1, sub32 = attempt   */
 #define SWIM_STREAM_SYNC_OUT 31        /* SYNC sender -> receiver, sub24 = sender ordinal     */
 #define SWIM_STREAM_SYNCACK_OUT 32     /* SYNC_ACK, member = acker, sub24 = inbox rank        */
+#define SWIM_STREAM_SYNC_DELAY 33      /* SYNC delay, member = sender, sub24 = sender ordinal */
+#define SWIM_STREAM_SYNCACK_DELAY 34   /* SYNC_ACK delay, member = acker, sub24 = inbox rank  */
 #define SWIM_STREAM_FETCH_REQ 40       /* GET_METADATA_REQ, sub24 = phase, sub32 = fetch ordinal */
 #define SWIM_STREAM_FETCH_RESP 41      /* GET_METADATA_RESP                                   */
+#define SWIM_STREAM_FETCH_REQ_DELAY 42 /* GET_METADATA_REQ delay, same sub keys as FETCH_REQ */
+#define SWIM_STREAM_FETCH_RESP_DELAY 43 /* GET_METADATA_RESP delay                           */
 #define SWIM_STREAM_PING_INSERT 50     /* pingMembers.add(nextInt(size)), sub24 = phase, sub32 = event minor */
 
 #define SWIM_SYNC_SELECT_ATTEMPTS 64

@@ -131,6 +131,11 @@ struct GossipState {
 
 struct Member {
   bool up = false, joined = false, join_pending = false, join_now = false;
+  // start0's initial sync (:250-291): requests sent / resolved (failed fast or answered), the tick
+  // of the last answer (or of the start), and whether the merged Flux is still subscribed
+  uint32_t init_total = 0, init_done = 0;
+  uint64_t init_last = 0;
+  bool init_wait = false;
   bool leave_pending = false, leave_done = false;
   uint32_t leave_gossiper = NONE;
   uint64_t leave_seq = 0;
@@ -454,6 +459,13 @@ struct swim_engine {
     // the request goes to s's address; another member listening there does not answer (:209)
     const uint32_t d = dst(s);
     bool ok = d == s && !out_fail(v, d, w1) && in_pass(d, v) && !out_fail(d, v, w2) && in_pass(v, d);
+    // requestResponse(...).timeout(metadataTimeout) (:160-165): both legs delayed (tryDelayOutbound
+    // on the request and on the response's send)
+    if (ok && !delay_tab.empty()) {
+      const uint64_t rtt = (uint64_t)delay_ticks(v, d, v, SWIM_STREAM_FETCH_REQ_DELAY, phase, f) +
+                           delay_ticks(d, v, v, SWIM_STREAM_FETCH_RESP_DELAY, phase, f);
+      ok = rtt * tick_ms < (uint64_t)cfg.metadata_timeout;
+    }
     if (ok) STT().fetch_ok++;
     return ok;
   }
@@ -970,6 +982,33 @@ struct swim_engine {
     flush_pending(v, pending, reason, phase);
   }
 
+  // SYNCs / SYNC_ACKs the network emulator delays (tryDelayOutbound :190-202 on doSync's send
+  // :339-357, onSync's SYNC_ACK send :394-415 and start0's requestResponse :268-276): arrival tick ->
+  // messages, each with its content as prepared (the sender's table when it was sent)
+  struct SyncFlight {
+    uint32_t to, from, ordinal;  // ordinal: the sender's SYNC ordinal, or the SYNC_ACK's inbox rank
+    uint64_t sent;
+    bool initial, ack;
+    std::vector<uint64_t> content;
+  };
+  std::map<uint64_t, std::vector<SyncFlight>> sync_in_flight;
+  // a message merged this tick: arrivals sent in earlier ticks first (canonical order (receiver,
+  // sending tick, sender, ordinal / rank))
+  struct SyncArr {
+    uint32_t to, from, ordinal;
+    uint64_t sent;
+    bool initial;
+    const std::vector<uint64_t>* content;
+  };
+  static void sort_arrivals(std::vector<SyncArr>& a) {
+    std::stable_sort(a.begin(), a.end(), [](const SyncArr& x, const SyncArr& y) {
+      if (x.to != y.to) return x.to < y.to;
+      if (x.sent != y.sent) return x.sent < y.sent;
+      if (x.from != y.from) return x.from < y.from;
+      return x.ordinal < y.ordinal;
+    });
+  }
+
   void phase_sync() {
     const uint32_t nt = std::max(1u, threads);
     std::vector<std::vector<SyncReq>> rq(nt);
@@ -992,8 +1031,16 @@ struct swim_engine {
     });
     std::vector<SyncReq> reqs;
     for (auto& x : rq) reqs.insert(reqs.end(), x.begin(), x.end());
-    if (reqs.empty()) {
-      finish_joins(reqs);
+    std::vector<SyncFlight> arriving;
+    {
+      auto it = sync_in_flight.find(T);
+      if (it != sync_in_flight.end()) {
+        arriving.swap(it->second);
+        sync_in_flight.erase(it);
+      }
+    }
+    if (reqs.empty() && arriving.empty()) {
+      finish_joins();
       return;
     }
     // request content: the sender's table when the SYNC is prepared (:485-489)
@@ -1008,90 +1055,112 @@ struct swim_engine {
     auto content_of = [&](uint32_t s) -> const std::vector<uint64_t>& {
       return rows[std::lower_bound(senders.begin(), senders.end(), s) - senders.begin()];
     };
-    std::vector<size_t> delivered;
+    std::vector<SyncArr> in;
     for (size_t i = 0; i < reqs.size(); ++i) {
       SyncReq& q = reqs[i];
+      Member& mf = m[q.from];
       STT().syncs++;
-      if (out_fail(q.from, q.to, draw(q.from, SWIM_STREAM_SYNC_OUT, q.ordinal, 0))) { q.outfail = true; continue; }
+      if (q.initial) mf.init_total++;
+      if (out_fail(q.from, q.to, draw(q.from, SWIM_STREAM_SYNC_OUT, q.ordinal, 0))) {
+        q.outfail = true;
+        if (q.initial) mf.init_done++;  // an error resumes empty: that source completes now
+        continue;
+      }
       if (!in_pass(q.to, q.from)) continue;
       q.delivered = true;
-      delivered.push_back(i);
+      const uint32_t k = delay_ticks(q.from, q.to, q.from, SWIM_STREAM_SYNC_DELAY, q.ordinal, 0);
+      if (k) sync_in_flight[T + k].push_back(SyncFlight{q.to, q.from, q.ordinal, T, q.initial, false, content_of(q.from)});
+      else in.push_back(SyncArr{q.to, q.from, q.ordinal, T, q.initial, &content_of(q.from)});
     }
-    std::stable_sort(delivered.begin(), delivered.end(), [&](size_t a, size_t b) {
-      if (reqs[a].to != reqs[b].to) return reqs[a].to < reqs[b].to;
-      if (reqs[a].from != reqs[b].from) return reqs[a].from < reqs[b].from;
-      return reqs[a].ordinal < reqs[b].ordinal;
-    });
-    // receivers' inboxes: delivered[gs[g] .. gs[g + 1])
+    std::vector<SyncFlight*> ack_arriving;
+    for (auto& f : arriving) {
+      if (f.ack) { ack_arriving.push_back(&f); continue; }
+      if (!m[f.to].up) continue;  // the receiver stopped while the message was in flight
+      in.push_back(SyncArr{f.to, f.from, f.ordinal, f.sent, f.initial, &f.content});
+    }
+    sort_arrivals(in);
+    // receivers' inboxes: in[gs[g] .. gs[g + 1])
     std::vector<size_t> gs;
-    for (size_t i = 0; i < delivered.size(); ++i)
-      if (i == 0 || reqs[delivered[i]].to != reqs[delivered[i - 1]].to) gs.push_back(i);
+    for (size_t i = 0; i < in.size(); ++i)
+      if (i == 0 || in[i].to != in[i - 1].to) gs.push_back(i);
     const uint32_t ng = (uint32_t)gs.size();
-    gs.push_back(delivered.size());
+    gs.push_back(in.size());
     // D1: onSync at each receiver (:394-415)
     par(0, ng, [&](uint32_t a, uint32_t b, uint32_t) {
       for (uint32_t g = a; g < b; ++g) {
-        const uint32_t r = reqs[delivered[gs[g]]].to;
+        const uint32_t r = in[gs[g]].to;
         m[r].ev_minor = 0;
         m[r].fetch_ctr = 0;
-        for (size_t i = gs[g]; i < gs[g + 1]; ++i)
-          sync_membership(r, content_of(reqs[delivered[i]].from), SYNC, SWIM_PHASE_SYNC);
+        for (size_t i = gs[g]; i < gs[g + 1]; ++i) sync_membership(r, *in[i].content, SYNC, SWIM_PHASE_SYNC);
       }
     });
     // SYNC_ACK content: the receiver's table once all its requests are merged
     std::vector<std::vector<uint64_t>> arows(ng);
     par(0, ng, [&](uint32_t a, uint32_t b, uint32_t) {
-      for (uint32_t g = a; g < b; ++g) arows[g] = m[reqs[delivered[gs[g]]].to].row;
+      for (uint32_t g = a; g < b; ++g) arows[g] = m[in[gs[g]].to].row;
     });
-    struct Ack { uint32_t to, from, rank, grp; bool initial; };
-    std::vector<Ack> acks;
+    std::vector<SyncArr> acks;
     for (uint32_t g = 0; g < ng; ++g) {
       for (size_t i = gs[g]; i < gs[g + 1]; ++i) {
-        SyncReq& q = reqs[delivered[i]];
+        const SyncArr& q = in[i];
         const uint32_t qr = (uint32_t)(i - gs[g]);
         if (out_fail(q.to, q.from, draw(q.to, SWIM_STREAM_SYNCACK_OUT, qr, 0))) continue;
         if (!in_pass(q.from, q.to)) continue;
-        q.acked = true;
-        acks.push_back(Ack{q.from, q.to, qr, g, q.initial});
+        const uint32_t k = delay_ticks(q.to, q.from, q.to, SWIM_STREAM_SYNCACK_DELAY, qr, 0);
+        if (k) sync_in_flight[T + k].push_back(SyncFlight{q.from, q.to, qr, T, q.initial, true, arows[g]});
+        else acks.push_back(SyncArr{q.from, q.to, qr, T, q.initial, &arows[g]});
       }
     }
-    std::stable_sort(acks.begin(), acks.end(), [](const Ack& a, const Ack& b) {
-      if (a.to != b.to) return a.to < b.to;
-      if (a.from != b.from) return a.from < b.from;
-      return a.rank < b.rank;
-    });
+    for (SyncFlight* f : ack_arriving)
+      if (m[f->to].up) acks.push_back(SyncArr{f->to, f->from, f->ordinal, f->sent, f->initial, &f->content});
+    sort_arrivals(acks);
     std::vector<size_t> as;
     for (size_t i = 0; i < acks.size(); ++i)
       if (i == 0 || acks[i].to != acks[i - 1].to) as.push_back(i);
     const uint32_t na = (uint32_t)as.size();
     as.push_back(acks.size());
-    // D2: SYNC_ACK merge at the original sender (:363-391), INITIAL_SYNC for start0's requests
+    // D2: SYNC_ACK merge at the original sender (:363-391), INITIAL_SYNC for start0's requests; an
+    // initial answer after start0's Flux completed or timed out has no subscriber any more
     par(0, na, [&](uint32_t a, uint32_t b, uint32_t) {
       for (uint32_t g = a; g < b; ++g) {
         const uint32_t s = acks[as[g]].to;
-        m[s].ev_minor = 0;
-        m[s].fetch_ctr = 0;
+        Member& ms = m[s];
+        ms.ev_minor = 0;
+        ms.fetch_ctr = 0;
         for (size_t i = as[g]; i < as[g + 1]; ++i) {
+          if (acks[i].initial && !ms.init_wait) continue;
           STT().sync_acks++;
-          sync_membership(s, arows[acks[i].grp], acks[i].initial ? INITIAL_SYNC : SYNC, SWIM_PHASE_SYNCACK);
+          sync_membership(s, *acks[i].content, acks[i].initial ? INITIAL_SYNC : SYNC, SWIM_PHASE_SYNCACK);
+          if (acks[i].initial) {
+            ms.init_done++;
+            ms.init_last = T;
+          }
         }
       }
     });
-    finish_joins(reqs);
+    finish_joins();
   }
 
-  // start0's doFinally (:285-289): periodic sync starts once every seed answered or failed fast,
-  // else after syncTimeout.
-  void finish_joins(const std::vector<SyncReq>& reqs) {
+  // start0's doFinally (:285-289): periodic sync starts once every initial SYNC was answered or
+  // failed fast; else after syncTimeout without an answer (Flux.timeout :281 restarts at every
+  // answer).  Without message delay every source resolves within the start tick (the start is
+  // decided then, as complete ? now : now + syncTimeout); with delay the decision waits for the last
+  // answer or the timeout, which fires at the tick init_last + syncTimeout (an answer arriving in
+  // that tick is too late).
+  void finish_joins() {
+    const bool delayed = !delay_tab.empty();
     for (uint32_t v = 0; v < n; ++v) {
       Member& mv = m[v];
-      if (!mv.join_now) continue;
-      bool complete = true;
-      for (auto& q : reqs)
-        if (q.from == v && q.initial && !(q.outfail || q.acked)) complete = false;
-      mv.sync_on = true;
-      mv.sync_start = (int64_t)T + (complete ? 0 : (int64_t)sync_to_ticks);
       mv.join_now = false;
+      if (!mv.init_wait) continue;
+      int64_t start;
+      if (!delayed) start = (int64_t)T + (mv.init_done == mv.init_total ? 0 : (int64_t)sync_to_ticks);
+      else if (mv.init_done == mv.init_total) start = (int64_t)mv.init_last;
+      else if (T + 1 >= mv.init_last + sync_to_ticks) start = (int64_t)(mv.init_last + sync_to_ticks);
+      else continue;
+      mv.sync_on = true;
+      mv.sync_start = start;
+      mv.init_wait = false;
     }
   }
 
@@ -1106,6 +1175,9 @@ struct swim_engine {
       mv.up = true;
       mv.joined = true;
       mv.join_now = true;
+      mv.init_total = mv.init_done = 0;
+      mv.init_last = T;
+      mv.init_wait = true;
       mv.fd_start = (int64_t)T;
       mv.g_start = (int64_t)T;
       mv.row[v] = B_IN_TABLE | B_IN_MEMBERS;  // ALIVE inc 0 (MembershipProtocolImpl :146-149)

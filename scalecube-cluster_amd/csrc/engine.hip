@@ -513,6 +513,11 @@ static int32_t run_tick(swim_engine* e) {
   }
   // ---- D: SYNC / SYNC_ACK
   // (SYNC requests were collected by k_gossip_deliver on gossip ticks, by k_fd on the others)
+  if (e->sh[0].c.delay_on) {  // delayed SYNCs: contents parked, arrivals into the inboxes
+    Shard& sd = e->sh[0];
+    k_sync_delay<<<256, 256, 0, s>>>(sd.d_par, T);
+    TICK_CHECK("k_sync_delay");
+  }
   for (int d2 = 0; d2 < 2; ++d2) {
     if (multi) {
       for (Shard& sd : e->sh) {
@@ -541,6 +546,10 @@ static int32_t run_tick(swim_engine* e) {
       TICK_CHECK("k_sync_classify");
       launch_apply(e, sd, d2, classified, fused);
       TICK_CHECK("k_sync_apply");
+      if (d2 == 0 && sd.c.delay_on) {  // delayed SYNC_ACKs: contents parked, the acks deferred
+        k_ack_delay<<<256, 256, 0, s>>>(sd.d_par, T);
+        TICK_CHECK("k_ack_delay");
+      }
     }
   }
   for (Shard& sd : e->sh) {
@@ -701,6 +710,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.G = e->G;
   c.S = e->S;
   c.sync_to_ticks = (uint32_t)cf.sync_timeout / e->tick_ms;
+  c.metadata_timeout = (uint32_t)cf.metadata_timeout;
   c.tick_ms = e->tick_ms;
   c.ping_interval = cf.ping_interval;
   c.suspicion_mult = cf.suspicion_mult;
@@ -1354,6 +1364,20 @@ static int32_t enable_delay(swim_engine* e) {
   if (!sd.alloc(&dq, (size_t)DQ_BUCKETS * bcap)) return SWIM_ENOMEM;
   sd.b.dq = dq;
   sd.b.dq_bcap = bcap;
+  // delayed SYNCs / SYNC_ACKs: a bucket holds a few ticks' worth of SYNCs (N / S per tick, and as
+  // many acks); every message in flight parks its content row (at most 1 GiB of rows)
+  const uint32_t per_tick = (e->n + sd.c.S - 1) / std::max(sd.c.S, 1u);
+  const uint32_t sbcap = 64 + 8 * per_tick;
+  const uint32_t pcap = (uint32_t)std::min<uint64_t>(4ull * sbcap, std::max<uint64_t>(64, (1ull << 28) / e->n));
+  Bufs& b = sd.b;
+  if (!sd.alloc(&b.sdq, (size_t)DQ_BUCKETS * sbcap) || !sd.alloc(&b.sdq_cnt, DQ_BUCKETS) ||
+      !sd.alloc(&b.park, (size_t)pcap * e->n) || !sd.alloc(&b.park_avail, pcap) || !sd.alloc(&b.park_freed, pcap) ||
+      !sd.alloc(&b.park_jobs, pcap) || !sd.alloc(&b.park_ctl, 1))
+    return SWIM_ENOMEM;
+  if (hipMemset(b.sdq_cnt, 0, 4ull * DQ_BUCKETS) != hipSuccess || hipMemset(b.park_ctl, 0, sizeof(SpillCtl)) != hipSuccess)
+    return SWIM_EDEVICE;
+  b.sdq_bcap = sbcap;
+  b.park_cap = pcap;
   sd.c.delay_on = 1;
   return SWIM_OK;
 }

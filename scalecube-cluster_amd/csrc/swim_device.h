@@ -39,6 +39,7 @@ enum : uint32_t {
   ERR_COLL_TOP = 1u << 15,  // a collector outgrew the top spill tier (ERR_INTERVALS: a tier's pool ran dry)
   ERR_DELAY = 1u << 16,     // more delayed GOSSIP_REQs arrive in one tick than a delay bucket holds
   ERR_XPTR = 1u << 17,      // SWIM_DEBUG_SYNC: a sharded tick would dereference a null exchange pointer
+  ERR_SDELAY = 1u << 18,    // delayed SYNCs / SYNC_ACKs: a delay bucket or the park slots ran out
 };
 
 // stats slots (swim_stats order)
@@ -78,11 +79,12 @@ struct alignas(16) MemberDev {
   uint32_t ins_rank, ins_head, ins_tail;  // this phase's deferred pingMembers inserts (op chain)
   uint32_t gix_base, gix_used;  // serial of slab[0]; gix slots taken since the index was (re)built
   uint32_t ack_late;  // 1 + ticks after the ping timeout that a late direct ack arrives (0 = none)
+  uint32_t init_last;  // start0's initial sync: tick of the last answer (or of the start)
   uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, gix_valid;
   uint8_t ack_ok;    // ack_due is the tick the (delayed) ack arrives, not the ping timeout
   uint8_t relay_ok;  // relay_due is the tick the first relayed ack arrives, not the timeout
   uint8_t ack_gone, relay_gone;  // that ack says DEST_GONE (another member listens at the target's address)
-  uint8_t pad[1];
+  uint8_t init_wait;  // start0's initial-sync Flux is still subscribed (init_total / init_done)
 };
 
 // GossipState + Gossip + MembershipRecord payload, 48 B.  GossipState.infected gains a member only
@@ -251,6 +253,7 @@ struct Ctx {
   uint32_t n, gcap, hcap, wheel_mask, wheel_nq;
   uint32_t lo, nl, sz, rank, world;
   uint32_t P, to_ticks, relay_ticks, G, S, sync_to_ticks, tick_ms;
+  uint32_t metadata_timeout;  // ms (a delayed GET_METADATA round trip must finish before it)
   int32_t ping_interval, suspicion_mult, repeat_mult, fanout, ping_req_members, seg_threshold, record_fd;
   uint32_t key0, key1;
   uint64_t T;
@@ -965,6 +968,13 @@ __device__ inline bool fetch_ok(const Ctx& c, uint32_t v, uint32_t s, uint32_t p
   const uint32_t d = dst(c, s);
   bool ok = d == s && !out_fail(c, v, d, v, SWIM_STREAM_FETCH_REQ, phase, f) && in_pass(c, d, v) &&
             !out_fail(c, d, v, v, SWIM_STREAM_FETCH_RESP, phase, f) && in_pass(c, v, d);
+  // requestResponse(...).timeout(metadataTimeout) (:160-165): both legs delayed (tryDelayOutbound on
+  // the request and on the response's send)
+  if (ok && c.delay_on) {
+    const uint64_t rtt = (uint64_t)delay_ticks(c, v, d, v, SWIM_STREAM_FETCH_REQ_DELAY, phase, f) +
+                         delay_ticks(c, d, v, v, SWIM_STREAM_FETCH_RESP_DELAY, phase, f);
+    ok = rtt * c.tick_ms < (uint64_t)c.metadata_timeout;
+  }
   if (ok) stat_add(c, ST_FETCH_OK, 1);
   return ok;
 }

@@ -17,7 +17,7 @@ namespace swimdev {
 
 // per-tick scratch counters, zeroed by one hipMemsetAsync at the start of every tick
 struct Counters {
-  uint32_t msg_total, pg_cursor, pad0;  // messages materialised this round; inbox pages taken
+  uint32_t msg_total, pg_cursor, park_jobs;  // messages materialised this round; inbox pages taken; SYNC rows to park
   uint32_t req_total, req_recv_cnt, req_pg;  // SYNC items, receivers, inbox pages taken
   uint32_t ack_total, ack_recv_cnt, ack_pg;  // the same for SYNC_ACKs
   uint32_t ins_total, pad1;   // overflow list-insert ops of the gossip phase
@@ -89,6 +89,19 @@ struct Bufs {
   GMsgFull* dq;        // [DQ_BUCKETS][dq_bcap]
   uint32_t* dq_cnt;    // [DQ_BUCKETS]
   uint32_t dq_bcap;
+  // SYNCs / SYNC_ACKs delayed by the network emulator: bucket (arrival tick & DQ_MASK) holds up to
+  // sdq_bcap messages (RQ_PARKED: .snap = the park slot holding the content as it was prepared, .pad
+  // = the sending tick).  k_sync_delay copies this tick's delayed SYNC contents into their slots and
+  // moves the arrivals into the inboxes; a SYNC_ACK's content is parked by its acker's workgroup.
+  SyncReq* sdq;         // [DQ_BUCKETS][sdq_bcap]
+  uint32_t* sdq_cnt;    // [DQ_BUCKETS]
+  uint32_t sdq_bcap;
+  uint32_t* park;       // [park_cap][n] content rows of the messages in flight
+  uint32_t park_cap;
+  uint32_t* park_avail; // [park_cap] reusable slots (refilled from park_freed by k_end_tick)
+  uint32_t* park_freed; // [park_cap] slots whose message arrived this tick
+  uint2* park_jobs;     // [park_cap] (slot, sender): SYNC content rows to copy this tick
+  SpillCtl* park_ctl;   // (bump, avail, freed) of the slots
   // SYNC / SYNC_ACK sub-phases (swim_sync.h): items in enqueue order; a receiver's inbox is paged
   // like the gossip inboxes: its k-th message is item pool[tab[r][k / 64]][k % 64]
   SyncReq* reqs;
@@ -275,6 +288,8 @@ __global__ void k_start_joins(KP) {
   m.join_pending = 0;
   m.joined = 1;
   m.join_now = 1;
+  m.init_wait = 1;
+  m.init_last = (uint32_t)c.T;
   m.fd_start = (int64_t)c.T;
   m.g_start = (int64_t)c.T;
   c.gs[i].next = (uint32_t)c.T + c.G;
@@ -1615,7 +1630,11 @@ __device__ inline uint32_t select_sync_address(const Ctx& c, uint32_t v) {
 
 // SyncReq.flags: bits 0..2 below; bits 8..31 the number of records the message carries (the
 // sender's table size when the message is prepared: the count syncMembership iterates, :491-509)
-enum : uint32_t { RQ_INITIAL = 1, RQ_OUTFAIL = 2, RQ_DELIVERED = 4, RQ_RECS_SHIFT = 8 };
+// RQ_PARKED: a delayed message (content in park slot .snap, sent in tick .pad); RQ_ACK: in the delay
+// queue, a SYNC_ACK (else a SYNC)
+// RQ_DEFER: a SYNC_ACK of this tick that k_ack_delay parked (its SYNC_ACK sub-phase skips it)
+enum : uint32_t { RQ_INITIAL = 1, RQ_OUTFAIL = 2, RQ_DELIVERED = 4, RQ_PARKED = 16, RQ_ACK = 32, RQ_DEFER = 64,
+                  RQ_RECS_SHIFT = 8 };
 
 // per-member SYNC roles of the tick (Bufs.sflag)
 enum : uint32_t {
@@ -1753,6 +1772,41 @@ __device__ __forceinline__ void enqueue_sync(const Ctx& c, const Bufs& b, int d2
   enqueue_sync(c, b, d2, q, valid, valid && !d2 ? b.sflag[q.to - c.lo] : 0u);
 }
 
+// ---- delayed SYNC / SYNC_ACK (tryDelayOutbound :190-202 on doSync's and onSync's send, :339-357,
+// :394-415, and start0's requestResponse :268-276)
+__device__ __forceinline__ uint32_t* park_row(const Ctx& c, const Bufs& b, uint32_t slot) {
+  return b.park + (size_t)slot * c.n;
+}
+__device__ inline uint32_t park_alloc(const Ctx& c, const Bufs& b) {
+  const int32_t a = atomicSub(&b.park_ctl->avail, 1);
+  if (a > 0) return b.park_avail[a - 1];
+  const uint32_t i = atomicAdd(&b.park_ctl->bump, 1u);
+  if (i < b.park_cap) return i;
+  set_err(c, ERR_SDELAY);
+  return NONE;
+}
+// message q (its content already in park slot q.snap) arrives `k` ticks from now
+__device__ inline void park_put(const Ctx& c, const Bufs& b, SyncReq q, uint32_t k, bool ack) {
+  q.flags |= RQ_PARKED | (ack ? RQ_ACK : 0u);
+  q.pad = (uint32_t)c.T;
+  q.content = NONE;
+  const uint32_t bk = (uint32_t)(c.T + k) & DQ_MASK;
+  const uint32_t i = atomicAdd(&b.sdq_cnt[bk], 1u);
+  if (i >= b.sdq_bcap) { set_err(c, ERR_SDELAY); return; }
+  b.sdq[(size_t)bk * b.sdq_bcap + i] = q;
+}
+// a delayed SYNC: its content (the sender's row now, before any merge of this tick) is copied by
+// k_sync_delay
+__device__ inline void park_request(const Ctx& c, const Bufs& b, SyncReq q, uint32_t k) {
+  const uint32_t slot = park_alloc(c, b);
+  if (slot == NONE) return;
+  const uint32_t j = atomicAdd(&b.k->park_jobs, 1u);
+  if (j >= b.park_cap) { set_err(c, ERR_SDELAY); return; }
+  b.park_jobs[j] = make_uint2(slot, q.from);
+  q.snap = slot;
+  park_put(c, b, q, k, false);
+}
+
 __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t to, uint32_t ordinal, bool initial) {
   MemberDev& m = mem(c, v);
   SyncReq q;
@@ -1766,6 +1820,10 @@ __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t
   }
   if (!in_pass(c, to, v)) return;  // inbound-blocked at the receiver: silently dropped
   q.flags |= RQ_DELIVERED;
+  if (c.delay_on) {  // (single-shard engines only)
+    const uint32_t k = delay_ticks(c, v, to, v, SWIM_STREAM_SYNC_DELAY, ordinal, 0);
+    if (k) { park_request(c, b, q, k); return; }
+  }
   sflag_set(c, b, v - c.lo, owned(c, to) ? SF_SENT | SF_SENT_LOCAL : SF_SENT);
   if (!owned(c, to)) {  // content (this row) travels with the request: k_pack_rows
     const uint32_t d = owner(c, to);
@@ -1829,7 +1887,8 @@ __device__ inline unsigned long long sync_collect_pre(const Ctx& c, const Bufs& 
   const uint32_t i = v - c.lo, t32 = (uint32_t)c.T;
   const bool due = sn == t32;  // the periodic doSync timer fires (sync_on, phase sync_start)
   if (!due && !(fl & (MF_FDSYNC | MF_JOIN))) return 0;
-  if (due && !(fl & (MF_FDSYNC | MF_JOIN)) && !c.n_links && !c.partition && !c.route) return sync_collect_fast(c, b, v);
+  if (due && !(fl & (MF_FDSYNC | MF_JOIN)) && !c.n_links && !c.partition && !c.route && !c.delay_on)
+    return sync_collect_fast(c, b, v);
   if (due) c.sync_next[i] = t32 + c.S;
   if (fl & MF_FDSYNC) c.mflag[i] = fl & ~MF_FDSYNC;
   MemberDev& m = mem(c, v);
@@ -1988,6 +2047,20 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
       c.wheel_ctl->freed = 0;
     }
   }
+  // park slots of the delayed SYNCs / SYNC_ACKs delivered this tick become allocatable (workgroup
+  // NTIER + 1, as above)
+  if (c.delay_on && blockIdx.x == (gridDim.x > NTIER + 1 ? (uint32_t)NTIER + 1 : 0u)) {
+    const Bufs& b = P->b;
+    const int32_t a0 = b.park_ctl->avail;
+    const uint32_t a = a0 > 0 ? (uint32_t)a0 : 0u, f = min(b.park_ctl->freed, b.park_cap - a);
+    for (uint32_t j = threadIdx.x; j < f; j += blockDim.x) b.park_avail[a + j] = b.park_freed[j];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      b.park_ctl->avail = (int32_t)(a + f);
+      b.park_ctl->freed = 0;
+      b.sdq_cnt[(uint32_t)T & DQ_MASK] = 0;  // this tick's delayed SYNC arrivals are in the inboxes
+    }
+  }
   // receipt-bitmap slots requested this tick change owner (no other kernel runs now): zeroed bits,
   // valid from the next tick; the other parity's queue (next tick's) is emptied
   {
@@ -2015,15 +2088,30 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
   if (i >= c.nl) return;
   const uint32_t fl = c.mflag[i];
   if (!(fl & (MF_JOIN | MF_LEAVE))) return;
-  c.mflag[i] = fl & ~(MF_JOIN | MF_LEAVE);
   const uint32_t v = c.lo + i;
   MemberDev& m = c.mem[i];
-  if (m.join_now) {
-    m.sync_on = 1;
-    m.sync_start = (int64_t)c.T + (m.init_done == m.init_total ? 0 : (int64_t)c.sync_to_ticks);
-    m.join_now = 0;
-    c.sync_next[i] = next_due(m.sync_start, c.T, c.S);
+  uint32_t keep = 0;
+  // start0's doFinally (:285-289): periodic sync starts once every initial SYNC was answered or
+  // failed fast, else syncTimeout after the last answer (Flux.timeout :281).  Without message delay
+  // every source resolves within the start tick; with delay the decision may wait (MF_JOIN is kept)
+  // until the last answer or the timeout, which fires at tick init_last + syncTimeout.
+  if (m.init_wait) {
+    const uint64_t last = m.init_last;
+    int64_t start = -1;
+    if (!c.delay_on) start = (int64_t)c.T + (m.init_done == m.init_total ? 0 : (int64_t)c.sync_to_ticks);
+    else if (m.init_done == m.init_total) start = (int64_t)last;
+    else if (c.T + 1 >= last + c.sync_to_ticks) start = (int64_t)(last + c.sync_to_ticks);
+    if (start >= 0) {
+      m.sync_on = 1;
+      m.sync_start = start;
+      m.init_wait = 0;
+      c.sync_next[i] = next_due(m.sync_start, c.T, c.S);
+    } else {
+      keep = MF_JOIN;
+    }
   }
+  m.join_now = 0;
+  c.mflag[i] = (fl & ~(MF_JOIN | MF_LEAVE)) | keep;
   if (m.leave_done) {
     m.leave_done = 0;
     m.leave_pending = 0;

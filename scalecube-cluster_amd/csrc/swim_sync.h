@@ -445,6 +445,7 @@ __device__ inline uint32_t content_at(const Content& k, uint32_t x) {
 }
 // the content of message q (received rows, the sender's slot or its live row)
 __device__ __forceinline__ Content msg_content(const Ctx& c, const Bufs& b, const SyncReq& q, int d2) {
+  if (q.flags & RQ_PARKED) return Content{park_row(c, b, q.snap), nullptr, nullptr, 0};  // delayed
   if (q.content != NONE) return Content{remote_row(c, b, d2, q.content), nullptr, nullptr, 0};
   const uint32_t i = q.from - c.lo;
   const uint32_t si = (d2 ? b.ack_snap : b.snap_idx)[i];
@@ -687,7 +688,13 @@ __device__ void sync_msg_wg(const Ctx& c, const Bufs& b, uint32_t r, uint32_t it
   __syncthreads();
 }
 
-// the receiver's inbox in canonical order (sender, ordinal) -> s_it (item indices); its page table
+// canonical inbox order: messages sent in earlier ticks (delayed) first, then (sender, ordinal / rank)
+__device__ __forceinline__ uint64_t inbox_key(const Ctx& c, const SyncReq& q) {
+  const uint32_t age = (q.flags & RQ_PARKED) ? min((uint32_t)c.T - q.pad, 2047u) : 0u;
+  return ((uint64_t)(2047u - age) << 53) | ((uint64_t)q.from << 24) | (q.ordinal & 0xffffffu);
+}
+
+// the receiver's inbox in canonical order (sending tick, sender, ordinal) -> s_it (item indices); its page table
 // is reset for the next sub-phase.  Every thread of the workgroup calls it; returns the count.
 // (inl0: the inbox's first inline slot, loaded by the caller with the receiver's other words)
 __device__ inline uint32_t load_inbox(const Ctx& c, const Bufs& b, const SyInbox& x, uint32_t r, uint32_t k,
@@ -709,7 +716,7 @@ __device__ inline uint32_t load_inbox(const Ctx& c, const Bufs& b, const SyInbox
     }
     s_raw[q] = it;
     const SyncReq rq = x.items[it < b.req_cap ? it : 0];
-    s_key[q] = it < b.req_cap ? (((uint64_t)rq.from << 32) | rq.ordinal) : ~0ull;  // unique per inbox
+    s_key[q] = it < b.req_cap ? inbox_key(c, rq) : ~0ull;  // unique per inbox
   }
   __syncthreads();
   for (uint32_t q = threadIdx.x; q < k; q += blockDim.x) {
@@ -723,6 +730,72 @@ __device__ inline uint32_t load_inbox(const Ctx& c, const Bufs& b, const SyInbox
       x.tab[(size_t)r * b.sy_max + pg] = NONE;
   __syncthreads();
   return k;
+}
+
+// With message delay, between the SYNC and the SYNC_ACK sub-phases: each SYNC_ACK sent this tick draws
+// its delay (the acker's SYNCACK_DELAY stream, keyed by the ack's inbox rank); a delayed one parks
+// the acker's row as it is now (after its SYNC merges) and is deferred (RQ_DEFER: the SYNC_ACK
+// sub-phase skips it).  One workgroup per ack; out of k_sync_apply, whose ack loop keeps its registers.
+__global__ void __launch_bounds__(256) k_ack_delay(KP) {
+  const Ctx c = pctx_sync(P, T);
+  const Bufs b = P->b;
+  __shared__ uint32_t s_slot;
+  const uint32_t na = min(b.k->ack_total, b.req_cap);
+  for (uint32_t it = blockIdx.x; it < na; it += gridDim.x) {
+    SyncReq a = b.acks[it];
+    if (a.flags & RQ_PARKED) continue;  // an arrival from the delay queue (uniform)
+    const uint32_t dl = delay_ticks(c, a.from, a.to, a.from, SWIM_STREAM_SYNCACK_DELAY, a.ordinal, 0);
+    if (!dl) continue;
+    if (threadIdx.x == 0) s_slot = park_alloc(c, b);
+    __syncthreads();
+    const uint32_t slot = s_slot;
+    if (slot != NONE) copy_row(rec_row(c, a.from), park_row(c, b, slot), c.n);
+    __syncthreads();  // (the row is parked before the message is queued, and s_slot is reused)
+    if (threadIdx.x == 0) {
+      b.acks[it].flags = a.flags | RQ_DEFER;
+      if (slot != NONE) {
+        a.slot = 0;
+        a.snap = slot;
+        park_put(c, b, a, dl, true);
+      }
+    }
+  }
+}
+
+// With message delay, before the SYNC sub-phase: (1) the content rows of this tick's delayed SYNCs
+// (their senders' rows before any merge of the tick) into their park slots, one workgroup per row;
+// (2) the delayed SYNCs and SYNC_ACKs arriving now into the inboxes (a message whose receiver stopped
+// meanwhile is dropped); their slots are reusable from the next tick (k_end_tick).
+__global__ void __launch_bounds__(256) k_sync_delay(KP) {
+  const Ctx c = pctx_sync(P, T);
+  const Bufs b = P->b;
+  const uint32_t nj = min(b.k->park_jobs, b.park_cap);
+  for (uint32_t j = blockIdx.x; j < nj; j += gridDim.x) {
+    const uint2 jb = b.park_jobs[j];
+    copy_row(rec_row(c, jb.y), park_row(c, b, jb.x), c.n);
+  }
+  const uint32_t bk = (uint32_t)T & DQ_MASK;
+  const uint32_t cnt = min(b.sdq_cnt[bk], b.sdq_bcap);
+  const SyncReq* dq = b.sdq + (size_t)bk * b.sdq_bcap;
+  const uint32_t lane = threadIdx.x & 63;
+  // (wave-uniform trip count: enqueue_sync's page discipline wants every lane of the wave)
+  for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); i0 < cnt; i0 += gridDim.x * blockDim.x) {
+    const uint32_t i = i0 + lane;
+    SyncReq q{};
+    bool valid = i < cnt, ack = false;
+    if (valid) {
+      q = dq[i];
+      ack = (q.flags & RQ_ACK) != 0;
+      b.park_freed[atomicAdd(&b.park_ctl->freed, 1u)] = q.snap;
+      valid = c.up[q.to] != 0;
+      // an ack's receiver — and a SYNC's sender, whose ack may come back this tick — is merged into in
+      // the SYNC_ACK sub-phase: if it is also read as SYNC_ACK content this tick (it received a SYNC),
+      // it takes a snapshot slot (sflag_set_from)
+      if (valid) sflag_set(c, b, (ack ? q.to : q.from) - c.lo, SF_SENT);
+    }
+    enqueue_sync(c, b, 0, q, valid && !ack);
+    enqueue_sync(c, b, 1, q, valid && ack);
+  }
 }
 
 // D1 (d2 = 0): onSync at each receiver, then its SYNC_ACKs.  D2 (d2 = 1): the SYNC_ACK merge at
@@ -762,6 +835,8 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
     const uint32_t k = min(x.cnt[li], SY_INBOX);
     const uint32_t inl0 = x.inl[(size_t)li * SY_INLINE];
     const uint32_t tsz0 = mem(c, s).table_size, ins0 = mem(c, s).ins_rank;
+    // start0's Flux still takes initial SYNC_ACKs (an answer after its completion or timeout is dropped)
+    const bool iwait = d2 && mem(c, s).init_wait;
     // s both sent and received this tick (its roles are final since collection): other receivers
     // read this row as content while this workgroup merges into it, so it is copied into its slot
     // before the first change (lazy snapshot, Content above)
@@ -779,27 +854,29 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       const uint32_t it = s_it[q];
       if (it >= b.req_cap) continue;  // a page the pool could not give (ERR_REQS is set); uniform
       const SyncReq rq = x.items[it];
+      if (d2 && ((rq.flags & RQ_DEFER) || ((rq.flags & RQ_INITIAL) && !iwait))) continue;  // (uniform)
+      const bool parked = (rq.flags & RQ_PARKED) != 0;
       const uint32_t tot_q = fused ? 0u : itot[it];  // issued with the header (stable since classify)
       const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
       uint32_t npend = 0;
       const uint32_t mod = s_mod;
       const bool own = d2 && !classified;  // this kernel classifies the ack
       uint32_t d1 = NONE;
-      if (own && rq.pad != 0 && rq.content == NONE && b.row_mod[rq.from - c.lo] != (uint32_t)c.T &&
+      if (own && !parked && rq.pad != 0 && rq.content == NONE && b.row_mod[rq.from - c.lo] != (uint32_t)c.T &&
           b.row_mod[s - c.lo] != (uint32_t)c.T)
         d1 = rq.pad - 1;
       const bool pre = !fused && mod == 0 && (!own || d1 != NONE);  // precomputed classification is exact
       const uint32_t at = d1 != NONE ? d1 : it;
       const uint32_t tot = pre ? (d1 != NONE ? b.rev_total[at] : tot_q) : 0u;
       __syncthreads();  // every lane has read s_mod before lane 0 may set it
-      if (fused) {  // unsharded SYNC sub-phase: the in-workgroup witness merge (no classify launch)
+      if (fused && !parked) {  // unsharded SYNC sub-phase: the in-workgroup witness merge (no classify launch)
         sync_msg_wg(c, b, s, it, rq, CLS_REV && mod == 0, reason, phase, pend, npend, s_list, s_wave, &s_mod,
                     s_need, slot, copied, prof);
       } else if (!copied && (!pre || tot != 0)) {  // this message may change the row: the lazy snapshot first
         lazy_snapshot(c, b, s, slot, d2);
         copied = true;
       }
-      if (fused) {
+      if (fused && !parked) {
       } else if (pre) {  // the row is unchanged since classify
         if (threadIdx.x < 64 && tot != 0) {
           const Content kc = msg_content(c, b, rq, d2);
@@ -850,7 +927,8 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
           if (!out_fail(c, s, rq.from, s, SWIM_STREAM_SYNCACK_OUT, q, 0) && in_pass(c, rq.from, s)) {
             a.from = s; a.to = rq.from; a.ordinal = q; a.slot = 0;
             a.flags = RQ_DELIVERED | (rq.flags & RQ_INITIAL) | (tsz << RQ_RECS_SHIFT);
-            a.content = NONE; a.snap = NONE; a.pad = CLS_REV && rq.content == NONE ? it + 1 : 0;
+            a.content = NONE; a.snap = NONE;
+            a.pad = CLS_REV && rq.content == NONE && !(rq.flags & RQ_PARKED) ? it + 1 : 0;
             valid = true;
             // the lone SYNC_ACK shortcut: the ack is the only one its receiver gets this tick (it sent
             // one SYNC and received none, so its row is unchanged since classify), this row did not
@@ -858,7 +936,7 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
             // that could change the receiver: its merge is a no-op, so the SYNC_ACK sub-phase's
             // bookkeeping for it (onSyncAck :385-391: the phase's minor / fetch counters restart, an
             // INITIAL ack completes a join step, the counters) is done here and nothing is enqueued
-            if (CLS_REV && rq.content == NONE && s_mod == 0 && owned(c, rq.from) &&
+            if (valid && CLS_REV && !c.delay_on && rq.content == NONE && s_mod == 0 && owned(c, rq.from) &&
                 (ACK_NORECV_EXPERIMENT || !sflag_has(c, b, rq.from - c.lo, SF_RECV)) &&
                 !sflag_has(c, b, rq.from - c.lo, SF_MULTI) &&
                 b.rev_total[it] == 0) {
@@ -887,11 +965,20 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
         if (s_mod) b.row_mod[s - c.lo] = (uint32_t)c.T;  // invalidates the reverse classifications
       } else {
         // start0's initial-sync completion counts the acks of its INITIAL SYNCs (:270-284)
-        uint32_t init = 0;
-        for (uint32_t q = 0; q < k; ++q)
-          init += (s_it[q] < b.req_cap && (x.items[s_it[q]].flags & RQ_INITIAL)) ? 1u : 0u;
-        mem(c, s).init_done += init;
-        stat_add(c, ST_SYNC_ACKS, k);
+        uint32_t init = 0, acks = 0;
+        for (uint32_t q = 0; q < k; ++q) {
+          if (s_it[q] >= b.req_cap) continue;
+          const uint32_t fl = x.items[s_it[q]].flags;
+          const bool ini = (fl & RQ_INITIAL) != 0;
+          if ((fl & RQ_DEFER) || (ini && !iwait)) continue;  // skipped above
+          init += ini ? 1u : 0u;
+          acks++;
+        }
+        if (init) {
+          mem(c, s).init_done += init;
+          mem(c, s).init_last = (uint32_t)c.T;
+        }
+        stat_add(c, ST_SYNC_ACKS, acks);
       }
       x.cnt[s - c.lo] = 0;
       stat_add(c, ST_SYNC_RECORDS, s_recs);

@@ -210,6 +210,18 @@ def catalog() -> list[Scenario]:
                       (30, "kill", 9), (45, "join_at", 32, 5), (60, "join_at", 33, 9), (200, "kill", 33),
                       (215, "join_at", 34, 9)],
                  check_every=50, shardable=False),
+        # SYNC / SYNC_ACK and GET_METADATA under delay (NetworkEmulatorTransport :59-75 delays every
+        # send and requestResponse): a 120 ms mean on every link, a 600 ms link, 2 % loss; members join
+        # through two seeds (initial SYNCs answered late or timed out), a kill, a metadata update (every
+        # viewer's fetch races the 300 ms metadata timeout)
+        Scenario("sync_delay_24", 24, 16, 420, seed=27, seeds=(0, 3),
+                 cfg=dict(sync_interval=2000, sync_timeout=300, ping_interval=600, ping_timeout=300,
+                          metadata_timeout=300, record_fd_events=1, delay_capacity=16384),
+                 ops=[(0, "default_delay", 120, abi.ALL_MEMBERS), (0, "loss", 2, abi.ALL_MEMBERS),
+                      (0, "link_delay", 3, 0, 600), (4, "join", 16), (9, "join", 17), (9, "join", 18),
+                      (30, "join", 19), (31, "join", 20), (60, "kill", 7), (80, "update_meta", 2),
+                      (150, "join", 21), (150, "join", 22), (151, "join", 23)],
+                 check_every=20, shardable=False),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),
                  cfg=dict(sync_interval=5000), ops=[(100, "partition", _partition(32, 16)), (1100, "partition", None)],
