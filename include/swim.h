@@ -254,8 +254,12 @@ int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t l
  * evaluateDelay (:359-369) from the Philox hook (swim_delay.h).  Applies to the failure
  * detector's pings, ping-reqs and acks (a round trip completes when both legs arrived; a late
  * direct ack joins the ping-req race, :153-210) and to GOSSIP_REQs (delivered in the gossip phase
- * of their arrival tick, after the arrivals of earlier rounds).  SYNC / SYNC_ACK and metadata
- * round trips are not delayed.  Single-shard engines only (SWIM_EINVAL otherwise).
+ * of their arrival tick, after the arrivals of earlier rounds), to SYNC / SYNC_ACK (each delayed
+ * message carries its content as prepared; start0's initial-sync timeout restarts at every
+ * answer, MembershipProtocolImpl.java:268-289) and to GET_METADATA round trips (a fetch whose round
+ * trip reaches metadataTimeout fails, MetadataStoreImpl.java:146-185); DESIGN.md §3.  Sharded
+ * engines too (a delayed message waits in its sender's shard and joins the exchange of its
+ * arrival tick); N <= 2^20 (SWIM_EINVAL otherwise).
  * A mean above SWIM_DELAY_MEAN_MAX_TICKS (64) ticks is refused with SWIM_EINVAL: the quantised
  * delay is capped at SWIM_DELAY_TICKS_MAX ticks and would truncate draws (swim_delay.h). */
 int32_t swim_set_default_delay(swim_engine* e, uint32_t m, int32_t mean_ms);

@@ -513,11 +513,11 @@ static int32_t run_tick(swim_engine* e) {
   }
   // ---- D: SYNC / SYNC_ACK
   // (SYNC requests were collected by k_gossip_deliver on gossip ticks, by k_fd on the others)
-  if (e->sh[0].c.delay_on) {  // delayed SYNCs: contents parked, arrivals into the inboxes
-    Shard& sd = e->sh[0];
-    k_sync_delay<<<256, 256, 0, s>>>(sd.d_par, T);
-    TICK_CHECK("k_sync_delay");
-  }
+  if (e->sh[0].c.delay_on)  // delayed SYNCs: contents parked, arrivals into the inboxes / the exchange
+    for (Shard& sd : e->sh) {
+      k_sync_delay<<<256, 256, 0, s>>>(sd.d_par, T);
+      TICK_CHECK("k_sync_delay");
+    }
   for (int d2 = 0; d2 < 2; ++d2) {
     if (multi) {
       for (Shard& sd : e->sh) {
@@ -1354,31 +1354,34 @@ static int32_t delay_table(swim_engine* e, int32_t mean_ms, int32_t* idx) {
   *idx = (int32_t)(nt - 1);
   return SWIM_OK;
 }
-// the delay ring and the per-tick release are set up the first time a delay is configured
+// the delay rings and the per-tick release are set up on every shard the first time a delay is
+// configured.  A delayed message waits in its SENDER's shard and joins the exchange of its arrival
+// tick (GOSSIP_REQs: k_dq_release; SYNC / SYNC_ACK: k_sync_delay), so sharded engines need nothing more.
 static int32_t enable_delay(swim_engine* e) {
-  if (e->world > 1 || e->sh.size() != 1 || e->n > (1u << 20)) return SWIM_EINVAL;  // single shard only
-  Shard& sd = e->sh[0];
-  if (sd.c.delay_on) return SWIM_OK;
-  const uint32_t bcap = e->cfg.delay_capacity ? e->cfg.delay_capacity : 1024;
-  GMsgFull* dq = nullptr;
-  if (!sd.alloc(&dq, (size_t)DQ_BUCKETS * bcap)) return SWIM_ENOMEM;
-  sd.b.dq = dq;
-  sd.b.dq_bcap = bcap;
-  // delayed SYNCs / SYNC_ACKs: a bucket holds a few ticks' worth of SYNCs (N / S per tick, and as
-  // many acks); every message in flight parks its content row (at most 1 GiB of rows)
-  const uint32_t per_tick = (e->n + sd.c.S - 1) / std::max(sd.c.S, 1u);
-  const uint32_t sbcap = 64 + 8 * per_tick;
-  const uint32_t pcap = (uint32_t)std::min<uint64_t>(4ull * sbcap, std::max<uint64_t>(64, (1ull << 28) / e->n));
-  Bufs& b = sd.b;
-  if (!sd.alloc(&b.sdq, (size_t)DQ_BUCKETS * sbcap) || !sd.alloc(&b.sdq_cnt, DQ_BUCKETS) ||
-      !sd.alloc(&b.park, (size_t)pcap * e->n) || !sd.alloc(&b.park_avail, pcap) || !sd.alloc(&b.park_freed, pcap) ||
-      !sd.alloc(&b.park_jobs, pcap) || !sd.alloc(&b.park_ctl, 1))
-    return SWIM_ENOMEM;
-  if (hipMemset(b.sdq_cnt, 0, 4ull * DQ_BUCKETS) != hipSuccess || hipMemset(b.park_ctl, 0, sizeof(SpillCtl)) != hipSuccess)
-    return SWIM_EDEVICE;
-  b.sdq_bcap = sbcap;
-  b.park_cap = pcap;
-  sd.c.delay_on = 1;
+  if (e->n > (1u << 20)) return SWIM_EINVAL;  // (a released GOSSIP_REQ carries its age above bit 20 of `from`)
+  for (Shard& sd : e->sh) {
+    if (sd.c.delay_on) continue;
+    const uint32_t bcap = e->cfg.delay_capacity ? e->cfg.delay_capacity : 1024;
+    GMsgFull* dq = nullptr;
+    if (!sd.alloc(&dq, (size_t)DQ_BUCKETS * bcap)) return SWIM_ENOMEM;
+    sd.b.dq = dq;
+    sd.b.dq_bcap = bcap;
+    // delayed SYNCs / SYNC_ACKs: a bucket holds a few ticks' worth of SYNCs (N / S per tick, and as
+    // many acks); every message in flight parks its content row (at most 1 GiB of rows)
+    const uint32_t per_tick = (e->n + sd.c.S - 1) / std::max(sd.c.S, 1u);
+    const uint32_t sbcap = 64 + 8 * per_tick;
+    const uint32_t pcap = (uint32_t)std::min<uint64_t>(4ull * sbcap, std::max<uint64_t>(64, (1ull << 28) / e->n));
+    Bufs& b = sd.b;
+    if (!sd.alloc(&b.sdq, (size_t)DQ_BUCKETS * sbcap) || !sd.alloc(&b.sdq_cnt, DQ_BUCKETS) ||
+        !sd.alloc(&b.park, (size_t)pcap * e->n) || !sd.alloc(&b.park_avail, pcap) || !sd.alloc(&b.park_freed, pcap) ||
+        !sd.alloc(&b.park_jobs, pcap) || !sd.alloc(&b.park_ctl, 1))
+      return SWIM_ENOMEM;
+    if (hipMemset(b.sdq_cnt, 0, 4ull * DQ_BUCKETS) != hipSuccess || hipMemset(b.park_ctl, 0, sizeof(SpillCtl)) != hipSuccess)
+      return SWIM_EDEVICE;
+    b.sdq_bcap = sbcap;
+    b.park_cap = pcap;
+    sd.c.delay_on = 1;
+  }
   return SWIM_OK;
 }
 

@@ -1036,7 +1036,7 @@ __global__ void __launch_bounds__(256) k_dq_release(KP) {
   const uint32_t lane = threadIdx.x & 63;
   for (uint32_t i0 = blockIdx.x * blockDim.x + (threadIdx.x - lane); i0 < cnt; i0 += gridDim.x * blockDim.x) {
     const uint32_t i = i0 + lane;
-    const bool valid = i < cnt;
+    bool valid = i < cnt;
     GMsgFull msg{};
     uint32_t age = 0;
     if (valid) {
@@ -1051,6 +1051,16 @@ __global__ void __launch_bounds__(256) k_dq_release(KP) {
       }
       age = (uint32_t)T - msg.pseq;  // snd_key orders earlier rounds first
       msg.pseq = rank;
+      if (!owned(c, msg.to)) {
+        // a receiver on another shard: the message joins this tick's exchange (E1), its age in the
+        // top bits of `from` (< 2^20 while delays are on; k_recv_msgs takes it out)
+        GMsgFull fm = msg;
+        fm.from |= min(age, 2047u) << 20;
+        const uint32_t d = owner(c, msg.to);
+        const uint32_t bj = atomicAdd(&b.x->msg[d], 1u);
+        if (bj < b.tx_msg_cap) b.tx_msgs[(size_t)d * b.tx_msg_cap + bj] = fm; else set_err(c, ERR_MSGS);
+        valid = false;
+      }
     }
     deliver_local_msg(c, b, msg, valid, age);  // every lane of the wave takes part
   }
@@ -1135,13 +1145,18 @@ __global__ void k_recv_msgs(KP) {
     uint32_t i = i0 + lane;
     const bool valid = i < total;
     GMsgFull msg{};
+    uint32_t age = 0;
     if (valid) {
       const uint32_t p = peer_of(s_n, i);
       msg = ld_peer(pr->msgs[p] + (size_t)c.rank * b.tx_msg_cap + i);
+      if (c.delay_on) {  // a delayed message released by its sender's shard (k_dq_release)
+        age = msg.from >> 20;
+        msg.from &= 0xfffffu;
+      }
       // kept (flagged) so that each (sender, receiver) pair's pseq stays dense for deliver_big
       if (coll_contains(c, coll_find(c, msg.to, msg.gossiper), msg.seq)) msg.pos_dup |= 0x80000000u;
     }
-    deliver_local_msg(c, b, msg, valid, 0u);
+    deliver_local_msg(c, b, msg, valid, age);
   }
 }
 

@@ -92,11 +92,14 @@ __global__ void __launch_bounds__(256) k_pack_rows(KP, int d2) {
     uint32_t k = row, d = 0;
     while (k >= s_n[d]) { k -= s_n[d]; ++d; }
     SyncReq* q = tx + (size_t)d * b.tx_req_cap + k;
+    const uint32_t fl = q->flags;
     const bool fits = row < b.row_cap;
-    if (ch == 0 && threadIdx.x == 0) q->content = fits ? row : NONE;
-    if (!fits) continue;
+    // a SYNC_ACK k_ack_delay deferred travels later (content NONE: the receiver skips it)
+    if (ch == 0 && threadIdx.x == 0) q->content = fits && !(fl & RQ_DEFER) ? row : NONE;
+    if (!fits || (fl & RQ_DEFER)) continue;
     const uint32_t x0 = ch * PACK_CHUNK, len = min(PACK_CHUNK, n - x0);
-    const uint32_t* src = recs + (size_t)(q->from - lo) * n + x0;
+    // a delayed message's content is its park slot (the row as it was when the message was prepared)
+    const uint32_t* src = ((fl & RQ_PARKED) ? b.park + (size_t)q->snap * n : recs + (size_t)(q->from - lo) * n) + x0;
     uint32_t* dst = out + (size_t)row * n + x0;
     if (n & 3) {  // rows are only 4-B aligned
       for (uint32_t x = threadIdx.x; x < len; x += blockDim.x) dst[x] = src[x];
@@ -124,8 +127,10 @@ __global__ void k_recv_sync(KP, int d2) {
     if (valid) {
       const uint32_t p = peer_of(s_n, k);
       q = ld_peer(b.peers->hdr[d2][p] + (size_t)c.rank * b.tx_req_cap + k);
-      valid = q.content != NONE;  // its row did not fit the sender's tx_rows (ERR_REQS is set there)
+      valid = q.content != NONE;  // its row did not fit the sender's tx_rows (ERR_REQS is set there), or deferred
       q.content = p * b.row_cap + q.content;
+      // a delayed SYNC_ACK's receiver is merged into in this SYNC_ACK sub-phase (see k_sync_delay)
+      if (valid && d2 && (q.flags & RQ_PARKED)) sflag_set(c, b, q.to - c.lo, SF_SENT);
     }
     enqueue_sync(c, b, d2, q, valid);
   }
@@ -200,14 +205,15 @@ __device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SyInb
   SyncReq q = p.items[i];
   q.from = uni(q.from); q.to = uni(q.to); q.content = uni(q.content); q.pad = uni(q.pad);
   const bool remote = q.content != NONE;
-  h.content = remote ? remote_row(c, b, d2, q.content) : rec_row(c, q.from);
+  const bool parked = !remote && (q.flags & RQ_PARKED);  // (uniform: the header is)
+  h.content = remote ? remote_row(c, b, d2, q.content) : parked ? park_row(c, b, q.snap) : rec_row(c, q.from);
   h.rv = rec_row(c, q.to);
-  h.bdc = remote ? nullptr : c.bdiff + (size_t)(q.from - c.lo) * c.blocks;
+  h.bdc = remote || parked ? nullptr : c.bdiff + (size_t)(q.from - c.lo) * c.blocks;
   h.bdv = c.bdiff + (size_t)(q.to - c.lo) * c.blocks;
   h.i = i;
   h.r = q.to;
   h.s = q.from;
-  h.rev = (CLS_REV && !d2 && !remote) ? 1u : 0u;
+  h.rev = (CLS_REV && !d2 && !remote && !parked) ? 1u : 0u;
   h.pad = q.pad;
 }
 
@@ -445,8 +451,8 @@ __device__ inline uint32_t content_at(const Content& k, uint32_t x) {
 }
 // the content of message q (received rows, the sender's slot or its live row)
 __device__ __forceinline__ Content msg_content(const Ctx& c, const Bufs& b, const SyncReq& q, int d2) {
-  if (q.flags & RQ_PARKED) return Content{park_row(c, b, q.snap), nullptr, nullptr, 0};  // delayed
   if (q.content != NONE) return Content{remote_row(c, b, d2, q.content), nullptr, nullptr, 0};
+  if (q.flags & RQ_PARKED) return Content{park_row(c, b, q.snap), nullptr, nullptr, 0};  // delayed, parked here
   const uint32_t i = q.from - c.lo;
   const uint32_t si = (d2 ? b.ack_snap : b.snap_idx)[i];
   if (si >= b.snap_cap) return Content{rec_row(c, q.from), nullptr, nullptr, 0};
@@ -741,9 +747,26 @@ __global__ void __launch_bounds__(256) k_ack_delay(KP) {
   const Bufs b = P->b;
   __shared__ uint32_t s_slot;
   const uint32_t na = min(b.k->ack_total, b.req_cap);
-  for (uint32_t it = blockIdx.x; it < na; it += gridDim.x) {
-    SyncReq a = b.acks[it];
-    if (a.flags & RQ_PARKED) continue;  // an arrival from the delay queue (uniform)
+  // this shard's acks: the local ones (items), then those bound for each other shard (tx_acks)
+  uint32_t nt = na;
+  if (c.world > 1)
+    for (uint32_t d = 0; d < c.world; ++d) nt += d == c.rank ? 0u : min(b.x->ack[d], b.tx_req_cap);
+  for (uint32_t u = blockIdx.x; u < nt; u += gridDim.x) {
+    SyncReq* ap;
+    if (u < na) {
+      ap = b.acks + u;
+    } else {
+      uint32_t k = u - na, d = 0;
+      for (;; ++d) {
+        if (d == c.rank) continue;
+        const uint32_t m = min(b.x->ack[d], b.tx_req_cap);
+        if (k < m) break;
+        k -= m;
+      }
+      ap = b.tx_acks + (size_t)d * b.tx_req_cap + k;
+    }
+    SyncReq a = *ap;
+    if (a.flags & (RQ_PARKED | RQ_DEFER)) continue;  // an arrival from the delay queue (uniform)
     const uint32_t dl = delay_ticks(c, a.from, a.to, a.from, SWIM_STREAM_SYNCACK_DELAY, a.ordinal, 0);
     if (!dl) continue;
     if (threadIdx.x == 0) s_slot = park_alloc(c, b);
@@ -752,10 +775,11 @@ __global__ void __launch_bounds__(256) k_ack_delay(KP) {
     if (slot != NONE) copy_row(rec_row(c, a.from), park_row(c, b, slot), c.n);
     __syncthreads();  // (the row is parked before the message is queued, and s_slot is reused)
     if (threadIdx.x == 0) {
-      b.acks[it].flags = a.flags | RQ_DEFER;
+      ap->flags = a.flags | RQ_DEFER;
       if (slot != NONE) {
         a.slot = 0;
         a.snap = slot;
+        a.content = NONE;
         park_put(c, b, a, dl, true);
       }
     }
@@ -790,8 +814,16 @@ __global__ void __launch_bounds__(256) k_sync_delay(KP) {
       valid = c.up[q.to] != 0;
       // an ack's receiver — and a SYNC's sender, whose ack may come back this tick — is merged into in
       // the SYNC_ACK sub-phase: if it is also read as SYNC_ACK content this tick (it received a SYNC),
-      // it takes a snapshot slot (sflag_set_from)
-      if (valid) sflag_set(c, b, (ack ? q.to : q.from) - c.lo, SF_SENT);
+      // it takes a snapshot slot (sflag_set_from; a receiver on another shard: k_recv_sync)
+      const uint32_t who = ack ? q.to : q.from;
+      if (valid && owned(c, who)) sflag_set(c, b, who - c.lo, SF_SENT);
+      if (valid && !owned(c, q.to)) {  // into this tick's exchange (E2 / E3), content from the slot
+        const uint32_t d = owner(c, q.to);
+        const uint32_t j = atomicAdd(ack ? &b.x->ack[d] : &b.x->req[d], 1u);
+        if (j < b.tx_req_cap) (ack ? b.tx_acks : b.tx_reqs)[(size_t)d * b.tx_req_cap + j] = q;
+        else set_err(c, ERR_REQS);
+        valid = false;
+      }
     }
     enqueue_sync(c, b, 0, q, valid && !ack);
     enqueue_sync(c, b, 1, q, valid && ack);

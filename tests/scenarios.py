@@ -24,7 +24,7 @@ class Scenario:
     seeds: tuple = ()
     ops: list = dataclasses.field(default_factory=list)  # (tick, op, args...) applied before tick+1
     check_every: int = 10
-    shardable: bool = True  # False: uses a single-shard-only feature (message delay)
+    shardable: bool = True  # False: uses a feature sharded engines do not have
 
 
 def apply_op(e: abi.Engine, op, args):
@@ -170,14 +170,14 @@ def catalog() -> list[Scenario]:
         Scenario("gossip_delay_3", 3, 3, 190, seed=17, cfg=dict(ping_interval=3_600_000, sync_interval=3_600_000),
                  ops=[(0, "default_delay", 3000, 0), (0, "default_delay", 3000, 1), (0, "default_delay", 100, 2),
                       (1, "spread", 0, 1), (1, "spread", 0, 2), (1, "spread", 0, 3)],
-                 check_every=20, shardable=False),
+                 check_every=20),
         # the whole stack under delay: a 150 ms mean delay on every message (round trips beyond the
         # 500 ms ping timeout, late direct acks racing the relays, gossips arriving on non-gossip
         # ticks), a slow link, 5 % loss, a kill, a user gossip
         Scenario("delay_fd_gossip_12", 12, 12, 700, seed=18,
                  ops=[(0, "default_delay", 150, abi.ALL_MEMBERS), (0, "loss", 5, abi.ALL_MEMBERS),
                       (0, "link_delay", 2, 5, 2500), (50, "spread", 4, 77), (120, "kill", 9)],
-                 check_every=50, shardable=False),
+                 check_every=50),
         # ClusterTest.testUpdateMetadata (:179-247): members join through seed 0, member 1 updates its
         # metadata twice (updateIncarnation: ALIVE inc+1 gossiped; every viewer fetches -> UPDATED)
         Scenario("update_metadata_12", 12, 2, 300, seed=19, seeds=(0,), cfg=mp_test,
@@ -209,7 +209,7 @@ def catalog() -> list[Scenario]:
                  ops=[(0, "loss", 5, abi.ALL_MEMBERS), (0, "default_delay", 150, abi.ALL_MEMBERS), (30, "kill", 5),
                       (30, "kill", 9), (45, "join_at", 32, 5), (60, "join_at", 33, 9), (200, "kill", 33),
                       (215, "join_at", 34, 9)],
-                 check_every=50, shardable=False),
+                 check_every=50),
         # SYNC / SYNC_ACK and GET_METADATA under delay (NetworkEmulatorTransport :59-75 delays every
         # send and requestResponse): a 120 ms mean on every link, a 600 ms link, 2 % loss; members join
         # through two seeds (initial SYNCs answered late or timed out), a kill, a metadata update (every
@@ -221,7 +221,7 @@ def catalog() -> list[Scenario]:
                       (0, "link_delay", 3, 0, 600), (4, "join", 16), (9, "join", 17), (9, "join", 18),
                       (30, "join", 19), (31, "join", 20), (60, "kill", 7), (80, "update_meta", 2),
                       (150, "join", 21), (150, "join", 22), (151, "join", 23)],
-                 check_every=20, shardable=False),
+                 check_every=20),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),
                  cfg=dict(sync_interval=5000), ops=[(100, "partition", _partition(32, 16)), (1100, "partition", None)],

@@ -121,13 +121,14 @@ def _cases(shard_list=None):
 @pytest.mark.parametrize("sc,shards", _cases([2, 3]))
 def test_gpu_sharded_parity_scenario(glib, olib, sc, shards):
     if not sc.shardable:
-        pytest.skip("message delay is single-shard only")
+        pytest.skip("scenario uses a single-shard-only feature")
     _run_parity(glib, olib, dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": shards}))
 
 
 # the RCCL route of the content rows (k_pull_rows: pulled with system-scope loads into per-shard
 # copies, then classified from there) in the single-GPU rig (SWIM_EXCHANGE_PULL=1)
-PULL_SCENARIOS = ("mp_joins_via_seed", "churn_48", "config3_rates_200", "partition_heal_32", "restart_same_address_40")
+PULL_SCENARIOS = ("mp_joins_via_seed", "churn_48", "config3_rates_200", "partition_heal_32", "restart_same_address_40",
+                  "sync_delay_24")
 
 
 @pytest.mark.parametrize("name,shards", [
@@ -160,7 +161,7 @@ def test_gpu_matches_golden_digest(glib, sc, shards):
     if shards > sc.capacity:
         pytest.skip("more shards than members")
     if shards > 1 and not sc.shardable:
-        pytest.skip("message delay is single-shard only")
+        pytest.skip("scenario uses a single-shard-only feature")
     sc2 = dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": shards})
     e = scenarios.make_engine(glib, sc2)
     scenarios.run(e, sc2)

@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--collectors", action="store_true",
                     help="per period: collector sizes at member sample[1] (gossipers of its live gossips)")
     ap.add_argument("--message-capacity", type=int, default=1 << 28)
+    ap.add_argument("--deliver", action="store_true",
+                    help="per period: sampled k_gossip_deliver profile (ms / launch, messages, not flagged, accepted)")
     args = ap.parse_args()
     import swimgpu
     from swimgpu import abi
@@ -84,6 +86,8 @@ def main():
             if p == heal:
                 ops.append(("partition", None))
             plan.append((p, ops))
+    if args.deliver:
+        e.profile_enable(True)
     t0 = time.time()
     prev = e.stats()
     ev_total = 0
@@ -112,6 +116,14 @@ def main():
                           "removed": int((ev["type"] == abi.EV_REMOVED).sum()) if len(ev) else 0,
                           "max_live_gossips": glen}), flush=True)
         prev = st
+        if args.deliver:
+            d = e.profile_deliver()
+            n_l = max(1, d["launches"])
+            print(json.dumps({"deliver_ms_per_launch": round(d["total_ms"] / n_l, 3), "launches": d["launches"],
+                              "msgs": d["messages"], "fresh": d["alg_bytes"] // 24 - d["messages"],
+                              "accepted": d["records"]}), flush=True)
+            e.profile_enable(False)
+            e.profile_enable(True)
         if args.collectors:
             m = sample[1]
             gs = e.read_gossips(m)
