@@ -1691,6 +1691,33 @@ __device__ inline void sflag_set_from(const Ctx& c, const Bufs& b, uint32_t i, u
     old = prev;
   }
 }
+// sflag_set_from split in two, so that its CAS is in flight together with other atomics: sflag_cas
+// issues one attempt (none when the bits are already set), sflag_done finishes the update — the slot
+// claim on success, the retry loop after a lost race
+struct SfCas {
+  uint32_t old, nw, prev;
+};
+__device__ __forceinline__ SfCas sflag_cas(const Ctx& c, const Bufs& b, uint32_t i, uint32_t bits, uint32_t old) {
+  const uint32_t t3 = (uint32_t)c.T << SF_BITS;
+  const uint32_t base = (old & ~SF_MASK) == t3 ? old : t3;
+  SfCas r{old, base | bits, old};
+  if (r.nw != old) r.prev = atomicCAS(&b.sflag[i], old, r.nw);
+  return r;
+}
+__device__ __forceinline__ void sflag_done(const Ctx& c, const Bufs& b, uint32_t i, uint32_t bits, const SfCas& r) {
+  if (r.nw == r.old) return;
+  if (r.prev != r.old) {
+    sflag_set_from(c, b, i, bits, r.prev);
+    return;
+  }
+  const uint32_t t3 = (uint32_t)c.T << SF_BITS;
+  const uint32_t base = (r.old & ~SF_MASK) == t3 ? r.old : t3;
+  if ((r.nw & (SF_SENT | SF_RECV)) == (SF_SENT | SF_RECV) && (base & (SF_SENT | SF_RECV)) != (SF_SENT | SF_RECV)) {
+    const uint32_t slot = snap_take(c, b, i);
+    b.snap_idx[i] = slot;
+    b.ack_snap[i] = slot;
+  }
+}
 __device__ __forceinline__ void sflag_set(const Ctx& c, const Bufs& b, uint32_t i, uint32_t bits) {
   sflag_set_from(c, b, i, bits, b.sflag[i]);
 }
@@ -1745,16 +1772,21 @@ __device__ inline uint32_t sy_page_wait(const Ctx& c, const Bufs& b, const SyInb
 
 // a delivered SYNC / SYNC_ACK joins its receiver's inbox (the receiver is owned by this shard).
 // The item's classification counters start at zero here, before any classify launch adds to them.
-// (rsf: a guess of the receiver's sflag word, see sflag_set_from)
-__device__ inline void enqueue_sync(const Ctx& c, const Bufs& b, int d2, SyncReq q, bool valid, uint32_t rsf) {
+// (rsf: a guess of the receiver's sflag word, see sflag_set_from; sbits != 0: the sender's SF_* bits
+// of this message, set here from its guessed word sfv, the CAS in flight with the enqueue's atomics)
+__device__ inline void enqueue_sync(const Ctx& c, const Bufs& b, int d2, SyncReq q, bool valid, uint32_t rsf,
+                                    uint32_t sbits = 0, uint32_t sfv = 0) {
   const SyInbox x = sy_inbox(b, d2);
   uint32_t it = NONE, s = 0, pid = NONE, r = 0;
   if (valid) {
     // the item and the inbox slot are taken together (two independent atomics in flight at once); an
     // item beyond the capacity (ERR_REQS) still takes its slot, as NONE, which readers skip
     r = q.to - c.lo;
+    SfCas sc{};
+    if (sbits) sc = sflag_cas(c, b, q.from - c.lo, sbits, sfv);
     it = atomicAdd(x.total, 1u);
     s = atomicAdd(&x.cnt[r], 1u);
+    if (sbits) sflag_done(c, b, q.from - c.lo, sbits, sc);
     if (it >= b.req_cap) {
       set_err(c, ERR_REQS);
       it = NONE;
@@ -1768,9 +1800,11 @@ __device__ inline void enqueue_sync(const Ctx& c, const Bufs& b, int d2, SyncReq
         b.ack_ctot[it] = 0;
       }
     }
-    if (s == 0) {
+    if (s == 0) {  // the receiver list's entry and the receiver's SF_RECV, both atomics in flight together
+      SfCas rc{};
+      if (!d2) rc = sflag_cas(c, b, r, SF_RECV, rsf);
       x.recv[atomicAdd(x.recv_cnt, 1u)] = q.to;
-      if (!d2) sflag_set_from(c, b, r, SF_RECV, rsf);
+      if (!d2) sflag_done(c, b, r, SF_RECV, rc);
     }
     if (s < SY_INLINE) {
       x.inl[(size_t)r * SY_INLINE + s] = it;
@@ -1886,15 +1920,16 @@ __device__ inline unsigned long long sync_collect_fast(const Ctx& c, const Bufs&
   if (!(t == x0 ? inbx : c.default_inbound[t])) return 1;                   // inbound-blocked: dropped
   q.flags |= RQ_DELIVERED;
   const bool local = owned(c, t);
-  sflag_set_from(c, b, i, local ? SF_SENT | SF_SENT_LOCAL : SF_SENT, sfv);
   if (!local) {  // content (this row) travels with the request: k_pack_rows
+    sflag_set_from(c, b, i, SF_SENT, sfv);
     const uint32_t d = owner(c, t);
     const uint32_t k = atomicAdd(&b.x->req[d], 1u);
     if (k >= b.tx_req_cap) { set_err(c, ERR_REQS); return 1; }
     b.tx_reqs[(size_t)d * b.tx_req_cap + k] = q;
     return 1;
   }
-  enqueue_sync(c, b, 0, q, true, t == x0 ? sfx : b.sflag[t - c.lo]);
+  // (the sender's SF_SENT | SF_SENT_LOCAL is set inside, its CAS beside the enqueue's atomics)
+  enqueue_sync(c, b, 0, q, true, t == x0 ? sfx : b.sflag[t - c.lo], SF_SENT | SF_SENT_LOCAL, sfv);
   return 1;
 }
 

@@ -3,7 +3,7 @@
 # twice; one JSON summary line per run -> gpurun_out/variants.log
 set -uo pipefail
 mkdir -p gpurun_out
-for round in 1 2; do
+for round in $(seq 1 ${ROUNDS:-2}); do
   for v in ${VARIANTS:-A B C D E}; do
     SWIMGPU_LIB=exp/lib_$v.so timeout -k 10 120 python3 bench.py --steps ${STEPS:-60} --warmup 5 --no-extras --no-cpu-baseline \
       > gpurun_out/variant_$v.log 2>&1 || { echo "variant $v failed"; tail -5 gpurun_out/variant_$v.log; exit 1; }
