@@ -9,13 +9,18 @@ SURVEY.md §8 on synthetic input (a converged N-member cluster losing one member
 
 With N > 1 (launched by torch.distributed.run, one process per GPU) the SAME N-member cluster is
 row-sharded over the N GPUs (swim_create_shard): each rank owns members [r*N/G, (r+1)*N/G) and the
-cross-shard GOSSIP_REQ / SYNC / SYNC_ACK traffic moves by RCCL send/recv over xGMI inside the
-library.  Total work is fixed, so `scaling` is "strong".  torch.distributed (gloo) only broadcasts
+cross-shard GOSSIP_REQ / SYNC / SYNC_ACK traffic is pulled by device kernels from the producers'
+exchange regions over xGMI (IPC-mapped), one ncclAllToAll of counts per exchange inside the library
+(DESIGN.md §7).  Total work is fixed, so `scaling` is "strong".  torch.distributed only broadcasts
 the RCCL bootstrap id and brackets the timed region with barriers.
 
-Prints ONE JSON line with `value` (whole-job member-periods/s), the `roofline` object of the
-dominant kernel (k_sync_classify, the SYNC record classification; HIP events on the engine's stream) and the
-`cpu_baseline` (the CPU oracle on all of the box's cores and on 1 thread, 10 periods, rank 0 / N=1 only).
+Prints ONE JSON line with `value` (whole-job member-periods/s); `roofline`: the whole step against
+HBM (SURVEY.md §8(d) algorithmic bytes per member-period over the measured period time, traffic from
+the same workload's PMC passes under profiles/); `roofline_merge` (the SYNC merge, k_sync_apply with
+its classification fused), `roofline_fanout` / `roofline_deliver` (k_gossip_emit / k_gossip_deliver
+over a failures-workload storm window, side runs), `ks_mode` and the `cpu_baseline` (the CPU oracle
+on 16 of the box's cores and on 1 thread, rank 0 / N=1 only).  Kernel times are HIP events on the
+engine's own stream.
 """
 import argparse
 import json

@@ -881,6 +881,21 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
       s_mod = 0;
       s_recs = 0;
     }
+    // the words the SYNC sub-phase's ack checks read for the first blockDim messages (up and inbound
+    // filter of the ack's receiver, its sflag word) are loaded now, beside the merges' own loads, and
+    // used after the merges (which change none of them); only without per-link settings / partition
+    bool pre = false;
+    uint8_t pre_up = 0, pre_in = 0;
+    uint32_t pre_sf = 0;
+    int32_t pre_loss = 0;
+    if (!d2 && !c.n_links && !c.partition && threadIdx.x < k && s_it[threadIdx.x] < b.req_cap) {
+      const uint32_t f = x.items[s_it[threadIdx.x]].from;
+      pre = true;
+      pre_loss = c.default_loss[s];
+      pre_up = c.up[f];
+      pre_in = c.default_inbound[f];
+      pre_sf = owned(c, f) ? b.sflag[f - c.lo] : 0u;
+    }
     __syncthreads();
     for (uint32_t q = 0; q < k; ++q) {
       const uint32_t it = s_it[q];
@@ -956,7 +971,11 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
         if (q < k && s_it[q] < b.req_cap) {
           const uint32_t it = s_it[q];
           const SyncReq rq = x.items[it];
-          if (!out_fail(c, s, rq.from, s, SWIM_STREAM_SYNCACK_OUT, q, 0) && in_pass(c, rq.from, s)) {
+          const bool first = pre && q0 == 0;  // (pre_*: this message's words, loaded before the merges)
+          const uint32_t t3 = (uint32_t)c.T << SF_BITS;
+          const bool sf_now = first && (pre_sf & ~SF_MASK) == t3;
+          if (first ? pre_up && !lost_k(c, pre_loss, s, SWIM_STREAM_SYNCACK_OUT, q, 0) && pre_in
+                    : !out_fail(c, s, rq.from, s, SWIM_STREAM_SYNCACK_OUT, q, 0) && in_pass(c, rq.from, s)) {
             a.from = s; a.to = rq.from; a.ordinal = q; a.slot = 0;
             a.flags = RQ_DELIVERED | (rq.flags & RQ_INITIAL) | (tsz << RQ_RECS_SHIFT);
             a.content = NONE; a.snap = NONE;
@@ -968,9 +987,11 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
             // that could change the receiver: its merge is a no-op, so the SYNC_ACK sub-phase's
             // bookkeeping for it (onSyncAck :385-391: the phase's minor / fetch counters restart, an
             // INITIAL ack completes a join step, the counters) is done here and nothing is enqueued
-            if (valid && CLS_REV && !c.delay_on && rq.content == NONE && s_mod == 0 && owned(c, rq.from) &&
-                (ACK_NORECV_EXPERIMENT || !sflag_has(c, b, rq.from - c.lo, SF_RECV)) &&
-                !sflag_has(c, b, rq.from - c.lo, SF_MULTI) &&
+            if (valid && CLS_REV && !c.delay_on && rq.content == NONE && s_mod == 0 &&
+                (first ? owned(c, rq.from) && (ACK_NORECV_EXPERIMENT || !(sf_now && (pre_sf & SF_RECV))) &&
+                             !(sf_now && (pre_sf & SF_MULTI))
+                       : owned(c, rq.from) && (ACK_NORECV_EXPERIMENT || !sflag_has(c, b, rq.from - c.lo, SF_RECV)) &&
+                             !sflag_has(c, b, rq.from - c.lo, SF_MULTI)) &&
                 b.rev_total[it] == 0) {
               MemberDev& mf = mem(c, rq.from);
               mf.ev_minor = 0;
