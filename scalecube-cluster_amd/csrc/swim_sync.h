@@ -572,6 +572,13 @@ __device__ void sync_msg_wg(const Ctx& c, const Bufs& b, uint32_t r, uint32_t it
   __shared__ uint32_t s_pub3, s_rtot;
   const uint32_t n = c.n, chunks = b.chunks, tid = threadIdx.x, s = rq.from;
   const Content kc = msg_content(c, b, rq, 0);
+  const uint32_t* bdv = c.bdiff + (size_t)(r - c.lo) * c.blocks;
+  // the first chunk's witness words of both live rows and the self subjects' ref words, loaded beside
+  // the content's slot lookup (a live word read before the snapshot flag is checked predates every
+  // change of the sender's row; the receiver's row changes only in this workgroup)
+  const uint32_t pc = tid < chunks ? c.bdiff[(size_t)(s - c.lo) * c.blocks + tid] : 0u;
+  const uint32_t pv = tid < chunks ? bdv[tid] : 0u;
+  const uint32_t rfr = c.ref[r], rfs = c.ref[s];
   if (tid == 0) {
     s_pub3 = kc.snap && snap_published(kc) ? 1u : 0u;
     s_rtot = 0;
@@ -580,16 +587,15 @@ __device__ void sync_msg_wg(const Ctx& c, const Bufs& b, uint32_t r, uint32_t it
   __syncthreads();
   bool from_snap = s_pub3 != 0;
   const uint32_t* rv = rec_row(c, r);
-  const uint32_t* bdv = c.bdiff + (size_t)(r - c.lo) * c.blocks;
   const auto leaving = [](uint32_t rf) { return r_in_table(rf) && r_status(rf) == SWIM_LEAVING; };
-  const uint32_t rfr = c.ref[r], rfs = c.ref[s];
   uint2* const rch = b.rev_chunk + (size_t)it * chunks;
   // (1) witness, chunk per thread
   for (int pass = 0; pass < 2; ++pass) {
     const uint32_t* bdc = from_snap ? kc.snap + n : c.bdiff + (size_t)(s - c.lo) * c.blocks;
     for (uint32_t ch = tid; ch < chunks; ch += blockDim.x) {
       const uint32_t base = ch * SYNC_CHUNK;
-      const bool need = (bdc[ch] | bdv[ch]) != 0 || (r - base < (uint32_t)SYNC_CHUNK && leaving(rfr)) ||
+      const uint32_t wc = ch == tid && !from_snap ? pc : bdc[ch], wv = ch == tid ? pv : bdv[ch];
+      const bool need = (wc | wv) != 0 || (r - base < (uint32_t)SYNC_CHUNK && leaving(rfr)) ||
                         (do_rev && s - base < (uint32_t)SYNC_CHUNK && leaving(rfs));
       if (need) atomicOr(&s_need[ch >> 5], 1u << (ch & 31));
       else if (do_rev) rch[ch] = make_uint2(0, 0);
