@@ -1550,6 +1550,14 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect, u
   __shared__ uint32_t s_iP[DLV_BLOCK], s_iS[DLV_BLOCK], s_iR[DLV_BLOCK];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t t32 = (uint32_t)T;
+  // the schedule words of this thread's first member, loaded beside the inbox flag (nothing in the
+  // gossip phase changes them: k_fd set its mflag bits, the SYNC collection below consumes them)
+  const uint32_t i_first = blockIdx.x * DLV_BLOCK + tid;
+  uint32_t sn_first = NONE, fl_first = 0;
+  if (collect && i_first < c.nl) {
+    sn_first = c.sync_next[i_first];
+    fl_first = c.mflag[i_first];
+  }
   const bool any = b.k->msg_total != 0;  // else no receiver has an inbox
   unsigned long long acc = 0, nsync = 0;
   uint32_t nmsg = 0, nfresh = 0;
@@ -1602,7 +1610,8 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect, u
     __syncthreads();
     const uint32_t nv = s_nins;
     for (uint32_t q = 0; q < nv; ++q) apply_ins_batch<DLV_BLOCK, true>(c, s_ins[q], tid, s_iP, s_iS, s_iR);
-    if (collect && i < c.nl && !big) nsync += sync_collect_member(cs, b, c.lo + i);
+    if (collect && i < c.nl && !big)
+      nsync += i == i_first ? sync_collect_pre(cs, b, c.lo + i, sn_first, fl_first) : sync_collect_member(cs, b, c.lo + i);
   }
   wave_stat_add(c, ST_GOSSIP_ACCEPTED, acc);
   wave_stat_add(cs, ST_SYNCS, nsync);
