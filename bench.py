@@ -309,6 +309,34 @@ def cpu_baseline(n, p0, periods):
                       f"0..{p0} untimed): {dtn:.1f} s on {all_cores} threads, {dt1:.1f} s on 1 thread"}
 
 
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without a launcher: start `torch.distributed.run` with N ranks (one
+    process per GPU) as a CHILD process — nothing here has touched the GPU yet — and return its exit
+    code.  Rank 0's JSON line reaches stdout directly (the child inherits it)."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL and the exchange regions)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def load_engine_hook(spec: str):
+    """--engine-factory FILE.py:FN (test hook, CPU only): FN() returns a library exporting swim.h whose
+    engines every rank runs UNSHARDED (the whole cluster on each rank), so the multi-process host
+    path of this script — rank launch, rendezvous, barriers, max-over-ranks timing, the JSON line — is
+    exercised without a GPU (tests/test_bench_launch.py)."""
+    import importlib.util
+    path, fn = spec.rsplit(":", 1)
+    sp = importlib.util.spec_from_file_location("bench_engine_hook", path)
+    mod = importlib.util.module_from_spec(sp)
+    sp.loader.exec_module(mod)
+    return getattr(mod, fn)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -329,23 +357,30 @@ def main():
     ap.add_argument("--loss", type=int, default=None, help="churn workload: uniform outbound loss %% (default 5)")
     ap.add_argument("--local-shards", type=int, default=1,
                     help="single-process sharded test rig (cfg.local_shards); measurement of the exchange only")
+    ap.add_argument("--engine-factory", default=None, help=argparse.SUPPRESS)  # test hook, see load_engine_hook
     args = ap.parse_args()
     global WORKLOAD
     WORKLOAD = args.workload
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but this launch has WORLD_SIZE={world}")
+    hook = load_engine_hook(args.engine_factory) if args.engine_factory else None
 
     import torch
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
-    torch.cuda.set_device(local_rank)
+    if hook is None:
+        torch.cuda.set_device(local_rank)
 
     import swimgpu
     from swimgpu import abi
-    lib = swimgpu.load_library()
+    lib = hook() if hook else swimgpu.load_library()
     n = args.members or DEFAULT_MEMBERS[args.workload]
     sch = Schedule(args.workload, n, args.warmup + args.steps, args.churn, args.loss)
     sch.progress = args.progress
@@ -358,22 +393,32 @@ def main():
     se = None
     if world > 1:
         from swimgpu.dist import ShardedEngine
-        se = ShardedEngine(lib, cfg, sch.capacity, n, 1)
+        factory = (lambda: abi.Engine(lib, cfg, sch.capacity, n, 1)) if hook else None
+        se = ShardedEngine(lib, cfg, sch.capacity, n, 1, engine_factory=factory)
         e = se.engine
     else:
         e = abi.Engine(lib, cfg, sch.capacity, n, 1)
+    shard = e.shard_info()
+    if hook is None and shard["world"] != world:
+        raise SystemExit(f"bench.py: {world} ranks but the engine has {shard['world']} shards")
     sch.setup(e)
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        if hook is None:
+            torch.cuda.synchronize()
+
+    def all_stats():
+        return se.stats() if se is not None else e.stats()
 
     try:
         sch.run(e, 0, args.warmup)
         e.drain_events()
         barrier()
         e.profile_enable(True)
+        st0 = all_stats()  # the timed window's counters are deltas from here (warmup excluded)
+        barrier()
         t0 = time.perf_counter()
         sch.run(e, args.warmup, args.warmup + args.steps)
         barrier()
@@ -381,12 +426,12 @@ def main():
     except abi.SwimError as ex:
         raise SystemExit(f"{ex}; engine error bits {e.stats()['capacity_errors']:#x}")
     prof, fprof, dprof = e.profile_merge(), e.profile_fanout(), e.profile_deliver()
-    stats = e.stats()
+    st1 = all_stats()
+    stats = {k: (st1[k] - st0[k] if k != "capacity_errors" else st1[k]) for k in st1}
     tpp = e.now()[2]
     e.drain_events()
     if se is not None:
         dt = se.max_time(dt)
-        stats = se.stats()
 
         def reduce(p):
             st = torch.tensor([float(p["alg_bytes"]), p["total_ms"], float(p["launches"])], dtype=torch.float64)
@@ -408,6 +453,8 @@ def main():
         "value": value,
         "unit": "member-periods/s",
         "n_gpus": world,
+        "ranks": {"processes": world, "rccl_shards": shard["world"] if hook is None else None,
+                  "launch": "torch.distributed.run, one process per GPU" if world > 1 else "single process"},
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
@@ -447,7 +494,7 @@ def main():
         same = args.workload == "failures" and args.warmup == KILL_FIRST + KILL_EVERY and args.steps == 6 and n == 65536
         line["roofline_fanout"] = fanout_roofline(fprof, f"the timed window ({args.workload})", same)
         line["roofline_deliver"] = deliver_roofline(dprof, f"the timed window ({args.workload})", same)
-    if world == 1 and args.workload == "quiet" and not args.no_extras and args.local_shards == 1:
+    if world == 1 and args.workload == "quiet" and not args.no_extras and args.local_shards == 1 and hook is None:
         e.close()
         # the quiet headline sends no gossip: the fanout kernel is measured on the failures workload
         # over a window that starts with its second kill (period 30: FD detection, the SUSPECT storm
@@ -467,7 +514,9 @@ def main():
                            "ms_per_step": k_dt / args.ks_steps * 1e3, "steps": args.ks_steps,
                            "config": "same workload, timer_stagger=1, tick_ms=10 (100 ticks per period)",
                            "ks": "tests/test_ks_des.py::test_ks_gpu_vs_des (N=64 and 1,024, 200 seeds, p >= 0.01)"}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if hook is not None:
+        line["engine"] = f"TEST HOOK {args.engine_factory}: not a measurement"
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and hook is None:
         e.close()
         # churn: the oracle needs minutes per period once the storm builds, so the sample is the
         # first timed period only

@@ -13,7 +13,9 @@ import static io.scalecube.cluster.sim.SwimNative.call;
  * per-link override this member holds ({@code outboundSettings.clear()} / {@code inboundSettings.clear()}).
  * The engine keeps per-link overrides itself; the cluster remembers which links this member set so
  * that a clear can remove them (swimgpu/cluster.py NetworkEmulator issues the same call sequence,
- * tests/test_java_shim.py checks that method by method).
+ * tests/test_java_shim.py checks that method by method).  A setting the engine refuses changes nothing:
+ * the loss percentage is range-checked before any call and the delay (which the engine may refuse:
+ * a mean above its tick cap) is set first, so a refusal leaves loss and delay as they were.
  */
 public final class SimNetworkEmulator {
   private final SimulatedCluster cluster;
@@ -27,17 +29,19 @@ public final class SimNetworkEmulator {
   /** outboundSettings(destination, lossPercent, meanDelay) (:70-74). */
   public void outboundSettings(int destination, int lossPercent, int meanDelay) {
     cluster.run(() -> {
+      cluster.checkLossPercent(lossPercent);
+      call(SwimNative.SET_LINK_DELAY, "swim_set_link_delay", cluster.engine(), member, destination, meanDelay);
       cluster.noteOutLink(member, destination);
       call(SwimNative.SET_LINK_LOSS, "swim_set_link_loss", cluster.engine(), member, destination, lossPercent);
-      call(SwimNative.SET_LINK_DELAY, "swim_set_link_delay", cluster.engine(), member, destination, meanDelay);
     });
   }
 
   /** setDefaultOutboundSettings(lossPercent, meanDelay) (:82-85). */
   public void setDefaultOutboundSettings(int lossPercent, int meanDelay) {
     cluster.run(() -> {
-      call(SwimNative.SET_DEFAULT_LOSS, "swim_set_default_loss", cluster.engine(), member, lossPercent);
+      cluster.checkLossPercent(lossPercent);
       call(SwimNative.SET_DEFAULT_DELAY, "swim_set_default_delay", cluster.engine(), member, meanDelay);
+      call(SwimNative.SET_DEFAULT_LOSS, "swim_set_default_loss", cluster.engine(), member, lossPercent);
     });
   }
 

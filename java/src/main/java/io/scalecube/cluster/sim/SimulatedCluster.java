@@ -289,6 +289,13 @@ public final class SimulatedCluster implements AutoCloseable {
   // ------------------------------------------------------------------ plumbing
   MemorySegment engine() { return engine; }
 
+  /** OutboundSettings' loss is a percentage (NetworkEmulator.java:349-352); checked before any engine call */
+  void checkLossPercent(int lossPercent) {
+    if (lossPercent < 0 || lossPercent > 100) {
+      throw new IllegalArgumentException("lossPercent must be within 0..100: " + lossPercent);
+    }
+  }
+
   void noteOutLink(int member, int destination) {
     outLinks.computeIfAbsent(member, k -> new TreeSet<>()).add(destination);
   }

@@ -363,6 +363,11 @@ struct swim_engine {
     const uint64_t u53 = ((uint64_t)(o[0] >> 11) << 32) | o[1];
     return swim_delay_ticks(delay_tab.at(mean).data(), u53);
   }
+  // a mean the engine refuses changes nothing (swim_delay_mean_ok; at most 4,096 distinct means, the
+  // GPU engine's delay-table limit)
+  bool delay_mean_acceptable(int32_t mean) const {
+    return swim_delay_mean_ok(mean, tick_ms) && (delay_tab.count(mean) || delay_tab.size() < 4096);
+  }
   void ensure_delay_tab(int32_t mean) {
     if (mean <= 0 || delay_tab.count(mean)) return;
     std::vector<uint64_t> th(SWIM_DELAY_TICKS_MAX);
@@ -1572,7 +1577,7 @@ int32_t swim_update_metadata(swim_engine* e, uint32_t v) {
 int32_t swim_set_default_delay(swim_engine* e, uint32_t mm, int32_t mean_ms) {
   if (!e || mean_ms < 0) return SWIM_EINVAL;
   if (mm != 0xffffffffu && mm >= e->n) return SWIM_EINVAL;
-  if (mean_ms > 0 && !swim_delay_mean_ok(mean_ms, e->tick_ms)) return SWIM_EINVAL;  // swim_delay.h cap
+  if (mean_ms > 0 && !e->delay_mean_acceptable(mean_ms)) return SWIM_EINVAL;  // swim_delay.h cap, 4,096 tables
   e->ensure_delay_tab(mean_ms);
   if (mm == 0xffffffffu) std::fill(e->default_delay.begin(), e->default_delay.end(), mean_ms);
   else e->default_delay[mm] = mean_ms;
@@ -1584,7 +1589,7 @@ int32_t swim_set_link_delay(swim_engine* e, uint32_t src, uint32_t dst, int32_t 
   if (mean_ms < 0) {
     e->link_delay.erase({src, dst});
   } else {
-    if (mean_ms > 0 && !swim_delay_mean_ok(mean_ms, e->tick_ms)) return SWIM_EINVAL;  // swim_delay.h cap
+    if (mean_ms > 0 && !e->delay_mean_acceptable(mean_ms)) return SWIM_EINVAL;  // swim_delay.h cap, 4,096 tables
     e->ensure_delay_tab(mean_ms);
     e->link_delay[{src, dst}] = mean_ms;
   }

@@ -835,6 +835,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(c.coll, 0, sizeof(CollEnt) * (size_t)nl * c.hcap, s);
   hipMemsetAsync(c.spill_ctl, 0, sizeof(SpillCtl) * NTIER, s);
   hipMemsetAsync(c.seg_flag, 0, 4 * (size_t)nl, s);
+  hipMemsetAsync(c.wheel, 0xff, sizeof(uint64_t) * ((size_t)c.wheel_pages << c.wheel_pshift), s);  // WHEEL_EMPTY
   hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1) * c.wheel_nq, s);
   hipMemsetAsync(c.wheel_pt, 0xff, sizeof(uint32_t) * (c.wheel_mask + 1) * c.wheel_nq * c.wheel_ptmax, s);
   hipMemsetAsync(c.wheel_ctl, 0, sizeof(SpillCtl), s);
@@ -1335,10 +1336,18 @@ int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t p
 // stream drained), and only the new table is written.  A mean above SWIM_DELAY_MEAN_MAX_TICKS ticks
 // is refused: beyond it the SWIM_DELAY_TICKS_MAX cap would truncate draws with non-negligible
 // probability (swim_delay_mean_ok, shared with the oracle).
+// whether delay_table would accept mean_ms: checked before any state changes (a refused mean must
+// leave the engine exactly as it was, as the oracle's setter does)
+static bool delay_mean_acceptable(const swim_engine* e, int32_t mean_ms) {
+  if (!swim_delay_mean_ok(mean_ms, e->tick_ms)) return false;
+  for (int32_t m : e->delay_means)
+    if (m == mean_ms) return true;
+  return e->delay_means.size() < 4096;
+}
 static int32_t delay_table(swim_engine* e, int32_t mean_ms, int32_t* idx) {
   for (size_t i = 0; i < e->delay_means.size(); ++i)
     if (e->delay_means[i] == mean_ms) { *idx = (int32_t)i; return SWIM_OK; }
-  if (e->delay_means.size() >= 4096 || !swim_delay_mean_ok(mean_ms, e->tick_ms)) return SWIM_EINVAL;
+  if (!delay_mean_acceptable(e, mean_ms)) return SWIM_EINVAL;
   std::vector<uint64_t> th(SWIM_DELAY_TICKS_MAX);
   swim_delay_thresholds(mean_ms, e->tick_ms, th.data());
   const size_t nt = e->delay_means.size() + 1;
@@ -1389,6 +1398,7 @@ int32_t swim_set_default_delay(swim_engine* e, uint32_t m, int32_t mean_ms) {
   if (!e || mean_ms < 0 || (m != 0xffffffffu && m >= e->n)) return SWIM_EINVAL;
   int32_t idx = -1;
   if (mean_ms > 0) {
+    if (!delay_mean_acceptable(e, mean_ms)) return SWIM_EINVAL;
     if (int32_t rc = enable_delay(e)) return rc;
     if (int32_t rc = delay_table(e, mean_ms, &idx)) return rc;
   }
@@ -1406,6 +1416,7 @@ int32_t swim_set_link_delay(swim_engine* e, uint32_t src, uint32_t dst, int32_t 
   if (!e || src >= e->n || dst >= e->n) return SWIM_EINVAL;
   int32_t idx = mean_ms < 0 ? -1 : -2;
   if (mean_ms > 0) {
+    if (!delay_mean_acceptable(e, mean_ms)) return SWIM_EINVAL;
     if (int32_t rc = enable_delay(e)) return rc;
     if (int32_t rc = delay_table(e, mean_ms, &idx)) return rc;
   }

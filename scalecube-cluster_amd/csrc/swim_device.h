@@ -912,6 +912,7 @@ __device__ inline void spread_user(const Ctx& c, uint32_t v, uint32_t payload) {
 
 // ------------------------------------------------------------------------------- timers
 constexpr uint32_t WHEEL_FAILED = 0xfffffffeu;  // the page pool ran dry: releases the page's waiters
+constexpr uint64_t WHEEL_EMPTY = ~0ull;  // an unwritten or consumed wheel slot (the pool starts all-empty)
 __device__ __forceinline__ uint32_t b_of_deadline(const Ctx& c, uint64_t deadline) {
   return (uint32_t)(deadline & c.wheel_mask);
 }

@@ -319,9 +319,11 @@ __device__ inline void timers_block(const Ctx& c, uint64_t T) {
   for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
     const uint32_t pid = pt[i >> c.wheel_pshift];
     if (pid >= c.wheel_pages) continue;  // never allocated (ERR_WHEEL is set)
-    uint64_t e = c.wheel[((size_t)pid << c.wheel_pshift) + (i & pmask)];
-    uint32_t v = (uint32_t)(e >> 32), s = (uint32_t)e;
-    if (!c.up[v]) continue;
+    uint64_t* slot = c.wheel + ((size_t)pid << c.wheel_pshift) + (i & pmask);
+    const uint64_t e = *slot;
+    *slot = WHEEL_EMPTY;  // consumed: a recycled page holds no stale entry (schedule_timer may give up on a slot)
+    const uint32_t v = (uint32_t)(e >> 32), s = (uint32_t)e;
+    if (v - c.lo >= c.nl || !c.up[v]) continue;  // (WHEEL_EMPTY: a slot whose writer gave up, ERR_WHEEL)
     uint32_t* ap = aux_row(c, v) + s;
     uint32_t old = *ap;
     bool claimed = false;
@@ -660,7 +662,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     }
     s_t[49] = alias;
   }
-  __syncwarp();
+  wave_order();
   const uint32_t nt = s_t[0];
   // what depends on the target only, once per round instead of once per (target, gossip): whether
   // it is up and its inbound filter passes v (s_t[50 + j]), v's outbound loss towards it
@@ -888,7 +890,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       }
     }
   }
-  __syncwarp();
+  wave_order();
   return nmsg;
 }
 
@@ -1843,6 +1845,11 @@ __device__ inline uint32_t park_alloc(const Ctx& c, const Bufs& b) {
   set_err(c, ERR_SDELAY);
   return NONE;
 }
+// a park slot whose message could not be queued goes back to the pool (reusable from the next tick)
+__device__ inline void park_release(const Bufs& b, uint32_t slot) {
+  const uint32_t j = atomicAdd(&b.park_ctl->freed, 1u);
+  if (j < b.park_cap) b.park_freed[j] = slot;
+}
 // message q (its content already in park slot q.snap) arrives `k` ticks from now
 __device__ inline void park_put(const Ctx& c, const Bufs& b, SyncReq q, uint32_t k, bool ack) {
   q.flags |= RQ_PARKED | (ack ? RQ_ACK : 0u);
@@ -1850,7 +1857,7 @@ __device__ inline void park_put(const Ctx& c, const Bufs& b, SyncReq q, uint32_t
   q.content = NONE;
   const uint32_t bk = (uint32_t)(c.T + k) & DQ_MASK;
   const uint32_t i = atomicAdd(&b.sdq_cnt[bk], 1u);
-  if (i >= b.sdq_bcap) { set_err(c, ERR_SDELAY); return; }
+  if (i >= b.sdq_bcap) { set_err(c, ERR_SDELAY); park_release(b, q.snap); return; }
   b.sdq[(size_t)bk * b.sdq_bcap + i] = q;
 }
 // a delayed SYNC: its content (the sender's row now, before any merge of this tick) is copied by
@@ -1859,7 +1866,7 @@ __device__ inline void park_request(const Ctx& c, const Bufs& b, SyncReq q, uint
   const uint32_t slot = park_alloc(c, b);
   if (slot == NONE) return;
   const uint32_t j = atomicAdd(&b.k->park_jobs, 1u);
-  if (j >= b.park_cap) { set_err(c, ERR_SDELAY); return; }
+  if (j >= b.park_cap) { set_err(c, ERR_SDELAY); park_release(b, slot); return; }
   b.park_jobs[j] = make_uint2(slot, q.from);
   q.snap = slot;
   park_put(c, b, q, k, false);

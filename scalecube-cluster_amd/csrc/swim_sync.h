@@ -25,19 +25,14 @@
 #ifndef CLS_MINWAVES
 #define CLS_MINWAVES 4  // waves per SIMD the classify kernels are register-limited to
 #endif
-#ifndef ACK_NORECV_EXPERIMENT
-#define ACK_NORECV_EXPERIMENT 0  // timing experiment only (NOT exact): lone-ack shortcut ignores SF_RECV
-#endif
-#ifndef CLS_SKIPZERO
-#define CLS_SKIPZERO 0  // timing experiment only: skip the stores of empty chunk results (NOT exact)
-#endif
 #ifndef CLS_REV
 #define CLS_REV 1       // SYNC classify also classifies the reverse (SYNC_ACK) direction
 #endif
 #ifndef CLS_WITNESS
-#define CLS_WITNESS 1   // 1: units the block witness proves identical are skipped (0: stream all;
-                        // 2, 3: timing experiments only, NOT exact)
+#define CLS_WITNESS 1   // 1: units the block witness proves identical are skipped (0: stream all)
 #endif
+static_assert(CLS_WITNESS == 0 || CLS_WITNESS == 1, "CLS_WITNESS is an exact 0 / 1 switch");
+static_assert(CLS_REV == 0 || CLS_REV == 1, "CLS_REV is an exact 0 / 1 switch");
 constexpr int SYNC_CHUNK = 1024;                 // subjects per classify unit (one wave)
 constexpr int CLS_BLOCK = 256;
 constexpr int CLS_LOADS = SYNC_CHUNK / 256;      // 16-B record loads per lane per row
@@ -340,9 +335,8 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
       // an identical record on a viewer's own subject is complex when it is LEAVING (sync_complex)
       const auto leaving = [](uint32_t rf) { return r_in_table(rf) && r_status(rf) == SWIM_LEAVING; };
       if (CLS_WITNESS && d1 == NONE && local) {
-        if (CLS_WITNESS == 3) dc = dv = 0;
         if ((uni(dc) | uni(dv)) == 0 && !(r_here && leaving(uni(rfr))) && !(s_here && leaving(uni(rfs)))) {
-          if (lane == 0 && CLS_WITNESS != 2) {
+          if (lane == 0) {
             ichunk[(size_t)hc.i * chunks + ch] = make_uint2(0, 0);
             if (hc.rev) b.rev_chunk[(size_t)hc.i * chunks + ch] = make_uint2(0, 0);
           }
@@ -389,14 +383,14 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
         }
       }
       const uint2 res = cls_compact(c, b, flags, base, lane);
-      if (lane == 0 && (!CLS_SKIPZERO || res.y)) {
+      if (lane == 0) {
         ichunk[(size_t)hc.i * chunks + ch] = res;
         if (res.y) atomicAdd(&itot[hc.i], res.y);
       }
       cplx += res.y;
       if (hc.rev) {
         const uint2 rres = cls_compact(c, b, rflags, base, lane);
-        if (lane == 0 && (!CLS_SKIPZERO || rres.y)) {
+        if (lane == 0) {
           b.rev_chunk[(size_t)hc.i * chunks + ch] = rres;
           if (rres.y) atomicAdd(&b.rev_total[hc.i], rres.y);
         }
@@ -816,7 +810,7 @@ __global__ void __launch_bounds__(256) k_sync_delay(KP) {
     if (valid) {
       q = dq[i];
       ack = (q.flags & RQ_ACK) != 0;
-      b.park_freed[atomicAdd(&b.park_ctl->freed, 1u)] = q.snap;
+      park_release(b, q.snap);
       valid = c.up[q.to] != 0;
       // an ack's receiver — and a SYNC's sender, whose ack may come back this tick — is merged into in
       // the SYNC_ACK sub-phase: if it is also read as SYNC_ACK content this tick (it received a SYNC),
@@ -994,9 +988,9 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
             // bookkeeping for it (onSyncAck :385-391: the phase's minor / fetch counters restart, an
             // INITIAL ack completes a join step, the counters) is done here and nothing is enqueued
             if (valid && CLS_REV && !c.delay_on && rq.content == NONE && s_mod == 0 &&
-                (first ? owned(c, rq.from) && (ACK_NORECV_EXPERIMENT || !(sf_now && (pre_sf & SF_RECV))) &&
+                (first ? owned(c, rq.from) && !(sf_now && (pre_sf & SF_RECV)) &&
                              !(sf_now && (pre_sf & SF_MULTI))
-                       : owned(c, rq.from) && (ACK_NORECV_EXPERIMENT || !sflag_has(c, b, rq.from - c.lo, SF_RECV)) &&
+                       : owned(c, rq.from) && !sflag_has(c, b, rq.from - c.lo, SF_RECV) &&
                              !sflag_has(c, b, rq.from - c.lo, SF_MULTI)) &&
                 b.rev_total[it] == 0) {
               MemberDev& mf = mem(c, rq.from);

@@ -382,6 +382,12 @@ class GossipProtocolView:
         return out
 
 
+def _check_loss_percent(loss_percent: int) -> None:
+    """OutboundSettings' loss is a percentage (NetworkEmulator.java:349-352)."""
+    if not 0 <= int(loss_percent) <= 100:
+        raise ValueError(f"loss_percent must be within 0..100: {loss_percent}")
+
+
 class NetworkEmulator:
     """NetworkEmulator of one member (NetworkEmulator.java): outbound loss and mean delay per
     destination or by default, inbound pass/block per source or by default.  Delays are quantised to
@@ -390,14 +396,18 @@ class NetworkEmulator:
     def __init__(self, cluster: "SimulatedCluster", m: int):
         self._c, self._m = cluster, m
 
+    # a refused setting changes nothing: the loss is range-checked first and the delay (which the
+    # engine refuses above its tick cap) is set before the loss
     def outbound_settings(self, destination: int, loss_percent: int, mean_delay: int = 0):  # :69-73
+        _check_loss_percent(loss_percent)
+        self._c.engine.set_link_delay(self._m, destination, mean_delay)
         self._c._note_link(self._m, destination)
         self._c.engine.set_link_loss(self._m, destination, loss_percent)
-        self._c.engine.set_link_delay(self._m, destination, mean_delay)
 
     def set_default_outbound_settings(self, loss_percent: int, mean_delay: int = 0):  # :80-83
-        self._c.engine.set_default_loss(loss_percent, self._m)
+        _check_loss_percent(loss_percent)
         self._c.engine.set_default_delay(mean_delay, self._m)
+        self._c.engine.set_default_loss(loss_percent, self._m)
 
     def block_all_outbound(self):  # :86-90
         for d in self._c._links_from(self._m):

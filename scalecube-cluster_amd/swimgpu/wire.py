@@ -137,13 +137,16 @@ class SyncData:
 class Message:
     headers: tuple  # ((name, value), ...) in insertion order; serialised in HashMap order
     data: Any = None
+    # the header map's construction: None = Message.Builder's `new HashMap<>()`; n = readExternal's
+    # `new HashMap<>(n)` (a message a JVM deserialised and re-sends, e.g. a relayed gossip)
+    map_capacity: Any = field(default=None, compare=False)
     JAVA = "io.scalecube.cluster.transport.api.Message"
 
     def header(self, name):
         return dict(self.headers).get(name)
 
     def write_external(self, out):  # Message.java:206-215
-        hs = java_hashmap_order(self.headers)
+        hs = java_hashmap_order(self.headers, self.map_capacity)
         out.write_int(len(hs))
         for k, v in hs:
             out.write_utf(k)
@@ -153,10 +156,11 @@ class Message:
     @classmethod
     def read_external(cls, inp):  # Message.java:218-230
         hs = []
-        for _ in range(inp.read_int()):
+        n = inp.read_int()
+        for _ in range(n):
             k, v = inp.read_utf(), inp.read_utf()
             hs.append((k, None if v == "null" else v))
-        return cls(tuple(hs), inp.read_object())
+        return cls(tuple(hs), inp.read_object(), n)
 
 
 @dataclass(frozen=True)
@@ -259,18 +263,29 @@ def java_string_hash(s: str) -> int:
     return h - (1 << 32) if h & 0x80000000 else h
 
 
-def java_hashmap_order(items) -> list:
-    """Iteration order of a java.util.HashMap filled by put() in the given order (default capacity
-    16, doubled past 0.75 load; a resize keeps the relative order inside each bucket): by bucket
-    index (h ^ h >>> 16) & (capacity - 1), then insertion order.  Re-putting a key keeps its place."""
+def java_hashmap_order(items, initial_capacity=None) -> list:
+    """Iteration order of a java.util.HashMap filled by put() in the given order: by bucket index
+    (h ^ h >>> 16) & (capacity - 1), then insertion order (a resize keeps the relative order inside
+    each bucket).  Re-putting a key keeps its place.  `initial_capacity` None: `new HashMap<>()`
+    (Message.Builder, Message.java:234: a 16-bucket table at the first put); n: `new HashMap<>(n)`
+    (Message.readExternal, :221: tableSizeFor(n) buckets).  The table doubles when the size passes
+    0.75 of the capacity (HashMap.putVal / resize)."""
     seen, order = {}, []
     for k, v in items:
         if k not in seen:
             order.append(k)
         seen[k] = v
-    cap = 16
-    while len(order) > cap * 3 // 4:
-        cap *= 2
+    if initial_capacity is None:
+        cap = 16
+    else:
+        cap = 1
+        while cap < initial_capacity:  # tableSizeFor
+            cap *= 2
+    thr = int(cap * 0.75)
+    for size in range(1, len(order) + 1):
+        if size > thr:
+            cap *= 2
+            thr = int(cap * 0.75)
 
     def bucket(k):
         h = java_string_hash(k) & 0xFFFFFFFF

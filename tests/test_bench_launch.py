@@ -1,0 +1,41 @@
+"""bench.py's launch contract on CPU: `python bench.py --gpus 2` (no WORLD_SIZE) starts
+torch.distributed.run with 2 ranks as a child process and relays rank 0's JSON line; every rank
+checks that the launch's WORLD_SIZE equals --gpus.  The engines come from the --engine-factory test
+hook (the CPU oracle, tests/bench_hooks.py), so the ranks rendezvous over gloo on 127.0.0.1 and time
+the same schedule without a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, env_extra=None, timeout=300):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], cwd=REPO, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+HOOK = ["--engine-factory", os.path.join(REPO, "tests", "bench_hooks.py") + ":oracle_lib", "--members", "64",
+        "--steps", "3", "--warmup", "2", "--no-cpu-baseline"]
+
+
+def test_gpus_2_spawns_two_ranks():
+    p = _bench("--gpus", "2", *HOOK)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["ranks"]["processes"] == 2
+    assert line["steps"] == 3 and line["warmup"] == 2 and line["value"] > 0
+    assert "TEST HOOK" in line["engine"]
+    # counters are the timed window's deltas: every member pings once per period (x 2 ranks, each
+    # running the whole cluster through the hook)
+    assert line["stats"]["pings"] == 2 * 64 * 3
+
+
+def test_world_size_must_match_gpus():
+    p = _bench("--gpus", "2", *HOOK, env_extra={"WORLD_SIZE": "1"})
+    assert p.returncode != 0 and "WORLD_SIZE=1" in (p.stderr + p.stdout)

@@ -95,3 +95,27 @@ def test_metadata_fetch_fails_past_timeout(lib):
     s, f = slow.stats(), fast.stats()
     assert f["fetches"] > 0 and f["fetch_ok"] == f["fetches"]
     assert s["fetches"] > 0 and s["fetch_ok"] < 0.3 * s["fetches"]
+
+
+def test_refused_delay_mean_changes_nothing(lib):
+    """A mean above the engine's tick cap (SWIM_DELAY_MEAN_MAX_TICKS ticks, swim_delay.h) is refused
+    with SWIM_EINVAL and leaves the engine exactly as it was: no delay machinery switched on, so a
+    joiner's start0 Flux still decides at its start tick (MembershipProtocolImpl.java:268-289) and the
+    run equals one where the call was never made."""
+    def run(refuse):
+        e = engine(lib, 3, 2, seed=5)
+        e.set_seeds([0, 1])
+        if refuse:
+            for call in (lambda: e.set_default_delay(10 ** 6, 0), lambda: e.set_default_delay(10 ** 6),
+                         lambda: e.set_link_delay(0, 1, 10 ** 6)):
+                with pytest.raises(abi.SwimError) as ex:
+                    call()
+                assert ex.value.code == abi.SWIM_EINVAL
+        e.join(2)
+        e.step_ticks(40)
+        return e, [e.read_member(m) for m in range(3)], e.stats(), e.drain_events()
+    a, ma, sa, ea = run(False)
+    b, mb, sb, eb = run(True)
+    assert mb[2]["sync_on"] == 1 and mb[2]["sync_start"] == 1
+    assert ma == mb and sa == sb
+    assert ea.tobytes() == eb.tobytes()

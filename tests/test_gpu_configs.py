@@ -269,7 +269,6 @@ def _partition_run(e, n, hold, log, stop_on_capacity=False):
     return np.concatenate(keys), None, 0
 
 
-@pytest.mark.slow
 def test_config5_partition_8192_removes_other_side(glib):
     """BASELINE config 5's partition phase at N = 8,192 on one MI355X (the largest power of two whose
     partition-phase gossip state fits one GPU, see the N = 16,384 test): seeds {0, N/2}, a 2-way
@@ -326,6 +325,10 @@ def test_config5_partition_16384_storm_is_sync_regossip(glib):
         assert sync >= 0.9 * total, (sync, total)
         if stopped is not None:
             assert bits & 0x1, f"stopped by {bits:#x}, not by the gossip slab"
+            # the storm property holds, but BASELINE config 5 at this size is NOT met on one GPU: the
+            # run cannot complete, so it is reported as an expected failure, never as a pass
+            pytest.xfail(f"config 5 at N={n} does not fit one MI355X: the gossip slab overflowed in period "
+                         f"{stopped} (SYNC-originated share {sync / max(1, total):.3f})")
         else:
             side = (np.arange(n) >= n // 2).astype(np.int64)
             assert len(np.unique(keys)) == len(keys) == n * (n // 2)
@@ -334,7 +337,6 @@ def test_config5_partition_16384_storm_is_sync_regossip(glib):
         e.close()
 
 
-@pytest.mark.slow
 def test_config5_heal_4096_reconverges_and_sync_originates_the_storm(glib):
     """Config 5's heal at N = 4,096 (twice the round-2 size): partition from period 2, held past the
     suspicion timeout (each side REMOVEs the other), healed through seeds {0, N/2}.  Every viewer

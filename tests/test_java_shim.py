@@ -149,6 +149,10 @@ class _JavaCluster:
     def __init__(self):
         self.out, self.inn = {}, {}
 
+    def checkLossPercent(self, pct):
+        if not 0 <= pct <= 100:
+            raise ValueError(pct)
+
     def noteOutLink(self, m, d):
         self.out.setdefault(m, set()).add(d)
 

@@ -136,3 +136,32 @@ def test_sync_message_from_engine_view():
         assert r.status == (int(row[s]) >> 32) & 3 and r.incarnation == int(row[s]) & 0xFFFFFFFF
         assert r.member.address == f"localhost:{4800 + s}"
     assert back.header("q") == wire.SYNC and back.header("cid") == "c1"
+
+
+def test_relayed_message_keeps_the_deserialised_map_capacity():
+    """Message.readExternal builds `new HashMap<>(headersSize)` (Message.java:218-230), so a message a
+    JVM deserialised and sends on (GossipProtocolImpl re-sends the Gossip objects it received) iterates
+    its headers in buckets of tableSizeFor(n) plus resizes, not in the Builder's 16 buckets
+    (Message.java:234).  Two headers whose bucket indices differ in bits 2-3 come out in opposite
+    orders; a deserialised message re-serialises in the read map's order."""
+    def bucket(k, cap):
+        h = wire.java_string_hash(k) & 0xFFFFFFFF
+        return (h ^ (h >> 16)) & (cap - 1)
+    names = [f"h{i}" for i in range(200)]
+    a, b = next((x, y) for x in names for y in names
+                if bucket(x, 16) > bucket(y, 16) and bucket(x, 4) < bucket(y, 4))
+    # new HashMap<>(2): a 2-bucket table, resized to 4 by the second put
+    assert [k for k, _ in wire.java_hashmap_order([(a, "1"), (b, "2")], 2)] == [a, b]
+    assert [k for k, _ in wire.java_hashmap_order([(a, "1"), (b, "2")])] == [b, a]
+    built = wire.Message(((a, "1"), (b, "2")), None)
+    raw = wire.serialize(built)
+    assert raw.index(utf(b)) < raw.index(utf(a))
+    back = wire.deserialize(raw)
+    assert dict(back.headers) == dict(built.headers) and back.map_capacity == 2
+    again = wire.serialize(back)
+    assert again.index(utf(a)) < again.index(utf(b))
+    # one header, and three (tableSizeFor(3) = 4, resized to 8 at the third put): sizes past a resize
+    assert [k for k, _ in wire.java_hashmap_order([(a, "1")], 1)] == [a]
+    three = [(f"k{i}", str(i)) for i in range(3)]
+    got = [k for k, _ in wire.java_hashmap_order(three, 3)]
+    assert got == sorted((k for k, _ in three), key=lambda k: (bucket(k, 8), int(k[1:])))
