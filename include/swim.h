@@ -408,6 +408,25 @@ int32_t swim_profile_fanout(swim_engine* e, swim_kernel_profile* out);
  * duplicates by the sender (SURVEY.md §8(d) merge). */
 int32_t swim_profile_deliver(swim_engine* e, swim_kernel_profile* out);
 
+/* ---- quiet windows ---------------------------------------------------------
+ * While the cluster is provably quiet — no live gossip, no pending failure-detector or suspicion
+ * work, every up member's table equal to the reference row with no SUSPECT / LEAVING record, no loss,
+ * per-link setting, partition, delay, address route or control operation pending — every tick is
+ * member-local (each ping acknowledged at once, gossip rounds with nothing to send,
+ * MembershipProtocolImpl.doSync merging identical tables), and swim_step_ticks advances a whole
+ * window of ticks with two kernel launches, the window ending at the first tick that needs the
+ * per-tick kernel chain.  Results are identical either way.  enable = 0 forces the per-tick chain
+ * (A/B measurement, tests); the default is on (SWIM_QUIET=0 in the environment at creation turns it
+ * off).  The CPU oracle accepts the call and ignores it. */
+int32_t swim_set_quiet_path(swim_engine* e, int32_t enable);
+typedef struct swim_quiet_stats {
+  uint64_t ticks;      /* ticks advanced inside quiet windows */
+  uint64_t windows;    /* windows that advanced at least one tick */
+  uint64_t attempts;   /* windows tried (a scan that found the cluster not quiet advances none) */
+  uint64_t cut_short;  /* windows that ended before their length at a tick needing the per-tick chain */
+} swim_quiet_stats;
+int32_t swim_get_quiet_stats(const swim_engine* e, swim_quiet_stats* out);
+
 /* ---- known-answer hooks (run the engine's own merge / dedupe code on given inputs) --------- */
 /* Philox4x32-10 block used by every draw site. */
 int32_t swim_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

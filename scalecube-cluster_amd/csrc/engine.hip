@@ -198,6 +198,16 @@ struct swim_engine {
   uint32_t route_of(uint32_t x) const { return route_h.empty() ? x : route_h[x]; }
   std::vector<swim_event> events;
   uint64_t host_ticks = 0, host_events = 0;
+  // quiet windows (swim_quiet.h): on unless disabled; after a window that advanced nothing, the next
+  // try waits quiet_backoff ticks (doubling), so a busy cluster pays a scan only now and then
+  bool quiet_on = true;
+  QuietCtl* d_quiet = nullptr;   // device control block (shared by the local shards)
+  QuietCtl* h_quiet = nullptr;   // pinned: the initial image, and the window length read back
+  uint64_t quiet_retry_at = 0;
+  uint32_t quiet_backoff = 1;
+  swim_quiet_stats qst{};
+  std::vector<uint8_t> loss_h;   // host mirror of the default outbound loss per member
+  uint32_t loss_nz = 0;          // members whose default loss is not 0
   uint32_t err_seen = 0;
   bool prof = false;
 
@@ -212,6 +222,8 @@ struct swim_engine {
       if (s.xreg) hipFree(s.xreg);
     }
     if (d_cnt) hipFree(d_cnt);
+    if (d_quiet) hipFree(d_quiet);
+    if (h_quiet) hipHostFree(h_quiet);
     if (h_par) hipHostFree(h_par);
     if (comm) ncclCommDestroy(comm);
     if (stream) hipStreamDestroy(stream);
@@ -558,6 +570,55 @@ static int32_t run_tick(swim_engine* e) {
     k_end_tick<<<ge, REB_BLOCK, 0, s>>>(sd.d_par, T, (T % kRebaseEvery) == 0 ? 1 : 0);
     TICK_CHECK("k_end_tick");
   }
+  return SWIM_OK;
+}
+
+// ---- quiet windows (swim_quiet.h).  The host side of the eligibility: nothing the device check does
+// not cover may be pending or configured — control operations (joins, address binds), the loss and
+// per-link settings of the NetworkEmulator, a partition, message delay, address routes, recorded FD
+// events — and the engine is unsharded or a local group.
+constexpr uint32_t kQuietMax = 4096;         // ticks per window at most
+constexpr uint32_t kQuietBackoffMax = 1024;  // ticks between tries while the cluster is not quiet
+static bool quiet_eligible(const swim_engine* e) {
+  if (!e->quiet_on || e->rccl || !e->joins.empty() || !e->binds.empty() || !e->route_h.empty()) return false;
+  if (!e->links_h.empty() || e->loss_nz) return false;
+  const Ctx& c = e->sh[0].c;
+  return !c.partition && !c.delay_on && !c.record_fd;
+}
+
+// One window of up to K ticks from tick T + 1: every shard's scan, then every shard's apply (a local
+// group shares one control block), then the window's length is read back.
+static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
+  hipStream_t s = e->stream;
+  const uint64_t T0 = e->T + 1;
+  for (Shard& sd : e->sh) {
+    sd.c.T = T0;
+    sync_params(e, sd);
+  }
+  e->h_quiet[0] = QuietCtl{K, 0xffffffffu, 0xffffffffu, 0u};
+  if (hipMemcpyAsync(e->d_quiet, e->h_quiet, sizeof(QuietCtl), hipMemcpyHostToDevice, s) != hipSuccess)
+    return SWIM_EDEVICE;
+  for (Shard& sd : e->sh) {
+    const uint32_t g = std::max<uint32_t>(64, grid_for(sd.c.nl, 256));
+    k_quiet_scan<<<g, 256, 0, s>>>(sd.d_par, T0, K, e->d_quiet);
+  }
+  for (Shard& sd : e->sh) {
+    const uint32_t g = std::max<uint32_t>(64, grid_for(sd.c.nl, 256));
+    k_quiet_apply<<<g, 256, 0, s>>>(sd.d_par, T0, K, e->d_quiet, &e->d_quiet->pad, (uint32_t)kRebaseEvery);
+  }
+  if (hipMemcpyAsync(&e->h_quiet[1].pad, &e->d_quiet->pad, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return hip_status() ? SWIM_EDEVICE : SWIM_EDEVICE;
+  e->par_slot = 0;  // (the stream drained: the Params staging ring restarts)
+  *done = std::min(e->h_quiet[1].pad, K);
+  e->T += *done;
+  e->host_ticks += *done;
+  e->qst.attempts++;
+  if (*done) {
+    e->qst.windows++;
+    e->qst.ticks += *done;
+  }
+  if (*done < K) e->qst.cut_short++;
   return SWIM_OK;
 }
 
@@ -1024,6 +1085,16 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
     if (rc != SWIM_OK) { delete e; return rc; }
   }
   if (hipHostMalloc((void**)&e->h_par, sizeof(Params) * kParRing) != hipSuccess) { delete e; return SWIM_ENOMEM; }
+  if (hipHostMalloc((void**)&e->h_quiet, 2 * sizeof(QuietCtl)) != hipSuccess ||
+      hipMalloc((void**)&e->d_quiet, sizeof(QuietCtl)) != hipSuccess) {
+    delete e;
+    return SWIM_ENOMEM;
+  }
+  {
+    const char* q = std::getenv("SWIM_QUIET");
+    e->quiet_on = !(q && q[0] == '0');
+  }
+  e->loss_h.assign(capacity, 0);
   if (world > 1) {
     if (hipMalloc((void**)&e->d_cnt, sizeof(uint32_t) * 2) != hipSuccess) {
       delete e;
@@ -1140,6 +1211,22 @@ int32_t swim_step_ticks(swim_engine* e, uint32_t ticks) {
   if (!e) return SWIM_EINVAL;
   if (hipSetDevice(e->device) != hipSuccess) return SWIM_EDEVICE;
   for (uint32_t i = 0; i < ticks; ++i) {
+    if (quiet_eligible(e) && e->T + 1 >= e->quiet_retry_at) {
+      const uint32_t K = std::min(ticks - i, kQuietMax);
+      uint32_t done = 0;
+      if (int32_t rc = run_quiet(e, K, &done)) return rc;
+      i += done;
+      if (done == K) {
+        e->quiet_backoff = 1;
+        --i;  // (the loop's ++i)
+        continue;
+      }
+      // the tick the window stopped at needs the per-tick chain; a window that advanced nothing means
+      // the cluster is busy: the next try backs off
+      e->quiet_backoff = done ? 1u : std::min(2 * e->quiet_backoff, kQuietBackoffMax);
+      e->quiet_retry_at = e->T + 1 + e->quiet_backoff;
+      if (i >= ticks) break;
+    }
     if (int32_t rc = run_tick(e)) return rc;
     if (++e->since_drain >= e->drain_every) {
       int32_t r = sync_and_collect(e);
@@ -1315,7 +1402,16 @@ int32_t swim_join_at(swim_engine* e, uint32_t m, uint32_t addr_of) {
 int32_t swim_set_default_loss(swim_engine* e, uint32_t m, int32_t pct) {
   if (!e || pct < 0 || pct > 100) return SWIM_EINVAL;
   if (m != 0xffffffffu && m >= e->n) return SWIM_EINVAL;
-  return set_replicated(e, offsetof(Ctx, default_loss), m, (uint8_t)pct, m == 0xffffffffu);
+  const int32_t rc = set_replicated(e, offsetof(Ctx, default_loss), m, (uint8_t)pct, m == 0xffffffffu);
+  if (rc != SWIM_OK) return rc;
+  if (m == 0xffffffffu) {
+    std::fill(e->loss_h.begin(), e->loss_h.end(), (uint8_t)pct);
+    e->loss_nz = pct ? e->n : 0;
+  } else {
+    e->loss_nz += (pct != 0 ? 1 : 0) - (e->loss_h[m] != 0 ? 1 : 0);
+    e->loss_h[m] = (uint8_t)pct;
+  }
+  return SWIM_OK;
 }
 
 int32_t swim_set_link_loss(swim_engine* e, uint32_t src, uint32_t dst, int32_t pct) {
@@ -1644,6 +1740,20 @@ int32_t swim_read_collector(swim_engine* e, uint32_t v, uint32_t gossiper, swim_
     }
     break;
   }
+  return SWIM_OK;
+}
+
+int32_t swim_set_quiet_path(swim_engine* e, int32_t enable) {
+  if (!e) return SWIM_EINVAL;
+  e->quiet_on = enable != 0;
+  e->quiet_retry_at = 0;
+  e->quiet_backoff = 1;
+  return SWIM_OK;
+}
+
+int32_t swim_get_quiet_stats(const swim_engine* e, swim_quiet_stats* out) {
+  if (!e || !out) return SWIM_EINVAL;
+  *out = e->qst;
   return SWIM_OK;
 }
 

@@ -1987,6 +1987,7 @@ __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Buf
 
 
 #include "swim_sync.h"
+#include "swim_quiet.h"
 
 
 // ------------------------------------------------------------------------------- end of tick

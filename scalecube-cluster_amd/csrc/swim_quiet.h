@@ -1,0 +1,210 @@
+// swim_quiet.h — the quiet fast path: many lockstep ticks in two launches while every member's work
+// is provably member-local (DESIGN.md §5 "Quiet windows").  Included by swim_phases.h inside
+// namespace swimdev, after the SYNC collection helpers.
+//
+// A cluster is QUIET at tick T when (checked on the device by k_quiet_scan):
+//   * no live gossip at any up member, no pending failure-detector state (ack / relay timeouts, FD
+//     SYNCs), no deferred list op, no join / leave / segmentation / compaction work pending;
+//   * every up member's record row equals the reference row `ref` (block witness counts all zero,
+//     DESIGN.md §5) and `ref` holds no SUSPECT or LEAVING record: every SYNC / SYNC_ACK merge is then
+//     a no-op (identical records never change a row, MembershipRecord.isOverrides :67-88, and only
+//     a LEAVING self record would re-run onSelfMemberDetected, MembershipProtocolImpl.java:604-607),
+//     and a failure detector ALIVE result never differs from the view (onFailureDetectorEvent
+//     :418-449 drops it);
+//   * every up member holds the same table size (equal rows), so a SYNC carries the same record
+//     count whoever sends it;
+//   * no suspicion timer falls due (the wheel buckets of the window are empty);
+// and the host has no control operation pending and no NetworkEmulator setting that a message's
+// fate could depend on beyond the up / inbound-default words checked here (no loss, per-link
+// setting, partition, delay, address route, recorded FD events: engine.hip quiet_eligible).
+//
+// Under these conditions a tick changes, per member, only the member's own scalars: doPing's period
+// and cursor (FailureDetectorImpl.java:126-171; every ping is acknowledged at once), the gossip
+// round's period++ with nothing to send (GossipProtocolImpl.java:143-151 returns before target
+// selection), the periodic doSync's schedule and selectSyncAddress draws (MembershipProtocolImpl.java
+// :339-357,461-472: the SYNC and its SYNC_ACK merge nothing), and the counters.  Members are then
+// independent, and one thread can advance its member through a whole window of ticks: k_quiet_scan
+// finds the first tick at which some member's step would leave this regime (a ping target that is
+// down or inbound-blocked, a ping list that must be reshuffled, a due timer bucket) — the window
+// ends there, and that tick runs on the per-tick kernel chain — and k_quiet_apply advances every
+// member through the ticks before it.  The result is bit-for-bit the per-tick chain's
+// (tests/test_quiet_path.py, tests/test_gpu_bench_parity.py).
+#pragma once
+
+struct QuietCtl {
+  uint32_t fail;      // first tick offset (from T0) the window cannot cover; K = the whole window
+  uint32_t tmin;      // min table size over up members (0xffffffff: none)
+  uint32_t tmax_neg;  // 0xffffffff - max table size over up members
+  uint32_t pad;
+};
+
+// the tick offset at which member v (up, owned) leaves the quiet regime within [T0, T0 + K), or K
+__device__ inline uint32_t quiet_member_scan(const Ctx& c, uint32_t v, uint64_t T0, uint32_t K, const MemberDev& m,
+                                             uint32_t fdn, const uint32_t* fail) {
+  const uint64_t Tend = T0 + K;
+  if ((uint64_t)fdn >= Tend || fdn == NONE) return K;
+  const uint32_t* pl = ping_list(c, v);
+  const bool in_v = c.default_inbound[v] != 0;
+  uint32_t cur = m.ping_cursor;
+  const uint32_t len = m.ping_len;
+  for (uint64_t t = fdn; t < Tend; t += c.P) {
+    const uint32_t off = (uint32_t)(t - T0);
+    if ((off & 15) == 0 && __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= off) return K;
+    if (len == 0) continue;       // doPing without members: period++ only
+    if (cur >= len) return off;   // the list wraps: Collections.shuffle (per-tick path)
+    const uint32_t tg = pl[cur++];
+    // the ping and its ack (tryFailOutbound on a stopped destination, the inbound filters); with no
+    // loss and no delay this is the whole round trip
+    if (!c.up[tg] || !c.default_inbound[tg] || !in_v) return off;
+  }
+  return K;
+}
+
+__device__ __forceinline__ void quiet_fail(uint32_t* fail, uint32_t off) {
+  if (off < __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(fail, off);
+}
+
+// k_quiet_scan: T = T0 (the window's first tick), K ticks.  Thread per owned member (grid-stride),
+// plus the global checks spread over the grid: `ref` (every subject), the wheel buckets of the window.
+__global__ void __launch_bounds__(256) k_quiet_scan(KP, uint32_t K, QuietCtl* q) {
+  const Ctx c = pctx(P, T);
+  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
+  uint32_t* fail = &q->fail;
+  // ref: no SUSPECT / LEAVING record in the table
+  for (uint32_t s = gtid; s < c.n; s += gsz) {
+    const uint32_t r = c.ref[s];
+    if (r_in_table(r) && r_status(r) != SWIM_ALIVE) quiet_fail(fail, 0);
+  }
+  // suspicion timers due in the window (a queued entry may be a cancelled timer; the per-tick path
+  // decides, so the window ends at the first non-empty bucket)
+  const uint32_t W = c.wheel_mask + 1, nb = min(K, W);
+  for (uint32_t x = gtid; x < nb * c.wheel_nq; x += gsz) {
+    const uint32_t j = x / c.wheel_nq, qi = x - j * c.wheel_nq;
+    if (c.wheel_cnt[(size_t)((T + j) & c.wheel_mask) * c.wheel_nq + qi]) quiet_fail(fail, j);
+  }
+  uint32_t tmin = 0xffffffffu, tmax = 0;
+  for (uint32_t i = gtid; i < c.nl; i += gsz) {
+    const uint32_t v = c.lo + i;
+    if (c.mflag[i]) { quiet_fail(fail, 0); continue; }  // FD SYNCs / start0 / graceful stop pending
+    if (!c.up[v]) continue;
+    const MemberDev m = c.mem[i];
+    const GossipSched g = c.gs[i];
+    // (an ack / relay deadline before T0 is a stale value of a member that was stopped: never due)
+    bool ok = g.len == 0 && c.compact_flag[i] == 0 && c.seg_flag[i] == 0 && m.ack_due < T && m.relay_due < T &&
+              m.fd_sync_cnt == 0 && m.ins_rank == 0 && !m.join_now && !m.join_pending && !m.leave_pending &&
+              !m.init_wait;
+    // the record row equals ref (its block witness counts are all zero)
+    const uint32_t* bd = c.bdiff + (size_t)i * c.blocks;
+    uint32_t any = 0;
+    for (uint32_t k = 0; k < c.blocks; ++k) any |= bd[k];
+    ok = ok && any == 0;
+    if (!ok) { quiet_fail(fail, 0); continue; }
+    tmin = min(tmin, m.table_size);
+    tmax = max(tmax, m.table_size);
+    const uint32_t off = quiet_member_scan(c, v, T, K, m, c.fd_next[i], fail);
+    if (off < K) quiet_fail(fail, off);
+  }
+  // table sizes (wave-reduced)
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    tmin = min(tmin, (uint32_t)__shfl_xor(tmin, d, 64));
+    tmax = max(tmax, (uint32_t)__shfl_xor(tmax, d, 64));
+  }
+  if ((threadIdx.x & 63) == 0 && tmin != 0xffffffffu) {
+    atomicMin(&q->tmin, tmin);
+    atomicMin(&q->tmax_neg, 0xffffffffu - tmax);
+  }
+}
+
+// the window the scan allowed (every shard's scan has completed: kernel boundary / collective)
+__device__ __forceinline__ uint32_t quiet_window(const QuietCtl* q) {
+  const uint32_t tmin = q->tmin, tmax = 0xffffffffu - q->tmax_neg;
+  return (tmin != 0xffffffffu && tmin != tmax) ? 0u : q->fail;
+}
+
+// doSync of up member v at tick t in a quiet window (sync_collect_fast / select_sync_address with the
+// same draws); the receiver's merge and the SYNC_ACK's are no-ops, so what remains is the counters:
+// ST_SYNCS for a selected target, the record counts of a delivered SYNC and its delivered ack
+__device__ inline void quiet_sync(const Ctx& c0, uint32_t v, uint64_t t, uint32_t tsz, unsigned long long& nsync,
+                                  unsigned long long& nack, unsigned long long& nrec) {
+  Ctx c = c0;
+  c.T = t;
+  const uint32_t x0 = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 0, 0), c.n);
+  uint32_t tg = x0;
+  if (!(x0 != v && ((aux_row(c, v)[x0] & A_IN_MEMBERS) || c.is_seed[x0]))) {
+    tg = select_sync_address(c, v);
+    if (tg == NONE) return;
+  }
+  nsync++;
+  if (!c.up[tg] || !c.default_inbound[tg]) return;  // tryFailOutbound (stopped) / inbound-blocked: dropped
+  nrec += tsz;                                        // onSync's syncMembership over the SYNC's records
+  if (!c.default_inbound[v]) return;                  // the SYNC_ACK is dropped at v's inbound filter
+  nack++;
+  nrec += tsz;                                        // onSyncAck (:385-391): the acker's records
+}
+
+// k_quiet_apply: every owned member advanced through ticks [T, T + F), F = quiet_window(q).  `done`
+// (host-mapped or device) receives F; thread 0 of workgroup 0 also performs the end-of-tick resets the
+// skipped k_end_tick launches would have made (per-parity scratch counters, the witness rebase's
+// dirty marks: with every up row equal to ref a rebase moves no reference record).
+__global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const QuietCtl* q, uint32_t* done,
+                                                     uint32_t rebase_every) {
+  const Ctx c = pctx(P, T);
+  const uint32_t F = quiet_window(q);
+  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
+  if (gtid == 0) *done = F;
+  if (F == 0) return;
+  const uint64_t Tend = T + F;
+  if (gtid == 0) {
+    const Bufs& b = P->b;
+    b.snap_cnt[0] = b.snap_cnt[1] = 0;
+    c.gclaim_cnt[0] = c.gclaim_cnt[1] = 0;
+  }
+  const uint64_t first_rebase = (T + rebase_every - 1) / rebase_every * rebase_every;
+  if (first_rebase < Tend)
+    for (uint32_t s = gtid; s < c.n; s += gsz) c.dirty[s] = 0u;
+  unsigned long long npings = 0, nsync = 0, nack = 0, nrec = 0;
+  for (uint32_t i = gtid; i < c.nl; i += gsz) {
+    const uint32_t v = c.lo + i;
+    const bool up = c.up[v] != 0;
+    MemberDev& m = c.mem[i];
+    // ---- FD (doPing every pingInterval; acknowledged at once)
+    if (up) {
+      uint64_t t = c.fd_next[i];
+      if (t < Tend) {
+        uint32_t k = 0;
+        for (; t < Tend; t += c.P) ++k;
+        m.fd_period += k;
+        m.ev_minor = 0;
+        if (m.ping_len) {
+          m.ping_cursor += k;
+          npings += k;
+        }
+        c.fd_next[i] = (uint32_t)t;
+      }
+    }
+    // ---- gossip rounds (the timer runs while down; period++ only while up)
+    {
+      GossipSched& g = c.gs[i];
+      const uint32_t gn = g.next;
+      if (gn < Tend) {
+        const uint32_t r = (uint32_t)((Tend - 1 - gn) / c.G) + 1;
+        g.next = gn + r * c.G;
+        if (up) g.period += r;
+      }
+    }
+    // ---- periodic SYNC (the schedule advances while down too, sync_collect_fast)
+    uint32_t sn = c.sync_next[i];
+    if (sn != NONE && sn < Tend) {
+      const uint32_t tsz = m.table_size;
+      for (; sn < Tend; sn += c.S)
+        if (up) quiet_sync(c, v, sn, tsz, nsync, nack, nrec);
+      c.sync_next[i] = sn;
+    }
+  }
+  wave_stat_add(c, ST_PINGS, npings);
+  wave_stat_add(c, ST_FD_EVENTS, npings);  // publishPingResult(ALIVE) per acknowledged ping
+  wave_stat_add(c, ST_SYNCS, nsync);
+  wave_stat_add(c, ST_SYNC_ACKS, nack);
+  wave_stat_add(c, ST_SYNC_RECORDS, nrec);
+}

@@ -154,6 +154,10 @@ class swim_interval(C.Structure):
     _fields_ = [("lo", C.c_uint64), ("hi", C.c_uint64)]
 
 
+class swim_quiet_stats(C.Structure):
+    _fields_ = [("ticks", C.c_uint64), ("windows", C.c_uint64), ("attempts", C.c_uint64), ("cut_short", C.c_uint64)]
+
+
 class swim_kernel_profile(C.Structure):
     _fields_ = [("launches", C.c_uint64), ("total_ms", C.c_double), ("messages", C.c_uint64),
                 ("records", C.c_uint64), ("alg_bytes", C.c_uint64)]
@@ -205,6 +209,8 @@ PROTOTYPES = {
     "swim_profile_merge": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_profile_fanout": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_profile_deliver": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
+    "swim_set_quiet_path": (C.c_int32, [_engp, C.c_int32]),
+    "swim_get_quiet_stats": (C.c_int32, [_engp, POINTER(swim_quiet_stats)]),
     "swim_philox": (C.c_int32, [_u32p, _u32p, _u32p]),
     "swim_kat_overrides": (C.c_int32, [POINTER(C.c_int32), C.c_uint32, POINTER(C.c_uint8)]),
     "swim_kat_collector": (C.c_int32, [POINTER(C.c_uint8), POINTER(C.c_int64), C.c_uint32, POINTER(C.c_int64)]),
@@ -441,6 +447,15 @@ class Engine:
         p = swim_kernel_profile()
         _check("swim_profile_deliver", self.lib.swim_profile_deliver(self._h, byref(p)))
         return {name: getattr(p, name) for name, _ in swim_kernel_profile._fields_}
+
+    def set_quiet_path(self, enable: bool) -> None:
+        """swim_set_quiet_path: quiet windows on (default) or the per-tick kernel chain only."""
+        _check("swim_set_quiet_path", self.lib.swim_set_quiet_path(self._h, 1 if enable else 0))
+
+    def quiet_stats(self) -> dict:
+        q = swim_quiet_stats()
+        _check("swim_get_quiet_stats", self.lib.swim_get_quiet_stats(self._h, byref(q)))
+        return {name: getattr(q, name) for name, _ in swim_quiet_stats._fields_}
 
     def read_collector(self, m: int, gossiper: int) -> list[tuple[int, int]]:
         ln = C.c_uint32()
