@@ -579,8 +579,11 @@ static int32_t run_tick(swim_engine* e) {
 // events — and the engine is unsharded or a local group.
 constexpr uint32_t kQuietMax = 4096;         // ticks per window at most
 constexpr uint32_t kQuietBackoffMax = 1024;  // ticks between tries while the cluster is not quiet
+// Every input here is replicated control state, identical on every rank of an RCCL engine (all
+// control calls are collective), so all ranks take the same decision — the window's collective below
+// is entered by all of them or by none.
 static bool quiet_eligible(const swim_engine* e) {
-  if (!e->quiet_on || e->rccl || !e->joins.empty() || !e->binds.empty() || !e->route_h.empty()) return false;
+  if (!e->quiet_on || !e->joins.empty() || !e->binds.empty() || !e->route_h.empty()) return false;
   if (!e->links_h.empty() || e->loss_nz) return false;
   const Ctx& c = e->sh[0].c;
   return !c.partition && !c.delay_on && !c.record_fd;
@@ -602,6 +605,9 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
     const uint32_t g = std::max<uint32_t>(64, grid_for(sd.c.nl, 256));
     k_quiet_scan<<<g, 256, 0, s>>>(sd.d_par, T0, K, e->d_quiet);
   }
+  // RCCL: the window is the minimum over the ranks (fail tick, min table size, 0xffffffff - max)
+  if (e->rccl && nccl_ok(ncclAllReduce(e->d_quiet, e->d_quiet, 3, ncclUint32, ncclMin, e->comm, s)) != SWIM_OK)
+    return SWIM_EDEVICE;
   for (Shard& sd : e->sh) {
     const uint32_t g = std::max<uint32_t>(64, grid_for(sd.c.nl, 256));
     k_quiet_apply<<<g, 256, 0, s>>>(sd.d_par, T0, K, e->d_quiet, &e->d_quiet->pad, (uint32_t)kRebaseEvery);
