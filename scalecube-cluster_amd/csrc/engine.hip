@@ -203,6 +203,7 @@ struct swim_engine {
   bool quiet_on = true;
   QuietCtl* d_quiet = nullptr;   // device control block (shared by the local shards)
   QuietCtl* h_quiet = nullptr;   // pinned: the initial image, and the window length read back
+  uint32_t* d_refmm = nullptr;   // RCCL: [2][n] elementwise min / max of the ranks' witness refs
   uint64_t quiet_retry_at = 0;
   uint32_t quiet_backoff = 1;
   swim_quiet_stats qst{};
@@ -223,6 +224,7 @@ struct swim_engine {
     }
     if (d_cnt) hipFree(d_cnt);
     if (d_quiet) hipFree(d_quiet);
+    if (d_refmm) hipFree(d_refmm);
     if (h_quiet) hipHostFree(h_quiet);
     if (h_par) hipHostFree(h_par);
     if (comm) ncclCommDestroy(comm);
@@ -601,9 +603,23 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
   e->h_quiet[0] = QuietCtl{K, 0xffffffffu, 0xffffffffu, 0u};
   if (hipMemcpyAsync(e->d_quiet, e->h_quiet, sizeof(QuietCtl), hipMemcpyHostToDevice, s) != hipSuccess)
     return SWIM_EDEVICE;
+  // the shards' witness refs must agree (k_quiet_scan): RCCL compares the ranks' elementwise min and max
+  if (e->rccl) {
+    const size_t n = e->n;
+    if (!e->d_refmm && hipMalloc((void**)&e->d_refmm, 8 * n) != hipSuccess) return SWIM_ENOMEM;
+    if (hipMemcpyAsync(e->d_refmm, e->sh[0].c.ref, 4 * n, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(e->d_refmm + n, e->sh[0].c.ref, 4 * n, hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return SWIM_EDEVICE;
+    if (ncclGroupStart() != ncclSuccess) return SWIM_EDEVICE;
+    ncclAllReduce(e->d_refmm, e->d_refmm, n, ncclUint32, ncclMin, e->comm, s);
+    ncclAllReduce(e->d_refmm + n, e->d_refmm + n, n, ncclUint32, ncclMax, e->comm, s);
+    if (nccl_ok(ncclGroupEnd()) != SWIM_OK) return SWIM_EDEVICE;
+  }
   for (Shard& sd : e->sh) {
     const uint32_t g = std::max<uint32_t>(64, grid_for(sd.c.nl, 256));
-    k_quiet_scan<<<g, 256, 0, s>>>(sd.d_par, T0, K, e->d_quiet);
+    const uint32_t* ra = e->rccl ? e->d_refmm : e->world > 1 ? e->sh[0].c.ref : nullptr;
+    const uint32_t* rb = e->rccl ? e->d_refmm + e->n : sd.c.ref;
+    k_quiet_scan<<<g, 256, 0, s>>>(sd.d_par, T0, K, e->d_quiet, ra, rb);
   }
   // RCCL: the window is the minimum over the ranks (fail tick, min table size, 0xffffffff - max)
   if (e->rccl && nccl_ok(ncclAllReduce(e->d_quiet, e->d_quiet, 3, ncclUint32, ncclMin, e->comm, s)) != SWIM_OK)

@@ -66,14 +66,20 @@ __device__ __forceinline__ void quiet_fail(uint32_t* fail, uint32_t off) {
 
 // k_quiet_scan: T = T0 (the window's first tick), K ticks.  Thread per owned member (grid-stride),
 // plus the global checks spread over the grid: `ref` (every subject), the wheel buckets of the window.
-__global__ void __launch_bounds__(256) k_quiet_scan(KP, uint32_t K, QuietCtl* q) {
+// Sharded engines: each shard's witness proves its rows equal ITS ref, so the shards' refs must be
+// equal too (a partition healed after removal leaves each side's shard with its own ref): ref_a / ref_b
+// are two arrays that agree at every subject iff they do — a local group passes shard 0's ref and
+// this shard's, an RCCL engine the elementwise min and max of the ranks' refs (allreduced).
+__global__ void __launch_bounds__(256) k_quiet_scan(KP, uint32_t K, QuietCtl* q, const uint32_t* ref_a,
+                                                    const uint32_t* ref_b) {
   const Ctx c = pctx(P, T);
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
   uint32_t* fail = &q->fail;
-  // ref: no SUSPECT / LEAVING record in the table
+  // ref: no SUSPECT / LEAVING record in the table, and one ref for every shard
   for (uint32_t s = gtid; s < c.n; s += gsz) {
     const uint32_t r = c.ref[s];
     if (r_in_table(r) && r_status(r) != SWIM_ALIVE) quiet_fail(fail, 0);
+    if (ref_a && ref_a[s] != ref_b[s]) quiet_fail(fail, 0);
   }
   // suspicion timers due in the window (a queued entry may be a cancelled timer; the per-tick path
   // decides, so the window ends at the first non-empty bucket)
