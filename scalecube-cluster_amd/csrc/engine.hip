@@ -201,8 +201,10 @@ struct swim_engine {
   // quiet windows (swim_quiet.h): on unless disabled; after a window that advanced nothing, the next
   // try waits quiet_backoff ticks (doubling), so a busy cluster pays a scan only now and then
   bool quiet_on = true;
-  QuietCtl* d_quiet = nullptr;   // device control block (shared by the local shards)
-  QuietCtl* h_quiet = nullptr;   // pinned: the initial image, and the window length read back
+  QuietCtl* d_quiet = nullptr;   // [2] device control blocks (shared by the local shards), alternating
+  uint32_t q_par = 0;            // the block the next window uses
+  uint32_t* h_done = nullptr;    // pinned host word: the last window's length (written by k_quiet_apply)
+  uint32_t* d_done = nullptr;    // its device address
   uint32_t* d_refmm = nullptr;   // RCCL: [2][n] elementwise min / max of the ranks' witness refs
   uint64_t quiet_retry_at = 0;
   uint32_t quiet_backoff = 1;
@@ -225,7 +227,7 @@ struct swim_engine {
     if (d_cnt) hipFree(d_cnt);
     if (d_quiet) hipFree(d_quiet);
     if (d_refmm) hipFree(d_refmm);
-    if (h_quiet) hipHostFree(h_quiet);
+    if (h_done) hipHostFree(h_done);
     if (h_par) hipHostFree(h_par);
     if (comm) ncclCommDestroy(comm);
     if (stream) hipStreamDestroy(stream);
@@ -600,9 +602,9 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
     sd.c.T = T0;
     sync_params(e, sd);
   }
-  e->h_quiet[0] = QuietCtl{K, 0xffffffffu, 0xffffffffu, 0u};
-  if (hipMemcpyAsync(e->d_quiet, e->h_quiet, sizeof(QuietCtl), hipMemcpyHostToDevice, s) != hipSuccess)
-    return SWIM_EDEVICE;
+  QuietCtl* q = e->d_quiet + e->q_par;  // reset by the previous window's apply (or at creation)
+  QuietCtl* q_next = e->d_quiet + (e->q_par ^ 1u);
+  e->q_par ^= 1u;
   // the shards' witness refs must agree (k_quiet_scan): RCCL compares the ranks' elementwise min and max
   if (e->rccl) {
     const size_t n = e->n;
@@ -619,20 +621,18 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
     const uint32_t g = std::max<uint32_t>(64, grid_for(sd.c.nl, 256));
     const uint32_t* ra = e->rccl ? e->d_refmm : e->world > 1 ? e->sh[0].c.ref : nullptr;
     const uint32_t* rb = e->rccl ? e->d_refmm + e->n : sd.c.ref;
-    k_quiet_scan<<<g, 256, 0, s>>>(sd.d_par, T0, K, e->d_quiet, ra, rb);
+    k_quiet_scan<<<g, 256, 0, s>>>(sd.d_par, T0, K, q, ra, rb);
   }
   // RCCL: the window is the minimum over the ranks (fail tick, min table size, 0xffffffff - max)
-  if (e->rccl && nccl_ok(ncclAllReduce(e->d_quiet, e->d_quiet, 3, ncclUint32, ncclMin, e->comm, s)) != SWIM_OK)
+  if (e->rccl && nccl_ok(ncclAllReduce(q, q, 3, ncclUint32, ncclMin, e->comm, s)) != SWIM_OK)
     return SWIM_EDEVICE;
   for (Shard& sd : e->sh) {
     const uint32_t g = std::max<uint32_t>(64, grid_for(sd.c.nl, 256));
-    k_quiet_apply<<<g, 256, 0, s>>>(sd.d_par, T0, K, e->d_quiet, &e->d_quiet->pad, (uint32_t)kRebaseEvery);
+    k_quiet_apply<<<g, 256, 0, s>>>(sd.d_par, T0, K, q, q_next, e->d_done, (uint32_t)kRebaseEvery);
   }
-  if (hipMemcpyAsync(&e->h_quiet[1].pad, &e->d_quiet->pad, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return hip_status() ? SWIM_EDEVICE : SWIM_EDEVICE;
+  if (hipStreamSynchronize(s) != hipSuccess) return SWIM_EDEVICE;
   e->par_slot = 0;  // (the stream drained: the Params staging ring restarts)
-  *done = std::min(e->h_quiet[1].pad, K);
+  *done = std::min(__atomic_load_n(e->h_done, __ATOMIC_ACQUIRE), K);
   e->T += *done;
   e->host_ticks += *done;
   e->qst.attempts++;
@@ -1107,8 +1107,10 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
     if (rc != SWIM_OK) { delete e; return rc; }
   }
   if (hipHostMalloc((void**)&e->h_par, sizeof(Params) * kParRing) != hipSuccess) { delete e; return SWIM_ENOMEM; }
-  if (hipHostMalloc((void**)&e->h_quiet, 2 * sizeof(QuietCtl)) != hipSuccess ||
-      hipMalloc((void**)&e->d_quiet, sizeof(QuietCtl)) != hipSuccess) {
+  if (hipHostMalloc((void**)&e->h_done, 64, hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&e->d_done, e->h_done, 0) != hipSuccess ||
+      hipMalloc((void**)&e->d_quiet, 2 * sizeof(QuietCtl)) != hipSuccess ||
+      hipMemset(e->d_quiet, 0xff, 2 * sizeof(QuietCtl)) != hipSuccess) {  // both blocks reset: no fail, no sizes
     delete e;
     return SWIM_ENOMEM;
   }

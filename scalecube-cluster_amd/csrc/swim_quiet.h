@@ -32,32 +32,48 @@
 #pragma once
 
 struct QuietCtl {
-  uint32_t fail;      // first tick offset (from T0) the window cannot cover; K = the whole window
+  uint32_t fail;      // first tick offset (from T0) the window cannot cover (0xffffffff: none found)
   uint32_t tmin;      // min table size over up members (0xffffffff: none)
   uint32_t tmax_neg;  // 0xffffffff - max table size over up members
   uint32_t pad;
 };
 
-// the tick offset at which member v (up, owned) leaves the quiet regime within [T0, T0 + K), or K
+// the tick offset at which member v (up, owned) leaves the quiet regime within [T0, T0 + K), or K.
+// Its pings of the window go to the next entries of its ping list (no reshuffle before the list's
+// end); they are checked eight at a time: the list words in one batch of loads, then the targets'
+// up / inbound words in another.
+constexpr uint32_t QUIET_BATCH = 8;
 __device__ inline uint32_t quiet_member_scan(const Ctx& c, uint32_t v, uint64_t T0, uint32_t K, const MemberDev& m,
                                              uint32_t fdn, const uint32_t* fail) {
   const uint64_t Tend = T0 + K;
-  if ((uint64_t)fdn >= Tend || fdn == NONE) return K;
-  const uint32_t* pl = ping_list(c, v);
-  const bool in_v = c.default_inbound[v] != 0;
-  uint32_t cur = m.ping_cursor;
-  const uint32_t len = m.ping_len;
-  for (uint64_t t = fdn; t < Tend; t += c.P) {
-    const uint32_t off = (uint32_t)(t - T0);
-    if ((off & 15) == 0 && __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= off) return K;
-    if (len == 0) continue;       // doPing without members: period++ only
-    if (cur >= len) return off;   // the list wraps: Collections.shuffle (per-tick path)
-    const uint32_t tg = pl[cur++];
-    // the ping and its ack (tryFailOutbound on a stopped destination, the inbound filters); with no
-    // loss and no delay this is the whole round trip
-    if (!c.up[tg] || !c.default_inbound[tg] || !in_v) return off;
+  const uint32_t len = m.ping_len, cur = m.ping_cursor;
+  if ((uint64_t)fdn >= Tend || fdn == NONE || len == 0) return K;  // no doPing, or period++ only
+  const uint32_t np = (uint32_t)((Tend - 1 - fdn) / c.P) + 1;     // doPing calls in the window
+  // the ping after the list's last entry reshuffles it (Collections.shuffle): the per-tick path
+  uint32_t limit = np, end_off = K;
+  if (cur + np > len) {
+    limit = cur < len ? len - cur : 0u;
+    end_off = (uint32_t)(fdn + (uint64_t)limit * c.P - T0);
   }
-  return K;
+  // the ping and its ack (tryFailOutbound on a stopped destination, both inbound filters); with no
+  // loss and no delay this is the whole round trip
+  if (limit && !c.default_inbound[v]) return (uint32_t)(fdn - T0);
+  const uint32_t* pl = ping_list(c, v) + cur;
+  for (uint32_t k0 = 0; k0 < limit; k0 += QUIET_BATCH) {
+    if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= (uint32_t)(fdn + (uint64_t)k0 * c.P - T0))
+      return K;  // an earlier tick already ends the window
+    uint32_t tg[QUIET_BATCH];
+#pragma unroll
+    for (uint32_t j = 0; j < QUIET_BATCH; ++j) tg[j] = k0 + j < limit ? pl[k0 + j] : v;
+    uint32_t bad = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < QUIET_BATCH; ++j) {
+      const bool ok = c.up[tg[j]] != 0 && c.default_inbound[tg[j]] != 0;
+      bad |= (k0 + j < limit && !ok) ? 1u << j : 0u;
+    }
+    if (bad) return (uint32_t)(fdn + (uint64_t)(k0 + __ffs(bad) - 1) * c.P - T0);
+  }
+  return end_off;
 }
 
 __device__ __forceinline__ void quiet_fail(uint32_t* fail, uint32_t off) {
@@ -123,9 +139,9 @@ __global__ void __launch_bounds__(256) k_quiet_scan(KP, uint32_t K, QuietCtl* q,
 }
 
 // the window the scan allowed (every shard's scan has completed: kernel boundary / collective)
-__device__ __forceinline__ uint32_t quiet_window(const QuietCtl* q) {
+__device__ __forceinline__ uint32_t quiet_window(const QuietCtl* q, uint32_t K) {
   const uint32_t tmin = q->tmin, tmax = 0xffffffffu - q->tmax_neg;
-  return (tmin != 0xffffffffu && tmin != tmax) ? 0u : q->fail;
+  return (tmin != 0xffffffffu && tmin != tmax) ? 0u : min(q->fail, K);
 }
 
 // doSync of up member v at tick t in a quiet window (sync_collect_fast / select_sync_address with the
@@ -150,15 +166,20 @@ __device__ inline void quiet_sync(const Ctx& c0, uint32_t v, uint64_t t, uint32_
 }
 
 // k_quiet_apply: every owned member advanced through ticks [T, T + F), F = quiet_window(q).  `done`
-// (host-mapped or device) receives F; thread 0 of workgroup 0 also performs the end-of-tick resets the
-// skipped k_end_tick launches would have made (per-parity scratch counters, the witness rebase's
-// dirty marks: with every up row equal to ref a rebase moves no reference record).
-__global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const QuietCtl* q, uint32_t* done,
-                                                     uint32_t rebase_every) {
+// (pinned host memory) receives F; `next` is the other control block, reset here for the next window
+// (windows alternate between the two, so no copy precedes a scan).  Thread 0 of workgroup 0 also
+// performs the end-of-tick resets the skipped k_end_tick launches would have made (per-parity scratch
+// counters, the witness rebase's dirty marks: with every up row equal to ref a rebase moves no
+// reference record).
+__global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const QuietCtl* q, QuietCtl* next,
+                                                     uint32_t* done, uint32_t rebase_every) {
   const Ctx c = pctx(P, T);
-  const uint32_t F = quiet_window(q);
+  const uint32_t F = quiet_window(q, K);
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
-  if (gtid == 0) *done = F;
+  if (gtid == 0) {
+    *done = F;
+    *next = QuietCtl{0xffffffffu, 0xffffffffu, 0xffffffffu, 0u};
+  }
   if (F == 0) return;
   const uint64_t Tend = T + F;
   if (gtid == 0) {
