@@ -3,24 +3,28 @@
 One step = one SWIM protocol period (ping_interval of virtual time: 10 ticks of 100 ms with the LAN
 defaults) for all N members: FD pings / ping-reqs, 5 gossip rounds, staggered periodic SYNC
 (N/300 full-table exchanges per tick), suspicion timers and event compaction — the whole hot path of
-SURVEY.md §8 on synthetic input (a converged N-member cluster losing one member every 20 periods).
+SURVEY.md §8 on synthetic input (the headline: a converged N-member cluster with no faults; the
+failures workload kills a member every 20 periods; the churn workload is BASELINE config 3).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--members 65536]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--members 65536] [--workload quiet|failures|churn]
 
-With N > 1 (launched by torch.distributed.run, one process per GPU) the SAME N-member cluster is
-row-sharded over the N GPUs (swim_create_shard): each rank owns members [r*N/G, (r+1)*N/G) and the
-cross-shard GOSSIP_REQ / SYNC / SYNC_ACK traffic is pulled by device kernels from the producers'
-exchange regions over xGMI (IPC-mapped), one ncclAllToAll of counts per exchange inside the library
-(DESIGN.md §7).  Total work is fixed, so `scaling` is "strong".  torch.distributed only broadcasts
-the RCCL bootstrap id and brackets the timed region with barriers.
+The engine advances a provably quiet cluster through whole windows of ticks with two kernel launches
+(swim_quiet.h, DESIGN.md §5: every member's tick is member-local, bit-exact with the per-tick kernel
+chain), and the per-tick chain for every tick that needs it.  With N > 1 (`--gpus N` starts
+torch.distributed.run with N ranks itself, as a child process; or the driver launches it) the SAME
+N-member cluster is row-sharded over the N GPUs (swim_create_shard): each rank owns members
+[r*N/G, (r+1)*N/G), cross-shard GOSSIP_REQ / SYNC / SYNC_ACK traffic is pulled by device kernels from
+the producers' exchange regions over xGMI, counts by ncclAllToAll inside the library.
+Total work is fixed, so `scaling` is "strong".  torch.distributed (gloo) only bootstraps RCCL and
+brackets the timed region with barriers.
 
-Prints ONE JSON line with `value` (whole-job member-periods/s); `roofline`: the whole step against
-HBM (SURVEY.md §8(d) algorithmic bytes per member-period over the measured period time, traffic from
-the same workload's PMC passes under profiles/); `roofline_merge` (the SYNC merge, k_sync_apply with
-its classification fused), `roofline_fanout` / `roofline_deliver` (k_gossip_emit / k_gossip_deliver
-over a failures-workload storm window, side runs), `ks_mode` and the `cpu_baseline` (the CPU oracle
-on 16 of the box's cores and on 1 thread, rank 0 / N=1 only).  Kernel times are HIP events on the
-engine's own stream.
+Prints ONE JSON line with `value` (whole-job member-periods/s) and the rooflines of the kernels that
+carried the step (`roofline`: the quiet windows' k_quiet_scan + k_quiet_apply; `roofline_step`: the
+whole step against its wall time), plus — single GPU, quiet workload — side runs on the same N: the
+per-tick kernel chain (`per_tick_path`, with the SYNC merge's roofline), the failures workload
+(`failures`, with the fanout and delivery kernels' rooflines), BASELINE config 3 (`churn`, N =
+16,384), the KS timing mode (`ks_mode`), and the CPU oracle on the box's cores (`cpu_baseline`).
+Every kernel time is HIP events on the engine's own stream.
 """
 import argparse
 import json
@@ -165,32 +169,76 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def side_run(lib, workload, n, warmup, steps, device=0, **knobs):
+def side_run(lib, workload, n, warmup, steps, device=0, quiet=True, **knobs):
     """A secondary single-GPU measurement on its own engine (the headline engine is closed first):
     `warmup` untimed periods, then `steps` timed ones.  Returns (seconds, merge profile, fanout
-    profile, stats, deliver profile)."""
+    profile, stats, deliver profile, quiet-window stats)."""
     import torch
     from swimgpu import abi
     sch = Schedule(workload, n, warmup + steps)
     cfg = make_config(lib, device)
+    if workload == "churn":
+        churn_capacities(cfg, sch.capacity)
     for k, v in knobs.items():
         setattr(cfg, k, v)
     e = abi.Engine(lib, cfg, sch.capacity, n, 1)
     try:
+        e.set_quiet_path(quiet)
         sch.setup(e)
         sch.run(e, 0, warmup)
         e.drain_events()
         torch.cuda.synchronize()
         e.profile_enable(True)
+        q0 = e.quiet_stats()
         t0 = time.perf_counter()
         sch.run(e, warmup, warmup + steps)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        out = (dt, e.profile_merge(), e.profile_fanout(), e.stats(), e.profile_deliver())
+        q1 = e.quiet_stats()
+        out = (dt, e.profile_merge(), e.profile_fanout(), e.stats(), e.profile_deliver(),
+               {k: q1[k] - q0[k] for k in q1})
         e.drain_events()
     finally:
         e.close()
     return out
+
+
+def quiet_roofline(qprof, workload, n):
+    """k_quiet_scan + k_quiet_apply (a quiet window's two launches) against HBM: swim_profile_quiet's
+    algorithmic bytes (SURVEY.md §8(d) ping phase, 21 B per member-period, plus the quiet check's
+    reads once per window) over the kernels' HIP-event time; traffic = the same kernels' HBM bytes
+    per window from the committed PMC passes of this workload."""
+    per_win = qprof["alg_bytes"] / max(1, qprof["launches"])
+    ach = qprof["alg_bytes"] / max(1e-12, qprof["total_ms"] / 1e3) / 1e9
+    ts, ta = pmc_traffic("k_quiet_scan", f"{workload}{n // 1024}k"), pmc_traffic("k_quiet_apply", f"{workload}{n // 1024}k")
+    traffic = ts[0] + ta[0] if ts[0] is not None and ta[0] is not None else None
+    return {"bound": "hbm", "kernel": "k_quiet_scan + k_quiet_apply (one quiet window)", "achieved": ach,
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
+            "traffic_unit": "HBM bytes per window (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of both kernels)",
+            "traffic_source": ts[1], "windows": qprof["launches"], "avg_window_ms": qprof["total_ms"] / max(1, qprof["launches"]),
+            "alg_bytes_per_window": per_win, "ticks_per_window": qprof["messages"] / max(1, qprof["launches"]),
+            "member_periods_per_window": qprof["records"] / max(1, qprof["launches"]),
+            "alg_bytes_rule": "21 B per member-period (SURVEY.md §8(d) ping phase) + per window the quiet check's "
+                              "reads: 4 B x 1,024-subject blocks of witness counts + 64 B of member words per row, "
+                              "4 B per subject of the reference row, 4 B per timer-bucket queue (swim.h "
+                              "swim_profile_quiet)"}
+
+
+def merge_roofline(prof, world, local_shards, workload, n, dt, steps, tpp):
+    """The SYNC merge: k_sync_apply's SYNC launch (unsharded: classification fused) or k_sync_classify
+    (sharded), HIP events on one launch in three."""
+    merge_kernel = "k_sync_apply" if world == 1 and local_shards == 1 else "k_sync_classify"
+    traffic, src = pmc_traffic(merge_kernel, f"{workload}{n // 1024}k")
+    avg_ms = prof["total_ms"] / max(1, prof["launches"])
+    ach = prof["alg_bytes"] / max(1e-12, prof["total_ms"] / 1e3) / 1e9
+    return {"bound": "hbm", "kernel": merge_kernel + (" (SYNC launch, classification fused)"
+                                                      if merge_kernel == "k_sync_apply" else ""),
+            "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
+            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the same kernel)",
+            "traffic_source": src, "launches": prof["launches"], "avg_launch_ms": avg_ms,
+            "alg_bytes_per_launch": prof["alg_bytes"] / max(1, prof["launches"]),
+            # one SYNC merge launch per tick (the SYNC_ACK launch, k_ack_apply, reuses its results)
+            "kernel_time_share": avg_ms * tpp / (dt * 1e3 / steps)}
 
 
 def fanout_roofline(fprof, window, same_window_pmc):
@@ -238,7 +286,7 @@ def deliver_roofline(dprof, window, same_window_pmc):
             "window": window}
 
 
-def step_roofline(stats, prof, fprof, dprof, ticks, gossip_ticks, dt, steps, workload, n):
+def step_roofline(stats, prof, fprof, dprof, qprof, ticks, gossip_ticks, dt, steps, workload, n):
     """The whole step against the HBM roofline (the quiet step is a chain of latency-bound launches,
     no single kernel owns it): SURVEY.md §8(d)'s algorithmic bytes of everything the step did in the
     timed window — ping phase 21 B per ping, events 16 B each, timers 4 B per fired timer, and the
@@ -246,16 +294,22 @@ def step_roofline(stats, prof, fprof, dprof, ticks, gossip_ticks, dt, steps, wor
     window's launches of each — over the timed wall time.  `traffic`: the HBM bytes per tick of every
     kernel (the committed rocprofv3 PMC passes of this workload) times the window's ticks."""
     per = lambda p: p["alg_bytes"] / max(1, p["launches"])
-    parts = {"fd_pings": 21.0 * stats["pings"], "events": 16.0 * stats["events"],
-             "timers": 4.0 * stats["timers_fired"], "sync_classify": per(prof) * ticks,
-             "fanout": per(fprof) * gossip_ticks, "deliver": per(dprof) * gossip_ticks}
+    # the ticks that ran on the per-tick chain (the others ran inside quiet windows, whose bytes are
+    # swim_profile_quiet's; the per-tick kernels are sampled one launch in three)
+    chain = max(0, ticks - qprof["messages"])
+    parts = {"fd_pings": 21.0 * stats["pings"] if not qprof["launches"] else 0.0, "events": 16.0 * stats["events"],
+             "timers": 4.0 * stats["timers_fired"], "sync_classify": per(prof) * chain,
+             "fanout": per(fprof) * gossip_ticks * chain / max(1, ticks), "deliver": per(dprof) * gossip_ticks * chain / max(1, ticks),
+             "quiet_windows": float(qprof["alg_bytes"])}
     total = sum(parts.values())
     ach = total / dt / 1e9
     import glob
     traffic, src = None, None
     paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}{n // 1024}k_pmc.json")))
     kst = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}{n // 1024}k_kernel_stats.csv")))
-    if paths and kst and os.path.basename(paths[-1]).split("_")[0] == os.path.basename(kst[-1]).split("_")[0]:
+    # (a PMC profile of the per-tick chain only: with quiet windows the windows' roofline carries the traffic)
+    if paths and kst and os.path.basename(paths[-1]).split("_")[0] == os.path.basename(kst[-1]).split("_")[0] \
+            and not qprof["launches"]:
         import csv
         doc = json.load(open(paths[-1]))
         calls = {r["kernel"]: int(r["calls"]) for r in csv.DictReader(open(kst[-1]))}
@@ -271,7 +325,7 @@ def step_roofline(stats, prof, fprof, dprof, ticks, gossip_ticks, dt, steps, wor
             "alg_bytes_per_member_period": total / steps / n,
             "alg_bytes_parts_per_step": {k: v / steps for k, v in parts.items()},
             "rule": "SURVEY.md §8(d): ping 21 B, event 16 B, timer 4 B, SYNC classify / fanout / delivery per "
-                    "their swim_profile_* rules"}
+                    "their swim_profile_* rules, quiet windows per swim_profile_quiet"}
 
 
 def cpu_baseline(n, p0, periods):
@@ -349,6 +403,7 @@ def main():
                     help="quiet workload: skip the fanout-roofline (failures window) and KS-mode side runs")
     ap.add_argument("--fanout-steps", type=int, default=6)
     ap.add_argument("--ks-steps", type=int, default=5)
+    ap.add_argument("--no-churn", action="store_true", help="skip the config-3 churn side run")
     ap.add_argument("--progress", action="store_true", help="print a stderr line after every period")
     ap.add_argument("--workload", choices=("quiet", "failures", "churn"), default="quiet")
     ap.add_argument("--gossip-capacity", type=int, default=0)
@@ -430,24 +485,23 @@ def main():
     stats = {k: (st1[k] - st0[k] if k != "capacity_errors" else st1[k]) for k in st1}
     tpp = e.now()[2]
     e.drain_events()
+    def reduce(p):  # summed over ranks (the line's kernel figures are the whole job's)
+        st = torch.tensor([float(p["alg_bytes"]), p["total_ms"], float(p["launches"])], dtype=torch.float64)
+        dist.all_reduce(st, op=dist.ReduceOp.SUM)
+        return {**p, "alg_bytes": st[0].item(), "total_ms": st[1].item(), "launches": int(st[2].item())}
     if se is not None:
         dt = se.max_time(dt)
-
-        def reduce(p):
-            st = torch.tensor([float(p["alg_bytes"]), p["total_ms"], float(p["launches"])], dtype=torch.float64)
-            dist.all_reduce(st, op=dist.ReduceOp.SUM)
-            return {"alg_bytes": st[0].item(), "total_ms": st[1].item(), "launches": int(st[2].item())}
         prof, fprof, dprof = reduce(prof), reduce(fprof), reduce(dprof)
     if stats["capacity_errors"]:
         raise SystemExit(f"capacity error during the benchmark: {stats['capacity_errors']:#x}")
 
+    qprof = e.profile_quiet()
+    if se is not None:
+        qprof = {**qprof, **reduce(qprof)}
+    qst = e.quiet_stats()
     value = n * args.steps / dt  # one cluster of n members, sharded over `world` GPUs
-    avg_ms = prof["total_ms"] / max(1, prof["launches"])
-    achieved = prof["alg_bytes"] / max(1e-12, prof["total_ms"] / 1e3) / 1e9
-    # unsharded: the SYNC classification runs inside the SYNC launch of k_sync_apply (fused, no
-    # classify launch); sharded: k_sync_classify streams the rows that arrived from other shards
-    merge_kernel = "k_sync_apply" if world == 1 and args.local_shards == 1 else "k_sync_classify"
-    traffic, traffic_src = pmc_traffic(merge_kernel, f"{args.workload}{n // 1024}k")
+    ticks = args.steps * tpp
+    gossip_ticks = ticks // max(1, cfg.gossip_interval // e.now()[1])  # ticks with a gossip round
     line = {
         "metric": "simulated member-protocol-periods/sec at N=65,536; achieved HBM GB/s",
         "value": value,
@@ -469,25 +523,22 @@ def main():
                    "parallelism": (f"rows sharded over {world} GPUs, RCCL send/recv over xGMI" if world > 1 else
                                    f"single GPU, {args.local_shards} in-process shards" if args.local_shards > 1
                                    else "single GPU")},
+        "timing": "every kernel time on this line is HIP events on the engine's own stream, measured in this "
+                  "run; profiles/<round>_*_kernel_stats.csv (rocprofv3 --kernel-trace --stats of the same command) "
+                  "must agree with them; PMC passes give traffic only (their durations include counter overhead)",
         "roofline": None,
-        "roofline_merge": {"bound": "hbm", "kernel": merge_kernel + (" (SYNC launch, classification fused)"
-                                                                     if merge_kernel == "k_sync_apply" else ""),
-                     "achieved": achieved, "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                     "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE; k_sync_apply: its SYNC "
-                                     "and SYNC_ACK launches averaged)",
-                     "traffic_source": traffic_src,
-                     "launches": prof["launches"], "avg_launch_ms": avg_ms,
-                     "alg_bytes_per_launch": prof["alg_bytes"] / max(1, prof["launches"]),
-                     # one SYNC merge launch per tick (the SYNC_ACK launch reuses its results); 1 in 3 timed
-                     "kernel_time_share": avg_ms * e.now()[2] / (dt * 1e3 / args.steps)},
+        "quiet_windows": {"ticks": qst["ticks"], "windows": qst["windows"], "attempts": qst["attempts"],
+                          "cut_short": qst["cut_short"], "timed_ticks": ticks},
         "stats": {k: stats[k] for k in ("syncs", "sync_records", "gossip_messages", "gossips_created", "pings",
                                          "timers_fired", "events")},
     }
-    ticks = args.steps * tpp
-    gossip_ticks = ticks // max(1, cfg.gossip_interval // e.now()[1])  # ticks with a gossip round
-    line["roofline"] = step_roofline(stats, prof, fprof, dprof, ticks, gossip_ticks, dt, args.steps,
-                                     args.workload, n)
+    step = step_roofline(stats, prof, fprof, dprof, qprof, ticks, gossip_ticks, dt, args.steps, args.workload, n)
+    # the roofline of the step's dominant kernels: the quiet windows' (k_quiet_scan + k_quiet_apply)
+    # when they carried the step, else the whole per-tick chain against its wall time
+    line["roofline"] = quiet_roofline(qprof, args.workload, n) if qprof["launches"] else step
+    line["roofline_step"] = step
+    if prof["launches"]:
+        line["roofline_merge"] = merge_roofline(prof, world, args.local_shards, args.workload, n, dt, args.steps, tpp)
     if fprof["alg_bytes"] > 0:
         # the gossip fanout kernel (north_star: merge AND fanout against the HBM roofline); only
         # workloads with gossip traffic (failures, churn) give it work
@@ -496,22 +547,43 @@ def main():
         line["roofline_deliver"] = deliver_roofline(dprof, f"the timed window ({args.workload})", same)
     if world == 1 and args.workload == "quiet" and not args.no_extras and args.local_shards == 1 and hook is None:
         e.close()
-        # the quiet headline sends no gossip: the fanout kernel is measured on the failures workload
-        # over a window that starts with its second kill (period 30: FD detection, the SUSPECT storm
-        # through all N members, then the gossip's remaining rounds).  The first storm also holds
-        # every member's first selectGossipMembers shuffle of its 65,535-entry remote list (once per
-        # member, then every N / fanout rounds), which is not the steady state.
+        # (1) the per-tick kernel chain on the same workload (quiet windows off): the SYNC merge's
+        # roofline (k_sync_apply's SYNC launch, classification fused) is measured there
+        p_dt, p_prof, _, _, _, _ = side_run(lib, "quiet", n, 2, args.ks_steps, local_rank, quiet=False)
+        line["per_tick_path"] = {
+            "value": n * args.ks_steps / p_dt, "unit": "member-periods/s", "ms_per_step": p_dt / args.ks_steps * 1e3,
+            "steps": args.ks_steps, "config": "same workload, quiet windows off (swim_set_quiet_path(0)): the "
+                                              "per-tick kernel chain of DESIGN.md §5",
+            "roofline_merge": merge_roofline(p_prof, 1, 1, "quiet", n, p_dt, args.ks_steps, tpp)}
+        # (2) the failures workload over a window that starts with its second kill (period 30: FD
+        # detection, the SUSPECT storm through all N members, the gossip's remaining rounds): the
+        # fanout and delivery kernels.  The first storm also holds every member's first
+        # selectGossipMembers shuffle of its 65,535-entry remote list, which is not the steady state.
         fw, fs = KILL_FIRST + KILL_EVERY, args.fanout_steps
-        f_dt, _, f_fprof, f_st, f_dprof = side_run(lib, "failures", n, fw, fs, local_rank)
+        f_dt, _, f_fprof, f_st, f_dprof, _ = side_run(lib, "failures", n, fw, fs, local_rank)
         window = (f"config4-lan-failures N={n}: periods {fw}..{fw + fs} (member killed at period {fw}), "
-                  f"{n * fs / f_dt:.3g} member-periods/s, {f_st['gossip_messages']} GOSSIP_REQs sent")
-        line["roofline_fanout"] = fanout_roofline(f_fprof, window, fs == 6 and n == 65536)
-        line["roofline_deliver"] = deliver_roofline(f_dprof, window, fs == 6 and n == 65536)
-        # the timing mode whose latency distributions pass the KS test against the reference-timing
+                  f"{f_st['gossip_messages']} GOSSIP_REQs sent")
+        line["failures"] = {"value": n * fs / f_dt, "unit": "member-periods/s", "ms_per_step": f_dt / fs * 1e3,
+                            "steps": fs, "window": window,
+                            "roofline_fanout": fanout_roofline(f_fprof, window, fs == 6 and n == 65536),
+                            "roofline_deliver": deliver_roofline(f_dprof, window, fs == 6 and n == 65536)}
+        line["roofline_fanout"] = line["failures"]["roofline_fanout"]
+        line["roofline_deliver"] = line["failures"]["roofline_deliver"]
+        # (3) BASELINE config 3 (churn) at its stated N = 16,384, its first timed period
+        if not args.no_churn:
+            c_dt, _, _, c_st, _, _ = side_run(lib, "churn", DEFAULT_MEMBERS["churn"], 1, 1, local_rank)
+            line["churn"] = {"value": DEFAULT_MEMBERS["churn"] / c_dt, "unit": "member-periods/s",
+                             "ms_per_step": c_dt * 1e3, "steps": 1, "warmup": 1,
+                             "config": WORKLOAD_TEXT["churn"].format(n=DEFAULT_MEMBERS["churn"],
+                                                                     churn=DEFAULT_MEMBERS["churn"] * CHURN_PER_MILLE // 1000,
+                                                                     loss=CHURN_LOSS),
+                             "gossip_messages": c_st["gossip_messages"]}
+        # (4) the timing mode whose latency distributions pass the KS test against the reference-timing
         # DES (tests/test_ks_des.py: independent timer phases, 10 ms ticks); same quiet workload
-        k_dt, _, _, _, _ = side_run(lib, "quiet", n, 2, args.ks_steps, local_rank, timer_stagger=1, tick_ms=10)
+        k_dt, _, _, _, _, k_q = side_run(lib, "quiet", n, 2, args.ks_steps, local_rank, timer_stagger=1, tick_ms=10)
         line["ks_mode"] = {"value": n * args.ks_steps / k_dt, "unit": "member-periods/s",
                            "ms_per_step": k_dt / args.ks_steps * 1e3, "steps": args.ks_steps,
+                           "quiet_windows": k_q,
                            "config": "same workload, timer_stagger=1, tick_ms=10 (100 ticks per period)",
                            "ks": "tests/test_ks_des.py::test_ks_gpu_vs_des (N=64 and 1,024, 200 seeds, p >= 0.01)"}
     if hook is not None:

@@ -426,6 +426,14 @@ typedef struct swim_quiet_stats {
   uint64_t cut_short;  /* windows that ended before their length at a tick needing the per-tick chain */
 } swim_quiet_stats;
 int32_t swim_get_quiet_stats(const swim_engine* e, swim_quiet_stats* out);
+/* The quiet windows' kernels (k_quiet_scan .. k_quiet_apply of one window, HIP events on the engine's
+ * stream), every window while profiling is enabled (swim_profile_enable): launches = windows,
+ * messages = ticks advanced, records = member-periods advanced (rows x ticks / ticks per period),
+ * alg_bytes = 21 B per member-period (SURVEY.md §8(d) ping phase: list word, cursor, up word, view
+ * word) + per window what the quiet check reads: 4 B x blocks of witness counts and 64 B of member
+ * words per row, the reference row (4 B per subject per shard), 4 B per timer-bucket queue of the
+ * window.  The CPU oracle reports zeros. */
+int32_t swim_profile_quiet(swim_engine* e, swim_kernel_profile* out);
 
 /* ---- known-answer hooks (run the engine's own merge / dedupe code on given inputs) --------- */
 /* Philox4x32-10 block used by every draw site. */

@@ -209,6 +209,10 @@ struct swim_engine {
   uint64_t quiet_retry_at = 0;
   uint32_t quiet_backoff = 1;
   swim_quiet_stats qst{};
+  // swim_profile_quiet: HIP events around every window's kernels (scan .. apply) while profiling
+  hipEvent_t qev[2] = {nullptr, nullptr};
+  double qprof_ms = 0.0;
+  uint64_t qprof_windows = 0, qprof_ticks = 0, qprof_mp = 0, qprof_bytes = 0;
   std::vector<uint8_t> loss_h;   // host mirror of the default outbound loss per member
   uint32_t loss_nz = 0;          // members whose default loss is not 0
   uint32_t err_seen = 0;
@@ -227,6 +231,8 @@ struct swim_engine {
     if (d_cnt) hipFree(d_cnt);
     if (d_quiet) hipFree(d_quiet);
     if (d_refmm) hipFree(d_refmm);
+    for (hipEvent_t ev : qev)
+      if (ev) hipEventDestroy(ev);
     if (h_done) hipHostFree(h_done);
     if (h_par) hipHostFree(h_par);
     if (comm) ncclCommDestroy(comm);
@@ -299,12 +305,16 @@ static void launch_emit(swim_engine* e, Shard& s) {
 // the fused SYNC apply (unsharded) carries the merge profile that k_sync_classify carries otherwise
 static void launch_apply(swim_engine* e, Shard& s, int d2, int classified, int fused) {
   KProf& k = s.prof_cls;
+  if (d2) {
+    k_ack_apply<<<kApplyGrid, APPLY_BLOCK, 0, e->stream>>>(s.d_par, e->T, classified);
+    return;
+  }
   if (!fused || !k.take(e->prof)) {
-    k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, e->stream>>>(s.d_par, e->T, d2, classified, fused, nullptr);
+    k_sync_apply<<<kApplyGrid, APPLY_BLOCK, 0, e->stream>>>(s.d_par, e->T, classified, fused, nullptr);
     return;
   }
   hipExtLaunchKernelGGL(k_sync_apply, dim3(kApplyGrid), dim3(APPLY_BLOCK), 0, e->stream, k.ev[2 * k.used],
-                        k.ev[2 * k.used + 1], 0, s.d_par, e->T, d2, classified, fused, k.slots + 3 * k.used);
+                        k.ev[2 * k.used + 1], 0, s.d_par, e->T, classified, fused, k.slots + 3 * k.used);
   k.used++;
 }
 
@@ -561,7 +571,7 @@ static int32_t run_tick(swim_engine* e) {
       if (classified) launch_classify(e, sd, d2);
       TICK_CHECK("k_sync_classify");
       launch_apply(e, sd, d2, classified, fused);
-      TICK_CHECK("k_sync_apply");
+      TICK_CHECK(d2 ? "k_ack_apply" : "k_sync_apply");
       if (d2 == 0 && sd.c.delay_on) {  // delayed SYNC_ACKs: contents parked, the acks deferred
         k_ack_delay<<<256, 256, 0, s>>>(sd.d_par, T);
         TICK_CHECK("k_ack_delay");
@@ -605,6 +615,8 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
   QuietCtl* q = e->d_quiet + e->q_par;  // reset by the previous window's apply (or at creation)
   QuietCtl* q_next = e->d_quiet + (e->q_par ^ 1u);
   e->q_par ^= 1u;
+  const bool prof = e->prof && e->qev[0];
+  if (prof) hipEventRecord(e->qev[0], s);
   // the shards' witness refs must agree (k_quiet_scan): RCCL compares the ranks' elementwise min and max
   if (e->rccl) {
     const size_t n = e->n;
@@ -630,9 +642,29 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
     const uint32_t g = std::max<uint32_t>(64, grid_for(sd.c.nl, 256));
     k_quiet_apply<<<g, 256, 0, s>>>(sd.d_par, T0, K, q, q_next, e->d_done, (uint32_t)kRebaseEvery);
   }
+  if (prof) hipEventRecord(e->qev[1], s);
   if (hipStreamSynchronize(s) != hipSuccess) return SWIM_EDEVICE;
   e->par_slot = 0;  // (the stream drained: the Params staging ring restarts)
   *done = std::min(__atomic_load_n(e->h_done, __ATOMIC_ACQUIRE), K);
+  if (prof) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e->qev[0], e->qev[1]) == hipSuccess) e->qprof_ms += ms;
+    // algorithmic bytes (swim.h swim_profile_quiet): SURVEY.md §8(d)'s 21 B per member-period of the
+    // ping phase, plus what the quiet check must read once per window: every owned row's block
+    // witness counts, 64 B of per-member words, the reference row, the window's timer buckets
+    uint64_t rows = 0, blocks = 0, nq = 0;
+    for (const Shard& sd : e->sh) {
+      rows += sd.c.nl;
+      blocks = sd.c.blocks;
+      nq += sd.c.wheel_nq;
+    }
+    const uint64_t mp = rows * (uint64_t)*done / e->P;
+    e->qprof_windows++;
+    e->qprof_ticks += *done;
+    e->qprof_mp += mp;
+    e->qprof_bytes += 21ull * mp + rows * (4ull * blocks + 64ull) + 4ull * e->n * e->sh.size() +
+                      4ull * std::min<uint64_t>(K, e->sh[0].c.wheel_mask + 1ull) * nq;
+  }
   e->T += *done;
   e->host_ticks += *done;
   e->qst.attempts++;
@@ -1781,9 +1813,24 @@ int32_t swim_get_quiet_stats(const swim_engine* e, swim_quiet_stats* out) {
   return SWIM_OK;
 }
 
+int32_t swim_profile_quiet(swim_engine* e, swim_kernel_profile* out) {
+  if (!e || !out) return SWIM_EINVAL;
+  std::memset(out, 0, sizeof(*out));
+  out->launches = e->qprof_windows;
+  out->total_ms = e->qprof_ms;
+  out->messages = e->qprof_ticks;
+  out->records = e->qprof_mp;
+  out->alg_bytes = e->qprof_bytes;
+  return SWIM_OK;
+}
+
 int32_t swim_profile_enable(swim_engine* e, int32_t enable) {
   if (!e) return SWIM_EINVAL;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  for (hipEvent_t& ev : e->qev)
+    if (!ev && hipEventCreate(&ev) != hipSuccess) return SWIM_EDEVICE;
+  e->qprof_ms = 0.0;
+  e->qprof_windows = e->qprof_ticks = e->qprof_mp = e->qprof_bytes = 0;
   for (Shard& sd : e->sh) {
     for (KProf* k : {&sd.prof_cls, &sd.prof_emit, &sd.prof_dlv}) {
       if (k->ev.empty()) {

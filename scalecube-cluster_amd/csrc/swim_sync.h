@@ -837,8 +837,8 @@ __global__ void __launch_bounds__(256) k_sync_delay(KP) {
 // classified in-workgroup (merge_row_wg) otherwise.
 // fused = 1 (unsharded SYNC sub-phase): no k_sync_classify launch, every message is classified in
 // the receiver's workgroup with the block witness (sync_msg_wg); prof as k_sync_classify's.
-__global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int classified, int fused,
-                                                            unsigned long long* prof) {
+__device__ __forceinline__ void sync_apply_body(const Params* __restrict__ P, uint64_t T, int d2, int classified,
+                                                int fused, unsigned long long* prof) {
   const Ctx c = pctx_sync(P, T);
   const Bufs b = P->b;
   __shared__ uint32_t s_need[NEED_WORDS];
@@ -1041,4 +1041,13 @@ __global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int d2, int clas
     // when no merge changed the row and none were pending)
     if (s_mod || ins0) apply_ins_batch<APPLY_BLOCK, true>(c, s, threadIdx.x, s_iP, s_iS, s_iR);
   }
+}
+
+// the two sub-phases as two kernel symbols, so that a kernel trace times the SYNC merge (k_sync_apply)
+// and the SYNC_ACK merge (k_ack_apply) separately, as the engine's HIP-event samples do
+__global__ void __launch_bounds__(APPLY_BLOCK) k_sync_apply(KP, int classified, int fused, unsigned long long* prof) {
+  sync_apply_body(P, T, 0, classified, fused, prof);
+}
+__global__ void __launch_bounds__(APPLY_BLOCK) k_ack_apply(KP, int classified) {
+  sync_apply_body(P, T, 1, classified, 0, nullptr);
 }

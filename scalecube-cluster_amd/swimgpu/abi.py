@@ -209,6 +209,7 @@ PROTOTYPES = {
     "swim_profile_merge": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_profile_fanout": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_profile_deliver": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
+    "swim_profile_quiet": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_set_quiet_path": (C.c_int32, [_engp, C.c_int32]),
     "swim_get_quiet_stats": (C.c_int32, [_engp, POINTER(swim_quiet_stats)]),
     "swim_philox": (C.c_int32, [_u32p, _u32p, _u32p]),
@@ -456,6 +457,12 @@ class Engine:
         q = swim_quiet_stats()
         _check("swim_get_quiet_stats", self.lib.swim_get_quiet_stats(self._h, byref(q)))
         return {name: getattr(q, name) for name, _ in swim_quiet_stats._fields_}
+
+    def profile_quiet(self) -> dict:
+        """HIP-event timing of the quiet windows' kernels (k_quiet_scan .. k_quiet_apply), see swim.h."""
+        p = swim_kernel_profile()
+        _check("swim_profile_quiet", self.lib.swim_profile_quiet(self._h, byref(p)))
+        return {name: getattr(p, name) for name, _ in swim_kernel_profile._fields_}
 
     def read_collector(self, m: int, gossiper: int) -> list[tuple[int, int]]:
         ln = C.c_uint32()
