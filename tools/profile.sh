@@ -14,6 +14,6 @@ mkdir -p gpurun_out/prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof/${tag}_stats -o run \
   -- python3 bench.py --workload "$wl" --steps "$steps" --warmup "$warm" --no-cpu-baseline --no-extras > gpurun_out/prof/${tag}_stats.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d gpurun_out/prof/${tag}_fetch -o run \
-  -- python3 bench.py --workload "$wl" --steps "${PMC_STEPS:-4}" --warmup "$warm" --no-cpu-baseline --no-extras > gpurun_out/prof/${tag}_fetch.log 2>&1
+  -- python3 bench.py --workload "$wl" --steps "${PMC_STEPS:-$steps}" --warmup "$warm" --no-cpu-baseline --no-extras > gpurun_out/prof/${tag}_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d gpurun_out/prof/${tag}_write -o run \
-  -- python3 bench.py --workload "$wl" --steps "${PMC_STEPS:-4}" --warmup "$warm" --no-cpu-baseline --no-extras > gpurun_out/prof/${tag}_write.log 2>&1
+  -- python3 bench.py --workload "$wl" --steps "${PMC_STEPS:-$steps}" --warmup "$warm" --no-cpu-baseline --no-extras > gpurun_out/prof/${tag}_write.log 2>&1
