@@ -435,6 +435,11 @@ int32_t swim_get_quiet_stats(const swim_engine* e, swim_quiet_stats* out);
  * window.  The CPU oracle reports zeros. */
 int32_t swim_profile_quiet(swim_engine* e, swim_kernel_profile* out);
 
+/* Profiling builds (-DSWIM_PHASE_PROF, tools/phase_prof.sh) only: per-phase wall-time sums of the
+ * instrumented kernels (100 MHz ticks); reset = 1 zeroes them.  The product build and the CPU
+ * oracle report zeros. */
+int32_t swim_debug_counters(uint64_t* out, uint32_t n, int32_t reset);
+
 /* ---- known-answer hooks (run the engine's own merge / dedupe code on given inputs) --------- */
 /* Philox4x32-10 block used by every draw site. */
 int32_t swim_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

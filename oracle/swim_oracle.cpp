@@ -1222,6 +1222,11 @@ int32_t swim_profile_enable(swim_engine* e, int32_t) { return e ? SWIM_OK : SWIM
 // the GPU engine's quiet-window fast path has no counterpart here: the oracle runs every tick
 int32_t swim_set_quiet_path(swim_engine* e, int32_t) { return e ? SWIM_OK : SWIM_EINVAL; }
 int32_t swim_profile_quiet(swim_engine* e, swim_kernel_profile* out) { return swim_profile_merge(e, out); }
+int32_t swim_debug_counters(uint64_t* out, uint32_t n, int32_t) {
+  if (!out || n > 16) return SWIM_EINVAL;
+  std::memset(out, 0, 8ull * n);
+  return SWIM_OK;
+}
 int32_t swim_get_quiet_stats(const swim_engine* e, swim_quiet_stats* out) {
   if (!e || !out) return SWIM_EINVAL;
   std::memset(out, 0, sizeof(*out));

@@ -1901,6 +1901,21 @@ int32_t swim_profile_deliver(swim_engine* e, swim_kernel_profile* out) {
   return SWIM_OK;
 }
 
+// profiling builds (-DSWIM_PHASE_PROF): the per-phase wall-time sums of the instrumented kernels
+// (swim_phases.h g_dbg); reset = 1 zeroes them after the read.  Zeros in the product build.
+int32_t swim_debug_counters(uint64_t* out, uint32_t n, int32_t reset) {
+  if (!out || n > 16) return SWIM_EINVAL;
+  unsigned long long h[16] = {};
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dbg), sizeof h) != hipSuccess)
+    return SWIM_EDEVICE;
+  for (uint32_t i = 0; i < n; ++i) out[i] = h[i];
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof z) != hipSuccess) return SWIM_EDEVICE;
+  }
+  return SWIM_OK;
+}
+
 // ---- KAT hooks: run the device code paths on given inputs
 int32_t swim_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
   if (!ctr || !key || !out) return SWIM_EINVAL;

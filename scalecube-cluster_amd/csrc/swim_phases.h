@@ -15,6 +15,26 @@
 
 namespace swimdev {
 
+// Phase timing for profiling builds only (-DSWIM_PHASE_PROF, tools/phase_prof.sh): per-wave wall
+// time (s_memrealtime, 100 MHz) of the delivery kernel's parts, summed into g_dbg; read with
+// swim_debug_counters.  The product build compiles none of it.
+__device__ unsigned long long g_dbg[16];
+#ifdef SWIM_PHASE_PROF
+#define PPROF_T0(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#define PPROF_ADD(slot, t0)                                                                          \
+  do {                                                                                               \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_dbg[slot], __builtin_amdgcn_s_memrealtime() - (t0)); \
+  } while (0)
+#define PPROF_CNT(slot, val)                                     \
+  do {                                                           \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_dbg[slot], (val)); \
+  } while (0)
+#else
+#define PPROF_T0(v)
+#define PPROF_ADD(slot, t0)
+#define PPROF_CNT(slot, val)
+#endif
+
 // per-tick scratch counters, zeroed by one hipMemsetAsync at the start of every tick
 struct Counters {
   uint32_t msg_total, pg_cursor, park_jobs;  // messages materialised this round; inbox pages taken; SYNC rows to park
@@ -1463,6 +1483,9 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
                                                 unsigned long long& nsync, uint32_t& nmsg, uint32_t& nfresh) {
   // 1. rank every inbox of the batch; lane j keeps receiver j's message count (0: nothing to
   //    deliver) and the count of inbox pages to hand back
+  PPROF_T0(tp0);
+  PPROF_CNT(4, 1ull);
+  PPROF_CNT(5, (unsigned long long)nb);
   uint32_t my_k = 0, my_pages = 0;
   for (uint32_t j = 0; j < nb; ++j) {
     const uint32_t i = list[j];
@@ -1485,6 +1508,8 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     }
   }
   wave_sync();
+  PPROF_ADD(0, tp0);
+  PPROF_T0(tp1);
   // 2. the onGossipReq chains, lane j for receiver j
   unsigned long long acc = 0;
   if (lane < nb && my_k) {
@@ -1520,6 +1545,8 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     if (sink == 0x5bd1e995u && my_k == 0x7fffffffu) set_err(c, 0u);  // keeps the warming loads; sets no bit
   }
   wave_sync();
+  PPROF_ADD(1, tp1);
+  PPROF_T0(tp2);
   // 3. per receiver: the inbox pages go back to the pool (the pool itself restarts every tick),
   //    the phase's pingMembers inserts, phase D's SYNC collection
   for (uint32_t j = 0; j < nb; ++j) {
@@ -1529,6 +1556,7 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     apply_ins_batch<64, false>(c, r, lane, L.iP, L.iS, L.iR);
     if (lane == 0 && collect) nsync += sync_collect_member(cs, b, r);
   }
+  PPROF_ADD(2, tp2);
   return acc;
 }
 
@@ -1571,6 +1599,7 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect, u
       acc += deliver_big_batch(c, cs, b, b.big_list + x, min(bsz, nbig - x), lane, collect, s_big[wv], nsync, nmsg,
                                nfresh);
   }
+  PPROF_T0(tp3);
   for (uint32_t base = blockIdx.x * DLV_BLOCK; base < c.nl; base += gridDim.x * DLV_BLOCK) {
     if (tid == 0) s_nins = 0;
     __syncthreads();
@@ -1615,6 +1644,7 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect, u
     if (collect && i < c.nl && !big)
       nsync += i == i_first ? sync_collect_pre(cs, b, c.lo + i, sn_first, fl_first) : sync_collect_member(cs, b, c.lo + i);
   }
+  PPROF_ADD(3, tp3);
   wave_stat_add(c, ST_GOSSIP_ACCEPTED, acc);
   wave_stat_add(cs, ST_SYNCS, nsync);
   if (prof) {

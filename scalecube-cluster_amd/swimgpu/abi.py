@@ -211,6 +211,7 @@ PROTOTYPES = {
     "swim_profile_deliver": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_profile_quiet": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_set_quiet_path": (C.c_int32, [_engp, C.c_int32]),
+    "swim_debug_counters": (C.c_int32, [_u64p, C.c_uint32, C.c_int32]),
     "swim_get_quiet_stats": (C.c_int32, [_engp, POINTER(swim_quiet_stats)]),
     "swim_philox": (C.c_int32, [_u32p, _u32p, _u32p]),
     "swim_kat_overrides": (C.c_int32, [POINTER(C.c_int32), C.c_uint32, POINTER(C.c_uint8)]),
@@ -532,3 +533,10 @@ def cell_has_timer(c):
 
 def cell_deadline(c):
     return (np.asarray(c, dtype=np.uint64) >> np.uint64(39)).astype(np.uint32)
+
+
+def debug_counters(lib, n: int = 16, reset: bool = False) -> list[int]:
+    """swim_debug_counters: phase-timing sums of a profiling build (zeros otherwise)."""
+    out = (C.c_uint64 * n)()
+    _check("swim_debug_counters", lib.swim_debug_counters(out, n, 1 if reset else 0))
+    return list(out)

@@ -1,0 +1,59 @@
+"""Phase times of k_gossip_deliver over the failures window (bench.py's fanout side run: periods
+30..36 after the second kill), from the profiling build (tools/phase_prof.sh):
+
+    SWIMGPU_LIB=tools/libswimgpu_prof.so python tools/deliver_phases.py [--workload failures]
+
+g_dbg slots: 0 big-inbox ranking, 1 big-inbox onGossipReq chains, 2 big-inbox tail (page reset,
+pingMembers inserts, SYNC collection), 3 small inboxes + their collection (every wave), 4 batches,
+5 big inboxes.  Times are per-wave sums (100 MHz ticks); divided by the waves of a launch they give
+each part's share of a launch."""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "scalecube-cluster_amd"))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="failures")
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--members", type=int, default=65536)
+    args = ap.parse_args()
+    import torch
+    import swimgpu
+    from swimgpu import abi
+    import bench
+    lib = swimgpu.load_library()
+    sch = bench.Schedule(args.workload, args.members, args.warmup + args.steps)
+    cfg = bench.make_config(lib)
+    if args.workload == "churn":
+        bench.churn_capacities(cfg, sch.capacity)
+    e = abi.Engine(lib, cfg, sch.capacity, args.members, 1)
+    sch.setup(e)
+    sch.run(e, 0, args.warmup)
+    torch.cuda.synchronize()
+    abi.debug_counters(lib, reset=True)
+    e.profile_enable(True)
+    t0 = time.perf_counter()
+    sch.run(e, args.warmup, args.warmup + args.steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    d = abi.debug_counters(lib)
+    dp = e.profile_deliver()
+    launches = args.steps * 5  # gossip rounds in the window
+    waves = 512 * 4  # DLV_GRID x DLV_WAVES
+    per = lambda x: x / 100.0 / waves / launches  # us of an average wave per launch
+    print(json.dumps({"workload": args.workload, "window_s": dt, "deliver_ms_per_launch": dp["total_ms"] / max(1, dp["launches"]),
+                      "big_rank_us": per(d[0]), "big_chain_us": per(d[1]), "big_tail_us": per(d[2]),
+                      "small_and_collect_us": per(d[3]), "batches": d[4], "big_inboxes": d[5],
+                      "messages_per_launch": dp["messages"] / max(1, dp["launches"])}))
+
+
+if __name__ == "__main__":
+    main()
