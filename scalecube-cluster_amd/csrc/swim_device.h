@@ -624,6 +624,41 @@ __device__ inline bool coll_contains(const Ctx& c, const CollEnt* e, uint32_t x)
   const int f = coll_floor(iv, blk[0], x);
   return f >= 0 && x <= iv[f].y;
 }
+// coll_contains on an entry already loaded (by value): the inline interval, else the spilled block
+__device__ inline bool coll_contains_v(const Ctx& c, const CollEnt& e, uint32_t x) {
+  const uint32_t n = e.meta & 7u;
+  if (n == 1) return e.lo <= x && x <= e.hi;
+  if (n != COLL_SPILLED) return false;
+  const uint32_t* blk = coll_block(c, e.meta);
+  const uint2* iv = reinterpret_cast<const uint2*>(blk + 4);
+  const int f = coll_floor(iv, blk[0], x);
+  return f >= 0 && x <= iv[f].y;
+}
+// "does receiver t's collector of `gossiper` hold seq?" for up to four receivers t at once (all owned):
+// the first probe of each is loaded in one batch (the hash slot depends on the gossiper only), the
+// rare continued probes and spilled blocks follow.  Bit q of the result: receiver tg[q] holds it
+// (only bits set in `need` are examined).
+__device__ inline uint32_t coll_known4(const Ctx& c, const uint32_t* tg, uint32_t need, uint32_t gossiper,
+                                       uint32_t seq) {
+  const uint32_t mask = c.hcap - 1, h = hash32(gossiper) & mask, key = gossiper + 1;
+  CollEnt e[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if ((need >> q) & 1u) e[q] = c.coll[(size_t)(tg[q] - c.lo) * c.hcap + h];
+  uint32_t known = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (!((need >> q) & 1u)) continue;
+    if (e[q].key != key) {
+      if (e[q].key == 0) continue;  // not in the table: nothing received from this gossiper
+      const CollEnt* f = coll_find(c, tg[q], gossiper);
+      if (!f) continue;
+      e[q] = *f;
+    }
+    known |= coll_contains_v(c, e[q], seq) ? 1u << q : 0u;
+  }
+  return known;
+}
 // SequenceIdCollector.add (SequenceIdCollector.java:43-72).  `seg` (the viewer's segmentation flag)
 // is raised when the collector ends up with more than c.seg_threshold intervals.
 __device__ inline bool coll_add(const Ctx& c, CollEnt* e, uint32_t x, uint32_t* seg = nullptr) {

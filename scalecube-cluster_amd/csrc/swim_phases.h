@@ -772,6 +772,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         return (win && jj < nt) ? c.gbits[(size_t)sl * c.gwords + (i >> 5)] : 0u;
       };
       const uint32_t wb0 = rword(0), wb1 = rword(1), wb2 = rword(2), wb3 = rword(3);
+      uint32_t probe = 0;  // bit j: target j's collector must be probed (its receipt bit does not answer)
       for (uint32_t j = 0; j < nt; ++j) {
         const uint32_t t = s_t[1 + j], tm = s_t[17 + j];
         bool infected = h.inf0 == tm;
@@ -805,15 +806,23 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         if (mat && owned(c, t)) {
           // exact: does t's collector hold (gossiper, seq)?  The receipt bit answers without the
           // collector probe when it is set and trustworthy (set after the slot's claim, and no
-          // collector of t was cleared since the claim)
+          // collector of t was cleared since the claim); else the collector is probed below, the
+          // targets' probes in one batch
           const uint32_t i = t - c.lo;
           const uint32_t word = j == 0 ? wb0 : j == 1 ? wb1 : j == 2 ? wb2 : j == 3 ? wb3
                                                  : c.gbits[(size_t)sl * c.gwords + (i >> 5)];
-          bool known = gs_ok && s_t[82 + j] < gs.tick && ((word >> (i & 31)) & 1u);
-          if (!known) known = coll_contains(c, coll_find(c, t, h.gossiper), h.seq);
-          mat = !known;
+          const bool known = gs_ok && s_t[82 + j] < gs.tick && ((word >> (i & 31)) & 1u);
+          if (known) mat = false;
+          else probe |= 1u << j;
         }
         matb |= (mat ? 1u : 0u) << j;
+      }
+      for (uint32_t j0 = 0; probe >> j0; j0 += 4) {  // the collector probes, four targets at a time
+        const uint32_t need = (probe >> j0) & 0xfu;
+        if (!need) continue;
+        const uint32_t tg4[4] = {s_t[1 + min(j0, nt - 1)], s_t[1 + min(j0 + 1, nt - 1)], s_t[1 + min(j0 + 2, nt - 1)],
+                                 s_t[1 + min(j0 + 3, nt - 1)]};
+        matb &= ~(coll_known4(c, tg4, need, h.gossiper, h.seq) << j0);
       }
       if (s_t[49]) {
         // two targets at one address: their copies of this gossip are the same message to the same
@@ -1547,15 +1556,17 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
   wave_sync();
   PPROF_ADD(1, tp1);
   PPROF_T0(tp2);
-  // 3. per receiver: the inbox pages go back to the pool (the pool itself restarts every tick),
-  //    the phase's pingMembers inserts, phase D's SYNC collection
+  // 3. per receiver: the inbox pages go back to the pool (the pool itself restarts every tick) and
+  //    the phase's pingMembers inserts run (wave-cooperative, receiver by receiver); then phase D's
+  //    SYNC collection of the batch's receivers, lane j for receiver j (member-local, as in the
+  //    small-inbox path: each reads only its own lists, schedule and FD-SYNC queue)
   for (uint32_t j = 0; j < nb; ++j) {
     const uint32_t i = list[j], r = c.lo + i;
     const uint32_t np = __shfl(my_pages, (int)j, 64);
     for (uint32_t pg = lane; pg < np; pg += 64) b.pg_tab[(size_t)i * b.pg_max + pg] = NONE;
     apply_ins_batch<64, false>(c, r, lane, L.iP, L.iS, L.iR);
-    if (lane == 0 && collect) nsync += sync_collect_member(cs, b, r);
   }
+  if (lane < nb && collect) nsync += sync_collect_member(cs, b, c.lo + list[lane]);
   PPROF_ADD(2, tp2);
   return acc;
 }
