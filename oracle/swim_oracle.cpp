@@ -148,10 +148,13 @@ struct Member {
   bool ack_ok = false;    // ack_due is the tick the (delayed) ack arrives, not the timeout
   bool ack_gone = false;  // that ack says DEST_GONE (another member answers at the target's address)
   uint32_t ack_late = 0;  // 1 + ticks after the timeout that a late direct ack arrives (0 = none)
+  uint64_t ack_to = 0;    // the ping's timeout tick (an ack dropped on arrival leaves the ping waiting)
   uint32_t relay_target = NONE, relay_pending = 0;
   uint64_t relay_due = 0;
   bool relay_ok = false;  // relay_due is the tick the first relayed ack arrives, not the timeout
   bool relay_gone = false;  // that ack says DEST_GONE
+  uint32_t relay_first = NONE;  // the member that sent that ack (the issuer's inbound filter, on arrival)
+  uint64_t relay_to = 0;  // the relay requests' timeout tick
   uint32_t join_addr = NONE;  // swim_join_at: the member whose address this joiner binds
   // ---- GossipProtocolImpl (:48-55)
   uint64_t g_period = 0, g_counter = 0, period_used = 0;
@@ -683,7 +686,9 @@ struct swim_engine {
   // ack (ties: lowest relay), or a late ack of the direct ping (`late` = 1 + its arrival in ticks
   // after the ping-req went out, 0 = none; it carries the same cid and arrives after the relay
   // requests subscribed), and only if the issuer's inbound filter passes its sender
-  // (NetworkEmulatorTransport.requestResponse :65-74); none before pingInterval - pingTimeout: SUSPECT.
+  // (NetworkEmulatorTransport.requestResponse :65-74, applied when that message ARRIVES: each
+  // requestResponse takes the first message with its cid and drops it there if the filter blocks it,
+  // so a blocked first ack completes none of them); none before pingInterval - pingTimeout: SUSPECT.
   // Every message goes to an address (dst): a relay's transit ping reaches whoever listens at t's
   // address, and that member's onPing answers DEST_GONE when it is not t (:227-259), which every
   // ack carries back (onTransitPingAck :291-315) and computeMemberStatus turns into DEAD (:382-404).
@@ -720,14 +725,16 @@ struct swim_engine {
     }
     if (late && late - 1 < best) { best = late - 1; first = d; first_gone = late_gone; }
     Member& mv = m[v];
-    if (first != NONE && best < relay_ticks && in_pass(v, first)) {
+    if (first != NONE && best < relay_ticks && (best > 0 || in_pass(v, first))) {
       if (best == 0) {
         for (size_t i = 0; i < pending.size(); ++i) publish_fd(v, t, first_gone ? SWIM_DEAD : SWIM_ALIVE);
         return;
       }
-      mv.relay_due = T + best;  // the acks complete every pending relay request then
+      mv.relay_due = T + best;  // the first ack arrives then (its inbound filter is applied then)
       mv.relay_ok = true;
       mv.relay_gone = first_gone;
+      mv.relay_first = first;
+      mv.relay_to = T + relay_ticks;
     } else {
       mv.relay_due = T + relay_ticks;
       mv.relay_ok = false;
@@ -754,11 +761,22 @@ struct swim_engine {
       Member& mv = m[v];
       if (!mv.up) continue;
       mv.ev_minor = 0;
+      if (mv.relay_due == T && mv.relay_ok && !in_pass(v, mv.relay_first)) {
+        // the first relayed ack arrives and the inbound filter drops it: no pending relay request
+        // completes, they time out (NetworkEmulatorTransport.requestResponse :72-74)
+        mv.relay_ok = false;
+        mv.relay_due = mv.relay_to;
+      }
       if (mv.relay_due == T) {  // relayed acks arrive (:190-199) or the relay timeouts (:200-209)
         uint32_t t = mv.relay_target, k = mv.relay_pending;
         mv.relay_due = 0;
         const uint32_t ok_status = mv.relay_gone ? SWIM_DEAD : SWIM_ALIVE;
         for (uint32_t i = 0; i < k; ++i) publish_fd(v, t, mv.relay_ok ? ok_status : SWIM_SUSPECT);
+      }
+      if (mv.ack_due == T && mv.ack_ok && !in_pass(v, dst(mv.ack_target))) {
+        // the delayed ack arrives and the inbound filter drops it: the ping waits for its timeout
+        mv.ack_ok = false;
+        mv.ack_due = mv.ack_to;
       }
       if (mv.ack_due == T) {  // the delayed ack arrives, or pingTimeout elapsed (:153-170)
         uint32_t t = mv.ack_target;
@@ -785,9 +803,11 @@ struct swim_engine {
           if (acked && rtt == 0 && in_pass(v, d)) {
             publish_fd(v, t, mv.ack_gone ? SWIM_DEAD : SWIM_ALIVE);
           } else {
+            // a delayed ack meets the issuer's inbound filter when it arrives (phase above)
             mv.ack_target = t;
-            mv.ack_ok = acked && rtt < to_ticks && in_pass(v, d);
+            mv.ack_ok = acked && rtt > 0 && rtt < to_ticks;
             mv.ack_due = T + (mv.ack_ok ? rtt : to_ticks);
+            mv.ack_to = T + to_ticks;
             mv.ack_late = acked && rtt >= to_ticks ? rtt - to_ticks + 1 : 0;
           }
         }
@@ -868,10 +888,11 @@ struct swim_engine {
             if (g.is_infected(tg)) continue;
             STT().gossip_messages++;
             if (out_fail(v, rc, draw(v, SWIM_STREAM_GOSSIP_OUT, j, p))) continue;
-            if (!in_pass(rc, v)) continue;
+            // the receiver's inbound filter applies when the message arrives (listen() :78-83): now,
+            // or at the delayed message's arrival tick
             const uint32_t k = delay_ticks(v, rc, v, SWIM_STREAM_GOSSIP_DELAY, j, p);
             if (k) later[t].push_back(GMsg{rc, v, p, g, T + k});
-            else bucket[t][consumer(rc)].push_back(GMsg{rc, v, p, g, T});
+            else if (in_pass(rc, v)) bucket[t][consumer(rc)].push_back(GMsg{rc, v, p, g, T});
           }
         }
         // sweep (:158-164, :350-358)
@@ -899,7 +920,8 @@ struct swim_engine {
         x.sent = T;
         gossip_in_flight[at].push_back(std::move(x));
       }
-    for (auto& x : arriving) bucket[0][consumer(x.to)].push_back(std::move(x));
+    for (auto& x : arriving)  // delayed GOSSIP_REQs arriving now: the receiver's inbound filter now
+      if (in_pass(x.to, x.from)) bucket[0][consumer(x.to)].push_back(std::move(x));
     for (auto& bp : bucket)
       for (auto& bc : bp) any |= !bc.empty();
     if (!any) return;
@@ -1066,21 +1088,32 @@ struct swim_engine {
       Member& mf = m[q.from];
       STT().syncs++;
       if (q.initial) mf.init_total++;
-      if (out_fail(q.from, q.to, draw(q.from, SWIM_STREAM_SYNC_OUT, q.ordinal, 0))) {
+      // tryFailOutbound (loss) now; the transport's send after tryDelayOutbound meets the receiver
+      // — stopped (an error), or its inbound filter — when the message arrives
+      // (NetworkEmulatorTransport.send / requestResponse :49-75)
+      const uint32_t k = lost(out_loss(q.from, q.to), draw(q.from, SWIM_STREAM_SYNC_OUT, q.ordinal, 0))
+                             ? 0u : delay_ticks(q.from, q.to, q.from, SWIM_STREAM_SYNC_DELAY, q.ordinal, 0);
+      if (k == 0 && out_fail(q.from, q.to, draw(q.from, SWIM_STREAM_SYNC_OUT, q.ordinal, 0))) {
         q.outfail = true;
         if (q.initial) mf.init_done++;  // an error resumes empty: that source completes now
         continue;
       }
+      if (k) {
+        sync_in_flight[T + k].push_back(SyncFlight{q.to, q.from, q.ordinal, T, q.initial, false, content_of(q.from)});
+        continue;
+      }
       if (!in_pass(q.to, q.from)) continue;
       q.delivered = true;
-      const uint32_t k = delay_ticks(q.from, q.to, q.from, SWIM_STREAM_SYNC_DELAY, q.ordinal, 0);
-      if (k) sync_in_flight[T + k].push_back(SyncFlight{q.to, q.from, q.ordinal, T, q.initial, false, content_of(q.from)});
-      else in.push_back(SyncArr{q.to, q.from, q.ordinal, T, q.initial, &content_of(q.from)});
+      in.push_back(SyncArr{q.to, q.from, q.ordinal, T, q.initial, &content_of(q.from)});
     }
     std::vector<SyncFlight*> ack_arriving;
     for (auto& f : arriving) {
       if (f.ack) { ack_arriving.push_back(&f); continue; }
-      if (!m[f.to].up) continue;  // the receiver stopped while the message was in flight
+      if (!m[f.to].up) {  // the receiver stopped: the transport's send fails now
+        if (f.initial && m[f.from].up) m[f.from].init_done++;  // that start0 source completes (an error)
+        continue;
+      }
+      if (!in_pass(f.to, f.from)) continue;  // dropped by the receiver's inbound filter on arrival
       in.push_back(SyncArr{f.to, f.from, f.ordinal, f.sent, f.initial, &f.content});
     }
     sort_arrivals(in);
@@ -1109,15 +1142,19 @@ struct swim_engine {
       for (size_t i = gs[g]; i < gs[g + 1]; ++i) {
         const SyncArr& q = in[i];
         const uint32_t qr = (uint32_t)(i - gs[g]);
-        if (out_fail(q.to, q.from, draw(q.to, SWIM_STREAM_SYNCACK_OUT, qr, 0))) continue;
-        if (!in_pass(q.from, q.to)) continue;
+        if (lost(out_loss(q.to, q.from), draw(q.to, SWIM_STREAM_SYNCACK_OUT, qr, 0))) continue;
         const uint32_t k = delay_ticks(q.to, q.from, q.to, SWIM_STREAM_SYNCACK_DELAY, qr, 0);
-        if (k) sync_in_flight[T + k].push_back(SyncFlight{q.from, q.to, qr, T, q.initial, true, arows[g]});
-        else acks.push_back(SyncArr{q.from, q.to, qr, T, q.initial, &arows[g]});
+        if (k) {  // the receiver's state and inbound filter when it arrives
+          sync_in_flight[T + k].push_back(SyncFlight{q.from, q.to, qr, T, q.initial, true, arows[g]});
+          continue;
+        }
+        if (!m[q.from].up || !in_pass(q.from, q.to)) continue;
+        acks.push_back(SyncArr{q.from, q.to, qr, T, q.initial, &arows[g]});
       }
     }
     for (SyncFlight* f : ack_arriving)
-      if (m[f->to].up) acks.push_back(SyncArr{f->to, f->from, f->ordinal, f->sent, f->initial, &f->content});
+      if (m[f->to].up && in_pass(f->to, f->from))
+        acks.push_back(SyncArr{f->to, f->from, f->ordinal, f->sent, f->initial, &f->content});
     sort_arrivals(acks);
     std::vector<size_t> as;
     for (size_t i = 0; i < acks.size(); ++i)
@@ -1160,7 +1197,7 @@ struct swim_engine {
       if (!mv.init_wait) continue;
       int64_t start;
       if (!delayed) start = (int64_t)T + (mv.init_done == mv.init_total ? 0 : (int64_t)sync_to_ticks);
-      else if (mv.init_done == mv.init_total) start = (int64_t)mv.init_last;
+      else if (mv.init_done == mv.init_total) start = (int64_t)T;  // the last source completed now
       else if (T + 1 >= mv.init_last + sync_to_ticks) start = (int64_t)(mv.init_last + sync_to_ticks);
       else continue;
       mv.sync_on = true;

@@ -79,6 +79,9 @@ struct alignas(16) MemberDev {
   uint32_t ins_rank, ins_head, ins_tail;  // this phase's deferred pingMembers inserts (op chain)
   uint32_t gix_base, gix_used;  // serial of slab[0]; gix slots taken since the index was (re)built
   uint32_t ack_late;  // 1 + ticks after the ping timeout that a late direct ack arrives (0 = none)
+  uint64_t ack_to, relay_to;  // the ping's / the relay requests' timeout tick (an ack the inbound
+                              // filter drops on arrival leaves them waiting until then)
+  uint32_t relay_first;       // the sender of the first relayed ack (filtered when it arrives)
   uint32_t init_last;  // start0's initial sync: tick of the last answer (or of the start)
   uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, gix_valid;
   uint8_t ack_ok;    // ack_due is the tick the (delayed) ack arrives, not the ping timeout

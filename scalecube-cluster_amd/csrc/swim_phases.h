@@ -500,14 +500,18 @@ __device__ inline void ping_req(const Ctx& c, uint32_t v, uint32_t t, unsigned l
   }
   if (late && late - 1 < best) { best = late - 1; first = d; first_gone = late_gone; }
   MemberDev& m = mem(c, v);
-  if (first != NONE && best < c.relay_ticks && in_pass(c, v, first)) {
+  // the issuer's inbound filter meets the first ack when it arrives (NetworkEmulatorTransport
+  // .requestResponse :72-74): now, or at relay_due (fd_member)
+  if (first != NONE && best < c.relay_ticks && (best > 0 || in_pass(c, v, first))) {
     if (best == 0) {
       for (uint32_t i = 0; i < npend; ++i) publish_fd(c, v, t, first_gone ? SWIM_DEAD : SWIM_ALIVE, nev);
       return;
     }
-    m.relay_due = c.T + best;  // the acks complete every pending relay request then
+    m.relay_due = c.T + best;  // the first ack arrives then and completes every pending relay request
     m.relay_ok = 1;
     m.relay_gone = first_gone ? 1 : 0;
+    m.relay_first = first;
+    m.relay_to = c.T + c.relay_ticks;
   } else {
     m.relay_due = c.T + c.relay_ticks;
     m.relay_ok = 0;
@@ -524,6 +528,16 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
   c.fd_next[v - c.lo] = fd_next_of(c, m, c.T);  // ack / relay timeouts set below are > T
   if (!due && m.relay_due != c.T && m.ack_due != c.T) return;
   m.ev_minor = 0;
+  if (m.relay_due == c.T && m.relay_ok && !in_pass(c, v, m.relay_first)) {
+    // the first relayed ack arrives and the inbound filter drops it: no pending relay request
+    // completes (each took the first message with the cid), they time out
+    m.relay_ok = 0;
+    m.relay_due = m.relay_to;
+  }
+  if (m.ack_due == c.T && m.ack_ok && !in_pass(c, v, dst(c, m.ack_target))) {
+    m.ack_ok = 0;  // the delayed ack is dropped on arrival: the ping waits for its timeout
+    m.ack_due = m.ack_to;
+  }
   if (m.relay_due == c.T) {  // relayed acks arrive (:190-199) or the relay timeouts (:200-209)
     uint32_t t = m.relay_target, k = m.relay_pending;
     m.relay_due = 0;
@@ -560,9 +574,11 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
         if (acked && rtt == 0 && in_pass(c, v, d)) {
           publish_fd(c, v, t, d != t ? SWIM_DEAD : SWIM_ALIVE, nev);
         } else {
+          // a delayed ack meets the issuer's inbound filter when it arrives (above)
           m.ack_target = t;
-          m.ack_ok = acked && rtt < c.to_ticks && in_pass(c, v, d);
+          m.ack_ok = acked && rtt > 0 && rtt < c.to_ticks;
           m.ack_due = c.T + (m.ack_ok ? rtt : c.to_ticks);
+          m.ack_to = c.T + c.to_ticks;
           m.ack_late = acked && rtt >= c.to_ticks ? rtt - c.to_ticks + 1 : 0;
         }
       }
@@ -685,12 +701,12 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   wave_order();
   const uint32_t nt = s_t[0];
   // what depends on the target only, once per round instead of once per (target, gossip): whether
-  // it is up and its inbound filter passes v (s_t[50 + j]), v's outbound loss towards it
-  // (s_t[66 + j]), the tick its collectors were last cleared (s_t[82 + j]; receipt bits older than
-  // that are void)
+  // it is up (s_t[50 + j]; bit 1: its inbound filter passes v now — a delayed message meets the filter
+  // when it arrives, k_dq_release), v's outbound loss towards it (s_t[66 + j]), the tick its
+  // collectors were last cleared (s_t[82 + j]; receipt bits older than that are void)
   if (lane < nt) {
     const uint32_t t = s_t[1 + lane];
-    s_t[50 + lane] = (c.up[t] && in_pass(c, t, v)) ? 1u : 0u;
+    s_t[50 + lane] = (c.up[t] ? 1u : 0u) | (in_pass(c, t, v) ? 2u : 0u);
     s_t[66 + lane] = (uint32_t)out_loss(c, v, t);
     s_t[82 + lane] = owned(c, t) ? c.clr_tick[t - c.lo] : 0xffffffffu;
   }
@@ -785,10 +801,11 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         nmsg += send ? 1u : 0u;
         // delivered copies; a receiver on this shard that already holds the sequence id drops it
         // (its collector only grows until delivery), another shard flags it on arrival
-        bool mat = send && s_t[50 + j] && !lost_k(c, (int32_t)s_t[66 + j], v, SWIM_STREAM_GOSSIP_OUT, j, p);
+        bool mat = send && (s_t[50 + j] & 1u) && !lost_k(c, (int32_t)s_t[66 + j], v, SWIM_STREAM_GOSSIP_OUT, j, p);
         // a delayed copy waits in the arrival tick's bucket (delivered whatever the receiver's
-        // collector holds by then: a clear may come in between)
+        // collector holds by then: a clear may come in between; its inbound filter applies then)
         const uint32_t k = mat ? delay_ticks(c, v, t, v, SWIM_STREAM_GOSSIP_DELAY, j, p) : 0u;
+        if (!k && !(s_t[50 + j] & 2u)) mat = false;  // dropped by the receiver's inbound filter now
         if (k) {
           mat = false;
           load_cold();
@@ -1072,6 +1089,11 @@ __global__ void __launch_bounds__(256) k_dq_release(KP) {
     uint32_t age = 0;
     if (valid) {
       msg = q[i];
+      // the receiver's inbound filter when the message arrives (listen() :78-83); it depends on the
+      // (receiver, sender) pair only, so a dropped pair's ranks vanish together and the others stay dense
+      valid = in_pass(c, msg.to, msg.from);
+    }
+    if (valid) {
       uint32_t rank = 0;
       for (uint32_t j = 0; j < cnt; ++j) {
         const GMsgFull& o = q[j];
@@ -1920,16 +1942,17 @@ __device__ inline void add_req(const Ctx& c, const Bufs& b, uint32_t v, uint32_t
   q.flags = (initial ? RQ_INITIAL : 0) | (m.table_size << RQ_RECS_SHIFT);
   q.content = NONE; q.snap = NONE; q.pad = 0;
   if (initial) m.init_total++;
-  if (out_fail(c, v, to, v, SWIM_STREAM_SYNC_OUT, ordinal, 0)) {
+  // tryFailOutbound (loss) now; the transport's send after tryDelayOutbound meets the receiver —
+  // stopped (an error), or its inbound filter — when the message arrives (:49-75; k_sync_delay)
+  const bool loss = lost_k(c, out_loss(c, v, to), v, SWIM_STREAM_SYNC_OUT, ordinal, 0);
+  const uint32_t k = !loss && c.delay_on ? delay_ticks(c, v, to, v, SWIM_STREAM_SYNC_DELAY, ordinal, 0) : 0u;
+  if (!k && (loss || !c.up[to])) {
     if (initial) m.init_done++;
     return;
   }
-  if (!in_pass(c, to, v)) return;  // inbound-blocked at the receiver: silently dropped
   q.flags |= RQ_DELIVERED;
-  if (c.delay_on) {  // (single-shard engines only)
-    const uint32_t k = delay_ticks(c, v, to, v, SWIM_STREAM_SYNC_DELAY, ordinal, 0);
-    if (k) { park_request(c, b, q, k); return; }
-  }
+  if (k) { park_request(c, b, q, k); return; }
+  if (!in_pass(c, to, v)) return;  // inbound-blocked at the receiver: silently dropped
   sflag_set(c, b, v - c.lo, owned(c, to) ? SF_SENT | SF_SENT_LOCAL : SF_SENT);
   if (!owned(c, to)) {  // content (this row) travels with the request: k_pack_rows
     const uint32_t d = owner(c, to);
@@ -2207,7 +2230,7 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
     const uint64_t last = m.init_last;
     int64_t start = -1;
     if (!c.delay_on) start = (int64_t)c.T + (m.init_done == m.init_total ? 0 : (int64_t)c.sync_to_ticks);
-    else if (m.init_done == m.init_total) start = (int64_t)last;
+    else if (m.init_done == m.init_total) start = (int64_t)c.T;  // the last source completed now
     else if (c.T + 1 >= last + c.sync_to_ticks) start = (int64_t)(last + c.sync_to_ticks);
     if (start >= 0) {
       m.sync_on = 1;

@@ -768,7 +768,10 @@ __global__ void __launch_bounds__(256) k_ack_delay(KP) {
     SyncReq a = *ap;
     if (a.flags & (RQ_PARKED | RQ_DEFER)) continue;  // an arrival from the delay queue (uniform)
     const uint32_t dl = delay_ticks(c, a.from, a.to, a.from, SWIM_STREAM_SYNCACK_DELAY, a.ordinal, 0);
-    if (!dl) continue;
+    if (!dl) {  // arrives now: a stopped receiver or its inbound filter drops it (skipped, as deferred)
+      if (threadIdx.x == 0 && (!c.up[a.to] || !in_pass(c, a.to, a.from))) ap->flags = a.flags | RQ_DEFER;
+      continue;
+    }
     if (threadIdx.x == 0) s_slot = park_alloc(c, b);
     __syncthreads();
     const uint32_t slot = s_slot;
@@ -812,6 +815,10 @@ __global__ void __launch_bounds__(256) k_sync_delay(KP) {
       ack = (q.flags & RQ_ACK) != 0;
       park_release(b, q.snap);
       valid = c.up[q.to] != 0;
+      // the receiver stopped: the transport's send fails now — a start0 request's source completes
+      // (an error resumes empty, MembershipProtocolImpl.java:268-276); its sender is owned here
+      if (!valid && !ack && (q.flags & RQ_INITIAL) && c.up[q.from]) atomicAdd(&mem(c, q.from).init_done, 1u);
+      valid = valid && in_pass(c, q.to, q.from);  // the receiver's inbound filter on arrival
       // an ack's receiver — and a SYNC's sender, whose ack may come back this tick — is merged into in
       // the SYNC_ACK sub-phase: if it is also read as SYNC_ACK content this tick (it received a SYNC),
       // it takes a snapshot slot (sflag_set_from; a receiver on another shard: k_recv_sync)
@@ -974,7 +981,10 @@ __device__ __forceinline__ void sync_apply_body(const Params* __restrict__ P, ui
           const bool first = pre && q0 == 0;  // (pre_*: this message's words, loaded before the merges)
           const uint32_t t3 = (uint32_t)c.T << SF_BITS;
           const bool sf_now = first && (pre_sf & ~SF_MASK) == t3;
-          if (first ? pre_up && !lost_k(c, pre_loss, s, SWIM_STREAM_SYNCACK_OUT, q, 0) && pre_in
+          // with message delay only the loss is decided now: the receiver's state and inbound filter
+          // meet the ack when it arrives (k_ack_delay for an undelayed one, k_sync_delay else)
+          if (c.delay_on ? !lost_k(c, out_loss(c, s, rq.from), s, SWIM_STREAM_SYNCACK_OUT, q, 0)
+              : first ? pre_up && !lost_k(c, pre_loss, s, SWIM_STREAM_SYNCACK_OUT, q, 0) && pre_in
                     : !out_fail(c, s, rq.from, s, SWIM_STREAM_SYNCACK_OUT, q, 0) && in_pass(c, rq.from, s)) {
             a.from = s; a.to = rq.from; a.ordinal = q; a.slot = 0;
             a.flags = RQ_DELIVERED | (rq.flags & RQ_INITIAL) | (tsz << RQ_RECS_SHIFT);

@@ -96,6 +96,9 @@ def _partition(n, split):
     return g
 
 
+ALL_ = abi.ALL_MEMBERS
+
+
 def catalog() -> list[Scenario]:
     """Small scenarios (oracle-fast) used for bit-exact parity."""
     fd_test = dict(ping_interval=200, ping_timeout=100, ping_req_members=2, gossip_interval=100,
@@ -221,6 +224,21 @@ def catalog() -> list[Scenario]:
                       (0, "link_delay", 3, 0, 600), (4, "join", 16), (9, "join", 17), (9, "join", 18),
                       (30, "join", 19), (31, "join", 20), (60, "kill", 7), (80, "update_meta", 2),
                       (150, "join", 21), (150, "join", 22), (151, "join", 23)],
+                 check_every=20),
+        # NetworkEmulatorTransport applies the receiver's inbound filter when a message ARRIVES
+        # (listen :78-83, requestResponse :72-74), and the transport's send after tryDelayOutbound
+        # meets a receiver that stopped meanwhile: inbound blocks switched on and off while delayed
+        # GOSSIP_REQs, SYNCs / SYNC_ACKs (a joiner's initial SYNCs among them) and FD acks are in
+        # flight, a seed stopped while the joiners' initial SYNCs travel to it
+        Scenario("inbound_block_in_flight_16", 16, 12, 400, seed=28, seeds=(0, 2),
+                 cfg=dict(sync_interval=1000, sync_timeout=600, ping_interval=600, ping_timeout=300,
+                          metadata_timeout=2000, record_fd_events=1, delay_capacity=16384),
+                 ops=[(0, "default_delay", 200, ALL_), (0, "link_delay", 4, 1, 900), (9, "spread", 2, 55),
+                      (10, "default_in", 0, 3), (12, "join", 12), (12, "join", 13), (13, "default_in", 1, 3),
+                      (14, "kill", 2), (30, "link_in", 5, 1, 0), (33, "link_in", 5, 1, -1),
+                      (50, "spread", 6, 56), (51, "default_in", 0, 7), (53, "default_in", 1, 7),
+                      (70, "link_in", 1, 4, 0), (74, "link_in", 1, 4, -1), (90, "join", 14),
+                      (91, "default_in", 0, 0), (95, "default_in", 1, 0)],
                  check_every=20),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),
