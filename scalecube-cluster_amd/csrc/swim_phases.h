@@ -1229,6 +1229,20 @@ __device__ __forceinline__ uint64_t msg_key(const Ctx& c, const GMsgFull& m) {
 }
 
 
+// The next message's lines, loaded while the current one is processed: its collector slot, its
+// receipt-bitmap slot, the view cell and reference record of its subject — the dependent loads its
+// onGossipReq starts with, so that they hit the cache (values are re-read, never trusted: the current
+// message may change them).  Returns a value the caller folds into a sink that is never true.
+__device__ __forceinline__ uint32_t warm_gossip_req(const Ctx& c, uint32_t r, const CollEnt* cbase, const GMsgFull& g) {
+  uint32_t x = cbase[hash32(g.gossiper) & (c.hcap - 1)].key;
+  x ^= (uint32_t)c.gslot[gslot_of(gkey(g.gossiper, g.seq))].key;
+  if (g.status() < SWIM_GOSSIP_USER && g.subject < c.n) {
+    const size_t i = (size_t)(r - c.lo) * c.n + g.subject;
+    x ^= c.recs[i] ^ c.aux[i] ^ c.ref[g.subject];
+  }
+  return x;
+}
+
 // onGossipReq (GossipProtocolImpl.java:201-215) for one received message, in canonical order
 __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, const SlabRef& slab, const GMsgFull& g) {
   if (g.dup()) return false;  // the collector held it on arrival and only grows until now
@@ -1375,20 +1389,29 @@ __device__ inline unsigned long long deliver_sorted(const Ctx& c, uint32_t r, co
   m.ev_minor = 0;
   m.fetch_ctr = 0;
   const SlabRef slab = slab_of(c, r);
+  const CollEnt* cbase = c.coll + (size_t)(r - c.lo) * c.hcap;
   unsigned long long acc = 0;
+  uint32_t sink = 0;
+  GMsgFull next = a[ix8 ? ix8[0] : 0];
   for (uint32_t q = 0; q < k; ++q) {
-    const uint32_t at = ix8 ? ix8[q * ix8_stride] : q;
-    const GMsgFull g = a[at];
+    const GMsgFull g = next;
+    if (q + 1 < k) {
+      next = a[ix8 ? ix8[(q + 1) * ix8_stride] : q + 1];
+      sink ^= warm_gossip_req(c, r, cbase, next);
+    }
     nfresh += g.dup() ? 0u : 1u;
     if (on_gossip_req(c, r, m, slab, g)) acc++;
   }
+  if (sink == 0x5bd1e995u && k == 0x7fffffffu) set_err(c, 0u);  // keeps the warming loads; sets no bit
   return acc;
 }
 
+constexpr uint32_t BIG_FO = 256;  // ranks of a big inbox whose (gossiper, seq) the first-occurrence pass compares
 struct BigLds {  // per wave
   uint32_t snd[BIG_MAXD];  // distinct senders (found order, then ascending)
   uint32_t cnt[BIG_MAXD];  // their message counts, then running inbox bases
   uint32_t iP[64], iS[64], iR[64];  // apply_ins_batch scratch
+  uint2 fo[BIG_FO];        // (gossiper, seq) of the inbox's first BIG_FO messages in rank order
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -1509,6 +1532,53 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
   return k;
 }
 
+// The first-occurrence pass over a ranked big inbox (all lanes on one inbox): onGossipReq
+// (GossipProtocolImpl.java:201-215) changes state only for a message whose sequence id its
+// receiver's collector does not hold yet, and a collector only grows during delivery, so a message
+// can be accepted only if it is (a) not flagged as a provable duplicate, (b) not held by the
+// collector before the delivery, and (c) the first copy of its (gossiper, seq) in canonical order.
+// (a) and (b) are per message; (c) compares the first BIG_FO ranks pairwise in LDS (a later copy
+// beyond them is rejected by the collector in the chain, as before).  The candidates' inbox
+// positions are compacted in rank order to the front of pg_perm; the count is returned, and *nfresh
+// gets the messages not flagged.
+__device__ uint32_t accept_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L,
+                                     uint32_t& nfresh) {
+  const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
+  const uint32_t r_mem = c.lo + i;
+  auto perm_at = [&](uint32_t q) -> uint32_t& { return b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)]; };
+  uint32_t nacc = 0;
+  for (uint32_t r0 = 0; r0 < k; r0 += 64) {
+    const uint32_t r = r0 + lane;
+    uint32_t q = NONE;
+    GMsgFull g{};
+    bool ok = false;
+    if (r < k) {
+      q = perm_at(r);
+      if (q < k) {
+        g = b.pg_msgs[(size_t)pt[q >> 6] * 64 + (q & 63)];
+        ok = !g.dup();
+        nfresh += ok ? 1u : 0u;
+      } else {
+        set_err(c, ERR_MSGS);  // a hole: only after an inbox overflow
+      }
+      if (r < BIG_FO) L.fo[r] = make_uint2(q < k ? g.gossiper : NONE, q < k ? g.seq : NONE);
+    }
+    if (ok) ok = !coll_contains(c, coll_find(c, r_mem, g.gossiper), g.seq);
+    wave_sync();
+    if (ok && r < BIG_FO)
+      for (uint32_t j = 0; j < r; ++j) {
+        const uint2 o = L.fo[j];
+        if (o.x == g.gossiper && o.y == g.seq) { ok = false; break; }
+      }
+    const uint64_t mk = __ballot(ok);
+    // compaction in place: every lane has read its rank's entry, and the writes go to ranks <= r
+    if (ok) perm_at(nacc + lanes_below(mk)) = q;
+    nacc += (uint32_t)__popcll(mk);
+    wave_sync();
+  }
+  return nacc;
+}
+
 __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, const Bufs& b, const uint32_t* list,
                                                 uint32_t nb, uint32_t lane, int collect, BigLds& L,
                                                 unsigned long long& nsync, uint32_t& nmsg, uint32_t& nfresh) {
@@ -1517,7 +1587,7 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
   PPROF_T0(tp0);
   PPROF_CNT(4, 1ull);
   PPROF_CNT(5, (unsigned long long)nb);
-  uint32_t my_k = 0, my_pages = 0;
+  uint32_t my_k = 0, my_n = 0, my_pages = 0;
   for (uint32_t j = 0; j < nb; ++j) {
     const uint32_t i = list[j];
     const uint32_t r = c.lo + i;
@@ -1532,9 +1602,16 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) pages_ok &= pt[pg] < b.pg_cap;
     pages_ok = __ballot(!pages_ok) == 0;
     const bool go = c.up[r] && k && pages_ok;
-    if (go) rank_big_inbox(c, b, i, k, lane, L);
+    uint32_t nacc = 0, nf = 0;
+    if (go) {
+      rank_big_inbox(c, b, i, k, lane, L);
+      nacc = accept_big_inbox(c, b, i, k, lane, L, nf);
+      nmsg += lane == 0 ? k : 0u;
+      nfresh += nf;
+    }
     if (lane == j) {
-      my_k = go ? k : 0;
+      my_k = go ? nacc : 0;  // the chain walks the candidates only
+      my_n = k;
       my_pages = (k + 63) / 64;
     }
   }
@@ -1554,7 +1631,7 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     // chain's own dependent round trips are the cost of a big inbox
     auto fetch = [&](uint32_t q) -> GMsgFull {
       uint32_t jq = b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)];
-      if (jq >= my_k) {  // a hole: only after an inbox overflow (ERR_MSGS is set)
+      if (jq >= my_n) {  // a hole: only after an inbox overflow (ERR_MSGS is set)
         set_err(c, ERR_MSGS);
         jq = q;
       }
@@ -1563,14 +1640,12 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     const CollEnt* cbase = c.coll + (size_t)i * c.hcap;
     uint32_t sink = 0;
     GMsgFull next = fetch(0);
-    nmsg += my_k;
     for (uint32_t q = 0; q < my_k; ++q) {
       const GMsgFull g = next;
       if (q + 1 < my_k) {
         next = fetch(q + 1);
-        sink ^= cbase[hash32(next.gossiper) & (c.hcap - 1)].key;  // warms the slot coll_find probes first
+        sink ^= warm_gossip_req(c, r, cbase, next);
       }
-      nfresh += g.dup() ? 0u : 1u;
       if (on_gossip_req(c, r, m, slab, g)) acc++;
     }
     if (sink == 0x5bd1e995u && my_k == 0x7fffffffu) set_err(c, 0u);  // keeps the warming loads; sets no bit
