@@ -729,6 +729,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   // or below the current pass's)
   GossipHot hn{};
   if (lane < glen) hn = slab.hot[lane];
+  uint32_t sinkw = 0;  // the next pass's receipt-slot lines, warmed at the end of this one
   for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
     const uint32_t p = p0 + lane;
     const GossipHot h = hn;
@@ -913,6 +914,16 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     const bool wb = keep && (to != p || changed);
     GossipCold kc{};
     if (wb && to != p) kc = slab.cold[p];
+    // the next pass's hot bytes have arrived by now: its in-window gossips' receipt slots and the
+    // first targets' receipt words are loaded here, so that the next pass's check hits the cache
+    if (p + 64 < glen && (uint64_t)hn.inf_period() + spread >= period) {
+      const uint32_t sn = gslot_of(gkey(hn.gossiper, hn.seq));
+      sinkw ^= (uint32_t)c.gslot[sn].key;
+      for (uint32_t jj = 0; jj < min(nt, 3u); ++jj) {
+        const uint32_t tj = s_t[1 + jj];
+        if (owned(c, tj)) sinkw ^= c.gbits[(size_t)sn * c.gwords + ((tj - c.lo) >> 5)];
+      }
+    }
     wave_order();
     if (wb) {
       GossipHot hw = h;
@@ -921,6 +932,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       if (to != p) slab.cold[to] = kc;
     }
   }
+  if (sinkw == 0x5bd1e995u && glen == 0x7fffffffu) set_err(c, 0u);  // keeps the warming loads; sets no bit
   const bool any_done = __ballot(done) != 0;
   if (lane == 0) {
     // the sweep dropped a prefix (infection periods grow along the slab): the index keeps its serials
