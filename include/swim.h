@@ -408,6 +408,25 @@ int32_t swim_profile_fanout(swim_engine* e, swim_kernel_profile* out);
  * duplicates by the sender (SURVEY.md §8(d) merge). */
 int32_t swim_profile_deliver(swim_engine* e, swim_kernel_profile* out);
 
+/* ---- external SYNC ingestion (parity with a JVM unpinned) ---------------
+ * onSyncAck for a SYNC / SYNC_ACK that arrived from outside the simulation, e.g. decoded with
+ * swimgpu.wire from a real JVM node's bytes (MembershipProtocolImpl.java:363-391): syncMembership
+ * (:491-509) at viewer v over n records — member slot, status (SWIM_ALIVE / SWIM_SUSPECT / SWIM_LEAVING),
+ * incarnation — in the given order, reason SYNC (initial = 0) or INITIAL_SYNC, applied between ticks
+ * at the current tick with phase SWIM_PHASE_CONTROL: every updateMembership branch (namespace filter,
+ * isOverrides, refutation, LEAVING, SUSPECT timers, ALIVE admissions through the metadata round trip),
+ * gossip origination, events, ping / remote list updates.  Counted as one SYNC_ACK carrying n
+ * records.  SWIM_EINVAL for n > members, a member out of range, a negative incarnation or a DEAD
+ * record (a SyncData never holds one: the table drops DEAD members, :617-618 / onDeadMemberDetected);
+ * SWIM_ESTATE if v is not running; sharded: the owning rank applies it. */
+typedef struct swim_record {
+  uint32_t member;
+  uint32_t status;
+  int32_t inc;
+  uint32_t pad;
+} swim_record;
+int32_t swim_ingest_sync(swim_engine* e, uint32_t viewer, const swim_record* records, uint32_t n, int32_t initial);
+
 /* ---- quiet windows ---------------------------------------------------------
  * While the cluster is provably quiet — no live gossip, no pending failure-detector or suspicion
  * work, every up member's table equal to the reference row with no SUSPECT / LEAVING record, no loss,

@@ -1547,6 +1547,25 @@ int32_t swim_leave(swim_engine* e, uint32_t v, int32_t stop_after) {
   return SWIM_OK;
 }
 
+// external SYNC ingestion (swim.h): onSyncAck (MembershipProtocolImpl.java:363-391) between ticks
+int32_t swim_ingest_sync(swim_engine* e, uint32_t v, const swim_record* records, uint32_t n, int32_t initial) {
+  if (!e || v >= e->n || n > e->n || (n && !records)) return SWIM_EINVAL;
+  for (uint32_t i = 0; i < n; ++i)
+    if (records[i].member >= e->n || records[i].status >= SWIM_DEAD || records[i].inc < 0) return SWIM_EINVAL;
+  if (!e->m[v].up) return SWIM_ESTATE;
+  const Reason reason = initial ? INITIAL_SYNC : SYNC;
+  e->m[v].ev_minor = 0;
+  e->m[v].fetch_ctr = 0;
+  std::vector<PendingAlive> pending;
+  for (uint32_t i = 0; i < n; ++i)
+    e->update_membership(v, Record{records[i].member, records[i].status, records[i].inc}, reason, SWIM_PHASE_CONTROL,
+                         pending);
+  e->flush_pending(v, pending, reason, SWIM_PHASE_CONTROL);
+  e->STT().sync_acks++;
+  e->STT().sync_records += n;
+  return SWIM_OK;
+}
+
 int32_t swim_spread(swim_engine* e, uint32_t v, uint32_t payload) {
   if (!e || v >= e->n) return SWIM_EINVAL;
   if (!e->m[v].up) return SWIM_ESTATE;

@@ -763,6 +763,33 @@ __global__ void k_update_meta(Ctx c, uint32_t v, int owner) {
   spread_gossip(c, v, v, SWIM_ALIVE, inc, SWIM_ORIG_METADATA);
 }
 
+// swim_ingest_sync: syncMembership (MembershipProtocolImpl.java:491-509) at viewer v over externally
+// supplied records, one workgroup: thread 0 runs updateMembership record by record, then the ALIVE
+// admissions whose fetch succeeded; the workgroup then applies the pingMembers inserts in event order.
+// No REMOVED arises (DEAD records are refused by the host side), so the lists need no compaction.
+__global__ void __launch_bounds__(256) k_ingest_sync(Params* P, uint64_t T, uint32_t v, const swim_record* rec,
+                                                     uint32_t n, int32_t initial) {
+  const Ctx c = pctx_sync(P, T);
+  __shared__ uint32_t s_iP[256], s_iS[256], s_iR[256];
+  const int reason = initial ? R_INITIAL_SYNC : R_SYNC;
+  uint64_t* pend = P->b.pend;  // (workgroup 0's slice of the SYNC apply's pending admissions)
+  if (threadIdx.x == 0) {
+    MemberDev& m = mem(c, v);
+    m.ev_minor = 0;
+    m.fetch_ctr = 0;
+    uint32_t npend = 0;
+    for (uint32_t i = 0; i < n; ++i)
+      if (update_membership(c, v, rec[i].member, rec[i].status, rec[i].inc, reason, SWIM_PHASE_CONTROL))
+        pend[npend++] = ((uint64_t)rec[i].member << 32) | (uint32_t)rec[i].inc;
+    for (uint32_t j = 0; j < npend; ++j)
+      apply_alive(c, v, (uint32_t)(pend[j] >> 32), (int32_t)(uint32_t)pend[j], reason, SWIM_PHASE_CONTROL);
+    stat_add(c, ST_SYNC_ACKS, 1);
+    stat_add(c, ST_SYNC_RECORDS, n);
+  }
+  __syncthreads();
+  apply_ins_batch<256, true>(c, v, threadIdx.x, s_iP, s_iS, s_iR);
+}
+
 __global__ void k_spread(Ctx c, uint32_t v, uint32_t payload) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   spread_user(c, v, payload);
@@ -1423,6 +1450,30 @@ int32_t swim_spread(swim_engine* e, uint32_t m, uint32_t payload) {
   sd->c.T = e->T;
   k_spread<<<1, 64, 0, e->stream>>>(sd->c, m, payload);
   return hip_status();
+}
+
+int32_t swim_ingest_sync(swim_engine* e, uint32_t v, const swim_record* records, uint32_t n, int32_t initial) {
+  if (!e || v >= e->n || n > e->n || (n && !records)) return SWIM_EINVAL;
+  for (uint32_t i = 0; i < n; ++i)
+    if (records[i].member >= e->n || records[i].status >= SWIM_DEAD || records[i].inc < 0) return SWIM_EINVAL;
+  uint8_t up = 0;
+  if (read_up(e, v, &up) != SWIM_OK) return SWIM_EDEVICE;
+  if (!up) return SWIM_ESTATE;
+  Shard* sd = e->owner_of(v);
+  if (!sd) return SWIM_OK;  // RCCL: the owning rank applies it
+  swim_record* d = nullptr;
+  if (hipMalloc((void**)&d, sizeof(swim_record) * std::max(n, 1u)) != hipSuccess) return SWIM_ENOMEM;
+  int32_t rc = SWIM_OK;
+  sd->c.T = e->T;
+  sync_params(e, *sd);
+  if (n && hipMemcpy(d, records, sizeof(swim_record) * n, hipMemcpyHostToDevice) != hipSuccess) rc = SWIM_EDEVICE;
+  if (rc == SWIM_OK) {
+    k_ingest_sync<<<1, 256, 0, e->stream>>>(sd->d_par, e->T, v, d, n, initial);
+    if (hipStreamSynchronize(e->stream) != hipSuccess) rc = SWIM_EDEVICE;
+    e->par_slot = 0;
+  }
+  hipFree(d);
+  return rc == SWIM_OK ? hip_status() : rc;
 }
 
 int32_t swim_join(swim_engine* e, uint32_t m) {

@@ -154,6 +154,13 @@ class swim_interval(C.Structure):
     _fields_ = [("lo", C.c_uint64), ("hi", C.c_uint64)]
 
 
+class swim_record(C.Structure):
+    _fields_ = [("member", C.c_uint32), ("status", C.c_uint32), ("inc", C.c_int32), ("pad", C.c_uint32)]
+
+
+RECORD_DTYPE = np.dtype([("member", "<u4"), ("status", "<u4"), ("inc", "<i4"), ("pad", "<u4")])
+
+
 class swim_quiet_stats(C.Structure):
     _fields_ = [("ticks", C.c_uint64), ("windows", C.c_uint64), ("attempts", C.c_uint64), ("cut_short", C.c_uint64)]
 
@@ -210,6 +217,7 @@ PROTOTYPES = {
     "swim_profile_fanout": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_profile_deliver": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
     "swim_profile_quiet": (C.c_int32, [_engp, POINTER(swim_kernel_profile)]),
+    "swim_ingest_sync": (C.c_int32, [_engp, C.c_uint32, POINTER(swim_record), C.c_uint32, C.c_int32]),
     "swim_set_quiet_path": (C.c_int32, [_engp, C.c_int32]),
     "swim_debug_counters": (C.c_int32, [_u64p, C.c_uint32, C.c_int32]),
     "swim_get_quiet_stats": (C.c_int32, [_engp, POINTER(swim_quiet_stats)]),
@@ -449,6 +457,15 @@ class Engine:
         p = swim_kernel_profile()
         _check("swim_profile_deliver", self.lib.swim_profile_deliver(self._h, byref(p)))
         return {name: getattr(p, name) for name, _ in swim_kernel_profile._fields_}
+
+    def ingest_sync(self, viewer: int, records, initial: bool = False) -> None:
+        """swim_ingest_sync: onSyncAck at `viewer` for externally supplied (member, status, inc) records,
+        in the given order (e.g. swimgpu.wire.engine_records of a decoded SYNC / SYNC_ACK)."""
+        arr = np.zeros(len(records), dtype=RECORD_DTYPE)
+        for i, (m, st, inc) in enumerate(records):
+            arr[i] = (m, st, inc, 0)
+        _check("swim_ingest_sync", self.lib.swim_ingest_sync(
+            self._h, viewer, arr.ctypes.data_as(POINTER(swim_record)), len(arr), 1 if initial else 0))
 
     def set_quiet_path(self, enable: bool) -> None:
         """swim_set_quiet_path: quiet windows on (default) or the per-tick kernel chain only."""

@@ -592,6 +592,19 @@ def sync_message(engine, viewer: int, directory: Directory, ack: bool = False, c
     return Message(tuple(hs), SyncData(tuple(recs)))
 
 
+def engine_records(message: Message, directory: Directory) -> list:
+    """The records of a decoded SYNC / SYNC_ACK (its SyncData, in list order) as (member slot, status,
+    incarnation) for swim_ingest_sync (Engine.ingest_sync); members the directory does not know are
+    left out (the engine simulates a fixed set of slots)."""
+    index = {mid: m for m, mid in enumerate(directory.ids)}
+    out = []
+    for r in message.data.membership:
+        m = index.get(r.member.id)
+        if m is not None:
+            out.append((m, r.status, r.incarnation))
+    return out
+
+
 def gossip_request(engine, sender: int, gossips: list, directory: Directory) -> Message:
     """A GOSSIP_REQ of a simulated member carrying membership gossips (GossipProtocolImpl.java:288-300,
     MembershipProtocolImpl.java:847-852), `gossips` = (gossiper slot, sequence id, subject slot, status,

@@ -60,6 +60,14 @@ def apply_op(e: abi.Engine, op, args):
         e.spread(*args)
     elif op == "partition":
         e.set_partition(None if args[0] is None else np.asarray(args[0], dtype=np.uint16))
+    elif op == "ingest":  # (viewer, [(member, status, inc), ...], initial): an external SYNC_ACK off the wire
+        from swimgpu import wire
+        v, recs, initial = args
+        d = wire.Directory.local(e.capacity)
+        stranger = wire.MembershipRecord(wire.Member("f" * 8, "elsewhere:4800"), abi.ALIVE, 0)  # not a slot: dropped
+        data = wire.SyncData(tuple(wire.MembershipRecord(d.member(m), st, inc) for m, st, inc in recs) + (stranger,))
+        msg = wire.Message(((wire.HEADER_QUALIFIER, wire.SYNC_ACK), (wire.HEADER_SENDER, "elsewhere:4800")), data)
+        e.ingest_sync(v, wire.engine_records(wire.deserialize(wire.serialize(msg)), d), initial)
     else:
         raise ValueError(op)
 
@@ -239,6 +247,20 @@ def catalog() -> list[Scenario]:
                       (50, "spread", 6, 56), (51, "default_in", 0, 7), (53, "default_in", 1, 7),
                       (70, "link_in", 1, 4, 0), (74, "link_in", 1, 4, -1), (90, "join", 14),
                       (91, "default_in", 0, 0), (95, "default_in", 1, 0)],
+                 check_every=20),
+        # SYNC_ACKs from outside the simulation (swim_ingest_sync, onSyncAck MembershipProtocolImpl.java
+        # :363-391) decoded from the wire: a SUSPECT record of a live member (suspicion timer), one of the
+        # viewer itself (refutation, inc+1 gossip), a LEAVING record, ALIVE records of a stopped slot
+        # (metadata fetch fails) and of a fresh joiner (fetch, ADDED), a stale record, an initial-sync
+        # ingestion, SUSPECT of a just-killed member, an empty table, a higher incarnation under delay
+        Scenario("external_sync_16", 16, 12, 320, seed=29, seeds=(0,), cfg=mp_test,
+                 ops=[(15, "ingest", 3, [(5, abi.SUSPECT, 1), (3, abi.SUSPECT, 0), (7, abi.LEAVING, 1),
+                                         (12, abi.ALIVE, 0), (9, abi.ALIVE, 0)], False),
+                      (25, "join", 12), (26, "ingest", 9, [(12, abi.ALIVE, 0), (13, abi.ALIVE, 0)], True),
+                      (60, "kill", 4), (61, "ingest", 1, [(4, abi.SUSPECT, 0)], False), (100, "ingest", 6, [], False),
+                      (120, "default_delay", 80, ALL_), (121, "ingest", 2, [(11, abi.ALIVE, 5), (10, abi.SUSPECT, 0)],
+                                                                     False),
+                      (200, "ingest", 8, [(5, abi.LEAVING, 0), (14, abi.SUSPECT, 3)], False)],
                  check_every=20),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),

@@ -165,3 +165,46 @@ def test_relayed_message_keeps_the_deserialised_map_capacity():
     three = [(f"k{i}", str(i)) for i in range(3)]
     got = [k for k, _ in wire.java_hashmap_order(three, 3)]
     assert got == sorted((k for k, _ in three), key=lambda k: (bucket(k, 8), int(k[1:])))
+
+
+def test_ingest_external_sync_ack():
+    """swim_ingest_sync (onSyncAck, MembershipProtocolImpl.java:363-391) fed from the wire: a SYNC_ACK
+    a JVM node would send, decoded and mapped onto the engine's slots (unknown ids dropped), merged into
+    a viewer of the CPU oracle (the GPU path is compared with it in the external_sync_16 scenario).
+    Parity with a JVM unpinned (no JVM here)."""
+    import oracle
+    lib = oracle.lib()
+    e = abi.Engine(lib, abi.default_config(lib), 8, 8, seed=5)
+    e.step(2)
+    d = wire.Directory.local(8)
+    recs = (wire.MembershipRecord(d.member(4), abi.SUSPECT, 0), wire.MembershipRecord(d.member(2), abi.SUSPECT, 0),
+            wire.MembershipRecord(d.member(6), abi.ALIVE, 0),  # equal incarnation: no change
+            wire.MembershipRecord(wire.Member("beef", "other:1"), abi.ALIVE, 3))
+    msg = wire.Message(((wire.HEADER_QUALIFIER, wire.SYNC_ACK),), wire.SyncData(recs))
+    got = wire.engine_records(wire.deserialize(wire.serialize(msg)), d)
+    assert got == [(4, abi.SUSPECT, 0), (2, abi.SUSPECT, 0), (6, abi.ALIVE, 0)]
+    before = e.stats()
+    e.drain_events()
+    e.ingest_sync(2, got)
+    row = e.read_view(2).astype(np.int64)
+    st = lambda s: int(row[s] >> 32) & 3
+    inc = lambda s: int(row[s] & 0xFFFFFFFF)
+    assert (st(4), inc(4)) == (abi.SUSPECT, 0)   # suspected, suspicion timer scheduled
+    assert (st(2), inc(2)) == (abi.ALIVE, 1)     # a SUSPECT record of the viewer itself: refuted
+    assert (st(6), inc(6)) == (abi.ALIVE, 0)
+    g = e.read_gossips(2)
+    assert sorted(int(x) for x in g["subject"]) == [2, 4]  # the refutation and the suspicion spread
+    after = e.stats()
+    assert after["sync_acks"] == before["sync_acks"] + 1
+    assert after["sync_records"] == before["sync_records"] + 3
+    # refused: a stopped viewer, a DEAD record (a SyncData never holds one), an out-of-range member
+    e.kill(7)
+    with pytest.raises(RuntimeError):
+        e.ingest_sync(7, [(1, abi.ALIVE, 0)])
+    with pytest.raises(RuntimeError):
+        e.ingest_sync(1, [(3, abi.DEAD, 0)])
+    with pytest.raises(RuntimeError):
+        e.ingest_sync(1, [(8, abi.ALIVE, 0)])
+    e.ingest_sync(1, [])  # an empty table is a no-op apart from the counters
+    e.step(30)
+    assert e.stats()["capacity_errors"] == 0
