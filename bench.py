@@ -129,7 +129,7 @@ def churn_capacities(cfg, capacity):
     the live gossips per member grow by ~8 x N per period); a period's kills put a suspicion timer
     at every viewer within a few seconds."""
     cfg.event_capacity = 1 << 25
-    cfg.gossip_capacity = 1 << 17
+    cfg.gossip_capacity = 1 << 18  # 24 B per (member, gossip): 103 GB of slab at N = 16,384
     # one gossip round's GOSSIP_REQs: ~4 x 10^8 in the third period at N = 16,384
     cfg.message_capacity = 1 << 30 if capacity > 12288 else 1 << 28
     # a viewer keeps a SequenceIdCollector per gossiper heard until it is removed

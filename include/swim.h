@@ -69,6 +69,8 @@ extern "C" {
 #define SWIM_PHASE_SYNC 4    /* SYNC requests delivered  (MembershipProtocolImpl.java:394-415)*/
 #define SWIM_PHASE_SYNCACK 5 /* SYNC_ACKs delivered      (MembershipProtocolImpl.java:385-391)*/
 #define SWIM_PHASE_CONTROL 6 /* host control ops (leave, join) applied between ticks          */
+#define SWIM_PHASE_FETCH 7   /* delayed GET_METADATA round trips arriving (MetadataStoreImpl.java:146-185),
+                                processed first in the tick; events sort by (tick, viewer, phase, minor) */
 
 /*
  * Packed view cell: one 64-bit word per (viewer, subject).  This is also the readback format of

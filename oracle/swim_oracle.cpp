@@ -68,6 +68,16 @@ bool is_overrides(const Record& r1, const Record* r0) {
   return r1.inc > r0->inc;
 }
 
+// A GET_METADATA round trip in flight under message delay (MetadataStoreImpl.fetchMetadata
+// :146-185): stage 1 = the request travelling to the subject's address d, stage 2 = the response
+// travelling back; `due` = the arrival tick of the current leg.  Draws stay keyed by the issue tick t0.
+struct PendingFetch {
+  uint32_t s;
+  int32_t inc;
+  uint32_t reason, phase, stage, f, d, ver;
+  uint64_t t0, due;
+};
+
 // ----------------------------------------------------------------------------- SequenceIdCollector
 // gossip/SequenceIdCollector.java:11-94 — closed intervals [a,b] in a TreeMap.
 struct SeqCollector {
@@ -188,6 +198,7 @@ struct Member {
   bool sync_on = false;
   // per-tick bookkeeping
   uint32_t ev_minor = 0, fetch_ctr = 0;
+  std::vector<PendingFetch> fq;  // metadata round trips in flight, in issue order
 };
 
 // cell helpers
@@ -217,6 +228,7 @@ struct SyncReq {
 struct PendingAlive {
   Record r1;
 };
+
 
 // Side effects a worker thread of a parallel phase region collects instead of writing the engine's
 // shared stats / event list / timer queue; merged in thread order after the region (the CPU
@@ -359,9 +371,13 @@ struct swim_engine {
     return it != link_delay.end() ? it->second : default_delay[a];
   }
   uint32_t delay_ticks(uint32_t a, uint32_t b, uint32_t member, uint32_t stream, uint32_t sub24, uint32_t sub32) {
+    return delay_ticks_at(a, b, member, stream, sub24, sub32, T);
+  }
+  uint32_t delay_ticks_at(uint32_t a, uint32_t b, uint32_t member, uint32_t stream, uint32_t sub24, uint32_t sub32,
+                          uint64_t tick) {
     const int32_t mean = out_delay(a, b);
     if (mean <= 0) return 0;
-    uint32_t c[4] = {member, (uint32_t)T, (stream << 24) | (sub24 & 0xffffffu), sub32}, o[4];
+    uint32_t c[4] = {member, (uint32_t)tick, (stream << 24) | (sub24 & 0xffffffu), sub32}, o[4];
     philox4x32_10(c, key, o);
     const uint64_t u53 = ((uint64_t)(o[0] >> 11) << 32) | o[1];
     return swim_delay_ticks(delay_tab.at(mean).data(), u53);
@@ -458,25 +474,47 @@ struct swim_engine {
   void cancel_timer(uint32_t v, uint32_t s) { m[v].row[s] &= ~B_HAS_TIMER; }
 
   // ------------------------------------------------------------------------- metadata fetch
-  // MetadataStoreImpl.fetchMetadata (:146-185) round trip + onMetadataRequest (:201-240).
-  bool fetch_ok(uint32_t v, uint32_t s, uint32_t phase) {
-    uint32_t f = m[v].fetch_ctr++;
-    uint32_t w1 = draw(v, SWIM_STREAM_FETCH_REQ, phase, f);
-    uint32_t w2 = draw(v, SWIM_STREAM_FETCH_RESP, phase, f);
+  // MetadataStoreImpl.fetchMetadata (:146-185) round trip + onMetadataRequest (:201-240), with the
+  // NetworkEmulator's arrival-time semantics: the request is lost or refused at its send, meets the
+  // subject's transport (stopped, inbound filter) when it arrives; the response likewise; the whole
+  // round trip must end before metadataTimeout (:160-165).  Returns true when the response is in
+  // within the calling phase (no delay on either leg: the caller applies the admission at its flush
+  // point); a delayed round trip goes to the viewer's queue and completes in the FETCH phase of its
+  // arrival tick (phase_fetch).
+  bool fetch_start(uint32_t v, const Record& r1, Reason reason, uint32_t phase) {
+    const uint32_t f = m[v].fetch_ctr++;
     STT().fetches++;
+    const uint32_t s = r1.member, d = dst(s);
     // the request goes to s's address; another member listening there does not answer (:209)
-    const uint32_t d = dst(s);
-    bool ok = d == s && !out_fail(v, d, w1) && in_pass(d, v) && !out_fail(d, v, w2) && in_pass(v, d);
-    // requestResponse(...).timeout(metadataTimeout) (:160-165): both legs delayed (tryDelayOutbound
-    // on the request and on the response's send)
-    if (ok && !delay_tab.empty()) {
-      const uint64_t rtt = (uint64_t)delay_ticks(v, d, v, SWIM_STREAM_FETCH_REQ_DELAY, phase, f) +
-                           delay_ticks(d, v, v, SWIM_STREAM_FETCH_RESP_DELAY, phase, f);
-      ok = rtt * tick_ms < (uint64_t)cfg.metadata_timeout;
+    if (d != s || out_fail(v, d, draw(v, SWIM_STREAM_FETCH_REQ, phase, f))) return false;
+    const uint32_t d1 = delay_tab.empty() ? 0 : delay_ticks(v, d, v, SWIM_STREAM_FETCH_REQ_DELAY, phase, f);
+    if ((uint64_t)d1 * tick_ms >= (uint64_t)cfg.metadata_timeout) return false;
+    PendingFetch p{s, r1.inc, (uint32_t)reason, phase, 1, f, d, 0, T, T + d1};
+    if (d1 == 0) {
+      const int r = fetch_stage1(v, p);
+      if (r == 1) STT().fetch_ok++;
+      if (r != 2) return r == 1;
     }
-    if (ok) STT().fetch_ok++;
-    return ok;
+    m[v].fq.push_back(p);
+    return false;
   }
+  // the request arrives at d (now): 0 = the round trip failed, 1 = the response arrived too (no delay
+  // on it), 2 = the response is in flight (p.due = its arrival tick)
+  int fetch_stage1(uint32_t v, PendingFetch& p) {
+    const uint32_t d = p.d;
+    if (!m[d].up || !in_pass(d, v)) return 0;
+    if (out_fail(d, v, draw(v, SWIM_STREAM_FETCH_RESP, p.phase, p.f, p.t0))) return 0;
+    const uint32_t d2 =
+        delay_tab.empty() ? 0 : delay_ticks_at(d, v, v, SWIM_STREAM_FETCH_RESP_DELAY, p.phase, p.f, p.t0);
+    if ((T - p.t0 + d2) * tick_ms >= (uint64_t)cfg.metadata_timeout) return 0;
+    p.ver = meta_ver.empty() ? 0 : meta_ver[p.s];  // the metadata the response carries
+    p.stage = 2;
+    p.due = T + d2;
+    if (d2 == 0) return fetch_stage2(v, p) ? 1 : 0;
+    return 2;
+  }
+  // the response arrives at v (now)
+  bool fetch_stage2(uint32_t v, const PendingFetch& p) const { return m[v].up && in_pass(v, p.d); }
 
   // ------------------------------------------------------------------------- updateMembership
   // MembershipProtocolImpl.updateMembership (:569-664).  ALIVE admissions whose metadata fetch
@@ -544,24 +582,28 @@ struct swim_engine {
       return;
     }
     if (!present || r0v.inc < r1.inc) {
-      if (fetch_ok(v, s, phase)) pending.push_back(PendingAlive{r1});
+      if (fetch_start(v, r1, reason, phase)) pending.push_back(PendingAlive{r1});
     }
   }
 
   // doOnSuccess of the fetch (:648-656) + onAliveMemberDetected (:769-795)
   void apply_alive(uint32_t v, const Record& r1, Reason reason, uint32_t phase) {
+    apply_alive(v, r1, reason, phase, meta_ver.empty() ? 0 : meta_ver[r1.member]);
+  }
+  // ver: the subject's metadata version the response carried
+  void apply_alive(uint32_t v, const Record& r1, Reason reason, uint32_t phase, uint32_t ver) {
     Member& mv = m[v];
     const uint32_t s = r1.member;
     cancel_timer(v, s);
     if (reason != MEMBERSHIP_GOSSIP && reason != INITIAL_SYNC) spread_gossip(v, r1, orig_of(reason));
     uint64_t& c = mv.row[s];
     // metadataStore.updateMetadata(member, metadata1) returns metadata0 (null when none is stored);
-    // metadata1 is the subject's metadata now (the fetch answers within the tick)
+    // metadata1 is the subject's metadata when it answered
     const bool had_meta = c_has(c, B_HAS_METADATA);
     bool same_meta = had_meta;
     if (!meta_seen.empty()) {
-      same_meta = had_meta && meta_seen[v][s] == meta_ver[s];
-      meta_seen[v][s] = meta_ver[s];
+      same_meta = had_meta && meta_seen[v][s] == ver;
+      meta_seen[v][s] = ver;
     }
     c |= B_HAS_METADATA;
     const bool exists = c_has(c, B_IN_MEMBERS);
@@ -1228,10 +1270,40 @@ struct swim_engine {
     }
   }
 
+  // ------------------------------------------------------------------------- FETCH phase
+  // delayed GET_METADATA legs arriving this tick, per viewer in issue order; a completed round trip
+  // is the fetch's doOnSuccess (apply_alive).  A stopped viewer's round trips are void.
+  void phase_fetch() {
+    for (uint32_t v = 0; v < n; ++v) {
+      Member& mv = m[v];
+      if (mv.fq.empty()) continue;
+      if (!mv.up) {
+        mv.fq.clear();
+        continue;
+      }
+      mv.ev_minor = 0;
+      std::vector<PendingFetch> keep;
+      for (PendingFetch p : mv.fq) {
+        if (p.due > T) {
+          keep.push_back(p);
+          continue;
+        }
+        const int r = p.stage == 1 ? fetch_stage1(v, p) : (fetch_stage2(v, p) ? 1 : 0);
+        if (r == 2) keep.push_back(p);
+        if (r == 1) {
+          STT().fetch_ok++;
+          apply_alive(v, Record{p.s, SWIM_ALIVE, p.inc}, (Reason)p.reason, SWIM_PHASE_FETCH, p.ver);
+        }
+      }
+      mv.fq.swap(keep);
+    }
+  }
+
   void step_tick() {
     T += 1;
     st.ticks++;
     start_joins();
+    phase_fetch();
     phase_timers();
     phase_fd();
     phase_gossip();

@@ -128,6 +128,7 @@ struct Shard {
   // `peers` (device) says where this shard reads what the others produced for it
   void* xreg = nullptr;
   size_t xreg_bytes = 0;
+  void* rx_rows_h[2] = {nullptr, nullptr};  // the pulled-row copies Peers points at (RCCL / pull rig)
   Peers* peers = nullptr;
   std::vector<void*> ipc_open;  // peers' regions mapped here (RCCL)
   uint32_t links_dev_cap = 0;
@@ -146,6 +147,11 @@ struct Shard {
     if (dalloc(p, count) != hipSuccess) return false;
     allocs.push_back((void*)*p);
     return true;
+  }
+  void release(void* p) {
+    if (!p) return;
+    allocs.erase(std::remove(allocs.begin(), allocs.end(), p), allocs.end());
+    hipFree(p);
   }
   // (keep: the first *cap elements are copied into the new allocation; the caller has drained the stream)
   template <typename T>
@@ -198,6 +204,7 @@ struct swim_engine {
   uint32_t route_of(uint32_t x) const { return route_h.empty() ? x : route_h[x]; }
   std::vector<swim_event> events;
   uint64_t host_ticks = 0, host_events = 0;
+  uint32_t row_grows = 0;  // times row_cap grew before a join burst (grow_rows_for_joins)
   // quiet windows (swim_quiet.h): on unless disabled; after a window that advanced nothing, the next
   // try waits quiet_backoff ticks (doubling), so a busy cluster pays a scan only now and then
   bool quiet_on = true;
@@ -472,12 +479,55 @@ static int32_t apply_binds(swim_engine* e) {
   return SWIM_OK;
 }
 
+// row_cap — the content rows one shard may send in one SYNC (or SYNC_ACK) exchange — grows before a
+// tick whose joins could exceed it: every joiner sends its initial SYNC to every seed
+// (MembershipProtocolImpl.start0 :250-291) and each seed answers every one, so a join burst needs up
+// to (joins on a shard) x seeds rows on the joiners' side and joins x (seeds on a shard) on the seeds'
+// side, on top of the periodic SYNCs.  Only replicated control state decides (the pending joins, the
+// seeds), so every RCCL rank grows at the same tick and all of them enter the re-exchange of the
+// regions' IPC handles.  Rows are bounded at 4 GiB per direction.
+static int32_t alloc_xreg(swim_engine* e, Shard& sd, bool uncached);
+static int32_t setup_peers_local(swim_engine* e);
+static int32_t setup_peers_rccl(swim_engine* e);
+static int32_t grow_rows_for_joins(swim_engine* e) {
+  if (e->world <= 1 || e->joins.empty() || e->sh.empty()) return SWIM_OK;
+  const uint32_t W = (uint32_t)e->world;
+  std::vector<uint64_t> jn(W, 0), sn(W, 0);
+  for (uint32_t m : e->joins) jn[std::min(W - 1, m / e->sz)]++;
+  for (uint32_t x : e->seeds) sn[std::min(W - 1, x / e->sz)]++;
+  const uint64_t J = e->joins.size(), S = std::max<uint64_t>(1, e->seeds.size());
+  uint64_t need = 0;
+  for (uint32_t p = 0; p < W; ++p) need = std::max({need, jn[p] * S, J * sn[p]});
+  need += 64 + (uint64_t)e->sz / std::max(e->S, 1u);  // the tick's periodic SYNCs beside them
+  const uint32_t cur = e->sh[0].b.row_cap;
+  uint64_t cap = cur;
+  while (cap < need) cap *= 2;
+  cap = std::min<uint64_t>(cap, std::max<uint64_t>(cur, (4ull << 30) / (4ull * e->n)));
+  if (cap <= cur) return SWIM_OK;
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  if (e->rccl) {  // every rank unmaps the others' regions before any region is freed
+    Shard& sd = e->sh[0];
+    for (void* q : sd.ipc_open) hipIpcCloseMemHandle(q);
+    sd.ipc_open.clear();
+    if (nccl_ok(ncclAllReduce(e->d_cnt, e->d_cnt, 1, ncclUint32, ncclMax, e->comm, e->stream)) != SWIM_OK ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
+      return SWIM_EDEVICE;
+  }
+  for (Shard& sd : e->sh) {
+    sd.b.row_cap = (uint32_t)cap;
+    if (int32_t rc = alloc_xreg(e, sd, e->rccl)) return rc;
+  }
+  e->row_grows++;
+  return e->rccl ? setup_peers_rccl(e) : setup_peers_local(e);
+}
+
 static int32_t run_tick(swim_engine* e) {
   e->T += 1;
   e->host_ticks += 1;
   hipStream_t s = e->stream;
   if (!e->binds.empty())
     if (int32_t rc = apply_binds(e)) return rc;
+  if (int32_t rc = grow_rows_for_joins(e)) return rc;
   const uint64_t T = e->T;
   const bool multi = e->world > 1;
   const bool gossip_tick = e->g_residue[e->T % e->G] != 0;
@@ -514,6 +564,10 @@ static int32_t run_tick(swim_engine* e) {
     // with message delay every tick may deliver GOSSIP_REQs, so the SYNC collection that follows a
     // member's deliveries moves into k_gossip_deliver on every tick
     const bool delay = sd.c.delay_on != 0;
+    if (delay) {  // ---- the FETCH phase: delayed metadata round trips arriving now
+      k_fetch_due<<<gm, 256, 0, s>>>(sd.d_par, T);
+      TICK_CHECK("k_fetch_due");
+    }
     k_fd<<<gm, 256, 0, s>>>(sd.d_par, T, gossip_tick ? 1 : 0, gossip_tick || delay ? 0 : 1);
     TICK_CHECK("k_fd");
     if (gossip_tick) {
@@ -806,13 +860,21 @@ static int32_t alloc_xreg(swim_engine* e, Shard& sd, bool uncached) {
   const size_t o_msgs = take(W * b.tx_msg_cap * sizeof(GMsgFull)), o_reqs = take(W * b.tx_req_cap * sizeof(SyncReq)),
                o_acks = take(W * b.tx_req_cap * sizeof(SyncReq)), o_stops = take(4ull * b.tx_stop_cap),
                o_rows0 = take(rows), o_rows1 = take(rows);
-  if (sd.xreg) hipFree(sd.xreg);
+  // a re-allocation (row_cap grew) keeps everything before the rows — message and SYNC headers,
+  // stops, deferred acks — at the same offsets
+  void* old = sd.xreg;
+  const size_t keep = old ? std::min(o_rows0, sd.xreg_bytes) : 0;
   sd.xreg = nullptr;
   sd.xreg_bytes = off;
   hipError_t r = hipErrorUnknown;
   if (uncached) r = hipExtMallocWithFlags(&sd.xreg, off, hipDeviceMallocUncached);
   if (r != hipSuccess) r = hipMalloc(&sd.xreg, off);
   if (r != hipSuccess) return SWIM_ENOMEM;
+  if (old) {
+    const bool ok = !keep || hipMemcpy(sd.xreg, old, keep, hipMemcpyDeviceToDevice) == hipSuccess;
+    hipFree(old);
+    if (!ok) return SWIM_EDEVICE;
+  }
   char* base = static_cast<char*>(sd.xreg);
   b.tx_msgs = reinterpret_cast<GMsgFull*>(base + o_msgs);
   b.tx_reqs = reinterpret_cast<SyncReq*>(base + o_reqs);
@@ -838,6 +900,9 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.gcap = cf.gossip_capacity ? cf.gossip_capacity : 1024;
   c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 4096);
   c.gix_mask = next_pow2(2 * c.gcap) - 1;
+  // infected overflows a member holds at once: states that took a second sender after a collector
+  // clear (segmentation), a small fraction of the slab
+  c.inf_mask = next_pow2(std::max<uint32_t>(64, std::min<uint32_t>(4096, c.gcap / 8))) - 1;
   // spilled collectors by tier (6 / 62 / 510 / 16,382 intervals); blocks are recycled, so these
   // bound the collectors spilled at once, not over the run
   const uint64_t icap = cf.interval_capacity ? cf.interval_capacity : 64;  // tier-0 blocks per row
@@ -913,12 +978,15 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.tx_stop_cap = multi ? kStopCap : 0;
   // content rows one shard may send in one SYNC (or SYNC_ACK) exchange: 256 MiB of rows, 64..4,096
   b.row_cap = multi ? std::min<uint32_t>(4096, std::max<uint32_t>(64, (1u << 26) / std::max(n, 1u))) : 0;
+  if (const char* rc = std::getenv("SWIM_DEBUG_ROW_CAP"))  // tests: start small so that joins grow it
+    if (multi && std::atoi(rc) > 0) b.row_cap = (uint32_t)std::atoi(rc);
 
   const size_t nn = (size_t)nl * n;
   c.blocks = (n + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
   bool ok = sd.alloc(&c.recs, nn) && sd.alloc(&c.aux, nn) && sd.alloc(&c.ref, n) && sd.alloc(&c.dirty, n) &&
             sd.alloc(&c.bdiff, (size_t)std::max(nl, 1u) * c.blocks) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
             sd.alloc(&c.remote, nn) && sd.alloc(&c.slab_hot, (size_t)nl * c.gcap) && sd.alloc(&c.slab_cold, (size_t)nl * c.gcap) &&
+            sd.alloc(&c.inf_over, (size_t)std::max(nl, 1u) * (c.inf_mask + 1)) &&
             sd.alloc(&c.gix, (size_t)nl * (c.gix_mask + 1)) && sd.alloc(&c.coll, (size_t)nl * c.hcap) &&
             sd.alloc(&c.spill[0], (size_t)c.spill_cap[0] * tier_words(0)) &&
             sd.alloc(&c.spill[1], (size_t)c.spill_cap[1] * tier_words(1)) &&
@@ -975,6 +1043,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.x = sd.x;
   hipStream_t s = e->stream;
   hipMemsetAsync(c.coll, 0, sizeof(CollEnt) * (size_t)nl * c.hcap, s);
+  hipMemsetAsync(c.inf_over, 0xff, sizeof(InfOver) * (size_t)std::max(nl, 1u) * (c.inf_mask + 1), s);  // INF_EMPTY
   hipMemsetAsync(c.spill_ctl, 0, sizeof(SpillCtl) * NTIER, s);
   hipMemsetAsync(c.seg_flag, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(c.wheel, 0xff, sizeof(uint64_t) * ((size_t)c.wheel_pages << c.wheel_pshift), s);  // WHEEL_EMPTY
@@ -1046,8 +1115,11 @@ static int32_t setup_peers_local(swim_engine* e) {
   for (Shard& sd : e->sh) {
     Peers ph{};
     if (e->pull_rows)
-      for (int k = 0; k < 2; ++k)
+      for (int k = 0; k < 2; ++k) {
+        sd.release(sd.rx_rows_h[k]);
         if (!sd.alloc(&ph.rx_rows[k], (size_t)e->world * sd.b.row_cap * e->n)) return SWIM_ENOMEM;
+        sd.rx_rows_h[k] = ph.rx_rows[k];
+      }
     for (uint32_t p = 0; p < (uint32_t)e->world; ++p) {
       const Bufs& pb = e->sh[p].b;
       ph.msgs[p] = pb.tx_msgs;
@@ -1091,7 +1163,9 @@ static int32_t setup_peers_rccl(swim_engine* e) {
   if (rc) return rc;
   Peers ph{};
   for (int k = 0; k < 2; ++k) {
+    sd.release(sd.rx_rows_h[k]);
     if (!sd.alloc(&ph.rx_rows[k], (size_t)W * sd.b.row_cap * e->n)) return SWIM_ENOMEM;
+    sd.rx_rows_h[k] = ph.rx_rows[k];
   }
   for (uint32_t p = 0; p < W; ++p) {
     char* base = static_cast<char*>(sd.xreg);
@@ -1592,6 +1666,15 @@ static int32_t enable_delay(swim_engine* e) {
       return SWIM_EDEVICE;
     b.sdq_bcap = sbcap;
     b.park_cap = pcap;
+    // delayed metadata round trips: every viewer may have a whole table's admissions in flight
+    const uint32_t fcap = std::max<uint32_t>(4096, 2 * e->n);
+    const size_t nl2 = 2ull * std::max(sd.c.nl, 1u);
+    if (!sd.alloc(&sd.c.fq, 2ull * fcap) || !sd.alloc(&sd.c.fq_head, nl2) || !sd.alloc(&sd.c.fq_tail, nl2) ||
+        !sd.alloc(&sd.c.fq_cnt, 2))
+      return SWIM_ENOMEM;
+    if (hipMemset(sd.c.fq_head, 0xff, 4 * nl2) != hipSuccess || hipMemset(sd.c.fq_cnt, 0, 8) != hipSuccess)
+      return SWIM_EDEVICE;
+    sd.c.fq_cap = fcap;
     sd.c.delay_on = 1;
   }
   return SWIM_OK;
@@ -1805,6 +1888,7 @@ int32_t swim_read_gossips(swim_engine* e, uint32_t v, swim_gossip* out, uint32_t
   if (hipMemcpy(gh.data(), sd->c.slab_hot + o, sizeof(GossipHot) * k, hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(gc.data(), sd->c.slab_cold + o, sizeof(GossipCold) * k, hipMemcpyDeviceToHost) != hipSuccess)
     return SWIM_EDEVICE;
+  std::vector<InfOver> io;  // the member's infected overflows, read when a state has one
   for (uint32_t i = 0; i < k; ++i) {  // (the SlabRef layout, swim_device.h)
     out[i].gossiper = gh[i].gossiper;
     out[i].subject = gc[i].subject;
@@ -1813,7 +1897,18 @@ int32_t swim_read_gossips(swim_engine* e, uint32_t v, swim_gossip* out, uint32_t
     out[i].status = (gh[i].per_st >> PER_BITS) & 7u;
     out[i].infection_period = gh[i].per_st & PER_MASK;
     out[i].infected[0] = gh[i].inf0;
-    out[i].infected[1] = gc[i].inf[0];
+    out[i].infected[1] = NONE;
+    if (gh[i].per_st >> 31) {
+      const uint32_t cap = sd->c.inf_mask + 1;
+      if (io.empty()) {
+        io.resize(cap);
+        if (hipMemcpy(io.data(), sd->c.inf_over + (size_t)(v - sd->c.lo) * cap, sizeof(InfOver) * cap,
+                      hipMemcpyDeviceToHost) != hipSuccess)
+          return SWIM_EDEVICE;
+      }
+      for (uint32_t j = 0; j < cap; ++j)
+        if (io[j].gossiper == gh[i].gossiper && io[j].seq == gh[i].seq) { out[i].infected[1] = io[j].inf[0]; break; }
+    }
   }
   return SWIM_OK;
 }

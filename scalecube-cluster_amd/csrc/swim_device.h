@@ -40,6 +40,19 @@ enum : uint32_t {
   ERR_DELAY = 1u << 16,     // more delayed GOSSIP_REQs arrive in one tick than a delay bucket holds
   ERR_XPTR = 1u << 17,      // SWIM_DEBUG_SYNC: a sharded tick would dereference a null exchange pointer
   ERR_SDELAY = 1u << 18,    // delayed SYNCs / SYNC_ACKs: a delay bucket or the park slots ran out
+  ERR_FETCHQ = 1u << 19,    // more delayed GET_METADATA round trips in flight than the fetch queue holds
+};
+
+// A GET_METADATA round trip in flight under message delay (MetadataStoreImpl.fetchMetadata :146-185):
+// stage 1 = the request travelling to the subject's address d, stage 2 = the response travelling
+// back; due = the arrival tick of the current leg; draws stay keyed by the issue tick t0.  Per viewer
+// a chain in issue order (next), in the queue of the tick it was written in (Ctx.fq, by tick parity).
+struct FetchEnt {
+  uint32_t s;
+  int32_t inc;
+  uint32_t f;
+  uint32_t info;  // phase | reason << 4 | stage << 8
+  uint32_t d, ver, t0, due, next;
 };
 
 // stats slots (swim_stats order)
@@ -110,7 +123,11 @@ __device__ __forceinline__ bool gossip_infected(const GossipDev& g, uint32_t m) 
 
 // The slab stores a GossipDev in two parts at the same position: 16 hot bytes — all that a gossip
 // round reads for every live gossip (window, sweep, futures, first infected member, receipt key) —
-// and 32 cold bytes read only for the gossips a round actually sends, moves or marks.
+// and 8 cold bytes (the payload record) read only for the gossips a round actually sends or moves:
+// 24 B per GossipState.  GossipState.infected beyond its first member (`more`: only after a
+// collector clear lets a known gossip in again, GossipProtocolImpl.java:205-213 with :217-236) lives
+// in the member's infected-overflow table, keyed by (gossiper, seq), so it does not move when the
+// sweep compacts the slab.
 constexpr uint32_t PER_BITS = 28, PER_MASK = (1u << PER_BITS) - 1;  // infection period: 2^28 rounds
 struct alignas(16) GossipHot {
   uint32_t gossiper, seq;
@@ -120,16 +137,37 @@ struct alignas(16) GossipHot {
   __device__ __forceinline__ uint32_t status() const { return (per_st >> PER_BITS) & 7u; }
   __device__ __forceinline__ bool more() const { return (per_st >> 31) != 0; }
 };
-struct alignas(16) GossipCold {
-  uint32_t subject;
+struct alignas(8) GossipCold {
+  uint32_t subject;  // the record's member, or a user gossip's payload handle
   int32_t inc;
-  uint32_t inf[GINF - 1];  // GossipState.infected after the first, NONE = empty
+};
+static_assert(sizeof(GossipHot) == 16 && sizeof(GossipCold) == 8, "24 B per GossipState");
+// infected-overflow entry: GossipState.infected[1..] of one (gossiper, seq) of one member
+constexpr uint32_t INF_EMPTY = 0xffffffffu, INF_TOMB = 0xfffffffeu;  // gossiper values of free slots
+struct alignas(16) InfOver {
+  uint32_t gossiper, seq;
+  uint32_t inf[GINF - 1];
   uint32_t pad;
 };
-static_assert(sizeof(GossipHot) == 16 && sizeof(GossipCold) == 32, "48 B per GossipState");
+static_assert(sizeof(InfOver) == 32, "32 B per infected overflow");
+// linear probing from the key's hash; a lookup stops at an empty slot, an insert reuses the first
+// tombstone before it.  One writer per member at a time (its delivery thread, or its sender wave's
+// sweep, which only tombstones entries it found).
+__device__ __forceinline__ uint32_t inf_hash(uint32_t g, uint32_t q) { return (g * 0x9e3779b1u) ^ (q * 0x85ebca77u); }
+__device__ inline int32_t inf_find(const InfOver* t, uint32_t mask, uint32_t g, uint32_t q) {
+  for (uint32_t i = 0, h = inf_hash(g, q) & mask; i <= mask; ++i, h = (h + 1) & mask) {
+    const uint32_t k = t[h].gossiper;
+    if (k == INF_EMPTY) return -1;
+    if (k == g && t[h].seq == q) return (int32_t)h;
+  }
+  return -1;
+}
 struct SlabRef {
   GossipHot* hot;
   GossipCold* cold;
+  InfOver* inf;      // the member's infected-overflow table
+  uint32_t inf_mask;
+  uint32_t* err;
   __device__ __forceinline__ GossipDev get(uint32_t p) const {
     const GossipHot h = hot[p];
     const GossipCold k = cold[p];
@@ -142,23 +180,50 @@ struct SlabRef {
     g.inc = k.inc;
     g.inf[0] = h.inf0;
 #pragma unroll
-    for (int i = 1; i < GINF; ++i) g.inf[i] = k.inf[i - 1];
+    for (int i = 1; i < GINF; ++i) g.inf[i] = NONE;
+    if (h.more()) {
+      const int32_t f = inf_find(inf, inf_mask, h.gossiper, h.seq);
+      if (f >= 0)
+#pragma unroll
+        for (int i = 1; i < GINF; ++i) g.inf[i] = inf[f].inf[i - 1];
+    }
     return g;
   }
   __device__ __forceinline__ void put(uint32_t p, const GossipDev& g) const {
     GossipHot h;
     h.gossiper = g.gossiper;
     h.seq = g.seq;
-    h.per_st = (g.inf_period & PER_MASK) | (g.status << PER_BITS) | (g.inf[1] != NONE ? 1u << 31 : 0u);
+    const bool more = g.inf[1] != NONE;
+    h.per_st = (g.inf_period & PER_MASK) | (g.status << PER_BITS) | (more ? 1u << 31 : 0u);
     h.inf0 = g.inf[0];
     GossipCold k;
     k.subject = g.subject;
     k.inc = g.inc;
+    if (more) {
+      int32_t f = inf_find(inf, inf_mask, g.gossiper, g.seq);
+      if (f < 0) {  // a new entry: the first free slot on the probe path
+        for (uint32_t i = 0, x = inf_hash(g.gossiper, g.seq) & inf_mask; i <= inf_mask; ++i, x = (x + 1) & inf_mask)
+          if (inf[x].gossiper == INF_EMPTY || inf[x].gossiper == INF_TOMB) { f = (int32_t)x; break; }
+      }
+      if (f < 0) {
+        atomicOr(err, ERR_INFECTED);  // the member's overflow table is full
+      } else {
+        InfOver o;
+        o.gossiper = g.gossiper;
+        o.seq = g.seq;
 #pragma unroll
-    for (int i = 1; i < GINF; ++i) k.inf[i - 1] = g.inf[i];
-    k.pad = 0;
+        for (int i = 1; i < GINF; ++i) o.inf[i - 1] = g.inf[i];
+        o.pad = 0;
+        inf[f] = o;
+      }
+    }
     hot[p] = h;
     cold[p] = k;
+  }
+  // the sweep dropped a state whose infected list overflowed
+  __device__ __forceinline__ void drop_more(uint32_t g, uint32_t q) const {
+    const int32_t f = inf_find(inf, inf_mask, g, q);
+    if (f >= 0) inf[f].gossiper = INF_TOMB;
   }
 };
 
@@ -281,6 +346,8 @@ struct Ctx {
   uint32_t* remote;
   GossipHot* slab_hot;   // [nl][gcap] (SlabRef)
   GossipCold* slab_cold;  // [nl][gcap]
+  InfOver* inf_over;      // [nl][inf_mask + 1] GossipState.infected beyond the first member
+  uint32_t inf_mask;
   uint32_t* gix;       // [nl][gix_mask + 1] slab serials by (gossiper, seq), open addressing
   uint32_t gix_mask;
   CollEnt* coll;       // [nl][hcap] open addressing by gossiper
@@ -328,6 +395,13 @@ struct Ctx {
   const uint64_t* delay_th;  // [tables][SWIM_DELAY_TICKS_MAX]
   int16_t* default_delay;    // replicated [n]
   uint32_t delay_on;
+  // delayed metadata round trips (allocated with the delay machinery): entries [2][fq_cap] and
+  // per-viewer chain heads / tails [2][nl] by tick parity, entry counts [2]
+  FetchEnt* fq;
+  uint32_t* fq_head;
+  uint32_t* fq_tail;
+  uint32_t* fq_cnt;
+  uint32_t fq_cap;
   uint8_t* is_seed;
   uint32_t* seeds;
   uint32_t n_seeds;
@@ -456,7 +530,7 @@ __device__ __forceinline__ uint32_t* ping_list(const Ctx& c, uint32_t v) { retur
 __device__ __forceinline__ uint32_t* remote_list(const Ctx& c, uint32_t v) { return c.remote + (size_t)(v - c.lo) * c.n; }
 __device__ __forceinline__ SlabRef slab_of(const Ctx& c, uint32_t v) {
   const size_t o = (size_t)(v - c.lo) * c.gcap;
-  return SlabRef{c.slab_hot + o, c.slab_cold + o};
+  return SlabRef{c.slab_hot + o, c.slab_cold + o, c.inf_over + (size_t)(v - c.lo) * (c.inf_mask + 1), c.inf_mask, c.err};
 }
 __device__ __forceinline__ bool owned(const Ctx& c, uint32_t v) { return v - c.lo < c.nl; }
 __device__ __forceinline__ uint32_t owner(const Ctx& c, uint32_t v) { return v / c.sz; }
@@ -999,23 +1073,59 @@ __device__ inline void schedule_timer(const Ctx& c, uint32_t v, uint32_t s) {
 }
 
 // ------------------------------------------------------------------------------- metadata fetch
-// MetadataStoreImpl.fetchMetadata (:146-185) + onMetadataRequest (:201-240): one round trip.
-__device__ inline bool fetch_ok(const Ctx& c, uint32_t v, uint32_t s, uint32_t phase) {
-  uint32_t f = mem(c, v).fetch_ctr++;
+// MetadataStoreImpl.fetchMetadata (:146-185) round trip + onMetadataRequest (:201-240), with the
+// NetworkEmulator's arrival-time semantics: the request is lost or refused at its send and meets the
+// subject's transport (stopped, inbound filter) when it arrives; the response likewise; the round
+// trip must end before metadataTimeout (:160-165).  fetch_start returns true when the response is in
+// within the calling phase (no delay on either leg: the caller applies the admission at its flush
+// point); a delayed round trip is queued and completes in the FETCH phase of its arrival tick
+// (k_fetch_due).  The oracle's fetch_start / fetch_stage1 / fetch_stage2 are the same steps.
+__device__ inline void fq_push(const Ctx& c, uint32_t v, FetchEnt e) {
+  const uint32_t p = (uint32_t)c.T & 1u;  // the queue written during tick T, read by tick T + 1
+  const uint32_t slot = atomicAdd(&c.fq_cnt[p], 1u);
+  if (slot >= c.fq_cap) { set_err(c, ERR_FETCHQ); return; }
+  e.next = NONE;
+  FetchEnt* q = c.fq + (size_t)p * c.fq_cap;
+  q[slot] = e;
+  const size_t li = (size_t)p * c.nl + (v - c.lo);
+  if (c.fq_head[li] == NONE) c.fq_head[li] = slot;
+  else q[c.fq_tail[li]].next = slot;
+  c.fq_tail[li] = slot;
+}
+// the request arrives at d (now): 0 = the round trip failed, 1 = the response arrived too (no delay on
+// it), 2 = the response is in flight (e.due = its arrival tick)
+__device__ inline int fetch_stage1(const Ctx& c, uint32_t v, FetchEnt& e) {
+  const uint32_t d = e.d, phase = e.info & 15u;
+  if (!c.up[d] || !in_pass(c, d, v)) return 0;
+  Ctx c0 = c;  // draws keyed by the issue tick
+  c0.T = e.t0;
+  if (out_fail(c0, d, v, v, SWIM_STREAM_FETCH_RESP, phase, e.f)) return 0;
+  const uint32_t d2 = delay_ticks(c0, d, v, v, SWIM_STREAM_FETCH_RESP_DELAY, phase, e.f);
+  if ((uint64_t)((uint32_t)c.T - e.t0 + d2) * c.tick_ms >= (uint64_t)c.metadata_timeout) return 0;
+  e.ver = c.meta_ver[e.s];  // the metadata the response carries
+  e.info = (e.info & 0xffu) | (2u << 8);
+  e.due = (uint32_t)c.T + d2;
+  if (d2 == 0) return c.up[v] && in_pass(c, v, d) ? 1 : 0;
+  return 2;
+}
+__device__ inline bool fetch_start(const Ctx& c, uint32_t v, uint32_t s, int32_t inc, int reason, uint32_t phase) {
+  const uint32_t f = mem(c, v).fetch_ctr++;
   stat_add(c, ST_FETCHES, 1);
   // the request goes to s's address; another member listening there does not answer (:209)
   const uint32_t d = dst(c, s);
-  bool ok = d == s && !out_fail(c, v, d, v, SWIM_STREAM_FETCH_REQ, phase, f) && in_pass(c, d, v) &&
-            !out_fail(c, d, v, v, SWIM_STREAM_FETCH_RESP, phase, f) && in_pass(c, v, d);
-  // requestResponse(...).timeout(metadataTimeout) (:160-165): both legs delayed (tryDelayOutbound on
-  // the request and on the response's send)
-  if (ok && c.delay_on) {
-    const uint64_t rtt = (uint64_t)delay_ticks(c, v, d, v, SWIM_STREAM_FETCH_REQ_DELAY, phase, f) +
-                         delay_ticks(c, d, v, v, SWIM_STREAM_FETCH_RESP_DELAY, phase, f);
-    ok = rtt * c.tick_ms < (uint64_t)c.metadata_timeout;
+  if (d != s || out_fail(c, v, d, v, SWIM_STREAM_FETCH_REQ, phase, f)) return false;
+  const uint32_t d1 = delay_ticks(c, v, d, v, SWIM_STREAM_FETCH_REQ_DELAY, phase, f);
+  if ((uint64_t)d1 * c.tick_ms >= (uint64_t)c.metadata_timeout) return false;
+  FetchEnt e;
+  e.s = s; e.inc = inc; e.f = f; e.info = phase | ((uint32_t)reason << 4) | (1u << 8);
+  e.d = d; e.ver = 0; e.t0 = (uint32_t)c.T; e.due = (uint32_t)c.T + d1; e.next = NONE;
+  if (d1 == 0) {
+    const int r = fetch_stage1(c, v, e);
+    if (r == 1) stat_add(c, ST_FETCH_OK, 1);
+    if (r != 2) return r == 1;
   }
-  if (ok) stat_add(c, ST_FETCH_OK, 1);
-  return ok;
+  fq_push(c, v, e);
+  return false;
 }
 
 // ------------------------------------------------------------------------------- updateMembership
@@ -1082,21 +1192,21 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
     }
     return false;
   }
-  if (!present || inc0 < inc1) return fetch_ok(c, v, s, phase);
+  if (!present || inc0 < inc1) return fetch_start(c, v, s, inc1, reason, phase);
   return false;
 }
 
-// doOnSuccess of the metadata fetch (:648-656) + onAliveMemberDetected (:769-795)
-__device__ inline void apply_alive(const Ctx& c, uint32_t v, uint32_t s, int32_t inc1, int reason, uint32_t phase) {
+// doOnSuccess of the metadata fetch (:648-656) + onAliveMemberDetected (:769-795); ver = the
+// subject's metadata version the response carried
+__device__ inline void apply_alive(const Ctx& c, uint32_t v, uint32_t s, int32_t inc1, int reason, uint32_t phase,
+                                   uint32_t ver) {
   MemberDev& m = mem(c, v);
   // cancelSuspicionTimeoutTask
   uint64_t cell = cell_get(c, v, s) & ~B_HAS_TIMER;
-  // metadataStore.updateMetadata(member, metadata1) returns metadata0 (null when none is stored);
-  // metadata1 is the subject's metadata now (the fetch answers within the tick)
+  // metadataStore.updateMetadata(member, metadata1) returns metadata0 (null when none is stored)
   bool same_meta = c_has(cell, B_HAS_METADATA);
   if (c.meta_seen) {
     uint32_t& seen = c.meta_seen[(size_t)(v - c.lo) * c.n + s];
-    const uint32_t ver = c.meta_ver[s];
     same_meta = same_meta && seen == ver;
     seen = ver;
   }
@@ -1111,6 +1221,11 @@ __device__ inline void apply_alive(const Ctx& c, uint32_t v, uint32_t s, int32_t
   if (!exists) publish_event(c, v, s, SWIM_EV_ADDED, phase, next_minor(c, v, phase, s));
   else if (!same_meta)  // !metadata1.equals(metadata0) (:780-781)
     publish_event(c, v, s, SWIM_EV_UPDATED, phase, next_minor(c, v, phase, s));
+}
+
+// a round trip answered within the phase: metadata1 is the subject's metadata now
+__device__ inline void apply_alive(const Ctx& c, uint32_t v, uint32_t s, int32_t inc1, int reason, uint32_t phase) {
+  apply_alive(c, v, s, inc1, reason, phase, c.meta_ver[s]);
 }
 
 // Collections.shuffle: for (i = size; i > 1; i--) swap(i-1, nextInt(i))

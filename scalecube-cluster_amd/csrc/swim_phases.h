@@ -29,10 +29,17 @@ __device__ unsigned long long g_dbg[16];
   do {                                                           \
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_dbg[slot], (val)); \
   } while (0)
+// wave time of a section that runs with some lanes inactive: added by the wave's first active lane
+#define PPROF_WADD(slot, t0)                                                                          \
+  do {                                                                                               \
+    if ((threadIdx.x & 63) == (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1)                 \
+      atomicAdd(&g_dbg[slot], __builtin_amdgcn_s_memrealtime() - (t0));                              \
+  } while (0)
 #else
 #define PPROF_T0(v)
 #define PPROF_ADD(slot, t0)
 #define PPROF_CNT(slot, val)
+#define PPROF_WADD(slot, t0)
 #endif
 
 // per-tick scratch counters, zeroed by one hipMemsetAsync at the start of every tick
@@ -723,8 +730,8 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   bool done = false;
   // lane = slab position: one GossipState read serves all nt targets, whose loss draws and
   // receiver checks are independent (issued together); messages keep the (target, position) keys.
-  // A pass reads the 16 hot bytes of each state; the 32 cold ones only where a message is
-  // materialised, the first-infected check is not enough, or the entry moves.
+  // A pass reads the 16 hot bytes of each state; the 8 cold ones only where a message is
+  // materialised or the entry moves (the infected overflow only for a state that has one).
   // the next pass's hot bytes are loaded while this pass runs (the sweep writes only positions at
   // or below the current pass's)
   GossipHot hn{};
@@ -789,15 +796,22 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         return (win && jj < nt) ? c.gbits[(size_t)sl * c.gwords + (i >> 5)] : 0u;
       };
       const uint32_t wb0 = rword(0), wb1 = rword(1), wb2 = rword(2), wb3 = rword(3);
+      // GossipState.infected beyond its first member (rare: the overflow table, once per pass)
+      uint32_t xinf[GINF - 1];
+#pragma unroll
+      for (int q = 0; q < GINF - 1; ++q) xinf[q] = NONE;
+      if (win && h.more()) {
+        const int32_t f = inf_find(slab.inf, slab.inf_mask, h.gossiper, h.seq);
+        if (f >= 0)
+#pragma unroll
+          for (int q = 0; q < GINF - 1; ++q) xinf[q] = slab.inf[f].inf[q];
+      }
       uint32_t probe = 0;  // bit j: target j's collector must be probed (its receipt bit does not answer)
       for (uint32_t j = 0; j < nt; ++j) {
         const uint32_t t = s_t[1 + j], tm = s_t[17 + j];
         bool infected = h.inf0 == tm;
-        if (win && !infected && h.more()) {  // GossipState.infected beyond its first member
-          const GossipCold k = slab.cold[p];
 #pragma unroll
-          for (int q = 0; q < GINF - 1; ++q) infected |= k.inf[q] == tm;
-        }
+        for (int q = 0; q < GINF - 1; ++q) infected |= xinf[q] == tm;
         const bool send = win && !infected;
         nmsg += send ? 1u : 0u;
         // delivered copies; a receiver on this shard that already holds the sequence id drops it
@@ -914,6 +928,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     const bool wb = keep && (to != p || changed);
     GossipCold kc{};
     if (wb && to != p) kc = slab.cold[p];
+    if (p < glen && !keep && h.more()) slab.drop_more(h.gossiper, h.seq);  // its infected overflow goes too
     // the next pass's hot bytes have arrived by now: its in-window gossips' receipt slots and the
     // first targets' receipt words are loaded here, so that the next pass's check hits the cache
     if (p + 64 < glen && (uint64_t)hn.inf_period() + spread >= period) {
@@ -1246,6 +1261,9 @@ __device__ __forceinline__ uint64_t msg_key(const Ctx& c, const GMsgFull& m) {
 // onGossipReq starts with, so that they hit the cache (values are re-read, never trusted: the current
 // message may change them).  Returns a value the caller folds into a sink that is never true.
 __device__ __forceinline__ uint32_t warm_gossip_req(const Ctx& c, uint32_t r, const CollEnt* cbase, const GMsgFull& g) {
+#ifdef SWIM_DLV_NO_WARM  // (profiling A/B builds only)
+  return 0;
+#endif
   uint32_t x = cbase[hash32(g.gossiper) & (c.hcap - 1)].key;
   x ^= (uint32_t)c.gslot[gslot_of(gkey(g.gossiper, g.seq))].key;
   if (g.status() < SWIM_GOSSIP_USER && g.subject < c.n) {
@@ -1258,11 +1276,17 @@ __device__ __forceinline__ uint32_t warm_gossip_req(const Ctx& c, uint32_t r, co
 // onGossipReq (GossipProtocolImpl.java:201-215) for one received message, in canonical order
 __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, const SlabRef& slab, const GMsgFull& g) {
   if (g.dup()) return false;  // the collector held it on arrival and only grows until now
+  PPROF_T0(ta);
   CollEnt* col = coll_ensure(c, r, g.gossiper);
   if (!col) return false;
   const bool was_cleared = (col->meta & COLL_CLEARED) != 0;
-  if (!coll_add(c, col, g.seq, &c.seg_flag[r - c.lo])) return false;
+  const bool added = coll_add(c, col, g.seq, &c.seg_flag[r - c.lo]);
+  PPROF_WADD(6, ta);
+  if (!added) return false;
+  PPROF_T0(tb);
   receipt_mark(c, r, g.gossiper, g.seq);
+  PPROF_WADD(7, tb);
+  PPROF_T0(tc);
   // a GossipState can outlive its collector entry only after a clear
   const int32_t found = was_cleared ? gix_find(c, m, r, slab, g.gossiper, g.seq) : -1;
   if (found < 0) {
@@ -1277,11 +1301,14 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, con
     if (gs.period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
     slab.put(gs.len++, ns);
     gix_note(c, m, r, ns.gossiper, ns.seq);
+    PPROF_WADD(8, tc);
+    PPROF_T0(td);
     if (g.status() >= SWIM_GOSSIP_USER)  // sink.next(gossip.message()) (:209): listen() subscribers
       emit(c, r, g.gossiper, SWIM_EV_GOSSIP, SWIM_PHASE_GOSSIP, m.ev_minor++, g.subject);
     // onMembershipGossip (MembershipProtocolImpl.java:452-459)
     else if (update_membership(c, r, g.subject, g.status(), g.inc(), R_GOSSIP, SWIM_PHASE_GOSSIP))
       apply_alive(c, r, g.subject, g.inc(), R_GOSSIP, SWIM_PHASE_GOSSIP);
+    PPROF_WADD(9, td);
   } else {
     GossipDev st = slab.get((uint32_t)found);
     if (!gossip_infected(st, g.from)) {
@@ -1418,12 +1445,10 @@ __device__ inline unsigned long long deliver_sorted(const Ctx& c, uint32_t r, co
   return acc;
 }
 
-constexpr uint32_t BIG_FO = 256;  // ranks of a big inbox whose (gossiper, seq) the first-occurrence pass compares
 struct BigLds {  // per wave
   uint32_t snd[BIG_MAXD];  // distinct senders (found order, then ascending)
   uint32_t cnt[BIG_MAXD];  // their message counts, then running inbox bases
   uint32_t iP[64], iS[64], iR[64];  // apply_ins_batch scratch
-  uint2 fo[BIG_FO];        // (gossiper, seq) of the inbox's first BIG_FO messages in rank order
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -1544,53 +1569,6 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
   return k;
 }
 
-// The first-occurrence pass over a ranked big inbox (all lanes on one inbox): onGossipReq
-// (GossipProtocolImpl.java:201-215) changes state only for a message whose sequence id its
-// receiver's collector does not hold yet, and a collector only grows during delivery, so a message
-// can be accepted only if it is (a) not flagged as a provable duplicate, (b) not held by the
-// collector before the delivery, and (c) the first copy of its (gossiper, seq) in canonical order.
-// (a) and (b) are per message; (c) compares the first BIG_FO ranks pairwise in LDS (a later copy
-// beyond them is rejected by the collector in the chain, as before).  The candidates' inbox
-// positions are compacted in rank order to the front of pg_perm; the count is returned, and *nfresh
-// gets the messages not flagged.
-__device__ uint32_t accept_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L,
-                                     uint32_t& nfresh) {
-  const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
-  const uint32_t r_mem = c.lo + i;
-  auto perm_at = [&](uint32_t q) -> uint32_t& { return b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)]; };
-  uint32_t nacc = 0;
-  for (uint32_t r0 = 0; r0 < k; r0 += 64) {
-    const uint32_t r = r0 + lane;
-    uint32_t q = NONE;
-    GMsgFull g{};
-    bool ok = false;
-    if (r < k) {
-      q = perm_at(r);
-      if (q < k) {
-        g = b.pg_msgs[(size_t)pt[q >> 6] * 64 + (q & 63)];
-        ok = !g.dup();
-        nfresh += ok ? 1u : 0u;
-      } else {
-        set_err(c, ERR_MSGS);  // a hole: only after an inbox overflow
-      }
-      if (r < BIG_FO) L.fo[r] = make_uint2(q < k ? g.gossiper : NONE, q < k ? g.seq : NONE);
-    }
-    if (ok) ok = !coll_contains(c, coll_find(c, r_mem, g.gossiper), g.seq);
-    wave_sync();
-    if (ok && r < BIG_FO)
-      for (uint32_t j = 0; j < r; ++j) {
-        const uint2 o = L.fo[j];
-        if (o.x == g.gossiper && o.y == g.seq) { ok = false; break; }
-      }
-    const uint64_t mk = __ballot(ok);
-    // compaction in place: every lane has read its rank's entry, and the writes go to ranks <= r
-    if (ok) perm_at(nacc + lanes_below(mk)) = q;
-    nacc += (uint32_t)__popcll(mk);
-    wave_sync();
-  }
-  return nacc;
-}
-
 __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, const Bufs& b, const uint32_t* list,
                                                 uint32_t nb, uint32_t lane, int collect, BigLds& L,
                                                 unsigned long long& nsync, uint32_t& nmsg, uint32_t& nfresh) {
@@ -1599,7 +1577,7 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
   PPROF_T0(tp0);
   PPROF_CNT(4, 1ull);
   PPROF_CNT(5, (unsigned long long)nb);
-  uint32_t my_k = 0, my_n = 0, my_pages = 0;
+  uint32_t my_k = 0, my_pages = 0;
   for (uint32_t j = 0; j < nb; ++j) {
     const uint32_t i = list[j];
     const uint32_t r = c.lo + i;
@@ -1614,16 +1592,12 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) pages_ok &= pt[pg] < b.pg_cap;
     pages_ok = __ballot(!pages_ok) == 0;
     const bool go = c.up[r] && k && pages_ok;
-    uint32_t nacc = 0, nf = 0;
     if (go) {
       rank_big_inbox(c, b, i, k, lane, L);
-      nacc = accept_big_inbox(c, b, i, k, lane, L, nf);
       nmsg += lane == 0 ? k : 0u;
-      nfresh += nf;
     }
     if (lane == j) {
-      my_k = go ? nacc : 0;  // the chain walks the candidates only
-      my_n = k;
+      my_k = go ? k : 0;
       my_pages = (k + 63) / 64;
     }
   }
@@ -1643,7 +1617,7 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     // chain's own dependent round trips are the cost of a big inbox
     auto fetch = [&](uint32_t q) -> GMsgFull {
       uint32_t jq = b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)];
-      if (jq >= my_n) {  // a hole: only after an inbox overflow (ERR_MSGS is set)
+      if (jq >= my_k) {  // a hole: only after an inbox overflow (ERR_MSGS is set)
         set_err(c, ERR_MSGS);
         jq = q;
       }
@@ -1658,6 +1632,7 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
         next = fetch(q + 1);
         sink ^= warm_gossip_req(c, r, cbase, next);
       }
+      nfresh += g.dup() ? 0u : 1u;
       if (on_gossip_req(c, r, m, slab, g)) acc++;
     }
     if (sink == 0x5bd1e995u && my_k == 0x7fffffffu) set_err(c, 0u);  // keeps the warming loads; sets no bit
@@ -2223,6 +2198,48 @@ __device__ void rebase_witness(const Ctx& c) {
 }
 
 // start0's doFinally (:285-289) for members that joined this tick; graceful leaves complete.
+// ---- FETCH phase (message delay only): the delayed GET_METADATA legs arriving this tick, thread per
+// owned viewer walking its chain of the previous tick's queue in issue order — a leg not due yet or a
+// response now in flight moves to this tick's queue, a completed round trip is the fetch's doOnSuccess
+// (apply_alive, events of SWIM_PHASE_FETCH) — then the workgroup applies the pingMembers inserts of its
+// viewers.  A stopped viewer's round trips are void.  Oracle: phase_fetch.
+__global__ void __launch_bounds__(256) k_fetch_due(KP) {
+  const Ctx c = pctx(P, T);
+  __shared__ uint32_t s_iP[256], s_iS[256], s_iR[256], s_list[256], s_n;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  if (i < c.nl) {
+    const uint32_t pn = (uint32_t)T & 1u, po = pn ^ 1u;
+    uint32_t cur = c.fq_head[(size_t)po * c.nl + i];
+    c.fq_head[(size_t)pn * c.nl + i] = NONE;
+    const uint32_t v = c.lo + i;
+    if (cur != NONE && c.up[v]) {
+      const FetchEnt* q = c.fq + (size_t)po * c.fq_cap;
+      mem(c, v).ev_minor = 0;
+      for (uint32_t guard = 0; cur != NONE && guard < c.fq_cap; ++guard) {
+        if (cur >= c.fq_cap) { set_err(c, ERR_FETCHQ); break; }
+        FetchEnt e = q[cur];
+        cur = e.next;
+        if (e.due > (uint32_t)T) {
+          fq_push(c, v, e);
+          continue;
+        }
+        const int r = (e.info >> 8) == 1u ? fetch_stage1(c, v, e) : (in_pass(c, v, e.d) ? 1 : 0);
+        if (r == 2) fq_push(c, v, e);
+        if (r == 1) {
+          stat_add(c, ST_FETCH_OK, 1);
+          apply_alive(c, v, e.s, e.inc, (int)((e.info >> 4) & 15u), SWIM_PHASE_FETCH, e.ver);
+        }
+      }
+      if (mem(c, v).ins_rank) s_list[atomicAdd(&s_n, 1u)] = v;
+    }
+  }
+  __syncthreads();
+  const uint32_t nv = s_n;
+  for (uint32_t k = 0; k < nv; ++k) apply_ins_batch<256, true>(c, s_list[k], threadIdx.x, s_iP, s_iS, s_iR);
+}
+
 __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
   const Ctx c = pctx(P, T);
   Counters* k = P->b.k;
@@ -2240,6 +2257,8 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
     }
     if (i == 0) b.snap_cnt[par ^ 1u] = 0;
     if (i == 0 && c.delay_on) b.dq_cnt[(uint32_t)T & DQ_MASK] = 0;  // this tick's delayed arrivals are delivered
+    // the metadata queue read by this tick's FETCH phase is written next during tick T + 1
+    if (i == 0 && c.fq) c.fq_cnt[((uint32_t)T & 1u) ^ 1u] = 0;
   }
   // collector blocks freed this tick become allocatable: tier t by workgroup t (the counters are
   // read, then rewritten, by the same threads), all tiers by workgroup 0 in a grid of fewer than 5

@@ -5,7 +5,7 @@
 
 g_dbg slots: 0 big-inbox ranking, 1 big-inbox onGossipReq chains, 2 big-inbox tail (page reset,
 pingMembers inserts, SYNC collection), 3 small inboxes + their collection (every wave), 4 batches,
-5 big inboxes.  Times are per-wave sums (100 MHz ticks); divided by the waves of a launch they give
+5 big inboxes, 6-9 onGossipReq sections (collector, receipt, slab, updateMembership).  Times are per-wave sums (100 MHz ticks); divided by the waves of a launch they give
 each part's share of a launch."""
 import argparse
 import json
@@ -52,6 +52,10 @@ def main():
     print(json.dumps({"workload": args.workload, "window_s": dt, "deliver_ms_per_launch": dp["total_ms"] / max(1, dp["launches"]),
                       "big_rank_us": per(d[0]), "big_chain_us": per(d[1]), "big_tail_us": per(d[2]),
                       "small_and_collect_us": per(d[3]), "batches": d[4], "big_inboxes": d[5],
+                      # onGossipReq sections (every path; wave time, first active lane): collector
+                      # ensure + add, receipt mark, slab put + index, updateMembership
+                      "ogr_collector_us": per(d[6]), "ogr_receipt_us": per(d[7]), "ogr_slab_us": per(d[8]),
+                      "ogr_update_us": per(d[9]),
                       "messages_per_launch": dp["messages"] / max(1, dp["launches"])}))
 
 
