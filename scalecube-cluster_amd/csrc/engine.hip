@@ -962,6 +962,9 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.pg_max = std::min<uint32_t>(b.pg_max, 1u << 14);
   b.req_cap = std::max<uint32_t>(1u << 12, 4 * n);
   b.wave_min = cf.deliver_wave_min ? std::min<uint32_t>(cf.deliver_wave_min, DLV_SORT) : (uint32_t)DLV_SORT;
+  b.coop_min = COOP_MIN;
+  if (const char* cm = std::getenv("SWIM_DEBUG_COOP_MIN"))  // tests: the whole-wave path for small inboxes too
+    if (std::atoi(cm) > 0) b.coop_min = (uint32_t)std::atoi(cm);
   b.dq_bcap = 0;  // the delay ring is allocated when a delay is first set (swim_set_*_delay)
   // snapshot rows for members that both send and receive a SYNC in one tick (at most two each: the
   // SYNC content and, when its merges changed the row, the SYNC_ACK content): a few per tick in

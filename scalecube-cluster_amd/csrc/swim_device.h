@@ -235,7 +235,7 @@ struct SlabRef {
 // The reference keeps up to gossipSegmentationThreshold (1,000) intervals before a gossip round
 // clears the collector (checkGossipSegmentation, GossipProtocolImpl.java:217-236); the top tier
 // leaves room for a round's growth beyond that.  Freed blocks are recycled from the next tick on.
-struct CollEnt {
+struct alignas(16) CollEnt {
   uint32_t key;   // gossiper + 1; 0 = empty slot
   uint32_t lo, hi;
   uint32_t meta;  // bits 0..2: inline interval count (0 / 1) or COLL_SPILLED; bit 3: cleared;
@@ -655,6 +655,50 @@ __device__ inline CollEnt* coll_ensure(const Ctx& c, uint32_t v, uint32_t gossip
   set_err(c, ERR_HASH);
   return nullptr;
 }
+// coll_ensure that also returns the entry's value (each probe one 16-B load; a new entry is the
+// value it was initialised with)
+__device__ inline CollEnt* coll_ensure_v(const Ctx& c, uint32_t v, uint32_t gossiper, CollEnt& out) {
+  CollEnt* base = c.coll + (size_t)(v - c.lo) * c.hcap;
+  uint32_t mask = c.hcap - 1, h = hash32(gossiper) & mask, key = gossiper + 1;
+  for (uint32_t i = 0; i < c.hcap; ++i) {
+    CollEnt* e = base + ((h + i) & mask);
+    const CollEnt x = *e;
+    if (x.key == key) { out = x; return e; }
+    if (x.key == 0) {
+      CollEnt ne;
+      ne.key = key; ne.lo = 0; ne.hi = 0; ne.meta = 0;
+      *e = ne;
+      out = ne;
+      return e;
+    }
+  }
+  set_err(c, ERR_HASH);
+  return nullptr;
+}
+// coll_ensure_v for lanes of one wave inserting different gossipers into one member's table at once:
+// an empty slot is claimed with a compare-and-swap (a lane that loses it probes on)
+__device__ inline CollEnt* coll_ensure_cas(const Ctx& c, uint32_t v, uint32_t gossiper, CollEnt& out) {
+  CollEnt* base = c.coll + (size_t)(v - c.lo) * c.hcap;
+  uint32_t mask = c.hcap - 1, h = hash32(gossiper) & mask, key = gossiper + 1;
+  for (uint32_t i = 0; i < c.hcap; ++i) {
+    CollEnt* e = base + ((h + i) & mask);
+    const CollEnt x = *e;
+    if (x.key == key) { out = x; return e; }
+    if (x.key == 0) {
+      const uint32_t prev = atomicCAS(&e->key, 0u, key);
+      if (prev == 0u) {
+        e->lo = 0;
+        e->hi = 0;
+        e->meta = 0;
+        out.key = key; out.lo = 0; out.hi = 0; out.meta = 0;
+        return e;
+      }
+      if (prev == key) { out = *e; return e; }
+    }
+  }
+  set_err(c, ERR_HASH);
+  return nullptr;
+}
 // ---- spilled-collector blocks.  Tier-indexed Ctx members are read through selects, never a runtime
 // array index: indexing an array member of the kernel's register-resident Ctx copy with a runtime
 // value spills the whole Ctx to scratch (measured: 520-660 B/lane in every collector kernel).
@@ -737,10 +781,12 @@ __device__ inline uint32_t coll_known4(const Ctx& c, const uint32_t* tg, uint32_
   return known;
 }
 // SequenceIdCollector.add (SequenceIdCollector.java:43-72).  `seg` (the viewer's segmentation flag)
-// is raised when the collector ends up with more than c.seg_threshold intervals.
-__device__ inline bool coll_add(const Ctx& c, CollEnt* e, uint32_t x, uint32_t* seg = nullptr) {
+// is raised when the collector ends up with more than c.seg_threshold intervals.  `pre`: the entry's
+// current value when the caller holds it already (coll_ensure_v), so no load waits on it.
+__device__ inline bool coll_add(const Ctx& c, CollEnt* e, uint32_t x, uint32_t* seg = nullptr,
+                                const CollEnt* pre = nullptr) {
   if (!e) return true;
-  uint32_t meta = e->meta;
+  uint32_t meta = pre ? pre->meta : e->meta;
   const uint32_t n0 = meta & 7u;
   if (n0 == 0) {
     e->lo = e->hi = x;
@@ -748,16 +794,18 @@ __device__ inline bool coll_add(const Ctx& c, CollEnt* e, uint32_t x, uint32_t* 
     return true;
   }
   if (n0 == 1) {
-    if (e->lo <= x && x <= e->hi) return false;
-    if ((int64_t)x == (int64_t)e->hi + 1) { e->hi = x; return true; }
-    if ((int64_t)x + 1 == (int64_t)e->lo) { e->lo = x; return true; }
+    const uint32_t elo = pre ? pre->lo : e->lo, ehi = pre ? pre->hi : e->hi;
+    if (elo <= x && x <= ehi) return false;
+    if ((int64_t)x == (int64_t)ehi + 1) { e->hi = x; return true; }
+    if ((int64_t)x + 1 == (int64_t)elo) { e->lo = x; return true; }
+    const uint32_t lo0 = elo, hi0 = ehi;
     // a second disjoint interval: spill to the smallest tier
     const uint32_t i = spill_alloc(c, 0);
     if (i == NONE) return true;
     uint32_t* blk = c.spill[0] + (size_t)i * tier_words(0);
     uint2* iv = reinterpret_cast<uint2*>(blk + 4);
-    if (x < e->lo) { iv[0] = make_uint2(x, x); iv[1] = make_uint2(e->lo, e->hi); }
-    else { iv[0] = make_uint2(e->lo, e->hi); iv[1] = make_uint2(x, x); }
+    if (x < lo0) { iv[0] = make_uint2(x, x); iv[1] = make_uint2(lo0, hi0); }
+    else { iv[0] = make_uint2(lo0, hi0); iv[1] = make_uint2(x, x); }
     blk[0] = 2;
     e->meta = (meta & COLL_CLEARED) | COLL_SPILLED | (i << 8);
     if (seg && 2 > (uint32_t)c.seg_threshold) *seg = 1;
@@ -828,7 +876,9 @@ __device__ inline void receipt_mark(const Ctx& c, uint32_t r, uint32_t gossiper,
   if (c.gslot[sl].key == key) {
     const uint32_t i = r - c.lo;
     atomicOr(&c.gbits[(size_t)sl * c.gwords + (i >> 5)], 1u << (i & 31));
-  } else if (atomicCAS(reinterpret_cast<unsigned long long*>(&c.gpend[sl]), 0ull, (unsigned long long)key) == 0ull) {
+  } else if (c.gpend[sl] == 0ull &&  // (a plain read first: once claimed, the thousands of receivers of a
+                                     // new gossip skip the contended compare-and-swap)
+             atomicCAS(reinterpret_cast<unsigned long long*>(&c.gpend[sl]), 0ull, (unsigned long long)key) == 0ull) {
     const uint32_t par = (uint32_t)(c.T & 1);
     c.gclaim[par * GSLOTS + atomicAdd(&c.gclaim_cnt[par], 1u)] = sl;  // at most one entry per slot
   }
@@ -943,6 +993,13 @@ __device__ __forceinline__ void gix_note(const Ctx& c, MemberDev& m, uint32_t v,
   if (2 * m.gix_used >= c.gix_mask + 1) { m.gix_valid = 0; return; }
   const uint32_t len = gsched(c, v).len;
   gix_put(c, m, len, gix_of(c, v), g, s, m.gix_base + len - 1);
+}
+// a gossip was written at slab position pos (the whole-wave delivery, which appends several at once)
+__device__ __forceinline__ void gix_note_at(const Ctx& c, MemberDev& m, uint32_t v, uint32_t g, uint32_t s, uint32_t pos,
+                                            uint32_t len) {
+  if (!m.gix_valid) return;
+  if (2 * m.gix_used >= c.gix_mask + 1) { m.gix_valid = 0; return; }
+  gix_put(c, m, len, gix_of(c, v), g, s, m.gix_base + pos);
 }
 // slab position of (g, s), or -1
 __device__ inline int32_t gix_find(const Ctx& c, MemberDev& m, uint32_t v, const SlabRef& slab, uint32_t g,

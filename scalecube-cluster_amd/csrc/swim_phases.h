@@ -111,6 +111,7 @@ struct Bufs {
   uint32_t* big_list;  // local indices of receivers with big inboxes (the writer that crosses wave_min)
   uint32_t* big_tick;  // per receiver: tick whose inbox took the wave-parallel path
   uint32_t wave_min;   // inboxes above this many messages take it (<= DLV_SORT)
+  uint32_t coop_min;   // big inboxes of at least this many messages are delivered by the whole wave
   // GOSSIP_REQs delayed by the network emulator (swim_delay.h): bucket (arrival tick & DQ_MASK) holds
   // up to dq_bcap messages, .pad = the sending tick; released into the inboxes by k_dq_release
   GMsgFull* dq;        // [DQ_BUCKETS][dq_bcap]
@@ -1265,7 +1266,8 @@ __device__ __forceinline__ uint32_t warm_gossip_req(const Ctx& c, uint32_t r, co
   return 0;
 #endif
   uint32_t x = cbase[hash32(g.gossiper) & (c.hcap - 1)].key;
-  x ^= (uint32_t)c.gslot[gslot_of(gkey(g.gossiper, g.seq))].key;
+  const uint32_t sl = gslot_of(gkey(g.gossiper, g.seq));
+  x ^= (uint32_t)c.gslot[sl].key ^ (uint32_t)c.gpend[sl];
   if (g.status() < SWIM_GOSSIP_USER && g.subject < c.n) {
     const size_t i = (size_t)(r - c.lo) * c.n + g.subject;
     x ^= c.recs[i] ^ c.aux[i] ^ c.ref[g.subject];
@@ -1277,10 +1279,11 @@ __device__ __forceinline__ uint32_t warm_gossip_req(const Ctx& c, uint32_t r, co
 __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, const SlabRef& slab, const GMsgFull& g) {
   if (g.dup()) return false;  // the collector held it on arrival and only grows until now
   PPROF_T0(ta);
-  CollEnt* col = coll_ensure(c, r, g.gossiper);
+  CollEnt cv;
+  CollEnt* col = coll_ensure_v(c, r, g.gossiper, cv);
   if (!col) return false;
-  const bool was_cleared = (col->meta & COLL_CLEARED) != 0;
-  const bool added = coll_add(c, col, g.seq, &c.seg_flag[r - c.lo]);
+  const bool was_cleared = (cv.meta & COLL_CLEARED) != 0;
+  const bool added = coll_add(c, col, g.seq, &c.seg_flag[r - c.lo], &cv);
   PPROF_WADD(6, ta);
   if (!added) return false;
   PPROF_T0(tb);
@@ -1569,6 +1572,176 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
   return k;
 }
 
+// Whole-wave delivery of one big inbox (k >= b.coop_min ranked messages): the same onGossipReq
+// sequence (GossipProtocolImpl.java:201-215) as the lane chain, 64 ranks at a time.
+//  (a) collectors: each gossiper of the chunk gets one leader lane, which adds its lanes' sequence ids
+//      in rank order (a collector's intervals — and the segmentation flag — see the same sequence of
+//      adds as in the chain); leaders of different gossipers run side by side (new table entries are
+//      claimed by compare-and-swap).  A lane whose add fails holds a copy the collector already had:
+//      rejected, as in the chain.  Messages of the member's own gossips, and of gossipers whose
+//      collector was cleared (a GossipState may outlive it: the gix lookup), take the chain's own
+//      onGossipReq at their turn in (c) instead.
+//  (b) receipt marks of the accepted lanes; then which accepted records cannot change the view: the
+//      namespace filter drops them, or they do not override the subject's record as it stands after
+//      the earlier chunks and no earlier lane of the chunk may change that subject
+//      (MembershipRecord.isOverrides, updateMembership :593-602) — their onMembershipGossip is a no-op.
+//  (c) in rank order, lane by lane, the others: slab position and state, then onMembershipGossip (or
+//      the user gossip's listen() event) — which may spread gossips (slab appends) and emit events;
+//      the no-op lanes between them take the next positions and write their states together.
+// Returns this lane's share of the accepted messages; nfresh counts those not flagged as provable
+// duplicates (per lane as well).
+constexpr uint32_t COOP_MIN = 64;  // Bufs.coop_min's default
+__device__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L,
+                                           uint32_t& nfresh) {
+  const uint32_t r = c.lo + i;
+  const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
+  MemberDev& m = mem(c, r);
+  GossipSched& gsr = gsched(c, r);
+  const SlabRef slab = slab_of(c, r);
+  if (lane == 0) {
+    m.ev_minor = 0;
+    m.fetch_ctr = 0;
+  }
+  uint32_t len = __builtin_amdgcn_readfirstlane(gsr.len);
+  const uint32_t period = gsr.period;
+  if (lane == 0 && period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
+  unsigned long long acc = 0;
+  wave_sync();
+  for (uint32_t r0 = 0; r0 < k; r0 += 64) {
+    const uint32_t q = r0 + lane;
+    GMsgFull g{};
+    bool valid = false;
+    if (q < k) {
+      uint32_t jq = b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)];
+      if (jq >= k) {  // a hole: only after an inbox overflow (ERR_MSGS is set)
+        set_err(c, ERR_MSGS);
+        jq = q;
+      }
+      g = b.pg_msgs[(size_t)pt[jq >> 6] * 64 + (jq & 63)];
+      valid = !g.dup();
+      nfresh += valid ? 1u : 0u;
+    }
+    // (a) one leader per gossiper
+    const bool coop = valid && g.gossiper != r;
+    L.iP[lane] = g.seq;
+    L.iS[lane] = 0;  // 1: accepted, 2: onGossipReq at its turn
+    uint64_t grp = 0;
+    for (uint64_t todo = __ballot(coop); todo;) {
+      const int l = __ffsll((unsigned long long)todo) - 1;
+      const uint32_t gl = __shfl(g.gossiper, l, 64);
+      const uint64_t same = __ballot(coop && g.gossiper == gl) & todo;
+      if (lane == (uint32_t)l) grp = same;
+      todo &= ~same;
+    }
+    wave_sync();
+    if (grp) {
+      CollEnt cv;
+      CollEnt* col = coll_ensure_cas(c, r, g.gossiper, cv);
+      if (col && (cv.meta & COLL_CLEARED)) {
+        for (uint64_t mm = grp; mm; mm &= mm - 1) L.iS[__ffsll((unsigned long long)mm) - 1] = 2;
+      } else if (col) {
+        bool first = true;
+        for (uint64_t mm = grp; mm; mm &= mm - 1) {
+          const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
+          const bool ok = coll_add(c, col, L.iP[j], &c.seg_flag[i], first ? &cv : nullptr);
+          first = false;
+          L.iS[j] = ok ? 1u : 0u;
+        }
+      }
+    }
+    wave_sync();
+    const uint32_t fl = L.iS[lane];
+    const bool accepted = fl == 1u;
+    const bool full = (valid && !coop) || fl == 2u;  // the chain's onGossipReq, at its turn
+    // (b) receipts; the records that cannot change the view
+    if (accepted) receipt_mark(c, r, g.gossiper, g.seq);
+    const bool user = g.status() >= SWIM_GOSSIP_USER;
+    bool noop = false;
+    if (accepted && !user) {
+      if (c.n_ns && !c.ns_rel[(size_t)c.ns[r] * c.n_ns + c.ns[g.subject]]) {
+        noop = true;
+      } else {
+        const uint64_t cell = cell_get(c, r, g.subject);
+        const bool present = c_has(cell, B_IN_TABLE);
+        const uint32_t st0 = c_status(cell);
+        noop = !(present && st0 == SWIM_LEAVING) && !is_overrides(g.status(), g.inc(), present, st0, c_inc(cell));
+      }
+    }
+    bool skip = accepted && noop;
+    // (a lane that may change its subject's record: an accepted non-no-op one, or one taking the
+    // chain's onGossipReq)
+    for (uint64_t mm = __ballot(((accepted && !noop) || full) && !user); mm; mm &= mm - 1) {
+      const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
+      const uint32_t sj = __shfl(g.subject, (int)j, 64);
+      if (lane > j && !user && g.subject == sj) skip = false;
+    }
+    // (c) positions and the serial steps, in rank order.  Each state is written (and indexed) as soon
+    // as its position is known, before any later lane's onGossipReq may look the slab up (gix_find
+    // after a collector clear rebuilds the index from the slab)
+    const uint64_t accm = __ballot(accepted);
+    const uint64_t serm = __ballot((accepted && !skip) || full);
+    const uint64_t below_me = (1ull << lane) - 1;
+    GossipDev ns;
+    ns.gossiper = g.gossiper; ns.seq = g.seq; ns.subject = g.subject; ns.status = g.status(); ns.inc = g.inc();
+    ns.inf_period = period;
+    ns.inf[0] = g.from;
+#pragma unroll
+    for (int x = 1; x < GINF; ++x) ns.inf[x] = NONE;
+    unsigned long long fullacc = 0;
+    uint64_t done = 0;
+    for (uint64_t mm = serm;;) {
+      const uint32_t jn = mm ? (uint32_t)__ffsll((unsigned long long)mm) - 1 : 64u;
+      const uint64_t below = jn == 64u ? ~0ull : ((1ull << jn) - 1);
+      const uint64_t blk = accm & ~serm & below & ~done;  // no-op lanes before the next serial one
+      if (blk) {
+        uint32_t pos = NONE;
+        if ((blk >> lane) & 1ull) {
+          const uint32_t p = len + (uint32_t)__popcll(blk & below_me);
+          if (p < c.gcap) {
+            pos = p;
+            slab.put(p, ns);
+          } else {
+            set_err(c, ERR_SLAB);
+          }
+        }
+        len = min(len + (uint32_t)__popcll(blk), c.gcap);
+        if (__builtin_amdgcn_readfirstlane(m.gix_valid))  // (only after a collector clear needed the index)
+          for (uint64_t bm = __ballot(pos != NONE); bm; bm &= bm - 1)
+            if (lane == (uint32_t)__ffsll((unsigned long long)bm) - 1) gix_note_at(c, m, r, g.gossiper, g.seq, pos, len);
+        done |= blk;
+        wave_sync();
+      }
+      if (!mm) break;
+      uint32_t nl = 0;
+      if (lane == jn) {
+        gsr.len = len;
+        if (full) {
+          fullacc += on_gossip_req(c, r, m, slab, g) ? 1u : 0u;
+        } else if (len >= c.gcap) {
+          set_err(c, ERR_SLAB);
+        } else {
+          slab.put(len, ns);
+          gsr.len = len + 1;
+          gix_note(c, m, r, ns.gossiper, ns.seq);
+          if (user)  // sink.next(gossip.message()) (:209): listen() subscribers
+            emit(c, r, g.gossiper, SWIM_EV_GOSSIP, SWIM_PHASE_GOSSIP, m.ev_minor++, g.subject);
+          else if (update_membership(c, r, g.subject, g.status(), g.inc(), R_GOSSIP, SWIM_PHASE_GOSSIP))
+            apply_alive(c, r, g.subject, g.inc(), R_GOSSIP, SWIM_PHASE_GOSSIP);
+        }
+        nl = gsr.len;
+      }
+      len = __shfl(nl, (int)jn, 64);
+      done |= 1ull << jn;
+      mm &= mm - 1;
+      wave_sync();
+    }
+    acc += (accepted ? 1ull : 0ull) + fullacc;  // (per lane: the caller sums the wave)
+    if (lane == 0) gsr.len = len;
+    wave_sync();
+  }
+  return acc;
+}
+
 __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, const Bufs& b, const uint32_t* list,
                                                 uint32_t nb, uint32_t lane, int collect, BigLds& L,
                                                 unsigned long long& nsync, uint32_t& nmsg, uint32_t& nfresh) {
@@ -1578,6 +1751,7 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
   PPROF_CNT(4, 1ull);
   PPROF_CNT(5, (unsigned long long)nb);
   uint32_t my_k = 0, my_pages = 0;
+  unsigned long long coop_acc = 0;  // (per lane, summed by the caller's wave reduction)
   for (uint32_t j = 0; j < nb; ++j) {
     const uint32_t i = list[j];
     const uint32_t r = c.lo + i;
@@ -1595,9 +1769,10 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     if (go) {
       rank_big_inbox(c, b, i, k, lane, L);
       nmsg += lane == 0 ? k : 0u;
+      if (k >= b.coop_min) coop_acc += deliver_coop(c, b, i, k, lane, L, nfresh);  // the whole wave, now
     }
     if (lane == j) {
-      my_k = go ? k : 0;
+      my_k = go && k < b.coop_min ? k : 0;  // the chains below take the smaller inboxes
       my_pages = (k + 63) / 64;
     }
   }
@@ -1605,7 +1780,19 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
   PPROF_ADD(0, tp0);
   PPROF_T0(tp1);
   // 2. the onGossipReq chains, lane j for receiver j
-  unsigned long long acc = 0;
+#ifdef SWIM_PHASE_PROF
+  if (lane < nb && my_k) {
+    atomicMax(&g_dbg[10], (unsigned long long)my_k);  // the longest chain of the launches
+    atomicAdd(&g_dbg[11], (unsigned long long)my_k);  // messages walked by the chains
+  }
+  {
+    uint32_t mx = lane < nb ? my_k : 0u;  // the wave's longest chain (its time is that chain's)
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+    PPROF_CNT(12, (unsigned long long)mx);
+  }
+#endif
+  unsigned long long acc = coop_acc;
   if (lane < nb && my_k) {
     const uint32_t i = list[lane], r = c.lo + i;
     const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;

@@ -140,6 +140,20 @@ def test_gpu_sharded_pull_parity_scenario(glib, olib, name, shards, monkeypatch)
     _run_parity(glib, olib, dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": shards}))
 
 
+# row_cap (the content rows a shard sends in one SYNC / SYNC_ACK exchange) grows before a join burst
+# that could exceed it (engine.hip grow_rows_for_joins): started at 16 rows (SWIM_DEBUG_ROW_CAP), the
+# bursts of 80 joiners through one seed need 80 rows each way; without the growth the tick fails with
+# a capacity error (ERR_REQS), with it the run stays bit-exact with the unsharded oracle
+@pytest.mark.parametrize("name,shards,pull", [("join_burst_144", 2, False), ("join_burst_144", 3, True),
+                                              ("mp_joins_via_seed", 2, False)])
+def test_gpu_sharded_row_cap_grows_for_join_burst(glib, olib, name, shards, pull, monkeypatch):
+    sc = {s.name: s for s in scenarios.catalog()}[name]
+    monkeypatch.setenv("SWIM_DEBUG_ROW_CAP", "16")
+    if pull:
+        monkeypatch.setenv("SWIM_EXCHANGE_PULL", "1")
+    _run_parity(glib, olib, dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": shards}))
+
+
 def test_gpu_sharded_parity_config2_1024(glib, olib):
     sc = scenarios.config2()
     sc = dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": 4})
@@ -180,3 +194,20 @@ def test_gpu_matches_golden_digest(glib, sc, shards):
                                 for sc in scenarios.catalog()])
 def test_gpu_parity_wave_delivery(glib, olib, sc):
     _run_parity(glib, olib, dataclasses.replace(sc, cfg={**sc.cfg, "deliver_wave_min": 1}))
+
+
+# ---- the whole-wave delivery (deliver_coop: leader lanes per gossiper, the no-op records skipped, the
+# rest in rank order) for every inbox of two or more messages, unsharded and with 3 shards
+COOP_SCENARIOS = ("join_burst_144", "join_burst_seg", "churn_48", "loss5_kills_64", "user_gossip_10_loss25",
+                  "delay_fd_gossip_12", "namespaces_9", "mp_leave_cluster", "restart_same_address_40",
+                  "update_metadata_12", "external_sync_16", "sync_delay_24", "partition_heal_32")
+
+
+@pytest.mark.parametrize("name,shards", [(nm, sh) for nm in COOP_SCENARIOS for sh in (1, 3)])
+def test_gpu_parity_coop_delivery(glib, olib, name, shards, monkeypatch):
+    sc = {s.name: s for s in scenarios.catalog()}[name]
+    monkeypatch.setenv("SWIM_DEBUG_COOP_MIN", "2")
+    cfg = {**sc.cfg, "deliver_wave_min": 1}
+    if shards > 1:
+        cfg["local_shards"] = shards
+    _run_parity(glib, olib, dataclasses.replace(sc, cfg=cfg))

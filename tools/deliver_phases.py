@@ -56,6 +56,8 @@ def main():
                       # ensure + add, receipt mark, slab put + index, updateMembership
                       "ogr_collector_us": per(d[6]), "ogr_receipt_us": per(d[7]), "ogr_slab_us": per(d[8]),
                       "ogr_update_us": per(d[9]),
+                      "longest_chain_msgs": d[10], "chain_msgs_per_launch": d[11] / launches,
+                      "sum_of_wave_longest_chains": d[12] / launches,
                       "messages_per_launch": dp["messages"] / max(1, dp["launches"])}))
 
 
