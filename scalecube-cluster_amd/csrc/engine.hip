@@ -897,7 +897,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.lo = std::min(n, shard * e->sz);
   c.nl = std::min(n, c.lo + e->sz) - c.lo;
   const uint32_t nl = c.nl;
-  c.gcap = cf.gossip_capacity ? cf.gossip_capacity : 1024;
+  c.gcap = next_pow2(cf.gossip_capacity ? cf.gossip_capacity : 1024);  // (a power of two: the slab is a ring)
   c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 4096);
   c.gix_mask = next_pow2(2 * c.gcap) - 1;
   // infected overflows a member holds at once: states that took a second sender after a collector
@@ -1888,8 +1888,13 @@ int32_t swim_read_gossips(swim_engine* e, uint32_t v, swim_gossip* out, uint32_t
   std::vector<GossipHot> gh(k);
   std::vector<GossipCold> gc(k);
   const size_t o = (size_t)(v - sd->c.lo) * sd->c.gcap;
-  if (hipMemcpy(gh.data(), sd->c.slab_hot + o, sizeof(GossipHot) * k, hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(gc.data(), sd->c.slab_cold + o, sizeof(GossipCold) * k, hipMemcpyDeviceToHost) != hipSuccess)
+  // the slab is a ring from gs.base (swim_device.h SlabRef): at most two segments
+  const uint32_t start = gs.base & (sd->c.gcap - 1), first = std::min(k, sd->c.gcap - start);
+  if (hipMemcpy(gh.data(), sd->c.slab_hot + o + start, sizeof(GossipHot) * first, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(gc.data(), sd->c.slab_cold + o + start, sizeof(GossipCold) * first, hipMemcpyDeviceToHost) != hipSuccess ||
+      (k > first &&
+       (hipMemcpy(gh.data() + first, sd->c.slab_hot + o, sizeof(GossipHot) * (k - first), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(gc.data() + first, sd->c.slab_cold + o, sizeof(GossipCold) * (k - first), hipMemcpyDeviceToHost) != hipSuccess)))
     return SWIM_EDEVICE;
   std::vector<InfOver> io;  // the member's infected overflows, read when a state has one
   for (uint32_t i = 0; i < k; ++i) {  // (the SlabRef layout, swim_device.h)

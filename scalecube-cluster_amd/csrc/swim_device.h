@@ -78,7 +78,8 @@ struct alignas(16) GossipSched {
   uint32_t next;    // tick of the next gossip round (schedule phase g_start, period G; kept while down)
   uint32_t period;  // GossipProtocolImpl.currentPeriod (< 2^28: ERR_INC)
   uint32_t len;     // live gossips in the member's slab (GossipProtocolImpl.gossips.size())
-  uint32_t pad;
+  uint32_t base;    // the slab is a ring: gossip p (insertion order) lives at (base + p) mod gcap; the
+                    // sweep drops a prefix by advancing base (nothing moves)
 };
 
 struct alignas(16) MemberDev {
@@ -168,9 +169,12 @@ struct SlabRef {
   InfOver* inf;      // the member's infected-overflow table
   uint32_t inf_mask;
   uint32_t* err;
+  uint32_t base, mask;  // ring: gossip p at (base + p) & mask
+  __device__ __forceinline__ GossipHot& H(uint32_t p) const { return hot[(base + p) & mask]; }
+  __device__ __forceinline__ GossipCold& C(uint32_t p) const { return cold[(base + p) & mask]; }
   __device__ __forceinline__ GossipDev get(uint32_t p) const {
-    const GossipHot h = hot[p];
-    const GossipCold k = cold[p];
+    const GossipHot h = H(p);
+    const GossipCold k = C(p);
     GossipDev g;
     g.gossiper = h.gossiper;
     g.seq = h.seq;
@@ -217,8 +221,8 @@ struct SlabRef {
         inf[f] = o;
       }
     }
-    hot[p] = h;
-    cold[p] = k;
+    H(p) = h;
+    C(p) = k;
   }
   // the sweep dropped a state whose infected list overflowed
   __device__ __forceinline__ void drop_more(uint32_t g, uint32_t q) const {
@@ -530,7 +534,8 @@ __device__ __forceinline__ uint32_t* ping_list(const Ctx& c, uint32_t v) { retur
 __device__ __forceinline__ uint32_t* remote_list(const Ctx& c, uint32_t v) { return c.remote + (size_t)(v - c.lo) * c.n; }
 __device__ __forceinline__ SlabRef slab_of(const Ctx& c, uint32_t v) {
   const size_t o = (size_t)(v - c.lo) * c.gcap;
-  return SlabRef{c.slab_hot + o, c.slab_cold + o, c.inf_over + (size_t)(v - c.lo) * (c.inf_mask + 1), c.inf_mask, c.err};
+  return SlabRef{c.slab_hot + o, c.slab_cold + o, c.inf_over + (size_t)(v - c.lo) * (c.inf_mask + 1), c.inf_mask, c.err,
+                 c.gs[v - c.lo].base, c.gcap - 1};
 }
 __device__ __forceinline__ bool owned(const Ctx& c, uint32_t v) { return v - c.lo < c.nl; }
 __device__ __forceinline__ uint32_t owner(const Ctx& c, uint32_t v) { return v / c.sz; }
@@ -1011,14 +1016,14 @@ __device__ inline int32_t gix_find(const Ctx& c, MemberDev& m, uint32_t v, const
     for (uint32_t i = 0; i <= mask; ++i) ix[i] = NONE;
     m.gix_used = 0;
     m.gix_valid = 1;
-    for (uint32_t p = 0; p < len; ++p) gix_put(c, m, len, ix, slab.hot[p].gossiper, slab.hot[p].seq, m.gix_base + p);
+    for (uint32_t p = 0; p < len; ++p) gix_put(c, m, len, ix, slab.H(p).gossiper, slab.H(p).seq, m.gix_base + p);
   }
   uint32_t h = gix_hash(g, s);
   for (uint32_t i = 0; i <= mask; ++i, ++h) {
     const uint32_t e = ix[h & mask];
     if (e == NONE) return -1;
     const uint32_t p = e - m.gix_base;
-    if (p < len && slab.hot[p].gossiper == g && slab.hot[p].seq == s) return (int32_t)p;
+    if (p < len && slab.H(p).gossiper == g && slab.H(p).seq == s) return (int32_t)p;
   }
   return -1;
 }

@@ -732,23 +732,23 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   // lane = slab position: one GossipState read serves all nt targets, whose loss draws and
   // receiver checks are independent (issued together); messages keep the (target, position) keys.
   // A pass reads the 16 hot bytes of each state; the 8 cold ones only where a message is
-  // materialised or the entry moves (the infected overflow only for a state that has one).
-  // the next pass's hot bytes are loaded while this pass runs (the sweep writes only positions at
-  // or below the current pass's)
+  // materialised (the infected overflow only for a state that has one).  The slab is a ring: the
+  // sweep drops a prefix by advancing its base after the round, so nothing moves.
+  // the next pass's hot bytes are loaded while this pass runs
   GossipHot hn{};
-  if (lane < glen) hn = slab.hot[lane];
+  if (lane < glen) hn = slab.H(lane);
   uint32_t sinkw = 0;  // the next pass's receipt-slot lines, warmed at the end of this one
   for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
     const uint32_t p = p0 + lane;
     const GossipHot h = hn;
-    if (p + 64 < glen) hn = slab.hot[p + 64];
+    if (p + 64 < glen) hn = slab.H(p + 64);
     bool win = false, keep = false;
     if (p < glen) {
       win = (uint64_t)h.inf_period() + spread >= period;
       keep = !(period > (uint64_t)h.inf_period() + sweep);
     }
-    // sweep (:158-164, :350-358): a pass's survivors land at or below their own positions, all of
-    // which the wave has already read
+    // sweep (:158-164, :350-358): infection periods grow along the slab, so the swept states are a
+    // prefix (lead) and the survivors keep their places
     const uint64_t kmask = __ballot(keep);
     if (!seen_keep) {
       lead += kmask ? (uint32_t)__ffsll((unsigned long long)kmask) - 1 : min(64u, glen - p0);
@@ -761,10 +761,9 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       if (leaving && h.gossiper == m.leave_gossiper && h.seq == (uint32_t)m.leave_seq) done = true;
       if (h.status() == SWIM_GOSSIP_USER && h.gossiper == v) {
         changed = true;
-        emit(c, v, v, SWIM_EV_SPREAD_DONE, SWIM_PHASE_GOSSIP, 0x80000000u | (h.seq & 0x7fffffffu), slab.cold[p].subject);
+        emit(c, v, v, SWIM_EV_SPREAD_DONE, SWIM_PHASE_GOSSIP, 0x80000000u | (h.seq & 0x7fffffffu), slab.C(p).subject);
       }
     }
-    const uint32_t to = w + lanes_below(kmask);
     w += (uint32_t)__popcll(kmask);
     uint32_t matb = 0;  // bit j: a message to target j is materialised
     uint32_t subj = 0;
@@ -772,7 +771,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     bool have_cold = false;
     auto load_cold = [&]() {
       if (!have_cold) {
-        const GossipCold k = slab.cold[p];
+        const GossipCold k = slab.C(p);
         subj = k.subject;
         inc = k.inc;
         have_cold = true;
@@ -923,13 +922,13 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       }
       pseq += cnt_mine;  // lane j: target j's messages so far this round
     }
-    // the sweep's write-back, last in the pass (every lane's reads of this pass are done): only
-    // entries that move (a swept prefix before them) or changed; a round that sweeps nothing
-    // rewrites nothing.  Every moving lane loads its cold part before any lane stores.
-    const bool wb = keep && (to != p || changed);
-    GossipCold kc{};
-    if (wb && to != p) kc = slab.cold[p];
-    if (p < glen && !keep && h.more()) slab.drop_more(h.gossiper, h.seq);  // its infected overflow goes too
+    // a state whose status changed is written back in place; a swept one's infected overflow goes
+    if (changed) {
+      GossipHot hw = h;
+      hw.per_st = (hw.per_st & ~(7u << PER_BITS)) | (SWIM_GOSSIP_USER_SPREAD << PER_BITS);
+      slab.H(p) = hw;
+    }
+    if (p < glen && !keep && h.more()) slab.drop_more(h.gossiper, h.seq);
     // the next pass's hot bytes have arrived by now: its in-window gossips' receipt slots and the
     // first targets' receipt words are loaded here, so that the next pass's check hits the cache
     if (p + 64 < glen && (uint64_t)hn.inf_period() + spread >= period) {
@@ -940,21 +939,19 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         if (owned(c, tj)) sinkw ^= c.gbits[(size_t)sn * c.gwords + ((tj - c.lo) >> 5)];
       }
     }
-    wave_order();
-    if (wb) {
-      GossipHot hw = h;
-      if (changed) hw.per_st = (hw.per_st & ~(7u << PER_BITS)) | (SWIM_GOSSIP_USER_SPREAD << PER_BITS);
-      slab.hot[to] = hw;
-      if (to != p) slab.cold[to] = kc;
-    }
   }
   if (sinkw == 0x5bd1e995u && glen == 0x7fffffffu) set_err(c, 0u);  // keeps the warming loads; sets no bit
   const bool any_done = __ballot(done) != 0;
   if (lane == 0) {
-    // the sweep dropped a prefix (infection periods grow along the slab): the index keeps its serials
-    if (glen - w == lead) m.gix_base += lead;
-    else m.gix_valid = 0;
-    gsched(c, v).len = w;
+    // the sweep dropped a prefix: the ring's base and the index's serial base advance past it
+    GossipSched& gsv = gsched(c, v);
+    if (glen - w == lead) {
+      gsv.base += lead;
+      m.gix_base += lead;
+    } else {
+      set_err(c, ERR_SLAB);  // (unreachable: a state's infection period never falls below an earlier one's)
+    }
+    gsv.len = w;
     if (any_done) {
       m.leave_done = 1;
       c.mflag[v - c.lo] |= MF_LEAVE;
@@ -1278,17 +1275,13 @@ __device__ __forceinline__ uint32_t warm_gossip_req(const Ctx& c, uint32_t r, co
 // onGossipReq (GossipProtocolImpl.java:201-215) for one received message, in canonical order
 __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, const SlabRef& slab, const GMsgFull& g) {
   if (g.dup()) return false;  // the collector held it on arrival and only grows until now
-  PPROF_T0(ta);
   CollEnt cv;
   CollEnt* col = coll_ensure_v(c, r, g.gossiper, cv);
   if (!col) return false;
   const bool was_cleared = (cv.meta & COLL_CLEARED) != 0;
   const bool added = coll_add(c, col, g.seq, &c.seg_flag[r - c.lo], &cv);
-  PPROF_WADD(6, ta);
   if (!added) return false;
-  PPROF_T0(tb);
   receipt_mark(c, r, g.gossiper, g.seq);
-  PPROF_WADD(7, tb);
   PPROF_T0(tc);
   // a GossipState can outlive its collector entry only after a clear
   const int32_t found = was_cleared ? gix_find(c, m, r, slab, g.gossiper, g.seq) : -1;
@@ -1608,6 +1601,7 @@ __device__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t
   unsigned long long acc = 0;
   wave_sync();
   for (uint32_t r0 = 0; r0 < k; r0 += 64) {
+    PPROF_T0(tca);
     const uint32_t q = r0 + lane;
     GMsgFull g{};
     bool valid = false;
@@ -1650,6 +1644,8 @@ __device__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t
       }
     }
     wave_sync();
+    PPROF_ADD(13, tca);
+    PPROF_T0(tcb);
     const uint32_t fl = L.iS[lane];
     const bool accepted = fl == 1u;
     const bool full = (valid && !coop) || fl == 2u;  // the chain's onGossipReq, at its turn
@@ -1680,6 +1676,10 @@ __device__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t
     // after a collector clear rebuilds the index from the slab)
     const uint64_t accm = __ballot(accepted);
     const uint64_t serm = __ballot((accepted && !skip) || full);
+    PPROF_ADD(14, tcb);
+    PPROF_CNT(6, (unsigned long long)__popcll(serm));  // lanes taking a serial step
+    PPROF_CNT(7, (unsigned long long)__popcll(accm));  // accepted lanes
+    PPROF_T0(tcc);
     const uint64_t below_me = (1ull << lane) - 1;
     GossipDev ns;
     ns.gossiper = g.gossiper; ns.seq = g.seq; ns.subject = g.subject; ns.status = g.status(); ns.inc = g.inc();
@@ -1735,6 +1735,7 @@ __device__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t
       mm &= mm - 1;
       wave_sync();
     }
+    PPROF_ADD(15, tcc);
     acc += (accepted ? 1ull : 0ull) + fullacc;  // (per lane: the caller sums the wave)
     if (lane == 0) gsr.len = len;
     wave_sync();

@@ -5,7 +5,7 @@
 
 g_dbg slots: 0 big-inbox ranking, 1 big-inbox onGossipReq chains, 2 big-inbox tail (page reset,
 pingMembers inserts, SYNC collection), 3 small inboxes + their collection (every wave), 4 batches,
-5 big inboxes, 6-9 onGossipReq sections (collector, receipt, slab, updateMembership).  Times are per-wave sums (100 MHz ticks); divided by the waves of a launch they give
+5 big inboxes, 6/7 whole-wave serial / accepted lanes, 8-9 onGossipReq sections (slab, updateMembership), 13-15 whole-wave chunk parts.  Times are per-wave sums (100 MHz ticks); divided by the waves of a launch they give
 each part's share of a launch."""
 import argparse
 import json
@@ -54,8 +54,11 @@ def main():
                       "small_and_collect_us": per(d[3]), "batches": d[4], "big_inboxes": d[5],
                       # onGossipReq sections (every path; wave time, first active lane): collector
                       # ensure + add, receipt mark, slab put + index, updateMembership
-                      "ogr_collector_us": per(d[6]), "ogr_receipt_us": per(d[7]), "ogr_slab_us": per(d[8]),
+                      "coop_serial_lanes": d[6], "coop_accepted": d[7], "ogr_slab_us": per(d[8]),
                       "ogr_update_us": per(d[9]),
+                      # whole-wave delivery (deliver_coop) per chunk: (a) loads + collectors,
+                      # (b) receipts + no-op test, (c) the serial steps and state writes
+                      "coop_a_us": per(d[13]), "coop_b_us": per(d[14]), "coop_c_us": per(d[15]),
                       "longest_chain_msgs": d[10], "chain_msgs_per_launch": d[11] / launches,
                       "sum_of_wave_longest_chains": d[12] / launches,
                       "messages_per_launch": dp["messages"] / max(1, dp["launches"])}))
