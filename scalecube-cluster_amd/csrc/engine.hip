@@ -210,6 +210,8 @@ struct swim_engine {
   bool quiet_on = true;
   QuietCtl* d_quiet = nullptr;   // [2] device control blocks (shared by the local shards), alternating
   uint32_t q_par = 0;            // the block the next window uses
+  uint32_t* h_stat = nullptr;    // pinned host words: each local shard's event counts and error bits
+  uint32_t* d_stat = nullptr;    //   ([SUBQ + 1] per shard, written by k_status), and their device address
   uint32_t* h_done = nullptr;    // pinned host word: the last window's length (written by k_quiet_apply)
   uint32_t* d_done = nullptr;    // its device address
   uint32_t* d_refmm = nullptr;   // RCCL: [2][n] elementwise min / max of the ranks' witness refs
@@ -241,6 +243,7 @@ struct swim_engine {
     for (hipEvent_t ev : qev)
       if (ev) hipEventDestroy(ev);
     if (h_done) hipHostFree(h_done);
+    if (h_stat) hipHostFree(h_stat);
     if (h_par) hipHostFree(h_par);
     if (comm) ncclCommDestroy(comm);
     if (stream) hipStreamDestroy(stream);
@@ -338,15 +341,27 @@ static void launch_deliver(swim_engine* e, Shard& s) {
   k.used++;
 }
 
+// each shard's event counts and error bits into the pinned host words (one launch instead of two
+// blocking copies per shard: the drain that ends every swim_step call, quiet windows included)
+__global__ void k_status(const uint32_t* ev_cnt, const uint32_t* err, uint32_t* out) {
+  const uint32_t t = threadIdx.x;
+  if (t < SUBQ) out[t] = ev_cnt[t];
+  if (t == SUBQ) out[SUBQ] = *err;
+}
+
 static int32_t sync_and_collect(swim_engine* e) {
+  for (size_t i = 0; i < e->sh.size(); ++i)
+    k_status<<<1, 64, 0, e->stream>>>(e->sh[i].c.ev_cnt, e->sh[i].c.err, e->d_stat + i * (SUBQ + 1));
   if (hipStreamSynchronize(e->stream) != hipSuccess) return hip_status() ? SWIM_EDEVICE : SWIM_EDEVICE;
   e->par_slot = 0;  // every staged Params upload has completed
   uint32_t err_all = 0;
   double fill = 0.0;  // fullest event sub-queue since the last drain
-  for (Shard& s : e->sh) {
+  for (size_t si = 0; si < e->sh.size(); ++si) {
+    Shard& s = e->sh[si];
     uint32_t cnt[SUBQ], err = 0;
-    if (hipMemcpy(cnt, s.c.ev_cnt, 4 * SUBQ, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
-    if (hipMemcpy(&err, s.c.err, 4, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+    const volatile uint32_t* st = e->h_stat + si * (SUBQ + 1);
+    for (uint32_t q = 0; q < SUBQ; ++q) cnt[q] = st[q];
+    err = st[SUBQ];
     bool any = false;
     for (uint32_t q = 0; q < SUBQ; ++q) {
       const uint32_t k = std::min(cnt[q], s.c.ev_cap);
@@ -1245,6 +1260,8 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
   if (hipHostMalloc((void**)&e->h_par, sizeof(Params) * kParRing) != hipSuccess) { delete e; return SWIM_ENOMEM; }
   if (hipHostMalloc((void**)&e->h_done, 64, hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void**)&e->d_done, e->h_done, 0) != hipSuccess ||
+      hipHostMalloc((void**)&e->h_stat, 4 * (SUBQ + 1) * e->sh.size(), hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&e->d_stat, e->h_stat, 0) != hipSuccess ||
       hipMalloc((void**)&e->d_quiet, 2 * sizeof(QuietCtl)) != hipSuccess ||
       hipMemset(e->d_quiet, 0xff, 2 * sizeof(QuietCtl)) != hipSuccess) {  // both blocks reset: no fail, no sizes
     delete e;
@@ -2058,13 +2075,13 @@ int32_t swim_profile_deliver(swim_engine* e, swim_kernel_profile* out) {
 // profiling builds (-DSWIM_PHASE_PROF): the per-phase wall-time sums of the instrumented kernels
 // (swim_phases.h g_dbg); reset = 1 zeroes them after the read.  Zeros in the product build.
 int32_t swim_debug_counters(uint64_t* out, uint32_t n, int32_t reset) {
-  if (!out || n > 16) return SWIM_EINVAL;
-  unsigned long long h[16] = {};
+  if (!out || n > 32) return SWIM_EINVAL;
+  unsigned long long h[32] = {};
   if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dbg), sizeof h) != hipSuccess)
     return SWIM_EDEVICE;
   for (uint32_t i = 0; i < n; ++i) out[i] = h[i];
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof z) != hipSuccess) return SWIM_EDEVICE;
   }
   return SWIM_OK;

@@ -97,6 +97,8 @@ struct alignas(16) MemberDev {
                               // filter drops on arrival leaves them waiting until then)
   uint32_t relay_first;       // the sender of the first relayed ack (filtered when it arrives)
   uint32_t init_last;  // start0's initial sync: tick of the last answer (or of the start)
+  uint32_t user_live;  // this member's own user gossips whose spread() has not completed (the emit
+                       // round reads the states past the spreading window only while one is pending)
   uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, gix_valid;
   uint8_t ack_ok;    // ack_due is the tick the (delayed) ack arrives, not the ping timeout
   uint8_t relay_ok;  // relay_due is the tick the first relayed ack arrives, not the timeout
@@ -1078,6 +1080,7 @@ __device__ inline void spread_user(const Ctx& c, uint32_t v, uint32_t payload) {
   gs.len++;
   gix_note(c, m, v, g.gossiper, g.seq);
   m.g_counter++;
+  m.user_live++;
   CollEnt* e = coll_ensure(c, v, v);
   if (coll_add(c, e, g.seq, &c.seg_flag[v - c.lo])) receipt_mark(c, v, v, g.seq);
   stat_add(c, ST_GOSSIPS_CREATED, 1);

@@ -18,7 +18,7 @@ namespace swimdev {
 // Phase timing for profiling builds only (-DSWIM_PHASE_PROF, tools/phase_prof.sh): per-wave wall
 // time (s_memrealtime, 100 MHz) of the delivery kernel's parts, summed into g_dbg; read with
 // swim_debug_counters.  The product build compiles none of it.
-__device__ unsigned long long g_dbg[16];
+__device__ unsigned long long g_dbg[32];
 #ifdef SWIM_PHASE_PROF
 #define PPROF_T0(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
 #define PPROF_ADD(slot, t0)                                                                          \
@@ -35,11 +35,14 @@ __device__ unsigned long long g_dbg[16];
     if ((threadIdx.x & 63) == (uint32_t)__ffsll((unsigned long long)__ballot(1)) - 1)                 \
       atomicAdd(&g_dbg[slot], __builtin_amdgcn_s_memrealtime() - (t0));                              \
   } while (0)
+// wave-local accumulation (added to g_dbg once, with PPROF_CNT): no atomic per loop iteration
+#define PPROF_ACC(var, t0) var += __builtin_amdgcn_s_memrealtime() - (t0)
 #else
 #define PPROF_T0(v)
 #define PPROF_ADD(slot, t0)
 #define PPROF_CNT(slot, val)
 #define PPROF_WADD(slot, t0)
+#define PPROF_ACC(var, t0)
 #endif
 
 // per-tick scratch counters, zeroed by one hipMemsetAsync at the start of every tick
@@ -635,6 +638,12 @@ __device__ __forceinline__ void wave_order() {
   __threadfence_block();
   __builtin_amdgcn_wave_barrier();
 }
+// LDS writes of one lane made visible to the wave's other lanes without waiting for the wave's
+// outstanding global loads (s_waitcnt lgkmcnt(0) only: a wave's LDS operations complete in order)
+__device__ __forceinline__ void lds_order() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+}
 
 // a GOSSIP_REQ for a receiver owned by this shard joins the receiver's inbox (every lane of the wave
 // calls it: `valid` masks the lanes without a message); in the inbox, `to` holds the message's age
@@ -672,10 +681,31 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 // one inbox atomic per (target, pass) — and the same pass over the slab also sweeps it (:158-164,
 // order preserving) and checks the futures.
 constexpr int EMIT_WAVES = 4;
+// profiling builds: the emit kernel's part times and counts, per wave in registers (added to g_dbg
+// 16..23 once per wave at the end of the kernel: no contended atomic per sender or per pass)
+struct EmitProf {
+  unsigned long long t_setup = 0, t_pass = 0, t_win = 0, t_mat = 0, n_all = 0, n_win = 0, n_mat = 0, n_snd = 0;
+};
 __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs& b, uint32_t v, uint64_t period,
                                                         uint32_t glen, uint32_t lane, uint32_t* s_t,
-                                                        unsigned long long& nmat) {
+                                                        unsigned long long& nmat, EmitProf& ep) {
+  PPROF_T0(te0);
+#ifdef SWIM_PHASE_PROF
+  ep.n_snd++;
+  unsigned long long& np_all = ep.n_all;
+  unsigned long long& np_win = ep.n_win;
+  unsigned long long& np_mat = ep.n_mat;
+  unsigned long long& t_win = ep.t_win;
+  unsigned long long& t_mat = ep.t_mat;
+#endif
   MemberDev& m = mem(c, v);
+  const SlabRef slab = slab_of(c, v);
+  // both ends of the slab first (see below), in flight while the targets are chosen: the first 64
+  // states and the last 64
+  const uint32_t tail0 = glen > 64 ? glen - 64 : 0u;
+  GossipHot h_head{}, h_tail{};
+  if (lane < glen) h_head = slab.H(lane);
+  if (glen > 64 && tail0 + lane < glen) h_tail = slab.H(tail0 + lane);
   const uint32_t rlen = m.remote_len;
   const uint32_t F = (uint32_t)c.fanout;
   if (lane == 0) {  // selectGossipMembers (:322-343)
@@ -706,7 +736,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     }
     s_t[49] = alias;
   }
-  wave_order();
+  lds_order();
   const uint32_t nt = s_t[0];
   // what depends on the target only, once per round instead of once per (target, gossip): whether
   // it is up (s_t[50 + j]; bit 1: its inbound filter passes v now — a delayed message meets the filter
@@ -718,44 +748,88 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     s_t[66 + lane] = (uint32_t)out_loss(c, v, t);
     s_t[82 + lane] = owned(c, t) ? c.clr_tick[t - c.lo] : 0xffffffffu;
   }
-  wave_order();
+  lds_order();
   const uint64_t spread = (uint64_t)(c.repeat_mult * ceil_log2(rlen + 1));
   const uint64_t sweep = 2 * (spread + 1);
   const bool leaving = m.leave_pending != 0;
-  const SlabRef slab = slab_of(c, v);
   unsigned long long nmsg = 0;
   uint32_t pseq = 0;  // lane j < nt: messages materialised to target j so far (GMsgFull.pseq)
-  uint32_t w = 0;     // sweep: survivors so far
-  uint32_t lead = 0;  // sweep: entries before the first survivor
-  bool seen_keep = false;
   bool done = false;
+  // Infection periods grow along the slab (every state is appended with the current period), so the
+  // states a round must look at are ranges found from the ends: (1) the swept prefix, sweep
+  // (:158-164, :350-358): period > infectionPeriod + periodsToSweep; (2) the in-window suffix
+  // (:145-151, selectGossipsToSend): infectionPeriod + periodsToSpread >= period.  The states between
+  // matter only to the futures (:167-180, :360-368) — a graceful leave's, or a user gossip's
+  // spread() of this member — and are read only while one is pending.
+  uint32_t lead = 0;  // (1): the first state kept
+  for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
+    const uint32_t p = p0 + lane;
+    bool sw = false;
+    if (p < glen) {
+      const GossipHot h = p0 == 0 ? h_head : slab.H(p);
+      sw = period > (uint64_t)h.inf_period() + sweep;
+      if (sw && h.more()) slab.drop_more(h.gossiper, h.seq);  // its infected overflow goes too
+    }
+    const uint64_t km = __ballot(p < glen && !sw);
+    if (km) {
+      lead = p0 + (uint32_t)__ffsll((unsigned long long)km) - 1;
+      break;
+    }
+    lead = min(p0 + 64, glen);
+  }
+  uint32_t wst = glen;  // (2): the first in-window state (a swept state is out of the window too)
+  for (uint32_t e0 = glen; e0 > lead;) {
+    const bool last = e0 == glen;
+    const uint32_t s0 = last ? tail0 : (e0 - lead > 64 ? e0 - 64 : lead);
+    const uint32_t p = s0 + lane;
+    bool out = false;
+    if (p < e0) {
+      const GossipHot h = last ? (glen > 64 ? h_tail : h_head) : slab.H(p);
+      out = !((uint64_t)h.inf_period() + spread >= period);
+    }
+    const uint64_t om = __ballot(out);
+    if (om) {
+      wst = max(lead, s0 + (64u - (uint32_t)__clzll((unsigned long long)om)));
+      break;
+    }
+    wst = max(lead, s0);
+    e0 = s0;
+  }
+  const uint32_t first = (leaving || m.user_live) ? lead : wst;
   // lane = slab position: one GossipState read serves all nt targets, whose loss draws and
   // receiver checks are independent (issued together); messages keep the (target, position) keys.
   // A pass reads the 16 hot bytes of each state; the 8 cold ones only where a message is
   // materialised (the infected overflow only for a state that has one).  The slab is a ring: the
-  // sweep drops a prefix by advancing its base after the round, so nothing moves.
+  // sweep drops the prefix by advancing its base after the round, so nothing moves.
   // the next pass's hot bytes are loaded while this pass runs
   GossipHot hn{};
-  if (lane < glen) hn = slab.H(lane);
+  if (first >= tail0) {  // the first pass lies in the tail already loaded: moved across lanes
+    const GossipHot& src = glen > 64 ? h_tail : h_head;
+    const int from = (int)(first - tail0 + lane);
+    hn.gossiper = __shfl(src.gossiper, from & 63, 64);
+    hn.seq = __shfl(src.seq, from & 63, 64);
+    hn.per_st = __shfl(src.per_st, from & 63, 64);
+    hn.inf0 = __shfl(src.inf0, from & 63, 64);
+  } else if (first + lane < glen) {
+    hn = slab.H(first + lane);
+  }
   uint32_t sinkw = 0;  // the next pass's receipt-slot lines, warmed at the end of this one
-  for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
+  PPROF_ACC(ep.t_setup, te0);
+  PPROF_T0(te1);
+  for (uint32_t p0 = first; p0 < glen; p0 += 64) {
+#ifdef SWIM_PHASE_PROF
+    np_all++;
+#endif
     const uint32_t p = p0 + lane;
     const GossipHot h = hn;
     if (p + 64 < glen) hn = slab.H(p + 64);
     bool win = false, keep = false;
     if (p < glen) {
       win = (uint64_t)h.inf_period() + spread >= period;
-      keep = !(period > (uint64_t)h.inf_period() + sweep);
+      keep = true;  // (p >= lead)
     }
-    // sweep (:158-164, :350-358): infection periods grow along the slab, so the swept states are a
-    // prefix (lead) and the survivors keep their places
-    const uint64_t kmask = __ballot(keep);
-    if (!seen_keep) {
-      lead += kmask ? (uint32_t)__ffsll((unsigned long long)kmask) - 1 : min(64u, glen - p0);
-      seen_keep = kmask != 0;
-    }
-    // futures (:167-180, :360-368): the graceful-leave future stops the member at the end of the
-    // tick; a user gossip's spread() completes (this round's copies carry the status read above)
+    // futures: the graceful-leave future stops the member at the end of the tick; a user gossip's
+    // spread() completes (this round's copies carry the status read above)
     bool changed = false;
     if (keep && period > (uint64_t)h.inf_period() + spread) {
       if (leaving && h.gossiper == m.leave_gossiper && h.seq == (uint32_t)m.leave_seq) done = true;
@@ -764,7 +838,10 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         emit(c, v, v, SWIM_EV_SPREAD_DONE, SWIM_PHASE_GOSSIP, 0x80000000u | (h.seq & 0x7fffffffu), slab.C(p).subject);
       }
     }
-    w += (uint32_t)__popcll(kmask);
+    {
+      const uint32_t nch = (uint32_t)__popcll(__ballot(changed));
+      if (lane == 0 && nch) m.user_live -= nch;
+    }
     uint32_t matb = 0;  // bit j: a message to target j is materialised
     uint32_t subj = 0;
     int32_t inc = 0;
@@ -777,7 +854,11 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         have_cold = true;
       }
     };
+    PPROF_T0(te2);
     if (__ballot(win)) {
+#ifdef SWIM_PHASE_PROF
+      np_win++;
+#endif
       // the gossip's receipt-bitmap slot serves every target (one load per gossip)
       uint64_t key = 0;
       uint32_t sl = 0;
@@ -867,7 +948,12 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
         }
       }
     }
+    PPROF_ACC(t_win, te2);
+    PPROF_T0(te3);
     if (__ballot(matb != 0)) {
+#ifdef SWIM_PHASE_PROF
+      np_mat++;
+#endif
       if (matb) load_cold();
       // one inbox reservation per target present in this pass: lane j issues target j's atomic and
       // makes sure the (at most two) inbox pages of its slot range exist
@@ -922,13 +1008,13 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
       }
       pseq += cnt_mine;  // lane j: target j's messages so far this round
     }
-    // a state whose status changed is written back in place; a swept one's infected overflow goes
+    PPROF_ACC(t_mat, te3);
+    // a state whose status changed is written back in place
     if (changed) {
       GossipHot hw = h;
       hw.per_st = (hw.per_st & ~(7u << PER_BITS)) | (SWIM_GOSSIP_USER_SPREAD << PER_BITS);
       slab.H(p) = hw;
     }
-    if (p < glen && !keep && h.more()) slab.drop_more(h.gossiper, h.seq);
     // the next pass's hot bytes have arrived by now: its in-window gossips' receipt slots and the
     // first targets' receipt words are loaded here, so that the next pass's check hits the cache
     if (p + 64 < glen && (uint64_t)hn.inf_period() + spread >= period) {
@@ -941,17 +1027,14 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     }
   }
   if (sinkw == 0x5bd1e995u && glen == 0x7fffffffu) set_err(c, 0u);  // keeps the warming loads; sets no bit
+  PPROF_ACC(ep.t_pass, te1);
   const bool any_done = __ballot(done) != 0;
   if (lane == 0) {
-    // the sweep dropped a prefix: the ring's base and the index's serial base advance past it
+    // the sweep dropped the prefix: the ring's base and the index's serial base advance past it
     GossipSched& gsv = gsched(c, v);
-    if (glen - w == lead) {
-      gsv.base += lead;
-      m.gix_base += lead;
-    } else {
-      set_err(c, ERR_SLAB);  // (unreachable: a state's infection period never falls below an earlier one's)
-    }
-    gsv.len = w;
+    gsv.base += lead;
+    m.gix_base += lead;
+    gsv.len = glen - lead;
     if (any_done) {
       m.leave_done = 1;
       c.mflag[v - c.lo] |= MF_LEAVE;
@@ -1082,12 +1165,21 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned lo
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t ns = b.k->sender_cnt;
   unsigned long long nmsg = 0, nmat = 0, nstate = 0;
+  EmitProf ep;
   for (uint32_t k = __builtin_amdgcn_readfirstlane(blockIdx.x * EMIT_WAVES + wv); k < ns; k += gridDim.x * EMIT_WAVES) {
     const uint32_t i = b.senders[k];
     const GossipSched gs = c.gs[i];
     nstate += gs.len;
-    nmsg += gossip_emit_sender(c, b, c.lo + i, gs.period - 1, gs.len, lane, s_t[wv], nmat);
+    nmsg += gossip_emit_sender(c, b, c.lo + i, gs.period - 1, gs.len, lane, s_t[wv], nmat, ep);
   }
+  PPROF_CNT(16, ep.t_setup);
+  PPROF_CNT(17, ep.t_pass);
+  PPROF_CNT(18, ep.t_win);
+  PPROF_CNT(19, ep.t_mat);
+  PPROF_CNT(20, ep.n_all);
+  PPROF_CNT(21, ep.n_win);
+  PPROF_CNT(22, ep.n_mat);
+  PPROF_CNT(23, ep.n_snd);
   if (lane == 0 && nmat) atomicAdd(&b.k->msg_total, (uint32_t)nmat);
   if (prof && lane == 0 && nstate) {
     atomicAdd(prof, nmat);
@@ -1599,21 +1691,32 @@ __device__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t
   const uint32_t period = gsr.period;
   if (lane == 0 && period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
   unsigned long long acc = 0;
-  wave_sync();
-  for (uint32_t r0 = 0; r0 < k; r0 += 64) {
-    PPROF_T0(tca);
-    const uint32_t q = r0 + lane;
-    GMsgFull g{};
-    bool valid = false;
+  // rank q's message (the next chunk's is loaded while a chunk is processed, with its collector slot)
+  auto load_msg = [&](uint32_t q) -> GMsgFull {
+    GMsgFull x{};
     if (q < k) {
       uint32_t jq = b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)];
       if (jq >= k) {  // a hole: only after an inbox overflow (ERR_MSGS is set)
         set_err(c, ERR_MSGS);
         jq = q;
       }
-      g = b.pg_msgs[(size_t)pt[jq >> 6] * 64 + (jq & 63)];
-      valid = !g.dup();
-      nfresh += valid ? 1u : 0u;
+      x = b.pg_msgs[(size_t)pt[jq >> 6] * 64 + (jq & 63)];
+    }
+    return x;
+  };
+  const CollEnt* cbase = c.coll + (size_t)i * c.hcap;
+  uint32_t sink = 0;
+  GMsgFull gn = load_msg(lane);
+  wave_sync();
+  for (uint32_t r0 = 0; r0 < k; r0 += 64) {
+    PPROF_T0(tca);
+    const uint32_t q = r0 + lane;
+    const GMsgFull g = gn;
+    const bool valid = q < k && !g.dup();
+    nfresh += valid ? 1u : 0u;
+    if (r0 + 64 < k) {
+      gn = load_msg(q + 64);
+      if (q + 64 < k) sink ^= cbase[hash32(gn.gossiper) & (c.hcap - 1)].key;
     }
     // (a) one leader per gossiper
     const bool coop = valid && g.gossiper != r;
@@ -1740,6 +1843,7 @@ __device__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t
     if (lane == 0) gsr.len = len;
     wave_sync();
   }
+  if (sink == 0x5bd1e995u && k == 0x7fffffffu) set_err(c, 0u);  // keeps the warming loads; sets no bit
   return acc;
 }
 
