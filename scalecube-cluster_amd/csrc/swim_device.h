@@ -165,6 +165,17 @@ __device__ inline int32_t inf_find(const InfOver* t, uint32_t mask, uint32_t g, 
   }
   return -1;
 }
+// a load through the global address space (global_load: counted by vmcnt only, while a generic-pointer
+// flat load also holds lgkmcnt, so an LDS-only wait would wait for it too)
+template <typename T>
+__device__ __forceinline__ T gload(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass of hipcc has no address space 1; it never runs this)
+  typedef const __attribute__((address_space(1))) T* gptr;
+  return *(gptr)(p);
+#else
+  return *p;
+#endif
+}
 struct SlabRef {
   GossipHot* hot;
   GossipCold* cold;
@@ -174,6 +185,7 @@ struct SlabRef {
   uint32_t base, mask;  // ring: gossip p at (base + p) & mask
   __device__ __forceinline__ GossipHot& H(uint32_t p) const { return hot[(base + p) & mask]; }
   __device__ __forceinline__ GossipCold& C(uint32_t p) const { return cold[(base + p) & mask]; }
+  __device__ __forceinline__ GossipHot Hg(uint32_t p) const { return gload(hot + ((base + p) & mask)); }
   __device__ __forceinline__ GossipDev get(uint32_t p) const {
     const GossipHot h = H(p);
     const GossipCold k = C(p);
@@ -534,11 +546,12 @@ __device__ __forceinline__ MemberDev& mem(const Ctx& c, uint32_t v) { return c.m
 __device__ __forceinline__ GossipSched& gsched(const Ctx& c, uint32_t v) { return c.gs[v - c.lo]; }
 __device__ __forceinline__ uint32_t* ping_list(const Ctx& c, uint32_t v) { return c.ping + (size_t)(v - c.lo) * c.n; }
 __device__ __forceinline__ uint32_t* remote_list(const Ctx& c, uint32_t v) { return c.remote + (size_t)(v - c.lo) * c.n; }
-__device__ __forceinline__ SlabRef slab_of(const Ctx& c, uint32_t v) {
+__device__ __forceinline__ SlabRef slab_of(const Ctx& c, uint32_t v, uint32_t base) {
   const size_t o = (size_t)(v - c.lo) * c.gcap;
   return SlabRef{c.slab_hot + o, c.slab_cold + o, c.inf_over + (size_t)(v - c.lo) * (c.inf_mask + 1), c.inf_mask, c.err,
-                 c.gs[v - c.lo].base, c.gcap - 1};
+                 base, c.gcap - 1};
 }
+__device__ __forceinline__ SlabRef slab_of(const Ctx& c, uint32_t v) { return slab_of(c, v, c.gs[v - c.lo].base); }
 __device__ __forceinline__ bool owned(const Ctx& c, uint32_t v) { return v - c.lo < c.nl; }
 __device__ __forceinline__ uint32_t owner(const Ctx& c, uint32_t v) { return v / c.sz; }
 

@@ -685,10 +685,67 @@ constexpr int EMIT_WAVES = 4;
 // 16..23 once per wave at the end of the kernel: no contended atomic per sender or per pass)
 struct EmitProf {
   unsigned long long t_setup = 0, t_pass = 0, t_win = 0, t_mat = 0, n_all = 0, n_win = 0, n_mat = 0, n_snd = 0;
+  unsigned long long t_sel = 0, t_tgt = 0;  // setup parts: target selection, per-target words
 };
-__device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs& b, uint32_t v, uint64_t period,
-                                                        uint32_t glen, uint32_t lane, uint32_t* s_t,
-                                                        unsigned long long& nmat, EmitProf& ep) {
+// A sender's round setup loaded ahead, for all of a wave's senders at once (lane j: its j-th sender):
+// the targets selectGossipMembers takes without a reshuffle (remoteMembers[idx .. idx + F), every
+// member on its own address) and their per-target words.  ok = 0: the sender selects in line.
+constexpr uint32_t PRE_F = 4;  // fanouts up to this are taken ahead
+struct SenderPre {
+  uint32_t ok;
+  uint32_t rlen;       // remoteMembers.size()
+  int32_t idx;         // remoteMembersIndex
+  uint32_t fut;        // a graceful leave or an own user gossip is pending (futures to check)
+  uint32_t t[PRE_F];   // targets
+  uint32_t tw[PRE_F];  // up | inbound-passes << 1 | v's outbound loss towards it << 2
+  uint32_t clr[PRE_F]; // its collectors' last clear tick (owned), else ~0
+};
+__device__ __forceinline__ void sender_pre_load(const Ctx& c, uint32_t i, SenderPre& sp) {
+  sp.ok = 0;
+  const MemberDev& m = c.mem[i];
+  const uint32_t rlen = m.remote_len;
+  const int32_t idx = m.remote_idx;
+  sp.rlen = rlen;
+  sp.idx = idx;
+  sp.fut = (m.leave_pending || m.user_live) ? 1u : 0u;
+  const uint32_t F = (uint32_t)c.fanout;
+  if (F > PRE_F || c.route) return;
+  if (rlen < F || idx < 0 || (uint32_t)idx + F > rlen) return;
+  const uint32_t v = c.lo + i;
+  const uint32_t* rl = remote_list(c, v) + idx;
+#pragma unroll
+  for (uint32_t q = 0; q < PRE_F; ++q) sp.t[q] = q < F ? rl[q] : 0u;
+#pragma unroll
+  for (uint32_t q = 0; q < PRE_F; ++q) {
+    if (q >= F) continue;
+    const uint32_t t = sp.t[q];
+    sp.tw[q] = (c.up[t] ? 1u : 0u) | (in_pass(c, t, v) ? 2u : 0u) | ((uint32_t)out_loss(c, v, t) << 2);
+    sp.clr[q] = owned(c, t) ? c.clr_tick[t - c.lo] : 0xffffffffu;
+  }
+  sp.ok = 1;
+}
+__device__ __forceinline__ uint32_t pick4(const uint32_t (&a)[PRE_F], uint32_t q) {
+  return q == 0 ? a[0] : q == 1 ? a[1] : q == 2 ? a[2] : a[3];
+}
+__device__ __forceinline__ SenderPre sender_pre_from(const SenderPre& x, int j) {
+  SenderPre sp;
+  sp.ok = __shfl(x.ok, j, 64);
+  sp.rlen = __shfl(x.rlen, j, 64);
+  sp.idx = __shfl(x.idx, j, 64);
+  sp.fut = __shfl(x.fut, j, 64);
+#pragma unroll
+  for (uint32_t q = 0; q < PRE_F; ++q) {
+    sp.t[q] = __shfl(x.t[q], j, 64);
+    sp.tw[q] = __shfl(x.tw[q], j, 64);
+    sp.clr[q] = __shfl(x.clr[q], j, 64);
+  }
+  return sp;
+}
+
+__device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, const Bufs& b, uint32_t v, uint64_t period,
+                                                        uint32_t glen, uint32_t gbase, uint32_t lane, uint32_t* s_t,
+                                                        unsigned long long& nmat, EmitProf& ep,
+                                                        const SenderPre& sp) {
   PPROF_T0(te0);
 #ifdef SWIM_PHASE_PROF
   ep.n_snd++;
@@ -699,16 +756,31 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   unsigned long long& t_mat = ep.t_mat;
 #endif
   MemberDev& m = mem(c, v);
-  const SlabRef slab = slab_of(c, v);
+  const SlabRef slab = slab_of(c, v, gbase);
   // both ends of the slab first (see below), in flight while the targets are chosen: the first 64
   // states and the last 64
   const uint32_t tail0 = glen > 64 ? glen - 64 : 0u;
   GossipHot h_head{}, h_tail{};
-  if (lane < glen) h_head = slab.H(lane);
-  if (glen > 64 && tail0 + lane < glen) h_tail = slab.H(tail0 + lane);
-  const uint32_t rlen = m.remote_len;
+  if (lane < glen) h_head = slab.Hg(lane);
+  if (glen > 64 && tail0 + lane < glen) h_tail = slab.Hg(tail0 + lane);
+  const uint32_t rlen = sp.rlen;
   const uint32_t F = (uint32_t)c.fanout;
-  if (lane == 0) {  // selectGossipMembers (:322-343)
+  if (sp.ok) {  // the targets and their words were loaded ahead (no reshuffle, no shared address)
+    if (lane == 0) {
+      s_t[0] = F;
+      s_t[49] = 0;
+      m.remote_idx = sp.idx + (int32_t)F;
+    }
+    if (lane < F) {  // (register arrays read through selects, never a runtime index: no scratch)
+      const uint32_t t = pick4(sp.t, lane), tw = pick4(sp.tw, lane);
+      s_t[1 + lane] = t;
+      s_t[17 + lane] = t;
+      s_t[33 + lane] = lane;
+      s_t[50 + lane] = tw & 3u;
+      s_t[66 + lane] = tw >> 2;
+      s_t[82 + lane] = pick4(sp.clr, lane);
+    }
+  } else if (lane == 0) {  // selectGossipMembers (:322-343)
     uint32_t* rl = remote_list(c, v);
     uint32_t nt = 0;
     if (rlen < F) {
@@ -737,21 +809,24 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     s_t[49] = alias;
   }
   lds_order();
+  PPROF_ACC(ep.t_sel, te0);
+  PPROF_T0(te_t);
   const uint32_t nt = s_t[0];
   // what depends on the target only, once per round instead of once per (target, gossip): whether
   // it is up (s_t[50 + j]; bit 1: its inbound filter passes v now — a delayed message meets the filter
   // when it arrives, k_dq_release), v's outbound loss towards it (s_t[66 + j]), the tick its
   // collectors were last cleared (s_t[82 + j]; receipt bits older than that are void)
-  if (lane < nt) {
+  if (!sp.ok && lane < nt) {
     const uint32_t t = s_t[1 + lane];
     s_t[50 + lane] = (c.up[t] ? 1u : 0u) | (in_pass(c, t, v) ? 2u : 0u);
     s_t[66 + lane] = (uint32_t)out_loss(c, v, t);
     s_t[82 + lane] = owned(c, t) ? c.clr_tick[t - c.lo] : 0xffffffffu;
   }
   lds_order();
+  PPROF_ACC(ep.t_tgt, te_t);
   const uint64_t spread = (uint64_t)(c.repeat_mult * ceil_log2(rlen + 1));
   const uint64_t sweep = 2 * (spread + 1);
-  const bool leaving = m.leave_pending != 0;
+  const bool leaving = sp.fut && m.leave_pending != 0;
   unsigned long long nmsg = 0;
   uint32_t pseq = 0;  // lane j < nt: messages materialised to target j so far (GMsgFull.pseq)
   bool done = false;
@@ -784,8 +859,8 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     const uint32_t p = s0 + lane;
     bool out = false;
     if (p < e0) {
-      const GossipHot h = last ? (glen > 64 ? h_tail : h_head) : slab.H(p);
-      out = !((uint64_t)h.inf_period() + spread >= period);
+      const uint32_t per_st = last ? (glen > 64 ? h_tail.per_st : h_head.per_st) : slab.H(p).per_st;
+      out = !((uint64_t)(per_st & PER_MASK) + spread >= period);
     }
     const uint64_t om = __ballot(out);
     if (om) {
@@ -795,7 +870,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     wst = max(lead, s0);
     e0 = s0;
   }
-  const uint32_t first = (leaving || m.user_live) ? lead : wst;
+  const uint32_t first = sp.fut ? lead : wst;
   // lane = slab position: one GossipState read serves all nt targets, whose loss draws and
   // receiver checks are independent (issued together); messages keep the (target, position) keys.
   // A pass reads the 16 hot bytes of each state; the 8 cold ones only where a message is
@@ -804,14 +879,14 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
   // the next pass's hot bytes are loaded while this pass runs
   GossipHot hn{};
   if (first >= tail0) {  // the first pass lies in the tail already loaded: moved across lanes
-    const GossipHot& src = glen > 64 ? h_tail : h_head;
-    const int from = (int)(first - tail0 + lane);
-    hn.gossiper = __shfl(src.gossiper, from & 63, 64);
-    hn.seq = __shfl(src.seq, from & 63, 64);
-    hn.per_st = __shfl(src.per_st, from & 63, 64);
-    hn.inf0 = __shfl(src.inf0, from & 63, 64);
+    const bool tl = glen > 64;
+    const int from = (int)(first - tail0 + lane) & 63;
+    hn.gossiper = __shfl(tl ? h_tail.gossiper : h_head.gossiper, from, 64);
+    hn.seq = __shfl(tl ? h_tail.seq : h_head.seq, from, 64);
+    hn.per_st = __shfl(tl ? h_tail.per_st : h_head.per_st, from, 64);
+    hn.inf0 = __shfl(tl ? h_tail.inf0 : h_head.inf0, from, 64);
   } else if (first + lane < glen) {
-    hn = slab.H(first + lane);
+    hn = slab.Hg(first + lane);
   }
   uint32_t sinkw = 0;  // the next pass's receipt-slot lines, warmed at the end of this one
   PPROF_ACC(ep.t_setup, te0);
@@ -822,7 +897,7 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
 #endif
     const uint32_t p = p0 + lane;
     const GossipHot h = hn;
-    if (p + 64 < glen) hn = slab.H(p + 64);
+    if (p + 64 < glen) hn = slab.Hg(p + 64);  // (a global load: the pass's LDS waits do not wait for it)
     bool win = false, keep = false;
     if (p < glen) {
       win = (uint64_t)h.inf_period() + spread >= period;
@@ -1019,10 +1094,10 @@ __device__ inline unsigned long long gossip_emit_sender(const Ctx& c, const Bufs
     // first targets' receipt words are loaded here, so that the next pass's check hits the cache
     if (p + 64 < glen && (uint64_t)hn.inf_period() + spread >= period) {
       const uint32_t sn = gslot_of(gkey(hn.gossiper, hn.seq));
-      sinkw ^= (uint32_t)c.gslot[sn].key;
+      sinkw ^= (uint32_t)gload(&c.gslot[sn].key);
       for (uint32_t jj = 0; jj < min(nt, 3u); ++jj) {
         const uint32_t tj = s_t[1 + jj];
-        if (owned(c, tj)) sinkw ^= c.gbits[(size_t)sn * c.gwords + ((tj - c.lo) >> 5)];
+        if (owned(c, tj)) sinkw ^= gload(&c.gbits[(size_t)sn * c.gwords + ((tj - c.lo) >> 5)]);
       }
     }
   }
@@ -1158,7 +1233,10 @@ __global__ void k_debug_exchange(KP) {
 
 // the rest of the round for the listed senders: one sender per wave at a time
 // prof (sampled launches only): {GOSSIP_REQs materialised, (gossip, sender round) states read}
-__global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned long long* prof) {
+#ifndef EMIT_OCC
+#define EMIT_OCC 4  // waves per SIMD the emit kernel is compiled for (its grid fills them: EMIT_GRID)
+#endif
+__global__ void __launch_bounds__(64 * EMIT_WAVES, EMIT_OCC) k_gossip_emit(KP, unsigned long long* prof) {
   __shared__ uint32_t s_t[EMIT_WAVES][98];
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
@@ -1166,11 +1244,35 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned lo
   const uint32_t ns = b.k->sender_cnt;
   unsigned long long nmsg = 0, nmat = 0, nstate = 0;
   EmitProf ep;
-  for (uint32_t k = __builtin_amdgcn_readfirstlane(blockIdx.x * EMIT_WAVES + wv); k < ns; k += gridDim.x * EMIT_WAVES) {
-    const uint32_t i = b.senders[k];
-    const GossipSched gs = c.gs[i];
-    nstate += gs.len;
-    nmsg += gossip_emit_sender(c, b, c.lo + i, gs.period - 1, gs.len, lane, s_t[wv], nmat, ep);
+  // the wave's senders, up to 64 at a time: lane j loads the j-th one's index, schedule word and round
+  // setup (SenderPre) in one batch of independent loads; then the senders run one after the other
+  const uint32_t S = gridDim.x * EMIT_WAVES;
+  for (uint32_t k0 = __builtin_amdgcn_readfirstlane(blockIdx.x * EMIT_WAVES + wv); k0 < ns; k0 += 64 * S) {
+    const uint32_t kj = k0 + lane * S;
+    uint32_t pi = 0, plen = 0, pper = 0, pbase = 0;
+    SenderPre pre;
+    pre.ok = 0;
+    pre.rlen = 0;
+    pre.idx = -1;
+    pre.fut = 0;
+    if (kj < ns) {
+      pi = b.senders[kj];
+      const GossipSched g = c.gs[pi];
+      plen = g.len;
+      pper = g.period;
+      pbase = g.base;
+      sender_pre_load(c, pi, pre);
+    }
+    const uint32_t nb = min(64u, (ns - k0 + S - 1) / S);
+    for (uint32_t j = 0; j < nb; ++j) {
+      const uint32_t i = __builtin_amdgcn_readfirstlane(__shfl(pi, (int)j, 64));
+      const uint32_t glen = __builtin_amdgcn_readfirstlane(__shfl(plen, (int)j, 64));
+      const uint32_t per = __builtin_amdgcn_readfirstlane(__shfl(pper, (int)j, 64));
+      const uint32_t gb = __builtin_amdgcn_readfirstlane(__shfl(pbase, (int)j, 64));
+      const SenderPre sp = sender_pre_from(pre, (int)j);
+      nstate += glen;
+      nmsg += gossip_emit_sender(c, b, c.lo + i, per - 1, glen, gb, lane, s_t[wv], nmat, ep, sp);
+    }
   }
   PPROF_CNT(16, ep.t_setup);
   PPROF_CNT(17, ep.t_pass);
@@ -1180,6 +1282,8 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES) k_gossip_emit(KP, unsigned lo
   PPROF_CNT(21, ep.n_win);
   PPROF_CNT(22, ep.n_mat);
   PPROF_CNT(23, ep.n_snd);
+  PPROF_CNT(24, ep.t_sel);
+  PPROF_CNT(25, ep.t_tgt);
   if (lane == 0 && nmat) atomicAdd(&b.k->msg_total, (uint32_t)nmat);
   if (prof && lane == 0 && nstate) {
     atomicAdd(prof, nmat);

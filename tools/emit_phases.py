@@ -6,7 +6,7 @@ after the second kill), from the profiling build (tools/phase_prof.sh):
 g_dbg slots 16-23: 16 target selection and per-target setup, 17 the slab passes, 18 their in-window
 checks (receipt slot and words, collector probes, loss / delay draws), 19 their materialisation
 (inbox reservations and message writes); counts: 20 passes, 21 passes with an in-window state, 22
-passes that materialise, 23 senders.  Times are per-wave sums (100 MHz ticks) divided by the grid's
+passes that materialise, 23 senders; setup parts 24 target selection, 25 per-target words.  Times are per-wave sums (100 MHz ticks) divided by the grid's
 waves and the launches: each part's share of an average wave's launch."""
 import argparse
 import json
@@ -48,7 +48,8 @@ def main():
     per = lambda x: x / 100.0 / waves / launches
     print(json.dumps({"workload": args.workload, "emit_ms_per_launch": fp["total_ms"] / max(1, fp["launches"]),
                       "setup_us": per(d[16]), "passes_us": per(d[17]), "window_check_us": per(d[18]),
-                      "materialise_us": per(d[19]), "passes": d[20] / launches, "window_passes": d[21] / launches,
+                      "materialise_us": per(d[19]), "select_us": per(d[24]), "target_words_us": per(d[25]),
+                      "passes": d[20] / launches, "window_passes": d[21] / launches,
                       "mat_passes": d[22] / launches, "senders": d[23] / launches}))
 
 
