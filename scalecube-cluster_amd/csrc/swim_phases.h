@@ -1779,7 +1779,7 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
 //      the no-op lanes between them take the next positions and write their states together.
 // Returns this lane's share of the accepted messages; nfresh counts those not flagged as provable
 // duplicates (per lane as well).
-constexpr uint32_t COOP_MIN = 64;  // Bufs.coop_min's default
+constexpr uint32_t COOP_MIN = 16;  // Bufs.coop_min's default (every big inbox: measured best, 16 / 32 / 64)
 __device__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L,
                                            uint32_t& nfresh) {
   const uint32_t r = c.lo + i;
