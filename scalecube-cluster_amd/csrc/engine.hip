@@ -330,13 +330,18 @@ static void launch_apply(swim_engine* e, Shard& s, int d2, int classified, int f
 
 static void launch_deliver(swim_engine* e, Shard& s) {
   // at least kDeliverGrid workgroups: big inboxes are delivered a wave each, grid-stride
+  // (the whole-wave delivery of the biggest inboxes first, its own kernel; both are "deliver" in the
+  // profile: the events bracket the pair)
   const uint32_t grid = std::max<uint32_t>(kDeliverGrid, grid_for(s.c.nl, DLV_BLOCK));
   KProf& k = s.prof_dlv;
   if (!k.take(e->prof)) {
+    k_deliver_coop<<<kDeliverGrid, DLV_BLOCK, 0, e->stream>>>(s.d_par, e->T, nullptr);
     k_gossip_deliver<<<grid, DLV_BLOCK, 0, e->stream>>>(s.d_par, e->T, 1, nullptr);
     return;
   }
-  hipExtLaunchKernelGGL(k_gossip_deliver, dim3(grid), dim3(DLV_BLOCK), 0, e->stream, k.ev[2 * k.used],
+  hipExtLaunchKernelGGL(k_deliver_coop, dim3(kDeliverGrid), dim3(DLV_BLOCK), 0, e->stream, k.ev[2 * k.used], nullptr,
+                        0, s.d_par, e->T, k.slots + 3 * k.used);
+  hipExtLaunchKernelGGL(k_gossip_deliver, dim3(grid), dim3(DLV_BLOCK), 0, e->stream, nullptr,
                         k.ev[2 * k.used + 1], 0, s.d_par, e->T, 1, k.slots + 3 * k.used);
   k.used++;
 }

@@ -1780,7 +1780,7 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
 // Returns this lane's share of the accepted messages; nfresh counts those not flagged as provable
 // duplicates (per lane as well).
 constexpr uint32_t COOP_MIN = 16;  // Bufs.coop_min's default (every big inbox: measured best, 16 / 32 / 64)
-__device__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L,
+__device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L,
                                            uint32_t& nfresh) {
   const uint32_t r = c.lo + i;
   const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
@@ -1951,6 +1951,51 @@ __device__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t
   return acc;
 }
 
+// The big inboxes of at least coop_min messages, before k_gossip_deliver (a kernel of its own: the
+// whole-wave delivery's registers do not weigh on the main delivery kernel): a wave per inbox,
+// grid-stride over big_list — rank, deliver_coop, the inbox pages back to the pool, msg_cnt = 0; the
+// main kernel then finds the inbox empty and does the receiver's pingMembers inserts and SYNC
+// collection as for any big inbox.  prof as k_gossip_deliver's.
+__global__ void __launch_bounds__(DLV_BLOCK, 2) k_deliver_coop(KP, unsigned long long* prof) {
+  const Ctx c = pctx(P, T);
+  const Bufs b = P->b;
+  __shared__ BigLds s_big[DLV_WAVES];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long acc = 0;
+  uint32_t nmsg = 0, nfresh = 0;
+  if (b.k->msg_total != 0) {
+    const uint32_t nbig = b.k->big_cnt;
+    for (uint32_t x = __builtin_amdgcn_readfirstlane(blockIdx.x * DLV_WAVES + wv); x < nbig; x += gridDim.x * DLV_WAVES) {
+      const uint32_t i = b.big_list[x];
+      const uint32_t r = c.lo + i;
+      const uint32_t k = min(b.msg_cnt[i], b.pg_max * 64u);  // (beyond the page table: ERR_INBOX is set)
+      if (k < b.coop_min) continue;  // (wave-uniform) the main kernel's lane chains take it
+      uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
+      bool pages_ok = true;
+      for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) pages_ok &= pt[pg] < b.pg_cap;
+      pages_ok = __ballot(!pages_ok) == 0;
+      wave_sync();
+      if (lane == 0) b.msg_cnt[i] = 0;
+      if (c.up[r] && pages_ok) {
+        rank_big_inbox(c, b, i, k, lane, s_big[wv]);
+        nmsg += lane == 0 ? k : 0u;
+        acc += deliver_coop(c, b, i, k, lane, s_big[wv], nfresh);
+      }
+      wave_sync();
+      for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) pt[pg] = NONE;
+    }
+  }
+  wave_stat_add(c, ST_GOSSIP_ACCEPTED, acc);
+  if (prof) {
+    const unsigned long long a0 = wave_sum(nmsg), a1 = wave_sum(nfresh), a2 = wave_sum(acc);
+    if (lane == 0 && (a0 | a1 | a2)) {
+      atomicAdd(prof, a0);
+      atomicAdd(prof + 1, a1);
+      atomicAdd(prof + 2, a2);
+    }
+  }
+}
+
 __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, const Bufs& b, const uint32_t* list,
                                                 uint32_t nb, uint32_t lane, int collect, BigLds& L,
                                                 unsigned long long& nsync, uint32_t& nmsg, uint32_t& nfresh) {
@@ -1960,7 +2005,6 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
   PPROF_CNT(4, 1ull);
   PPROF_CNT(5, (unsigned long long)nb);
   uint32_t my_k = 0, my_pages = 0;
-  unsigned long long coop_acc = 0;  // (per lane, summed by the caller's wave reduction)
   for (uint32_t j = 0; j < nb; ++j) {
     const uint32_t i = list[j];
     const uint32_t r = c.lo + i;
@@ -1978,10 +2022,9 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     if (go) {
       rank_big_inbox(c, b, i, k, lane, L);
       nmsg += lane == 0 ? k : 0u;
-      if (k >= b.coop_min) coop_acc += deliver_coop(c, b, i, k, lane, L, nfresh);  // the whole wave, now
     }
     if (lane == j) {
-      my_k = go && k < b.coop_min ? k : 0;  // the chains below take the smaller inboxes
+      my_k = go ? k : 0;  // (an inbox of >= coop_min messages was delivered by k_deliver_coop: k = 0 here)
       my_pages = (k + 63) / 64;
     }
   }
@@ -2001,7 +2044,7 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     PPROF_CNT(12, (unsigned long long)mx);
   }
 #endif
-  unsigned long long acc = coop_acc;
+  unsigned long long acc = 0;
   if (lane < nb && my_k) {
     const uint32_t i = list[lane], r = c.lo + i;
     const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
