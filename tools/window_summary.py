@@ -18,18 +18,25 @@ def last_dispatches(db, kernel, k, table, cols):
 
 
 def main():
+    # kernel: one name, or several joined by '+' (one launch of each per round, e.g. the delivery pair
+    # k_deliver_coop+k_gossip_deliver): times and bytes are summed per round
     prefix, kernel, k = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    t = last_dispatches(f"{prefix}_stats", kernel, k, "kernels", "dispatch_id, duration")
-    out = {"kernel": kernel, "launches": len(t), "window": f"last {k} launches of the run",
-           "avg_us": sum(r[1] for r in t) / max(1, len(t)) / 1e3}
+    names = kernel.split("+")
+    ts = [last_dispatches(f"{prefix}_stats", kn, k, "kernels", "dispatch_id, duration") for kn in names]
+    out = {"kernel": kernel, "launches": min(len(t) for t in ts), "window": f"last {k} launches of the run",
+           "avg_us": sum(sum(r[1] for r in t) / max(1, len(t)) for t in ts) / 1e3}
     con_f = sqlite3.connect(f"{prefix}_fetch/run_results.db")
     con_w = sqlite3.connect(f"{prefix}_write/run_results.db")
 
     def per_launch(con, counter):
-        rows = list(con.execute("select dispatch_id, sum(value) from counters_collection where kernel_name like ? "
-                                "and counter_name = ? group by dispatch_id order by dispatch_id", (kernel + "%", counter)))
-        rows = rows[-k:]
-        return sum(r[1] for r in rows) / max(1, len(rows)), len(rows)
+        tot, n = 0.0, None
+        for kn in names:
+            rows = list(con.execute("select dispatch_id, sum(value) from counters_collection where kernel_name like ? "
+                                    "and counter_name = ? group by dispatch_id order by dispatch_id", (kn + "%", counter)))
+            rows = rows[-k:]
+            tot += sum(r[1] for r in rows) / max(1, len(rows))
+            n = len(rows) if n is None else min(n, len(rows))
+        return tot, n
 
     fetch_kib, nf = per_launch(con_f, "FETCH_SIZE")
     write_kib, nw = per_launch(con_w, "WRITE_SIZE")
