@@ -165,6 +165,14 @@ __device__ inline int32_t inf_find(const InfOver* t, uint32_t mask, uint32_t g, 
   }
   return -1;
 }
+// lane l's value to every lane when l is wave-uniform: v_readlane (a register read) instead of the
+// LDS crossbar round trip __shfl takes
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, uint32_t l) {
+  return (uint64_t)rdlane((uint32_t)v, l) | ((uint64_t)rdlane((uint32_t)(v >> 32), l) << 32);
+}
 // a load through the global address space (global_load: counted by vmcnt only, while a generic-pointer
 // flat load also holds lgkmcnt, so an LDS-only wait would wait for it too)
 template <typename T>

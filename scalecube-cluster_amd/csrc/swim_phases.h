@@ -729,15 +729,15 @@ __device__ __forceinline__ uint32_t pick4(const uint32_t (&a)[PRE_F], uint32_t q
 }
 __device__ __forceinline__ SenderPre sender_pre_from(const SenderPre& x, int j) {
   SenderPre sp;
-  sp.ok = __shfl(x.ok, j, 64);
-  sp.rlen = __shfl(x.rlen, j, 64);
-  sp.idx = __shfl(x.idx, j, 64);
-  sp.fut = __shfl(x.fut, j, 64);
+  sp.ok = rdlane(x.ok, j);
+  sp.rlen = rdlane(x.rlen, j);
+  sp.idx = (int32_t)rdlane((uint32_t)x.idx, j);
+  sp.fut = rdlane(x.fut, j);
 #pragma unroll
   for (uint32_t q = 0; q < PRE_F; ++q) {
-    sp.t[q] = __shfl(x.t[q], j, 64);
-    sp.tw[q] = __shfl(x.tw[q], j, 64);
-    sp.clr[q] = __shfl(x.clr[q], j, 64);
+    sp.t[q] = rdlane(x.t[q], j);
+    sp.tw[q] = rdlane(x.tw[q], j);
+    sp.clr[q] = rdlane(x.clr[q], j);
   }
   return sp;
 }
@@ -1063,8 +1063,8 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
         const bool mat = (matb >> j) & 1u;
         const uint64_t mk = __ballot(mat);
         if (!mk) continue;
-        const uint32_t bj = __shfl(base, (int)j, 64), qj = __shfl(pseq, (int)j, 64);
-        const uint32_t p0j = __shfl(pid0, (int)j, 64), p1j = __shfl(pid1, (int)j, 64);
+        const uint32_t bj = rdlane(base, j), qj = rdlane(pseq, j);
+        const uint32_t p0j = rdlane(pid0, j), p1j = rdlane(pid1, j);
         if (!mat) continue;
         const uint32_t pre = lanes_below(mk);
         const uint32_t t = s_t[1 + j];
@@ -1265,10 +1265,10 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES, EMIT_OCC) k_gossip_emit(KP, u
     }
     const uint32_t nb = min(64u, (ns - k0 + S - 1) / S);
     for (uint32_t j = 0; j < nb; ++j) {
-      const uint32_t i = __builtin_amdgcn_readfirstlane(__shfl(pi, (int)j, 64));
-      const uint32_t glen = __builtin_amdgcn_readfirstlane(__shfl(plen, (int)j, 64));
-      const uint32_t per = __builtin_amdgcn_readfirstlane(__shfl(pper, (int)j, 64));
-      const uint32_t gb = __builtin_amdgcn_readfirstlane(__shfl(pbase, (int)j, 64));
+      const uint32_t i = rdlane(pi, j);
+      const uint32_t glen = rdlane(plen, j);
+      const uint32_t per = rdlane(pper, j);
+      const uint32_t gb = rdlane(pbase, j);
       const SenderPre sp = sender_pre_from(pre, (int)j);
       nstate += glen;
       nmsg += gossip_emit_sender(c, b, c.lo + i, per - 1, glen, gb, lane, s_t[wv], nmat, ep, sp);
@@ -1679,7 +1679,7 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
     const uint32_t f = q < k ? snd_key(c, msg_at(q)) : NONE;
     uint64_t todo = __ballot(q < k);
     while (todo) {
-      const uint32_t sf = __shfl(f, (int)__ffsll((unsigned long long)todo) - 1, 64);
+      const uint32_t sf = rdlane(f, (uint32_t)__ffsll((unsigned long long)todo) - 1);
       const uint64_t same = __ballot(f == sf) & todo;
       int slot = big_find(L.snd, nd, sf, lane);
       if (slot < 0) {
@@ -1749,7 +1749,7 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
       }
       uint64_t todo = __ballot(q < k);
       while (todo) {
-        const uint32_t sf = __shfl(f, (int)__ffsll((unsigned long long)todo) - 1, 64);
+        const uint32_t sf = rdlane(f, (uint32_t)__ffsll((unsigned long long)todo) - 1);
         const uint64_t same = __ballot(f == sf) & todo;
         const uint32_t at = L.cnt[big_find(L.snd, nd, sf, lane)] + ps;
         if (((same >> lane) & 1ull) && at < k) perm_at(at) = q;
@@ -1829,7 +1829,7 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
     uint64_t grp = 0;
     for (uint64_t todo = __ballot(coop); todo;) {
       const int l = __ffsll((unsigned long long)todo) - 1;
-      const uint32_t gl = __shfl(g.gossiper, l, 64);
+      const uint32_t gl = rdlane(g.gossiper, (uint32_t)l);
       const uint64_t same = __ballot(coop && g.gossiper == gl) & todo;
       if (lane == (uint32_t)l) grp = same;
       todo &= ~same;
@@ -1875,7 +1875,7 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
     // chain's onGossipReq)
     for (uint64_t mm = __ballot(((accepted && !noop) || full) && !user); mm; mm &= mm - 1) {
       const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
-      const uint32_t sj = __shfl(g.subject, (int)j, 64);
+      const uint32_t sj = rdlane(g.subject, j);
       if (lane > j && !user && g.subject == sj) skip = false;
     }
     // (c) positions and the serial steps, in rank order.  Each state is written (and indexed) as soon
@@ -1937,7 +1937,7 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
         }
         nl = gsr.len;
       }
-      len = __shfl(nl, (int)jn, 64);
+      len = rdlane(nl, jn);
       done |= 1ull << jn;
       mm &= mm - 1;
       wave_sync();
@@ -2085,7 +2085,7 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
   //    small-inbox path: each reads only its own lists, schedule and FD-SYNC queue)
   for (uint32_t j = 0; j < nb; ++j) {
     const uint32_t i = list[j], r = c.lo + i;
-    const uint32_t np = __shfl(my_pages, (int)j, 64);
+    const uint32_t np = rdlane(my_pages, j);
     for (uint32_t pg = lane; pg < np; pg += 64) b.pg_tab[(size_t)i * b.pg_max + pg] = NONE;
     apply_ins_batch<64, false>(c, r, lane, L.iP, L.iS, L.iR);
   }
