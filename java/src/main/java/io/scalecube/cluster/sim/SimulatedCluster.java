@@ -286,6 +286,30 @@ public final class SimulatedCluster implements AutoCloseable {
 
   private static long key(int member, int handle) { return ((long) member << 32) | (handle & 0xffffffffL); }
 
+  // ------------------------------------------------------------------ SYNC from outside the simulation
+  /**
+   * onSyncAck (MembershipProtocolImpl.java:363-391) at member {@code viewer} for a SyncData that arrived
+   * from a real node (decoded by the caller's codec): its records in order, as (member slot, status,
+   * incarnation) — swim_ingest_sync, {@code initial} for start0's INITIAL_SYNC reason.
+   */
+  public void ingestSync(int viewer, int[] members, int[] statuses, int[] incarnations, boolean initial) {
+    if (members.length != statuses.length || members.length != incarnations.length) {
+      throw new IllegalArgumentException("record arrays differ in length");
+    }
+    run(() -> {
+      try (Arena a = Arena.ofConfined()) {
+        MemorySegment recs = a.allocate(16L * Math.max(1, members.length), 16);  // swim_record: 4 x u32
+        for (int i = 0; i < members.length; i++) {
+          recs.setAtIndex(JAVA_INT, 4L * i, members[i]);
+          recs.setAtIndex(JAVA_INT, 4L * i + 1, statuses[i]);
+          recs.setAtIndex(JAVA_INT, 4L * i + 2, incarnations[i]);
+          recs.setAtIndex(JAVA_INT, 4L * i + 3, 0);
+        }
+        call(SwimNative.INGEST_SYNC, "swim_ingest_sync", engine, viewer, recs, members.length, initial ? 1 : 0);
+      }
+    });
+  }
+
   // ------------------------------------------------------------------ plumbing
   MemorySegment engine() { return engine; }
 

@@ -126,6 +126,7 @@ public final class SwimNative {
   static final MethodHandle JOIN = h("swim_join", JAVA_INT, ADDRESS, JAVA_INT);
   static final MethodHandle JOIN_AT = h("swim_join_at", JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT);
   static final MethodHandle SPREAD = h("swim_spread", JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT);
+  static final MethodHandle INGEST_SYNC = h("swim_ingest_sync", JAVA_INT, ADDRESS, JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT);
   static final MethodHandle UPDATE_METADATA = h("swim_update_metadata", JAVA_INT, ADDRESS, JAVA_INT);
   static final MethodHandle SET_NAMESPACES =
       h("swim_set_namespaces", JAVA_INT, ADDRESS, ADDRESS, JAVA_INT, ADDRESS);
