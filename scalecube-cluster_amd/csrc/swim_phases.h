@@ -745,7 +745,8 @@ __device__ __forceinline__ SenderPre sender_pre_from(const SenderPre& x, int j) 
 __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, const Bufs& b, uint32_t v, uint64_t period,
                                                         uint32_t glen, uint32_t gbase, uint32_t lane, uint32_t* s_t,
                                                         unsigned long long& nmat, EmitProf& ep,
-                                                        const SenderPre& sp) {
+                                                        const SenderPre& sp, const GossipHot h_head,
+                                                        const GossipHot h_tail) {
   PPROF_T0(te0);
 #ifdef SWIM_PHASE_PROF
   ep.n_snd++;
@@ -757,12 +758,9 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
 #endif
   MemberDev& m = mem(c, v);
   const SlabRef slab = slab_of(c, v, gbase);
-  // both ends of the slab first (see below), in flight while the targets are chosen: the first 64
-  // states and the last 64
+  // both ends of the slab (see below) were loaded by the caller during the previous sender: the first
+  // 64 states and the last 64
   const uint32_t tail0 = glen > 64 ? glen - 64 : 0u;
-  GossipHot h_head{}, h_tail{};
-  if (lane < glen) h_head = slab.Hg(lane);
-  if (glen > 64 && tail0 + lane < glen) h_tail = slab.Hg(tail0 + lane);
   const uint32_t rlen = sp.rlen;
   const uint32_t F = (uint32_t)c.fanout;
   if (sp.ok) {  // the targets and their words were loaded ahead (no reshuffle, no shared address)
@@ -1264,14 +1262,29 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES, EMIT_OCC) k_gossip_emit(KP, u
       sender_pre_load(c, pi, pre);
     }
     const uint32_t nb = min(64u, (ns - k0 + S - 1) / S);
+    // the two ends of a sender's slab (its first and last 64 states), loaded one sender ahead
+    auto slab_ends = [&](uint32_t j, GossipHot& hh, GossipHot& ht) {
+      const uint32_t i = rdlane(pi, j), glen = rdlane(plen, j), gb = rdlane(pbase, j);
+      const SlabRef sl = slab_of(c, c.lo + i, gb);
+      hh = GossipHot{};
+      ht = GossipHot{};
+      if (lane < glen) hh = sl.Hg(lane);
+      if (glen > 64 && glen - 64 + lane < glen) ht = sl.Hg(glen - 64 + lane);
+    };
+    GossipHot ch, ct;
+    if (nb) slab_ends(0, ch, ct);
     for (uint32_t j = 0; j < nb; ++j) {
       const uint32_t i = rdlane(pi, j);
       const uint32_t glen = rdlane(plen, j);
       const uint32_t per = rdlane(pper, j);
       const uint32_t gb = rdlane(pbase, j);
       const SenderPre sp = sender_pre_from(pre, (int)j);
+      GossipHot nh{}, nt{};
+      if (j + 1 < nb) slab_ends(j + 1, nh, nt);
       nstate += glen;
-      nmsg += gossip_emit_sender(c, b, c.lo + i, per - 1, glen, gb, lane, s_t[wv], nmat, ep, sp);
+      nmsg += gossip_emit_sender(c, b, c.lo + i, per - 1, glen, gb, lane, s_t[wv], nmat, ep, sp, ch, ct);
+      ch = nh;
+      ct = nt;
     }
   }
   PPROF_CNT(16, ep.t_setup);
