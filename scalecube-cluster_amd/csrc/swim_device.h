@@ -703,29 +703,48 @@ __device__ inline CollEnt* coll_ensure_v(const Ctx& c, uint32_t v, uint32_t goss
   set_err(c, ERR_HASH);
   return nullptr;
 }
-// coll_ensure_v for lanes of one wave inserting different gossipers into one member's table at once:
-// an empty slot is claimed with a compare-and-swap (a lane that loses it probes on)
-__device__ inline CollEnt* coll_ensure_cas(const Ctx& c, uint32_t v, uint32_t gossiper, CollEnt& out) {
+// coll_ensure_v for the leader lanes of one wave (lead: one per distinct gossiper) inserting into one
+// member's table that no other wave touches meanwhile: two leaders finding the same empty slot are
+// told apart by ballot (the lowest lane takes it, the others probe on), so no compare-and-swap round
+// trip.  Called by the whole wave; returns the leader's entry (null: not a leader, or the table is full).
+__device__ inline CollEnt* coll_ensure_wave(const Ctx& c, uint32_t v, bool lead, uint32_t gossiper, uint32_t lane,
+                                            CollEnt& out) {
   CollEnt* base = c.coll + (size_t)(v - c.lo) * c.hcap;
-  uint32_t mask = c.hcap - 1, h = hash32(gossiper) & mask, key = gossiper + 1;
-  for (uint32_t i = 0; i < c.hcap; ++i) {
-    CollEnt* e = base + ((h + i) & mask);
-    const CollEnt x = *e;
-    if (x.key == key) { out = x; return e; }
-    if (x.key == 0) {
-      const uint32_t prev = atomicCAS(&e->key, 0u, key);
-      if (prev == 0u) {
-        e->lo = 0;
-        e->hi = 0;
-        e->meta = 0;
-        out.key = key; out.lo = 0; out.hi = 0; out.meta = 0;
-        return e;
-      }
-      if (prev == key) { out = *e; return e; }
+  const uint32_t mask = c.hcap - 1, key = gossiper + 1;
+  uint32_t h = hash32(gossiper) & mask;
+  CollEnt* res = nullptr;
+  bool act = lead;
+  for (uint32_t it = 0; __ballot(act); ++it) {
+    if (it == c.hcap) {  // (wave-uniform)
+      if (act) set_err(c, ERR_HASH);
+      break;
     }
+    CollEnt x{};
+    if (act) x = base[h];
+    if (act && x.key == key) {
+      out = x;
+      res = base + h;
+      act = false;
+    }
+    const bool claim = act && x.key == 0;
+    bool won = false;
+    for (uint64_t todo = __ballot(claim); todo;) {
+      const uint32_t l = (uint32_t)__ffsll((unsigned long long)todo) - 1;
+      const uint32_t sl = rdlane(h, l);
+      todo &= ~__ballot(claim && h == sl);
+      won |= lane == l;
+    }
+    if (won) {
+      CollEnt ne;
+      ne.key = key; ne.lo = 0; ne.hi = 0; ne.meta = 0;
+      base[h] = ne;
+      out = ne;
+      res = base + h;
+      act = false;
+    }
+    h = (h + 1) & mask;
   }
-  set_err(c, ERR_HASH);
-  return nullptr;
+  return res;
 }
 // ---- spilled-collector blocks.  Tier-indexed Ctx members are read through selects, never a runtime
 // array index: indexing an array member of the kernel's register-resident Ctx copy with a runtime

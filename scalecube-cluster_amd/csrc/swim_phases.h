@@ -1778,8 +1778,8 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
 // sequence (GossipProtocolImpl.java:201-215) as the lane chain, 64 ranks at a time.
 //  (a) collectors: each gossiper of the chunk gets one leader lane, which adds its lanes' sequence ids
 //      in rank order (a collector's intervals — and the segmentation flag — see the same sequence of
-//      adds as in the chain); leaders of different gossipers run side by side (new table entries are
-//      claimed by compare-and-swap).  A lane whose add fails holds a copy the collector already had:
+//      adds as in the chain); leaders of different gossipers run side by side (two finding one empty
+//      table slot are told apart by ballot, coll_ensure_wave: no compare-and-swap round trip).  A lane whose add fails holds a copy the collector already had:
 //      rejected, as in the chain.  Messages of the member's own gossips, and of gossipers whose
 //      collector was cleared (a GossipState may outlive it: the gix lookup), take the chain's own
 //      onGossipReq at their turn in (c) instead.
@@ -1848,9 +1848,9 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
       todo &= ~same;
     }
     wave_sync();
-    if (grp) {
+    {
       CollEnt cv;
-      CollEnt* col = coll_ensure_cas(c, r, g.gossiper, cv);
+      CollEnt* col = coll_ensure_wave(c, r, grp != 0, g.gossiper, lane, cv);
       if (col && (cv.meta & COLL_CLEARED)) {
         for (uint64_t mm = grp; mm; mm &= mm - 1) L.iS[__ffsll((unsigned long long)mm) - 1] = 2;
       } else if (col) {
@@ -1870,14 +1870,20 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
     const bool accepted = fl == 1u;
     const bool full = (valid && !coop) || fl == 2u;  // the chain's onGossipReq, at its turn
     // (b) receipts; the records that cannot change the view
-    if (accepted) receipt_mark(c, r, g.gossiper, g.seq);
     const bool user = g.status() >= SWIM_GOSSIP_USER;
+#ifdef COOP_CELL_FIRST
+    // the subject's cell is loaded before the receipt mark's slot read: both in flight at once
+    const uint64_t cell = accepted && !user ? cell_get(c, r, g.subject) : 0ull;
+#endif
+    if (accepted) receipt_mark(c, r, g.gossiper, g.seq);
     bool noop = false;
     if (accepted && !user) {
       if (c.n_ns && !c.ns_rel[(size_t)c.ns[r] * c.n_ns + c.ns[g.subject]]) {
         noop = true;
       } else {
+#ifndef COOP_CELL_FIRST
         const uint64_t cell = cell_get(c, r, g.subject);
+#endif
         const bool present = c_has(cell, B_IN_TABLE);
         const uint32_t st0 = c_status(cell);
         noop = !(present && st0 == SWIM_LEAVING) && !is_overrides(g.status(), g.inc(), present, st0, c_inc(cell));
