@@ -1871,19 +1871,14 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
     const bool full = (valid && !coop) || fl == 2u;  // the chain's onGossipReq, at its turn
     // (b) receipts; the records that cannot change the view
     const bool user = g.status() >= SWIM_GOSSIP_USER;
-#ifdef COOP_CELL_FIRST
     // the subject's cell is loaded before the receipt mark's slot read: both in flight at once
     const uint64_t cell = accepted && !user ? cell_get(c, r, g.subject) : 0ull;
-#endif
     if (accepted) receipt_mark(c, r, g.gossiper, g.seq);
     bool noop = false;
     if (accepted && !user) {
       if (c.n_ns && !c.ns_rel[(size_t)c.ns[r] * c.n_ns + c.ns[g.subject]]) {
         noop = true;
       } else {
-#ifndef COOP_CELL_FIRST
-        const uint64_t cell = cell_get(c, r, g.subject);
-#endif
         const bool present = c_has(cell, B_IN_TABLE);
         const uint32_t st0 = c_status(cell);
         noop = !(present && st0 == SWIM_LEAVING) && !is_overrides(g.status(), g.inc(), present, st0, c_inc(cell));
