@@ -1970,7 +1970,10 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
 // grid-stride over big_list — rank, deliver_coop, the inbox pages back to the pool, msg_cnt = 0; the
 // main kernel then finds the inbox empty and does the receiver's pingMembers inserts and SYNC
 // collection as for any big inbox.  prof as k_gossip_deliver's.
-__global__ void __launch_bounds__(DLV_BLOCK, 2) k_deliver_coop(KP, unsigned long long* prof) {
+#ifndef COOP_OCC
+#define COOP_OCC 2  // blocks per CU the whole-wave delivery kernel is compiled for (3 / 4 spill: 0.44 / 0.53 ms vs 0.41)
+#endif
+__global__ void __launch_bounds__(DLV_BLOCK, COOP_OCC) k_deliver_coop(KP, unsigned long long* prof) {
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
   __shared__ BigLds s_big[DLV_WAVES];
