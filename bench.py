@@ -203,25 +203,91 @@ def side_run(lib, workload, n, warmup, steps, device=0, quiet=True, **knobs):
     return out
 
 
-def quiet_roofline(qprof, workload, n):
+def window_pmc_traffic(workload, n, steps, warmup):
+    """HBM bytes of the timed quiet window (k_quiet_scan + k_quiet_apply, the LAST launch of each in
+    the profiled command) from the committed PMC passes — only when that command ran the same window
+    (same --steps and --warmup: the window's length is steps x ticks per period).  (None, reason)
+    otherwise: traffic is never borrowed from a window of another length."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}{n // 1024}k_pmc.json")))
+    if not paths:
+        return None, "no PMC profile of this workload"
+    doc = json.load(open(paths[-1]))
+    src = os.path.relpath(paths[-1], REPO)
+    ba = doc.get("bench_args") or {}
+    if ba.get("steps") != steps or ba.get("warmup") != warmup:
+        return None, f"{src} profiled --steps {ba.get('steps')} --warmup {ba.get('warmup')}, not this window"
+    tot = 0.0
+    for k in ("k_quiet_scan", "k_quiet_apply"):
+        last = (doc["kernels"].get(k) or {}).get("last_launch_hbm_bytes")
+        if last is None:
+            return None, f"{src} holds no per-launch bytes of {k}"
+        tot += last
+    return tot, src
+
+
+def quiet_roofline(qprof, workload, n, steps, warmup):
     """k_quiet_scan + k_quiet_apply (a quiet window's two launches) against HBM: swim_profile_quiet's
     algorithmic bytes (SURVEY.md §8(d) ping phase, 21 B per member-period, plus the quiet check's
-    reads once per window) over the kernels' HIP-event time; traffic = the same kernels' HBM bytes
-    per window from the committed PMC passes of this workload."""
+    reads once per window) over the kernels' HIP-event time; traffic = the same window's HBM bytes
+    from the committed PMC passes of this exact command (window_pmc_traffic)."""
     per_win = qprof["alg_bytes"] / max(1, qprof["launches"])
     ach = qprof["alg_bytes"] / max(1e-12, qprof["total_ms"] / 1e3) / 1e9
-    ts, ta = pmc_traffic("k_quiet_scan", f"{workload}{n // 1024}k"), pmc_traffic("k_quiet_apply", f"{workload}{n // 1024}k")
-    traffic = ts[0] + ta[0] if ts[0] is not None and ta[0] is not None else None
+    traffic, src = window_pmc_traffic(workload, n, steps, warmup) if qprof["launches"] == 1 else \
+        (None, "more than one window in the timed region")
+    ts = (None, src)
     return {"bound": "hbm", "kernel": "k_quiet_scan + k_quiet_apply (one quiet window)", "achieved": ach,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
-            "traffic_unit": "HBM bytes per window (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of both kernels)",
+            "traffic_unit": "HBM bytes of the timed window (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of both kernels, "
+                            "the same command's last window)",
             "traffic_source": ts[1], "windows": qprof["launches"], "avg_window_ms": qprof["total_ms"] / max(1, qprof["launches"]),
             "alg_bytes_per_window": per_win, "ticks_per_window": qprof["messages"] / max(1, qprof["launches"]),
             "member_periods_per_window": qprof["records"] / max(1, qprof["launches"]),
             "alg_bytes_rule": "21 B per member-period (SURVEY.md §8(d) ping phase) + per window the quiet check's "
-                              "reads: 4 B x 1,024-subject blocks of witness counts + 64 B of member words per row, "
+                              "reads: the 4-B count of non-zero witness blocks + 64 B of member words per row, "
                               "4 B per subject of the reference row, 4 B per timer-bucket queue (swim.h "
                               "swim_profile_quiet)"}
+
+
+def quiet_window_model(e, n, tpp, lengths=(1, 4, 20, 100), budget_s=3.0):
+    """How the headline depends on how far one swim_step call advances (after the timed region, on
+    the same engine): for calls of L periods each, the quiet window's GPU time (HIP events) and the
+    wall time per call; a least-squares fit window_us = fixed + per_tick x ticks gives the fixed cost
+    of a window and the marginal member-periods/s of its length-proportional part.  `one_period_step`
+    is the rate a caller sees that advances one period per call (the Java shim's
+    SimulatedCluster.advance)."""
+    import torch
+    pts = []
+    for L in lengths:
+        reps = max(2, min(50, int(200 // L)))
+        e.profile_enable(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        done = 0
+        for _ in range(reps):
+            e.step(L)
+            done += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / done
+        q = e.profile_quiet()
+        pts.append({"periods_per_call": L, "ticks_per_call": L * tpp, "calls": done,
+                    "windows": q["launches"], "window_us": q["total_ms"] * 1e3 / max(1, q["launches"]),
+                    "call_us": wall * 1e6, "member_periods_per_s": n * L / wall})
+    import numpy as np
+    xs = np.array([p["ticks_per_call"] for p in pts], dtype=float)
+    ys = np.array([p["window_us"] for p in pts], dtype=float)
+    cs = np.array([p["call_us"] for p in pts], dtype=float)
+    slope, fixed = np.polyfit(xs, ys, 1)
+    cslope, cfixed = np.polyfit(xs, cs, 1)
+    e.profile_enable(False)
+    return {"points": pts, "fixed_us_per_window": float(fixed), "us_per_tick": float(slope),
+            "marginal_member_periods_per_s": float(n / (slope * tpp) * 1e6) if slope > 0 else None,
+            "fixed_us_per_call": float(cfixed),
+            "one_period_step": pts[0]["member_periods_per_s"],
+            "note": "value = N x periods / wall time of ONE swim_step call over the timed periods: it rises with "
+                    "the periods per call (fixed_us_per_call is paid once per call); see points"}
 
 
 def merge_roofline(prof, world, local_shards, workload, n, dt, steps, tpp):
@@ -299,7 +365,10 @@ def step_roofline(stats, prof, fprof, dprof, qprof, ticks, gossip_ticks, dt, ste
     # the ticks that ran on the per-tick chain (the others ran inside quiet windows, whose bytes are
     # swim_profile_quiet's; the per-tick kernels are sampled one launch in three)
     chain = max(0, ticks - qprof["messages"])
-    parts = {"fd_pings": 21.0 * stats["pings"] if not qprof["launches"] else 0.0, "events": 16.0 * stats["events"],
+    # pings of the ticks on the per-tick chain: the quiet windows' pings are inside their own bytes
+    # (one ping per member-period they advanced, swim_profile_quiet's `records`)
+    chain_pings = max(0, stats["pings"] - qprof["records"])
+    parts = {"fd_pings": 21.0 * chain_pings, "events": 16.0 * stats["events"],
              "timers": 4.0 * stats["timers_fired"], "sync_classify": per(prof) * chain,
              "fanout": per(fprof) * gossip_ticks * chain / max(1, ticks), "deliver": per(dprof) * gossip_ticks * chain / max(1, ticks),
              "quiet_windows": float(qprof["alg_bytes"])}
@@ -537,7 +606,7 @@ def main():
     step = step_roofline(stats, prof, fprof, dprof, qprof, ticks, gossip_ticks, dt, args.steps, args.workload, n)
     # the roofline of the step's dominant kernels: the quiet windows' (k_quiet_scan + k_quiet_apply)
     # when they carried the step, else the whole per-tick chain against its wall time
-    line["roofline"] = quiet_roofline(qprof, args.workload, n) if qprof["launches"] else step
+    line["roofline"] = quiet_roofline(qprof, args.workload, n, args.steps, args.warmup) if qprof["launches"] else step
     line["roofline_step"] = step
     if prof["launches"]:
         line["roofline_merge"] = merge_roofline(prof, world, args.local_shards, args.workload, n, dt, args.steps, tpp)
@@ -547,6 +616,8 @@ def main():
         same = args.workload == "failures" and args.warmup == KILL_FIRST + KILL_EVERY and args.steps == 6 and n == 65536
         line["roofline_fanout"] = fanout_roofline(fprof, f"the timed window ({args.workload})", same)
         line["roofline_deliver"] = deliver_roofline(dprof, f"the timed window ({args.workload})", same)
+    if world == 1 and args.workload == "quiet" and qprof["launches"] and hook is None:
+        line["quiet_window_model"] = quiet_window_model(e, n, tpp)
     if world == 1 and args.workload == "quiet" and not args.no_extras and args.local_shards == 1 and hook is None:
         e.close()
         # (1) the per-tick kernel chain on the same workload (quiet windows off): the SYNC merge's

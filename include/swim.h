@@ -451,8 +451,8 @@ int32_t swim_get_quiet_stats(const swim_engine* e, swim_quiet_stats* out);
  * stream), every window while profiling is enabled (swim_profile_enable): launches = windows,
  * messages = ticks advanced, records = member-periods advanced (rows x ticks / ticks per period),
  * alg_bytes = 21 B per member-period (SURVEY.md §8(d) ping phase: list word, cursor, up word, view
- * word) + per window what the quiet check reads: 4 B x blocks of witness counts and 64 B of member
- * words per row, the reference row (4 B per subject per shard), 4 B per timer-bucket queue of the
+ * word) + per window what the quiet check reads: the 4-B count of non-zero witness blocks and 64 B
+ * of member words per row, the reference row (4 B per subject per shard), 4 B per timer-bucket queue of the
  * window.  The CPU oracle reports zeros. */
 int32_t swim_profile_quiet(swim_engine* e, swim_kernel_profile* out);
 

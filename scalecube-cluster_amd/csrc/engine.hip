@@ -354,10 +354,17 @@ __global__ void k_status(const uint32_t* ev_cnt, const uint32_t* err, uint32_t* 
   if (t == SUBQ) out[SUBQ] = *err;
 }
 
-static int32_t sync_and_collect(swim_engine* e) {
+static void launch_status(swim_engine* e) {
   for (size_t i = 0; i < e->sh.size(); ++i)
     k_status<<<1, 64, 0, e->stream>>>(e->sh[i].c.ev_cnt, e->sh[i].c.err, e->d_stat + i * (SUBQ + 1));
-  if (hipStreamSynchronize(e->stream) != hipSuccess) return hip_status() ? SWIM_EDEVICE : SWIM_EDEVICE;
+}
+// fresh: the status words were written by the last work on the stream and the stream has drained
+// (a quiet window launches k_status before its own synchronisation): no launch, no second wait
+static int32_t sync_and_collect(swim_engine* e, bool fresh = false) {
+  if (!fresh) {
+    launch_status(e);
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  }
   e->par_slot = 0;  // every staged Params upload has completed
   uint32_t err_all = 0;
   double fill = 0.0;  // fullest event sub-queue since the last drain
@@ -717,6 +724,7 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
     k_quiet_apply<<<g, 256, 0, s>>>(sd.d_par, T0, K, q, q_next, e->d_done, (uint32_t)kRebaseEvery);
   }
   if (prof) hipEventRecord(e->qev[1], s);
+  launch_status(e);  // (the drain after a window that ends the swim_step call needs no wait of its own)
   if (hipStreamSynchronize(s) != hipSuccess) return SWIM_EDEVICE;
   e->par_slot = 0;  // (the stream drained: the Params staging ring restarts)
   *done = std::min(__atomic_load_n(e->h_done, __ATOMIC_ACQUIRE), K);
@@ -724,19 +732,18 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, e->qev[0], e->qev[1]) == hipSuccess) e->qprof_ms += ms;
     // algorithmic bytes (swim.h swim_profile_quiet): SURVEY.md §8(d)'s 21 B per member-period of the
-    // ping phase, plus what the quiet check must read once per window: every owned row's block
-    // witness counts, 64 B of per-member words, the reference row, the window's timer buckets
-    uint64_t rows = 0, blocks = 0, nq = 0;
+    // ping phase, plus what the quiet check must read once per window: every owned row's count of
+    // non-zero witness blocks, 64 B of per-member words, the reference row, the window's timer buckets
+    uint64_t rows = 0, nq = 0;
     for (const Shard& sd : e->sh) {
       rows += sd.c.nl;
-      blocks = sd.c.blocks;
       nq += sd.c.wheel_nq;
     }
     const uint64_t mp = rows * (uint64_t)*done / e->P;
     e->qprof_windows++;
     e->qprof_ticks += *done;
     e->qprof_mp += mp;
-    e->qprof_bytes += 21ull * mp + rows * (4ull * blocks + 64ull) + 4ull * e->n * e->sh.size() +
+    e->qprof_bytes += 21ull * mp + rows * (4ull + 64ull) + 4ull * e->n * e->sh.size() +
                       4ull * std::min<uint64_t>(K, e->sh[0].c.wheel_mask + 1ull) * nq;
   }
   e->T += *done;
@@ -1007,7 +1014,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   const size_t nn = (size_t)nl * n;
   c.blocks = (n + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
   bool ok = sd.alloc(&c.recs, nn) && sd.alloc(&c.aux, nn) && sd.alloc(&c.ref, n) && sd.alloc(&c.dirty, n) &&
-            sd.alloc(&c.bdiff, (size_t)std::max(nl, 1u) * c.blocks) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
+            sd.alloc(&c.bdiff, (size_t)std::max(nl, 1u) * c.blocks) && sd.alloc(&c.bnz, std::max(nl, 1u)) && sd.alloc(&c.mem, nl) && sd.alloc(&c.up, n) && sd.alloc(&c.ping, nn) &&
             sd.alloc(&c.remote, nn) && sd.alloc(&c.slab_hot, (size_t)nl * c.gcap) && sd.alloc(&c.slab_cold, (size_t)nl * c.gcap) &&
             sd.alloc(&c.inf_over, (size_t)std::max(nl, 1u) * (c.inf_mask + 1)) &&
             sd.alloc(&c.gix, (size_t)nl * (c.gix_mask + 1)) && sd.alloc(&c.coll, (size_t)nl * c.hcap) &&
@@ -1392,11 +1399,13 @@ int32_t swim_destroy(swim_engine* e) {
 int32_t swim_step_ticks(swim_engine* e, uint32_t ticks) {
   if (!e) return SWIM_EINVAL;
   if (hipSetDevice(e->device) != hipSuccess) return SWIM_EDEVICE;
+  bool fresh = false;  // the last work on the stream was a quiet window (status words written, drained)
   for (uint32_t i = 0; i < ticks; ++i) {
     if (quiet_eligible(e) && e->T + 1 >= e->quiet_retry_at) {
       const uint32_t K = std::min(ticks - i, kQuietMax);
       uint32_t done = 0;
       if (int32_t rc = run_quiet(e, K, &done)) return rc;
+      fresh = true;
       i += done;
       if (done == K) {
         e->quiet_backoff = 1;
@@ -1410,13 +1419,14 @@ int32_t swim_step_ticks(swim_engine* e, uint32_t ticks) {
       if (i >= ticks) break;
     }
     if (int32_t rc = run_tick(e)) return rc;
+    fresh = false;
     if (++e->since_drain >= e->drain_every) {
       int32_t r = sync_and_collect(e);
       if (r == SWIM_EDEVICE) return r;
     }
   }
   if (hip_status() != SWIM_OK) return SWIM_EDEVICE;
-  int32_t rc = sync_and_collect(e);
+  int32_t rc = sync_and_collect(e, fresh);
   if (rc == SWIM_EDEVICE) return rc;
   if (e->rccl) {  // every rank reports a capacity error if any rank saw one
     uint32_t mine = e->err_seen ? 1u : 0u, any = 0;

@@ -83,14 +83,20 @@ struct alignas(16) GossipSched {
 };
 
 struct alignas(16) MemberDev {
-  uint64_t fd_period, ack_due, relay_due, g_counter, leave_seq;
+  // first 40 B: every word the quiet scan reads (k_quiet_scan, one 64-B sector per member)
+  uint64_t ack_due, relay_due;
+  uint32_t ping_cursor, ping_len, table_size, fd_sync_cnt;
+  uint32_t ins_rank;  // this phase's deferred pingMembers inserts (op chain: ins_head / ins_tail)
+  uint8_t join_now, join_pending, leave_pending;
+  uint8_t init_wait;  // start0's initial-sync Flux is still subscribed (init_total / init_done)
+  uint64_t fd_period, g_counter, leave_seq;
   int64_t fd_start, g_start, sync_start;
-  uint32_t ping_cursor, ping_len, ack_target, relay_target, relay_pending;
+  uint32_t ack_target, relay_target, relay_pending;
   uint32_t remote_len;
   int32_t remote_idx;
-  uint32_t table_size, members_size, leave_gossiper;
-  uint32_t ev_minor, fetch_ctr, fd_sync_cnt, init_total, init_done;
-  uint32_t ins_rank, ins_head, ins_tail;  // this phase's deferred pingMembers inserts (op chain)
+  uint32_t members_size, leave_gossiper;
+  uint32_t ev_minor, fetch_ctr, init_total, init_done;
+  uint32_t ins_head, ins_tail;
   uint32_t gix_base, gix_used;  // serial of slab[0]; gix slots taken since the index was (re)built
   uint32_t ack_late;  // 1 + ticks after the ping timeout that a late direct ack arrives (0 = none)
   uint64_t ack_to, relay_to;  // the ping's / the relay requests' timeout tick (an ack the inbound
@@ -99,12 +105,12 @@ struct alignas(16) MemberDev {
   uint32_t init_last;  // start0's initial sync: tick of the last answer (or of the start)
   uint32_t user_live;  // this member's own user gossips whose spread() has not completed (the emit
                        // round reads the states past the spreading window only while one is pending)
-  uint8_t joined, join_now, join_pending, leave_pending, leave_done, sync_on, gix_valid;
+  uint8_t joined, leave_done, sync_on, gix_valid;
   uint8_t ack_ok;    // ack_due is the tick the (delayed) ack arrives, not the ping timeout
   uint8_t relay_ok;  // relay_due is the tick the first relayed ack arrives, not the timeout
   uint8_t ack_gone, relay_gone;  // that ack says DEST_GONE (another member listens at the target's address)
-  uint8_t init_wait;  // start0's initial-sync Flux is still subscribed (init_total / init_done)
 };
+static_assert(sizeof(MemberDev) == 192, "MemberDev: 192 B (three 64-B sectors)");
 
 // GossipState + Gossip + MembershipRecord payload, 48 B.  GossipState.infected gains a member only
 // when the collector accepts the sequence id (onGossipReq :205-212): the first sender, plus one more
@@ -361,6 +367,7 @@ struct Ctx {
   // marked dirty).
   uint32_t* ref;     // [n]
   uint32_t* bdiff;   // [nl][blocks]
+  uint32_t* bnz;     // [nl] blocks of the row whose bdiff is non-zero (the quiet scan's O(1) row check)
   uint32_t* dirty;   // [n] 1: some row's record of the subject changed since the last rebase
   uint32_t blocks;   // ceil(n / 1024)
   MemberDev* mem;
@@ -532,12 +539,20 @@ __device__ __forceinline__ uint64_t cell_get(const Ctx& c, uint32_t v, uint32_t 
   return compose_cell(c.recs[i], c.aux[i]);
 }
 constexpr uint32_t BLK_SHIFT = 10;  // 1,024-subject blocks (= the SYNC classify unit)
+// bdiff[row][blk] += d (d = +-1), and the row's count of non-zero blocks follows the 0 <-> 1
+// transitions.  Each atomic returns a distinct old value, so the transitions of one block alternate
+// in atomic order and bnz is exact once the kernel's updates have all completed.
+__device__ __forceinline__ void bdiff_add(const Ctx& c, uint32_t row, uint32_t blk, int d) {
+  const uint32_t old = atomicAdd(&c.bdiff[(size_t)row * c.blocks + blk], (uint32_t)d);
+  if (d > 0 && old == 0u) atomicAdd(&c.bnz[row], 1u);
+  else if (d < 0 && old == 1u) atomicSub(&c.bnz[row], 1u);
+}
 // the block witness follows a record change of (v, s): old -> nr (atomic: a row's cells may change
 // from several threads of one kernel, e.g. entry-parallel timers)
 __device__ inline void rec_changed(const Ctx& c, uint32_t v, uint32_t s, uint32_t old, uint32_t nr) {
   const uint32_t rf = c.ref[s];
   const int d = (nr != rf ? 1 : 0) - (old != rf ? 1 : 0);
-  if (d) atomicAdd(&c.bdiff[(size_t)(v - c.lo) * c.blocks + (s >> BLK_SHIFT)], (uint32_t)d);
+  if (d) bdiff_add(c, v - c.lo, s >> BLK_SHIFT, d);
   c.dirty[s] = 1u;
 }
 __device__ __forceinline__ void cell_put(const Ctx& c, uint32_t v, uint32_t s, uint64_t cell) {

@@ -221,6 +221,7 @@ __global__ void k_init_rows(Ctx c, uint32_t n_initial) {
       const uint32_t in_blk = n_initial > b0 ? min(n_initial, b1) - b0 : 0u;
       c.bdiff[(size_t)(v - c.lo) * c.blocks + blk] = init ? 0u : in_blk;
     }
+    if (threadIdx.x == 0) c.bnz[v - c.lo] = init ? 0u : (n_initial + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
   }
 }
 
@@ -2644,7 +2645,7 @@ __device__ void rebase_witness(const Ctx& c) {
         for (uint32_t v = tid; v < c.nl; v += REB_BLOCK) {
           const uint32_t x = col[(size_t)v * c.n];
           const int d = (x != cand ? 1 : 0) - (x != rf ? 1 : 0);
-          if (d) atomicAdd(&c.bdiff[(size_t)v * c.blocks + blk], (uint32_t)d);
+          if (d) bdiff_add(c, v, blk, d);
         }
         if (tid == 0) c.ref[s] = cand;
       }

@@ -115,18 +115,9 @@ __global__ void __launch_bounds__(256) k_quiet_scan(KP, uint32_t K, QuietCtl* q,
     bool ok = g.len == 0 && c.compact_flag[i] == 0 && c.seg_flag[i] == 0 && m.ack_due < T && m.relay_due < T &&
               m.fd_sync_cnt == 0 && m.ins_rank == 0 && !m.join_now && !m.join_pending && !m.leave_pending &&
               !m.init_wait;
-    // the record row equals ref (its block witness counts are all zero)
-    const uint32_t* bd = c.bdiff + (size_t)i * c.blocks;
-    uint32_t any = 0;
-    if ((c.blocks & 3u) == 0) {  // 16-B loads (the row starts 16-B aligned)
-      const uint4* b4 = reinterpret_cast<const uint4*>(bd);
-      for (uint32_t k = 0; k < c.blocks / 4; ++k) {
-        const uint4 x = b4[k];
-        any |= x.x | x.y | x.z | x.w;
-      }
-    } else {
-      for (uint32_t k = 0; k < c.blocks; ++k) any |= bd[k];
-    }
+    // the record row equals ref (its block witness counts are all zero: the maintained count of
+    // non-zero blocks, swim_device.h bdiff_add)
+    const uint32_t any = c.bnz[i];
     ok = ok && any == 0;
     if (!ok) { quiet_fail(fail, 0); continue; }
     tmin = min(tmin, m.table_size);

@@ -1,4 +1,5 @@
-"""bench.py's own workloads at their own size, GPU against the threaded CPU oracle, bit-exact.
+"""bench.py's own workloads at their own size, GPU against the threaded CPU oracle, bit-exact —
+unsharded and over 8 in-process shards (BASELINE config 4's deployment plan on one GPU).
 
 The headline (config4-lan-quiet: N = 65,536, LAN defaults, aligned timers, staggered periodic SYNC)
 and the failures workload through its first kill's failure detection are run on libswimgpu.so and
@@ -25,16 +26,34 @@ N = 65536
 BOUNDARY_ROWS = [0, 1, 1023, 1024, 2047, 2048, 4095, 4096, 32767, 32768, 65534, 65535]
 
 
-def _engines(glib, workload, periods):
+def _engines(glib, workload, periods, local_shards=1):
     from swimgpu import abi
     out = {}
     for k, lib in (("gpu", glib), ("oracle", oracle.lib())):
         sch = bench.Schedule(workload, N, periods)
-        e = abi.Engine(lib, bench.make_config(lib), sch.capacity, N, 1)
+        cfg = bench.make_config(lib)
+        if k == "gpu":
+            cfg.local_shards = local_shards
+        e = abi.Engine(lib, cfg, sch.capacity, N, 1)
         sch.setup(e)
         out[k] = (e, sch)
     oracle.set_threads(out["oracle"][0], THREADS)
+    if local_shards > 1:
+        assert out["gpu"][0].shard_info()["world"] == local_shards
     return out
+
+
+def _run_steps(eng, members, steps, p=0):
+    """advance both engines by e.step(k) for each k of `steps` (one swim_step call each, exactly as
+    bench.py times them), comparing after every call; returns the last counters"""
+    st = None
+    for k in steps:
+        for key in ("gpu", "oracle"):
+            e, _ = eng[key]
+            e.step(k)
+        p += k
+        _, st = _compare(eng, members, f"period {p} (after step({k}))")
+    return st
 
 
 def _compare(eng, members, where):
@@ -88,6 +107,78 @@ def test_failures_first_kill_65536_matches_oracle(glib):
             p = upto
             _, st = _compare(eng, members, f"period {p}")
         assert st["gossips_created"] > 0 and st["gossip_messages"] > 0  # the SUSPECT storm started
+    finally:
+        for e, _ in eng.values():
+            e.close()
+
+
+def test_headline_quiet_65536_stepped_like_bench(glib):
+    """config4-lan-quiet stepped exactly as the driver's bench command times it (`bench.py --steps 20
+    --warmup 5`: step(5), then ONE step(20), a 200-tick quiet window) and as the default command
+    does (`--steps 40`: one 400-tick window): sampled full state, every event, every counter against
+    the oracle after each call, and the windows really ran on the GPU."""
+    eng = _engines(glib, "quiet", 65)
+    members = BOUNDARY_ROWS + list(range(517, N, 2311))[:28]
+    try:
+        g = eng["gpu"][0]
+        q0 = g.quiet_stats()
+        st = _run_steps(eng, members, (5, 20, 40))
+        q1 = g.quiet_stats()
+        assert st["pings"] == N * 65 and st["syncs"] > 0
+        assert q1["ticks"] - q0["ticks"] >= 600, q1  # the 200- and 400-tick calls ran as windows
+    finally:
+        for e, _ in eng.values():
+            e.close()
+
+
+@pytest.mark.parametrize("pull", [False, True], ids=["local", "pull"])
+def test_config4_sharded8_65536_quiet_matches_oracle(glib, monkeypatch, pull):
+    """BASELINE config 4 at its stated N = 65,536 over 8 in-process shards (the RCCL plan's exchange
+    kernels; `pull`: content rows through k_pull_rows' copies as over RCCL, SWIM_EXCHANGE_PULL=1)
+    against the UNSHARDED oracle, 14 periods with quiet windows on: step(2) on the per-tick chain
+    (cross-shard SYNC / SYNC_ACK exchange every tick), then windows of 2 / 5 / 5 periods, each of
+    which needs every shard's witness ref to agree.  Sampled full state incl. the
+    shard boundaries, all events, all counters."""
+    if pull:
+        monkeypatch.setenv("SWIM_EXCHANGE_PULL", "1")
+    eng = _engines(glib, "quiet", 14, local_shards=8)
+    sz = N // 8
+    members = sorted(set(BOUNDARY_ROWS + [sz - 1, sz, 3 * sz - 1, 3 * sz, 7 * sz - 1, 7 * sz] +
+                         list(range(211, N, 3001))[:20]))
+    try:
+        g = eng["gpu"][0]
+        g.set_quiet_path(False)
+        st = _run_steps(eng, members, (2,))
+        g.set_quiet_path(True)
+        q0 = g.quiet_stats()
+        st = _run_steps(eng, members, (2, 5, 5), p=2)
+        q1 = g.quiet_stats()
+        assert st["pings"] == N * 14 and st["syncs"] > 0
+        assert q1["windows"] > q0["windows"] and q1["ticks"] - q0["ticks"] >= 100, (q0, q1)
+    finally:
+        for e, _ in eng.values():
+            e.close()
+
+
+def test_failures_sharded8_65536_first_kill_matches_oracle(glib):
+    """The failures workload at N = 65,536 over 8 in-process shards through its first kill (member 17
+    at period 10) and the SUSPECT storm that follows: every GOSSIP_REQ to a member of another shard
+    crosses E1 (k_recv_msgs), SYNCs E2 / E3; against the unsharded oracle after periods 10, 11, 12,
+    14."""
+    eng = _engines(glib, "failures", 14, local_shards=8)
+    sz = N // 8
+    victim = 17
+    members = sorted(set(BOUNDARY_ROWS + [16, victim, 18, sz - 1, sz, 5 * sz - 1, 5 * sz] +
+                         list(range(733, N, 2729))[:20]))
+    p = 0
+    try:
+        for upto in (10, 11, 12, 14):
+            for k in ("gpu", "oracle"):
+                e, sch = eng[k]
+                sch.run(e, p, upto)
+            p = upto
+            _, st = _compare(eng, members, f"period {p}")
+        assert st["gossips_created"] > 0 and st["gossip_messages"] > 0
     finally:
         for e, _ in eng.values():
             e.close()

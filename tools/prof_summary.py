@@ -1,10 +1,11 @@
 """Summarise tools/profile.sh output (rocprofv3 SQLite databases) into committed profile files.
 
-    python tools/prof_summary.py gpurun_out/prof/<tag> profiles/<round>_<tag>
+    python tools/prof_summary.py gpurun_out/prof/<tag> profiles/<round>_<tag> [STEPS WARMUP]
 
 writes <out>_kernel_stats.csv (per-kernel calls / total / average / share, from the kernel-trace
 pass) and <out>_pmc.json (per-kernel, per-launch HBM bytes from the separate FETCH_SIZE and
-WRITE_SIZE passes).  Corrections follow /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE is
+WRITE_SIZE passes; per kernel also the bytes of its last launch, and the profiled bench command's
+--steps / --warmup, so that bench.py attaches traffic only to the window of the same length).  Corrections follow /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE is
 in KiB and on gfx950 reports exactly half the bytes of a wide (16 B / lane) coalesced streaming
 read, so it is doubled; WRITE_SIZE (KiB) is exact for 16-B-per-lane streaming stores.
 """
@@ -32,6 +33,16 @@ def pmc(prefix, which):
     return {(r[0], r[1]): (int(r[2]), float(r[3])) for r in con.execute(q)}
 
 
+def pmc_last(prefix, which):
+    """per kernel, the counter value of its LAST dispatch (the bench's timed window is the last one)"""
+    con = _db(f"{prefix}_{which}")
+    q = "select kernel_name, value from counters_collection order by dispatch_id"
+    last = {}
+    for name, v in con.execute(q):
+        last[name] = float(v)
+    return last
+
+
 def main(src, out):
     ks = kernel_stats(src)
     with open(f"{out}_kernel_stats.csv", "w", newline="") as f:
@@ -48,9 +59,15 @@ def main(src, out):
         per.setdefault(name, {})["write_bytes_per_launch"] = avg * 1024.0
     for v in per.values():
         v["hbm_bytes_per_launch"] = v.get("fetch_bytes_per_launch", 0.0) + v.get("write_bytes_per_launch", 0.0)
+    lf, lw = pmc_last(src, "fetch"), pmc_last(src, "write")
+    for name, v in per.items():
+        if name in lf and name in lw:
+            v["last_launch_hbm_bytes"] = 2.0 * lf[name] * 1024.0 + lw[name] * 1024.0
     doc = {"source": src, "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count of 16-B/lane streaming "
                                         "reads, MI355X_MICROARCH.md HBM); WRITE_SIZE KiB x 1024",
            "kernels": per}
+    if len(sys.argv) > 4:  # the profiled bench command's window: --steps, --warmup
+        doc["bench_args"] = {"steps": int(sys.argv[3]), "warmup": int(sys.argv[4])}
     with open(f"{out}_pmc.json", "w") as f:
         json.dump(doc, f, indent=1, sort_keys=True)
     for k in ks[:12]:
