@@ -354,7 +354,8 @@ typedef struct swim_member_state {
   uint32_t relay_pending;
   uint64_t relay_due;        /* 0 = none */
   uint32_t leave_gossiper;   /* id of the LEAVING gossip a graceful leave waits on */
-  uint32_t pad2;
+  uint32_t pending_acks;     /* merged SYNCs whose SYNC_ACK waits for their updateMembership Monos
+                                (onSync :394-415) + start0 groups its doFinally waits for (:277-289) */
   uint64_t leave_seq;
 } swim_member_state;
 int32_t swim_read_member(swim_engine* e, uint32_t m, swim_member_state* out);

@@ -76,6 +76,26 @@ struct PendingFetch {
   int32_t inc;
   uint32_t reason, phase, stage, f, d, ver;
   uint64_t t0, due;
+  uint32_t link;  // the PendingAck (seq) whose Mono waits on this fetch, or NONE
+};
+
+// A merged message whose updateMembership Monos have not all completed (MembershipProtocolImpl.java
+// syncMembership :491-509, Flux.mergeDelayError): onSync's SYNC_ACK waits for them (:394-415, the
+// ack is prepared and sent in doOnSuccess), and so does start0's doFinally for an initial SYNC_ACK
+// merged through its flatMap (:277-289).  A Mono waits on (a) an ALIVE admission's metadata fetch
+// (:630-660 -> MetadataStoreImpl.fetchMetadata :146-185): a response ends it at its arrival, a failed
+// send at once, anything unanswered at metadataTimeout; (b) a new LEAVING record's gossip
+// (onLeavingDetected :710-733 returns spreadMembershipGossip, i.e. GossipProtocolImpl.spread's Mono,
+// which completes when the gossip is most likely disseminated, :167-180 / :360-368).  Every other
+// branch completes synchronously.
+enum : uint32_t { PA_INITIAL_ACK = 1, PA_INIT = 2 };
+struct PendingAck {
+  uint32_t to;     // the SYNC's sender (the SYNC_ACK's receiver); PA_INIT: none
+  uint32_t flags;  // PA_INITIAL_ACK: the SYNC was start0's (the ack goes to its Flux); PA_INIT: a start0 group
+  uint32_t wn;     // fetches still in flight
+  uint64_t ready;  // the tick the last completed / timed-out wait ended
+  uint64_t gp;     // 1 + the infection period of the LEAVING gossips waited on (0: none)
+  uint32_t seq;    // per member, in creation order (canonical order of the deferred acks)
 };
 
 // ----------------------------------------------------------------------------- SequenceIdCollector
@@ -199,6 +219,12 @@ struct Member {
   // per-tick bookkeeping
   uint32_t ev_minor = 0, fetch_ctr = 0;
   std::vector<PendingFetch> fq;  // metadata round trips in flight, in issue order
+  // deferred SYNC_ACKs and start0 groups (PendingAck), in creation order; the waits of the message
+  // being merged (w_link = the seq its PendingAck will take, NONE outside such a merge)
+  std::vector<PendingAck> pack;
+  uint32_t pack_seq = 0, init_pend = 0;
+  uint32_t w_link = NONE, w_n = 0;
+  uint64_t w_ready = 0, w_gp = 0;
 };
 
 // cell helpers
@@ -250,6 +276,7 @@ struct swim_engine {
   uint32_t key[2]{};
   uint64_t T = 0;
   uint32_t tick_ms = 0, P = 0, to_ticks = 0, relay_ticks = 0, G = 0, S = 0, sync_to_ticks = 0;
+  uint32_t mt_ticks = 0;  // ceil(metadataTimeout / tick): an unanswered fetch fails this many ticks after it was sent
   std::vector<Member> m;
   std::vector<uint32_t> seeds;
   std::vector<uint8_t> is_seed;
@@ -482,21 +509,50 @@ struct swim_engine {
   // point); a delayed round trip goes to the viewer's queue and completes in the FETCH phase of its
   // arrival tick (phase_fetch).
   bool fetch_start(uint32_t v, const Record& r1, Reason reason, uint32_t phase) {
-    const uint32_t f = m[v].fetch_ctr++;
+    Member& mv = m[v];
+    const uint32_t f = mv.fetch_ctr++;
     STT().fetches++;
     const uint32_t s = r1.member, d = dst(s);
+    // an unanswered request fails at metadataTimeout (:160-165): a Mono waiting on it ends then
+    auto timeout = [&] { if (mv.w_link != NONE) mv.w_ready = std::max(mv.w_ready, T + mt_ticks); };
     // the request goes to s's address; another member listening there does not answer (:209)
-    if (d != s || out_fail(v, d, draw(v, SWIM_STREAM_FETCH_REQ, phase, f))) return false;
+    if (d != s) { timeout(); return false; }
+    if (out_fail(v, d, draw(v, SWIM_STREAM_FETCH_REQ, phase, f))) return false;  // fails at once
     const uint32_t d1 = delay_tab.empty() ? 0 : delay_ticks(v, d, v, SWIM_STREAM_FETCH_REQ_DELAY, phase, f);
-    if ((uint64_t)d1 * tick_ms >= (uint64_t)cfg.metadata_timeout) return false;
-    PendingFetch p{s, r1.inc, (uint32_t)reason, phase, 1, f, d, 0, T, T + d1};
+    if ((uint64_t)d1 * tick_ms >= (uint64_t)cfg.metadata_timeout) { timeout(); return false; }
+    PendingFetch p{s, r1.inc, (uint32_t)reason, phase, 1, f, d, 0, T, T + d1, mv.w_link};
     if (d1 == 0) {
       const int r = fetch_stage1(v, p);
       if (r == 1) STT().fetch_ok++;
+      if (r == 0) timeout();
       if (r != 2) return r == 1;
     }
-    m[v].fq.push_back(p);
+    if (mv.w_link != NONE) mv.w_n++;
+    mv.fq.push_back(p);
     return false;
+  }
+  // the PendingAck of member v with sequence number seq (nullptr: none — cancelled with start0's Flux)
+  PendingAck* pack_find(uint32_t v, uint32_t seq) {
+    for (auto& a : m[v].pack)
+      if (a.seq == seq) return &a;
+    return nullptr;
+  }
+  // a message's merge starts / ends: its waits are collected, and a message whose Monos have not all
+  // completed by now becomes a PendingAck (returns true: the SYNC_ACK waits)
+  void wait_begin(uint32_t v) {
+    Member& mv = m[v];
+    mv.w_link = mv.pack_seq;
+    mv.w_n = 0;
+    mv.w_ready = 0;
+    mv.w_gp = 0;
+  }
+  bool wait_end(uint32_t v, uint32_t to, uint32_t flags) {
+    Member& mv = m[v];
+    mv.w_link = NONE;
+    if (mv.w_n == 0 && mv.w_gp == 0 && mv.w_ready <= T) return false;
+    mv.pack.push_back(PendingAck{to, flags, mv.w_n, mv.w_ready, mv.w_gp, mv.pack_seq++});
+    if (flags & PA_INIT) mv.init_pend++;
+    return true;
   }
   // the request arrives at d (now): 0 = the round trip failed, 1 = the response arrived too (no delay
   // on it), 2 = the response is in flight (p.due = its arrival tick)
@@ -550,6 +606,8 @@ struct swim_engine {
       if (!present || r0v.status != SWIM_LEAVING) {
         schedule_timer(v, s);
         spread_gossip(v, r1, SWIM_ORIG_LEAVING);
+        // onLeavingDetected returns the gossip's spread() Mono: a merge waits until it disseminated
+        if (mv.w_link != NONE) mv.w_gp = mv.g_period + 1;
       }
       return;
     }
@@ -954,6 +1012,15 @@ struct swim_engine {
                  g.rec.member);
           }
         }
+        // PendingAck waits on LEAVING gossips (onLeavingDetected's spread() Monos): every gossip of one
+        // wait has the same infection period, so they complete together — in this round if it finds
+        // them disseminated and the sweep above has not dropped them (a swept gossip's Mono never
+        // completes)
+        for (auto& a : mv.pack)
+          if (a.gp && period > a.gp - 1 + spread && !(period > a.gp - 1 + sweep)) {
+            a.gp = 0;
+            a.ready = std::max(a.ready, T);
+          }
       }
     });
     for (auto& lt : later)
@@ -1063,15 +1130,21 @@ struct swim_engine {
   std::map<uint64_t, std::vector<SyncFlight>> sync_in_flight;
   // a message merged this tick: arrivals sent in earlier ticks first (canonical order (receiver,
   // sending tick, sender, ordinal / rank))
+  // phantom: a deferred SYNC_ACK whose waits completed (PendingAck) — it merges nothing and takes its
+  // ack's place at the front of its sender's inbox, in creation order (pre = its seq); wait: the
+  // message's Monos are still running, its SYNC_ACK waits (a PendingAck was made)
   struct SyncArr {
     uint32_t to, from, ordinal;
     uint64_t sent;
     bool initial;
     const std::vector<uint64_t>* content;
+    uint64_t pre = ~0ull;
+    bool phantom = false, wait = false;
   };
   static void sort_arrivals(std::vector<SyncArr>& a) {
     std::stable_sort(a.begin(), a.end(), [](const SyncArr& x, const SyncArr& y) {
       if (x.to != y.to) return x.to < y.to;
+      if (x.pre != y.pre) return x.pre < y.pre;
       if (x.sent != y.sent) return x.sent < y.sent;
       if (x.from != y.from) return x.from < y.from;
       return x.ordinal < y.ordinal;
@@ -1081,10 +1154,30 @@ struct swim_engine {
   void phase_sync() {
     const uint32_t nt = std::max(1u, threads);
     std::vector<std::vector<SyncReq>> rq(nt);
+    std::vector<std::vector<SyncArr>> ph(nt);
     par(0, n, [&](uint32_t a, uint32_t b, uint32_t t) {
       for (uint32_t v = a; v < b; ++v) {
         Member& mv = m[v];
-        if (!mv.up) { mv.fd_sync.clear(); continue; }
+        if (!mv.up) {  // (a stopped member's waits and deferred acks are void)
+          mv.fd_sync.clear();
+          mv.pack.clear();
+          mv.init_pend = 0;
+          continue;
+        }
+        // PendingAcks whose Monos have all completed: a deferred SYNC_ACK is sent now (doOnSuccess,
+        // :399-413), a start0 group leaves the count its doFinally waits for
+        if (!mv.pack.empty()) {
+          std::vector<PendingAck> keep;
+          for (const PendingAck& pa : mv.pack) {
+            if (pa.wn || pa.gp || pa.ready > T) { keep.push_back(pa); continue; }
+            if (pa.flags & PA_INIT) { mv.init_pend--; continue; }
+            SyncArr x{v, pa.to, 0, T, (pa.flags & PA_INITIAL_ACK) != 0, nullptr};
+            x.pre = pa.seq;
+            x.phantom = true;
+            ph[t].push_back(x);
+          }
+          mv.pack.swap(keep);
+        }
         uint32_t k = 0;
         if (sync_due(mv)) {  // doSync (:339-357)
           uint32_t tg = select_sync_address(v);
@@ -1108,7 +1201,9 @@ struct swim_engine {
         sync_in_flight.erase(it);
       }
     }
-    if (reqs.empty() && arriving.empty()) {
+    std::vector<SyncArr> phantoms;
+    for (auto& x : ph) phantoms.insert(phantoms.end(), x.begin(), x.end());
+    if (reqs.empty() && arriving.empty() && phantoms.empty()) {
       finish_joins();
       return;
     }
@@ -1158,6 +1253,7 @@ struct swim_engine {
       if (!in_pass(f.to, f.from)) continue;  // dropped by the receiver's inbound filter on arrival
       in.push_back(SyncArr{f.to, f.from, f.ordinal, f.sent, f.initial, &f.content});
     }
+    in.insert(in.end(), phantoms.begin(), phantoms.end());
     sort_arrivals(in);
     // receivers' inboxes: in[gs[g] .. gs[g + 1])
     std::vector<size_t> gs;
@@ -1171,7 +1267,12 @@ struct swim_engine {
         const uint32_t r = in[gs[g]].to;
         m[r].ev_minor = 0;
         m[r].fetch_ctr = 0;
-        for (size_t i = gs[g]; i < gs[g + 1]; ++i) sync_membership(r, *in[i].content, SYNC, SWIM_PHASE_SYNC);
+        for (size_t i = gs[g]; i < gs[g + 1]; ++i) {
+          if (in[i].phantom) continue;
+          wait_begin(r);
+          sync_membership(r, *in[i].content, SYNC, SWIM_PHASE_SYNC);
+          in[i].wait = wait_end(r, in[i].from, in[i].initial ? (uint32_t)PA_INITIAL_ACK : 0u);
+        }
       }
     });
     // SYNC_ACK content: the receiver's table once all its requests are merged
@@ -1184,6 +1285,7 @@ struct swim_engine {
       for (size_t i = gs[g]; i < gs[g + 1]; ++i) {
         const SyncArr& q = in[i];
         const uint32_t qr = (uint32_t)(i - gs[g]);
+        if (q.wait) continue;  // sent when the message's Monos have completed (a phantom then)
         if (lost(out_loss(q.to, q.from), draw(q.to, SWIM_STREAM_SYNCACK_OUT, qr, 0))) continue;
         const uint32_t k = delay_ticks(q.to, q.from, q.to, SWIM_STREAM_SYNCACK_DELAY, qr, 0);
         if (k) {  // the receiver's state and inbound filter when it arrives
@@ -1214,7 +1316,10 @@ struct swim_engine {
         for (size_t i = as[g]; i < as[g + 1]; ++i) {
           if (acks[i].initial && !ms.init_wait) continue;
           STT().sync_acks++;
+          // start0's flatMap (:283): its doFinally waits for the initial merge's Monos too
+          if (acks[i].initial) wait_begin(s);
           sync_membership(s, *acks[i].content, acks[i].initial ? INITIAL_SYNC : SYNC, SWIM_PHASE_SYNCACK);
+          if (acks[i].initial) wait_end(s, NONE, PA_INIT);
           if (acks[i].initial) {
             ms.init_done++;
             ms.init_last = T;
@@ -1225,23 +1330,31 @@ struct swim_engine {
     finish_joins();
   }
 
-  // start0's doFinally (:285-289): periodic sync starts once every initial SYNC was answered or
-  // failed fast; else after syncTimeout without an answer (Flux.timeout :281 restarts at every
-  // answer).  Without message delay every source resolves within the start tick (the start is
-  // decided then, as complete ? now : now + syncTimeout); with delay the decision waits for the last
-  // answer or the timeout, which fires at the tick init_last + syncTimeout (an answer arriving in
-  // that tick is too late).
+  // start0's doFinally (:285-289).  When every initial SYNC was answered or failed fast, Flux.take
+  // completes and doFinally runs once the flatMap's inner Monos — the initial merges' fetches and
+  // LEAVING spreads (PendingAck groups, PA_INIT) — have completed: periodic sync starts at the tick the
+  // last of them ends.  Otherwise Flux.timeout (:281, restarted at every answer) fires at tick init_last
+  // + syncTimeout (an answer arriving in that tick is too late), cancels the inner Monos still running
+  // (their fetches complete into nothing) and doFinally runs then.
   void finish_joins() {
-    const bool delayed = !delay_tab.empty();
     for (uint32_t v = 0; v < n; ++v) {
       Member& mv = m[v];
       mv.join_now = false;
       if (!mv.init_wait) continue;
       int64_t start;
-      if (!delayed) start = (int64_t)T + (mv.init_done == mv.init_total ? 0 : (int64_t)sync_to_ticks);
-      else if (mv.init_done == mv.init_total) start = (int64_t)T;  // the last source completed now
-      else if (T + 1 >= mv.init_last + sync_to_ticks) start = (int64_t)(mv.init_last + sync_to_ticks);
-      else continue;
+      if (mv.init_done == mv.init_total) {
+        if (mv.init_pend) continue;
+        start = (int64_t)T;
+      } else if (T + 1 >= mv.init_last + sync_to_ticks) {
+        start = (int64_t)(mv.init_last + sync_to_ticks);
+        std::vector<PendingAck> keep;
+        for (const PendingAck& pa : mv.pack)
+          if (!(pa.flags & PA_INIT)) keep.push_back(pa);
+        mv.pack.swap(keep);
+        mv.init_pend = 0;
+      } else {
+        continue;
+      }
       mv.sync_on = true;
       mv.sync_start = start;
       mv.init_wait = false;
@@ -1262,6 +1375,8 @@ struct swim_engine {
       mv.init_total = mv.init_done = 0;
       mv.init_last = T;
       mv.init_wait = true;
+      mv.pack.clear();
+      mv.init_pend = 0;
       mv.fd_start = (int64_t)T;
       mv.g_start = (int64_t)T;
       mv.row[v] = B_IN_TABLE | B_IN_MEMBERS;  // ALIVE inc 0 (MembershipProtocolImpl :146-149)
@@ -1289,7 +1404,16 @@ struct swim_engine {
           continue;
         }
         const int r = p.stage == 1 ? fetch_stage1(v, p) : (fetch_stage2(v, p) ? 1 : 0);
-        if (r == 2) keep.push_back(p);
+        if (r == 2) {
+          keep.push_back(p);
+          continue;
+        }
+        if (p.link != NONE) {  // the Mono waiting on it ends now (a response) or at the timeout
+          PendingAck* pa = pack_find(v, p.link);
+          if (!pa) continue;  // cancelled with start0's Flux: its doOnSuccess never runs
+          pa->wn--;
+          pa->ready = std::max(pa->ready, r == 1 ? T : p.t0 + mt_ticks);
+        }
         if (r == 1) {
           STT().fetch_ok++;
           apply_alive(v, Record{p.s, SWIM_ALIVE, p.inc}, (Reason)p.reason, SWIM_PHASE_FETCH, p.ver);
@@ -1469,6 +1593,7 @@ int32_t swim_create(const swim_config* cfg, uint32_t capacity, uint32_t n_initia
   e->G = (uint32_t)c.gossip_interval / tick;
   e->S = (uint32_t)c.sync_interval / tick;
   e->sync_to_ticks = (uint32_t)c.sync_timeout / tick;
+  e->mt_ticks = (uint32_t)(((int64_t)c.metadata_timeout + tick - 1) / tick);
   try {
     e->m.resize(capacity);
     e->is_seed.assign(capacity, 0);
@@ -1815,6 +1940,7 @@ int32_t swim_read_member(swim_engine* e, uint32_t v, swim_member_state* o) {
   o->relay_due = mv.relay_due;
   o->leave_gossiper = mv.leave_pending ? mv.leave_gossiper : 0xffffffffu;
   o->leave_seq = mv.leave_pending ? mv.leave_seq : 0;
+  o->pending_acks = (uint32_t)mv.pack.size();
   return SWIM_OK;
 }
 

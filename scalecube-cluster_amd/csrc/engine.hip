@@ -1060,7 +1060,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&b.item_total, b.req_cap) && sd.alloc(&b.pool, b.pool_cap) &&
             sd.alloc(&b.rev_chunk, (size_t)b.req_cap * b.chunks) && sd.alloc(&b.rev_total, b.req_cap) &&
             sd.alloc(&b.row_mod, nl) &&
-            sd.alloc(&b.pend, (size_t)kApplyGrid * n) && sd.alloc(&sd.d_par, 1) && sd.alloc(&b.senders, nl);
+            sd.alloc(&b.pend, (size_t)kApplyGrid * n) && sd.alloc(&sd.d_par, 1) && sd.alloc(&b.senders, nl) &&
+            sd.alloc(&c.pa, (size_t)std::max(nl, 1u) * PA_CAP) && sd.alloc(&c.pa_n, std::max(nl, 1u));
   if (ok && multi) {
     ok = alloc_xreg(e, sd, e->rccl) == SWIM_OK && sd.alloc(&b.rx_cnt, 4 * MAXW) &&
          sd.alloc(&b.rx_stops, (size_t)e->world * b.tx_stop_cap) && sd.alloc(&b.rx_stop_n, 1) && sd.alloc(&sd.peers, 1);
@@ -1076,6 +1077,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(c.inf_over, 0xff, sizeof(InfOver) * (size_t)std::max(nl, 1u) * (c.inf_mask + 1), s);  // INF_EMPTY
   hipMemsetAsync(c.spill_ctl, 0, sizeof(SpillCtl) * NTIER, s);
   hipMemsetAsync(c.seg_flag, 0, 4 * (size_t)nl, s);
+  hipMemsetAsync(c.pa_n, 0, 4 * (size_t)std::max(nl, 1u), s);
   hipMemsetAsync(c.wheel, 0xff, sizeof(uint64_t) * ((size_t)c.wheel_pages << c.wheel_pshift), s);  // WHEEL_EMPTY
   hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1) * c.wheel_nq, s);
   hipMemsetAsync(c.wheel_pt, 0xff, sizeof(uint32_t) * (c.wheel_mask + 1) * c.wheel_nq * c.wheel_ptmax, s);
@@ -1876,6 +1878,9 @@ int32_t swim_read_member(swim_engine* e, uint32_t v, swim_member_state* o) {
   o->relay_due = m.relay_due;
   o->leave_gossiper = m.leave_pending ? m.leave_gossiper : 0xffffffffu;
   o->leave_seq = m.leave_pending ? m.leave_seq : 0;
+  uint32_t pn = 0;
+  if (hipMemcpy(&pn, sd->c.pa_n + (v - sd->c.lo), 4, hipMemcpyDeviceToHost) != hipSuccess) return SWIM_EDEVICE;
+  o->pending_acks = pn;
   return SWIM_OK;
 }
 

@@ -25,7 +25,8 @@
 namespace swimdev {
 
 constexpr uint32_t NONE = 0xffffffffu;
-enum : uint32_t { MF_FDSYNC = 1, MF_JOIN = 2, MF_LEAVE = 4 };  // Ctx.mflag bits
+// Ctx.mflag bits (MF_PACK: the member holds PendingAcks, see PAck)
+enum : uint32_t { MF_FDSYNC = 1, MF_JOIN = 2, MF_LEAVE = 4, MF_PACK = 8 };
 constexpr int NTIER = 4;       // spilled-collector block tiers
 constexpr int FD_SYNC_MAX = 33;  // FD-triggered SYNCs per member per tick (<= 2k+1)
 
@@ -41,6 +42,7 @@ enum : uint32_t {
   ERR_XPTR = 1u << 17,      // SWIM_DEBUG_SYNC: a sharded tick would dereference a null exchange pointer
   ERR_SDELAY = 1u << 18,    // delayed SYNCs / SYNC_ACKs: a delay bucket or the park slots ran out
   ERR_FETCHQ = 1u << 19,    // more delayed GET_METADATA round trips in flight than the fetch queue holds
+  ERR_PACK = 1u << 20,      // a member holds more merged messages waiting on their Monos than PA_CAP
 };
 
 // A GET_METADATA round trip in flight under message delay (MetadataStoreImpl.fetchMetadata :146-185):
@@ -53,6 +55,26 @@ struct FetchEnt {
   uint32_t f;
   uint32_t info;  // phase | reason << 4 | stage << 8
   uint32_t d, ver, t0, due, next;
+  uint32_t link;  // seq of the viewer's PAck waiting on this fetch, or NONE
+};
+
+// A merged message whose updateMembership Monos have not all completed (syncMembership
+// :491-509, Flux.mergeDelayError): onSync's SYNC_ACK waits for them (MembershipProtocolImpl.java
+// :394-415, prepared and sent in doOnSuccess), and so does start0's doFinally for an initial SYNC_ACK
+// merged through its flatMap (:277-289).  A Mono waits on an ALIVE admission's metadata fetch (ended
+// by its response, at once by a failed send, else at metadataTimeout) or on a new LEAVING record's
+// gossip (onLeavingDetected returns spreadMembershipGossip: GossipProtocolImpl.spread's Mono ends when
+// the gossip most likely disseminated, :167-180).  Per member, in creation order (Ctx.pa, pa_n);
+// oracle: PendingAck.
+constexpr uint32_t PA_CAP = 64;
+enum : uint32_t { PA_INITIAL_ACK = 1, PA_INIT = 2 };  // the deferred ack answers start0 / a start0 group
+struct PAck {
+  uint32_t to;     // the SYNC's sender (PA_INIT: unused)
+  uint32_t flags;
+  uint32_t wn;     // fetches still in flight
+  uint32_t ready;  // the tick the last completed or timed-out wait ended
+  uint32_t gp;     // 1 + the infection period of the LEAVING gossips waited on (0: none)
+  uint32_t seq;
 };
 
 // stats slots (swim_stats order)
@@ -109,8 +131,12 @@ struct alignas(16) MemberDev {
   uint8_t ack_ok;    // ack_due is the tick the (delayed) ack arrives, not the ping timeout
   uint8_t relay_ok;  // relay_due is the tick the first relayed ack arrives, not the timeout
   uint8_t ack_gone, relay_gone;  // that ack says DEST_GONE (another member listens at the target's address)
+  // PendingAcks (PAck): the next seq, the start0 groups pending; the waits of the message being merged
+  // (w_link1 = 1 + the seq its PAck will take, 0 outside such a merge)
+  uint32_t pack_seq, init_pend;
+  uint32_t w_link1, w_n, w_ready, w_gp;
 };
-static_assert(sizeof(MemberDev) == 192, "MemberDev: 192 B (three 64-B sectors)");
+static_assert(sizeof(MemberDev) == 224, "MemberDev: 224 B (the quiet scan's words in the first 64-B sector)");
 
 // GossipState + Gossip + MembershipRecord payload, 48 B.  GossipState.infected gains a member only
 // when the collector accepts the sequence id (onGossipReq :205-212): the first sender, plus one more
@@ -435,6 +461,8 @@ struct Ctx {
   uint32_t* fq_tail;
   uint32_t* fq_cnt;
   uint32_t fq_cap;
+  PAck* pa;        // [nl][PA_CAP] PendingAcks, creation order
+  uint32_t* pa_n;  // [nl]
   uint8_t* is_seed;
   uint32_t* seeds;
   uint32_t n_seeds;
@@ -1228,22 +1256,38 @@ __device__ inline int fetch_stage1(const Ctx& c, uint32_t v, FetchEnt& e) {
   if (d2 == 0) return c.up[v] && in_pass(c, v, d) ? 1 : 0;
   return 2;
 }
+// ticks from a fetch's send to its metadataTimeout (:160-165)
+__device__ __forceinline__ uint32_t mt_ticks(const Ctx& c) { return (c.metadata_timeout + c.tick_ms - 1) / c.tick_ms; }
 __device__ inline bool fetch_start(const Ctx& c, uint32_t v, uint32_t s, int32_t inc, int reason, uint32_t phase) {
-  const uint32_t f = mem(c, v).fetch_ctr++;
+  MemberDev& m = mem(c, v);
+  const uint32_t f = m.fetch_ctr++;
   stat_add(c, ST_FETCHES, 1);
-  // the request goes to s's address; another member listening there does not answer (:209)
+  const uint32_t lk1 = m.w_link1;  // a merge whose Monos are waited for (PAck)
+  // the request goes to s's address; another member listening there does not answer (:209): the
+  // Mono fails at metadataTimeout
   const uint32_t d = dst(c, s);
-  if (d != s || out_fail(c, v, d, v, SWIM_STREAM_FETCH_REQ, phase, f)) return false;
+  const uint32_t to_tick = (uint32_t)c.T + mt_ticks(c);
+  if (d != s) {
+    if (lk1) m.w_ready = max(m.w_ready, to_tick);
+    return false;
+  }
+  if (out_fail(c, v, d, v, SWIM_STREAM_FETCH_REQ, phase, f)) return false;  // fails at once
   const uint32_t d1 = delay_ticks(c, v, d, v, SWIM_STREAM_FETCH_REQ_DELAY, phase, f);
-  if ((uint64_t)d1 * c.tick_ms >= (uint64_t)c.metadata_timeout) return false;
+  if ((uint64_t)d1 * c.tick_ms >= (uint64_t)c.metadata_timeout) {
+    if (lk1) m.w_ready = max(m.w_ready, to_tick);
+    return false;
+  }
   FetchEnt e;
   e.s = s; e.inc = inc; e.f = f; e.info = phase | ((uint32_t)reason << 4) | (1u << 8);
   e.d = d; e.ver = 0; e.t0 = (uint32_t)c.T; e.due = (uint32_t)c.T + d1; e.next = NONE;
+  e.link = lk1 ? lk1 - 1 : NONE;
   if (d1 == 0) {
     const int r = fetch_stage1(c, v, e);
     if (r == 1) stat_add(c, ST_FETCH_OK, 1);
+    if (r == 0 && lk1) m.w_ready = max(m.w_ready, to_tick);
     if (r != 2) return r == 1;
   }
+  if (lk1) m.w_n++;
   fq_push(c, v, e);
   return false;
 }
@@ -1278,6 +1322,8 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
     if (!present || st0 != SWIM_LEAVING) {
       schedule_timer(c, v, s);
       spread_gossip(c, v, s, SWIM_LEAVING, inc1, SWIM_ORIG_LEAVING);
+      // onLeavingDetected returns the gossip's spread() Mono: a merge waits until it disseminated
+      if (m.w_link1) m.w_gp = gsched(c, v).period + 1;
     }
     return false;
   }
@@ -1314,6 +1360,39 @@ __device__ inline bool update_membership(const Ctx& c, uint32_t v, uint32_t s, u
   }
   if (!present || inc0 < inc1) return fetch_start(c, v, s, inc1, reason, phase);
   return false;
+}
+
+// A merged message's waits (PAck): collected between wait_begin and wait_end by the one thread that
+// merges the message; wait_end makes a PAck when the message's Monos have not all completed by now
+// (returns true: its SYNC_ACK, or the start0 group, waits).  Oracle: wait_begin / wait_end.
+__device__ inline void wait_begin(const Ctx& c, uint32_t v) {
+  MemberDev& m = mem(c, v);
+  m.w_link1 = m.pack_seq + 1;
+  m.w_n = m.w_ready = m.w_gp = 0;
+}
+__device__ inline bool wait_end(const Ctx& c, uint32_t v, uint32_t to, uint32_t flags) {
+  MemberDev& m = mem(c, v);
+  m.w_link1 = 0;
+  if (m.w_n == 0 && m.w_gp == 0 && m.w_ready <= (uint32_t)c.T) return false;
+  const uint32_t i = v - c.lo, k = c.pa_n[i];
+  if (k >= PA_CAP) {
+    set_err(c, ERR_PACK);
+    return true;
+  }
+  c.pa[(size_t)i * PA_CAP + k] = PAck{to, flags, m.w_n, m.w_ready, m.w_gp, m.pack_seq};
+  c.pa_n[i] = k + 1;
+  m.pack_seq++;
+  if (flags & PA_INIT) m.init_pend++;
+  atomicOr(&c.mflag[i], MF_PACK);
+  return true;
+}
+// the PAck of viewer v with sequence number seq (nullptr: none — a start0 group cancelled with its Flux)
+__device__ inline PAck* pack_find(const Ctx& c, uint32_t v, uint32_t seq) {
+  const uint32_t i = v - c.lo, k = min(c.pa_n[i], PA_CAP);
+  PAck* L = c.pa + (size_t)i * PA_CAP;
+  for (uint32_t j = 0; j < k; ++j)
+    if (L[j].seq == seq) return L + j;
+  return nullptr;
 }
 
 // doOnSuccess of the metadata fetch (:648-656) + onAliveMemberDetected (:769-795); ver = the

@@ -321,6 +321,9 @@ __global__ void k_start_joins(KP) {
   m.joined = 1;
   m.join_now = 1;
   m.init_wait = 1;
+  m.init_pend = 0;
+  c.pa_n[i] = 0;
+  c.mflag[i] &= ~MF_PACK;
   m.init_last = (uint32_t)c.T;
   m.fd_start = (int64_t)c.T;
   m.g_start = (int64_t)c.T;
@@ -697,6 +700,7 @@ struct SenderPre {
   uint32_t rlen;       // remoteMembers.size()
   int32_t idx;         // remoteMembersIndex
   uint32_t fut;        // a graceful leave or an own user gossip is pending (futures to check)
+  uint32_t pw;         // the member holds PAcks (some may wait on its LEAVING gossips)
   uint32_t t[PRE_F];   // targets
   uint32_t tw[PRE_F];  // up | inbound-passes << 1 | v's outbound loss towards it << 2
   uint32_t clr[PRE_F]; // its collectors' last clear tick (owned), else ~0
@@ -709,6 +713,7 @@ __device__ __forceinline__ void sender_pre_load(const Ctx& c, uint32_t i, Sender
   sp.rlen = rlen;
   sp.idx = idx;
   sp.fut = (m.leave_pending || m.user_live) ? 1u : 0u;
+  sp.pw = (c.mflag[i] & MF_PACK) ? 1u : 0u;
   const uint32_t F = (uint32_t)c.fanout;
   if (F > PRE_F || c.route) return;
   if (rlen < F || idx < 0 || (uint32_t)idx + F > rlen) return;
@@ -734,6 +739,7 @@ __device__ __forceinline__ SenderPre sender_pre_from(const SenderPre& x, int j) 
   sp.rlen = rdlane(x.rlen, j);
   sp.idx = (int32_t)rdlane((uint32_t)x.idx, j);
   sp.fut = rdlane(x.fut, j);
+  sp.pw = rdlane(x.pw, j);
 #pragma unroll
   for (uint32_t q = 0; q < PRE_F; ++q) {
     sp.t[q] = rdlane(x.t[q], j);
@@ -1102,6 +1108,20 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
   }
   if (sinkw == 0x5bd1e995u && glen == 0x7fffffffu) set_err(c, 0u);  // keeps the warming loads; sets no bit
   PPROF_ACC(ep.t_pass, te1);
+  // PAck waits on this member's LEAVING gossips (onLeavingDetected's spread() Monos): the gossips of
+  // one wait share their infection period, so they complete together — in this round if it finds them
+  // disseminated and the sweep has not dropped them (a swept gossip's Mono never completes)
+  if (lane == 0 && sp.pw) {
+    const uint32_t i = v - c.lo, np = min(c.pa_n[i], PA_CAP);
+    PAck* L = c.pa + (size_t)i * PA_CAP;
+    for (uint32_t k = 0; k < np; ++k) {
+      const uint32_t gp = L[k].gp;
+      if (gp && period > (uint64_t)(gp - 1) + spread && !(period > (uint64_t)(gp - 1) + sweep)) {
+        L[k].gp = 0;
+        L[k].ready = max(L[k].ready, (uint32_t)c.T);
+      }
+    }
+  }
   const bool any_done = __ballot(done) != 0;
   if (lane == 0) {
     // the sweep dropped the prefix: the ring's base and the index's serial base advance past it
@@ -2241,8 +2261,13 @@ __device__ inline uint32_t select_sync_address(const Ctx& c, uint32_t v) {
 // RQ_PARKED: a delayed message (content in park slot .snap, sent in tick .pad); RQ_ACK: in the delay
 // queue, a SYNC_ACK (else a SYNC)
 // RQ_DEFER: a SYNC_ACK of this tick that k_ack_delay parked (its SYNC_ACK sub-phase skips it)
-enum : uint32_t { RQ_INITIAL = 1, RQ_OUTFAIL = 2, RQ_DELIVERED = 4, RQ_PARKED = 16, RQ_ACK = 32, RQ_DEFER = 64,
-                  RQ_RECS_SHIFT = 8 };
+// RQ_PHANTOM: a deferred SYNC_ACK whose waits completed (PAck): it takes the place of a SYNC in the
+// acker's inbox, merges nothing and gets its SYNC_ACK like every SYNC of the tick (.from = the ack's
+// receiver, .pad = the PAck's seq); with RQ_DEFER, in tx_reqs: a marker telling the shard of the
+// ack's receiver, before its SYNC merges, that an ack will come (SF_SENT | SF_MULTI)
+// RQ_WAIT: a SYNC whose Monos are still running (a PAck holds its SYNC_ACK)
+enum : uint32_t { RQ_INITIAL = 1, RQ_OUTFAIL = 2, RQ_DELIVERED = 4, RQ_PHANTOM = 8, RQ_PARKED = 16, RQ_ACK = 32,
+                  RQ_DEFER = 64, RQ_WAIT = 128, RQ_RECS_SHIFT = 8 };
 
 // per-member SYNC roles of the tick (Bufs.sflag)
 enum : uint32_t {
@@ -2532,16 +2557,65 @@ __device__ inline unsigned long long sync_collect_fast(const Ctx& c, const Bufs&
   return 1;
 }
 
+// PAcks whose Monos have all completed (collection of tick T, member v up): a deferred SYNC_ACK is
+// sent now (onSync's doOnSuccess, MembershipProtocolImpl.java:399-413) — a phantom SYNC at the front of
+// v's inbox, whose SYNC_ACK this sub-phase sends with v's table after its SYNC merges; a start0 group
+// leaves the count its doFinally waits for.  The ack's receiver is marked SF_SENT | SF_MULTI (merged
+// into in the SYNC_ACK sub-phase; no lone-SYNC_ACK shortcut for another ack it gets), on another
+// shard through an E2 marker.  Oracle: phase_sync's collection.
+__device__ inline void pack_inject(const Ctx& c, const Bufs& b, uint32_t v) {
+  const uint32_t i = v - c.lo, n = min(c.pa_n[i], PA_CAP), t32 = (uint32_t)c.T;
+  PAck* L = c.pa + (size_t)i * PA_CAP;
+  MemberDev& m = mem(c, v);
+  uint32_t w = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    const PAck a = L[k];
+    if (a.wn || a.gp || a.ready > t32) {
+      if (w != k) L[w] = a;
+      ++w;
+      continue;
+    }
+    if (a.flags & PA_INIT) {
+      m.init_pend--;
+      continue;
+    }
+    SyncReq q;
+    q.from = a.to; q.to = v; q.ordinal = 0; q.slot = 0;
+    q.flags = RQ_PHANTOM | RQ_DELIVERED | ((a.flags & PA_INITIAL_ACK) ? RQ_INITIAL : 0u);
+    q.content = NONE; q.snap = NONE; q.pad = a.seq;
+    if (owned(c, a.to)) {
+      sflag_set(c, b, a.to - c.lo, SF_SENT | SF_MULTI);
+    } else {
+      SyncReq mk = q;
+      mk.from = v; mk.to = a.to; mk.flags = RQ_PHANTOM | RQ_DEFER;
+      const uint32_t d = owner(c, a.to);
+      const uint32_t j = atomicAdd(&b.x->req[d], 1u);
+      if (j < b.tx_req_cap) b.tx_reqs[(size_t)d * b.tx_req_cap + j] = mk; else set_err(c, ERR_REQS);
+    }
+    enqueue_sync(c, b, 0, q, true);
+  }
+  c.pa_n[i] = w;
+  if (w == 0) c.mflag[i] &= ~MF_PACK;
+}
+
 __device__ inline unsigned long long sync_collect_pre(const Ctx& c, const Bufs& b, uint32_t v, uint32_t sn, uint32_t fl) {
   const uint32_t i = v - c.lo, t32 = (uint32_t)c.T;
   const bool due = sn == t32;  // the periodic doSync timer fires (sync_on, phase sync_start)
-  if (!due && !(fl & (MF_FDSYNC | MF_JOIN))) return 0;
-  if (due && !(fl & (MF_FDSYNC | MF_JOIN)) && !c.n_links && !c.partition && !c.route && !c.delay_on)
+  if (!due && !(fl & (MF_FDSYNC | MF_JOIN | MF_PACK))) return 0;
+  if (due && !(fl & (MF_FDSYNC | MF_JOIN | MF_PACK)) && !c.n_links && !c.partition && !c.route && !c.delay_on)
     return sync_collect_fast(c, b, v);
   if (due) c.sync_next[i] = t32 + c.S;
   if (fl & MF_FDSYNC) c.mflag[i] = fl & ~MF_FDSYNC;
   MemberDev& m = mem(c, v);
-  if (!c.up[v]) { m.fd_sync_cnt = 0; return 0; }
+  if (!c.up[v]) {
+    m.fd_sync_cnt = 0;
+    if (fl & MF_PACK) {  // a stopped member's waits and deferred acks are void
+      c.pa_n[i] = 0;
+      m.init_pend = 0;
+      c.mflag[i] &= ~MF_PACK;
+    }
+    return 0;
+  }
   uint32_t k = 0;
   unsigned long long nsync = 0;
   if (due) {
@@ -2562,6 +2636,7 @@ __device__ inline unsigned long long sync_collect_pre(const Ctx& c, const Bufs& 
     }
   }
   if (k > 1) sflag_set(c, b, i, SF_MULTI);  // (k_sync_apply's lone-SYNC_ACK shortcut needs k = 1)
+  if (fl & MF_PACK) pack_inject(c, b, v);
   return nsync;
 }
 __device__ inline unsigned long long sync_collect_member(const Ctx& c, const Bufs& b, uint32_t v) {
@@ -2683,7 +2758,16 @@ __global__ void __launch_bounds__(256) k_fetch_due(KP) {
           continue;
         }
         const int r = (e.info >> 8) == 1u ? fetch_stage1(c, v, e) : (in_pass(c, v, e.d) ? 1 : 0);
-        if (r == 2) fq_push(c, v, e);
+        if (r == 2) {
+          fq_push(c, v, e);
+          continue;
+        }
+        if (e.link != NONE) {  // the Mono waiting on it ends now (a response) or at the timeout
+          PAck* pa = pack_find(c, v, e.link);
+          if (!pa) continue;  // cancelled with start0's Flux: its doOnSuccess never runs
+          pa->wn--;
+          pa->ready = max(pa->ready, r == 1 ? (uint32_t)T : e.t0 + mt_ticks(c));
+        }
         if (r == 1) {
           stat_add(c, ST_FETCH_OK, 1);
           apply_alive(c, v, e.s, e.inc, (int)((e.info >> 4) & 15u), SWIM_PHASE_FETCH, e.ver);
@@ -2780,21 +2864,35 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
     for (uint32_t q = i; q < ns; q += gridDim.x * blockDim.x) c.up[P->b.rx_stops[q]] = 0;
   }
   if (i >= c.nl) return;
-  const uint32_t fl = c.mflag[i];
+  uint32_t fl = c.mflag[i];
   if (!(fl & (MF_JOIN | MF_LEAVE))) return;
   const uint32_t v = c.lo + i;
   MemberDev& m = c.mem[i];
   uint32_t keep = 0;
-  // start0's doFinally (:285-289): periodic sync starts once every initial SYNC was answered or
-  // failed fast, else syncTimeout after the last answer (Flux.timeout :281).  Without message delay
-  // every source resolves within the start tick; with delay the decision may wait (MF_JOIN is kept)
-  // until the last answer or the timeout, which fires at tick init_last + syncTimeout.
+  // start0's doFinally (:285-289).  Every initial SYNC answered or failed fast: Flux.take completes,
+  // and doFinally runs once the flatMap's inner Monos (the initial merges' fetches and LEAVING
+  // spreads: PAck groups PA_INIT) have completed — periodic sync starts at the tick the last ended.
+  // Else Flux.timeout (:281, restarted at every answer) fires at tick init_last + syncTimeout, cancels
+  // the inner Monos still running (their fetches complete into nothing) and doFinally runs then.
+  // MF_JOIN is kept while undecided.  Oracle: finish_joins.
   if (m.init_wait) {
     const uint64_t last = m.init_last;
     int64_t start = -1;
-    if (!c.delay_on) start = (int64_t)c.T + (m.init_done == m.init_total ? 0 : (int64_t)c.sync_to_ticks);
-    else if (m.init_done == m.init_total) start = (int64_t)c.T;  // the last source completed now
-    else if (c.T + 1 >= last + c.sync_to_ticks) start = (int64_t)(last + c.sync_to_ticks);
+    if (m.init_done == m.init_total) {
+      if (m.init_pend == 0) start = (int64_t)c.T;
+    } else if (c.T + 1 >= last + c.sync_to_ticks) {
+      start = (int64_t)(last + c.sync_to_ticks);
+      if (m.init_pend) {  // the start0 groups are cancelled
+        PAck* L = c.pa + (size_t)i * PA_CAP;
+        const uint32_t n = min(c.pa_n[i], PA_CAP);
+        uint32_t w = 0;
+        for (uint32_t k = 0; k < n; ++k)
+          if (!(L[k].flags & PA_INIT)) L[w++] = L[k];
+        c.pa_n[i] = w;
+        m.init_pend = 0;
+        if (w == 0) fl &= ~MF_PACK;
+      }
+    }
     if (start >= 0) {
       m.sync_on = 1;
       m.sync_start = start;

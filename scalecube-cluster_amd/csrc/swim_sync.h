@@ -122,6 +122,9 @@ __global__ void k_recv_sync(KP, int d2) {
     if (valid) {
       const uint32_t p = peer_of(s_n, k);
       q = ld_peer(b.peers->hdr[d2][p] + (size_t)c.rank * b.tx_req_cap + k);
+      // a marker (pack_inject): a deferred SYNC_ACK for q.to leaves this tick — merged into in the
+      // SYNC_ACK sub-phase, no lone-SYNC_ACK shortcut for another ack it gets
+      if (!d2 && (q.flags & RQ_PHANTOM)) sflag_set(c, b, q.to - c.lo, SF_SENT | SF_MULTI);
       valid = q.content != NONE;  // its row did not fit the sender's tx_rows (ERR_REQS is set there), or deferred
       q.content = p * b.row_cap + q.content;
       // a delayed SYNC_ACK's receiver is merged into in this SYNC_ACK sub-phase (see k_sync_delay)
@@ -189,6 +192,7 @@ struct ClsHdr {
   uint32_t i, r, s;
   uint32_t rev;  // d2 = 0: 1 = also classify the reverse direction (a local SYNC)
   uint32_t pad;  // d2 = 1: 1 + the SYNC whose reverse classification this ack may reuse, or 0
+  uint32_t ph;   // a phantom (deferred SYNC_ACK): nothing to classify
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -201,6 +205,8 @@ __device__ __forceinline__ void cls_hdr(const Ctx& c, const Bufs& b, const SyInb
   q.from = uni(q.from); q.to = uni(q.to); q.content = uni(q.content); q.pad = uni(q.pad);
   const bool remote = q.content != NONE;
   const bool parked = !remote && (q.flags & RQ_PARKED);  // (uniform: the header is)
+  h.ph = !d2 && !remote && (q.flags & RQ_PHANTOM) ? 1u : 0u;
+  if (h.ph) q.from = q.to;  // (its sender may live on another shard: no pointer into its row)
   h.content = remote ? remote_row(c, b, d2, q.content) : parked ? park_row(c, b, q.snap) : rec_row(c, q.from);
   h.rv = rec_row(c, q.to);
   h.bdc = remote || parked ? nullptr : c.bdiff + (size_t)(q.from - c.lo) * c.blocks;
@@ -313,6 +319,10 @@ __device__ __forceinline__ void classify_body(const Params* __restrict__ P, uint
       if (i != hc.i) cls_hdr(c, b, p, d2, i, hc);
       const uint32_t ch = u - i * chunks;
       const uint32_t base = ch * SYNC_CHUNK;
+      if (hc.ph) {  // a phantom merges nothing (k_sync_apply skips it)
+        if (lane == 0) ichunk[(size_t)hc.i * chunks + ch] = make_uint2(0, 0);
+        continue;
+      }
       // one batch of loads that depend only on the header: the receiver's snapshot slot (a SYNC
       // receiver that also sent a SYNC this tick, sflag_set: this launch copies its row, streamed
       // here before any merge, into the slot; the SYNC_ACK launch needs none), the SYNC_ACK reuse
@@ -694,10 +704,12 @@ __device__ void sync_msg_wg(const Ctx& c, const Bufs& b, uint32_t r, uint32_t it
   __syncthreads();
 }
 
-// canonical inbox order: messages sent in earlier ticks (delayed) first, then (sender, ordinal / rank)
+// canonical inbox order: deferred SYNC_ACKs (phantoms) first in their PAcks' creation order, then
+// messages sent in earlier ticks (delayed), then (sender, ordinal / rank)
 __device__ __forceinline__ uint64_t inbox_key(const Ctx& c, const SyncReq& q) {
+  if (q.flags & RQ_PHANTOM) return q.pad;
   const uint32_t age = (q.flags & RQ_PARKED) ? min((uint32_t)c.T - q.pad, 2047u) : 0u;
-  return ((uint64_t)(2047u - age) << 53) | ((uint64_t)q.from << 24) | (q.ordinal & 0xffffffu);
+  return (1ull << 63) | ((uint64_t)(2047u - age) << 52) | ((uint64_t)q.from << 24) | (q.ordinal & 0xffffffu);
 }
 
 // the receiver's inbox in canonical order (sending tick, sender, ordinal) -> s_it (item indices); its page table
@@ -909,9 +921,14 @@ __device__ __forceinline__ void sync_apply_body(const Params* __restrict__ P, ui
       if (it >= b.req_cap) continue;  // a page the pool could not give (ERR_REQS is set); uniform
       const SyncReq rq = x.items[it];
       if (d2 && ((rq.flags & RQ_DEFER) || ((rq.flags & RQ_INITIAL) && !iwait))) continue;  // (uniform)
+      if (!d2 && (rq.flags & RQ_PHANTOM)) continue;  // a deferred SYNC_ACK: nothing to merge (uniform)
       const bool parked = (rq.flags & RQ_PARKED) != 0;
       const uint32_t tot_q = fused ? 0u : itot[it];  // issued with the header (stable since classify)
       const int reason = (d2 && (rq.flags & RQ_INITIAL)) ? R_INITIAL_SYNC : R_SYNC;
+      // onSync's SYNC_ACK and start0's doFinally wait for the message's Monos (PAck): their waits are
+      // collected while thread 0 merges it
+      const bool waits = !d2 || reason == R_INITIAL_SYNC;
+      if (waits && threadIdx.x == 0) wait_begin(c, s);
       uint32_t npend = 0;
       const uint32_t mod = s_mod;
       const bool own = d2 && !classified;  // this kernel classifies the ack
@@ -964,6 +981,12 @@ __device__ __forceinline__ void sync_apply_body(const Params* __restrict__ P, ui
         for (uint32_t j = 0; j < npend; ++j)
           apply_alive(c, s, (uint32_t)(pend[j] >> 32), (int32_t)(uint32_t)pend[j], reason, phase);
         s_recs += rq.flags >> RQ_RECS_SHIFT;
+        if (!d2) {
+          if (wait_end(c, s, rq.from, (rq.flags & RQ_INITIAL) ? PA_INITIAL_ACK : 0u))
+            x.items[it].flags = rq.flags | RQ_WAIT;  // its SYNC_ACK waits
+        } else if (waits) {
+          wait_end(c, s, NONE, PA_INIT);
+        }
       }
       __syncthreads();
     }
@@ -978,18 +1001,21 @@ __device__ __forceinline__ void sync_apply_body(const Params* __restrict__ P, ui
         if (q < k && s_it[q] < b.req_cap) {
           const uint32_t it = s_it[q];
           const SyncReq rq = x.items[it];
+          const bool ph = (rq.flags & RQ_PHANTOM) != 0;
           const bool first = pre && q0 == 0;  // (pre_*: this message's words, loaded before the merges)
           const uint32_t t3 = (uint32_t)c.T << SF_BITS;
           const bool sf_now = first && (pre_sf & ~SF_MASK) == t3;
           // with message delay only the loss is decided now: the receiver's state and inbound filter
           // meet the ack when it arrives (k_ack_delay for an undelayed one, k_sync_delay else)
-          if (c.delay_on ? !lost_k(c, out_loss(c, s, rq.from), s, SWIM_STREAM_SYNCACK_OUT, q, 0)
+          // (a message whose Monos are still running sends its SYNC_ACK later, as a phantom)
+          if (rq.flags & RQ_WAIT) {
+          } else if (c.delay_on ? !lost_k(c, out_loss(c, s, rq.from), s, SWIM_STREAM_SYNCACK_OUT, q, 0)
               : first ? pre_up && !lost_k(c, pre_loss, s, SWIM_STREAM_SYNCACK_OUT, q, 0) && pre_in
                     : !out_fail(c, s, rq.from, s, SWIM_STREAM_SYNCACK_OUT, q, 0) && in_pass(c, rq.from, s)) {
             a.from = s; a.to = rq.from; a.ordinal = q; a.slot = 0;
             a.flags = RQ_DELIVERED | (rq.flags & RQ_INITIAL) | (tsz << RQ_RECS_SHIFT);
             a.content = NONE; a.snap = NONE;
-            a.pad = CLS_REV && rq.content == NONE && !(rq.flags & RQ_PARKED) ? it + 1 : 0;
+            a.pad = CLS_REV && !ph && rq.content == NONE && !(rq.flags & RQ_PARKED) ? it + 1 : 0;
             valid = true;
             // the lone SYNC_ACK shortcut: the ack is the only one its receiver gets this tick (it sent
             // one SYNC and received none, so its row is unchanged since classify), this row did not
@@ -997,7 +1023,7 @@ __device__ __forceinline__ void sync_apply_body(const Params* __restrict__ P, ui
             // that could change the receiver: its merge is a no-op, so the SYNC_ACK sub-phase's
             // bookkeeping for it (onSyncAck :385-391: the phase's minor / fetch counters restart, an
             // INITIAL ack completes a join step, the counters) is done here and nothing is enqueued
-            if (valid && CLS_REV && !c.delay_on && rq.content == NONE && s_mod == 0 &&
+            if (valid && CLS_REV && !c.delay_on && !ph && rq.content == NONE && s_mod == 0 &&
                 (first ? owned(c, rq.from) && !(sf_now && (pre_sf & SF_RECV)) &&
                              !(sf_now && (pre_sf & SF_MULTI))
                        : owned(c, rq.from) && !sflag_has(c, b, rq.from - c.lo, SF_RECV) &&

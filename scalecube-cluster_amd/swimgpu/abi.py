@@ -128,7 +128,7 @@ class swim_member_state(C.Structure):
         ("relay_pending", C.c_uint32),
         ("relay_due", C.c_uint64),
         ("leave_gossiper", C.c_uint32),
-        ("pad2", C.c_uint32),
+        ("pending_acks", C.c_uint32),
         ("leave_seq", C.c_uint64),
     ]
 

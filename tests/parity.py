@@ -8,7 +8,7 @@ from swimgpu import abi
 MEMBER_FIELDS = ("up", "joined", "leave_pending", "join_pending", "remote_idx", "fd_period", "ping_cursor",
                  "ping_len", "remote_len", "gossip_len", "gossip_period", "gossip_counter", "table_size",
                  "members_size", "fd_start", "gossip_start", "sync_start", "sync_on", "ack_target", "ack_due",
-                 "relay_target", "relay_pending", "relay_due", "leave_gossiper", "leave_seq")
+                 "relay_target", "relay_pending", "relay_due", "leave_gossiper", "leave_seq", "pending_acks")
 
 STAT_FIELDS = ("pings", "ping_reqs", "fd_events", "gossips_created", "gossip_messages", "gossip_accepted",
                "syncs", "sync_acks", "sync_records", "fetches", "fetch_ok", "timers_fired", "events") + tuple(

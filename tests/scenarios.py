@@ -262,6 +262,21 @@ def catalog() -> list[Scenario]:
                                                                      False),
                       (200, "ingest", 8, [(5, abi.LEAVING, 0), (14, abi.SUSPECT, 3)], False)],
                  check_every=20),
+        # onSync's SYNC_ACK waits for the SYNC's updateMembership Monos (MembershipProtocolImpl.java
+        # :394-415, :491-509): admissions whose metadata fetch is lost (10 % loss: the request fails at
+        # once, a lost response waits out metadataTimeout), refused (member 1 drops everything from seed
+        # 0) or answered late; a LEAVING record learned by SYNC (member 7 was deaf while 5 left) waits
+        # for the re-gossip to spread; joiners' start0 Flux (:250-291) waits for its initial merges'
+        # fetches, or times out with fetches in flight (seed 3 slow: a 1.5 s link)
+        Scenario("sync_ack_waits_24", 24, 16, 500, seed=30, seeds=(0, 3),
+                 cfg=dict(sync_interval=1000, sync_timeout=1000, ping_interval=600, ping_timeout=300,
+                          metadata_timeout=400, record_fd_events=1, delay_capacity=16384),
+                 ops=[(0, "loss", 10, ALL_), (2, "link_in", 1, 0, 0), (5, "join", 16), (5, "join", 17),
+                      (9, "join", 18), (20, "default_in", 0, 7), (30, "leave", 5, 1), (45, "default_in", 1, 7),
+                      (60, "join", 19), (100, "kill", 11), (150, "join", 20), (150, "join", 21),
+                      (200, "link_delay", 3, 22, 1500), (200, "link_delay", 22, 3, 1500), (201, "join", 22),
+                      (230, "default_delay", 150, 8), (231, "join", 23), (300, "link_in", 1, 0, -1)],
+                 check_every=20),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),
                  cfg=dict(sync_interval=5000), ops=[(100, "partition", _partition(32, 16)), (1100, "partition", None)],
