@@ -203,7 +203,16 @@ int32_t swim_step(swim_engine* e, uint32_t periods);
 int32_t swim_now(const swim_engine* e, uint64_t* tick, uint32_t* tick_ms, uint32_t* ticks_per_period);
 
 /* ---- seeds (MembershipConfig.seedMembers, MembershipProtocolImpl.java:143,461-472) ------ */
+/* The seed list of every member that has no list of its own (duplicates dropped in order, as
+ * cleanUpSeedMembers' LinkedHashSet does, :171-190). */
 int32_t swim_set_seeds(swim_engine* e, const uint32_t* seeds, uint32_t n_seeds);
+/* Member m's own MembershipConfig.seedMembers (each member's ClusterConfig, MembershipProtocolImpl
+ * constructor :120-130 -> cleanUpSeedMembers :171-190; SimulatedCluster maps one config per member):
+ * duplicates dropped in order; from the next step on, m's start0 sends its initial SYNCs to these
+ * (:250-291) and its selectSyncAddress draws from them U otherMembers (:461-472) instead of the
+ * engine-wide list.  n_seeds = 0 gives m an empty list; seeds = NULL with n_seeds = UINT32_MAX puts m
+ * back on the engine-wide list.  Replicated: every rank of a sharded engine makes the same call. */
+int32_t swim_set_member_seeds(swim_engine* e, uint32_t m, const uint32_t* seeds, uint32_t n_seeds);
 
 /* ---- lifecycle --------------------------------------------------------------------------- */
 /* Stop member m's transport abruptly (TransportImpl.stop): sends to it fail at the sender. */

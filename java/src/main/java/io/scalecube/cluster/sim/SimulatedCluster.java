@@ -188,6 +188,23 @@ public final class SimulatedCluster implements AutoCloseable {
   /** ClusterImpl.start of a fresh member in free slot s: initial SYNC to every seed next tick. */
   public void start(int s) { run(() -> call(SwimNative.JOIN, "swim_join", engine, s)); }
 
+  /**
+   * ClusterImpl.start of a fresh member in free slot s with its own ClusterConfig: its
+   * membershipConfig().seedMembers() become s's seed list (MembershipProtocolImpl :120-130,
+   * cleanUpSeedMembers :171-190) — start0's initial SYNCs and selectSyncAddress use them.
+   */
+  public void start(int s, ClusterConfig config) {
+    run(() -> {
+      int[] slots = config.membershipConfig().seedMembers().stream().mapToInt(ad -> ad.port() - BASE_PORT).toArray();
+      try (Arena a = Arena.ofConfined()) {
+        MemorySegment sv = a.allocate(JAVA_INT, Math.max(1, slots.length));
+        for (int i = 0; i < slots.length; i++) sv.setAtIndex(JAVA_INT, i, slots[i]);
+        call(SwimNative.SET_MEMBER_SEEDS, "swim_set_member_seeds", engine, s, sv, slots.length);
+      }
+      call(SwimNative.JOIN, "swim_join", engine, s);
+    });
+  }
+
   /** A restart on the same port: s binds the address of stopped member `old` (DEST_GONE for `old`). */
   public void startOnAddressOf(int s, int old) {
     run(() -> call(SwimNative.JOIN_AT, "swim_join_at", engine, s, old));

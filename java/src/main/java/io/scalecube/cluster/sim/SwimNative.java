@@ -121,6 +121,7 @@ public final class SwimNative {
   static final MethodHandle STEP_TICKS = h("swim_step_ticks", JAVA_INT, ADDRESS, JAVA_INT);
   static final MethodHandle NOW = h("swim_now", JAVA_INT, ADDRESS, ADDRESS, ADDRESS, ADDRESS);
   static final MethodHandle SET_SEEDS = h("swim_set_seeds", JAVA_INT, ADDRESS, ADDRESS, JAVA_INT);
+  static final MethodHandle SET_MEMBER_SEEDS = h("swim_set_member_seeds", JAVA_INT, ADDRESS, JAVA_INT, ADDRESS, JAVA_INT);
   static final MethodHandle KILL = h("swim_kill", JAVA_INT, ADDRESS, JAVA_INT);
   static final MethodHandle LEAVE = h("swim_leave", JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT);
   static final MethodHandle JOIN = h("swim_join", JAVA_INT, ADDRESS, JAVA_INT);

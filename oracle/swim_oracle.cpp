@@ -223,6 +223,9 @@ struct Member {
   // being merged (w_link = the seq its PendingAck will take, NONE outside such a merge)
   std::vector<PendingAck> pack;
   uint32_t pack_seq = 0, init_pend = 0;
+  // this member's own MembershipConfig.seedMembers (swim_set_member_seeds), else the engine-wide list
+  bool own_seeds = false;
+  std::vector<uint32_t> seeds;
   uint32_t w_link = NONE, w_n = 0;
   uint64_t w_ready = 0, w_gp = 0;
 };
@@ -1085,16 +1088,24 @@ struct swim_engine {
   }
 
   // ------------------------------------------------------------------------- phase D: SYNC
+  // member v's MembershipConfig.seedMembers (:120-130, cleanUpSeedMembers :171-190): its own list
+  // (swim_set_member_seeds) or the engine-wide one
+  const std::vector<uint32_t>& seeds_of(uint32_t v) const { return m[v].own_seeds ? m[v].seeds : seeds; }
+  bool is_seed_of(uint32_t v, uint32_t x) const {
+    if (!m[v].own_seeds) return is_seed[x] != 0;
+    return std::find(m[v].seeds.begin(), m[v].seeds.end(), x) != m[v].seeds.end();
+  }
+
   // selectSyncAddress (:461-472): uniform over seeds U otherMembers, by seeded rejection sampling.
   uint32_t select_sync_address(uint32_t v) {
     const Member& mv = m[v];
     // seed addresses exclude the local one (cleanUpSeedMembers :171-190)
     uint32_t count = mv.members_size - 1;
-    for (uint32_t s : seeds)
+    for (uint32_t s : seeds_of(v))
       if (s != v && dst(s) != v && !c_has(mv.row[s], B_IN_MEMBERS)) count++;
     if (count == 0) return NONE;
     auto in_set = [&](uint32_t x) {
-      return x != v && (c_has(mv.row[x], B_IN_MEMBERS) || (is_seed[x] && dst(x) != v));
+      return x != v && (c_has(mv.row[x], B_IN_MEMBERS) || (is_seed_of(v, x) && dst(x) != v));
     };
     for (uint32_t i = 0; i < SWIM_SYNC_SELECT_ATTEMPTS; ++i) {
       uint32_t x = next_int(draw(v, SWIM_STREAM_SYNC_SELECT, 0, i), n);
@@ -1186,7 +1197,7 @@ struct swim_engine {
         for (uint32_t tg : mv.fd_sync) rq[t].push_back(SyncReq{v, dst(tg), k++, false, false, false, false});
         mv.fd_sync.clear();
         if (mv.join_now) {  // start0 initial sync to every seed (:250-291) but its own address
-          for (uint32_t s : seeds)
+          for (uint32_t s : seeds_of(v))
             if (s != v && dst(s) != v) rq[t].push_back(SyncReq{v, dst(s), k++, true, false, false, false});
         }
       }
@@ -1703,6 +1714,25 @@ int32_t swim_now(const swim_engine* e, uint64_t* tick, uint32_t* tick_ms, uint32
   if (tick) *tick = e->T;
   if (tick_ms) *tick_ms = e->tick_ms;
   if (tpp) *tpp = e->P;
+  return SWIM_OK;
+}
+
+int32_t swim_set_member_seeds(swim_engine* e, uint32_t v, const uint32_t* seeds, uint32_t n_seeds) {
+  if (!e || v >= e->n) return SWIM_EINVAL;
+  Member& mv = e->m[v];
+  if (!seeds && n_seeds == 0xffffffffu) {  // back on the engine-wide list
+    mv.own_seeds = false;
+    mv.seeds.clear();
+    return SWIM_OK;
+  }
+  if (n_seeds && !seeds) return SWIM_EINVAL;
+  std::vector<uint32_t> s;
+  for (uint32_t i = 0; i < n_seeds; ++i) {
+    if (seeds[i] >= e->n) return SWIM_EINVAL;
+    if (std::find(s.begin(), s.end(), seeds[i]) == s.end()) s.push_back(seeds[i]);  // LinkedHashSet
+  }
+  mv.seeds = std::move(s);
+  mv.own_seeds = true;
   return SWIM_OK;
 }
 

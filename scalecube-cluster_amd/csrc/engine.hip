@@ -132,6 +132,7 @@ struct Shard {
   Peers* peers = nullptr;
   std::vector<void*> ipc_open;  // peers' regions mapped here (RCCL)
   uint32_t links_dev_cap = 0;
+  size_t mseed_cap = 0;  // capacity of c.mseed (swim_set_member_seeds)
   uint64_t* delay_buf = nullptr;  // the delay threshold tables (Ctx.delay_th)
   size_t delay_cap = 0;           // words allocated
   // device-resident launch parameters (swim_phases.h Params) and the last uploaded image
@@ -192,6 +193,11 @@ struct swim_engine {
   std::vector<uint8_t> g_residue;  // gossip timer residues mod G in use
   uint32_t drain_every = kDrainFirst, since_drain = 0;  // event drain interval (ticks), adaptive
   std::vector<uint32_t> seeds;
+  // per-member seedMembers (swim_set_member_seeds): own list of each member (mseed_own_h), uploaded
+  // as CSR to every shard before the next step when changed
+  std::vector<std::vector<uint32_t>> mseeds_h;
+  std::vector<uint8_t> mseed_own_h;
+  bool mseed_dirty = false;
   std::vector<uint8_t> is_seed_h, joined_h, join_pending_h;
   std::vector<LinkDev> links_h;
   std::vector<int32_t> delay_means;  // NetworkEmulator meanDelay (ms) of each delay table, in table order
@@ -1398,10 +1404,13 @@ int32_t swim_destroy(swim_engine* e) {
   return SWIM_OK;
 }
 
+static int32_t upload_member_seeds(swim_engine* e);
 int32_t swim_step_ticks(swim_engine* e, uint32_t ticks) {
   if (!e) return SWIM_EINVAL;
   if (hipSetDevice(e->device) != hipSuccess) return SWIM_EDEVICE;
   bool fresh = false;  // the last work on the stream was a quiet window (status words written, drained)
+  if (e->mseed_dirty)
+    if (int32_t rc = upload_member_seeds(e)) return rc;
   for (uint32_t i = 0; i < ticks; ++i) {
     if (quiet_eligible(e) && e->T + 1 >= e->quiet_retry_at) {
       const uint32_t K = std::min(ticks - i, kQuietMax);
@@ -1471,6 +1480,63 @@ int32_t swim_set_seeds(swim_engine* e, const uint32_t* seeds, uint32_t n_seeds) 
       return SWIM_EDEVICE;
     if (hipMemcpy(sd.c.is_seed, e->is_seed_h.data(), e->n, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
     sd.c.n_seeds = (uint32_t)s.size();
+  }
+  return SWIM_OK;
+}
+
+int32_t swim_set_member_seeds(swim_engine* e, uint32_t m, const uint32_t* seeds, uint32_t n_seeds) {
+  if (!e || m >= e->n) return SWIM_EINVAL;
+  if (e->mseed_own_h.empty()) {
+    e->mseed_own_h.assign(e->n, 0);
+    e->mseeds_h.assign(e->n, {});
+  }
+  if (!seeds && n_seeds == 0xffffffffu) {  // back on the engine-wide list
+    e->mseed_own_h[m] = 0;
+    e->mseeds_h[m].clear();
+    e->mseed_dirty = true;
+    return SWIM_OK;
+  }
+  if (n_seeds && !seeds) return SWIM_EINVAL;
+  std::vector<uint32_t> s;
+  for (uint32_t i = 0; i < n_seeds; ++i) {
+    if (seeds[i] >= e->n) return SWIM_EINVAL;
+    if (std::find(s.begin(), s.end(), seeds[i]) == s.end()) s.push_back(seeds[i]);  // LinkedHashSet
+  }
+  e->mseeds_h[m] = std::move(s);
+  e->mseed_own_h[m] = 1;
+  e->mseed_dirty = true;
+  return SWIM_OK;
+}
+
+// the per-member seed lists as CSR (own flags, offsets, members) on every shard (replicated)
+static int32_t upload_member_seeds(swim_engine* e) {
+  e->mseed_dirty = false;
+  const uint32_t n = e->n;
+  std::vector<uint32_t> off(n + 1, 0), all;
+  for (uint32_t v = 0; v < n; ++v) {
+    off[v] = (uint32_t)all.size();
+    all.insert(all.end(), e->mseeds_h[v].begin(), e->mseeds_h[v].end());
+  }
+  off[n] = (uint32_t)all.size();
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+  for (Shard& sd : e->sh) {
+    uint8_t* own = const_cast<uint8_t*>(sd.c.mseed_own);
+    uint32_t* o = const_cast<uint32_t*>(sd.c.mseed_off);
+    uint32_t* l = const_cast<uint32_t*>(sd.c.mseed);
+    if (!own && (!sd.alloc(&own, n) || !sd.alloc(&o, n + 1))) return SWIM_ENOMEM;
+    if (all.size() > sd.mseed_cap) {
+      sd.release(l);
+      l = nullptr;
+      sd.mseed_cap = std::max<size_t>(all.size(), 2 * sd.mseed_cap);
+      if (!sd.alloc(&l, sd.mseed_cap)) return SWIM_ENOMEM;
+    }
+    if (hipMemcpy(own, e->mseed_own_h.data(), n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(o, off.data(), 4ull * (n + 1), hipMemcpyHostToDevice) != hipSuccess ||
+        (!all.empty() && hipMemcpy(l, all.data(), 4ull * all.size(), hipMemcpyHostToDevice) != hipSuccess))
+      return SWIM_EDEVICE;
+    sd.c.mseed_own = own;
+    sd.c.mseed_off = o;
+    sd.c.mseed = l;
   }
   return SWIM_OK;
 }

@@ -105,19 +105,22 @@ struct alignas(16) GossipSched {
 };
 
 struct alignas(16) MemberDev {
-  // first 40 B: every word the quiet scan reads (k_quiet_scan, one 64-B sector per member)
+  // first 64 B: every word the quiet scan reads and the quiet apply writes (k_quiet_scan /
+  // k_quiet_apply: one 64-B sector per member)
   uint64_t ack_due, relay_due;
   uint32_t ping_cursor, ping_len, table_size, fd_sync_cnt;
   uint32_t ins_rank;  // this phase's deferred pingMembers inserts (op chain: ins_head / ins_tail)
   uint8_t join_now, join_pending, leave_pending;
   uint8_t init_wait;  // start0's initial-sync Flux is still subscribed (init_total / init_done)
-  uint64_t fd_period, g_counter, leave_seq;
+  uint64_t fd_period;
+  uint32_t ev_minor, fetch_ctr;
+  uint64_t g_counter, leave_seq;
   int64_t fd_start, g_start, sync_start;
   uint32_t ack_target, relay_target, relay_pending;
   uint32_t remote_len;
   int32_t remote_idx;
   uint32_t members_size, leave_gossiper;
-  uint32_t ev_minor, fetch_ctr, init_total, init_done;
+  uint32_t init_total, init_done;
   uint32_t ins_head, ins_tail;
   uint32_t gix_base, gix_used;  // serial of slab[0]; gix slots taken since the index was (re)built
   uint32_t ack_late;  // 1 + ticks after the ping timeout that a late direct ack arrives (0 = none)
@@ -466,6 +469,11 @@ struct Ctx {
   uint8_t* is_seed;
   uint32_t* seeds;
   uint32_t n_seeds;
+  // per-member seedMembers (swim_set_member_seeds), replicated: member v with mseed_own[v] uses
+  // mseed[mseed_off[v] .. mseed_off[v + 1]) instead of the engine-wide list; nullptr: nobody does
+  const uint8_t* mseed_own;
+  const uint32_t* mseed_off;
+  const uint32_t* mseed;
   // deferred list ops: a viewer's ops of one phase are applied by whoever delivered to it, right
   // after its deliveries / merges (k_gossip_deliver, k_sync_apply)
   InsOp* ins;              // overflow chain storage, shared by the viewers of the phase

@@ -2231,25 +2231,44 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect, u
 
 
 // ------------------------------------------------------------------------------- phase D
+// member v's MembershipConfig.seedMembers (MembershipProtocolImpl.java:120-130, cleanUpSeedMembers
+// :171-190): its own list (swim_set_member_seeds) or the engine-wide one (swim_set_seeds)
+__device__ __forceinline__ bool own_seeds(const Ctx& c, uint32_t v) { return c.mseed_own && c.mseed_own[v]; }
+__device__ __forceinline__ const uint32_t* seeds_of(const Ctx& c, uint32_t v, uint32_t& ns) {
+  if (!own_seeds(c, v)) {
+    ns = c.n_seeds;
+    return c.seeds;
+  }
+  ns = c.mseed_off[v + 1] - c.mseed_off[v];
+  return c.mseed + c.mseed_off[v];
+}
+__device__ inline bool is_seed_of(const Ctx& c, uint32_t v, uint32_t x) {
+  if (!own_seeds(c, v)) return c.is_seed[x] != 0;
+  for (uint32_t k = c.mseed_off[v]; k < c.mseed_off[v + 1]; ++k)
+    if (c.mseed[k] == x) return true;
+  return false;
+}
+
 // selectSyncAddress (MembershipProtocolImpl.java:461-472): uniform over seeds U otherMembers by
 // seeded rejection sampling.
 __device__ inline uint32_t select_sync_address(const Ctx& c, uint32_t v) {
   const MemberDev& m = mem(c, v);
   const uint32_t* a = aux_row(c, v);
   // seed addresses exclude the local one (cleanUpSeedMembers :171-190)
-  uint32_t count = m.members_size - 1;
-  for (uint32_t i = 0; i < c.n_seeds; ++i) {
-    uint32_t s = c.seeds[i];
+  uint32_t count = m.members_size - 1, ns = 0;
+  const uint32_t* sl = seeds_of(c, v, ns);
+  for (uint32_t i = 0; i < ns; ++i) {
+    uint32_t s = sl[i];
     if (s != v && dst(c, s) != v && !(a[s] & A_IN_MEMBERS)) count++;
   }
   if (count == 0) return NONE;
   for (uint32_t i = 0; i < SWIM_SYNC_SELECT_ATTEMPTS; ++i) {
     uint32_t x = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 0, i), c.n);
-    if (x != v && ((a[x] & A_IN_MEMBERS) || (c.is_seed[x] && dst(c, x) != v))) return x;
+    if (x != v && ((a[x] & A_IN_MEMBERS) || (is_seed_of(c, v, x) && dst(c, x) != v))) return x;
   }
   uint32_t k = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 1, 0), count);
   for (uint32_t x = 0; x < c.n; ++x)
-    if (x != v && ((a[x] & A_IN_MEMBERS) || (c.is_seed[x] && dst(c, x) != v))) {
+    if (x != v && ((a[x] & A_IN_MEMBERS) || (is_seed_of(c, v, x) && dst(c, x) != v))) {
       if (k == 0) return x;
       --k;
     }
@@ -2602,7 +2621,8 @@ __device__ inline unsigned long long sync_collect_pre(const Ctx& c, const Bufs& 
   const uint32_t i = v - c.lo, t32 = (uint32_t)c.T;
   const bool due = sn == t32;  // the periodic doSync timer fires (sync_on, phase sync_start)
   if (!due && !(fl & (MF_FDSYNC | MF_JOIN | MF_PACK))) return 0;
-  if (due && !(fl & (MF_FDSYNC | MF_JOIN | MF_PACK)) && !c.n_links && !c.partition && !c.route && !c.delay_on)
+  if (due && !(fl & (MF_FDSYNC | MF_JOIN | MF_PACK)) && !c.n_links && !c.partition && !c.route && !c.delay_on &&
+      !own_seeds(c, v))
     return sync_collect_fast(c, b, v);
   if (due) c.sync_next[i] = t32 + c.S;
   if (fl & MF_FDSYNC) c.mflag[i] = fl & ~MF_FDSYNC;
@@ -2630,8 +2650,10 @@ __device__ inline unsigned long long sync_collect_pre(const Ctx& c, const Bufs& 
   if (m.join_now) {
     m.init_total = 0;
     m.init_done = 0;
-    for (uint32_t i = 0; i < c.n_seeds; ++i) {
-      uint32_t s = c.seeds[i];
+    uint32_t ns = 0;
+    const uint32_t* sl = seeds_of(c, v, ns);
+    for (uint32_t i = 0; i < ns; ++i) {
+      uint32_t s = sl[i];
       if (s != v && dst(c, s) != v) { add_req(c, b, v, dst(c, s), k++, true); nsync++; }
     }
   }

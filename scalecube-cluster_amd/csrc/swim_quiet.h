@@ -152,7 +152,7 @@ __device__ inline void quiet_sync(const Ctx& c0, uint32_t v, uint64_t t, uint32_
   c.T = t;
   const uint32_t x0 = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 0, 0), c.n);
   uint32_t tg = x0;
-  if (!(x0 != v && ((aux_row(c, v)[x0] & A_IN_MEMBERS) || c.is_seed[x0]))) {
+  if (!(x0 != v && ((aux_row(c, v)[x0] & A_IN_MEMBERS) || is_seed_of(c, v, x0)))) {
     tg = select_sync_address(c, v);
     if (tg == NONE) return;
   }

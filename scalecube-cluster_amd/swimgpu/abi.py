@@ -190,6 +190,7 @@ PROTOTYPES = {
     "swim_step": (C.c_int32, [_engp, C.c_uint32]),
     "swim_now": (C.c_int32, [_engp, _u64p, _u32p, _u32p]),
     "swim_set_seeds": (C.c_int32, [_engp, _u32p, C.c_uint32]),
+    "swim_set_member_seeds": (C.c_int32, [_engp, C.c_uint32, _u32p, C.c_uint32]),
     "swim_kill": (C.c_int32, [_engp, C.c_uint32]),
     "swim_leave": (C.c_int32, [_engp, C.c_uint32, C.c_int32]),
     "swim_spread": (C.c_int32, [_engp, C.c_uint32, C.c_uint32]),
@@ -326,6 +327,15 @@ class Engine:
     def set_seeds(self, seeds) -> None:
         arr = (C.c_uint32 * len(seeds))(*seeds)
         _check("swim_set_seeds", self.lib.swim_set_seeds(self._h, arr, len(seeds)))
+
+    def set_member_seeds(self, m: int, seeds) -> None:
+        """swim_set_member_seeds: member m's own seedMembers (None: back on the engine-wide list)."""
+        if seeds is None:
+            rc = self.lib.swim_set_member_seeds(self._h, m, None, 0xffffffff)
+        else:
+            arr = (C.c_uint32 * max(1, len(seeds)))(*seeds)
+            rc = self.lib.swim_set_member_seeds(self._h, m, arr, len(seeds))
+        _check("swim_set_member_seeds", rc)
 
     def kill(self, m: int) -> None:
         _check("swim_kill", self.lib.swim_kill(self._h, m))

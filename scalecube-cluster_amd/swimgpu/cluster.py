@@ -546,13 +546,22 @@ class SimulatedCluster:
         """MembershipProtocolImpl.leaveCluster (:233-242) without stopping the member."""
         self.engine.leave(m, False)
 
-    def join(self, m: int, same_address_as: int = None):
+    def join(self, m: int, same_address_as: int = None, config: "ClusterConfig | None" = None):
         """Start member m; with same_address_as, on that stopped member's address (a restart on the
-        same port, MembershipProtocolTest.testRestartStoppedMembersOnSameAddresses :654-711)."""
+        same port, MembershipProtocolTest.testRestartStoppedMembersOnSameAddresses :654-711); with
+        config, member m's own ClusterConfig: its membershipConfig().seedMembers() become m's seed
+        list (MembershipProtocolImpl :120-130, cleanUpSeedMembers :171-190)."""
+        if config is not None:
+            self.set_member_config(m, config)
         if same_address_as is None:
             self.engine.join(m)
         else:
             self.engine.join_at(m, same_address_as)
+
+    def set_member_config(self, m: int, config: "ClusterConfig"):
+        """Member m's own ClusterConfig, as far as the protocol layer reads it per member: its seed
+        members (start0's initial SYNCs, selectSyncAddress); the timing knobs are engine-wide."""
+        self.engine.set_member_seeds(m, _flatten(config.membership_config.seed_members))
 
     # -- views
     def membership(self, m: int) -> MembershipView:

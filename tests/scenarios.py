@@ -52,6 +52,8 @@ def apply_op(e: abi.Engine, op, args):
         gid = {x: i for i, x in enumerate(names)}
         rel = np.array([[namespaces_related(x, y) for y in names] for x in names], dtype=np.uint8)
         e.set_namespaces(np.array([gid[x] for x in args[0]], dtype=np.uint16), rel)
+    elif op == "member_seeds":  # (m, [seeds] or None): member m's own seedMembers
+        e.set_member_seeds(args[0], None if args[1] is None else list(args[1]))
     elif op == "default_delay":
         e.set_default_delay(*args)
     elif op == "link_delay":
@@ -276,6 +278,23 @@ def catalog() -> list[Scenario]:
                       (60, "join", 19), (100, "kill", 11), (150, "join", 20), (150, "join", 21),
                       (200, "link_delay", 3, 22, 1500), (200, "link_delay", 22, 3, 1500), (201, "join", 22),
                       (230, "default_delay", 150, 8), (231, "join", 23), (300, "link_in", 1, 0, -1)],
+                 check_every=20),
+        # per-member seedMembers (each member's own ClusterConfig; MembershipProtocolTest
+        # .testLimitedSeedMembers :713-743 in a bigger cluster): joiners seeded by different members,
+        # one by a chain (17 -> 16 -> 8), one with its own address among its seeds (dropped,
+        # cleanUpSeedMembers :171-190), one with a dead seed, one with no seeds (alone until someone
+        # SYNCs to it), one put back on the engine-wide list; 5 % loss
+        Scenario("member_seeds_20", 20, 6, 400, seed=31, seeds=(0,),
+                 cfg=dict(sync_interval=1000, sync_timeout=500, ping_interval=600, ping_timeout=300,
+                          metadata_timeout=500, record_fd_events=1),
+                 ops=[(0, "loss", 5, ALL_), (0, "member_seeds", 3, [5, 4]), (2, "member_seeds", 6, [1]),
+                      (2, "member_seeds", 7, [2, 1, 2]), (2, "member_seeds", 8, [6]), (3, "join", 6), (3, "join", 7),
+                      (6, "join", 8), (10, "kill", 4), (11, "member_seeds", 9, [4, 5]), (11, "join", 9),
+                      (20, "member_seeds", 10, [10, 3]), (20, "join", 10), (30, "member_seeds", 11, []),
+                      (30, "join", 11), (40, "member_seeds", 12, [11]), (40, "join", 12),
+                      (60, "member_seeds", 16, [8]), (60, "join", 16), (70, "member_seeds", 17, [16]),
+                      (70, "join", 17), (90, "member_seeds", 13, [2]), (91, "member_seeds", 13, None),
+                      (91, "join", 13), (120, "member_seeds", 1, [17]), (200, "join", 14)],
                  check_every=20),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),

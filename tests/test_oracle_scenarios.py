@@ -446,6 +446,39 @@ def test_isolated_parent_namespaces():  # :199-250
     assert (others(c, 3), others(c, 4), others(c, 5)) == ([4, 5], [3, 5], [3, 4])
 
 
+# ---- per-member seed lists (MembershipProtocolTest.createMembership(transport, testConfig(seeds)),
+# :1123-1177: every member its own ClusterConfig; start().block() — members start one after another)
+def _start_seeded(n, seeds_of, before_start=None):
+    lib = oracle.lib()
+    base = mp_config(n).membership(seed_members=())
+    e = abi.Engine(lib, base.to_abi(lib, record_fd_events=1), n, 1, 1)
+    c = SimulatedCluster.from_engine(e, base)
+    c.set_member_config(0, mp_config(n).membership(seed_members=tuple(seeds_of[0])))
+    if before_start:
+        before_start(c)
+    for m in range(1, n):
+        c.join(m, config=mp_config(n).membership(seed_members=tuple(seeds_of[m])))
+        c.step_ticks(3)  # start().block(): the initial SYNCs answered or timed out (syncTimeout 100 ms)
+    return c
+
+
+def test_mp_limited_seed_members():  # testLimitedSeedMembers (:713-743)
+    # A: no seeds; B, C: seed A; D, E: seed B
+    c = _start_seeded(5, [[], [0], [0], [1], [1]])
+    c.await_seconds(3)
+    for m in range(5):
+        assert trusted(c, m) == [0, 1, 2, 3, 4] and suspected(c, m) == []
+
+
+def test_mp_node_join_cluster_with_no_inbound():  # testNodeJoinClusterWithNoInbound (:788-813)
+    # C blocks all inbound before it starts: A admits nobody whose metadata it cannot fetch (its
+    # SYNC_ACK to C waits for that fetch, then C drops it), so C stays alone and A / B never add it
+    c = _start_seeded(3, [[], [0], [0]], before_start=lambda c: c.network_emulator(2).block_all_inbound())
+    c.await_seconds(3)
+    assert trusted(c, 0) == [0, 1] and trusted(c, 1) == [0, 1]
+    assert trusted(c, 2) == [2] and suspected(c, 2) == []
+
+
 # ------------------------------------------------------------------------------ ClusterTest
 def test_update_metadata():  # testUpdateMetadata (:179-247): every member sees the new metadata
     n = 12
