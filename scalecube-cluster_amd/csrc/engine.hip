@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -129,6 +130,7 @@ struct Shard {
   void* xreg = nullptr;
   size_t xreg_bytes = 0;
   void* rx_rows_h[2] = {nullptr, nullptr};  // the pulled-row copies Peers points at (RCCL / pull rig)
+  uint32_t rx_row_cap = 0;                    // the row_cap they were sized for
   Peers* peers = nullptr;
   std::vector<void*> ipc_open;  // peers' regions mapped here (RCCL)
   uint32_t links_dev_cap = 0;
@@ -218,7 +220,14 @@ struct swim_engine {
   uint32_t q_par = 0;            // the block the next window uses
   uint32_t* h_stat = nullptr;    // pinned host words: each local shard's event counts and error bits
   uint32_t* d_stat = nullptr;    //   ([SUBQ + 1] per shard, written by k_status), and their device address
-  uint32_t* h_done = nullptr;    // pinned host word: the last window's length (written by k_quiet_apply)
+  uint32_t* h_done = nullptr;    // pinned host words: the last window's length (written by k_quiet_apply),
+                                 //   [1] k_status's sequence number (the window's wait, wait_status_seq)
+  uint32_t status_seq = 0;
+  // no member has ever stopped (kill, graceful leave) or been given an inbound filter, and no
+  // external record was ingested: every member a ping list can hold is up and lets pings in, so a
+  // quiet window's pings need no target check (k_quiet_scan `pingable`)
+  bool pristine = true;
+  bool spin_wait = true;         // SWIM_SPIN=0: the window waits with hipStreamSynchronize
   uint32_t* d_done = nullptr;    // its device address
   uint32_t* d_refmm = nullptr;   // RCCL: [2][n] elementwise min / max of the ranks' witness refs
   uint64_t quiet_retry_at = 0;
@@ -354,15 +363,39 @@ static void launch_deliver(swim_engine* e, Shard& s) {
 
 // each shard's event counts and error bits into the pinned host words (one launch instead of two
 // blocking copies per shard: the drain that ends every swim_step call, quiet windows included)
-__global__ void k_status(const uint32_t* ev_cnt, const uint32_t* err, uint32_t* out) {
+// (seq_out, seq: the last shard's launch also publishes a sequence number after its words: a host
+// that sees it knows every earlier kernel of the stream has completed — the quiet window's wait)
+__global__ void k_status(const uint32_t* ev_cnt, const uint32_t* err, uint32_t* out, uint32_t* seq_out, uint32_t seq) {
   const uint32_t t = threadIdx.x;
   if (t < SUBQ) out[t] = ev_cnt[t];
   if (t == SUBQ) out[SUBQ] = *err;
+  if (seq_out) {
+    __syncthreads();
+    if (t == 0) {
+      __threadfence_system();
+      __hip_atomic_store(seq_out, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
-static void launch_status(swim_engine* e) {
+static void launch_status(swim_engine* e, uint32_t seq = 0) {
   for (size_t i = 0; i < e->sh.size(); ++i)
-    k_status<<<1, 64, 0, e->stream>>>(e->sh[i].c.ev_cnt, e->sh[i].c.err, e->d_stat + i * (SUBQ + 1));
+    k_status<<<1, 64, 0, e->stream>>>(e->sh[i].c.ev_cnt, e->sh[i].c.err, e->d_stat + i * (SUBQ + 1),
+                                      seq && i + 1 == e->sh.size() ? e->d_done + 1 : nullptr, seq);
+}
+// the quiet window's wait: spin on the pinned sequence word k_status publishes (no runtime
+// synchronisation: the sleep / wake-up of hipStreamSynchronize is most of a short window's host
+// time); a stream error ends the spin (hipStreamQuery every 1,024 polls)
+static int32_t wait_status_seq(swim_engine* e, uint32_t seq) {
+  for (uint32_t it = 1;; ++it) {
+    if (__atomic_load_n(e->h_done + 1, __ATOMIC_ACQUIRE) == seq) return SWIM_OK;
+    if ((it & 1023u) == 0) {
+      const hipError_t q = hipStreamQuery(e->stream);
+      if (q == hipSuccess) return __atomic_load_n(e->h_done + 1, __ATOMIC_ACQUIRE) == seq ? SWIM_OK : SWIM_EDEVICE;
+      if (q != hipErrorNotReady) return SWIM_EDEVICE;
+    }
+    __builtin_ia32_pause();
+  }
 }
 // fresh: the status words were written by the last work on the stream and the stream has drained
 // (a quiet window launches k_status before its own synchronisation): no launch, no second wait
@@ -522,6 +555,18 @@ static int32_t apply_binds(swim_engine* e) {
 static int32_t alloc_xreg(swim_engine* e, Shard& sd, bool uncached);
 static int32_t setup_peers_local(swim_engine* e);
 static int32_t setup_peers_rccl(swim_engine* e);
+// the minimum of x over the RCCL ranks (x itself on a local group)
+static int32_t rank_min(swim_engine* e, uint32_t& x) {
+  if (!e->rccl) return SWIM_OK;
+  if (hipMemcpy(e->d_cnt, &x, 4, hipMemcpyHostToDevice) != hipSuccess ||
+      nccl_ok(ncclAllReduce(e->d_cnt, e->d_cnt + 1, 1, ncclUint32, ncclMin, e->comm, e->stream)) != SWIM_OK ||
+      hipStreamSynchronize(e->stream) != hipSuccess || hipMemcpy(&x, e->d_cnt + 1, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return SWIM_EDEVICE;
+  return SWIM_OK;
+}
+static size_t xreg_bytes_for(const swim_engine* e, const Bufs& b, uint32_t row_cap);
+static void* xreg_alloc(size_t bytes, bool uncached);
+static void xreg_install(swim_engine* e, Shard& sd, void* fresh, uint32_t row_cap);
 static int32_t grow_rows_for_joins(swim_engine* e) {
   if (e->world <= 1 || e->joins.empty() || e->sh.empty()) return SWIM_OK;
   const uint32_t W = (uint32_t)e->world;
@@ -538,7 +583,43 @@ static int32_t grow_rows_for_joins(swim_engine* e) {
   cap = std::min<uint64_t>(cap, std::max<uint64_t>(cur, (4ull << 30) / (4ull * e->n)));
   if (cap <= cur) return SWIM_OK;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
-  if (e->rccl) {  // every rank unmaps the others' regions before any region is freed
+  // what the grown rows cost, beside the regions in use (they are released only once every rank has
+  // its new ones): both tx row regions and, where rows are pulled, the per-peer copies
+  const bool pulled = e->rccl || e->pull_rows;
+  const auto bytes_for = [&](uint64_t k) {
+    uint64_t b = 0;
+    for (const Shard& sd : e->sh) b += xreg_bytes_for(e, sd.b, (uint32_t)k) + (pulled ? 2ull * W * k * e->n * 4 : 0);
+    return b;
+  };
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return SWIM_EDEVICE;
+  while (cap > cur && bytes_for(cap) > fr - fr / 8) cap /= 2;
+  // every rank agrees on the size before anything changes (the inputs above differ by rank)
+  uint32_t c32 = (uint32_t)cap;
+  if (int32_t rc = rank_min(e, c32)) return rc;
+  cap = c32;
+  if (cap <= cur) return SWIM_OK;  // no room: the rows stay (a tick that overflows them reports ERR_REQS)
+  // 1. the new regions and pulled copies, the old ones still in place
+  std::vector<void*> fresh(e->sh.size(), nullptr);
+  std::vector<std::array<uint32_t*, 2>> rx(e->sh.size(), {nullptr, nullptr});
+  uint32_t ok = 1;
+  for (size_t i = 0; i < e->sh.size() && ok; ++i) {
+    fresh[i] = xreg_alloc(xreg_bytes_for(e, e->sh[i].b, (uint32_t)cap), e->rccl);
+    ok = fresh[i] != nullptr;
+    for (int k = 0; k < 2 && ok && pulled; ++k)
+      ok = dalloc(&rx[i][k], (size_t)W * cap * e->n) == hipSuccess;
+  }
+  if (int32_t rc = rank_min(e, ok)) return rc;
+  if (!ok) {  // some rank could not: every rank keeps its region and row_cap
+    for (size_t i = 0; i < e->sh.size(); ++i) {
+      if (fresh[i]) hipFree(fresh[i]);
+      for (uint32_t* q : rx[i])
+        if (q) hipFree(q);
+    }
+    return SWIM_OK;
+  }
+  // 2. every rank unmaps the others' regions before any region is freed
+  if (e->rccl) {
     Shard& sd = e->sh[0];
     for (void* q : sd.ipc_open) hipIpcCloseMemHandle(q);
     sd.ipc_open.clear();
@@ -546,9 +627,17 @@ static int32_t grow_rows_for_joins(swim_engine* e) {
         hipStreamSynchronize(e->stream) != hipSuccess)
       return SWIM_EDEVICE;
   }
-  for (Shard& sd : e->sh) {
-    sd.b.row_cap = (uint32_t)cap;
-    if (int32_t rc = alloc_xreg(e, sd, e->rccl)) return rc;
+  // 3. the switch: headers carried over, old regions and copies released
+  for (size_t i = 0; i < e->sh.size(); ++i) {
+    Shard& sd = e->sh[i];
+    xreg_install(e, sd, fresh[i], (uint32_t)cap);
+    if (pulled)
+      for (int k = 0; k < 2; ++k) {
+        sd.release(sd.rx_rows_h[k]);
+        sd.allocs.push_back(rx[i][k]);
+        sd.rx_rows_h[k] = rx[i][k];
+      }
+    sd.rx_row_cap = (uint32_t)cap;
   }
   e->row_grows++;
   return e->rccl ? setup_peers_rccl(e) : setup_peers_local(e);
@@ -720,7 +809,7 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
     const uint32_t g = std::max<uint32_t>(64, grid_for(sd.c.nl, 256));
     const uint32_t* ra = e->rccl ? e->d_refmm : e->world > 1 ? e->sh[0].c.ref : nullptr;
     const uint32_t* rb = e->rccl ? e->d_refmm + e->n : sd.c.ref;
-    k_quiet_scan<<<g, 256, 0, s>>>(sd.d_par, T0, K, q, ra, rb);
+    k_quiet_scan<<<g, 256, 0, s>>>(sd.d_par, T0, K, q, ra, rb, e->pristine ? 1u : 0u);
   }
   // RCCL: the window is the minimum over the ranks (fail tick, min table size, 0xffffffff - max)
   if (e->rccl && nccl_ok(ncclAllReduce(q, q, 3, ncclUint32, ncclMin, e->comm, s)) != SWIM_OK)
@@ -730,8 +819,15 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
     k_quiet_apply<<<g, 256, 0, s>>>(sd.d_par, T0, K, q, q_next, e->d_done, (uint32_t)kRebaseEvery);
   }
   if (prof) hipEventRecord(e->qev[1], s);
-  launch_status(e);  // (the drain after a window that ends the swim_step call needs no wait of its own)
-  if (hipStreamSynchronize(s) != hipSuccess) return SWIM_EDEVICE;
+  // (the drain after a window that ends the swim_step call needs no wait of its own)
+  if (e->spin_wait) {
+    const uint32_t seq = ++e->status_seq;
+    launch_status(e, seq);
+    if (wait_status_seq(e, seq) != SWIM_OK) return SWIM_EDEVICE;
+  } else {
+    launch_status(e);
+    if (hipStreamSynchronize(s) != hipSuccess) return SWIM_EDEVICE;
+  }
   e->par_slot = 0;  // (the stream drained: the Params staging ring restarts)
   *done = std::min(__atomic_load_n(e->h_done, __ATOMIC_ACQUIRE), K);
   if (prof) {
@@ -885,36 +981,59 @@ __global__ void k_spread(Ctx c, uint32_t v, uint32_t payload) {
 // The producer side of a shard's exchange, one region (one IPC handle): tx_msgs, tx_reqs, tx_acks,
 // tx_stops, tx_rows[2], at offsets that are the same on every rank.  With RCCL it is uncached, so the
 // producers' stores land in HBM, where the peers' system-scope loads over xGMI read them.
-static int32_t alloc_xreg(swim_engine* e, Shard& sd, bool uncached) {
-  Bufs& b = sd.b;
-  const size_t W = (size_t)e->world, rows = (size_t)b.row_cap * e->n * 4;
+struct XLayout {
+  size_t o_msgs, o_reqs, o_acks, o_stops, o_rows0, o_rows1, bytes;
+};
+static XLayout xlayout(const swim_engine* e, const Bufs& b, uint32_t row_cap) {
+  const size_t W = (size_t)e->world, rows = (size_t)row_cap * e->n * 4;
+  XLayout L{};
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-  const size_t o_msgs = take(W * b.tx_msg_cap * sizeof(GMsgFull)), o_reqs = take(W * b.tx_req_cap * sizeof(SyncReq)),
-               o_acks = take(W * b.tx_req_cap * sizeof(SyncReq)), o_stops = take(4ull * b.tx_stop_cap),
-               o_rows0 = take(rows), o_rows1 = take(rows);
-  // a re-allocation (row_cap grew) keeps everything before the rows — message and SYNC headers,
-  // stops, deferred acks — at the same offsets
-  void* old = sd.xreg;
-  const size_t keep = old ? std::min(o_rows0, sd.xreg_bytes) : 0;
-  sd.xreg = nullptr;
-  sd.xreg_bytes = off;
+  L.o_msgs = take(W * b.tx_msg_cap * sizeof(GMsgFull));
+  L.o_reqs = take(W * b.tx_req_cap * sizeof(SyncReq));
+  L.o_acks = take(W * b.tx_req_cap * sizeof(SyncReq));
+  L.o_stops = take(4ull * b.tx_stop_cap);
+  L.o_rows0 = take(rows);
+  L.o_rows1 = take(rows);
+  L.bytes = off;
+  return L;
+}
+static size_t xreg_bytes_for(const swim_engine* e, const Bufs& b, uint32_t row_cap) { return xlayout(e, b, row_cap).bytes; }
+static void* xreg_alloc(size_t bytes, bool uncached) {
+  void* p = nullptr;
   hipError_t r = hipErrorUnknown;
-  if (uncached) r = hipExtMallocWithFlags(&sd.xreg, off, hipDeviceMallocUncached);
-  if (r != hipSuccess) r = hipMalloc(&sd.xreg, off);
-  if (r != hipSuccess) return SWIM_ENOMEM;
+  if (uncached) r = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
+  if (r != hipSuccess) r = hipMalloc(&p, bytes);
+  return r == hipSuccess ? p : nullptr;
+}
+// the shard's exchange region becomes `fresh` (sized for row_cap): everything before the rows —
+// message and SYNC headers, stops, deferred acks — keeps its offset and is carried over; the old
+// region is freed
+static void xreg_install(swim_engine* e, Shard& sd, void* fresh, uint32_t row_cap) {
+  Bufs& b = sd.b;
+  const XLayout L = xlayout(e, b, row_cap);
+  void* old = sd.xreg;
   if (old) {
-    const bool ok = !keep || hipMemcpy(sd.xreg, old, keep, hipMemcpyDeviceToDevice) == hipSuccess;
+    const size_t keep = std::min(L.o_rows0, sd.xreg_bytes);
+    if (keep) hipMemcpy(fresh, old, keep, hipMemcpyDeviceToDevice);
     hipFree(old);
-    if (!ok) return SWIM_EDEVICE;
   }
-  char* base = static_cast<char*>(sd.xreg);
-  b.tx_msgs = reinterpret_cast<GMsgFull*>(base + o_msgs);
-  b.tx_reqs = reinterpret_cast<SyncReq*>(base + o_reqs);
-  b.tx_acks = reinterpret_cast<SyncReq*>(base + o_acks);
-  b.tx_stops = reinterpret_cast<uint32_t*>(base + o_stops);
-  b.tx_rows[0] = reinterpret_cast<uint32_t*>(base + o_rows0);
-  b.tx_rows[1] = reinterpret_cast<uint32_t*>(base + o_rows1);
+  sd.xreg = fresh;
+  sd.xreg_bytes = L.bytes;
+  b.row_cap = row_cap;
+  char* base = static_cast<char*>(fresh);
+  b.tx_msgs = reinterpret_cast<GMsgFull*>(base + L.o_msgs);
+  b.tx_reqs = reinterpret_cast<SyncReq*>(base + L.o_reqs);
+  b.tx_acks = reinterpret_cast<SyncReq*>(base + L.o_acks);
+  b.tx_stops = reinterpret_cast<uint32_t*>(base + L.o_stops);
+  b.tx_rows[0] = reinterpret_cast<uint32_t*>(base + L.o_rows0);
+  b.tx_rows[1] = reinterpret_cast<uint32_t*>(base + L.o_rows1);
+}
+// (re)allocates the shard's exchange region for its row_cap; on failure the old region stays
+static int32_t alloc_xreg(swim_engine* e, Shard& sd, bool uncached) {
+  void* fresh = xreg_alloc(xreg_bytes_for(e, sd.b, sd.b.row_cap), uncached);
+  if (!fresh) return SWIM_ENOMEM;
+  xreg_install(e, sd, fresh, sd.b.row_cap);
   return SWIM_OK;
 }
 
@@ -1152,11 +1271,18 @@ static size_t xoff(const Shard& sd, const void* p) {
 static int32_t setup_peers_local(swim_engine* e) {
   for (Shard& sd : e->sh) {
     Peers ph{};
+    const bool stale = sd.rx_row_cap != sd.b.row_cap;  // (both copies are sized together)
     if (e->pull_rows)
       for (int k = 0; k < 2; ++k) {
-        sd.release(sd.rx_rows_h[k]);
-        if (!sd.alloc(&ph.rx_rows[k], (size_t)e->world * sd.b.row_cap * e->n)) return SWIM_ENOMEM;
-        sd.rx_rows_h[k] = ph.rx_rows[k];
+        if (!sd.rx_rows_h[k] || stale) {
+          sd.release(sd.rx_rows_h[k]);
+          sd.rx_rows_h[k] = nullptr;
+          uint32_t* q = nullptr;
+          if (!sd.alloc(&q, (size_t)e->world * sd.b.row_cap * e->n)) return SWIM_ENOMEM;
+          sd.rx_rows_h[k] = q;
+          sd.rx_row_cap = sd.b.row_cap;
+        }
+        ph.rx_rows[k] = static_cast<uint32_t*>(sd.rx_rows_h[k]);
       }
     for (uint32_t p = 0; p < (uint32_t)e->world; ++p) {
       const Bufs& pb = e->sh[p].b;
@@ -1200,10 +1326,17 @@ static int32_t setup_peers_rccl(swim_engine* e) {
   hipFree(d_h);
   if (rc) return rc;
   Peers ph{};
-  for (int k = 0; k < 2; ++k) {
-    sd.release(sd.rx_rows_h[k]);
-    if (!sd.alloc(&ph.rx_rows[k], (size_t)W * sd.b.row_cap * e->n)) return SWIM_ENOMEM;
-    sd.rx_rows_h[k] = ph.rx_rows[k];
+  const bool stale = sd.rx_row_cap != sd.b.row_cap;  // (both copies are sized together)
+  for (int k = 0; k < 2; ++k) {  // (grow_rows_for_joins allocates them before the switch)
+    if (!sd.rx_rows_h[k] || stale) {
+      sd.release(sd.rx_rows_h[k]);
+      sd.rx_rows_h[k] = nullptr;
+      uint32_t* q = nullptr;
+      if (!sd.alloc(&q, (size_t)W * sd.b.row_cap * e->n)) return SWIM_ENOMEM;
+      sd.rx_rows_h[k] = q;
+      sd.rx_row_cap = sd.b.row_cap;
+    }
+    ph.rx_rows[k] = static_cast<uint32_t*>(sd.rx_rows_h[k]);
   }
   for (uint32_t p = 0; p < W; ++p) {
     char* base = static_cast<char*>(sd.xreg);
@@ -1287,9 +1420,12 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
     delete e;
     return SWIM_ENOMEM;
   }
+  std::memset(e->h_done, 0, 64);  // (status_seq starts at 0: no stale sequence number)
   {
     const char* q = std::getenv("SWIM_QUIET");
     e->quiet_on = !(q && q[0] == '0');
+    const char* sp = std::getenv("SWIM_SPIN");
+    e->spin_wait = !(sp && sp[0] == '0');
   }
   e->loss_h.assign(capacity, 0);
   if (world > 1) {
@@ -1543,6 +1679,7 @@ static int32_t upload_member_seeds(swim_engine* e) {
 
 int32_t swim_kill(swim_engine* e, uint32_t m) {
   if (!e || m >= e->n) return SWIM_EINVAL;
+  e->pristine = false;
   uint8_t up = 0;
   if (read_up(e, m, &up) != SWIM_OK) return SWIM_EDEVICE;
   if (!up) return SWIM_ESTATE;
@@ -1558,6 +1695,7 @@ int32_t swim_kill(swim_engine* e, uint32_t m) {
 
 int32_t swim_leave(swim_engine* e, uint32_t m, int32_t stop_after) {
   if (!e || m >= e->n) return SWIM_EINVAL;
+  e->pristine = false;
   uint8_t up = 0;
   if (read_up(e, m, &up) != SWIM_OK) return SWIM_EDEVICE;
   if (!up) return SWIM_ESTATE;
@@ -1631,6 +1769,7 @@ int32_t swim_spread(swim_engine* e, uint32_t m, uint32_t payload) {
 
 int32_t swim_ingest_sync(swim_engine* e, uint32_t v, const swim_record* records, uint32_t n, int32_t initial) {
   if (!e || v >= e->n || n > e->n || (n && !records)) return SWIM_EINVAL;
+  e->pristine = false;
   for (uint32_t i = 0; i < n; ++i)
     if (records[i].member >= e->n || records[i].status >= SWIM_DEAD || records[i].inc < 0) return SWIM_EINVAL;
   uint8_t up = 0;
@@ -1672,6 +1811,7 @@ int32_t swim_join(swim_engine* e, uint32_t m) {
 
 int32_t swim_join_at(swim_engine* e, uint32_t m, uint32_t addr_of) {
   if (!e || m >= e->n || addr_of >= e->n || addr_of == m) return SWIM_EINVAL;
+  e->pristine = false;
   const uint32_t holder = e->route_of(addr_of);
   uint8_t up = 0;
   if (read_up(e, holder, &up) != SWIM_OK) return SWIM_EDEVICE;
@@ -1822,6 +1962,7 @@ int32_t swim_set_link_delay(swim_engine* e, uint32_t src, uint32_t dst, int32_t 
 
 int32_t swim_set_link_inbound(swim_engine* e, uint32_t dst, uint32_t src, int32_t pass) {
   if (!e || src >= e->n || dst >= e->n) return SWIM_EINVAL;
+  e->pristine = false;
   if (pass < 0) {
     LinkDev* L = find_link_h(e, dst, src, false);
     if (L) L->in_pass = -1;
@@ -1835,6 +1976,7 @@ int32_t swim_set_link_inbound(swim_engine* e, uint32_t dst, uint32_t src, int32_
 
 int32_t swim_set_default_inbound(swim_engine* e, uint32_t m, int32_t pass) {
   if (!e) return SWIM_EINVAL;
+  e->pristine = false;
   if (m != 0xffffffffu && m >= e->n) return SWIM_EINVAL;
   return set_replicated(e, offsetof(Ctx, default_inbound), m, pass ? 1 : 0, m == 0xffffffffu);
 }

@@ -1572,7 +1572,7 @@ __device__ __forceinline__ void ins_bar() {
 // cooperate (a workgroup, WG = true, or one wave); every thread of the group calls it.  sP / sS / sR:
 // NT words of LDS each.
 template <int NT, bool WG>
-__device__ void apply_ins_batch(const Ctx& c, uint32_t v, uint32_t tid, uint32_t* sP, uint32_t* sS, uint32_t* sR) {
+__device__ __forceinline__ void apply_ins_batch(const Ctx& c, uint32_t v, uint32_t tid, uint32_t* sP, uint32_t* sS, uint32_t* sR) {
   MemberDev& m = mem(c, v);
   const uint32_t k = m.ins_rank;
   if (k == 0) return;

@@ -41,12 +41,13 @@ struct QuietCtl {
 // the tick offset at which member v (up, owned) leaves the quiet regime within [T0, T0 + K), or K.
 // Its pings of the window go to the next entries of its ping list (no reshuffle before the list's
 // end); they are checked eight at a time: the list words in one batch of loads, then the targets'
-// up / inbound words in another.
+// up / inbound words in another.  (cur, len, fdn, inbound: the member's words, loaded by the caller
+// in its first batch)
 constexpr uint32_t QUIET_BATCH = 8;
-__device__ inline uint32_t quiet_member_scan(const Ctx& c, uint32_t v, uint64_t T0, uint32_t K, const MemberDev& m,
-                                             uint32_t fdn, const uint32_t* fail) {
+__device__ inline uint32_t quiet_member_scan(const Ctx& c, uint32_t v, uint64_t T0, uint32_t K, uint32_t cur,
+                                             uint32_t len, uint32_t fdn, bool inbound, const uint32_t* fail,
+                                             bool pingable) {
   const uint64_t Tend = T0 + K;
-  const uint32_t len = m.ping_len, cur = m.ping_cursor;
   if ((uint64_t)fdn >= Tend || fdn == NONE || len == 0) return K;  // no doPing, or period++ only
   const uint32_t np = (uint32_t)((Tend - 1 - fdn) / c.P) + 1;     // doPing calls in the window
   // the ping after the list's last entry reshuffles it (Collections.shuffle): the per-tick path
@@ -55,12 +56,15 @@ __device__ inline uint32_t quiet_member_scan(const Ctx& c, uint32_t v, uint64_t 
     limit = cur < len ? len - cur : 0u;
     end_off = (uint32_t)(fdn + (uint64_t)limit * c.P - T0);
   }
+  // pingable: no member ever stopped or filtered its inbound traffic, so every target is up and
+  // both inbound filters pass (only the reshuffle can end the window)
+  if (pingable) return end_off;
   // the ping and its ack (tryFailOutbound on a stopped destination, both inbound filters); with no
   // loss and no delay this is the whole round trip
-  if (limit && !c.default_inbound[v]) return (uint32_t)(fdn - T0);
+  if (limit && !inbound) return (uint32_t)(fdn - T0);
   const uint32_t* pl = ping_list(c, v) + cur;
   for (uint32_t k0 = 0; k0 < limit; k0 += QUIET_BATCH) {
-    if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= (uint32_t)(fdn + (uint64_t)k0 * c.P - T0))
+    if (k0 && __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= (uint32_t)(fdn + (uint64_t)k0 * c.P - T0))
       return K;  // an earlier tick already ends the window
     uint32_t tg[QUIET_BATCH];
 #pragma unroll
@@ -80,60 +84,99 @@ __device__ __forceinline__ void quiet_fail(uint32_t* fail, uint32_t off) {
   if (off < __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(fail, off);
 }
 
+// the words of MemberDev's first 48 B (the quiet check's and the quiet apply's): three 16-B loads
+struct QuietMem {
+  uint64_t ack_due, relay_due;
+  uint32_t ping_cursor, ping_len, table_size, fd_sync_cnt, ins_rank;
+  uint8_t join_now, join_pending, leave_pending, init_wait;
+  uint64_t fd_period;
+};
+static_assert(sizeof(QuietMem) == 48 && offsetof(MemberDev, fd_period) == 40, "QuietMem mirrors MemberDev's head");
+__device__ __forceinline__ QuietMem quiet_mem(const Ctx& c, uint32_t i) {
+  const uint4* p = reinterpret_cast<const uint4*>(c.mem + i);
+  uint4 w[3] = {p[0], p[1], p[2]};
+  QuietMem m;
+  __builtin_memcpy(&m, w, sizeof m);
+  return m;
+}
+
 // k_quiet_scan: T = T0 (the window's first tick), K ticks.  Thread per owned member (grid-stride),
 // plus the global checks spread over the grid: `ref` (every subject), the wheel buckets of the window.
+// Every word a thread's first item needs — its ref word(s), its timer-bucket queue, the member's
+// schedule, flags, witness count and MemberDev head — is loaded in ONE batch before any decision;
+// the member's ping list and its targets' words follow (quiet_member_scan).  A thread's failing tick
+// goes to the control block once, wave-reduced.
 // Sharded engines: each shard's witness proves its rows equal ITS ref, so the shards' refs must be
 // equal too (a partition healed after removal leaves each side's shard with its own ref): ref_a / ref_b
 // are two arrays that agree at every subject iff they do — a local group passes shard 0's ref and
 // this shard's, an RCCL engine the elementwise min and max of the ranks' refs (allreduced).
 __global__ void __launch_bounds__(256) k_quiet_scan(KP, uint32_t K, QuietCtl* q, const uint32_t* ref_a,
-                                                    const uint32_t* ref_b) {
+                                                    const uint32_t* ref_b, uint32_t pingable) {
   const Ctx c = pctx(P, T);
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
   uint32_t* fail = &q->fail;
-  // ref: no SUSPECT / LEAVING record in the table, and one ref for every shard
-  for (uint32_t s = gtid; s < c.n; s += gsz) {
-    const uint32_t r = c.ref[s];
-    if (r_in_table(r) && r_status(r) != SWIM_ALIVE) quiet_fail(fail, 0);
-    if (ref_a && ref_a[s] != ref_b[s]) quiet_fail(fail, 0);
-  }
-  // suspicion timers due in the window (a queued entry may be a cancelled timer; the per-tick path
-  // decides, so the window ends at the first non-empty bucket)
-  const uint32_t W = c.wheel_mask + 1, nb = min(K, W);
-  for (uint32_t x = gtid; x < nb * c.wheel_nq; x += gsz) {
-    const uint32_t j = x / c.wheel_nq, qi = x - j * c.wheel_nq;
-    if (c.wheel_cnt[(size_t)((T + j) & c.wheel_mask) * c.wheel_nq + qi]) quiet_fail(fail, j);
-  }
-  uint32_t tmin = 0xffffffffu, tmax = 0;
-  for (uint32_t i = gtid; i < c.nl; i += gsz) {
-    const uint32_t v = c.lo + i;
-    if (c.mflag[i]) { quiet_fail(fail, 0); continue; }  // FD SYNCs / start0 / graceful stop pending
-    if (!c.up[v]) continue;
-    const MemberDev m = c.mem[i];
-    const GossipSched g = c.gs[i];
+  const uint32_t W = c.wheel_mask + 1, nb = min(K, W), nwq = nb * c.wheel_nq;
+  const uint32_t xmax = max(max(c.n, nwq), c.nl);
+  uint32_t tmin = 0xffffffffu, tmax = 0, worst = K;
+  for (uint32_t x = gtid; x < xmax; x += gsz) {
+    // ---- one batch of independent loads
+    const bool hs = x < c.n, hw = x < nwq, hm = x < c.nl;
+    const uint32_t rf = hs ? c.ref[x] : 0u;
+    const uint32_t ra = hs && ref_a ? ref_a[x] : 0u, rb = hs && ref_a ? ref_b[x] : 0u;
+    uint32_t wj = 0, wc = 0;
+    if (hw) {
+      wj = x / c.wheel_nq;
+      wc = c.wheel_cnt[(size_t)((T + wj) & c.wheel_mask) * c.wheel_nq + (x - wj * c.wheel_nq)];
+    }
+    const uint32_t v = c.lo + x;
+    uint32_t mfl = 0, bz = 0, cf = 0, sf = 0, fdn = NONE;
+    uint8_t upv = 0, inb = 0;
+    GossipSched g{};
+    QuietMem m{};
+    if (hm) {
+      mfl = c.mflag[x];
+      upv = c.up[v];
+      inb = c.default_inbound[v];
+      bz = c.bnz[x];
+      cf = c.compact_flag[x];
+      sf = c.seg_flag[x];
+      fdn = c.fd_next[x];
+      g = c.gs[x];
+      m = quiet_mem(c, x);
+    }
+    // ---- ref: no SUSPECT / LEAVING record in the table, and one ref for every shard
+    if (hs && r_in_table(rf) && r_status(rf) != SWIM_ALIVE) worst = 0;
+    if (hs && ref_a && ra != rb) worst = 0;
+    // ---- suspicion timers due in the window (a queued entry may be a cancelled timer; the per-tick
+    // path decides, so the window ends at the first non-empty bucket)
+    if (hw && wc) worst = min(worst, wj);
+    if (!hm) continue;
+    if (mfl) { worst = 0; continue; }  // FD SYNCs / start0 / graceful stop / deferred SYNC_ACKs pending
+    if (!upv) continue;
     // (an ack / relay deadline before T0 is a stale value of a member that was stopped: never due)
-    bool ok = g.len == 0 && c.compact_flag[i] == 0 && c.seg_flag[i] == 0 && m.ack_due < T && m.relay_due < T &&
-              m.fd_sync_cnt == 0 && m.ins_rank == 0 && !m.join_now && !m.join_pending && !m.leave_pending &&
-              !m.init_wait;
-    // the record row equals ref (its block witness counts are all zero: the maintained count of
+    // the record row equals ref: its block witness counts are all zero (the maintained count of
     // non-zero blocks, swim_device.h bdiff_add)
-    const uint32_t any = c.bnz[i];
-    ok = ok && any == 0;
-    if (!ok) { quiet_fail(fail, 0); continue; }
+    const bool ok = g.len == 0 && cf == 0 && sf == 0 && m.ack_due < T && m.relay_due < T && m.fd_sync_cnt == 0 &&
+                    m.ins_rank == 0 && !m.join_now && !m.join_pending && !m.leave_pending && !m.init_wait && bz == 0;
+    if (!ok) { worst = 0; continue; }
     tmin = min(tmin, m.table_size);
     tmax = max(tmax, m.table_size);
-    const uint32_t off = quiet_member_scan(c, v, T, K, m, c.fd_next[i], fail);
-    if (off < K) quiet_fail(fail, off);
+    if (worst == 0) continue;
+    worst = min(worst, quiet_member_scan(c, v, T, K, m.ping_cursor, m.ping_len, fdn, inb != 0, fail, pingable != 0));
   }
-  // table sizes (wave-reduced)
+  // the wave's earliest failing tick and table sizes, one atomic each
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) {
     tmin = min(tmin, (uint32_t)__shfl_xor(tmin, d, 64));
     tmax = max(tmax, (uint32_t)__shfl_xor(tmax, d, 64));
+    worst = min(worst, (uint32_t)__shfl_xor(worst, d, 64));
   }
-  if ((threadIdx.x & 63) == 0 && tmin != 0xffffffffu) {
-    atomicMin(&q->tmin, tmin);
-    atomicMin(&q->tmax_neg, 0xffffffffu - tmax);
+  if ((threadIdx.x & 63) == 0) {
+    if (worst < K) quiet_fail(fail, worst);
+    if (tmin != 0xffffffffu) {
+      atomicMin(&q->tmin, tmin);
+      atomicMin(&q->tmax_neg, 0xffffffffu - tmax);
+    }
   }
 }
 
@@ -192,39 +235,35 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
   unsigned long long npings = 0, nsync = 0, nack = 0, nrec = 0;
   for (uint32_t i = gtid; i < c.nl; i += gsz) {
     const uint32_t v = c.lo + i;
+    // every word the member's window reads, in one batch
     const bool up = c.up[v] != 0;
+    const uint32_t fdn = c.fd_next[i], sn0 = c.sync_next[i];
+    const GossipSched g = c.gs[i];
+    const QuietMem qm = quiet_mem(c, i);
     MemberDev& m = c.mem[i];
     // ---- FD (doPing every pingInterval; acknowledged at once)
-    if (up) {
-      uint64_t t = c.fd_next[i];
-      if (t < Tend) {
-        uint32_t k = 0;
-        for (; t < Tend; t += c.P) ++k;
-        m.fd_period += k;
-        m.ev_minor = 0;
-        if (m.ping_len) {
-          m.ping_cursor += k;
-          npings += k;
-        }
-        c.fd_next[i] = (uint32_t)t;
+    if (up && fdn < Tend) {
+      const uint32_t k = (uint32_t)((Tend - 1 - fdn) / c.P) + 1;
+      m.fd_period = qm.fd_period + k;
+      m.ev_minor = 0;
+      if (qm.ping_len) {
+        m.ping_cursor = qm.ping_cursor + k;
+        npings += k;
       }
+      c.fd_next[i] = fdn + k * c.P;
     }
     // ---- gossip rounds (the timer runs while down; period++ only while up)
-    {
-      GossipSched& g = c.gs[i];
-      const uint32_t gn = g.next;
-      if (gn < Tend) {
-        const uint32_t r = (uint32_t)((Tend - 1 - gn) / c.G) + 1;
-        g.next = gn + r * c.G;
-        if (up) g.period += r;
-      }
+    if (g.next < Tend) {
+      const uint32_t r = (uint32_t)((Tend - 1 - g.next) / c.G) + 1;
+      GossipSched& gw = c.gs[i];
+      gw.next = g.next + r * c.G;
+      if (up) gw.period = g.period + r;
     }
     // ---- periodic SYNC (the schedule advances while down too, sync_collect_fast)
-    uint32_t sn = c.sync_next[i];
+    uint32_t sn = sn0;
     if (sn != NONE && sn < Tend) {
-      const uint32_t tsz = m.table_size;
       for (; sn < Tend; sn += c.S)
-        if (up) quiet_sync(c, v, sn, tsz, nsync, nack, nrec);
+        if (up) quiet_sync(c, v, sn, qm.table_size, nsync, nack, nrec);
       c.sync_next[i] = sn;
     }
   }
