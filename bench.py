@@ -399,7 +399,7 @@ def step_roofline(stats, prof, fprof, dprof, qprof, ticks, gossip_ticks, dt, ste
                     "their swim_profile_* rules, quiet windows per swim_profile_quiet"}
 
 
-def cpu_baseline(n, p0, periods):
+def cpu_baseline(n, p0, periods, workload=None, single=True):
     """The CPU oracle (oracle/liboracle_swim.so, the C++ lockstep restatement) on the same N and
     workload, over the same periods the GPU timed ([p0, p0 + periods) of the schedule; the periods
     before p0 run untimed on all cores), bounded to `periods` periods: once with 1 thread and once
@@ -409,13 +409,14 @@ def cpu_baseline(n, p0, periods):
     import oracle
     from swimgpu import abi
     lib = oracle.lib()
+    workload = workload or WORKLOAD
     # the box's CPU share: OMP_NUM_THREADS is set to it there (os.cpu_count() is the whole machine)
     all_cores = max(1, min(64, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)))
     legs = {}
-    for threads in (1, all_cores):
+    for threads in ((1, all_cores) if single else (all_cores,)):
         cfg = make_config(lib)
-        sch = Schedule(WORKLOAD, n, p0 + periods)
-        if WORKLOAD == "churn":
+        sch = Schedule(workload, n, p0 + periods)
+        if workload == "churn":
             churn_capacities(cfg, sch.capacity)
         e = abi.Engine(lib, cfg, sch.capacity, n, 1)
         sch.setup(e)
@@ -426,12 +427,16 @@ def cpu_baseline(n, p0, periods):
         sch.run(e, p0, p0 + periods)
         legs[threads] = time.perf_counter() - t0
         e.close()
-    dt1, dtn = legs[1], legs[all_cores]
-    return {"value": n * periods / dtn, "unit": "member-periods/s", "cores": all_cores, "kind": "port",
-            "single_thread_value": n * periods / dt1, "nproc": os.cpu_count(), "cpu_model": cpu_model(),
-            "sample": f"CPU oracle (C++ lockstep restatement), N={n}, LAN defaults, workload {WORKLOAD}, "
-                      f"periods {p0}..{p0 + periods} of the schedule (the GPU's first timed periods; "
-                      f"0..{p0} untimed): {dtn:.1f} s on {all_cores} threads, {dt1:.1f} s on 1 thread"}
+    dt1, dtn = legs.get(1), legs[all_cores]
+    out = {"value": n * periods / dtn, "unit": "member-periods/s", "cores": all_cores, "kind": "port",
+           "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+           "sample": f"CPU oracle (C++ lockstep restatement), N={n}, LAN defaults, workload {workload}, "
+                     f"periods {p0}..{p0 + periods} of the schedule (the GPU's first timed periods; "
+                     f"0..{p0} untimed): {dtn:.1f} s on {all_cores} threads"
+                     + (f", {dt1:.1f} s on 1 thread" if dt1 else "")}
+    if dt1:
+        out["single_thread_value"] = n * periods / dt1
+    return out
 
 
 def launch_ranks(n: int) -> int:
@@ -473,7 +478,7 @@ def main():
     ap.add_argument("--no-extras", action="store_true",
                     help="quiet workload: skip the fanout-roofline (failures window) and KS-mode side runs")
     ap.add_argument("--fanout-steps", type=int, default=6)
-    ap.add_argument("--ks-steps", type=int, default=5)
+    ap.add_argument("--churn-steps", type=int, default=3, help="timed periods of the config-3 churn side run")
     ap.add_argument("--no-churn", action="store_true", help="skip the config-3 churn side run")
     ap.add_argument("--progress", action="store_true", help="print a stderr line after every period")
     ap.add_argument("--workload", choices=("quiet", "failures", "churn"), default="quiet")
@@ -620,14 +625,16 @@ def main():
         line["quiet_window_model"] = quiet_window_model(e, n, tpp)
     if world == 1 and args.workload == "quiet" and not args.no_extras and args.local_shards == 1 and hook is None:
         e.close()
-        # (1) the per-tick kernel chain on the same workload (quiet windows off): the SYNC merge's
-        # roofline (k_sync_apply's SYNC launch, classification fused) is measured there
-        p_dt, p_prof, _, _, _, _ = side_run(lib, "quiet", n, 2, args.ks_steps, local_rank, quiet=False)
+        # (1) the per-tick kernel chain on the same workload and the same timed periods (quiet windows
+        # off): the SYNC merge's roofline (k_sync_apply's SYNC launch, classification fused) is
+        # measured there
+        p_dt, p_prof, _, _, _, _ = side_run(lib, "quiet", n, args.warmup, args.steps, local_rank, quiet=False)
         line["per_tick_path"] = {
-            "value": n * args.ks_steps / p_dt, "unit": "member-periods/s", "ms_per_step": p_dt / args.ks_steps * 1e3,
-            "steps": args.ks_steps, "config": "same workload, quiet windows off (swim_set_quiet_path(0)): the "
-                                              "per-tick kernel chain of DESIGN.md §5",
-            "roofline_merge": merge_roofline(p_prof, 1, 1, "quiet", n, p_dt, args.ks_steps, tpp)}
+            "value": n * args.steps / p_dt, "unit": "member-periods/s", "ms_per_step": p_dt / args.steps * 1e3,
+            "steps": args.steps, "warmup": args.warmup,
+            "config": "same workload and timed periods, quiet windows off (swim_set_quiet_path(0)): the per-tick "
+                      "kernel chain of DESIGN.md §5",
+            "roofline_merge": merge_roofline(p_prof, 1, 1, "quiet", n, p_dt, args.steps, tpp)}
         # (2) the failures workload over a window that starts with its second kill (period 30: FD
         # detection, the SUSPECT storm through all N members, the gossip's remaining rounds): the
         # fanout and delivery kernels.  The first storm also holds every member's first
@@ -642,20 +649,23 @@ def main():
                             "roofline_deliver": deliver_roofline(f_dprof, window, fs == 6 and n == 65536)}
         line["roofline_fanout"] = line["failures"]["roofline_fanout"]
         line["roofline_deliver"] = line["failures"]["roofline_deliver"]
-        # (3) BASELINE config 3 (churn) at its stated N = 16,384, its first timed period
+        # (3) BASELINE config 3 (churn) at its stated N = 16,384: periods 1..1 + churn_steps (the SYNC
+        # re-gossip storm grows every period)
         if not args.no_churn:
-            c_dt, _, _, c_st, _, _ = side_run(lib, "churn", DEFAULT_MEMBERS["churn"], 1, 1, local_rank)
-            line["churn"] = {"value": DEFAULT_MEMBERS["churn"] / c_dt, "unit": "member-periods/s",
-                             "ms_per_step": c_dt * 1e3, "steps": 1, "warmup": 1,
+            cs = args.churn_steps
+            c_dt, _, _, c_st, _, _ = side_run(lib, "churn", DEFAULT_MEMBERS["churn"], 1, cs, local_rank)
+            line["churn"] = {"value": DEFAULT_MEMBERS["churn"] * cs / c_dt, "unit": "member-periods/s",
+                             "ms_per_step": c_dt * 1e3 / cs, "steps": cs, "warmup": 1,
                              "config": WORKLOAD_TEXT["churn"].format(n=DEFAULT_MEMBERS["churn"],
                                                                      churn=DEFAULT_MEMBERS["churn"] * CHURN_PER_MILLE // 1000,
                                                                      loss=CHURN_LOSS),
                              "gossip_messages": c_st["gossip_messages"]}
         # (4) the timing mode whose latency distributions pass the KS test against the reference-timing
         # DES (tests/test_ks_des.py: independent timer phases, 10 ms ticks); same quiet workload
-        k_dt, _, _, _, _, k_q = side_run(lib, "quiet", n, 2, args.ks_steps, local_rank, timer_stagger=1, tick_ms=10)
-        line["ks_mode"] = {"value": n * args.ks_steps / k_dt, "unit": "member-periods/s",
-                           "ms_per_step": k_dt / args.ks_steps * 1e3, "steps": args.ks_steps,
+        k_dt, _, _, _, _, k_q = side_run(lib, "quiet", n, args.warmup, args.steps, local_rank, timer_stagger=1,
+                                         tick_ms=10)
+        line["ks_mode"] = {"value": n * args.steps / k_dt, "unit": "member-periods/s",
+                           "ms_per_step": k_dt / args.steps * 1e3, "steps": args.steps, "warmup": args.warmup,
                            "quiet_windows": k_q,
                            "config": "same workload, timer_stagger=1, tick_ms=10 (100 ticks per period)",
                            "ks": "tests/test_ks_des.py::test_ks_gpu_vs_des (N=64 and 1,024, 200 seeds, p >= 0.01)"}
@@ -667,6 +677,8 @@ def main():
         # first timed period only
         cpu_periods = args.cpu_periods or (1 if args.workload == "churn" else 10)
         line["cpu_baseline"] = cpu_baseline(n, args.warmup, min(cpu_periods, args.steps))
+        if "churn" in line:  # config 3's first timed period on the oracle, all cores (the GPU side run's period 1)
+            line["churn"]["cpu_baseline"] = cpu_baseline(DEFAULT_MEMBERS["churn"], 1, 1, "churn", single=False)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -228,6 +228,7 @@ struct Member {
   std::vector<uint32_t> seeds;
   uint32_t w_link = NONE, w_n = 0;
   uint64_t w_ready = 0, w_gp = 0;
+  uint64_t ctl_tick1 = 0;  // 1 + the tick of the member's last control-phase operation (swim_ingest_sync)
 };
 
 // cell helpers
@@ -1781,8 +1782,13 @@ int32_t swim_ingest_sync(swim_engine* e, uint32_t v, const swim_record* records,
     if (records[i].member >= e->n || records[i].status >= SWIM_DEAD || records[i].inc < 0) return SWIM_EINVAL;
   if (!e->m[v].up) return SWIM_ESTATE;
   const Reason reason = initial ? INITIAL_SYNC : SYNC;
-  e->m[v].ev_minor = 0;
-  e->m[v].fetch_ctr = 0;
+  // the control phase's event minors and fetch draws run on across the operations of one tick (two
+  // ingestions between the same ticks: distinct event keys, distinct draws)
+  if (e->m[v].ctl_tick1 != e->T + 1) {
+    e->m[v].ev_minor = 0;
+    e->m[v].fetch_ctr = 0;
+    e->m[v].ctl_tick1 = e->T + 1;
+  }
   std::vector<PendingAlive> pending;
   for (uint32_t i = 0; i < n; ++i)
     e->update_membership(v, Record{records[i].member, records[i].status, records[i].inc}, reason, SWIM_PHASE_CONTROL,

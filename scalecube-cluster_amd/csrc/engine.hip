@@ -832,6 +832,8 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
   *done = std::min(__atomic_load_n(e->h_done, __ATOMIC_ACQUIRE), K);
   if (prof) {
     float ms = 0.f;
+    // (the spinning wait saw the stream's work complete before the runtime marks the event done)
+    hipEventSynchronize(e->qev[1]);
     if (hipEventElapsedTime(&ms, e->qev[0], e->qev[1]) == hipSuccess) e->qprof_ms += ms;
     // algorithmic bytes (swim.h swim_profile_quiet): SURVEY.md §8(d)'s 21 B per member-period of the
     // ping phase, plus what the quiet check must read once per window: every owned row's count of
@@ -958,8 +960,13 @@ __global__ void __launch_bounds__(256) k_ingest_sync(Params* P, uint64_t T, uint
   uint64_t* pend = P->b.pend;  // (workgroup 0's slice of the SYNC apply's pending admissions)
   if (threadIdx.x == 0) {
     MemberDev& m = mem(c, v);
-    m.ev_minor = 0;
-    m.fetch_ctr = 0;
+    // the control phase's event minors and fetch draws run on across the operations of one tick
+    // (two ingestions between the same ticks: distinct event keys, distinct draws)
+    if (m.ctl_tick1 != (uint32_t)T + 1) {
+      m.ev_minor = 0;
+      m.fetch_ctr = 0;
+      m.ctl_tick1 = (uint32_t)T + 1;
+    }
     uint32_t npend = 0;
     for (uint32_t i = 0; i < n; ++i)
       if (update_membership(c, v, rec[i].member, rec[i].status, rec[i].inc, reason, SWIM_PHASE_CONTROL))

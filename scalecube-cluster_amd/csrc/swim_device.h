@@ -138,6 +138,7 @@ struct alignas(16) MemberDev {
   // (w_link1 = 1 + the seq its PAck will take, 0 outside such a merge)
   uint32_t pack_seq, init_pend;
   uint32_t w_link1, w_n, w_ready, w_gp;
+  uint32_t ctl_tick1;  // 1 + the tick of the member's last control-phase operation (swim_ingest_sync)
 };
 static_assert(sizeof(MemberDev) == 224, "MemberDev: 224 B (the quiet scan's words in the first 64-B sector)");
 

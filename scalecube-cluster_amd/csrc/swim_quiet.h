@@ -171,11 +171,14 @@ __global__ void __launch_bounds__(256) k_quiet_scan(KP, uint32_t K, QuietCtl* q,
     tmax = max(tmax, (uint32_t)__shfl_xor(tmax, d, 64));
     worst = min(worst, (uint32_t)__shfl_xor(worst, d, 64));
   }
+  // (each atomic only when it would change the word: with one table size everywhere, the first
+  // waves set both words and the other ~1,000 skip them — same-address atomics serialise at the L2)
   if ((threadIdx.x & 63) == 0) {
     if (worst < K) quiet_fail(fail, worst);
     if (tmin != 0xffffffffu) {
-      atomicMin(&q->tmin, tmin);
-      atomicMin(&q->tmax_neg, 0xffffffffu - tmax);
+      if (tmin < __hip_atomic_load(&q->tmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&q->tmin, tmin);
+      const uint32_t tn = 0xffffffffu - tmax;
+      if (tn < __hip_atomic_load(&q->tmax_neg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&q->tmax_neg, tn);
     }
   }
 }

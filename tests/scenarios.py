@@ -262,7 +262,11 @@ def catalog() -> list[Scenario]:
                       (60, "kill", 4), (61, "ingest", 1, [(4, abi.SUSPECT, 0)], False), (100, "ingest", 6, [], False),
                       (120, "default_delay", 80, ALL_), (121, "ingest", 2, [(11, abi.ALIVE, 5), (10, abi.SUSPECT, 0)],
                                                                      False),
-                      (200, "ingest", 8, [(5, abi.LEAVING, 0), (14, abi.SUSPECT, 3)], False)],
+                      (200, "ingest", 8, [(5, abi.LEAVING, 0), (14, abi.SUSPECT, 3)], False),
+                      # two ingestions at one viewer between the same ticks: the second one's events and
+                      # metadata-fetch draws continue the first one's (distinct keys, distinct draws)
+                      (250, "ingest", 3, [(6, abi.LEAVING, 9), (10, abi.ALIVE, 9)], False),
+                      (250, "ingest", 3, [(9, abi.LEAVING, 9), (11, abi.ALIVE, 12)], False)],
                  check_every=20),
         # onSync's SYNC_ACK waits for the SYNC's updateMembership Monos (MembershipProtocolImpl.java
         # :394-415, :491-509): admissions whose metadata fetch is lost (10 % loss: the request fails at
