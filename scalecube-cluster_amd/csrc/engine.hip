@@ -204,6 +204,7 @@ struct swim_engine {
   std::vector<LinkDev> links_h;
   std::vector<int32_t> delay_means;  // NetworkEmulator meanDelay (ms) of each delay table, in table order
   std::vector<uint32_t> joins;  // joins starting at the next tick
+  std::vector<std::pair<uint64_t, uint32_t>> fq_joins;  // (tick, joiner) of the recent joins (grow_for_joins)
   // addresses (swim_join_at): addr_h[x] = the address member x was started on, route_h[x] = the
   // member listening on it now (both empty while every member is on its own address); binds: the
   // (joiner, member whose address it takes) pairs starting at the next tick
@@ -643,6 +644,81 @@ static int32_t grow_rows_for_joins(swim_engine* e) {
   return e->rccl ? setup_peers_rccl(e) : setup_peers_local(e);
 }
 
+// Join bursts size two per-shard structures whose need the reference does not bound (grow_for_joins,
+// before a tick that starts joins; the joins of the last 4 metadataTimeout spans are counted):
+// * the delayed metadata queue (Ctx.fq, per tick parity) holds every GET_METADATA round trip in
+//   flight on the shard.  Its base capacity, max(4096, 2n), covers the admissions of a cluster that
+//   is not joining; a join adds up to n round trips on its own shard (its first SYNC_ACK admits the
+//   whole table) and one per viewer of every shard (the joiner's admission, as the news spreads),
+//   each in flight for at most metadataTimeout after its send;
+// * the pending SYNC_ACKs of a member (Ctx.pa, pa_cap per member): a seed answers every joiner's
+//   SYNC after the admission fetches it waits on, so a burst of J joiners through one seed holds J
+//   of them at once beside the base PA_CAP.
+// The live entries keep their slots.  Shard-local (no collective): an allocation that fails keeps the
+// structure, and a tick that overflows it reports ERR_FETCHQ / ERR_PACK, never a silent drop.
+static int32_t grow_for_joins(swim_engine* e) {
+  if (e->joins.empty() || e->sh.empty()) return SWIM_OK;
+  const uint64_t span = 4ull * ((e->sh[0].c.metadata_timeout + e->tick_ms - 1) / e->tick_ms) + 1;
+  e->fq_joins.erase(std::remove_if(e->fq_joins.begin(), e->fq_joins.end(),
+                                   [&](const std::pair<uint64_t, uint32_t>& j) { return j.first + span < e->T; }),
+                    e->fq_joins.end());
+  for (uint32_t m : e->joins) e->fq_joins.push_back({e->T, m});
+  bool synced = false;
+  const uint64_t pa_need = PA_CAP + e->fq_joins.size();
+  for (Shard& sd : e->sh) {
+    if (pa_need > sd.c.pa_cap) {
+      const uint64_t cur = sd.c.pa_cap, rows = std::max(sd.c.nl, 1u);
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess) return SWIM_EDEVICE;
+      const uint64_t cap = std::min<uint64_t>(std::max(pa_need, 2 * cur), fr / 8 / (rows * sizeof(PAck)));
+      PAck* q = nullptr;
+      if (cap > cur) {
+        if (!synced) {
+          if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+          synced = true;
+        }
+        if (dalloc(&q, rows * cap) != hipSuccess) {
+          (void)hipGetLastError();
+        } else {
+          if (hipMemcpy2D(q, cap * sizeof(PAck), sd.c.pa, cur * sizeof(PAck), cur * sizeof(PAck), rows,
+                          hipMemcpyDeviceToDevice) != hipSuccess)
+            return SWIM_EDEVICE;
+          sd.release(sd.c.pa);
+          sd.allocs.push_back(q);
+          sd.c.pa = q;
+          sd.c.pa_cap = (uint32_t)cap;
+        }
+      }
+    }
+    if (!sd.c.delay_on) continue;
+    uint64_t need = std::max<uint64_t>(4096, 2ull * e->n);
+    for (const auto& j : e->fq_joins) need += sd.c.nl + (e->owner_of(j.second) == &sd ? e->n : 0u);
+    const uint64_t cur = sd.c.fq_cap;
+    if (need <= cur) continue;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return SWIM_EDEVICE;
+    const uint64_t cap = std::min<uint64_t>({std::max<uint64_t>(need, 2 * cur), fr / 8 / (2 * sizeof(FetchEnt)), NONE - 1});
+    if (cap <= cur) continue;
+    if (!synced) {
+      if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
+      synced = true;
+    }
+    FetchEnt* q = nullptr;
+    if (dalloc(&q, 2 * cap) != hipSuccess) {
+      (void)hipGetLastError();
+      continue;
+    }
+    for (int p = 0; p < 2; ++p)
+      if (hipMemcpy(q + p * cap, sd.c.fq + p * cur, sizeof(FetchEnt) * cur, hipMemcpyDeviceToDevice) != hipSuccess)
+        return SWIM_EDEVICE;
+    sd.release(sd.c.fq);
+    sd.allocs.push_back(q);
+    sd.c.fq = q;
+    sd.c.fq_cap = (uint32_t)cap;
+  }
+  return SWIM_OK;
+}
+
 static int32_t run_tick(swim_engine* e) {
   e->T += 1;
   e->host_ticks += 1;
@@ -650,6 +726,7 @@ static int32_t run_tick(swim_engine* e) {
   if (!e->binds.empty())
     if (int32_t rc = apply_binds(e)) return rc;
   if (int32_t rc = grow_rows_for_joins(e)) return rc;
+  if (int32_t rc = grow_for_joins(e)) return rc;
   const uint64_t T = e->T;
   const bool multi = e->world > 1;
   const bool gossip_tick = e->g_residue[e->T % e->G] != 0;
@@ -1060,8 +1137,9 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.hcap = next_pow2(cf.collector_capacity ? cf.collector_capacity : 4096);
   c.gix_mask = next_pow2(2 * c.gcap) - 1;
   // infected overflows a member holds at once: states that took a second sender after a collector
-  // clear (segmentation), a small fraction of the slab
-  c.inf_mask = next_pow2(std::max<uint32_t>(64, std::min<uint32_t>(4096, c.gcap / 8))) - 1;
+  // clear (segmentation), an eighth of the slab (32 B each: +1/6 of the slab's bytes).  Config 3's
+  // churn clears collectors every period: more than 4,096 live at N = 16,384 by its fourth period
+  c.inf_mask = next_pow2(std::max<uint32_t>(64, c.gcap / 8)) - 1;
   // spilled collectors by tier (6 / 62 / 510 / 16,382 intervals); blocks are recycled, so these
   // bound the collectors spilled at once, not over the run
   const uint64_t icap = cf.interval_capacity ? cf.interval_capacity : 64;  // tier-0 blocks per row
@@ -1210,6 +1288,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(c.spill_ctl, 0, sizeof(SpillCtl) * NTIER, s);
   hipMemsetAsync(c.seg_flag, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(c.pa_n, 0, 4 * (size_t)std::max(nl, 1u), s);
+  c.pa_cap = PA_CAP;
   hipMemsetAsync(c.wheel, 0xff, sizeof(uint64_t) * ((size_t)c.wheel_pages << c.wheel_pshift), s);  // WHEEL_EMPTY
   hipMemsetAsync(c.wheel_cnt, 0, sizeof(uint32_t) * (c.wheel_mask + 1) * c.wheel_nq, s);
   hipMemsetAsync(c.wheel_pt, 0xff, sizeof(uint32_t) * (c.wheel_mask + 1) * c.wheel_nq * c.wheel_ptmax, s);
@@ -1916,7 +1995,8 @@ static int32_t enable_delay(swim_engine* e) {
       return SWIM_EDEVICE;
     b.sdq_bcap = sbcap;
     b.park_cap = pcap;
-    // delayed metadata round trips: every viewer may have a whole table's admissions in flight
+    // delayed metadata round trips: the base capacity of a cluster that is not joining; a join
+    // burst grows it before its tick (grow_for_joins)
     const uint32_t fcap = std::max<uint32_t>(4096, 2 * e->n);
     const size_t nl2 = 2ull * std::max(sd.c.nl, 1u);
     if (!sd.alloc(&sd.c.fq, 2ull * fcap) || !sd.alloc(&sd.c.fq_head, nl2) || !sd.alloc(&sd.c.fq_tail, nl2) ||
@@ -2310,13 +2390,13 @@ int32_t swim_profile_deliver(swim_engine* e, swim_kernel_profile* out) {
 // profiling builds (-DSWIM_PHASE_PROF): the per-phase wall-time sums of the instrumented kernels
 // (swim_phases.h g_dbg); reset = 1 zeroes them after the read.  Zeros in the product build.
 int32_t swim_debug_counters(uint64_t* out, uint32_t n, int32_t reset) {
-  if (!out || n > 32) return SWIM_EINVAL;
-  unsigned long long h[32] = {};
+  if (!out || n > 48) return SWIM_EINVAL;
+  unsigned long long h[48] = {};
   if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dbg), sizeof h) != hipSuccess)
     return SWIM_EDEVICE;
   for (uint32_t i = 0; i < n; ++i) out[i] = h[i];
   if (reset) {
-    unsigned long long z[32] = {};
+    unsigned long long z[48] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof z) != hipSuccess) return SWIM_EDEVICE;
   }
   return SWIM_OK;

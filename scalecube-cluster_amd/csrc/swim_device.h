@@ -42,7 +42,7 @@ enum : uint32_t {
   ERR_XPTR = 1u << 17,      // SWIM_DEBUG_SYNC: a sharded tick would dereference a null exchange pointer
   ERR_SDELAY = 1u << 18,    // delayed SYNCs / SYNC_ACKs: a delay bucket or the park slots ran out
   ERR_FETCHQ = 1u << 19,    // more delayed GET_METADATA round trips in flight than the fetch queue holds
-  ERR_PACK = 1u << 20,      // a member holds more merged messages waiting on their Monos than PA_CAP
+  ERR_PACK = 1u << 20,      // a member holds more merged messages waiting on their Monos than pa_cap
 };
 
 // A GET_METADATA round trip in flight under message delay (MetadataStoreImpl.fetchMetadata :146-185):
@@ -66,7 +66,7 @@ struct FetchEnt {
 // gossip (onLeavingDetected returns spreadMembershipGossip: GossipProtocolImpl.spread's Mono ends when
 // the gossip most likely disseminated, :167-180).  Per member, in creation order (Ctx.pa, pa_n);
 // oracle: PendingAck.
-constexpr uint32_t PA_CAP = 64;
+constexpr uint32_t PA_CAP = 64;  // pa_cap's base (grown before join bursts: grow_for_joins)
 enum : uint32_t { PA_INITIAL_ACK = 1, PA_INIT = 2 };  // the deferred ack answers start0 / a start0 group
 struct PAck {
   uint32_t to;     // the SYNC's sender (PA_INIT: unused)
@@ -182,16 +182,18 @@ struct alignas(8) GossipCold {
 };
 static_assert(sizeof(GossipHot) == 16 && sizeof(GossipCold) == 8, "24 B per GossipState");
 // infected-overflow entry: GossipState.infected[1..] of one (gossiper, seq) of one member
-constexpr uint32_t INF_EMPTY = 0xffffffffu, INF_TOMB = 0xfffffffeu;  // gossiper values of free slots
+constexpr uint32_t INF_EMPTY = 0xffffffffu;  // gossiper value of a free slot
 struct alignas(16) InfOver {
   uint32_t gossiper, seq;
   uint32_t inf[GINF - 1];
   uint32_t pad;
 };
 static_assert(sizeof(InfOver) == 32, "32 B per infected overflow");
-// linear probing from the key's hash; a lookup stops at an empty slot, an insert reuses the first
-// tombstone before it.  One writer per member at a time (its delivery thread, or its sender wave's
-// sweep, which only tombstones entries it found).
+// linear probing from the key's hash; a lookup stops at an empty slot.  An entry is removed by
+// backward-shift deletion (inf_erase: the entries after it on its probe run move up), so the table
+// holds no tombstones and a miss stops at the first free slot however long the run has been going.
+// One writer per member at a time, one lane at a time: its delivery's serial steps, or one lane of
+// its sender wave's sweep after another (emit_one), with no reader of the table in between.
 __device__ __forceinline__ uint32_t inf_hash(uint32_t g, uint32_t q) { return (g * 0x9e3779b1u) ^ (q * 0x85ebca77u); }
 __device__ inline int32_t inf_find(const InfOver* t, uint32_t mask, uint32_t g, uint32_t q) {
   for (uint32_t i = 0, h = inf_hash(g, q) & mask; i <= mask; ++i, h = (h + 1) & mask) {
@@ -200,6 +202,22 @@ __device__ inline int32_t inf_find(const InfOver* t, uint32_t mask, uint32_t g, 
     if (k == g && t[h].seq == q) return (int32_t)h;
   }
   return -1;
+}
+// frees slot f: each later entry of the run whose home slot does not lie cyclically in (hole, its
+// slot] moves into the hole, until a free slot ends the run
+__device__ inline void inf_erase(InfOver* t, uint32_t mask, uint32_t f) {
+  uint32_t hole = f;
+  for (uint32_t n = 0, j = (f + 1) & mask; n < mask; ++n, j = (j + 1) & mask) {
+    const InfOver x = t[j];
+    if (x.gossiper == INF_EMPTY) break;
+    const uint32_t h = inf_hash(x.gossiper, x.seq) & mask;
+    const bool stays = hole <= j ? (h > hole && h <= j) : (h > hole || h <= j);
+    if (!stays) {
+      t[hole] = x;
+      hole = j;
+    }
+  }
+  t[hole].gossiper = INF_EMPTY;
 }
 // lane l's value to every lane when l is wave-uniform: v_readlane (a register read) instead of the
 // LDS crossbar round trip __shfl takes
@@ -265,7 +283,7 @@ struct SlabRef {
       int32_t f = inf_find(inf, inf_mask, g.gossiper, g.seq);
       if (f < 0) {  // a new entry: the first free slot on the probe path
         for (uint32_t i = 0, x = inf_hash(g.gossiper, g.seq) & inf_mask; i <= inf_mask; ++i, x = (x + 1) & inf_mask)
-          if (inf[x].gossiper == INF_EMPTY || inf[x].gossiper == INF_TOMB) { f = (int32_t)x; break; }
+          if (inf[x].gossiper == INF_EMPTY) { f = (int32_t)x; break; }
       }
       if (f < 0) {
         atomicOr(err, ERR_INFECTED);  // the member's overflow table is full
@@ -282,10 +300,10 @@ struct SlabRef {
     H(p) = h;
     C(p) = k;
   }
-  // the sweep dropped a state whose infected list overflowed
+  // the sweep dropped a state whose infected list overflowed (one lane of the wave at a time)
   __device__ __forceinline__ void drop_more(uint32_t g, uint32_t q) const {
     const int32_t f = inf_find(inf, inf_mask, g, q);
-    if (f >= 0) inf[f].gossiper = INF_TOMB;
+    if (f >= 0) inf_erase(inf, inf_mask, (uint32_t)f);
   }
 };
 
@@ -465,8 +483,9 @@ struct Ctx {
   uint32_t* fq_tail;
   uint32_t* fq_cnt;
   uint32_t fq_cap;
-  PAck* pa;        // [nl][PA_CAP] PendingAcks, creation order
+  PAck* pa;        // [nl][pa_cap] PendingAcks, creation order
   uint32_t* pa_n;  // [nl]
+  uint32_t pa_cap;
   uint8_t* is_seed;
   uint32_t* seeds;
   uint32_t n_seeds;
@@ -707,14 +726,22 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
 }
+// Linear probing, four slots per round trip: a round loads the keys of the next four slots of the
+// probe sequence together (a loaded table's runs are long: one dependent load per slot made the
+// storm's collector lookups the deepest chains of the delivery and fanout kernels), then takes the
+// first that matches or is empty, in probe order — the same slot a one-by-one probe finds.
 __device__ inline CollEnt* coll_find(const Ctx& c, uint32_t v, uint32_t gossiper) {
   CollEnt* base = c.coll + (size_t)(v - c.lo) * c.hcap;
   uint32_t mask = c.hcap - 1, h = hash32(gossiper) & mask, key = gossiper + 1;
-  for (uint32_t i = 0; i < c.hcap; ++i) {
-    CollEnt* e = base + ((h + i) & mask);
-    const uint32_t k = e->key;
-    if (k == key) return e;
-    if (k == 0) return nullptr;
+  for (uint32_t i = 0; i < c.hcap; i += 4) {
+    uint32_t k[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) k[q] = base[(h + i + q) & mask].key;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (k[q] == key) return base + ((h + i + q) & mask);
+      if (k[q] == 0) return nullptr;
+    }
   }
   return nullptr;
 }
@@ -760,41 +787,55 @@ __device__ inline CollEnt* coll_ensure_v(const Ctx& c, uint32_t v, uint32_t goss
 // told apart by ballot (the lowest lane takes it, the others probe on), so no compare-and-swap round
 // trip.  Called by the whole wave; returns the leader's entry (null: not a leader, or the table is full).
 __device__ inline CollEnt* coll_ensure_wave(const Ctx& c, uint32_t v, bool lead, uint32_t gossiper, uint32_t lane,
-                                            CollEnt& out) {
+                                            CollEnt& out, uint32_t* probes = nullptr) {
   CollEnt* base = c.coll + (size_t)(v - c.lo) * c.hcap;
   const uint32_t mask = c.hcap - 1, key = gossiper + 1;
   uint32_t h = hash32(gossiper) & mask;
   CollEnt* res = nullptr;
   bool act = lead;
+  // a round: the entry at h and the keys of the three slots after it, in one round trip; a match
+  // among those three moves h onto it (its entry comes with the next round), an empty one is claimed
   for (uint32_t it = 0; __ballot(act); ++it) {
+    if (probes) ++*probes;
     if (it == c.hcap) {  // (wave-uniform)
       if (act) set_err(c, ERR_HASH);
       break;
     }
     CollEnt x{};
-    if (act) x = base[h];
+    uint32_t k1 = 0, k2 = 0, k3 = 0;
+    if (act) {
+      x = base[h];
+      k1 = base[(h + 1) & mask].key;
+      k2 = base[(h + 2) & mask].key;
+      k3 = base[(h + 3) & mask].key;
+    }
     if (act && x.key == key) {
       out = x;
       res = base + h;
       act = false;
     }
-    const bool claim = act && x.key == 0;
+    // the first of the four slots that matches or is empty (4: none)
+    const uint32_t q = x.key == 0 ? 0u : k1 == key || k1 == 0 ? 1u : k2 == key || k2 == 0 ? 2u : k3 == key || k3 == 0 ? 3u : 4u;
+    const uint32_t kq = q == 1u ? k1 : q == 2u ? k2 : k3;
+    const bool claim = act && q < 4u && (q == 0u || kq == 0u);
+    const uint32_t slot = (h + q) & mask;
     bool won = false;
     for (uint64_t todo = __ballot(claim); todo;) {
       const uint32_t l = (uint32_t)__ffsll((unsigned long long)todo) - 1;
-      const uint32_t sl = rdlane(h, l);
-      todo &= ~__ballot(claim && h == sl);
+      const uint32_t sl = rdlane(slot, l);
+      todo &= ~__ballot(claim && slot == sl);
       won |= lane == l;
     }
     if (won) {
       CollEnt ne;
       ne.key = key; ne.lo = 0; ne.hi = 0; ne.meta = 0;
-      base[h] = ne;
+      base[slot] = ne;
       out = ne;
-      res = base + h;
+      res = base + slot;
       act = false;
     }
-    h = (h + 1) & mask;
+    // on: onto the match, past a slot another leader took, or past the four
+    h = act ? (claim ? (slot + 1) & mask : q < 4u ? slot : (h + 4) & mask) : h;
   }
   return res;
 }
@@ -955,6 +996,82 @@ __device__ inline bool coll_add(const Ctx& c, CollEnt* e, uint32_t x, uint32_t* 
   blk[0] = n;
   if (seg && n > (uint32_t)c.seg_threshold) *seg = 1;
   return true;
+}
+// coll_add for a whole wave's run of adds to one collector (deliver_coop): the entry held in registers
+// while it stays inline, else its intervals staged in LDS — the same sequence of adds, results and
+// segmentation checks as coll_add one after another, without a dependent global round trip per add.
+// On an inline value: 1 added, 0 held already, -1 a second disjoint interval (the caller stages it).
+__device__ __forceinline__ int coll_add_inline(CollEnt& v, uint32_t x) {
+  if ((v.meta & 7u) == 0u) {
+    v.lo = v.hi = x;
+    v.meta = (v.meta & ~7u) | 1u;
+    return 1;
+  }
+  if (v.lo <= x && x <= v.hi) return 0;
+  if ((int64_t)x == (int64_t)v.hi + 1) { v.hi = x; return 1; }
+  if ((int64_t)x + 1 == (int64_t)v.lo) { v.lo = x; return 1; }
+  return -1;
+}
+// on n sorted, disjoint, non-adjacent intervals in LDS (room for at least n + 1): 1 added, 0 held
+__device__ inline int coll_add_lds(uint2* iv, uint32_t& n, uint32_t x, uint32_t* moved = nullptr) {
+  int lo = 0, hi = (int)n - 1, fl = -1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    if (iv[mid].x <= x) { fl = mid; lo = mid + 1; } else { hi = mid - 1; }
+  }
+  if (fl >= 0 && x <= iv[fl].y) return 0;
+  const int ce = fl + 1;
+  const bool nf = fl >= 0 && (int64_t)x - 1 == (int64_t)iv[fl].y;
+  const bool nc = ce < (int)n && (int64_t)x + 1 == (int64_t)iv[ce].x;
+  if (nf && nc) {
+    iv[fl].y = iv[ce].y;
+    for (uint32_t i = (uint32_t)ce; i + 1 < n; ++i) iv[i] = iv[i + 1];
+    if (moved) *moved += n - 1 - (uint32_t)ce;
+    n--;
+  } else if (nf) {
+    iv[fl].y = x;
+  } else if (nc) {
+    iv[ce].x = x;
+  } else {
+    for (uint32_t i = n; i > (uint32_t)ce; --i) iv[i] = iv[i - 1];
+    if (moved) *moved += n - (uint32_t)ce;
+    iv[ce] = make_uint2(x, x);
+    n++;
+  }
+  return 1;
+}
+// the staged intervals' home once the run is done (n after it, maxn the most it held): inline when one
+// interval is left; else the entry's block if its tier holds maxn, or a block of the smallest tier that
+// does (coll_add grows one tier at a time at each full insert: the same tier in the end; the old block
+// is released).  Returns the block to copy the intervals into (header written), or null (inline, or the
+// pool is dry: ERR_INTERVALS set by spill_alloc).  One lane.
+__device__ inline uint32_t* coll_place(const Ctx& c, CollEnt* e, uint32_t meta, uint32_t n, uint32_t maxn,
+                                       uint32_t lo0, uint32_t hi0) {
+  const bool spilled = (meta & 7u) == COLL_SPILLED;
+  if (n == 1) {  // (lo0, hi0): the one interval
+    e->lo = lo0;
+    e->hi = hi0;
+    if (spilled) spill_free(c, meta);
+    e->meta = (meta & COLL_CLEARED) | 1u;
+    return nullptr;
+  }
+  const int t0 = spilled ? (int)((meta >> 4) & 3u) : 0;
+  int t = t0;
+  while (t + 1 < NTIER && tier_cap(t) < maxn) ++t;
+  if (tier_cap(t) < maxn) { set_err(c, ERR_COLL_TOP); return nullptr; }
+  uint32_t* blk;
+  if (spilled && t == t0) {
+    blk = coll_block(c, meta);
+  } else {
+    const uint32_t i = spill_alloc(c, t);
+    if (i == NONE) return nullptr;
+    if (spilled) spill_free(c, meta);
+    meta = (meta & COLL_CLEARED) | COLL_SPILLED | ((uint32_t)t << 4) | (i << 8);
+    e->meta = meta;
+    blk = coll_block(c, meta);
+  }
+  blk[0] = n;
+  return blk;
 }
 // number of intervals (checkGossipSegmentation's size())
 __device__ inline uint32_t coll_size(const Ctx& c, const CollEnt* e) {
@@ -1384,11 +1501,11 @@ __device__ inline bool wait_end(const Ctx& c, uint32_t v, uint32_t to, uint32_t 
   m.w_link1 = 0;
   if (m.w_n == 0 && m.w_gp == 0 && m.w_ready <= (uint32_t)c.T) return false;
   const uint32_t i = v - c.lo, k = c.pa_n[i];
-  if (k >= PA_CAP) {
+  if (k >= c.pa_cap) {
     set_err(c, ERR_PACK);
     return true;
   }
-  c.pa[(size_t)i * PA_CAP + k] = PAck{to, flags, m.w_n, m.w_ready, m.w_gp, m.pack_seq};
+  c.pa[(size_t)i * c.pa_cap + k] = PAck{to, flags, m.w_n, m.w_ready, m.w_gp, m.pack_seq};
   c.pa_n[i] = k + 1;
   m.pack_seq++;
   if (flags & PA_INIT) m.init_pend++;
@@ -1397,8 +1514,8 @@ __device__ inline bool wait_end(const Ctx& c, uint32_t v, uint32_t to, uint32_t 
 }
 // the PAck of viewer v with sequence number seq (nullptr: none — a start0 group cancelled with its Flux)
 __device__ inline PAck* pack_find(const Ctx& c, uint32_t v, uint32_t seq) {
-  const uint32_t i = v - c.lo, k = min(c.pa_n[i], PA_CAP);
-  PAck* L = c.pa + (size_t)i * PA_CAP;
+  const uint32_t i = v - c.lo, k = min(c.pa_n[i], c.pa_cap);
+  PAck* L = c.pa + (size_t)i * c.pa_cap;
   for (uint32_t j = 0; j < k; ++j)
     if (L[j].seq == seq) return L + j;
   return nullptr;

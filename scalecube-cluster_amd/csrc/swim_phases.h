@@ -18,7 +18,7 @@ namespace swimdev {
 // Phase timing for profiling builds only (-DSWIM_PHASE_PROF, tools/phase_prof.sh): per-wave wall
 // time (s_memrealtime, 100 MHz) of the delivery kernel's parts, summed into g_dbg; read with
 // swim_debug_counters.  The product build compiles none of it.
-__device__ unsigned long long g_dbg[32];
+__device__ unsigned long long g_dbg[48];
 #ifdef SWIM_PHASE_PROF
 #define PPROF_T0(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
 #define PPROF_ADD(slot, t0)                                                                          \
@@ -845,10 +845,16 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
   for (uint32_t p0 = 0; p0 < glen; p0 += 64) {
     const uint32_t p = p0 + lane;
     bool sw = false;
+    GossipHot h{};
     if (p < glen) {
-      const GossipHot h = p0 == 0 ? h_head : slab.H(p);
+      h = p0 == 0 ? h_head : slab.H(p);
       sw = period > (uint64_t)h.inf_period() + sweep;
-      if (sw && h.more()) slab.drop_more(h.gossiper, h.seq);  // its infected overflow goes too
+    }
+    // its infected overflow goes too: one lane at a time (inf_erase moves entries of the table)
+    for (uint64_t dm = __ballot(sw && h.more()); dm; dm &= dm - 1) {
+      if (lane == (uint32_t)__ffsll((unsigned long long)dm) - 1) slab.drop_more(h.gossiper, h.seq);
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
     }
     const uint64_t km = __ballot(p < glen && !sw);
     if (km) {
@@ -1112,8 +1118,8 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
   // one wait share their infection period, so they complete together — in this round if it finds them
   // disseminated and the sweep has not dropped them (a swept gossip's Mono never completes)
   if (lane == 0 && sp.pw) {
-    const uint32_t i = v - c.lo, np = min(c.pa_n[i], PA_CAP);
-    PAck* L = c.pa + (size_t)i * PA_CAP;
+    const uint32_t i = v - c.lo, np = min(c.pa_n[i], c.pa_cap);
+    PAck* L = c.pa + (size_t)i * c.pa_cap;
     for (uint32_t k = 0; k < np; ++k) {
       const uint32_t gp = L[k].gp;
       if (gp && period > (uint64_t)(gp - 1) + spread && !(period > (uint64_t)(gp - 1) + sweep)) {
@@ -1538,14 +1544,17 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, con
   } else {
     GossipDev st = slab.get((uint32_t)found);
     if (!gossip_infected(st, g.from)) {
-      int k = 0;
-      while (k < GINF && st.inf[k] != NONE) ++k;
-      if (k < GINF) {
-        st.inf[k] = g.from;
-        slab.put((uint32_t)found, st);
-      } else {
-        set_err(c, ERR_INFECTED);
+      // the first free slot, written through an unrolled select: a runtime index would put the
+      // whole array in scratch
+      bool put = false;
+#pragma unroll
+      for (int k = 0; k < GINF; ++k) {
+        const bool here = !put && st.inf[k] == NONE;
+        st.inf[k] = here ? g.from : st.inf[k];
+        put |= here;
       }
+      if (put) slab.put((uint32_t)found, st);
+      else set_err(c, ERR_INFECTED);
     }
   }
   return true;
@@ -1675,6 +1684,7 @@ struct BigLds {  // per wave
   uint32_t snd[BIG_MAXD];  // distinct senders (found order, then ascending)
   uint32_t cnt[BIG_MAXD];  // their message counts, then running inbox bases
   uint32_t iP[64], iS[64], iR[64];  // apply_ins_batch scratch
+  uint32_t perm[64];  // an inbox of at most 64 messages ranked for the whole-wave delivery: rank -> slot
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -1701,7 +1711,10 @@ __device__ __forceinline__ int big_find(const uint32_t* snd, uint32_t nd, uint32
 // of the batch run side by side, each touching only its own receiver's state — then, receiver by
 // receiver, the inbox pages go back, the pingMembers inserts of the phase run and the SYNC
 // collection follows.
-__device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L) {
+// lds_perm: an inbox of at most 64 messages keeps its permutation in L.perm instead of pg_perm (the
+// whole-wave delivery reads it from there: no dependent global round trip before its messages).
+__device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L,
+                                   bool lds_perm = false) {
   const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
   auto msg_at = [&](uint32_t q) -> const GMsgFull& { return b.pg_msgs[(size_t)pt[q >> 6] * 64 + (q & 63)]; };
   auto perm_at = [&](uint32_t q) -> uint32_t& { return b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)]; };
@@ -1771,6 +1784,8 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
       uint32_t acc0 = 0;
       for (uint32_t x = 0; x < nd; ++x) { const uint32_t t = L.cnt[x]; L.cnt[x] = acc0; acc0 += t; }
     }
+    lds_perm = lds_perm && k <= 64u;
+    if (lds_perm) L.perm[lane] = NONE;  // (a rank left unwritten is a hole, as in pg_perm)
     wave_sync();
     // pass 2: rank = base of the sender + the message's pseq (dense per (sender, receiver))
     for (uint32_t q0 = 0; q0 < k; q0 += 64) {
@@ -1786,7 +1801,10 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
         const uint32_t sf = rdlane(f, (uint32_t)__ffsll((unsigned long long)todo) - 1);
         const uint64_t same = __ballot(f == sf) & todo;
         const uint32_t at = L.cnt[big_find(L.snd, nd, sf, lane)] + ps;
-        if (((same >> lane) & 1ull) && at < k) perm_at(at) = q;
+        if (((same >> lane) & 1ull) && at < k) {
+          if (lds_perm) L.perm[at] = q;
+          else perm_at(at) = q;
+        }
         todo &= ~same;
       }
     }
@@ -1813,9 +1831,16 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
 //      the no-op lanes between them take the next positions and write their states together.
 // Returns this lane's share of the accepted messages; nfresh counts those not flagged as provable
 // duplicates (per lane as well).
+#ifndef COOP_STAGE
+#define COOP_STAGE 1  // spilled collectors' adds staged in LDS (0: coll_add one by one, for A/B)
+#endif
+#ifndef COOP_PIPE
+#define COOP_PIPE 1  // the chunk pipeline below (0: the next chunk's loads waited on at its start)
+#endif
+constexpr uint32_t COOP_LIV = 2048;  // intervals of one collector staged in LDS per wave (16 KB)
 constexpr uint32_t COOP_MIN = 16;  // Bufs.coop_min's default (every big inbox: measured best, 16 / 32 / 64)
 __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L,
-                                           uint32_t& nfresh) {
+                                           uint2* siv, uint32_t& nfresh) {
   const uint32_t r = c.lo + i;
   const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
   MemberDev& m = mem(c, r);
@@ -1829,22 +1854,38 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
   const uint32_t period = gsr.period;
   if (lane == 0 && period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
   unsigned long long acc = 0;
-  // rank q's message (the next chunk's is loaded while a chunk is processed, with its collector slot)
-  auto load_msg = [&](uint32_t q) -> GMsgFull {
-    GMsgFull x{};
-    if (q < k) {
-      uint32_t jq = b.pg_perm[(size_t)pt[q >> 6] * 64 + (q & 63)];
-      if (jq >= k) {  // a hole: only after an inbox overflow (ERR_MSGS is set)
-        set_err(c, ERR_MSGS);
-        jq = q;
-      }
-      x = b.pg_msgs[(size_t)pt[jq >> 6] * 64 + (jq & 63)];
+  // The messages in rank order, pipelined across chunks: a chunk's messages are loaded at the start
+  // of the chunk before it, their slots (pg_perm) one chunk earlier still, and the first 64 page ids
+  // are held one per lane — so a chunk waits on no dependent load of its own.  An inbox of one page
+  // has its permutation in LDS (rank_big_inbox).
+  const bool one_page = k <= 64u;
+  const uint32_t npg = (k + 63) / 64;
+  const uint32_t ptl = lane < npg ? gload(pt + lane) : 0u;
+  const uint32_t pg0 = rdlane(ptl, 0);
+  auto slot_of = [&](uint32_t q) -> uint32_t {  // rank q's slot; (q >> 6) is the same on every lane
+    if (one_page) return q < k ? L.perm[q] : NONE;
+    const uint32_t pgi = __builtin_amdgcn_readfirstlane(q >> 6);
+    const uint32_t pg = pgi < 64u ? rdlane(ptl, pgi) : __builtin_amdgcn_readfirstlane(gload(pt + pgi));
+    return q < k ? gload(b.pg_perm + (size_t)pg * 64 + (q & 63)) : NONE;
+  };
+  auto msg_at = [&](uint32_t q, uint32_t jq) -> GMsgFull {  // (every lane calls it: the page shuffle)
+    const bool ok = q < k;
+    if (ok && jq >= k) {  // a hole: only after an inbox overflow (ERR_MSGS is set)
+      set_err(c, ERR_MSGS);
+      jq = q;
     }
+    const uint32_t pgi = ok ? jq >> 6 : 0u;
+    const uint32_t viaL = (uint32_t)__shfl((int)ptl, (int)(pgi & 63u), 64);
+    GMsgFull x{};
+    if (ok) x = b.pg_msgs[(size_t)(one_page ? pg0 : pgi < 64u ? viaL : gload(pt + pgi)) * 64 + (jq & 63)];
     return x;
   };
   const CollEnt* cbase = c.coll + (size_t)i * c.hcap;
   uint32_t sink = 0;
-  GMsgFull gn = load_msg(lane);
+  GMsgFull gn = msg_at(lane, slot_of(lane));
+#if COOP_PIPE
+  uint32_t jn = k > 64u ? slot_of(64u + lane) : NONE;  // the next chunk's slots
+#endif
   wave_sync();
   for (uint32_t r0 = 0; r0 < k; r0 += 64) {
     PPROF_T0(tca);
@@ -1852,16 +1893,25 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
     const GMsgFull g = gn;
     const bool valid = q < k && !g.dup();
     nfresh += valid ? 1u : 0u;
-    if (r0 + 64 < k) {
-      gn = load_msg(q + 64);
+    const bool more = r0 + 64 < k;
+    if (more) {
+#if COOP_PIPE
+      gn = msg_at(q + 64, jn);
+      jn = r0 + 128 < k ? slot_of(q + 128) : NONE;
+#else
+      gn = msg_at(q + 64, slot_of(q + 64));
       if (q + 64 < k) sink ^= cbase[hash32(gn.gossiper) & (c.hcap - 1)].key;
+#endif
     }
     // (a) one leader per gossiper
     const bool coop = valid && g.gossiper != r;
     L.iP[lane] = g.seq;
     L.iS[lane] = 0;  // 1: accepted, 2: onGossipReq at its turn
     uint64_t grp = 0;
-    for (uint64_t todo = __ballot(coop); todo;) {
+    const uint64_t coopm = __ballot(coop);
+    PPROF_ADD(29, tca);
+    PPROF_T0(tcg);
+    for (uint64_t todo = coopm; todo;) {
       const int l = __ffsll((unsigned long long)todo) - 1;
       const uint32_t gl = rdlane(g.gossiper, (uint32_t)l);
       const uint64_t same = __ballot(coop && g.gossiper == gl) & todo;
@@ -1869,22 +1919,179 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
       todo &= ~same;
     }
     wave_sync();
+    PPROF_ADD(26, tcg);
     {
+      PPROF_T0(tce);
       CollEnt cv;
+#ifdef SWIM_PHASE_PROF
+      uint32_t probes = 0;
+      CollEnt* col = coll_ensure_wave(c, r, grp != 0, g.gossiper, lane, cv, &probes);
+      PPROF_CNT(31, (unsigned long long)probes);  // probe rounds of the wave
+#else
       CollEnt* col = coll_ensure_wave(c, r, grp != 0, g.gossiper, lane, cv);
+#endif
+      PPROF_ADD(27, tce);
+      PPROF_CNT(30, (unsigned long long)__popcll(__ballot(grp != 0)));  // leaders
+      // inline collectors: each leader runs its adds in registers (one store at the end); a run that
+      // needs a second interval, and every spilled collector, goes on to the staged pass with the
+      // lanes it has left (rest)
+      uint64_t rest = 0;
       if (col && (cv.meta & COLL_CLEARED)) {
         for (uint64_t mm = grp; mm; mm &= mm - 1) L.iS[__ffsll((unsigned long long)mm) - 1] = 2;
+      } else if (col && (cv.meta & 7u) == COLL_SPILLED) {
+        rest = grp;
       } else if (col) {
-        bool first = true;
+        const CollEnt v0 = cv;
         for (uint64_t mm = grp; mm; mm &= mm - 1) {
           const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
-          const bool ok = coll_add(c, col, L.iP[j], &c.seg_flag[i], first ? &cv : nullptr);
-          first = false;
-          L.iS[j] = ok ? 1u : 0u;
+          const int a = coll_add_inline(cv, L.iP[j]);
+          if (a < 0) {
+            rest = mm;
+            break;
+          }
+          L.iS[j] = (uint32_t)a;
         }
+        if (!rest && (cv.lo != v0.lo || cv.hi != v0.hi || cv.meta != v0.meta)) *col = cv;
       }
+      wave_sync();
+      // the staged pass, one collector at a time with the whole wave: its intervals into LDS, the
+      // leader's adds there, the result back (coll_place)
+      for (uint64_t lm = __ballot(rest != 0); lm; lm &= lm - 1) {
+        const uint32_t l = (uint32_t)__ffsll((unsigned long long)lm) - 1;
+        const uint64_t rm = rdlane64(rest, l);
+        CollEnt* e = reinterpret_cast<CollEnt*>(rdlane64(reinterpret_cast<uint64_t>(col), l));
+        const uint32_t meta = rdlane(cv.meta, l);
+        const bool spilled = (meta & 7u) == COLL_SPILLED;
+        const uint32_t* blk = spilled ? coll_block(c, meta) : nullptr;
+        const uint32_t n0 = spilled ? rdlane(gload(blk), 0) : 1u;
+        if (COOP_STAGE && n0 + (uint32_t)__popcll(rm) <= 64u) {
+          // small collectors (nearly all): interval q in lane q's registers, each add a ballot for
+          // its floor, register reads of the neighbours and a one-lane shift across the wave
+          PPROF_T0(tsr);
+          uint32_t vlo = 0, vhi = 0;
+          if (spilled) {
+            if (lane < n0) {
+              const uint2 t = gload(reinterpret_cast<const uint2*>(blk + 4) + lane);
+              vlo = t.x;
+              vhi = t.y;
+            }
+          } else if (lane == 0) {
+            vlo = rdlane(cv.lo, l);
+            vhi = rdlane(cv.hi, l);
+          }
+          uint32_t n = n0, maxn = n0, res = 0;
+          bool seg = false;
+          for (uint64_t mm = rm; mm; mm &= mm - 1) {
+            const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
+            const uint32_t x = rdlane(g.seq, j);
+            const uint64_t le = __ballot(lane < n && vlo <= x);
+            const int fl = le ? 63 - __clzll((long long)le) : -1;
+            const uint32_t fhi = rdlane(vhi, fl < 0 ? 0u : (uint32_t)fl);
+            if (fl >= 0 && x <= fhi) continue;  // held already (res stays 0)
+            const uint32_t ce = (uint32_t)(fl + 1);
+            const uint32_t clo = rdlane(vlo, ce < n ? ce : 0u), chi = rdlane(vhi, ce < n ? ce : 0u);
+            const bool nf = fl >= 0 && (int64_t)x - 1 == (int64_t)fhi;
+            const bool nc = ce < n && (int64_t)x + 1 == (int64_t)clo;
+            if (nf && nc) {  // x joins its two neighbours: the lanes after ce move down one
+              const uint32_t dlo = (uint32_t)__shfl_down((int)vlo, 1, 64), dhi = (uint32_t)__shfl_down((int)vhi, 1, 64);
+              if (lane == (uint32_t)fl) vhi = chi;
+              if (lane >= ce) { vlo = dlo; vhi = dhi; }
+              n--;
+            } else if (nf) {
+              if (lane == (uint32_t)fl) vhi = x;
+            } else if (nc) {
+              if (lane == ce) vlo = x;
+            } else {  // a new interval at ce: the lanes from ce on move up one
+              const uint32_t ulo = (uint32_t)__shfl_up((int)vlo, 1, 64), uhi = (uint32_t)__shfl_up((int)vhi, 1, 64);
+              if (lane > ce) { vlo = ulo; vhi = uhi; }
+              if (lane == ce) { vlo = x; vhi = x; }
+              n++;
+            }
+            if (lane == j) res = 1;
+            seg |= n >= 2 && n > (uint32_t)c.seg_threshold;
+            maxn = max(maxn, n);
+          }
+          if ((rm >> lane) & 1ull) L.iS[lane] = res;
+          uint32_t* dst = nullptr;
+          if (lane == l) {
+            if (seg) c.seg_flag[i] = 1;
+            dst = coll_place(c, e, meta, n, maxn, rdlane(vlo, 0), rdlane(vhi, 0));
+          }
+          dst = reinterpret_cast<uint32_t*>(rdlane64(reinterpret_cast<uint64_t>(dst), l));
+          if (dst && lane < n) reinterpret_cast<uint2*>(dst + 4)[lane] = make_uint2(vlo, vhi);
+          wave_sync();
+          PPROF_ADD(38, tsr);
+          PPROF_CNT(39, 1ull);
+          continue;
+        }
+        if (!COOP_STAGE || n0 + (uint32_t)__popcll(rm) > COOP_LIV) {  // beyond the staging area: coll_add one by one
+          if (lane == l) {
+            if (!spilled) *e = cv;
+            for (uint64_t mm = rm; mm; mm &= mm - 1) {
+              const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
+              L.iS[j] = coll_add(c, e, L.iP[j], &c.seg_flag[i]) ? 1u : 0u;
+            }
+          }
+          wave_sync();
+          continue;
+        }
+        PPROF_T0(tsi);
+        PPROF_CNT(35, 1ull);
+        PPROF_CNT(36, (unsigned long long)n0);
+        if (spilled) {
+          const uint2* giv = reinterpret_cast<const uint2*>(blk + 4);
+          for (uint32_t q2 = lane; q2 < n0; q2 += 64) siv[q2] = gload(giv + q2);
+        } else if (lane == 0) {
+          siv[0] = make_uint2(rdlane(cv.lo, l), rdlane(cv.hi, l));
+        }
+        wave_sync();
+        PPROF_ADD(32, tsi);
+        PPROF_T0(tsa);
+        uint32_t n = n0;
+        uint32_t* dst = nullptr;
+#ifdef SWIM_PHASE_PROF
+        uint32_t moved = 0;
+#endif
+        if (lane == l) {
+          uint32_t maxn = n;
+          bool seg = false;
+          for (uint64_t mm = rm; mm; mm &= mm - 1) {
+            const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
+#ifdef SWIM_PHASE_PROF
+            const int a = coll_add_lds(siv, n, L.iP[j], &moved);
+#else
+            const int a = coll_add_lds(siv, n, L.iP[j]);
+#endif
+            L.iS[j] = (uint32_t)a;
+            seg |= a && n >= 2 && n > (uint32_t)c.seg_threshold;
+            maxn = max(maxn, n);
+          }
+          if (seg) c.seg_flag[i] = 1;
+          dst = coll_place(c, e, meta, n, maxn, siv[0].x, siv[0].y);
+        }
+#ifdef SWIM_PHASE_PROF
+        PPROF_CNT(37, (unsigned long long)rdlane(moved, l));
+#endif
+        PPROF_ADD(33, tsa);
+        PPROF_T0(tsw);
+        n = rdlane(n, l);
+        dst = reinterpret_cast<uint32_t*>(rdlane64(reinterpret_cast<uint64_t>(dst), l));
+        if (dst) {
+          uint2* div = reinterpret_cast<uint2*>(dst + 4);
+          for (uint32_t q2 = lane; q2 < n; q2 += 64) div[q2] = siv[q2];
+        }
+        wave_sync();
+        PPROF_ADD(34, tsw);
+      }
+      PPROF_ADD(28, tce);
     }
     wave_sync();
+    // the next chunk's collector slots, warmed while (b) and (c) run (its messages are in by now)
+#if COOP_PIPE
+    const uint32_t warm = more && q + 64 < k ? cbase[hash32(gn.gossiper) & (c.hcap - 1)].key : 0u;
+#else
+    const uint32_t warm = 0u;
+#endif
     PPROF_ADD(13, tca);
     PPROF_T0(tcb);
     const uint32_t fl = L.iS[lane];
@@ -1980,6 +2187,7 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
     PPROF_ADD(15, tcc);
     acc += (accepted ? 1ull : 0ull) + fullacc;  // (per lane: the caller sums the wave)
     if (lane == 0) gsr.len = len;
+    sink ^= warm;
     wave_sync();
   }
   if (sink == 0x5bd1e995u && k == 0x7fffffffu) set_err(c, 0u);  // keeps the warming loads; sets no bit
@@ -1998,6 +2206,7 @@ __global__ void __launch_bounds__(DLV_BLOCK, COOP_OCC) k_deliver_coop(KP, unsign
   const Ctx c = pctx(P, T);
   const Bufs b = P->b;
   __shared__ BigLds s_big[DLV_WAVES];
+  __shared__ uint2 s_iv[DLV_WAVES][COOP_LIV];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   unsigned long long acc = 0;
   uint32_t nmsg = 0, nfresh = 0;
@@ -2015,9 +2224,9 @@ __global__ void __launch_bounds__(DLV_BLOCK, COOP_OCC) k_deliver_coop(KP, unsign
       wave_sync();
       if (lane == 0) b.msg_cnt[i] = 0;
       if (c.up[r] && pages_ok) {
-        rank_big_inbox(c, b, i, k, lane, s_big[wv]);
+        rank_big_inbox(c, b, i, k, lane, s_big[wv], true);
         nmsg += lane == 0 ? k : 0u;
-        acc += deliver_coop(c, b, i, k, lane, s_big[wv], nfresh);
+        acc += deliver_coop(c, b, i, k, lane, s_big[wv], s_iv[wv], nfresh);
       }
       wave_sync();
       for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) pt[pg] = NONE;
@@ -2583,8 +2792,8 @@ __device__ inline unsigned long long sync_collect_fast(const Ctx& c, const Bufs&
 // into in the SYNC_ACK sub-phase; no lone-SYNC_ACK shortcut for another ack it gets), on another
 // shard through an E2 marker.  Oracle: phase_sync's collection.
 __device__ inline void pack_inject(const Ctx& c, const Bufs& b, uint32_t v) {
-  const uint32_t i = v - c.lo, n = min(c.pa_n[i], PA_CAP), t32 = (uint32_t)c.T;
-  PAck* L = c.pa + (size_t)i * PA_CAP;
+  const uint32_t i = v - c.lo, n = min(c.pa_n[i], c.pa_cap), t32 = (uint32_t)c.T;
+  PAck* L = c.pa + (size_t)i * c.pa_cap;
   MemberDev& m = mem(c, v);
   uint32_t w = 0;
   for (uint32_t k = 0; k < n; ++k) {
@@ -2905,8 +3114,8 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
     } else if (c.T + 1 >= last + c.sync_to_ticks) {
       start = (int64_t)(last + c.sync_to_ticks);
       if (m.init_pend) {  // the start0 groups are cancelled
-        PAck* L = c.pa + (size_t)i * PA_CAP;
-        const uint32_t n = min(c.pa_n[i], PA_CAP);
+        PAck* L = c.pa + (size_t)i * c.pa_cap;
+        const uint32_t n = min(c.pa_n[i], c.pa_cap);
         uint32_t w = 0;
         for (uint32_t k = 0; k < n; ++k)
           if (!(L[k].flags & PA_INIT)) L[w++] = L[k];

@@ -52,13 +52,22 @@ def run(sc, members=None, collectors=True, threads=1):
 
 
 def main():
+    # python tests/golden/make_scenario_digests.py [NAME ...]: only the named scenarios are (re)made,
+    # the others' digests kept (a new scenario; the whole catalogue takes several minutes)
+    only = set(sys.argv[1:])
+    path = os.path.join(HERE, "scenario_digests.json")
     out = {"source": "tests/golden/make_scenario_digests.py (CPU oracle)", "scenarios": {}}
+    if only:
+        out["scenarios"] = json.load(open(path))["scenarios"]
     for sc in scenarios.catalog():
+        if only and sc.name not in only:
+            continue
         out["scenarios"][sc.name] = run(sc)
         print(sc.name, out["scenarios"][sc.name]["events"], "events")
     sc = scenarios.config2()
-    out["scenarios"][sc.name] = run(sc, members=scenarios.CONFIG2_MEMBERS, collectors=False)
-    with open(os.path.join(HERE, "scenario_digests.json"), "w") as f:
+    if not only or sc.name in only:
+        out["scenarios"][sc.name] = run(sc, members=scenarios.CONFIG2_MEMBERS, collectors=False)
+    with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 
 

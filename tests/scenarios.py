@@ -300,6 +300,16 @@ def catalog() -> list[Scenario]:
                       (70, "join", 17), (90, "member_seeds", 13, [2]), (91, "member_seeds", 13, None),
                       (91, "join", 13), (120, "member_seeds", 1, [17]), (200, "join", 14)],
                  check_every=20),
+        # a join burst under message delay: 160 members join through one seed at once, and each
+        # joiner's first SYNC_ACK admits the whole table through delayed GET_METADATA round trips
+        # (46 K round trips in 25 ticks, several thousand in flight together, beyond the delayed-fetch queue's base capacity of 4,096: the
+        # engine grows it before the joins' tick, grow_for_joins) — and the seed holds the 160
+        # joiners' SYNC_ACKs at once while their admission fetches run (pending acks beyond the base 64)
+        Scenario("join_burst_delay_256", 256, 96, 30, seed=32, seeds=(0,),
+                 cfg=dict(sync_interval=3000, sync_timeout=1000, ping_interval=1000, ping_timeout=500,
+                          metadata_timeout=1000, delay_capacity=1 << 20, gossip_capacity=8192),
+                 ops=[(0, "default_delay", 200, ALL_)] + [(5, "join", m) for m in range(96, 256)],
+                 check_every=10),
         # 2-way partition held past the suspicion timeout, heal via SYNC through seeds (config 5 in miniature)
         Scenario("partition_heal_32", 32, 32, 1600, seed=14, seeds=(0, 16),
                  cfg=dict(sync_interval=5000), ops=[(100, "partition", _partition(32, 16)), (1100, "partition", None)],

@@ -44,7 +44,7 @@ def main():
     sch.run(e, args.warmup, args.warmup + args.steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    d = abi.debug_counters(lib)
+    d = abi.debug_counters(lib, 48)
     dp = e.profile_deliver()
     launches = args.steps * 5  # gossip rounds in the window
     waves = 512 * 4  # DLV_GRID x DLV_WAVES
@@ -58,7 +58,19 @@ def main():
                       "ogr_update_us": per(d[9]),
                       # whole-wave delivery (deliver_coop) per chunk: (a) loads + collectors,
                       # (b) receipts + no-op test, (c) the serial steps and state writes
-                      "coop_a_us": per(d[13]), "coop_b_us": per(d[14]), "coop_c_us": per(d[15]),
+                      "coop_a_us": per(d[13]),
+                      # (a)'s parts: message loads wait, gossiper grouping, coll_ensure_wave,
+                      # ensure + coll_add loop; leaders (distinct gossipers) per launch
+                      "coop_a_msgwait_us": per(d[29]), "coop_a_group_us": per(d[26]),
+                      "coop_a_ensure_us": per(d[27]), "coop_a_ensure_add_us": per(d[28]),
+                      "coop_leaders": d[30] / launches, "coop_probe_rounds": d[31] / launches,
+                      # the staged collector pass: stage-in, the leader's adds, the copy back; staged
+                      # collectors, their intervals and the intervals the adds shifted, per launch
+                      "stage_in_us": per(d[32]), "stage_adds_us": per(d[33]), "stage_out_us": per(d[34]),
+                      "staged": d[35] / launches, "staged_intervals": d[36] / launches,
+                      "staged_shifted": d[37] / launches,
+                      # small collectors (<= 64 intervals) in registers: time, count
+                      "reg_pass_us": per(d[38]), "reg_staged": d[39] / launches, "coop_b_us": per(d[14]), "coop_c_us": per(d[15]),
                       "longest_chain_msgs": d[10], "chain_msgs_per_launch": d[11] / launches,
                       "sum_of_wave_longest_chains": d[12] / launches,
                       "messages_per_launch": dp["messages"] / max(1, dp["launches"])}))
