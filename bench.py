@@ -169,10 +169,11 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def side_run(lib, workload, n, warmup, steps, device=0, quiet=True, **knobs):
+def side_run(lib, workload, n, warmup, steps, device=0, quiet=True, period_times=None, **knobs):
     """A secondary single-GPU measurement on its own engine (the headline engine is closed first):
     `warmup` untimed periods, then `steps` timed ones.  Returns (seconds, merge profile, fanout
-    profile, stats, deliver profile, quiet-window stats)."""
+    profile, stats, deliver profile, quiet-window stats).  period_times (a list): each timed period's
+    seconds are appended (a synchronisation after each; for workloads whose periods take seconds)."""
     import torch
     from swimgpu import abi
     sch = Schedule(workload, n, warmup + steps)
@@ -191,7 +192,14 @@ def side_run(lib, workload, n, warmup, steps, device=0, quiet=True, **knobs):
         e.profile_enable(True)
         q0 = e.quiet_stats()
         t0 = time.perf_counter()
-        sch.run(e, warmup, warmup + steps)
+        if period_times is None:
+            sch.run(e, warmup, warmup + steps)
+        else:
+            for p in range(warmup, warmup + steps):
+                tp = time.perf_counter()
+                sch.run(e, p, p + 1)
+                torch.cuda.synchronize()
+                period_times.append(time.perf_counter() - tp)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         q1 = e.quiet_stats()
@@ -604,7 +612,8 @@ def main():
                   "must agree with them; PMC passes give traffic only (their durations include counter overhead)",
         "roofline": None,
         "quiet_windows": {"ticks": qst["ticks"], "windows": qst["windows"], "attempts": qst["attempts"],
-                          "cut_short": qst["cut_short"], "timed_ticks": ticks},
+                          "cut_short": qst["cut_short"], "precomputed": qst.get("precomputed", 0),
+                          "timed_ticks": ticks},
         "stats": {k: stats[k] for k in ("syncs", "sync_records", "gossip_messages", "gossips_created", "pings",
                                          "timers_fired", "events")},
     }
@@ -653,9 +662,14 @@ def main():
         # re-gossip storm grows every period)
         if not args.no_churn:
             cs = args.churn_steps
-            c_dt, _, _, c_st, _, _ = side_run(lib, "churn", DEFAULT_MEMBERS["churn"], 1, cs, local_rank)
+            c_pt = []
+            c_dt, _, _, c_st, _, _ = side_run(lib, "churn", DEFAULT_MEMBERS["churn"], 1, cs, local_rank,
+                                              period_times=c_pt)
             line["churn"] = {"value": DEFAULT_MEMBERS["churn"] * cs / c_dt, "unit": "member-periods/s",
                              "ms_per_step": c_dt * 1e3 / cs, "steps": cs, "warmup": 1,
+                             # each timed period (1, 2, ...): the storm grows every period, so the CPU
+                             # baseline below (period 1 on the oracle) compares with period 1 only
+                             "ms_per_period": [round(t * 1e3, 3) for t in c_pt],
                              "config": WORKLOAD_TEXT["churn"].format(n=DEFAULT_MEMBERS["churn"],
                                                                      churn=DEFAULT_MEMBERS["churn"] * CHURN_PER_MILLE // 1000,
                                                                      loss=CHURN_LOSS),
@@ -679,6 +693,9 @@ def main():
         line["cpu_baseline"] = cpu_baseline(n, args.warmup, min(cpu_periods, args.steps))
         if "churn" in line:  # config 3's first timed period on the oracle, all cores (the GPU side run's period 1)
             line["churn"]["cpu_baseline"] = cpu_baseline(DEFAULT_MEMBERS["churn"], 1, 1, "churn", single=False)
+            if line["churn"].get("ms_per_period"):  # the same period on the GPU
+                line["churn"]["cpu_baseline"]["gpu_same_period_value"] = (
+                    DEFAULT_MEMBERS["churn"] / (line["churn"]["ms_per_period"][0] / 1e3))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -455,6 +455,7 @@ typedef struct swim_quiet_stats {
   uint64_t windows;    /* windows that advanced at least one tick */
   uint64_t attempts;   /* windows tried (a scan that found the cluster not quiet advances none) */
   uint64_t cut_short;  /* windows that ended before their length at a tick needing the per-tick chain */
+  uint64_t precomputed; /* windows whose end the previous window's apply had found (no scan launch) */
 } swim_quiet_stats;
 int32_t swim_get_quiet_stats(const swim_engine* e, swim_quiet_stats* out);
 /* The quiet windows' kernels (k_quiet_scan .. k_quiet_apply of one window, HIP events on the engine's

@@ -1831,6 +1831,14 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
 //      the no-op lanes between them take the next positions and write their states together.
 // Returns this lane's share of the accepted messages; nfresh counts those not flagged as provable
 // duplicates (per lane as well).
+// lane i gets lane i + 1's / i - 1's value (DPP wave_shl:1 / wave_shr:1, GFX9: one VALU op across the
+// whole wave, no LDS crossbar round trip); the lane at the end keeps its own
+__device__ __forceinline__ uint32_t wave_from_next(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_from_prev(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xf, 0xf, false);
+}
 #ifndef COOP_STAGE
 #define COOP_STAGE 1  // spilled collectors' adds staged in LDS (0: coll_add one by one, for A/B)
 #endif
@@ -1993,7 +2001,7 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
             const bool nf = fl >= 0 && (int64_t)x - 1 == (int64_t)fhi;
             const bool nc = ce < n && (int64_t)x + 1 == (int64_t)clo;
             if (nf && nc) {  // x joins its two neighbours: the lanes after ce move down one
-              const uint32_t dlo = (uint32_t)__shfl_down((int)vlo, 1, 64), dhi = (uint32_t)__shfl_down((int)vhi, 1, 64);
+              const uint32_t dlo = wave_from_next(vlo), dhi = wave_from_next(vhi);
               if (lane == (uint32_t)fl) vhi = chi;
               if (lane >= ce) { vlo = dlo; vhi = dhi; }
               n--;
@@ -2002,7 +2010,7 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
             } else if (nc) {
               if (lane == ce) vlo = x;
             } else {  // a new interval at ce: the lanes from ce on move up one
-              const uint32_t ulo = (uint32_t)__shfl_up((int)vlo, 1, 64), uhi = (uint32_t)__shfl_up((int)vhi, 1, 64);
+              const uint32_t ulo = wave_from_prev(vlo), uhi = wave_from_prev(vhi);
               if (lane > ce) { vlo = ulo; vhi = uhi; }
               if (lane == ce) { vlo = x; vhi = x; }
               n++;

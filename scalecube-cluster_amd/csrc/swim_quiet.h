@@ -210,16 +210,39 @@ __device__ inline void quiet_sync(const Ctx& c0, uint32_t v, uint64_t t, uint32_
   nrec += tsz;                                        // onSyncAck (:385-391): the acker's records
 }
 
-// k_quiet_apply: every owned member advanced through ticks [T, T + F), F = quiet_window(q).  `done`
-// (pinned host memory) receives F; `next` is the other control block, reset here for the next window
-// (windows alternate between the two, so no copy precedes a scan).  Thread 0 of workgroup 0 also
+// The next window's scan, precomputed (QuietPre).  On a pristine cluster the scan's only per-window
+// results are the first tick some member's ping list must be reshuffled and the first non-empty timer
+// bucket; everything else it checks (flags, witness counts, ref, table sizes) no quiet window changes.
+// So the apply that ends window k, whose threads hold every member's new schedule, also finds window
+// k + 1's first failing tick for up to H ticks past its end, and window k + 1 — when nothing but
+// windows ran in between (the host's pre_valid: every other API call and every per-tick tick clears
+// it) — launches no scan.  The result is a tagged minimum, key = (~tag << 32) | offset, so a newer
+// window's keys win over stale ones with no reset between windows; apply k's thread 0 writes the
+// sentinel (tag, no failure) so that the tag is always present.
+__device__ __forceinline__ uint64_t pre_key(uint32_t tag, uint32_t off) {
+  return ((uint64_t)(0xffffffffu - tag) << 32) | off;
+}
+
+// k_quiet_apply: every owned member advanced through ticks [T, T + F), F = quiet_window(q) — or, when
+// q is null, the window precomputed by the previous apply (pre_in, tag_in; a missing tag gives F = 0).
+// `done` (pinned host memory) receives F; `next` is the other control block, reset here for the next
+// scanned window (windows alternate between the two, so no copy precedes a scan).  H > 0: the next
+// window is precomputed into pre_out under tag_out (pristine engines).  Thread 0 of workgroup 0 also
 // performs the end-of-tick resets the skipped k_end_tick launches would have made (per-parity scratch
 // counters, the witness rebase's dirty marks: with every up row equal to ref a rebase moves no
 // reference record).
 __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const QuietCtl* q, QuietCtl* next,
-                                                     uint32_t* done, uint32_t rebase_every) {
+                                                     uint32_t* done, uint32_t rebase_every, const uint64_t* pre_in,
+                                                     uint32_t tag_in, uint64_t* pre_out, uint32_t tag_out,
+                                                     uint32_t H) {
   const Ctx c = pctx(P, T);
-  const uint32_t F = quiet_window(q, K);
+  uint32_t F;
+  if (q) {
+    F = quiet_window(q, K);
+  } else {
+    const uint64_t key = *pre_in;
+    F = (uint32_t)(key >> 32) == 0xffffffffu - tag_in ? min((uint32_t)key, K) : 0u;
+  }
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
   if (gtid == 0) {
     *done = F;
@@ -227,6 +250,16 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
   }
   if (F == 0) return;
   const uint64_t Tend = T + F;
+  uint32_t nfail = H;  // this thread's share of the next window's first failing offset (from Tend)
+  if (H) {
+    if (gtid == 0) atomicMin(reinterpret_cast<unsigned long long*>(pre_out), pre_key(tag_out, 0xffffffffu));
+    // the timer buckets of the next window (k_quiet_scan's check)
+    const uint32_t W = c.wheel_mask + 1, nwq = min(H, W) * c.wheel_nq;
+    for (uint32_t x = gtid; x < nwq; x += gsz) {
+      const uint32_t wj = x / c.wheel_nq;
+      if (c.wheel_cnt[(size_t)((Tend + wj) & c.wheel_mask) * c.wheel_nq + (x - wj * c.wheel_nq)]) nfail = min(nfail, wj);
+    }
+  }
   if (gtid == 0) {
     const Bufs& b = P->b;
     b.snap_cnt[0] = b.snap_cnt[1] = 0;
@@ -269,6 +302,20 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
         if (up) quiet_sync(c, v, sn, qm.table_size, nsync, nack, nrec);
       c.sync_next[i] = sn;
     }
+    // ---- the next window (quiet_member_scan with every target pingable): the member's ping list
+    // reaches its end — the ping that would reshuffle it
+    if (H && up) {
+      const uint32_t fdn1 = fdn < Tend ? fdn + ((uint32_t)((Tend - 1 - fdn) / c.P) + 1) * c.P : fdn;
+      const uint32_t cur1 = fdn < Tend && qm.ping_len ? qm.ping_cursor + (uint32_t)((Tend - 1 - fdn) / c.P) + 1
+                                                      : qm.ping_cursor;
+      nfail = min(nfail, quiet_member_scan(c, v, Tend, H, cur1, qm.ping_len, fdn1, true, nullptr, true));
+    }
+  }
+  if (H) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) nfail = min(nfail, (uint32_t)__shfl_xor(nfail, d, 64));
+    if ((threadIdx.x & 63) == 0 && nfail < H)
+      atomicMin(reinterpret_cast<unsigned long long*>(pre_out), pre_key(tag_out, nfail));
   }
   wave_stat_add(c, ST_PINGS, npings);
   wave_stat_add(c, ST_FD_EVENTS, npings);  // publishPingResult(ALIVE) per acknowledged ping

@@ -162,7 +162,8 @@ RECORD_DTYPE = np.dtype([("member", "<u4"), ("status", "<u4"), ("inc", "<i4"), (
 
 
 class swim_quiet_stats(C.Structure):
-    _fields_ = [("ticks", C.c_uint64), ("windows", C.c_uint64), ("attempts", C.c_uint64), ("cut_short", C.c_uint64)]
+    _fields_ = [("ticks", C.c_uint64), ("windows", C.c_uint64), ("attempts", C.c_uint64), ("cut_short", C.c_uint64),
+                ("precomputed", C.c_uint64)]
 
 
 class swim_kernel_profile(C.Structure):

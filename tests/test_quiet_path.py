@@ -102,3 +102,36 @@ def test_quiet_on_equals_quiet_off_4096(glib):
     assert (ea["type"] == abi.EV_REMOVED).sum() == n - 1
     sa, sb = eng[False].stats(), eng[True].stats()
     assert not parity.diff_stats(sa, sb), parity.diff_stats(sa, sb)
+
+
+def test_precomputed_windows_match_oracle(glib):
+    """A pristine cluster (no member ever stopped or filtered) lets a window's apply find the next
+    window's end, so consecutive windows launch no scan (swim_quiet.h QuietPre).  Calls of varying
+    length with reads between them (which keep the precompute), ping lists wrapping every few
+    periods (N = 12: the reshuffle ends windows), and then a metadata update and a join (control
+    operations: the next window scans); compared with the oracle after every call, then the
+    precomputed windows are checked to have run (they cover the longest window a call may ask
+    for, kQuietMax ticks, so a longer call after a shorter one needs no scan either)."""
+    sc = S("quiet_pristine_12", 16, 12, 0, seed=38, seeds=(0,))
+    ge, oe = scenarios.make_engine(glib, sc), scenarios.make_engine(oracle.lib(), sc)
+    ge.set_quiet_path(True)
+    steps = [50, 50, 20, 20, 80, 10, 200, 200, 7, 7, 7, 300, 33, 33]
+    for i, k in enumerate(steps + ["meta", 60, 60, "join", 120, 120, 40]):
+        if k == "meta":
+            for e in (ge, oe):
+                e.update_metadata(3)
+            continue
+        if k == "join":
+            for e in (ge, oe):
+                e.join(12)
+            continue
+        ge.step_ticks(k)
+        oe.step_ticks(k)
+        d = parity.diff_states(parity.state_digest(oe), parity.state_digest(ge))
+        assert not d, f"call {i} ({k} ticks) diverged:\n" + "\n".join(d)
+    ea, eb = oe.drain_events(), ge.drain_events()
+    assert not parity.diff_events(ea, eb), parity.diff_events(ea, eb)
+    sa, sb = oe.stats(), ge.stats()
+    assert not parity.diff_stats(sa, sb), parity.diff_stats(sa, sb)
+    q = ge.quiet_stats()
+    assert q["precomputed"] > 0 and q["precomputed"] < q["attempts"], q
