@@ -244,7 +244,12 @@ struct swim_engine {
   uint32_t quiet_backoff = 1;
   swim_quiet_stats qst{};
   // swim_profile_quiet: HIP events around every window's kernels (scan .. apply) while profiling
-  hipEvent_t qev[2] = {nullptr, nullptr};
+  // (a ring of event pairs, read when the profile is read or the ring is full: a window's own wait
+  // never synchronises on an event, which would put the runtime's completion signalling into the
+  // measured call)
+  static constexpr uint32_t kQevRing = 64;
+  hipEvent_t qev[2 * kQevRing] = {};
+  uint32_t qev_n = 0;            // pairs recorded and not yet read
   double qprof_ms = 0.0;
   uint64_t qprof_windows = 0, qprof_ticks = 0, qprof_mp = 0, qprof_bytes = 0;
   std::vector<uint8_t> loss_h;   // host mirror of the default outbound loss per member
@@ -867,6 +872,17 @@ static bool quiet_eligible(const swim_engine* e) {
   return !c.partition && !c.delay_on && !c.record_fd;
 }
 
+// the recorded windows' kernel times into qprof_ms (the events are complete once synchronised; the
+// runtime may mark them done after the spinning wait saw the work finish)
+static void qev_flush(swim_engine* e) {
+  for (uint32_t k = 0; k < e->qev_n; ++k) {
+    float ms = 0.f;
+    hipEventSynchronize(e->qev[2 * k + 1]);
+    if (hipEventElapsedTime(&ms, e->qev[2 * k], e->qev[2 * k + 1]) == hipSuccess) e->qprof_ms += ms;
+  }
+  e->qev_n = 0;
+}
+
 // an API call that changes state or configuration: the next quiet window scans again
 static inline void mutated(swim_engine* e) {
   if (e) e->pre_valid = false;
@@ -894,7 +910,9 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
   uint64_t* pre_out = e->d_pre + (e->pre_slot ^ 1u);
   const uint32_t tag_in = e->pre_tag, tag_out = e->pre_tag + 1;
   const bool prof = e->prof && e->qev[0];
-  if (prof) hipEventRecord(e->qev[0], s);
+  if (prof && e->qev_n == swim_engine::kQevRing) qev_flush(e);
+  hipEvent_t* qp = e->qev + 2 * e->qev_n;
+  if (prof) hipEventRecord(qp[0], s);
   // the shards' witness refs must agree (k_quiet_scan): RCCL compares the ranks' elementwise min and max
   if (e->rccl && !use_pre) {
     const size_t n = e->n;
@@ -925,7 +943,10 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
   }
   e->pre_tag = tag_out;
   e->pre_slot ^= 1u;
-  if (prof) hipEventRecord(e->qev[1], s);
+  if (prof) {
+    hipEventRecord(qp[1], s);
+    e->qev_n++;
+  }
   // (the drain after a window that ends the swim_step call needs no wait of its own; folding k_status
   // into the apply's last workgroup was measured slower: every workgroup's release fence before the
   // finished count writes its XCD's L2 back, 1.98 vs 2.05 x 10^10 member-periods/s)
@@ -940,10 +961,6 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
   e->par_slot = 0;  // (the stream drained: the Params staging ring restarts)
   *done = std::min(__atomic_load_n(e->h_done, __ATOMIC_ACQUIRE), K);
   if (prof) {
-    float ms = 0.f;
-    // (the spinning wait saw the stream's work complete before the runtime marks the event done)
-    hipEventSynchronize(e->qev[1]);
-    if (hipEventElapsedTime(&ms, e->qev[0], e->qev[1]) == hipSuccess) e->qprof_ms += ms;
     // algorithmic bytes (swim.h swim_profile_quiet): SURVEY.md §8(d)'s 21 B per member-period of the
     // ping phase, plus what the quiet check must read once per window: every owned row's count of
     // non-zero witness blocks, 64 B of per-member words, the reference row, the window's timer buckets
@@ -2359,6 +2376,7 @@ int32_t swim_get_quiet_stats(const swim_engine* e, swim_quiet_stats* out) {
 
 int32_t swim_profile_quiet(swim_engine* e, swim_kernel_profile* out) {
   if (!e || !out) return SWIM_EINVAL;
+  qev_flush(e);
   std::memset(out, 0, sizeof(*out));
   out->launches = e->qprof_windows;
   out->total_ms = e->qprof_ms;
@@ -2373,6 +2391,7 @@ int32_t swim_profile_enable(swim_engine* e, int32_t enable) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return SWIM_EDEVICE;
   for (hipEvent_t& ev : e->qev)
     if (!ev && hipEventCreate(&ev) != hipSuccess) return SWIM_EDEVICE;
+  e->qev_n = 0;
   e->qprof_ms = 0.0;
   e->qprof_windows = e->qprof_ticks = e->qprof_mp = e->qprof_bytes = 0;
   for (Shard& sd : e->sh) {
