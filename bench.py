@@ -211,11 +211,12 @@ def side_run(lib, workload, n, warmup, steps, device=0, quiet=True, period_times
     return out
 
 
-def window_pmc_traffic(workload, n, steps, warmup):
+def window_pmc_traffic(workload, n, steps, warmup, scanned=True):
     """HBM bytes of the timed quiet window (k_quiet_scan + k_quiet_apply, the LAST launch of each in
-    the profiled command) from the committed PMC passes — only when that command ran the same window
-    (same --steps and --warmup: the window's length is steps x ticks per period).  (None, reason)
-    otherwise: traffic is never borrowed from a window of another length."""
+    the profiled command; only k_quiet_apply when the window was precomputed: scanned=False) from the
+    committed PMC passes — only when that command ran the same window (same --steps and --warmup: the
+    window's length is steps x ticks per period).  (None, reason) otherwise: traffic is never
+    borrowed from a window of another length."""
     import glob
     paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}{n // 1024}k_pmc.json")))
     if not paths:
@@ -226,7 +227,7 @@ def window_pmc_traffic(workload, n, steps, warmup):
     if ba.get("steps") != steps or ba.get("warmup") != warmup:
         return None, f"{src} profiled --steps {ba.get('steps')} --warmup {ba.get('warmup')}, not this window"
     tot = 0.0
-    for k in ("k_quiet_scan", "k_quiet_apply"):
+    for k in (("k_quiet_scan", "k_quiet_apply") if scanned else ("k_quiet_apply",)):
         last = (doc["kernels"].get(k) or {}).get("last_launch_hbm_bytes")
         if last is None:
             return None, f"{src} holds no per-launch bytes of {k}"
@@ -234,20 +235,22 @@ def window_pmc_traffic(workload, n, steps, warmup):
     return tot, src
 
 
-def quiet_roofline(qprof, workload, n, steps, warmup):
+def quiet_roofline(qprof, workload, n, steps, warmup, scanned=True):
     """k_quiet_scan + k_quiet_apply (a quiet window's two launches) against HBM: swim_profile_quiet's
     algorithmic bytes (SURVEY.md §8(d) ping phase, 21 B per member-period, plus the quiet check's
     reads once per window) over the kernels' HIP-event time; traffic = the same window's HBM bytes
     from the committed PMC passes of this exact command (window_pmc_traffic)."""
     per_win = qprof["alg_bytes"] / max(1, qprof["launches"])
     ach = qprof["alg_bytes"] / max(1e-12, qprof["total_ms"] / 1e3) / 1e9
-    traffic, src = window_pmc_traffic(workload, n, steps, warmup) if qprof["launches"] == 1 else \
+    traffic, src = window_pmc_traffic(workload, n, steps, warmup, scanned) if qprof["launches"] == 1 else \
         (None, "more than one window in the timed region")
     ts = (None, src)
-    return {"bound": "hbm", "kernel": "k_quiet_scan + k_quiet_apply (one quiet window)", "achieved": ach,
+    kern = ("k_quiet_scan + k_quiet_apply (one quiet window)" if scanned else
+            "k_quiet_apply (one quiet window, its end precomputed by the window before: no scan)")
+    return {"bound": "hbm", "kernel": kern, "achieved": ach,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
-            "traffic_unit": "HBM bytes of the timed window (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of both kernels, "
-                            "the same command's last window)",
+            "traffic_unit": "HBM bytes of the timed window (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the window's "
+                            "kernels, the same command's last window)",
             "traffic_source": ts[1], "windows": qprof["launches"], "avg_window_ms": qprof["total_ms"] / max(1, qprof["launches"]),
             "alg_bytes_per_window": per_win, "ticks_per_window": qprof["messages"] / max(1, qprof["launches"]),
             "member_periods_per_window": qprof["records"] / max(1, qprof["launches"]),
@@ -557,6 +560,7 @@ def main():
         barrier()
         e.profile_enable(True)
         st0 = all_stats()  # the timed window's counters are deltas from here (warmup excluded)
+        qs0 = e.quiet_stats()
         barrier()
         t0 = time.perf_counter()
         sch.run(e, args.warmup, args.warmup + args.steps)
@@ -583,6 +587,8 @@ def main():
     if se is not None:
         qprof = {**qprof, **reduce(qprof)}
     qst = e.quiet_stats()
+    # the timed region's windows all precomputed by the one before: no k_quiet_scan ran in it
+    timed_scans = (qst["windows"] - qs0["windows"]) - (qst.get("precomputed", 0) - qs0.get("precomputed", 0))
     value = n * args.steps / dt  # one cluster of n members, sharded over `world` GPUs
     ticks = args.steps * tpp
     gossip_ticks = ticks // max(1, cfg.gossip_interval // e.now()[1])  # ticks with a gossip round
@@ -620,7 +626,8 @@ def main():
     step = step_roofline(stats, prof, fprof, dprof, qprof, ticks, gossip_ticks, dt, args.steps, args.workload, n)
     # the roofline of the step's dominant kernels: the quiet windows' (k_quiet_scan + k_quiet_apply)
     # when they carried the step, else the whole per-tick chain against its wall time
-    line["roofline"] = quiet_roofline(qprof, args.workload, n, args.steps, args.warmup) if qprof["launches"] else step
+    line["roofline"] = quiet_roofline(qprof, args.workload, n, args.steps, args.warmup,
+                                      scanned=timed_scans > 0) if qprof["launches"] else step
     line["roofline_step"] = step
     if prof["launches"]:
         line["roofline_merge"] = merge_roofline(prof, world, args.local_shards, args.workload, n, dt, args.steps, tpp)
