@@ -223,8 +223,7 @@ struct swim_engine {
   // (alternating), the tag of the last one written, and whether it still holds: for the window that
   // starts at pre_T0 with at most pre_H ticks, and nothing but quiet windows ran since (pre_valid is
   // cleared by every per-tick tick and every API call that changes state or configuration: mutated())
-  uint64_t* d_pre = nullptr;     // [2] tagged keys, then (as uint32) the apply's finished-workgroup counter
-  bool fold_status = true;       // SWIM_QUIET_FOLD=0: k_status after each window instead
+  uint64_t* d_pre = nullptr;
   uint32_t pre_tag = 0, pre_slot = 0, pre_H = 0;
   uint64_t pre_T0 = 0;
   bool pre_valid = false;
@@ -937,16 +936,10 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
     if (e->rccl && nccl_ok(ncclAllReduce(q, q, 3, ncclUint32, ncclMin, e->comm, s)) != SWIM_OK)
       return SWIM_EDEVICE;
   }
-  // an unsharded engine's apply publishes the status words itself (QuietStatus, swim_quiet.h); a local
-  // group launches k_status per shard after the window
-  const bool fold = e->spin_wait && e->sh.size() == 1 && e->fold_status;
-  const uint32_t seq = e->spin_wait ? ++e->status_seq : 0u;
   for (Shard& sd : e->sh) {
     const uint32_t g = std::max<uint32_t>(64, grid_for(sd.c.nl, 256));
-    QuietStatus st{nullptr, nullptr, 0u, nullptr};
-    if (fold) st = QuietStatus{e->d_stat, e->d_done + 1, seq, reinterpret_cast<uint32_t*>(e->d_pre + 2)};
     k_quiet_apply<<<g, 256, 0, s>>>(sd.d_par, T0, K, use_pre ? nullptr : q, q_next, e->d_done,
-                                    (uint32_t)kRebaseEvery, pre_in, tag_in, pre_out, tag_out, H, st);
+                                    (uint32_t)kRebaseEvery, pre_in, tag_in, pre_out, tag_out, H);
   }
   e->pre_tag = tag_out;
   e->pre_slot ^= 1u;
@@ -954,9 +947,13 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
     hipEventRecord(qp[1], s);
     e->qev_n++;
   }
-  // (the drain after a window that ends the swim_step call needs no wait of its own)
+  // (the drain after a window that ends the swim_step call needs no wait of its own.  Publishing the
+  // status words from the apply's last workgroup instead of k_status measured slower both ways: with a
+  // release fence per workgroup (its XCD's L2 written back) and without (256 workgroups' counter
+  // atomics on one address serialise at the L2): 2.0 / 2.6 vs 2.9 x 10^10 member-periods/s)
   if (e->spin_wait) {
-    if (!fold) launch_status(e, seq);
+    const uint32_t seq = ++e->status_seq;
+    launch_status(e, seq);
     if (wait_status_seq(e, seq) != SWIM_OK) return SWIM_EDEVICE;
   } else {
     launch_status(e);
@@ -1560,9 +1557,8 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
       hipHostGetDevicePointer((void**)&e->d_stat, e->h_stat, 0) != hipSuccess ||
       hipMalloc((void**)&e->d_quiet, 2 * sizeof(QuietCtl)) != hipSuccess ||
       hipMemset(e->d_quiet, 0xff, 2 * sizeof(QuietCtl)) != hipSuccess ||  // both blocks reset: no fail, no sizes
-      hipMalloc((void**)&e->d_pre, 3 * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(e->d_pre, 0xff, 2 * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(e->d_pre + 2, 0, sizeof(uint64_t)) != hipSuccess) {
+      hipMalloc((void**)&e->d_pre, 2 * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(e->d_pre, 0xff, 2 * sizeof(uint64_t)) != hipSuccess) {
     delete e;
     return SWIM_ENOMEM;
   }
@@ -1574,8 +1570,6 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
     e->spin_wait = !(sp && sp[0] == '0');
     const char* qp = std::getenv("SWIM_QUIET_PRE");
     e->pre_on = !(qp && qp[0] == '0');
-    const char* qf = std::getenv("SWIM_QUIET_FOLD");
-    e->fold_status = !(qf && qf[0] == '0');
   }
   e->loss_h.assign(capacity, 0);
   if (world > 1) {

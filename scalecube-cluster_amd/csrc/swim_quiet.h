@@ -231,41 +231,10 @@ __device__ __forceinline__ uint64_t pre_key(uint32_t tag, uint32_t off) {
 // performs the end-of-tick resets the skipped k_end_tick launches would have made (per-parity scratch
 // counters, the witness rebase's dirty marks: with every up row equal to ref a rebase moves no
 // reference record).
-// QuietStatus: an unsharded engine's window publishes its status words from the apply itself — the
-// last workgroup to finish (a relaxed counter; that workgroup resets it) copies the event counts and
-// error bits to pinned host memory, with the window's length, and releases the sequence word the host
-// spins on: k_status's work without its launch.  No workgroup fences before its count: the host
-// reads only what the last workgroup writes (ordered by its system-scope release), and every device
-// write of the others reaches later work through the stream's kernel boundary.  (A release fence per
-// workgroup writes its XCD's L2 back: measured slower than the k_status launch it saves.)
-struct QuietStatus {
-  uint32_t* out;      // [SUBQ + 1] pinned words, or null: k_status is launched after the window
-  uint32_t* seq_out;  // the pinned sequence word
-  uint32_t seq;
-  uint32_t* ctr;      // workgroups finished (0 between launches)
-};
-__device__ inline void quiet_publish(const Ctx& c, const QuietStatus& st, uint32_t* done, uint32_t F) {
-  __shared__ uint32_t s_last;
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(st.ctr, 1u) == gridDim.x - 1 ? 1u : 0u;
-  __syncthreads();
-  if (!s_last) return;
-  const uint32_t t = threadIdx.x;
-  if (t < SUBQ) st.out[t] = __hip_atomic_load(&c.ev_cnt[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t == SUBQ) st.out[SUBQ] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t == SUBQ + 1) *done = F;
-  __syncthreads();
-  if (t == 0) {
-    *st.ctr = 0u;
-    __threadfence_system();
-    __hip_atomic_store(st.seq_out, st.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
 __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const QuietCtl* q, QuietCtl* next,
                                                      uint32_t* done, uint32_t rebase_every, const uint64_t* pre_in,
                                                      uint32_t tag_in, uint64_t* pre_out, uint32_t tag_out,
-                                                     uint32_t H, QuietStatus st) {
+                                                     uint32_t H) {
   const Ctx c = pctx(P, T);
   uint32_t F;
   if (q) {
@@ -279,10 +248,7 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
     *done = F;
     *next = QuietCtl{0xffffffffu, 0xffffffffu, 0xffffffffu, 0u};
   }
-  if (F == 0) {
-    if (st.out) quiet_publish(c, st, done, F);
-    return;
-  }
+  if (F == 0) return;
   const uint64_t Tend = T + F;
   uint32_t nfail = H;  // this thread's share of the next window's first failing offset (from Tend)
   if (H) {
@@ -356,5 +322,4 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
   wave_stat_add(c, ST_SYNCS, nsync);
   wave_stat_add(c, ST_SYNC_ACKS, nack);
   wave_stat_add(c, ST_SYNC_RECORDS, nrec);
-  if (st.out) quiet_publish(c, st, done, F);
 }
