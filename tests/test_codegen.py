@@ -17,7 +17,7 @@ LIB = os.path.join(REPO, "scalecube-cluster_amd", "lib", "libswimgpu.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 # scratch bytes per thread the hot kernels may use (the per-tick chain, the storm kernels, the
-# quiet windows); measured values in round 5: 80 / 144 / 144 / 0 / 64 / 0 / 0 / 0 (k_gossip_deliver
+# quiet windows); measured values in round 5: 80 / 144 / 144 / 0 / 56 / 0 / 0 / 0 (k_gossip_deliver
 # was 28 until onGossipReq's infected-list insert stopped indexing GossipDev.inf at run time: such an
 # index puts the array in scratch; k_deliver_coop runs at its 256-VGPR cap, these are spills)
 SCRATCH_MAX = {"k_fd": 128, "k_sync_apply": 256, "k_ack_apply": 256, "k_gossip_deliver": 32,
