@@ -337,7 +337,22 @@ def fanout_roofline(fprof, window, same_window_pmc):
             "messages_per_launch": fprof["messages"] / max(1, fprof["launches"]),
             "states_per_launch": fprof["records"] / max(1, fprof["launches"]),
             "alg_bytes_rule": "24 B per materialised GOSSIP_REQ + 32 B per (gossip, sender round) state read",
+            # the bytes the kernel must read and write: 16 hot bytes of every state it looks at (the
+            # swept prefix and the in-window suffix, not all live states), 8 cold bytes and the 32-B
+            # message of every materialised GOSSIP_REQ
+            "must_read": must_read_fanout(fprof),
             "window": window}
+
+
+def must_read_fanout(fprof):
+    if not fprof.get("examined"):
+        return None
+    b = 16.0 * fprof["examined"] + 40.0 * fprof["messages"]
+    ach = b / max(1e-12, fprof["total_ms"] / 1e3) / 1e9
+    return {"bytes_per_launch": b / max(1, fprof["launches"]), "achieved": ach, "frac": ach / HBM_PEAK_GBPS,
+            "examined_states_per_launch": fprof["examined"] / max(1, fprof["launches"]),
+            "rule": "16 B per examined state (swept prefix + in-window suffix) + 8 B cold + 32 B message per "
+                    "materialised GOSSIP_REQ"}
 
 
 def deliver_roofline(dprof, window, same_window_pmc):

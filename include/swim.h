@@ -407,6 +407,8 @@ typedef struct swim_kernel_profile {
                           fanout: GOSSIP_REQs materialised */
   uint64_t records;    /* records that changed a table (sequential merge path) */
   uint64_t alg_bytes;
+  uint64_t examined;   /* fanout: the states whose 16 hot bytes the rounds read (swept prefix + the
+                          passes over the in-window suffix), of the `records` live ones */
 } swim_kernel_profile;
 int32_t swim_profile_enable(swim_engine* e, int32_t enable);
 int32_t swim_profile_merge(swim_engine* e, swim_kernel_profile* out);

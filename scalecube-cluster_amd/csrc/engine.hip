@@ -2440,6 +2440,7 @@ int32_t swim_profile_fanout(swim_engine* e, swim_kernel_profile* out) {
     out->total_ms += sd.prof_emit.ms;
     out->messages += sd.prof_emit.a;
     out->records += sd.prof_emit.b;
+    out->examined += sd.prof_emit.c;
   }
   // SURVEY.md §8(d) fanout: 24 B per emitted GOSSIP_REQ + 32 B per (gossip, sender round) read
   out->alg_bytes = out->messages * 24ull + out->records * 32ull;

@@ -751,7 +751,8 @@ __device__ __forceinline__ SenderPre sender_pre_from(const SenderPre& x, int j) 
 
 __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, const Bufs& b, uint32_t v, uint64_t period,
                                                         uint32_t glen, uint32_t gbase, uint32_t lane, uint32_t* s_t,
-                                                        unsigned long long& nmat, EmitProf& ep,
+                                                        unsigned long long& nmat, unsigned long long& nexam,
+                                                        EmitProf& ep,
                                                         const SenderPre& sp, const GossipHot h_head,
                                                         const GossipHot h_tail) {
   PPROF_T0(te0);
@@ -882,6 +883,7 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
     e0 = s0;
   }
   const uint32_t first = sp.fut ? lead : wst;
+  nexam += lead + (glen > first ? glen - first : 0u);  // hot bytes read: the swept prefix and the passes
   // lane = slab position: one GossipState read serves all nt targets, whose loss draws and
   // receiver checks are independent (issued together); messages keep the (target, position) keys.
   // A pass reads the 16 hot bytes of each state; the 8 cold ones only where a message is
@@ -1257,7 +1259,8 @@ __global__ void k_debug_exchange(KP) {
 }
 
 // the rest of the round for the listed senders: one sender per wave at a time
-// prof (sampled launches only): {GOSSIP_REQs materialised, (gossip, sender round) states read}
+// prof (sampled launches only): {GOSSIP_REQs materialised, live (gossip, sender) states, states whose
+// hot bytes the round read: the swept prefix and the passes}
 #ifndef EMIT_OCC
 #define EMIT_OCC 4  // waves per SIMD the emit kernel is compiled for (its grid fills them: EMIT_GRID)
 #endif
@@ -1267,7 +1270,7 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES, EMIT_OCC) k_gossip_emit(KP, u
   const Bufs b = P->b;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t ns = b.k->sender_cnt;
-  unsigned long long nmsg = 0, nmat = 0, nstate = 0;
+  unsigned long long nmsg = 0, nmat = 0, nstate = 0, nexam = 0;
   EmitProf ep;
   // the wave's senders, up to 64 at a time: lane j loads the j-th one's index, schedule word and round
   // setup (SenderPre) in one batch of independent loads; then the senders run one after the other
@@ -1309,7 +1312,7 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES, EMIT_OCC) k_gossip_emit(KP, u
       GossipHot nh{}, nt{};
       if (j + 1 < nb) slab_ends(j + 1, nh, nt);
       nstate += glen;
-      nmsg += gossip_emit_sender(c, b, c.lo + i, per - 1, glen, gb, lane, s_t[wv], nmat, ep, sp, ch, ct);
+      nmsg += gossip_emit_sender(c, b, c.lo + i, per - 1, glen, gb, lane, s_t[wv], nmat, nexam, ep, sp, ch, ct);
       ch = nh;
       ct = nt;
     }
@@ -1328,6 +1331,7 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES, EMIT_OCC) k_gossip_emit(KP, u
   if (prof && lane == 0 && nstate) {
     atomicAdd(prof, nmat);
     atomicAdd(prof + 1, nstate);
+    atomicAdd(prof + 2, nexam);
   }
   wave_stat_add(c, ST_GOSSIP_MESSAGES, nmsg);
 }

@@ -168,7 +168,7 @@ class swim_quiet_stats(C.Structure):
 
 class swim_kernel_profile(C.Structure):
     _fields_ = [("launches", C.c_uint64), ("total_ms", C.c_double), ("messages", C.c_uint64),
-                ("records", C.c_uint64), ("alg_bytes", C.c_uint64)]
+                ("records", C.c_uint64), ("alg_bytes", C.c_uint64), ("examined", C.c_uint64)]
 
 
 _u32p = POINTER(C.c_uint32)
