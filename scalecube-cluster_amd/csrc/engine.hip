@@ -1247,7 +1247,8 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   // inbox pages: the message capacity in 64-message pages plus one partial page per receiver; one
   // receiver's inbox may span pg_max pages: 64x its even share of the capacity, at least 512 pages
   // (32 Ki messages: a storm's inboxes are uneven), at most the whole pool
-  b.pg_cap = (uint32_t)std::min<uint64_t>(1ull << 26, (uint64_t)b.msg_cap / 64 + nl + 64);
+  // (+ nl: every receiver's own first page, inbox_page_alloc)
+  b.pg_cap = (uint32_t)std::min<uint64_t>(1ull << 26, (uint64_t)b.msg_cap / 64 + 2ull * nl + 64);
   b.pg_max = (uint32_t)std::min<uint64_t>(b.pg_cap, std::max<uint64_t>(512, next_pow2((uint32_t)std::min<uint64_t>(
                                               1u << 30, 64ull * b.msg_cap / 64 / std::max(nl, 1u)))));
   b.pg_max = std::min<uint32_t>(b.pg_max, 1u << 14);
@@ -1381,6 +1382,14 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   }
   hipMemsetAsync(b.msg_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.pg_tab, 0xff, 4 * (size_t)std::max(nl, 1u) * b.pg_max, s);
+  {  // every receiver's first inbox page is its own: pg_tab[i][0] = i
+    std::vector<uint32_t> own(std::max(nl, 1u));
+    for (uint32_t x = 0; x < own.size(); ++x) own[x] = x;
+    if (hipMemcpy2DAsync(b.pg_tab, 4ull * b.pg_max, own.data(), 4, 4, own.size(), hipMemcpyHostToDevice, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return SWIM_EDEVICE;
+  }
   hipMemsetAsync(b.big_tick, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.req_cnt, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(b.ack_cnt, 0, 4 * (size_t)nl, s);

@@ -614,15 +614,20 @@ __device__ inline void fd_member(const Ctx& c, uint32_t v, unsigned long long& n
 // one whose reserved slots include the page's first slot; a writer whose slots start inside a page
 // waits for that page (its first slot was reserved earlier, by a writer that allocates it without
 // waiting).  Writers allocate before they wait, so a wave never waits on one of its own lanes.
+// A receiver's FIRST page is its own, pool page i, fixed for the engine's life (pg_tab[i][0] = i,
+// never handed back): a storm's inboxes mostly fit one page, so most writers neither allocate nor
+// wait, and the small-inbox delivery needs no page-table load; the bump pool starts after them.
 constexpr uint32_t PG_FAILED = 0xfffffffeu;  // the pool ran dry: releases the page's waiters
 __device__ inline uint32_t inbox_page_alloc(const Ctx& c, const Bufs& b, uint32_t i, uint32_t pg) {
+  if (pg == 0) return i;
   if (pg >= b.pg_max) { set_err(c, ERR_INBOX); return NONE; }
-  uint32_t np = atomicAdd(&b.k->pg_cursor, 1u);
+  uint32_t np = c.nl + atomicAdd(&b.k->pg_cursor, 1u);
   if (np >= b.pg_cap) { set_err(c, ERR_PAGES); np = PG_FAILED; }
   __atomic_store_n(b.pg_tab + (size_t)i * b.pg_max + pg, np, __ATOMIC_RELAXED);
   return np == PG_FAILED ? NONE : np;
 }
 __device__ inline uint32_t inbox_page_wait(const Ctx& c, const Bufs& b, uint32_t i, uint32_t pg) {
+  if (pg == 0) return i;
   if (pg >= b.pg_max) { set_err(c, ERR_INBOX); return NONE; }
   const uint32_t* e = b.pg_tab + (size_t)i * b.pg_max + pg;
   for (uint32_t it = 0; it < (1u << 20); ++it) {
@@ -2241,7 +2246,8 @@ __global__ void __launch_bounds__(DLV_BLOCK, COOP_OCC) k_deliver_coop(KP, unsign
         acc += deliver_coop(c, b, i, k, lane, s_big[wv], s_iv[wv], nfresh);
       }
       wave_sync();
-      for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64) pt[pg] = NONE;
+      for (uint32_t pg = lane; pg < (k + 63) / 64; pg += 64)
+        if (pg) pt[pg] = NONE;  // (page 0 is the receiver's own)
     }
   }
   wave_stat_add(c, ST_GOSSIP_ACCEPTED, acc);
@@ -2345,7 +2351,8 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
   for (uint32_t j = 0; j < nb; ++j) {
     const uint32_t i = list[j], r = c.lo + i;
     const uint32_t np = rdlane(my_pages, j);
-    for (uint32_t pg = lane; pg < np; pg += 64) b.pg_tab[(size_t)i * b.pg_max + pg] = NONE;
+    for (uint32_t pg = lane; pg < np; pg += 64)
+      if (pg) b.pg_tab[(size_t)i * b.pg_max + pg] = NONE;  // (page 0 is the receiver's own)
     apply_ins_batch<64, false>(c, r, lane, L.iP, L.iS, L.iR);
   }
   if (lane < nb && collect) nsync += sync_collect_member(cs, b, c.lo + list[lane]);
@@ -2404,11 +2411,9 @@ __global__ void __launch_bounds__(DLV_BLOCK) k_gossip_deliver(KP, int collect, u
       const uint32_t k = b.msg_cnt[i];
       const uint32_t r = c.lo + i;
       if (k != 0) {
-        // a small inbox fits its first page (k <= DLV_SORT < 64)
+        // a small inbox fits its first page (k <= DLV_SORT < 64): the receiver's own, page i
         b.msg_cnt[i] = 0;
-        uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
-        const uint32_t pid = *pt;
-        *pt = NONE;
+        const uint32_t pid = i;
         if (!c.up[r]) {
         } else if (pid >= b.pg_cap) {  // NONE or PG_FAILED: the page pool ran dry (ERR_PAGES is set)
           set_err(c, ERR_PAGES);
