@@ -556,8 +556,9 @@ def main():
     else:
         e = abi.Engine(lib, cfg, sch.capacity, n, 1)
     shard = e.shard_info()
-    if hook is None and shard["world"] != world:
-        raise SystemExit(f"bench.py: {world} ranks but the engine has {shard['world']} shards")
+    if hook is None and shard["world"] != world * args.local_shards:
+        raise SystemExit(f"bench.py: {world} ranks x {args.local_shards} local shards "
+                         f"but the engine has {shard['world']} shards")
     sch.setup(e)
 
     def barrier():

@@ -1242,8 +1242,13 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.ev_cap = std::max<uint32_t>(1024, (cf.event_capacity ? cf.event_capacity : (1u << 22)) / SUBQ);
   // deferred pingMembers inserts of one phase: a join burst adds every joiner at every viewer
   c.ins_cap = (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 22, 256ull * nl));
+  // a sharded engine's inboxes hold 4x as many per receiver: a GOSSIP_REQ from another shard is
+  // materialised even when the receiver already holds its gossip (k_recv_msgs flags it; the emitter
+  // could not read this shard's receipt bits): the failures storm at N = 65,536 sends ~1,500 a round
+  // per receiver
   b.msg_cap = cf.message_capacity ? cf.message_capacity
-                                 : (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 512ull * nl));
+                                 : (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(
+                                                                    1ull << 20, (e->world > 1 ? 2048ull : 512ull) * nl));
   // inbox pages: the message capacity in 64-message pages plus one partial page per receiver; one
   // receiver's inbox may span pg_max pages: 64x its even share of the capacity, at least 512 pages
   // (32 Ki messages: a storm's inboxes are uneven), at most the whole pool
@@ -1268,7 +1273,9 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.pool_cap = std::max<uint32_t>(1u << 22, 16 * n);
   const bool multi = e->world > 1;
   // tx capacities must be identical on every rank: both ends of a send clamp the count with them
-  b.tx_msg_cap = multi ? (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 256ull * e->sz)) : 0;
+  // (the failures storm at N = 65,536 over 2 shards sends ~24 M GOSSIP_REQs a round to the peer;
+  // all peers' buffers together: 32 KiB per member of the whole cluster, 2 GiB at N = 65,536)
+  b.tx_msg_cap = multi ? (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 1024ull * e->sz)) : 0;
   b.tx_req_cap = multi ? b.req_cap : 0;
   b.tx_stop_cap = multi ? kStopCap : 0;
   // content rows one shard may send in one SYNC (or SYNC_ACK) exchange: 256 MiB of rows, 64..4,096
