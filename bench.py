@@ -211,38 +211,55 @@ def side_run(lib, workload, n, warmup, steps, device=0, quiet=True, period_times
     return out
 
 
-def window_pmc_traffic(workload, n, steps, warmup, scanned=True):
-    """HBM bytes of the timed quiet window (k_quiet_scan + k_quiet_apply, the LAST launch of each in
-    the profiled command; only k_quiet_apply when the window was precomputed: scanned=False) from the
-    committed PMC passes — only when that command ran the same window (same --steps and --warmup: the
-    window's length is steps x ticks per period).  (None, reason) otherwise: traffic is never
-    borrowed from a window of another length."""
+def window_pmc_traffic(workload, n, steps, warmup, scanned=True, first=None):
+    """HBM bytes of the timed quiet window (k_quiet_scan + k_quiet_apply; only k_quiet_apply when the
+    window was precomputed: scanned=False) from the committed PMC passes — only when that command ran
+    the same window (same --steps and --warmup: the window's length is steps x ticks per period).
+    `first` = {kernel: launches of it before the timed window} picks the timed window's launch from
+    the profile's per-launch list (the side runs after it launch the same kernels); profiles without
+    the list give their last launch.  (None, reason) otherwise: traffic is never borrowed from a
+    window of another length."""
     import glob
     paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}{n // 1024}k_pmc.json")))
     if not paths:
         return None, "no PMC profile of this workload"
-    doc = json.load(open(paths[-1]))
-    src = os.path.relpath(paths[-1], REPO)
-    ba = doc.get("bench_args") or {}
-    if ba.get("steps") != steps or ba.get("warmup") != warmup:
-        return None, f"{src} profiled --steps {ba.get('steps')} --warmup {ba.get('warmup')}, not this window"
+    # the newest profile of this exact window (e.g. the driver's --steps 20 --warmup 5 and the
+    # default --steps 40 --warmup 10 each have their own)
+    doc = None
+    for path in reversed(paths):
+        d = json.load(open(path))
+        ba = d.get("bench_args") or {}
+        if ba.get("steps") == steps and ba.get("warmup") == warmup:
+            doc, src = d, os.path.relpath(path, REPO)
+            break
+    if doc is None:
+        ba = json.load(open(paths[-1])).get("bench_args") or {}
+        return None, (f"{os.path.relpath(paths[-1], REPO)} profiled --steps {ba.get('steps')} "
+                      f"--warmup {ba.get('warmup')}, not this window")
     tot = 0.0
     for k in (("k_quiet_scan", "k_quiet_apply") if scanned else ("k_quiet_apply",)):
-        last = (doc["kernels"].get(k) or {}).get("last_launch_hbm_bytes")
+        kd = doc["kernels"].get(k) or {}
+        seq = kd.get("launch_hbm_bytes")
+        if first is not None and seq is not None:
+            if first.get(k, 0) >= len(seq):
+                return None, f"{src} holds {len(seq)} launches of {k}, the timed one is #{first.get(k, 0)}"
+            tot += seq[first.get(k, 0)]
+            continue
+        last = kd.get("last_launch_hbm_bytes")
         if last is None:
             return None, f"{src} holds no per-launch bytes of {k}"
         tot += last
     return tot, src
 
 
-def quiet_roofline(qprof, workload, n, steps, warmup, scanned=True):
+def quiet_roofline(qprof, workload, n, steps, warmup, scanned=True, first=None):
     """k_quiet_scan + k_quiet_apply (a quiet window's two launches) against HBM: swim_profile_quiet's
     algorithmic bytes (SURVEY.md §8(d) ping phase, 21 B per member-period, plus the quiet check's
     reads once per window) over the kernels' HIP-event time; traffic = the same window's HBM bytes
     from the committed PMC passes of this exact command (window_pmc_traffic)."""
     per_win = qprof["alg_bytes"] / max(1, qprof["launches"])
     ach = qprof["alg_bytes"] / max(1e-12, qprof["total_ms"] / 1e3) / 1e9
-    traffic, src = window_pmc_traffic(workload, n, steps, warmup, scanned) if qprof["launches"] == 1 else \
+    traffic, src = window_pmc_traffic(workload, n, steps, warmup, scanned, first) if qprof["launches"] == 1 else \
         (None, "more than one window in the timed region")
     ts = (None, src)
     kern = ("k_quiet_scan + k_quiet_apply (one quiet window)" if scanned else
@@ -250,7 +267,7 @@ def quiet_roofline(qprof, workload, n, steps, warmup, scanned=True):
     return {"bound": "hbm", "kernel": kern, "achieved": ach,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
             "traffic_unit": "HBM bytes of the timed window (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the window's "
-                            "kernels, the same command's last window)",
+                            "kernels, the same command's timed window)",
             "traffic_source": ts[1], "windows": qprof["launches"], "avg_window_ms": qprof["total_ms"] / max(1, qprof["launches"]),
             "alg_bytes_per_window": per_win, "ticks_per_window": qprof["messages"] / max(1, qprof["launches"]),
             "member_periods_per_window": qprof["records"] / max(1, qprof["launches"]),
@@ -642,8 +659,11 @@ def main():
     step = step_roofline(stats, prof, fprof, dprof, qprof, ticks, gossip_ticks, dt, args.steps, args.workload, n)
     # the roofline of the step's dominant kernels: the quiet windows' (k_quiet_scan + k_quiet_apply)
     # when they carried the step, else the whole per-tick chain against its wall time
+    # the timed window's launches in the profiled command: after the warm-up's (one apply per window,
+    # one scan per window attempt whose end was not precomputed)
+    first = {"k_quiet_apply": qs0["windows"], "k_quiet_scan": qs0["attempts"] - qs0.get("precomputed", 0)}
     line["roofline"] = quiet_roofline(qprof, args.workload, n, args.steps, args.warmup,
-                                      scanned=timed_scans > 0) if qprof["launches"] else step
+                                      scanned=timed_scans > 0, first=first) if qprof["launches"] else step
     line["roofline_step"] = step
     if prof["launches"]:
         line["roofline_merge"] = merge_roofline(prof, world, args.local_shards, args.workload, n, dt, args.steps, tpp)

@@ -39,3 +39,22 @@ def test_gpus_2_spawns_two_ranks():
 def test_world_size_must_match_gpus():
     p = _bench("--gpus", "2", *HOOK, env_extra={"WORLD_SIZE": "1"})
     assert p.returncode != 0 and "WORLD_SIZE=1" in (p.stderr + p.stdout)
+
+
+def test_window_traffic_only_from_the_same_window(tmp_path, monkeypatch):
+    """roofline.traffic is taken from the newest committed PMC profile of the SAME window (same
+    --steps / --warmup), never borrowed from a window of another length."""
+    sys.path.insert(0, REPO)
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    for name, steps, warm, b in (("r01_quiet64k_pmc.json", 40, 10, 100.0), ("r02_quiet64k_pmc.json", 20, 5, 7.0),
+                                 ("r03_quiet64k_pmc.json", 20, 5, 9.0)):
+        (prof / name).write_text(json.dumps({"bench_args": {"steps": steps, "warmup": warm},
+                                             "kernels": {"k_quiet_apply": {"last_launch_hbm_bytes": b},
+                                                         "k_quiet_scan": {"last_launch_hbm_bytes": 1.0}}}))
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    assert bench.window_pmc_traffic("quiet", 65536, 20, 5, scanned=False) == (9.0, "profiles/r03_quiet64k_pmc.json")
+    assert bench.window_pmc_traffic("quiet", 65536, 40, 10, scanned=True) == (101.0, "profiles/r01_quiet64k_pmc.json")
+    t, why = bench.window_pmc_traffic("quiet", 65536, 7, 3)
+    assert t is None and "not this window" in why

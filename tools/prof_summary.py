@@ -4,7 +4,7 @@
 
 writes <out>_kernel_stats.csv (per-kernel calls / total / average / share, from the kernel-trace
 pass) and <out>_pmc.json (per-kernel, per-launch HBM bytes from the separate FETCH_SIZE and
-WRITE_SIZE passes; per kernel also the bytes of its last launch, and the profiled bench command's
+WRITE_SIZE passes; per kernel also the bytes of each launch and of its last, and the profiled bench command's
 --steps / --warmup, so that bench.py attaches traffic only to the window of the same length).  Corrections follow /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE is
 in KiB and on gfx950 reports exactly half the bytes of a wide (16 B / lane) coalesced streaming
 read, so it is doubled; WRITE_SIZE (KiB) is exact for 16-B-per-lane streaming stores.
@@ -43,6 +43,15 @@ def pmc_last(prefix, which):
     return last
 
 
+def pmc_all(prefix, which):
+    """per kernel, the counter value of each dispatch in dispatch order"""
+    con = _db(f"{prefix}_{which}")
+    out = {}
+    for name, v in con.execute("select kernel_name, value from counters_collection order by dispatch_id"):
+        out.setdefault(name, []).append(float(v))
+    return out
+
+
 def main(src, out):
     ks = kernel_stats(src)
     with open(f"{out}_kernel_stats.csv", "w", newline="") as f:
@@ -63,6 +72,12 @@ def main(src, out):
     for name, v in per.items():
         if name in lf and name in lw:
             v["last_launch_hbm_bytes"] = 2.0 * lf[name] * 1024.0 + lw[name] * 1024.0
+    # every launch in dispatch order (bench.py picks the timed window's by its index: the launches
+    # before it are the warm-up's, the ones after it the window-model side run's)
+    af, aw = pmc_all(src, "fetch"), pmc_all(src, "write")
+    for name, v in per.items():
+        if name in af and name in aw and len(af[name]) == len(aw[name]):
+            v["launch_hbm_bytes"] = [2.0 * f * 1024.0 + w * 1024.0 for f, w in zip(af[name], aw[name])]
     doc = {"source": src, "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count of 16-B/lane streaming "
                                         "reads, MI355X_MICROARCH.md HBM); WRITE_SIZE KiB x 1024",
            "kernels": per}
