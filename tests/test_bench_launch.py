@@ -58,3 +58,12 @@ def test_window_traffic_only_from_the_same_window(tmp_path, monkeypatch):
     assert bench.window_pmc_traffic("quiet", 65536, 40, 10, scanned=True) == (101.0, "profiles/r01_quiet64k_pmc.json")
     t, why = bench.window_pmc_traffic("quiet", 65536, 7, 3)
     assert t is None and "not this window" in why
+    # with per-launch bytes the timed window's own launch is taken, not the last (a side run's)
+    (prof / "r04_quiet64k_pmc.json").write_text(json.dumps({
+        "bench_args": {"steps": 20, "warmup": 5},
+        "kernels": {"k_quiet_apply": {"last_launch_hbm_bytes": 50.0, "launch_hbm_bytes": [20.0, 31.0, 19.0, 50.0]}}}))
+    first = {"k_quiet_apply": 1, "k_quiet_scan": 1}
+    assert bench.window_pmc_traffic("quiet", 65536, 20, 5, scanned=False, first=first) == \
+        (31.0, "profiles/r04_quiet64k_pmc.json")
+    t, why = bench.window_pmc_traffic("quiet", 65536, 20, 5, scanned=False, first={"k_quiet_apply": 9})
+    assert t is None and "the timed one is #9" in why
