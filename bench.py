@@ -144,19 +144,77 @@ def churn_capacities(cfg, capacity):
     return cfg
 
 
-def pmc_traffic(kernel, workload):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this bench
-    (tools/profile.sh -> tools/prof_summary.py -> profiles/<round>_<workload>_pmc.json: separate
-    FETCH_SIZE and WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
+def build_hash():
+    """The source hash of the libswimgpu.so build (the stamp __graft_entry__.build writes beside it):
+    a profile is attached to this run only if it measured the same build."""
+    try:
+        return open(os.path.join(REPO, "scalecube-cluster_amd", "lib", "libswimgpu.so.srchash")).read().strip()[:16]
+    except OSError:
+        return None
+
+
+def bench_key(args, n):
+    """What identifies this command's kernel launches: every argument that changes what the engines
+    run (tools/prof_summary.py stores the profiled command's key; a profile is used only by a run
+    with the same key and build)."""
+    return {"gpus": args.gpus, "steps": args.steps, "warmup": args.warmup, "workload": args.workload,
+            "members": n, "local_shards": args.local_shards, "extras": not args.no_extras,
+            "churn": not args.no_churn, "fanout_steps": args.fanout_steps, "churn_steps": args.churn_steps}
+
+
+_PROFILE = {}
+
+
+def find_profile(key):
+    """The newest committed per-launch PMC profile (profiles/*_pmc.json, tools/prof_driver.sh ->
+    tools/prof_summary.py) of THIS command on THIS build: (doc, path) or (None, reason).  Never picked
+    by file name order: a profile of another build or another command is not used."""
+    ck = json.dumps(key, sort_keys=True)
+    if ck in _PROFILE:
+        return _PROFILE[ck]
     import glob
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}_pmc.json")))
-    if not paths:
-        return None, None
-    doc = json.load(open(paths[-1]))
-    k = doc.get("kernels", {}).get(kernel)
+    bh, best, seen = build_hash(), None, 0
+    for path in glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if "engines" not in d:
+            continue
+        seen += 1
+        if d.get("build") != bh or d.get("bench_key") != key:
+            continue
+        if best is None or d.get("created", "") > best[0].get("created", ""):
+            best = (d, os.path.relpath(path, REPO))
+    _PROFILE[ck] = best or (None, f"none of the {seen} per-launch PMC profiles under profiles/ measured this "
+                                  f"command on this build ({bh})")
+    return _PROFILE[ck]
+
+
+def profile_launches(doc, engine, kernel, first=None, last=None):
+    """Per-launch HBM bytes (and kernel-trace microseconds) of `kernel` in the profiled command's
+    `engine`-th engine (engines in creation order): the launch #first, or the mean of the last `last`
+    launches.  None if the profile does not hold them."""
+    engs = doc.get("engines") or []
+    if engine >= len(engs):
+        return None
+    k = engs[engine].get(kernel)
     if not k:
-        return None, None
-    return k["hbm_bytes_per_launch"], os.path.relpath(paths[-1], REPO)
+        return None
+    hb, fb, wb, us = k["hbm_bytes"], k["fetch_bytes"], k["write_bytes"], k.get("us") or []
+    if first is not None:
+        if first >= len(hb):
+            return None
+        pick = [first]
+        tpick = pick if first < len(us) else None  # (launch #first of the trace pass: same program order)
+    else:
+        if not last or len(hb) < last:
+            return None
+        pick = list(range(len(hb) - last, len(hb)))
+        tpick = pick if len(us) == len(hb) else None
+    mean = lambda xs, ix: sum(xs[i] for i in ix) / len(ix) if ix else None
+    return {"hbm": mean(hb, pick), "fetch": mean(fb, pick), "write": mean(wb, pick), "us": mean(us, tpick),
+            "launches": len(pick)}
 
 
 def cpu_model() -> str:
@@ -211,70 +269,93 @@ def side_run(lib, workload, n, warmup, steps, device=0, quiet=True, period_times
     return out
 
 
-def window_pmc_traffic(workload, n, steps, warmup, scanned=True, first=None):
-    """HBM bytes of the timed quiet window (k_quiet_scan + k_quiet_apply; only k_quiet_apply when the
-    window was precomputed: scanned=False) from the committed PMC passes — only when that command ran
-    the same window (same --steps and --warmup: the window's length is steps x ticks per period).
-    `first` = {kernel: launches of it before the timed window} picks the timed window's launch from
-    the profile's per-launch list (the side runs after it launch the same kernels); profiles without
-    the list give their last launch.  (None, reason) otherwise: traffic is never borrowed from a
-    window of another length."""
-    import glob
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}{n // 1024}k_pmc.json")))
-    if not paths:
-        return None, "no PMC profile of this workload"
-    # the newest profile of this exact window (e.g. the driver's --steps 20 --warmup 5 and the
-    # default --steps 40 --warmup 10 each have their own)
-    doc = None
-    for path in reversed(paths):
-        d = json.load(open(path))
-        ba = d.get("bench_args") or {}
-        if ba.get("steps") == steps and ba.get("warmup") == warmup:
-            doc, src = d, os.path.relpath(path, REPO)
-            break
+def window_pmc_traffic(key, scanned=True, first=None):
+    """HBM bytes of the timed quiet window (k_quiet_apply, plus k_quiet_scan when the window's end was
+    not precomputed) from the per-launch PMC profile of this exact command and build: the launch
+    #first[kernel] of the main engine (the launches before it are the warm-up's).  (None, reason)
+    otherwise: traffic is never borrowed from another window, command or build."""
+    doc, src = find_profile(key)
     if doc is None:
-        ba = json.load(open(paths[-1])).get("bench_args") or {}
-        return None, (f"{os.path.relpath(paths[-1], REPO)} profiled --steps {ba.get('steps')} "
-                      f"--warmup {ba.get('warmup')}, not this window")
-    tot = 0.0
+        return None, src, None
+    tot, us = 0.0, 0.0
     for k in (("k_quiet_scan", "k_quiet_apply") if scanned else ("k_quiet_apply",)):
-        kd = doc["kernels"].get(k) or {}
-        seq = kd.get("launch_hbm_bytes")
-        if first is not None and seq is not None:
-            if first.get(k, 0) >= len(seq):
-                return None, f"{src} holds {len(seq)} launches of {k}, the timed one is #{first.get(k, 0)}"
-            tot += seq[first.get(k, 0)]
-            continue
-        last = kd.get("last_launch_hbm_bytes")
-        if last is None:
-            return None, f"{src} holds no per-launch bytes of {k}"
-        tot += last
-    return tot, src
+        pl = profile_launches(doc, 0, k, first=first.get(k, 0))
+        if pl is None:
+            return None, f"{src} holds no launch #{first.get(k, 0)} of {k}", None
+        tot += pl["hbm"]
+        us = None if us is None or pl["us"] is None else us + pl["us"]
+    return tot, src, us
 
 
-def quiet_roofline(qprof, workload, n, steps, warmup, scanned=True, first=None):
-    """k_quiet_scan + k_quiet_apply (a quiet window's two launches) against HBM: swim_profile_quiet's
-    algorithmic bytes (SURVEY.md §8(d) ping phase, 21 B per member-period, plus the quiet check's
-    reads once per window) over the kernels' HIP-event time; traffic = the same window's HBM bytes
-    from the committed PMC passes of this exact command (window_pmc_traffic)."""
+def timed_launch_index(qs0, local_shards=1):
+    """The timed window's launch of each quiet kernel in the profiled command (0-based): the warm-up's
+    launches come first — k_quiet_apply once per window ATTEMPT (an attempt that advances no tick
+    launches it too), k_quiet_scan once per attempt whose end was not precomputed, each once per
+    local shard (swim_quiet_stats counted before the timed region)."""
+    sh = max(1, local_shards)
+    return {"k_quiet_apply": qs0["attempts"] * sh, "k_quiet_scan": (qs0["attempts"] - qs0.get("precomputed", 0)) * sh}
+
+
+def hbm_fields(traffic, seconds):
+    """the real HBM rate beside the rule-based one: the profiled bytes of the launch over its HIP-event time"""
+    if traffic is None or not seconds:
+        return {"hbm_achieved": None, "hbm_frac": None}
+    a = traffic / seconds / 1e9
+    return {"hbm_achieved": a, "hbm_frac": a / HBM_PEAK_GBPS}
+
+
+def quiet_roofline(qprof, key, scanned=True, first=None):
+    """k_quiet_apply (+ k_quiet_scan when the window's end was not precomputed) of the timed window
+    against HBM, two ways: `frac` by SURVEY.md §8(d)'s rule — swim_profile_quiet's algorithmic bytes
+    (21 B per member-period of the ping phase, plus the quiet check's reads once per window) over the
+    kernels' HIP-event time — which credits per-period bytes the closed form does not move (it
+    advances a member's cursor and period in O(1)), so it grows with the window's length; and
+    `hbm_frac`, the bytes the timed launch really moved (per-launch PMC of this exact command and
+    build, window_pmc_traffic) over the same time."""
     per_win = qprof["alg_bytes"] / max(1, qprof["launches"])
+    secs = qprof["total_ms"] / max(1, qprof["launches"]) / 1e3
     ach = qprof["alg_bytes"] / max(1e-12, qprof["total_ms"] / 1e3) / 1e9
-    traffic, src = window_pmc_traffic(workload, n, steps, warmup, scanned, first) if qprof["launches"] == 1 else \
-        (None, "more than one window in the timed region")
-    ts = (None, src)
+    traffic, src, prof_us = window_pmc_traffic(key, scanned, first) if qprof["launches"] == 1 else \
+        (None, "more than one window in the timed region", None)
     kern = ("k_quiet_scan + k_quiet_apply (one quiet window)" if scanned else
             "k_quiet_apply (one quiet window, its end precomputed by the window before: no scan)")
     return {"bound": "hbm", "kernel": kern, "achieved": ach,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
-            "traffic_unit": "HBM bytes of the timed window (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the window's "
-                            "kernels, the same command's timed window)",
-            "traffic_source": ts[1], "windows": qprof["launches"], "avg_window_ms": qprof["total_ms"] / max(1, qprof["launches"]),
+            **hbm_fields(traffic, secs),
+            "traffic_unit": "HBM bytes of the timed window's launch (rocprofv3 memory-side read / write requests "
+                            "x their sizes, tools/prof_summary.py; this command, this build)",
+            "traffic_source": src, "profiled_launch_us": prof_us,
+            "windows": qprof["launches"], "avg_window_ms": secs * 1e3,
             "alg_bytes_per_window": per_win, "ticks_per_window": qprof["messages"] / max(1, qprof["launches"]),
             "member_periods_per_window": qprof["records"] / max(1, qprof["launches"]),
             "alg_bytes_rule": "21 B per member-period (SURVEY.md §8(d) ping phase) + per window the quiet check's "
                               "reads: the 4-B count of non-zero witness blocks + 64 B of member words per row, "
                               "4 B per subject of the reference row, 4 B per timer-bucket queue (swim.h "
                               "swim_profile_quiet)"}
+
+
+def steady_state(e, sch, args, n, cold_dt, barrier, se=None, calls=7):
+    """The headline repeated: `calls` further swim_step calls of the same length right after the timed
+    one (each bracketed by the same barrier + synchronisation), so the line carries the steady-state
+    rate beside the driver's single timed call.  `value` stays the driver's definition (the one
+    call); the first call after the warm-up pays more (cold_call_penalty_us)."""
+    import statistics
+    p, ts = args.warmup + args.steps, []
+    for _ in range(calls):
+        barrier()
+        t0 = time.perf_counter()
+        sch.run(e, p, p + args.steps)
+        barrier()
+        dt = time.perf_counter() - t0
+        ts.append(se.max_time(dt) if se is not None else dt)
+        p += args.steps
+    med = statistics.median(ts)
+    return {"calls": calls, "periods_per_call": args.steps, "call_us": [round(t * 1e6, 2) for t in ts],
+            "median_call_us": med * 1e6, "value": n * args.steps / med, "unit": "member-periods/s",
+            "ms_per_step": med / args.steps * 1e3, "cold_call_us": cold_dt * 1e6,
+            "cold_call_penalty_us": (cold_dt - med) * 1e6,
+            "note": "median of identical swim_step calls after the timed one (same length, barrier + synchronize "
+                    "around each); `value` above is the first (cold) call, as the driver defines it"}
 
 
 def quiet_window_model(e, n, tpp, lengths=(1, 4, 20, 100), budget_s=3.0):
@@ -318,40 +399,62 @@ def quiet_window_model(e, n, tpp, lengths=(1, 4, 20, 100), budget_s=3.0):
                     "the periods per call (fixed_us_per_call is paid once per call); see points"}
 
 
-def merge_roofline(prof, world, local_shards, workload, n, dt, steps, tpp):
+def merge_roofline(prof, world, local_shards, dt, steps, tpp, key=None, engine=None):
     """The SYNC merge: k_sync_apply's SYNC launch (unsharded: classification fused) or k_sync_classify
-    (sharded), HIP events on one launch in three."""
+    (sharded), HIP events on one launch in three; traffic = the mean of the timed periods' launches
+    in the per-launch PMC profile of this command and build (engine = the run's engine index)."""
     merge_kernel = "k_sync_apply" if world == 1 and local_shards == 1 else "k_sync_classify"
-    traffic, src = pmc_traffic(merge_kernel, f"{workload}{n // 1024}k")
     avg_ms = prof["total_ms"] / max(1, prof["launches"])
     ach = prof["alg_bytes"] / max(1e-12, prof["total_ms"] / 1e3) / 1e9
+    traffic, src, pl = None, "no engine index", None
+    if key is not None and engine is not None:
+        doc, src = find_profile(key)
+        pl = profile_launches(doc, engine, merge_kernel, last=steps * tpp) if doc else None
+        if doc is not None and pl is None:
+            src = f"{src} holds fewer than {steps * tpp} launches of {merge_kernel} in engine {engine}"
+        traffic = pl["hbm"] if pl else None
     return {"bound": "hbm", "kernel": merge_kernel + (" (SYNC launch, classification fused)"
                                                       if merge_kernel == "k_sync_apply" else ""),
             "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
-            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of the same kernel)",
-            "traffic_source": src, "launches": prof["launches"], "avg_launch_ms": avg_ms,
+            **hbm_fields(traffic, avg_ms / 1e3),
+            "traffic_unit": "HBM bytes per launch (mean over the timed periods' launches, per-launch PMC)",
+            "traffic_source": src, "profiled_launch_us": pl["us"] if pl else None,
+            "launches": prof["launches"], "avg_launch_ms": avg_ms,
             "alg_bytes_per_launch": prof["alg_bytes"] / max(1, prof["launches"]),
             # one SYNC merge launch per tick (the SYNC_ACK launch, k_ack_apply, reuses its results)
             "kernel_time_share": avg_ms * tpp / (dt * 1e3 / steps)}
 
 
-def fanout_roofline(fprof, window, same_window_pmc):
+def window_traffic(key, engine, kernels, launches):
+    """the mean HBM bytes (and kernel-trace us) per round of the last `launches` launches of each of
+    `kernels` (summed per round) in the profiled command's engine #engine"""
+    doc, src = find_profile(key)
+    if doc is None or engine is None:
+        return None, src if doc is None else "no engine index", None
+    tot = {"hbm": 0.0, "fetch": 0.0, "write": 0.0, "us": 0.0}
+    for k in kernels:
+        pl = profile_launches(doc, engine, k, last=launches)
+        if pl is None:
+            return None, f"{src} holds fewer than {launches} launches of {k} in engine {engine}", None
+        for f in tot:
+            tot[f] = None if tot[f] is None or pl[f] is None else tot[f] + pl[f]
+    return tot, src, launches
+
+
+def fanout_roofline(fprof, window, key=None, engine=None, launches=None):
     f_ms = fprof["total_ms"] / max(1, fprof["launches"])
     f_ach = fprof["alg_bytes"] / max(1e-12, fprof["total_ms"] / 1e3) / 1e9
-    # traffic: the same window's PMC passes (tools/window_prof.sh + tools/window_summary.py: the last
-    # 30 launches = this side run's 6 timed periods), else the whole-run summary
-    # (only when this run IS that window: the failures workload, periods 30-36)
-    import glob
-    wins = sorted(glob.glob(os.path.join(REPO, "profiles", "*_failures64k_window_emit_pmc.json")))
-    f_traffic, f_src = None, None
-    if wins and same_window_pmc:
-        doc = json.load(open(wins[-1]))
-        f_traffic, f_src = doc["hbm_bytes_per_launch"], os.path.relpath(wins[-1], REPO)
+    # traffic: the window's own launches in the per-launch PMC profile of this command and build
+    w, src, _ = window_traffic(key, engine, ("k_gossip_emit",), launches)
+    traffic = w["hbm"] if w else None
+    msgs = fprof["messages"] / max(1, fprof["launches"])
     return {"bound": "hbm", "kernel": "k_gossip_emit", "achieved": f_ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": f_ach / HBM_PEAK_GBPS, "traffic": f_traffic, "traffic_source": f_src,
+            "frac": f_ach / HBM_PEAK_GBPS, "traffic": traffic, **hbm_fields(traffic, f_ms / 1e3),
+            "traffic_source": src, "profiled_launch_us": w["us"] if w else None,
+            "fetch_bytes_per_launch": w["fetch"] if w else None, "write_bytes_per_launch": w["write"] if w else None,
             "launches": fprof["launches"], "avg_launch_ms": f_ms,
             "alg_bytes_per_launch": fprof["alg_bytes"] / max(1, fprof["launches"]),
-            "messages_per_launch": fprof["messages"] / max(1, fprof["launches"]),
+            "messages_per_launch": msgs,
             "states_per_launch": fprof["records"] / max(1, fprof["launches"]),
             "alg_bytes_rule": "24 B per materialised GOSSIP_REQ + 32 B per (gossip, sender round) state read",
             # the bytes the kernel must read and write: 16 hot bytes of every state it looks at (the
@@ -372,26 +475,28 @@ def must_read_fanout(fprof):
                     "materialised GOSSIP_REQ"}
 
 
-def deliver_roofline(dprof, window, same_window_pmc):
+def deliver_roofline(dprof, window, key=None, engine=None, launches=None):
     """The delivery phase — k_deliver_coop (the biggest inboxes, a wave each) then k_gossip_deliver
     (every other inbox), timed together — over the same window as the fanout roofline:
     SURVEY.md §8(d) merge bytes, 24 B per delivered GOSSIP_REQ + 24 B (dedupe + view RMW) per message
     that runs the collector check (swim_profile_deliver)."""
     d_ms = dprof["total_ms"] / max(1, dprof["launches"])
     d_ach = dprof["alg_bytes"] / max(1e-12, dprof["total_ms"] / 1e3) / 1e9
-    import glob
-    wins = sorted(glob.glob(os.path.join(REPO, "profiles", "*_failures64k_window_deliver_pmc.json")))
-    traffic, src = None, None
-    if wins and same_window_pmc:
-        doc = json.load(open(wins[-1]))
-        traffic, src = doc["hbm_bytes_per_launch"], os.path.relpath(wins[-1], REPO)
+    w, src, _ = window_traffic(key, engine, ("k_deliver_coop", "k_gossip_deliver"), launches)
+    traffic = w["hbm"] if w else None
+    msgs = dprof["messages"] / max(1, dprof["launches"])
+    acc = dprof["records"] / max(1, dprof["launches"])
     return {"bound": "hbm", "kernel": "k_deliver_coop + k_gossip_deliver (one delivery phase)", "achieved": d_ach,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": d_ach / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": src,
+            "frac": d_ach / HBM_PEAK_GBPS, "traffic": traffic, **hbm_fields(traffic, d_ms / 1e3),
+            "traffic_source": src, "profiled_launch_us": w["us"] if w else None,
+            "traffic_over_alg": traffic / (dprof["alg_bytes"] / max(1, dprof["launches"])) if traffic else None,
+            "fetch_bytes_per_message": w["fetch"] / msgs if w and w["fetch"] is not None and msgs else None,
+            "write_bytes_per_accepted": w["write"] / acc if w and w["write"] is not None and acc else None,
             "launches": dprof["launches"], "avg_launch_ms": d_ms,
             "alg_bytes_per_launch": dprof["alg_bytes"] / max(1, dprof["launches"]),
-            "messages_per_launch": dprof["messages"] / max(1, dprof["launches"]),
-            "accepted_per_launch": dprof["records"] / max(1, dprof["launches"]),
+            "messages_per_launch": msgs,
+            "accepted_per_launch": acc,
             "alg_bytes_rule": "24 B per delivered GOSSIP_REQ + 24 B (8 B dedupe RMW + 16 B view RMW) per message "
                               "not flagged as a provable duplicate",
             "window": window}
@@ -417,21 +522,9 @@ def step_roofline(stats, prof, fprof, dprof, qprof, ticks, gossip_ticks, dt, ste
              "quiet_windows": float(qprof["alg_bytes"])}
     total = sum(parts.values())
     ach = total / dt / 1e9
-    import glob
-    traffic, src = None, None
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}{n // 1024}k_pmc.json")))
-    kst = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{workload}{n // 1024}k_kernel_stats.csv")))
-    # (a PMC profile of the per-tick chain only: with quiet windows the windows' roofline carries the traffic)
-    if paths and kst and os.path.basename(paths[-1]).split("_")[0] == os.path.basename(kst[-1]).split("_")[0] \
-            and not qprof["launches"]:
-        import csv
-        doc = json.load(open(paths[-1]))
-        calls = {r["kernel"]: int(r["calls"]) for r in csv.DictReader(open(kst[-1]))}
-        ticks_prof = max(1, calls.get("k_end_tick", 1))
-        tick_kernel = lambda k: k.startswith("k_") and not k.startswith(("k_init", "k_kat"))  # not setup / copies
-        per_tick = sum(v.get("hbm_bytes_per_launch", 0.0) * calls.get(k, 0) for k, v in doc["kernels"].items()
-                       if tick_kernel(k)) / ticks_prof
-        traffic, src = per_tick * ticks / steps, os.path.relpath(paths[-1], REPO)
+    # (no HBM traffic here: the step is many launches of many kernels; the per-kernel rooflines carry
+    # the profiled bytes of their own launches)
+    traffic, src = None, "per kernel: see roofline, roofline_merge, roofline_fanout, roofline_deliver"
     return {"bound": "hbm", "scope": "step (one protocol period, every kernel)", "achieved": ach,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBPS,
             "traffic": traffic, "traffic_unit": "HBM bytes per step (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, all kernels)",
@@ -624,7 +717,8 @@ def main():
     timed_scans = (qst["windows"] - qs0["windows"]) - (qst.get("precomputed", 0) - qs0.get("precomputed", 0))
     value = n * args.steps / dt  # one cluster of n members, sharded over `world` GPUs
     ticks = args.steps * tpp
-    gossip_ticks = ticks // max(1, cfg.gossip_interval // e.now()[1])  # ticks with a gossip round
+    gper = max(1, cfg.gossip_interval // e.now()[1])  # ticks per gossip round
+    gossip_ticks = ticks // gper  # ticks with a gossip round
     line = {
         "metric": "simulated member-protocol-periods/sec at N=65,536; achieved HBM GB/s",
         "value": value,
@@ -659,20 +753,29 @@ def main():
     step = step_roofline(stats, prof, fprof, dprof, qprof, ticks, gossip_ticks, dt, args.steps, args.workload, n)
     # the roofline of the step's dominant kernels: the quiet windows' (k_quiet_scan + k_quiet_apply)
     # when they carried the step, else the whole per-tick chain against its wall time
-    # the timed window's launches in the profiled command: after the warm-up's (one apply per window,
-    # one scan per window attempt whose end was not precomputed)
-    first = {"k_quiet_apply": qs0["windows"], "k_quiet_scan": qs0["attempts"] - qs0.get("precomputed", 0)}
-    line["roofline"] = quiet_roofline(qprof, args.workload, n, args.steps, args.warmup,
-                                      scanned=timed_scans > 0, first=first) if qprof["launches"] else step
+    # the timed window's launches in the profiled command: after the warm-up's — k_quiet_apply once per
+    # window ATTEMPT (an attempt that advances no tick launches it too) and per local shard,
+    # k_quiet_scan once per attempt whose end was not precomputed, per local shard
+    key = bench_key(args, n)
+    first = timed_launch_index(qs0, args.local_shards)
+    line["bench_key"] = key
+    line["build"] = build_hash()
+    line["roofline"] = quiet_roofline(qprof, key, scanned=timed_scans > 0, first=first) \
+        if qprof["launches"] else step
     line["roofline_step"] = step
+    # per-tick kernel launches of the timed window, in the main engine (engine #0 of the profile)
+    gticks = gossip_ticks if args.workload != "quiet" or not qprof["launches"] else 0
     if prof["launches"]:
-        line["roofline_merge"] = merge_roofline(prof, world, args.local_shards, args.workload, n, dt, args.steps, tpp)
+        line["roofline_merge"] = merge_roofline(prof, world, args.local_shards, dt, args.steps, tpp, key,
+                                                0 if args.local_shards == 1 and world == 1 else None)
     if fprof["alg_bytes"] > 0:
         # the gossip fanout kernel (north_star: merge AND fanout against the HBM roofline); only
         # workloads with gossip traffic (failures, churn) give it work
-        same = args.workload == "failures" and args.warmup == KILL_FIRST + KILL_EVERY and args.steps == 6 and n == 65536
-        line["roofline_fanout"] = fanout_roofline(fprof, f"the timed window ({args.workload})", same)
-        line["roofline_deliver"] = deliver_roofline(dprof, f"the timed window ({args.workload})", same)
+        eng = 0 if args.local_shards == 1 and world == 1 and args.workload == "failures" else None
+        line["roofline_fanout"] = fanout_roofline(fprof, f"the timed window ({args.workload})", key, eng, gticks)
+        line["roofline_deliver"] = deliver_roofline(dprof, f"the timed window ({args.workload})", key, eng, gticks)
+    if args.workload == "quiet" and qprof["launches"] and hook is None:
+        line["steady_state"] = steady_state(e, sch, args, n, dt, barrier, se)
     if world == 1 and args.workload == "quiet" and qprof["launches"] and hook is None:
         line["quiet_window_model"] = quiet_window_model(e, n, tpp)
     if world == 1 and args.workload == "quiet" and not args.no_extras and args.local_shards == 1 and hook is None:
@@ -680,13 +783,15 @@ def main():
         # (1) the per-tick kernel chain on the same workload and the same timed periods (quiet windows
         # off): the SYNC merge's roofline (k_sync_apply's SYNC launch, classification fused) is
         # measured there
+        # (the engines of this command in creation order: #0 the headline's, #1 this one, #2 failures,
+        # #3 churn, then KS mode; a profile's per-launch lists are kept per engine)
         p_dt, p_prof, _, _, _, _ = side_run(lib, "quiet", n, args.warmup, args.steps, local_rank, quiet=False)
         line["per_tick_path"] = {
             "value": n * args.steps / p_dt, "unit": "member-periods/s", "ms_per_step": p_dt / args.steps * 1e3,
             "steps": args.steps, "warmup": args.warmup,
             "config": "same workload and timed periods, quiet windows off (swim_set_quiet_path(0)): the per-tick "
                       "kernel chain of DESIGN.md §5",
-            "roofline_merge": merge_roofline(p_prof, 1, 1, "quiet", n, p_dt, args.steps, tpp)}
+            "roofline_merge": merge_roofline(p_prof, 1, 1, p_dt, args.steps, tpp, key, 1)}
         # (2) the failures workload over a window that starts with its second kill (period 30: FD
         # detection, the SUSPECT storm through all N members, the gossip's remaining rounds): the
         # fanout and delivery kernels.  The first storm also holds every member's first
@@ -697,8 +802,8 @@ def main():
                   f"{f_st['gossip_messages']} GOSSIP_REQs sent")
         line["failures"] = {"value": n * fs / f_dt, "unit": "member-periods/s", "ms_per_step": f_dt / fs * 1e3,
                             "steps": fs, "window": window,
-                            "roofline_fanout": fanout_roofline(f_fprof, window, fs == 6 and n == 65536),
-                            "roofline_deliver": deliver_roofline(f_dprof, window, fs == 6 and n == 65536)}
+                            "roofline_fanout": fanout_roofline(f_fprof, window, key, 2, fs * tpp // gper),
+                            "roofline_deliver": deliver_roofline(f_dprof, window, key, 2, fs * tpp // gper)}
         line["roofline_fanout"] = line["failures"]["roofline_fanout"]
         line["roofline_deliver"] = line["failures"]["roofline_deliver"]
         # (3) BASELINE config 3 (churn) at its stated N = 16,384: periods 1..1 + churn_steps (the SYNC

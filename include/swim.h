@@ -196,6 +196,18 @@ int32_t swim_create_shard(const swim_config* cfg, uint32_t capacity, uint32_t n_
                           int32_t rank, int32_t world, const uint8_t* comm_id, swim_engine** out);
 /* rank / world of the engine and the viewer range [lo, lo + count) it answers reads for */
 int32_t swim_shard_info(const swim_engine* e, int32_t* rank, int32_t* world, uint32_t* lo, uint32_t* count);
+/*
+ * swim_create_shard with world = 1 and a comm_id is an RCCL engine of ONE rank: the whole exchange
+ * machinery runs (count all-to-alls, the IPC handle of its own exchange region and its all-gather,
+ * the row pulls, the quiet windows' allreduces) with nothing to exchange — the transport on one GPU.
+ * swim_exchange_info reports how the exchange is set up (no reference counterpart):
+ */
+#define SWIM_XCHG_ON 1u            /* sharded tick path with exchange kernels (world > 1 or RCCL) */
+#define SWIM_XCHG_RCCL 2u          /* RCCL transport (one process per GPU) */
+#define SWIM_XCHG_UNCACHED 4u      /* the exchange region is uncached device memory */
+#define SWIM_XCHG_IPC 8u           /* an IPC handle of the region was exported to the peers */
+#define SWIM_XCHG_IPC_FALLBACK 16u /* the uncached region had no IPC handle: re-allocated cached */
+int32_t swim_exchange_info(const swim_engine* e, uint32_t* flags);
 
 /* Advance virtual time.  swim_step advances `periods` * (ping_interval / tick) ticks. */
 int32_t swim_step_ticks(swim_engine* e, uint32_t ticks);

@@ -1468,7 +1468,7 @@ int32_t swim_profile_enable(swim_engine* e, int32_t) { return e ? SWIM_OK : SWIM
 int32_t swim_set_quiet_path(swim_engine* e, int32_t) { return e ? SWIM_OK : SWIM_EINVAL; }
 int32_t swim_profile_quiet(swim_engine* e, swim_kernel_profile* out) { return swim_profile_merge(e, out); }
 int32_t swim_debug_counters(uint64_t* out, uint32_t n, int32_t) {
-  if (!out || n > 32) return SWIM_EINVAL;
+  if (!out || n > 48) return SWIM_EINVAL;
   std::memset(out, 0, 8ull * n);
   return SWIM_OK;
 }
@@ -1688,6 +1688,12 @@ int32_t swim_create_shard(const swim_config* cfg, uint32_t capacity, uint32_t n_
                           int32_t world, const uint8_t*, swim_engine** out) {
   if (world != 1 || rank != 0) return SWIM_EINVAL;
   return swim_create(cfg, capacity, n_initial, seed, out);
+}
+
+int32_t swim_exchange_info(const swim_engine* e, uint32_t* flags) {  // (the oracle never exchanges)
+  if (!e || !flags) return SWIM_EINVAL;
+  *flags = 0;
+  return SWIM_OK;
 }
 
 int32_t swim_shard_info(const swim_engine* e, int32_t* rank, int32_t* world, uint32_t* lo, uint32_t* count) {

@@ -129,6 +129,7 @@ struct Shard {
   // `peers` (device) says where this shard reads what the others produced for it
   void* xreg = nullptr;
   size_t xreg_bytes = 0;
+  bool xreg_uncached = false;  // the region came from hipDeviceMallocUncached
   void* rx_rows_h[2] = {nullptr, nullptr};  // the pulled-row copies Peers points at (RCCL / pull rig)
   uint32_t rx_row_cap = 0;                    // the row_cap they were sized for
   Peers* peers = nullptr;
@@ -185,6 +186,8 @@ struct swim_engine {
   uint64_t T = 0;
   int32_t rank = 0, world = 1;  // this process's shard (RCCL) and the cluster's shard count
   bool rccl = false;
+  uint32_t xflags = 0;  // SWIM_XCHG_IPC* (swim_exchange_info): which branch of setup_peers_rccl ran
+  bool xchg = false;  // the exchange machinery runs: world > 1, or RCCL with one rank (swim_create_shard)
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
   std::vector<Shard> sh;  // local shards, in shard order
@@ -581,10 +584,10 @@ static int32_t rank_min(swim_engine* e, uint32_t& x) {
   return SWIM_OK;
 }
 static size_t xreg_bytes_for(const swim_engine* e, const Bufs& b, uint32_t row_cap);
-static void* xreg_alloc(size_t bytes, bool uncached);
-static void xreg_install(swim_engine* e, Shard& sd, void* fresh, uint32_t row_cap);
+static void* xreg_alloc(size_t bytes, bool uncached, bool* got_uncached = nullptr);
+static int32_t xreg_install(swim_engine* e, Shard& sd, void* fresh, uint32_t row_cap);
 static int32_t grow_rows_for_joins(swim_engine* e) {
-  if (e->world <= 1 || e->joins.empty() || e->sh.empty()) return SWIM_OK;
+  if (!e->xchg || e->joins.empty() || e->sh.empty()) return SWIM_OK;
   const uint32_t W = (uint32_t)e->world;
   std::vector<uint64_t> jn(W, 0), sn(W, 0);
   for (uint32_t m : e->joins) jn[std::min(W - 1, m / e->sz)]++;
@@ -620,18 +623,24 @@ static int32_t grow_rows_for_joins(swim_engine* e) {
   std::vector<std::array<uint32_t*, 2>> rx(e->sh.size(), {nullptr, nullptr});
   uint32_t ok = 1;
   for (size_t i = 0; i < e->sh.size() && ok; ++i) {
-    fresh[i] = xreg_alloc(xreg_bytes_for(e, e->sh[i].b, (uint32_t)cap), e->rccl);
+    fresh[i] = xreg_alloc(xreg_bytes_for(e, e->sh[i].b, (uint32_t)cap), e->rccl, &e->sh[i].xreg_uncached);
     ok = fresh[i] != nullptr;
     for (int k = 0; k < 2 && ok && pulled; ++k)
       ok = dalloc(&rx[i][k], (size_t)W * cap * e->n) == hipSuccess;
   }
-  if (int32_t rc = rank_min(e, ok)) return rc;
-  if (!ok) {  // some rank could not: every rank keeps its region and row_cap
-    for (size_t i = 0; i < e->sh.size(); ++i) {
+  const auto release_fresh = [&](size_t from) {
+    for (size_t i = from; i < e->sh.size(); ++i) {
       if (fresh[i]) hipFree(fresh[i]);
       for (uint32_t* q : rx[i])
         if (q) hipFree(q);
     }
+  };
+  if (int32_t rc = rank_min(e, ok)) {
+    release_fresh(0);
+    return rc;
+  }
+  if (!ok) {  // some rank could not: every rank keeps its region and row_cap
+    release_fresh(0);
     return SWIM_OK;
   }
   // 2. every rank unmaps the others' regions before any region is freed
@@ -640,13 +649,18 @@ static int32_t grow_rows_for_joins(swim_engine* e) {
     for (void* q : sd.ipc_open) hipIpcCloseMemHandle(q);
     sd.ipc_open.clear();
     if (nccl_ok(ncclAllReduce(e->d_cnt, e->d_cnt, 1, ncclUint32, ncclMax, e->comm, e->stream)) != SWIM_OK ||
-        hipStreamSynchronize(e->stream) != hipSuccess)
+        hipStreamSynchronize(e->stream) != hipSuccess) {
+      release_fresh(0);
       return SWIM_EDEVICE;
+    }
   }
   // 3. the switch: headers carried over, old regions and copies released
   for (size_t i = 0; i < e->sh.size(); ++i) {
     Shard& sd = e->sh[i];
-    xreg_install(e, sd, fresh[i], (uint32_t)cap);
+    if (int32_t rc = xreg_install(e, sd, fresh[i], (uint32_t)cap)) {
+      release_fresh(i);  // (shards before i switched; the device is unusable anyway)
+      return rc;
+    }
     if (pulled)
       for (int k = 0; k < 2; ++k) {
         sd.release(sd.rx_rows_h[k]);
@@ -744,7 +758,7 @@ static int32_t run_tick(swim_engine* e) {
   if (int32_t rc = grow_rows_for_joins(e)) return rc;
   if (int32_t rc = grow_for_joins(e)) return rc;
   const uint64_t T = e->T;
-  const bool multi = e->world > 1;
+  const bool multi = e->xchg;
   const bool gossip_tick = e->g_residue[e->T % e->G] != 0;
   for (Shard& sd : e->sh) {
     sd.c.T = e->T;
@@ -900,8 +914,13 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
   QuietCtl* q = e->d_quiet + e->q_par;  // reset by the previous window's apply (or at creation)
   QuietCtl* q_next = e->d_quiet + (e->q_par ^ 1u);
   e->q_par ^= 1u;
-  // the previous window's apply found this one's end already (no scan), and precomputes the next
-  const bool pre_ok = e->pre_on && !e->rccl && e->pristine;
+  // the previous window's apply found this one's end already (no scan), and precomputes the next.
+  // RCCL: each rank's apply precomputed its own rows' end; the window is their minimum (one 8-byte
+  // allreduce below instead of the scan and the refs' allreduces — a pristine cluster's refs do not
+  // change in a quiet window, so the agreement the last scan established still holds).  pre_on,
+  // pristine, pre_valid and the window's bounds are replicated host state: every rank takes the same
+  // branch and enters the same collectives.
+  const bool pre_ok = e->pre_on && e->pristine;
   const bool use_pre = pre_ok && e->pre_valid && e->pre_T0 == T0 && K <= e->pre_H;
   // (the precompute covers the longest window a call can ask for, so the next call's window, whatever
   // its length, needs no scan: the bench's timed call follows a shorter warmup call)
@@ -925,6 +944,9 @@ static int32_t run_quiet(swim_engine* e, uint32_t K, uint32_t* done) {
     ncclAllReduce(e->d_refmm + n, e->d_refmm + n, n, ncclUint32, ncclMax, e->comm, s);
     if (nccl_ok(ncclGroupEnd()) != SWIM_OK) return SWIM_EDEVICE;
   }
+  if (e->rccl && use_pre &&
+      nccl_ok(ncclAllReduce(pre_in, pre_in, 1, ncclUint64, ncclMin, e->comm, s)) != SWIM_OK)
+    return SWIM_EDEVICE;
   if (!use_pre) {
     for (Shard& sd : e->sh) {
       const uint32_t g = std::max<uint32_t>(64, grid_for(sd.c.nl, 256));
@@ -1137,23 +1159,24 @@ static XLayout xlayout(const swim_engine* e, const Bufs& b, uint32_t row_cap) {
   return L;
 }
 static size_t xreg_bytes_for(const swim_engine* e, const Bufs& b, uint32_t row_cap) { return xlayout(e, b, row_cap).bytes; }
-static void* xreg_alloc(size_t bytes, bool uncached) {
+static void* xreg_alloc(size_t bytes, bool uncached, bool* got_uncached) {
   void* p = nullptr;
   hipError_t r = hipErrorUnknown;
   if (uncached) r = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
+  if (got_uncached) *got_uncached = r == hipSuccess;
   if (r != hipSuccess) r = hipMalloc(&p, bytes);
   return r == hipSuccess ? p : nullptr;
 }
 // the shard's exchange region becomes `fresh` (sized for row_cap): everything before the rows —
 // message and SYNC headers, stops, deferred acks — keeps its offset and is carried over; the old
 // region is freed
-static void xreg_install(swim_engine* e, Shard& sd, void* fresh, uint32_t row_cap) {
+static int32_t xreg_install(swim_engine* e, Shard& sd, void* fresh, uint32_t row_cap) {
   Bufs& b = sd.b;
   const XLayout L = xlayout(e, b, row_cap);
   void* old = sd.xreg;
   if (old) {
     const size_t keep = std::min(L.o_rows0, sd.xreg_bytes);
-    if (keep) hipMemcpy(fresh, old, keep, hipMemcpyDeviceToDevice);
+    if (keep && hipMemcpy(fresh, old, keep, hipMemcpyDeviceToDevice) != hipSuccess) return SWIM_EDEVICE;
     hipFree(old);
   }
   sd.xreg = fresh;
@@ -1166,12 +1189,18 @@ static void xreg_install(swim_engine* e, Shard& sd, void* fresh, uint32_t row_ca
   b.tx_stops = reinterpret_cast<uint32_t*>(base + L.o_stops);
   b.tx_rows[0] = reinterpret_cast<uint32_t*>(base + L.o_rows0);
   b.tx_rows[1] = reinterpret_cast<uint32_t*>(base + L.o_rows1);
+  return SWIM_OK;
 }
 // (re)allocates the shard's exchange region for its row_cap; on failure the old region stays
 static int32_t alloc_xreg(swim_engine* e, Shard& sd, bool uncached) {
-  void* fresh = xreg_alloc(xreg_bytes_for(e, sd.b, sd.b.row_cap), uncached);
+  bool unc = false;
+  void* fresh = xreg_alloc(xreg_bytes_for(e, sd.b, sd.b.row_cap), uncached, &unc);
   if (!fresh) return SWIM_ENOMEM;
-  xreg_install(e, sd, fresh, sd.b.row_cap);
+  if (int32_t rc = xreg_install(e, sd, fresh, sd.b.row_cap)) {
+    hipFree(fresh);
+    return rc;
+  }
+  sd.xreg_uncached = unc;
   return SWIM_OK;
 }
 
@@ -1184,6 +1213,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.sz = e->sz;
   c.rank = shard;
   c.world = (uint32_t)e->world;
+  c.xchg = e->xchg ? 1u : 0u;
   c.lo = std::min(n, shard * e->sz);
   c.nl = std::min(n, c.lo + e->sz) - c.lo;
   const uint32_t nl = c.nl;
@@ -1248,7 +1278,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   // per receiver
   b.msg_cap = cf.message_capacity ? cf.message_capacity
                                  : (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(
-                                                                    1ull << 20, (e->world > 1 ? 2048ull : 512ull) * nl));
+                                                                    1ull << 20, (e->xchg ? 2048ull : 512ull) * nl));
   // inbox pages: the message capacity in 64-message pages plus one partial page per receiver; one
   // receiver's inbox may span pg_max pages: 64x its even share of the capacity, at least 512 pages
   // (32 Ki messages: a storm's inboxes are uneven), at most the whole pool
@@ -1271,7 +1301,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   b.sy_pool_cap = b.req_cap / 64 + std::min(nl, b.req_cap) + 64;
   b.chunks = (n + SYNC_CHUNK - 1) / SYNC_CHUNK;
   b.pool_cap = std::max<uint32_t>(1u << 22, 16 * n);
-  const bool multi = e->world > 1;
+  const bool multi = e->xchg;
   // tx capacities must be identical on every rank: both ends of a send clamp the count with them
   // (the failures storm at N = 65,536 over 2 shards sends ~24 M GOSSIP_REQs a round to the peer;
   // all peers' buffers together: 32 KiB per member of the whole cluster, 2 GiB at N = 65,536)
@@ -1467,8 +1497,10 @@ static int32_t setup_peers_rccl(swim_engine* e) {
     // no handle for an uncached allocation: an ordinary one (the consumers' loads are system-scope)
     if (alloc_xreg(e, sd, false) != SWIM_OK) return SWIM_ENOMEM;
     if (hipIpcGetMemHandle(&mine, sd.xreg) != hipSuccess) return SWIM_EDEVICE;
+    e->xflags |= SWIM_XCHG_IPC_FALLBACK;
     std::fprintf(stderr, "libswimgpu: rank %d: exchange region is cached (no IPC handle for uncached memory)\n", e->rank);
   }
+  e->xflags |= SWIM_XCHG_IPC;
   uint8_t* d_h = nullptr;
   if (hipMalloc((void**)&d_h, sizeof(hipIpcMemHandle_t) * (W + 1)) != hipSuccess) return SWIM_ENOMEM;
   std::vector<hipIpcMemHandle_t> all(W);
@@ -1555,6 +1587,7 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
   e->rank = rank;
   e->world = world;
   e->rccl = rccl;
+  e->xchg = world > 1 || rccl;
   {
     const char* p = std::getenv("SWIM_EXCHANGE_PULL");
     e->pull_rows = rccl || (p && p[0] == '1');
@@ -1588,7 +1621,7 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
     e->pre_on = !(qp && qp[0] == '0');
   }
   e->loss_h.assign(capacity, 0);
-  if (world > 1) {
+  if (e->xchg) {
     if (hipMalloc((void**)&e->d_cnt, sizeof(uint32_t) * 2) != hipSuccess) {
       delete e;
       return SWIM_ENOMEM;
@@ -1600,7 +1633,7 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
     std::memcpy(&id, comm_id, sizeof(id));
     if (nccl_ok(ncclCommInitRank(&e->comm, world, id, rank)) != SWIM_OK) { delete e; return SWIM_EDEVICE; }
   }
-  if (world > 1) {
+  if (e->xchg) {
     const int32_t rc = rccl ? setup_peers_rccl(e) : setup_peers_local(e);
     if (rc != SWIM_OK) { delete e; return rc; }
   }
@@ -1682,7 +1715,10 @@ int32_t swim_comm_unique_id(uint8_t* out) {
 int32_t swim_create_shard(const swim_config* cfg, uint32_t capacity, uint32_t n_initial, uint64_t seed, int32_t rank,
                           int32_t world, const uint8_t* comm_id, swim_engine** out) {
   if (!cfg || (world > 1 && !comm_id)) return SWIM_EINVAL;
-  if (world <= 1) return create_engine(cfg, capacity, n_initial, seed, 0, 1, false, nullptr, out);
+  // one rank without an id: the unsharded engine; one rank WITH an id: an RCCL engine of one rank,
+  // which runs the whole exchange machinery (count collectives, the IPC mapping of its own region,
+  // the row pulls, the quiet windows' allreduces) with nothing to exchange
+  if (world <= 1 && !comm_id) return create_engine(cfg, capacity, n_initial, seed, 0, 1, false, nullptr, out);
   return create_engine(cfg, capacity, n_initial, seed, rank, world, true, comm_id, out);
 }
 
@@ -1692,6 +1728,16 @@ int32_t swim_shard_info(const swim_engine* e, int32_t* rank, int32_t* world, uin
   if (world) *world = e->world;
   if (lo) *lo = e->rccl ? e->sh[0].c.lo : 0;
   if (count) *count = e->rccl ? e->sh[0].c.nl : e->n;
+  return SWIM_OK;
+}
+
+int32_t swim_exchange_info(const swim_engine* e, uint32_t* flags) {
+  if (!e || !flags) return SWIM_EINVAL;
+  uint32_t f = e->xflags;
+  if (e->xchg) f |= SWIM_XCHG_ON;
+  if (e->rccl) f |= SWIM_XCHG_RCCL;
+  if (e->xchg && e->sh[0].xreg_uncached) f |= SWIM_XCHG_UNCACHED;
+  *flags = f;
   return SWIM_OK;
 }
 
@@ -1808,7 +1854,6 @@ int32_t swim_set_member_seeds(swim_engine* e, uint32_t m, const uint32_t* seeds,
 
 // the per-member seed lists as CSR (own flags, offsets, members) on every shard (replicated)
 static int32_t upload_member_seeds(swim_engine* e) {
-  e->mseed_dirty = false;
   const uint32_t n = e->n;
   std::vector<uint32_t> off(n + 1, 0), all;
   for (uint32_t v = 0; v < n; ++v) {
@@ -1821,21 +1866,28 @@ static int32_t upload_member_seeds(swim_engine* e) {
     uint8_t* own = const_cast<uint8_t*>(sd.c.mseed_own);
     uint32_t* o = const_cast<uint32_t*>(sd.c.mseed_off);
     uint32_t* l = const_cast<uint32_t*>(sd.c.mseed);
-    if (!own && (!sd.alloc(&own, n) || !sd.alloc(&o, n + 1))) return SWIM_ENOMEM;
+    if (!own) {
+      if (!sd.alloc(&own, n) || !sd.alloc(&o, n + 1)) return SWIM_ENOMEM;
+      sd.c.mseed_own = own;
+      sd.c.mseed_off = o;
+    }
     if (all.size() > sd.mseed_cap) {
+      const size_t cap = std::max<size_t>(all.size(), 2 * sd.mseed_cap);
+      uint32_t* fresh = nullptr;
+      if (!sd.alloc(&fresh, cap)) return SWIM_ENOMEM;  // (the old list stays: the retry finds it)
       sd.release(l);
-      l = nullptr;
-      sd.mseed_cap = std::max<size_t>(all.size(), 2 * sd.mseed_cap);
-      if (!sd.alloc(&l, sd.mseed_cap)) return SWIM_ENOMEM;
+      l = fresh;
+      sd.mseed_cap = cap;
+      sd.c.mseed = l;
     }
     if (hipMemcpy(own, e->mseed_own_h.data(), n, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(o, off.data(), 4ull * (n + 1), hipMemcpyHostToDevice) != hipSuccess ||
         (!all.empty() && hipMemcpy(l, all.data(), 4ull * all.size(), hipMemcpyHostToDevice) != hipSuccess))
       return SWIM_EDEVICE;
-    sd.c.mseed_own = own;
-    sd.c.mseed_off = o;
-    sd.c.mseed = l;
   }
+  // (cleared only once every shard holds the new lists: a failure above leaves it set, and the next
+  // swim_step uploads every shard again)
+  e->mseed_dirty = false;
   return SWIM_OK;
 }
 

@@ -400,6 +400,7 @@ __device__ __forceinline__ uint32_t gslot_of(uint64_t key) {
 struct Ctx {
   uint32_t n, gcap, hcap, wheel_mask, wheel_nq;
   uint32_t lo, nl, sz, rank, world;
+  uint32_t xchg;  // the exchange machinery is on: world > 1, or an RCCL engine of one rank (swim.h)
   uint32_t P, to_ticks, relay_ticks, G, S, sync_to_ticks, tick_ms;
   uint32_t metadata_timeout;  // ms (a delayed GET_METADATA round trip must finish before it)
   int32_t ping_interval, suspicion_mult, repeat_mult, fanout, ping_req_members, seg_threshold, record_fd;

@@ -1145,7 +1145,7 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
     if (any_done) {
       m.leave_done = 1;
       c.mflag[v - c.lo] |= MF_LEAVE;
-      if (c.world > 1) {  // every shard stops sending to v at the end of this tick
+      if (c.xchg) {  // every shard stops sending to v at the end of this tick
         const uint32_t i = atomicAdd(&b.x->stop, 1u);
         if (i < b.tx_stop_cap) b.tx_stops[i] = v; else set_err(c, ERR_MSGS);
       }
@@ -1209,7 +1209,7 @@ __global__ void __launch_bounds__(256) k_fd(KP, int gossip, int collect) {
   const Ctx c = pctx(P, T);
   __shared__ uint32_t s_list[256];
   __shared__ uint32_t s_cnt;
-  if (c.world > 1 && blockIdx.x == 0 && threadIdx.x == 0) *P->b.rx_stop_n = 0;  // no leaves received yet
+  if (c.xchg && blockIdx.x == 0 && threadIdx.x == 0) *P->b.rx_stop_n = 0;  // no leaves received yet
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   // the member's schedule words, loaded alongside the timer queue's count (phase A changes none of
   // them; the FD step may set MF_FDSYNC, so mflag is reloaded after it)
@@ -1257,7 +1257,7 @@ __global__ void __launch_bounds__(256) k_fd(KP, int gossip, int collect) {
 __global__ void k_debug_exchange(KP) {
   const Ctx c = pctx(P, T);
   const Bufs& b = P->b;
-  if (threadIdx.x != 0 || blockIdx.x != 0 || c.world <= 1) return;
+  if (threadIdx.x != 0 || blockIdx.x != 0 || !c.xchg) return;
   const bool ok = b.x && b.tx_msgs && b.tx_reqs && b.tx_acks && b.tx_stops && b.tx_rows[0] && b.tx_rows[1] &&
                   b.peers && b.rx_cnt && b.rx_stops && b.rx_stop_n;
   if (!ok) atomicOr(c.err, ERR_XPTR);
@@ -3032,7 +3032,7 @@ __global__ void __launch_bounds__(256) k_fetch_due(KP) {
 __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
   const Ctx c = pctx(P, T);
   Counters* k = P->b.k;
-  Xc* x = P->c.world > 1 ? P->b.x : nullptr;
+  Xc* x = P->c.xchg ? P->b.x : nullptr;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (rebase) rebase_witness(c);
   {  // this tick's content snapshots are released; the next tick's slot counter starts at zero

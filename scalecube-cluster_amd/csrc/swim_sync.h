@@ -761,7 +761,7 @@ __global__ void __launch_bounds__(256) k_ack_delay(KP) {
   const uint32_t na = min(b.k->ack_total, b.req_cap);
   // this shard's acks: the local ones (items), then those bound for each other shard (tx_acks)
   uint32_t nt = na;
-  if (c.world > 1)
+  if (c.xchg)
     for (uint32_t d = 0; d < c.world; ++d) nt += d == c.rank ? 0u : min(b.x->ack[d], b.tx_req_cap);
   for (uint32_t u = blockIdx.x; u < nt; u += gridDim.x) {
     SyncReq* ap;

@@ -187,6 +187,7 @@ PROTOTYPES = {
     "swim_create_shard": (C.c_int32, [POINTER(swim_config), C.c_uint32, C.c_uint32, C.c_uint64, C.c_int32, C.c_int32,
                                       POINTER(C.c_uint8), POINTER(_engp)]),
     "swim_shard_info": (C.c_int32, [_engp, POINTER(C.c_int32), POINTER(C.c_int32), _u32p, _u32p]),
+    "swim_exchange_info": (C.c_int32, [_engp, _u32p]),
     "swim_step_ticks": (C.c_int32, [_engp, C.c_uint32]),
     "swim_step": (C.c_int32, [_engp, C.c_uint32]),
     "swim_now": (C.c_int32, [_engp, _u64p, _u32p, _u32p]),
@@ -275,7 +276,7 @@ class Engine:
         self.cfg = cfg
         self.capacity = int(capacity)
         h = _engp()
-        if world > 1:
+        if world > 1 or comm_id is not None:  # (world 1 with an id: an RCCL engine of one rank)
             if comm_id is None or len(comm_id) != COMM_ID_BYTES:
                 raise ValueError("a sharded engine needs the 128-byte id from comm_unique_id() on rank 0")
             cid = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(comm_id)
@@ -289,6 +290,14 @@ class Engine:
         r, w, lo, cnt = C.c_int32(), C.c_int32(), C.c_uint32(), C.c_uint32()
         _check("swim_shard_info", self.lib.swim_shard_info(self._h, byref(r), byref(w), byref(lo), byref(cnt)))
         return {"rank": r.value, "world": w.value, "lo": lo.value, "count": cnt.value}
+
+    def exchange_info(self) -> dict:
+        """swim_exchange_info: how the exchange is set up (which branch of the RCCL setup ran)"""
+        f = C.c_uint32()
+        _check("swim_exchange_info", self.lib.swim_exchange_info(self._h, byref(f)))
+        v = f.value
+        return {"flags": v, "exchange": bool(v & 1), "rccl": bool(v & 2), "uncached": bool(v & 4),
+                "ipc": bool(v & 8), "ipc_fallback_cached": bool(v & 16)}
 
     # -- lifecycle ------------------------------------------------------------------------
     def close(self) -> None:

@@ -74,9 +74,14 @@ def apply_op(e: abi.Engine, op, args):
         raise ValueError(op)
 
 
-def make_engine(lib, sc: Scenario) -> abi.Engine:
+def make_engine(lib, sc: Scenario, rccl: bool = False) -> abi.Engine:
+    """rccl: an RCCL engine of one rank (swim_create_shard with a comm id at world 1; GPU library)"""
     cfg = abi.default_config(lib, sc.preset, **sc.cfg)
-    e = abi.Engine(lib, cfg, sc.capacity, sc.n_initial, sc.seed)
+    if rccl:
+        e = abi.Engine(lib, cfg, sc.capacity, sc.n_initial, sc.seed, rank=0, world=1,
+                       comm_id=abi.comm_unique_id(lib))
+    else:
+        e = abi.Engine(lib, cfg, sc.capacity, sc.n_initial, sc.seed)
     if sc.seeds:
         e.set_seeds(list(sc.seeds))
     return e

@@ -41,29 +41,59 @@ def test_world_size_must_match_gpus():
     assert p.returncode != 0 and "WORLD_SIZE=1" in (p.stderr + p.stdout)
 
 
-def test_window_traffic_only_from_the_same_window(tmp_path, monkeypatch):
-    """roofline.traffic is taken from the newest committed PMC profile of the SAME window (same
-    --steps / --warmup), never borrowed from a window of another length."""
+def _profile(path, key, build, created, apply_bytes, emit_bytes=None):
+    eng0 = {"k_quiet_apply": {"hbm_bytes": apply_bytes, "fetch_bytes": apply_bytes, "write_bytes": [0.0] * len(apply_bytes),
+                              "us": [1.0] * len(apply_bytes)}}
+    engines = [eng0, {}]
+    if emit_bytes is not None:
+        engines.append({"k_gossip_emit": {"hbm_bytes": emit_bytes, "fetch_bytes": emit_bytes,
+                                          "write_bytes": [0.0] * len(emit_bytes), "us": [2.0] * len(emit_bytes)}})
+    path.write_text(json.dumps({"bench_key": key, "build": build, "created": created, "engines": engines}))
+
+
+def test_traffic_only_from_this_command_and_build(tmp_path, monkeypatch):
+    """roofline.traffic comes from the per-launch PMC profile of the SAME command (bench_key) and the
+    SAME build (the lib's source hash), newest by its own timestamp — never by file name order, never
+    from another window, command or build — and from the timed window's own launch."""
     sys.path.insert(0, REPO)
     import bench
     prof = tmp_path / "profiles"
     prof.mkdir()
-    for name, steps, warm, b in (("r01_quiet64k_pmc.json", 40, 10, 100.0), ("r02_quiet64k_pmc.json", 20, 5, 7.0),
-                                 ("r03_quiet64k_pmc.json", 20, 5, 9.0)):
-        (prof / name).write_text(json.dumps({"bench_args": {"steps": steps, "warmup": warm},
-                                             "kernels": {"k_quiet_apply": {"last_launch_hbm_bytes": b},
-                                                         "k_quiet_scan": {"last_launch_hbm_bytes": 1.0}}}))
+    key = {"gpus": 1, "steps": 20, "warmup": 5}
+    other = {"gpus": 1, "steps": 40, "warmup": 10}
+    # lexically last, but another build; a newer one of another command; the right one in the middle
+    _profile(prof / "r09_quiet64k_pmc.json", key, "oldbuild", "2026-01-03T00:00:00", [5.0, 6.0, 7.0])
+    _profile(prof / "r01_quiet64k_pmc.json", key, "thisbuild", "2026-01-01T00:00:00", [1.0, 2.0, 3.0])
+    _profile(prof / "r02_quiet64k_pmc.json", key, "thisbuild", "2026-01-02T00:00:00", [20.0, 31.0, 19.0],
+             emit_bytes=[1.0, 2.0, 4.0, 6.0])
+    _profile(prof / "r03_quiet64k_pmc.json", other, "thisbuild", "2026-01-05T00:00:00", [8.0, 8.0])
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
-    assert bench.window_pmc_traffic("quiet", 65536, 20, 5, scanned=False) == (9.0, "profiles/r03_quiet64k_pmc.json")
-    assert bench.window_pmc_traffic("quiet", 65536, 40, 10, scanned=True) == (101.0, "profiles/r01_quiet64k_pmc.json")
-    t, why = bench.window_pmc_traffic("quiet", 65536, 7, 3)
-    assert t is None and "not this window" in why
-    # with per-launch bytes the timed window's own launch is taken, not the last (a side run's)
-    (prof / "r04_quiet64k_pmc.json").write_text(json.dumps({
-        "bench_args": {"steps": 20, "warmup": 5},
-        "kernels": {"k_quiet_apply": {"last_launch_hbm_bytes": 50.0, "launch_hbm_bytes": [20.0, 31.0, 19.0, 50.0]}}}))
-    first = {"k_quiet_apply": 1, "k_quiet_scan": 1}
-    assert bench.window_pmc_traffic("quiet", 65536, 20, 5, scanned=False, first=first) == \
-        (31.0, "profiles/r04_quiet64k_pmc.json")
-    t, why = bench.window_pmc_traffic("quiet", 65536, 20, 5, scanned=False, first={"k_quiet_apply": 9})
-    assert t is None and "the timed one is #9" in why
+    monkeypatch.setattr(bench, "build_hash", lambda: "thisbuild")
+    monkeypatch.setattr(bench, "_PROFILE", {})
+    t, src, us = bench.window_pmc_traffic(key, scanned=False, first={"k_quiet_apply": 1})
+    assert (t, src, us) == (31.0, "profiles/r02_quiet64k_pmc.json", 1.0)
+    # the timed launch is past the profile's list: no traffic, and a reason
+    t, why, _ = bench.window_pmc_traffic(key, scanned=False, first={"k_quiet_apply": 9})
+    assert t is None and "no launch #9" in why
+    # a scanned window needs the scan's launch too
+    t, why, _ = bench.window_pmc_traffic(key, scanned=True, first={"k_quiet_apply": 1, "k_quiet_scan": 1})
+    assert t is None and "k_quiet_scan" in why
+    # a command nobody profiled on this build
+    t, why, _ = bench.window_pmc_traffic({"gpus": 1, "steps": 7, "warmup": 3}, scanned=False, first={"k_quiet_apply": 0})
+    assert t is None and "measured this command on this build" in why
+    # the storm window: the mean of the last launches of the side run's engine (#2)
+    w, src, n = bench.window_traffic(key, 2, ("k_gossip_emit",), 2)
+    assert w["hbm"] == 5.0 and w["us"] == 2.0 and src == "profiles/r02_quiet64k_pmc.json"
+    w, why, _ = bench.window_traffic(key, 2, ("k_gossip_emit",), 9)
+    assert w is None and "fewer than 9 launches" in why
+
+
+def test_headline_launch_index_counts_attempts():
+    """k_quiet_apply is launched on every window attempt (also one that advances no tick) and once per
+    local shard: the timed launch's index counts attempts x shards, not windows"""
+    sys.path.insert(0, REPO)
+    import bench
+    # a warm-up with a failed attempt (attempts > windows) and one precomputed window
+    qs0 = {"windows": 2, "attempts": 3, "precomputed": 1}
+    assert bench.timed_launch_index(qs0) == {"k_quiet_apply": 3, "k_quiet_scan": 2}
+    assert bench.timed_launch_index(qs0, 4) == {"k_quiet_apply": 12, "k_quiet_scan": 8}

@@ -26,7 +26,7 @@ N = 65536
 BOUNDARY_ROWS = [0, 1, 1023, 1024, 2047, 2048, 4095, 4096, 32767, 32768, 65534, 65535]
 
 
-def _engines(glib, workload, periods, local_shards=1):
+def _engines(glib, workload, periods, local_shards=1, rccl=False):
     from swimgpu import abi
     out = {}
     for k, lib in (("gpu", glib), ("oracle", oracle.lib())):
@@ -34,7 +34,10 @@ def _engines(glib, workload, periods, local_shards=1):
         cfg = bench.make_config(lib)
         if k == "gpu":
             cfg.local_shards = local_shards
-        e = abi.Engine(lib, cfg, sch.capacity, N, 1)
+        if k == "gpu" and rccl:  # an RCCL engine of one rank (swim_create_shard, world 1 with an id)
+            e = abi.Engine(lib, cfg, sch.capacity, N, 1, rank=0, world=1, comm_id=abi.comm_unique_id(lib))
+        else:
+            e = abi.Engine(lib, cfg, sch.capacity, N, 1)
         sch.setup(e)
         out[k] = (e, sch)
     oracle.set_threads(out["oracle"][0], THREADS)
@@ -172,6 +175,68 @@ def test_failures_sharded8_65536_first_kill_matches_oracle(glib):
                          list(range(733, N, 2729))[:20]))
     p = 0
     try:
+        for upto in (10, 11, 12, 14):
+            for k in ("gpu", "oracle"):
+                e, sch = eng[k]
+                sch.run(e, p, upto)
+            p = upto
+            _, st = _compare(eng, members, f"period {p}")
+        assert st["gossips_created"] > 0 and st["gossip_messages"] > 0
+    finally:
+        for e, _ in eng.values():
+            e.close()
+
+
+def _rccl_info(g):
+    """which branch of the RCCL setup ran (an IPC handle of the uncached region, or the cached
+    fallback), also written to gpurun_out/rccl_exchange_info.json on the GPU box"""
+    import json
+    info = g.exchange_info()
+    print("RCCL exchange on one GPU:", info, flush=True)
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, "rccl_exchange_info.json"), "w") as f:
+            json.dump(info, f)
+    assert info["exchange"] and info["rccl"] and info["ipc"], info
+    return info
+
+
+def test_rccl_world1_quiet_65536_stepped_like_bench(glib):
+    """The RCCL transport executed on hardware with one rank: swim_create_shard with a
+    comm id at world 1 runs the whole exchange machinery — the IPC handle of the exchange region
+    (uncached, or the cached fallback: exchange_info says which) and its ncclAllGather, a count
+    ncclAllToAll per exchange, k_recv_msgs / k_pack_rows / k_recv_sync / k_pull_rows every tick, and
+    the quiet windows' collectives — the refs' and the window end's allreduces of a scanned window,
+    the precomputed end's 8-byte allreduce of the windows after it — on the headline workload stepped
+    as bench.py times it, bit-exact against the unsharded oracle."""
+    eng = _engines(glib, "quiet", 30, rccl=True)
+    members = BOUNDARY_ROWS + list(range(517, N, 2311))[:28]
+    try:
+        g = eng["gpu"][0]
+        _rccl_info(g)
+        g.set_quiet_path(False)
+        st = _run_steps(eng, members, (2,))  # the per-tick chain with its exchange kernels
+        g.set_quiet_path(True)
+        q0 = g.quiet_stats()
+        st = _run_steps(eng, members, (3, 20, 5), p=2)
+        q1 = g.quiet_stats()
+        assert st["pings"] == N * 30 and st["syncs"] > 0
+        assert q1["ticks"] - q0["ticks"] >= 250 and q1["precomputed"] - q0["precomputed"] >= 2, (q0, q1)
+    finally:
+        for e, _ in eng.values():
+            e.close()
+
+
+def test_rccl_world1_failures_first_kill_65536_matches_oracle(glib):
+    """The failures workload through its first kill on the one-rank RCCL engine: the SUSPECT storm's
+    gossip rounds each run E1's count all-to-all and stop all-gather, the SYNC sub-phases E2 / E3's;
+    against the unsharded oracle after periods 10, 11, 12, 14."""
+    eng = _engines(glib, "failures", 14, rccl=True)
+    victim = 17
+    members = BOUNDARY_ROWS + [16, victim, 18] + list(range(733, N, 2729))[:24]
+    p = 0
+    try:
+        _rccl_info(eng["gpu"][0])
         for upto in (10, 11, 12, 14):
             for k in ("gpu", "oracle"):
                 e, sch = eng[k]

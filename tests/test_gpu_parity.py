@@ -52,9 +52,10 @@ def test_gpu_cluster_math(glib):
     kat.check_cluster_math(glib)
 
 
-def _run_parity(glib, olib, sc, members=None, collectors=True):
-    """Run both engines through `sc` in lockstep, comparing full state at every checkpoint."""
-    oe, ge = scenarios.make_engine(olib, sc), scenarios.make_engine(glib, sc)
+def _run_parity(glib, olib, sc, members=None, collectors=True, rccl=False):
+    """Run both engines through `sc` in lockstep, comparing full state at every checkpoint (rccl: the
+    GPU engine is an RCCL engine of one rank, swim_create_shard with a comm id at world 1)."""
+    oe, ge = scenarios.make_engine(olib, sc), scenarios.make_engine(glib, sc, rccl=rccl)
     ops = sorted(sc.ops, key=lambda x: x[0])
     t, oi = 0, 0
     oev, gev = [], []
@@ -154,6 +155,26 @@ def test_gpu_sharded_row_cap_grows_for_join_burst(glib, olib, name, shards, pull
     if pull:
         monkeypatch.setenv("SWIM_EXCHANGE_PULL", "1")
     _run_parity(glib, olib, dataclasses.replace(sc, cfg={**sc.cfg, "local_shards": shards}))
+
+
+# ---- the RCCL transport on one GPU: an RCCL engine of ONE rank runs every exchange step of the
+# sharded tick (the count ncclAllToAll / stop ncclAllGather per exchange, the IPC-mapped region,
+# k_recv_* / k_pack_rows / k_pull_rows, the quiet windows' allreduces, row_cap growth agreed by
+# rank_min) with nothing crossing; bit-exact against the unsharded oracle
+RCCL_SCENARIOS = ("config1_kill", "mp_joins_via_seed", "churn_48", "partition_heal_32", "restart_same_address_40",
+                  "sync_delay_24", "delay_fd_gossip_12", "user_gossip_10_loss25", "sync_ack_waits_24")
+
+
+@pytest.mark.parametrize("name", RCCL_SCENARIOS)
+def test_gpu_rccl_world1_parity_scenario(glib, olib, name):
+    sc = {s.name: s for s in scenarios.catalog()}[name]
+    _run_parity(glib, olib, sc, rccl=True)
+
+
+def test_gpu_rccl_world1_row_cap_grows_for_join_burst(glib, olib, monkeypatch):
+    sc = {s.name: s for s in scenarios.catalog()}["join_burst_144"]
+    monkeypatch.setenv("SWIM_DEBUG_ROW_CAP", "16")
+    _run_parity(glib, olib, sc, rccl=True)
 
 
 def test_gpu_sharded_parity_config2_1024(glib, olib):
