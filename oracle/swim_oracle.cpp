@@ -16,7 +16,9 @@
 // the JVM's ThreadLocalRandom.
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <new>
 #include <thread>
@@ -101,61 +103,154 @@ struct PendingAck {
 // ----------------------------------------------------------------------------- SequenceIdCollector
 // gossip/SequenceIdCollector.java:11-94 — closed intervals [a,b] in a TreeMap.
 struct SeqCollector {
-  std::map<int64_t, int64_t> iv;
-  static bool in_range(std::map<int64_t, int64_t>::iterator it, bool ok, int64_t x) {
-    return ok && it->first <= x && x <= it->second;
+  // the TreeMap<Long, Long> of disjoint closed intervals [a, b] keyed by a, as a vector sorted by a
+  // (a few intervals per collector: contiguous, 16 B each, where map nodes cost 64)
+  std::vector<std::pair<int64_t, int64_t>> iv;
+  // floorEntry(x): the last interval with a <= x, or -1
+  ptrdiff_t floor_idx(int64_t x) const {
+    auto it = std::upper_bound(iv.begin(), iv.end(), x,
+                               [](int64_t v, const std::pair<int64_t, int64_t>& p) { return v < p.first; });
+    return (it - iv.begin()) - 1;
   }
-  static bool next_to(std::map<int64_t, int64_t>::iterator it, bool ok, int64_t x) {
-    return ok && (x + 1 == it->first || x - 1 == it->second);
+  // ceilingEntry(x): the first interval with a >= x (iv.size() if none)
+  size_t ceil_idx(int64_t x) const {
+    return (size_t)(std::lower_bound(iv.begin(), iv.end(), x,
+                                     [](const std::pair<int64_t, int64_t>& p, int64_t v) { return p.first < v; }) -
+                    iv.begin());
   }
-  bool contains(int64_t x) {  // :32-35
-    auto it = iv.upper_bound(x);
-    if (it == iv.begin()) return false;
-    --it;
-    return in_range(it, true, x);
+  bool in_range(ptrdiff_t i, int64_t x) const { return i >= 0 && iv[i].first <= x && x <= iv[i].second; }
+  bool next_to(ptrdiff_t i, int64_t x) const {
+    return i >= 0 && (size_t)i < iv.size() && (x + 1 == iv[i].first || x - 1 == iv[i].second);
   }
+  bool contains(int64_t x) const { return in_range(floor_idx(x), x); }  // :32-35
   bool add(int64_t x) {  // :43-72
-    auto fl = iv.upper_bound(x);
-    bool has_fl = fl != iv.begin();
-    if (has_fl) --fl;
-    if (in_range(fl, has_fl, x)) return false;
-    auto ce = iv.lower_bound(x);
-    bool has_ce = ce != iv.end();
-    bool nf = next_to(fl, has_fl, x), nc = next_to(ce, has_ce, x);
-    if (nf && nc) {
-      int64_t a = fl->first, b = ce->second;
-      iv.erase(fl->first);
-      iv.erase(ce->first);
-      iv[a] = b;
+    const ptrdiff_t fl = floor_idx(x);
+    if (in_range(fl, x)) return false;
+    const ptrdiff_t ce = (ptrdiff_t)ceil_idx(x);  // (fl + 1: x is in no interval)
+    const bool nf = next_to(fl, x), nc = next_to(ce, x);
+    if (nf && nc) {  // both neighbours: one interval [floor.a, ceiling.b]
+      iv[fl].second = iv[ce].second;
+      iv.erase(iv.begin() + ce);
     } else if (nf) {
-      int64_t a = fl->first;
-      iv.erase(a);
-      iv[a] = x;
+      iv[fl].second = x;
     } else if (nc) {
-      int64_t b = ce->second;
-      iv.erase(ce->first);
-      iv[x] = b;
+      iv[ce].first = x;
     } else {
-      iv[x] = x;
+      iv.insert(iv.begin() + ce, {x, x});
     }
     return true;
   }
   size_t size() const { return iv.size(); }
-  void clear() { iv.clear(); }
+  void clear() {
+    iv.clear();
+    iv.shrink_to_fit();
+  }
 };
 
 // GossipState (gossip/GossipState.java:9-49) with its Gossip (Gossip.java, id = gossiper-seq)
-struct GossipState {
-  uint32_t gossiper;
-  uint64_t seq;
-  Record rec;
-  uint64_t infection_period;
-  std::vector<uint32_t> infected;  // HashSet<String>, kept in insertion order
-  bool is_infected(uint32_t m) const {
-    return std::find(infected.begin(), infected.end(), m) != infected.end();
+// GossipState.infected, a HashSet<String> (GossipState.java:14), kept in insertion order: the first
+// two members inline, the rest on the heap (almost every state holds one or two: no allocation)
+struct InfSet {
+  uint32_t a = 0xffffffffu, b = 0xffffffffu;
+  std::vector<uint32_t>* more = nullptr;  // owned
+  InfSet() = default;
+  InfSet(const InfSet& o) : a(o.a), b(o.b), more(o.more ? new std::vector<uint32_t>(*o.more) : nullptr) {}
+  InfSet(InfSet&& o) noexcept : a(o.a), b(o.b), more(o.more) { o.more = nullptr; }
+  InfSet& operator=(InfSet o) noexcept {
+    a = o.a;
+    b = o.b;
+    std::swap(more, o.more);
+    return *this;
   }
+  ~InfSet() { delete more; }
+  size_t size() const { return (a != 0xffffffffu) + (b != 0xffffffffu) + (more ? more->size() : 0); }
+  uint32_t operator[](size_t i) const { return i == 0 ? a : i == 1 ? b : (*more)[i - 2]; }
+  bool contains(uint32_t m) const {
+    return a == m || b == m || (more && std::find(more->begin(), more->end(), m) != more->end());
+  }
+  void push_back(uint32_t m) {
+    if (a == 0xffffffffu) a = m;
+    else if (b == 0xffffffffu) b = m;
+    else {
+      if (!more) more = new std::vector<uint32_t>();
+      more->push_back(m);
+    }
+  }
+};
+
+// 40 B: the oracle keeps every live state of every member (config 3 at N = 4,096: ~4 x 10^8)
+struct GossipState {
+  uint32_t seq;               // Gossip.sequenceId (a member's own counter: < 2^32)
+  uint32_t infection_period;  // GossipState.infectionPeriod (< 2^28, the engines' period bound)
+  uint32_t gossiper;
+  Record rec;
+  InfSet infected;  // HashSet<String>, kept in insertion order
+  bool is_infected(uint32_t m) const { return infected.contains(m); }
   void add_infected(uint32_t m) {
     if (!is_infected(m)) infected.push_back(m);
+  }
+};
+
+// gossips.get(gossipId) (GossipProtocolImpl.java:206), the HashMap index of a member's gossip map:
+// open addressing with linear probing and backward-shift deletion over 4-B slots, each the serial of
+// a state (its insertion number: its position plus the states swept before it); a slot's key is
+// read from the state itself (key_of)
+struct GossipIndex {
+  static constexpr uint32_t EMPTY = 0xffffffffu;
+  std::vector<uint32_t> slot;
+  size_t used = 0;
+  static size_t hash(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    return (size_t)x;
+  }
+  template <class KeyOf>
+  void rehash(size_t cap, KeyOf key_of) {
+    std::vector<uint32_t> old;
+    old.swap(slot);
+    slot.assign(cap, EMPTY);
+    used = 0;
+    for (uint32_t s : old)
+      if (s != EMPTY) put(key_of(s), s, key_of);
+  }
+  template <class KeyOf>
+  void put(uint64_t k, uint32_t s, KeyOf key_of) {
+    if (2 * (used + 1) > slot.size()) rehash(std::max<size_t>(64, 2 * slot.size()), key_of);
+    const size_t mask = slot.size() - 1;
+    for (size_t i = hash(k) & mask;; i = (i + 1) & mask) {
+      if (slot[i] == EMPTY) { slot[i] = s; ++used; return; }
+      if (key_of(slot[i]) == k) { slot[i] = s; return; }
+    }
+  }
+  template <class KeyOf>
+  bool get(uint64_t k, uint32_t& s, KeyOf key_of) const {
+    if (slot.empty()) return false;
+    const size_t mask = slot.size() - 1;
+    for (size_t i = hash(k) & mask;; i = (i + 1) & mask) {
+      if (slot[i] == EMPTY) return false;
+      if (key_of(slot[i]) == k) { s = slot[i]; return true; }
+    }
+  }
+  template <class KeyOf>
+  void erase(uint64_t k, KeyOf key_of) {
+    if (slot.empty()) return;
+    const size_t mask = slot.size() - 1;
+    size_t i = hash(k) & mask;
+    while (slot[i] == EMPTY || key_of(slot[i]) != k) {
+      if (slot[i] == EMPTY) return;
+      i = (i + 1) & mask;
+    }
+    // backward shift: move later entries of the run into the hole when their home allows it
+    for (size_t j = (i + 1) & mask; slot[j] != EMPTY; j = (j + 1) & mask) {
+      const size_t h = hash(key_of(slot[j])) & mask;
+      if (((j - h) & mask) >= ((j - i) & mask)) {
+        slot[i] = slot[j];
+        i = j;
+      }
+    }
+    slot[i] = EMPTY;
+    --used;
   }
 };
 
@@ -189,22 +284,50 @@ struct Member {
   // ---- GossipProtocolImpl (:48-55)
   uint64_t g_period = 0, g_counter = 0, period_used = 0;
   std::unordered_map<uint32_t, SeqCollector> collectors;
-  std::vector<GossipState> gossips;  // insertion order == canonical order
-  std::unordered_map<uint64_t, uint32_t> gidx;  // gossips.get(gossipId): id -> position (HashMap lookup)
+  std::deque<GossipState> gossips;  // insertion order == canonical order
+  GossipIndex gidx;                 // gossips.get(gossipId): id -> serial (HashMap lookup)
+  uint32_t gbase = 0;               // serial of gossips.front() (states swept so far)
+  uint32_t user_own = 0;            // own user gossips whose spread() has not completed
+  // the first state in the spreading window (infectionPeriod + periodsToSpread >= period): infection
+  // periods never decrease along the map, so the window is a suffix, found by binary search
+  size_t window_start(uint64_t period, uint64_t spread) const {
+    size_t lo = 0, hi = gossips.size();
+    while (lo < hi) {
+      const size_t mid = (lo + hi) / 2;
+      if (gossips[mid].infection_period + spread >= period) hi = mid;
+      else lo = mid + 1;
+    }
+    return lo;
+  }
+  // (injective: gossiper < 2^24, seq < 2^32)
   static uint64_t gkey(uint32_t gossiper, uint64_t seq) { return ((uint64_t)gossiper << 40) ^ seq; }
+  uint64_t key_at(uint32_t serial) const {
+    const GossipState& g = gossips[serial - gbase];
+    return gkey(g.gossiper, g.seq);
+  }
   GossipState* find_gossip(uint32_t gossiper, uint64_t seq) {
-    auto it = gidx.find(gkey(gossiper, seq));
-    if (it == gidx.end()) return nullptr;
-    GossipState& g = gossips[it->second];
-    return (g.gossiper == gossiper && g.seq == seq) ? &g : nullptr;
+    uint32_t s = 0;
+    if (!gidx.get(gkey(gossiper, seq), s, [&](uint32_t x) { return key_at(x); })) return nullptr;
+    return &gossips[s - gbase];
   }
   void add_gossip(const GossipState& g) {
-    gidx[gkey(g.gossiper, g.seq)] = (uint32_t)gossips.size();
+    if (gbase + gossips.size() >= 0xffffffffull) std::abort();  // (serials are 32-bit)
     gossips.push_back(g);
+    const uint32_t s = gbase + (uint32_t)gossips.size() - 1;
+    gidx.put(gkey(g.gossiper, g.seq), s, [&](uint32_t x) { return key_at(x); });
   }
-  void reindex_gossips() {
-    gidx.clear();
-    for (uint32_t i = 0; i < gossips.size(); ++i) gidx[gkey(gossips[i].gossiper, gossips[i].seq)] = i;
+  // the sweep (:158-164, :350-358) drops the states with period > infectionPeriod + sweep.  Infection
+  // periods never decrease along the map (a state takes its holder's current period when it is
+  // added), so those are a prefix: dropped from the front, the index loses their keys only
+  void sweep_gossips(uint64_t period, uint64_t sweep) {
+    size_t p0 = 0;
+    while (p0 < gossips.size() && period > gossips[p0].infection_period + sweep) ++p0;
+    for (size_t i = p0; i < gossips.size(); ++i)
+      if (period > gossips[i].infection_period + sweep) std::abort();  // (not a prefix: impossible)
+    for (size_t i = 0; i < p0; ++i)  // (the keys leave the index while their states still exist)
+      gidx.erase(key_at(gbase + (uint32_t)i), [&](uint32_t x) { return key_at(x); });
+    for (size_t i = 0; i < p0; ++i) gossips.pop_front();
+    gbase += (uint32_t)p0;
   }
   std::vector<uint32_t> remote;
   int32_t remote_index = -1;
@@ -474,9 +597,9 @@ struct swim_engine {
     Member& mv = m[v];
     GossipState g;
     g.gossiper = v;
-    g.seq = mv.g_counter++;
+    g.seq = (uint32_t)mv.g_counter++;
     g.rec = r;
-    g.infection_period = mv.g_period;
+    g.infection_period = (uint32_t)mv.g_period;
     mv.add_gossip(g);
     mv.collectors[v].add((int64_t)g.seq);
     STT().gossips_created++;
@@ -489,6 +612,7 @@ struct swim_engine {
   // the record's member field (status SWIM_GOSSIP_USER)
   void spread_user(uint32_t v, uint32_t payload) {
     spread_gossip(v, Record{payload, SWIM_GOSSIP_USER, 0}, SWIM_ORIG_USER);
+    m[v].user_own++;
   }
 
   // ------------------------------------------------------------------------- timers
@@ -920,12 +1044,28 @@ struct swim_engine {
   }
 
   // ------------------------------------------------------------------------- phase C: gossip
-  struct GMsg {
+  // what a GOSSIP_REQ carries that onGossipReq reads (:201-215): the gossip's id and its record — not
+  // the sender's GossipState (its infected set stays at the sender; a copy per message would allocate)
+  struct GossipRef {
+    uint32_t gossiper;
+    uint64_t seq;
+    Record rec;
+  };
+  // A delayed GOSSIP_REQ carries its gossip with it (GMsgD, in flight across ticks); a round's
+  // messages (GMsg, 20 B: a storm's round materialises 10^8-10^9 of them) refer to the round's table of
+  // the gossips its senders sent (ref = table << 26 | index: one table per producer thread, plus one
+  // for the delayed messages arriving now)
+  struct GMsgD {
     uint32_t to, from, pos;
-    GossipState g;
+    GossipRef g;
     uint64_t sent;  // tick of the round that sent it (a delayed message arrives in a later tick)
   };
-  std::map<uint64_t, std::vector<GMsg>> gossip_in_flight;  // arrival tick -> delayed GOSSIP_REQs
+  struct GMsg {
+    uint32_t to, from, pos, ref;
+    uint32_t sent;  // (ticks < 2^32)
+  };
+  static constexpr uint32_t REF_BITS = 26;
+  std::map<uint64_t, std::vector<GMsgD>> gossip_in_flight;  // arrival tick -> delayed GOSSIP_REQs
 
   // selectGossipMembers (GossipProtocolImpl.java:322-343)
   std::vector<uint32_t> select_gossip_members(uint32_t v) {
@@ -946,7 +1086,7 @@ struct swim_engine {
     for (uint32_t v = 0; v < n; ++v)
       if (gossip_due(m[v])) due.push_back(v);
     // GOSSIP_REQs delayed by the network emulator that arrive now (tryDelayOutbound :190-202)
-    std::vector<GMsg> arriving;
+    std::vector<GMsgD> arriving;
     {
       auto it = gossip_in_flight.find(T);
       if (it != gossip_in_flight.end()) {
@@ -972,7 +1112,8 @@ struct swim_engine {
     for (uint32_t t = 0; t <= nt; ++t) rb[t] = (uint32_t)((uint64_t)n * t / nt);
     auto consumer = [&](uint32_t to) { return (uint32_t)(std::upper_bound(rb.begin(), rb.end(), to) - rb.begin()) - 1; };
     std::vector<std::vector<std::vector<GMsg>>> bucket(nt, std::vector<std::vector<GMsg>>(nt));
-    std::vector<std::vector<GMsg>> later(nt);  // delayed sends, by producer
+    std::vector<std::vector<GMsgD>> later(nt);  // delayed sends, by producer
+    std::vector<std::vector<GossipRef>> sent_tab(nt + 1);  // the gossips sent this round, by producer
     bool any = false;
     par(0, nd, [&](uint32_t a, uint32_t b, uint32_t t) {
       for (uint32_t i = a; i < b; ++i) {
@@ -984,36 +1125,44 @@ struct swim_engine {
         const int32_t size1 = (int32_t)mv.remote.size() + 1;
         const uint64_t spread = (uint64_t)swim_gossip_periods_to_spread(cfg.gossip_repeat_mult, size1);
         const uint64_t sweep = (uint64_t)swim_gossip_periods_to_sweep(cfg.gossip_repeat_mult, size1);
+        // selectGossipsToSend (:311-320): the states in the window, a suffix of the map
+        const uint32_t w0 = (uint32_t)mv.window_start(period, spread), nw = (uint32_t)mv.gossips.size();
+        const uint32_t tab0 = (uint32_t)sent_tab[t].size();
+        for (uint32_t p = w0; p < nw; ++p) {
+          const GossipState& g = mv.gossips[p];
+          sent_tab[t].push_back(GossipRef{g.gossiper, g.seq, g.rec});
+        }
+        if (sent_tab[t].size() >= (1u << REF_BITS)) std::abort();  // (refs are 26-bit)
         for (uint32_t j = 0; j < targets.size(); ++j) {
           const uint32_t tg = targets[j], rc = dst(tg);  // sent to tg's address, received by rc
-          for (uint32_t p = 0; p < mv.gossips.size(); ++p) {  // selectGossipsToSend (:311-320)
+          for (uint32_t p = w0; p < nw; ++p) {
             const GossipState& g = mv.gossips[p];
-            if (!(g.infection_period + spread >= period)) continue;
             if (g.is_infected(tg)) continue;
             STT().gossip_messages++;
             if (out_fail(v, rc, draw(v, SWIM_STREAM_GOSSIP_OUT, j, p))) continue;
             // the receiver's inbound filter applies when the message arrives (listen() :78-83): now,
             // or at the delayed message's arrival tick
             const uint32_t k = delay_ticks(v, rc, v, SWIM_STREAM_GOSSIP_DELAY, j, p);
-            if (k) later[t].push_back(GMsg{rc, v, p, g, T + k});
-            else if (in_pass(rc, v)) bucket[t][consumer(rc)].push_back(GMsg{rc, v, p, g, T});
+            if (k) later[t].push_back(GMsgD{rc, v, p, GossipRef{g.gossiper, g.seq, g.rec}, T + k});
+            else if (in_pass(rc, v))
+              bucket[t][consumer(rc)].push_back(GMsg{rc, v, p, (t << REF_BITS) | (tab0 + p - w0), (uint32_t)T});
           }
         }
         // sweep (:158-164, :350-358)
-        std::vector<GossipState> keep;
-        keep.reserve(mv.gossips.size());
-        for (auto& g : mv.gossips)
-          if (!(period > g.infection_period + sweep)) keep.push_back(std::move(g));
-        mv.gossips.swap(keep);
-        mv.reindex_gossips();
-        // futures (:167-180, :360-368): the graceful-leave future, and spread() of user gossips
-        for (auto& g : mv.gossips) {
-          if (!(period > g.infection_period + spread)) continue;
-          if (mv.leave_pending && g.gossiper == mv.leave_gossiper && g.seq == mv.leave_seq) mv.leave_done = true;
-          if (g.rec.status == SWIM_GOSSIP_USER && g.gossiper == v) {
-            g.rec.status = SWIM_GOSSIP_USER_SPREAD;
-            emit(v, v, SWIM_EV_SPREAD_DONE, SWIM_PHASE_GOSSIP, 0x80000000u | (uint32_t)(g.seq & 0x7fffffffu),
-                 g.rec.member);
+        mv.sweep_gossips(period, sweep);
+        // futures (:167-180, :360-368): the graceful-leave future, and spread() of user gossips — the
+        // states before the window (a prefix), looked at only while such a future is pending
+        if (mv.leave_pending || mv.user_own) {
+          const size_t wf = mv.window_start(period, spread);  // (the states with period > infectionPeriod + spread)
+          for (size_t p = 0; p < wf; ++p) {
+            GossipState& g = mv.gossips[p];
+            if (mv.leave_pending && g.gossiper == mv.leave_gossiper && g.seq == mv.leave_seq) mv.leave_done = true;
+            if (g.rec.status == SWIM_GOSSIP_USER && g.gossiper == v) {
+              g.rec.status = SWIM_GOSSIP_USER_SPREAD;
+              mv.user_own--;
+              emit(v, v, SWIM_EV_SPREAD_DONE, SWIM_PHASE_GOSSIP, 0x80000000u | (uint32_t)(g.seq & 0x7fffffffu),
+                   g.rec.member);
+            }
           }
         }
         // PendingAck waits on LEAVING gossips (onLeavingDetected's spread() Monos): every gossip of one
@@ -1034,7 +1183,12 @@ struct swim_engine {
         gossip_in_flight[at].push_back(std::move(x));
       }
     for (auto& x : arriving)  // delayed GOSSIP_REQs arriving now: the receiver's inbound filter now
-      if (in_pass(x.to, x.from)) bucket[0][consumer(x.to)].push_back(std::move(x));
+      if (in_pass(x.to, x.from)) {
+        bucket[0][consumer(x.to)].push_back(
+            GMsg{x.to, x.from, x.pos, (nt << REF_BITS) | (uint32_t)sent_tab[nt].size(), (uint32_t)x.sent});
+        sent_tab[nt].push_back(x.g);
+      }
+    std::vector<GMsgD>().swap(arriving);
     for (auto& bp : bucket)
       for (auto& bc : bp) any |= !bc.empty();
     if (!any) return;
@@ -1043,7 +1197,10 @@ struct swim_engine {
       std::vector<GMsg> msgs;
       for (uint32_t d = 0; d < nt; ++d)
         if (rb[d] >= ra && rb[d + 1] <= rbnd)
-          for (uint32_t pr = 0; pr < nt; ++pr) msgs.insert(msgs.end(), bucket[pr][d].begin(), bucket[pr][d].end());
+          for (uint32_t pr = 0; pr < nt; ++pr) {
+            msgs.insert(msgs.end(), bucket[pr][d].begin(), bucket[pr][d].end());
+            std::vector<GMsg>().swap(bucket[pr][d]);  // (this worker is its only reader)
+          }
       // canonical order: (receiver, sending round, sender, slab position); keys are unique
       std::sort(msgs.begin(), msgs.end(), [](const GMsg& a, const GMsg& b) {
         if (a.to != b.to) return a.to < b.to;
@@ -1062,16 +1219,16 @@ struct swim_engine {
           mr.fetch_ctr = 0;
         }
         if (!mr.up) continue;
-        const GossipState& g = msg.g;
+        const GossipRef& g = sent_tab[msg.ref >> REF_BITS][msg.ref & ((1u << REF_BITS) - 1)];
         if (!mr.collectors[g.gossiper].add((int64_t)g.seq)) continue;
         STT().gossip_accepted++;
         GossipState* state = mr.find_gossip(g.gossiper, g.seq);  // gossips.get(gossipId) (:206)
         if (state == nullptr) {
           GossipState ns;
           ns.gossiper = g.gossiper;
-          ns.seq = g.seq;
+          ns.seq = (uint32_t)g.seq;
           ns.rec = g.rec;
-          ns.infection_period = mr.g_period;
+          ns.infection_period = (uint32_t)mr.g_period;
           ns.infected.push_back(msg.from);
           mr.add_gossip(ns);
           if (g.rec.status >= SWIM_GOSSIP_USER) {  // sink.next(gossip.message()) (:209): listen()

@@ -1305,7 +1305,11 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   // tx capacities must be identical on every rank: both ends of a send clamp the count with them
   // (the failures storm at N = 65,536 over 2 shards sends ~24 M GOSSIP_REQs a round to the peer;
   // all peers' buffers together: 32 KiB per member of the whole cluster, 2 GiB at N = 65,536)
-  b.tx_msg_cap = multi ? (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>(1ull << 20, 1024ull * e->sz)) : 0;
+  // (an explicit message_capacity — a shard's inbox — also sizes each destination's share of the
+  // outgoing buffer: message_capacity / world, when that is larger)
+  b.tx_msg_cap = multi ? (uint32_t)std::min<uint64_t>(1ull << 28, std::max<uint64_t>({1ull << 20, 1024ull * e->sz,
+                                                                                  (uint64_t)cf.message_capacity / (uint64_t)e->world}))
+                       : 0;
   b.tx_req_cap = multi ? b.req_cap : 0;
   b.tx_stop_cap = multi ? kStopCap : 0;
   // content rows one shard may send in one SYNC (or SYNC_ACK) exchange: 256 MiB of rows, 64..4,096

@@ -80,6 +80,25 @@ __device__ inline uint32_t quiet_member_scan(const Ctx& c, uint32_t v, uint64_t 
   return end_off;
 }
 
+// One wait point for a batch of independent loads.  The compiler sinks a load into the branch that
+// uses its value and waits for it there, so a batch written as one block of loads still ran as one
+// round trip per branch; an empty asm that "modifies" every loaded value makes them all needed — and
+// waited for — at one point, after all of them were issued.
+#define QUIET_BATCH_WAIT(...) __asm__ volatile("" : __VA_ARGS__)
+// a load through the global address space (global_load: waited for by vmcnt alone; a flat load —
+// what a pointer read out of Ctx compiles to — also waits on lgkmcnt and returns out of order)
+template <typename T>
+__device__ __forceinline__ T gld(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)p;
+}
+struct alignas(16) QU4 {
+  uint32_t x, y, z, w;
+};
+__device__ __forceinline__ uint4 gld4(const void* p) {  // 16 B, 16-B aligned
+  const __attribute__((address_space(1))) QU4* q = (const __attribute__((address_space(1))) QU4*)p;
+  return make_uint4(q->x, q->y, q->z, q->w);  // (one dwordx4 load: the struct is 16-B aligned)
+}
+
 __device__ __forceinline__ void quiet_fail(uint32_t* fail, uint32_t off) {
   if (off < __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(fail, off);
 }
@@ -192,22 +211,31 @@ __device__ __forceinline__ uint32_t quiet_window(const QuietCtl* q, uint32_t K) 
 // doSync of up member v at tick t in a quiet window (sync_collect_fast / select_sync_address with the
 // same draws); the receiver's merge and the SYNC_ACK's are no-ops, so what remains is the counters:
 // ST_SYNCS for a selected target, the record counts of a delivered SYNC and its delivered ack
-__device__ inline void quiet_sync(const Ctx& c0, uint32_t v, uint64_t t, uint32_t tsz, unsigned long long& nsync,
-                                  unsigned long long& nack, unsigned long long& nrec) {
+// (inb_v: v's inbound word, loaded by the caller.)  The first candidate is pure arithmetic (the
+// draw), so what the common case decides on — its membership word in v's row, its up and inbound
+// words — is loaded in ONE batch; a candidate that is not a member (a seed, or another draw: rare)
+// takes the general path
+__device__ inline void quiet_sync(const Ctx& c0, uint32_t v, uint64_t t, uint32_t tsz, bool inb_v,
+                                  unsigned long long& nsync, unsigned long long& nack, unsigned long long& nrec) {
   Ctx c = c0;
   c.T = t;
   const uint32_t x0 = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 0, 0), c.n);
+  uint32_t aw = gld(aux_row(c, v) + x0), up0 = gld(c.up + x0), in0 = gld(c.default_inbound + x0);
+  QUIET_BATCH_WAIT("+v"(aw), "+v"(up0), "+v"(in0));
   uint32_t tg = x0;
-  if (!(x0 != v && ((aux_row(c, v)[x0] & A_IN_MEMBERS) || is_seed_of(c, v, x0)))) {
+  bool ok = up0 != 0 && in0 != 0;
+  if (!(x0 != v && ((aw & A_IN_MEMBERS) || is_seed_of(c, v, x0)))) {
     tg = select_sync_address(c, v);
     if (tg == NONE) return;
+    ok = c.up[tg] && c.default_inbound[tg];
   }
+  // (branch-free counter updates: early returns here made the compiler keep the counters in scratch)
   nsync++;
-  if (!c.up[tg] || !c.default_inbound[tg]) return;  // tryFailOutbound (stopped) / inbound-blocked: dropped
-  nrec += tsz;                                        // onSync's syncMembership over the SYNC's records
-  if (!c.default_inbound[v]) return;                  // the SYNC_ACK is dropped at v's inbound filter
-  nack++;
-  nrec += tsz;                                        // onSyncAck (:385-391): the acker's records
+  const unsigned long long dlv = ok ? 1ull : 0ull;           // delivered (else tryFailOutbound on a
+                                                              // stopped target / inbound-blocked: dropped)
+  const unsigned long long ack = ok && inb_v ? 1ull : 0ull;  // its SYNC_ACK passes v's inbound filter
+  nack += ack;
+  nrec += (dlv + ack) * tsz;  // onSync's syncMembership over the SYNC's records, onSyncAck's (:385-391)
 }
 
 // The next window's scan, precomputed (QuietPre).  On a pristine cluster the scan's only per-window
@@ -253,11 +281,22 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
   uint32_t nfail = H;  // this thread's share of the next window's first failing offset (from Tend)
   if (H) {
     if (gtid == 0) atomicMin(reinterpret_cast<unsigned long long*>(pre_out), pre_key(tag_out, 0xffffffffu));
-    // the timer buckets of the next window (k_quiet_scan's check)
+    // the timer buckets of the next window (k_quiet_scan's check): four independent loads per round
+    // trip (a loop of one load each waited for every load: ~4 serial round trips at N = 65,536)
     const uint32_t W = c.wheel_mask + 1, nwq = min(H, W) * c.wheel_nq;
-    for (uint32_t x = gtid; x < nwq; x += gsz) {
-      const uint32_t wj = x / c.wheel_nq;
-      if (c.wheel_cnt[(size_t)((Tend + wj) & c.wheel_mask) * c.wheel_nq + (x - wj * c.wheel_nq)]) nfail = min(nfail, wj);
+    for (uint32_t x0 = gtid; x0 < nwq; x0 += 4 * gsz) {
+      // (past the end: a valid address, its count ignored)
+      const uint32_t xa = x0, xb = min(x0 + gsz, nwq - 1), xc = min(x0 + 2 * gsz, nwq - 1), xd = min(x0 + 3 * gsz, nwq - 1);
+      const uint32_t ja = xa / c.wheel_nq, jb = xb / c.wheel_nq, jc = xc / c.wheel_nq, jd = xd / c.wheel_nq;
+      auto qaddr = [&](uint32_t x, uint32_t j) {
+        return c.wheel_cnt + (size_t)((Tend + j) & c.wheel_mask) * c.wheel_nq + (x - j * c.wheel_nq);
+      };
+      uint32_t ca = *qaddr(xa, ja), cb = *qaddr(xb, jb), cc = *qaddr(xc, jc), cd = *qaddr(xd, jd);
+      QUIET_BATCH_WAIT("+v"(ca), "+v"(cb), "+v"(cc), "+v"(cd));
+      if (ca) nfail = min(nfail, ja);
+      if (cb && x0 + gsz < nwq) nfail = min(nfail, jb);
+      if (cc && x0 + 2 * gsz < nwq) nfail = min(nfail, jc);
+      if (cd && x0 + 3 * gsz < nwq) nfail = min(nfail, jd);
     }
   }
   if (gtid == 0) {
@@ -271,11 +310,33 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
   unsigned long long npings = 0, nsync = 0, nack = 0, nrec = 0;
   for (uint32_t i = gtid; i < c.nl; i += gsz) {
     const uint32_t v = c.lo + i;
-    // every word the member's window reads, in one batch
-    const bool up = c.up[v] != 0;
-    const uint32_t fdn = c.fd_next[i], sn0 = c.sync_next[i];
-    const GossipSched g = c.gs[i];
-    const QuietMem qm = quiet_mem(c, i);
+    // every word the member's window reads, in one batch, waited for once
+    uint32_t upw = gld(c.up + v), inbw = gld(c.default_inbound + v), fdn = gld(c.fd_next + i), sn0 = gld(c.sync_next + i);
+    const uint4 gw4 = gld4(c.gs + i);
+    const uint4* mp = reinterpret_cast<const uint4*>(c.mem + i);
+    const uint4 w0 = gld4(mp), w1 = gld4(mp + 1), w2 = gld4(mp + 2);
+    // (scalars for the asm operands: a vector component bound to an operand went through scratch)
+    uint32_t m0 = w0.x, m1 = w0.y, m2 = w0.z, m3 = w0.w, m4 = w1.x, m5 = w1.y, m6 = w1.z, m7 = w1.w, m8 = w2.x,
+             m9 = w2.y, m10 = w2.z, m11 = w2.w;
+    uint32_t gnext = gw4.x, gper = gw4.y;
+    QUIET_BATCH_WAIT("+v"(upw), "+v"(inbw), "+v"(fdn), "+v"(sn0), "+v"(gnext), "+v"(gper), "+v"(m0), "+v"(m1),
+                     "+v"(m2), "+v"(m3), "+v"(m4), "+v"(m5), "+v"(m6), "+v"(m7), "+v"(m8), "+v"(m9), "+v"(m10),
+                     "+v"(m11));
+    const bool up = upw != 0, inb = inbw != 0;
+    const GossipSched g{gnext, gper, gw4.z, gw4.w};
+    QuietMem qm;  // (field by field from the words: a memcpy of a uint4 array put it in scratch)
+    qm.ack_due = (uint64_t)m1 << 32 | m0;
+    qm.relay_due = (uint64_t)m3 << 32 | m2;
+    qm.ping_cursor = m4;
+    qm.ping_len = m5;
+    qm.table_size = m6;
+    qm.fd_sync_cnt = m7;
+    qm.ins_rank = m8;
+    qm.join_now = (uint8_t)m9;
+    qm.join_pending = (uint8_t)(m9 >> 8);
+    qm.leave_pending = (uint8_t)(m9 >> 16);
+    qm.init_wait = (uint8_t)(m9 >> 24);
+    qm.fd_period = (uint64_t)m11 << 32 | m10;
     MemberDev& m = c.mem[i];
     // ---- FD (doPing every pingInterval; acknowledged at once)
     if (up && fdn < Tend) {
@@ -299,7 +360,7 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
     uint32_t sn = sn0;
     if (sn != NONE && sn < Tend) {
       for (; sn < Tend; sn += c.S)
-        if (up) quiet_sync(c, v, sn, qm.table_size, nsync, nack, nrec);
+        if (up) quiet_sync(c, v, sn, qm.table_size, inb, nsync, nack, nrec);
       c.sync_next[i] = sn;
     }
     // ---- the next window (quiet_member_scan with every target pingable): the member's ping list

@@ -174,6 +174,85 @@ def test_config5_partition_heal_matches_oracle(glib, n, hold, after):
     assert sb["capacity_errors"] == 0
 
 
+def _golden_run(name):
+    import json
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "config_digests.json")
+    runs = json.load(open(path))["runs"] if os.path.exists(path) else {}
+    if name not in runs:
+        pytest.skip(f"{name} not in tests/golden/config_digests.json (tests/golden/make_config_digests.py)")
+    return runs[name]
+
+
+def _check_checkpoints(want, got, where):
+    """every checkpoint of the oracle's golden run, in order: state digest, events, counters"""
+    order = sorted(want["checkpoints"], key=int)  # (the JSON file keeps its keys sorted as strings)
+    assert sorted(got, key=int) == order, (list(got), order)
+    for p in order:
+        w = want["checkpoints"][p]
+        g = got[p]
+        assert g["stats"] == w["stats"], f"{where}: counters differ by period {p}: " + "; ".join(
+            f"{k} {w['stats'][k]} != {g['stats'][k]}" for k in w["stats"] if w["stats"][k] != g["stats"][k])
+        assert (g["events"], g["events_sha256"]) == (w["events"], w["events_sha256"]), \
+            f"{where}: events of the stretch ending at period {p} differ ({g['events']} vs {w['events']})"
+        assert g["state_sha256"] == w["state_sha256"], f"{where}: state differs at period {p}"
+
+
+@pytest.mark.parametrize("shards", [1, 8])
+def test_config5_partition_heal_1024_matches_oracle(glib, shards):
+    """BASELINE config 5 bit-exact over its whole run at N = 1,024, unsharded and over 8 in-process
+    shards: seeds {0, N/2}, a 2-way partition from period 2, held past the suspicion timeout (every
+    viewer REMOVEs the other side), healed at period 82, run to period 122.  Every 10 periods the
+    digest of EVERY member's full state, the stretch's events and every counter must equal the
+    threaded oracle's committed checkpoints (tests/golden/make_config_digests.py;
+    MembershipProtocolTest.java:1035-1109, MembershipProtocolImpl.java:339-357,461-472).  Then the
+    outcome itself: all views all-ALIVE again."""
+    import make_config_digests as mk
+    want = _golden_run("config5_partition_heal_1024")
+    # (sharded: every GOSSIP_REQ to another shard is materialised — no cross-shard receipt filter,
+    # DESIGN.md §7 — ~12 M a round in the heal's storm; a shard's inbox and its per-destination
+    # outgoing buffers are sized for them: 2^26 and 2^23 messages)
+    e = mk.c5_engine(glib, local_shards=shards, **({"message_capacity": 1 << 26} if shards > 1 else {}))
+    got = {}
+    try:
+        if shards > 1:
+            assert e.shard_info()["world"] == shards
+        mk.c5_run(e, lambda p, ev: got.__setitem__(str(p), mk.checkpoint(e, ev, None, False)))
+        _check_checkpoints(want, got, f"config 5, N = 1,024, {shards} shard(s)")
+        for v in range(mk.C5_N):
+            row = e.read_view(v)
+            assert (((row >> 34) & 1) == 1).all() and (((row >> 32) & 3) == 0).all(), f"view {v} not all-ALIVE"
+        st = e.stats()
+        assert st["capacity_errors"] == 0 and st["orig_sync"] > 0
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("shards", [1, 4])
+def test_config3_churn_4096_eight_periods_match_oracle(glib, shards):
+    """BASELINE config 3's churn schedule (bench.py: 5 % uniform loss, 1 % kills + 1 % fresh joins
+    through seed 0 per period) bit-exact for 8 periods at N = 4,096, unsharded and over 4 in-process
+    shards: every period the sampled members' full state (SequenceIdCollectors included), the
+    period's events and every counter against the oracle's committed checkpoints
+    (tests/golden/make_config_digests.py).  Period 8 carries ~10^9 GOSSIP_REQs."""
+    import make_config_digests as mk
+    want = _golden_run("config3_churn_4096")
+    e, sch, members = mk.c3_engine(glib, local_shards=shards)
+    assert members == want["members"]
+    got = {}
+    try:
+        for p in range(mk.C3_PERIODS):
+            sch.run(e, p, p + 1)
+            ev = e.drain_events(1 << 27)
+            got[str(p + 1)] = mk.checkpoint(e, ev, members, True)
+            if str(p + 1) in want["checkpoints"]:  # fail at the first differing period
+                _check_checkpoints({"checkpoints": {k: v for k, v in want["checkpoints"].items() if int(k) <= p + 1}},
+                                   got, f"config 3, N = 4,096, {shards} shard(s)")
+        _check_checkpoints(want, got, f"config 3, N = 4,096, {shards} shard(s)")
+        assert e.stats()["capacity_errors"] == 0
+    finally:
+        e.close()
+
+
 def test_config5_partition_heal_2048_reconverges(glib):
     """Config 5 at the largest size one MI355X holds for a heal after removal (the
     partition's SUSPECT gossips alone keep ~80 x N live gossips per member): N = 2,048, partition from
