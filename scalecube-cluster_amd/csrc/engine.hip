@@ -186,6 +186,7 @@ struct swim_engine {
   uint64_t T = 0;
   int32_t rank = 0, world = 1;  // this process's shard (RCCL) and the cluster's shard count
   bool rccl = false;
+  bool rfilter_on = false;  // emit's cross-shard receipt filter (local groups, setup_peers_local)
   uint32_t xflags = 0;  // SWIM_XCHG_IPC* (swim_exchange_info): which branch of setup_peers_rccl ran
   bool xchg = false;  // the exchange machinery runs: world > 1, or RCCL with one rank (swim_create_shard)
   ncclComm_t comm = nullptr;
@@ -786,6 +787,9 @@ static int32_t run_tick(swim_engine* e) {
     }
     e->joins.clear();
   }
+  // (every shard's FETCH / timers / FD / gossip-round setup before any shard's emit: the cross-shard
+  // receipt filter reads the other shards' collector clears of this tick, as the unsharded emit sees
+  // every member's)
   for (Shard& sd : e->sh) {
     const uint32_t gm = grid_for(sd.c.nl, 256);
     // ---- A: suspicion timeouts, B: list compaction of their REMOVED + failure detector
@@ -799,11 +803,13 @@ static int32_t run_tick(swim_engine* e) {
     }
     k_fd<<<gm, 256, 0, s>>>(sd.d_par, T, gossip_tick ? 1 : 0, gossip_tick || delay ? 0 : 1);
     TICK_CHECK("k_fd");
+  }
+  for (Shard& sd : e->sh) {
     if (gossip_tick) {
       launch_emit(e, sd);
       TICK_CHECK("k_gossip_emit");
     }
-    if (delay) {
+    if (sd.c.delay_on) {
       k_dq_release<<<(sd.b.dq_bcap + 255) / 256, 256, 0, s>>>(sd.d_par, T);
       TICK_CHECK("k_dq_release");
     }
@@ -1485,8 +1491,15 @@ static int32_t setup_peers_local(swim_engine* e) {
         ph.rows_in[k][p] = e->pull_rows ? ph.rx_rows[k] + (size_t)p * sd.b.row_cap * e->n : pb.tx_rows[k];
       }
       ph.x[p] = e->sh[p].x;
+      // the cross-shard receipt filter (emit): peer p's receipt slots, bits and clear ticks
+      const Ctx& pc = e->sh[p].c;
+      ph.gslot[p] = pc.gslot;
+      ph.gbits[p] = pc.gbits;
+      ph.clr_tick[p] = pc.clr_tick;
+      ph.gwords[p] = pc.gwords;
     }
     if (hipMemcpy(sd.peers, &ph, sizeof ph, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
+    sd.b.rfilter = e->rfilter_on ? 1u : 0u;
   }
   return SWIM_OK;
 }
@@ -1595,6 +1608,11 @@ static int32_t create_engine(const swim_config* cfg, uint32_t capacity, uint32_t
   {
     const char* p = std::getenv("SWIM_EXCHANGE_PULL");
     e->pull_rows = rccl || (p && p[0] == '1');
+    // the cross-shard receipt filter: a local group's emit reads the other shards' receipt bits in
+    // place (SWIM_RFILTER=0 turns it off: every GOSSIP_REQ to another shard is materialised and the
+    // receiver flags the duplicates, as over RCCL, whose peers' bitmaps are not mapped)
+    const char* rf = std::getenv("SWIM_RFILTER");
+    e->rfilter_on = !rccl && world > 1 && !(rf && rf[0] == '0');
   }
   e->sz = (capacity + (uint32_t)world - 1) / (uint32_t)world;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return SWIM_EDEVICE; }

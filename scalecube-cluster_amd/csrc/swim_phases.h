@@ -79,6 +79,12 @@ struct Peers {
                                      // this shard's pulled copy (RCCL)
   uint32_t* rx_rows[2];              // RCCL: the pulled copies, [world][row_cap][n]
   const Xc* x[MAXW];                 // local group: peer counters (RCCL: the counts arrive in rx_cnt)
+  // the cross-shard receipt filter (local group: Bufs.rfilter; over RCCL these stay null): peer p's
+  // receipt slots and bitmaps, its receivers' collector clear ticks, its bitmap words per slot
+  const GSlot* gslot[MAXW];
+  const uint32_t* gbits[MAXW];
+  const uint32_t* clr_tick[MAXW];
+  uint32_t gwords[MAXW];
 };
 // rx_cnt[kind][p]: what peer p produced for this shard this tick (kind 0 GOSSIP_REQs, 1 SYNCs,
 // 2 SYNC_ACKs) and, kind 3, its completed graceful leaves (broadcast)
@@ -101,6 +107,7 @@ struct Bufs {
   uint32_t* tx_rows[2];  // [row_cap][n] content rows of the outgoing SYNCs / SYNC_ACKs (k_pack_rows)
   uint32_t row_cap;
   const Peers* peers;
+  uint32_t rfilter;      // emit checks receivers on other shards against their receipt bits (Peers.gslot...)
   uint32_t* rx_cnt;      // [4][MAXW] (XK_*)
   uint32_t* rx_stops;    // [world * tx_stop_cap] other shards' completed leaves, applied by k_end_tick
   uint32_t* rx_stop_n;   // how many (zeroed by k_fd, set by k_recv_msgs)
@@ -708,9 +715,17 @@ struct SenderPre {
   uint32_t pw;         // the member holds PAcks (some may wait on its LEAVING gossips)
   uint32_t t[PRE_F];   // targets
   uint32_t tw[PRE_F];  // up | inbound-passes << 1 | v's outbound loss towards it << 2
-  uint32_t clr[PRE_F]; // its collectors' last clear tick (owned), else ~0
+  uint32_t clr[PRE_F]; // its collectors' last clear tick (owned, or the peer's: receipt filter), else ~0
 };
-__device__ __forceinline__ void sender_pre_load(const Ctx& c, uint32_t i, SenderPre& sp) {
+// the last clear tick of target t's collectors, as the receipt check compares it: t's own shard's, or
+// (cross-shard receipt filter) the peer's; ~0 = no receipt bit of t is trusted
+__device__ __forceinline__ uint32_t target_clr(const Ctx& c, const Bufs& b, uint32_t t) {
+  if (owned(c, t)) return c.clr_tick[t - c.lo];
+  if (!b.rfilter) return 0xffffffffu;
+  const uint32_t p = t / c.sz;
+  return b.peers->clr_tick[p][t - p * c.sz];
+}
+__device__ __forceinline__ void sender_pre_load(const Ctx& c, const Bufs& b, uint32_t i, SenderPre& sp) {
   sp.ok = 0;
   const MemberDev& m = c.mem[i];
   const uint32_t rlen = m.remote_len;
@@ -731,7 +746,7 @@ __device__ __forceinline__ void sender_pre_load(const Ctx& c, uint32_t i, Sender
     if (q >= F) continue;
     const uint32_t t = sp.t[q];
     sp.tw[q] = (c.up[t] ? 1u : 0u) | (in_pass(c, t, v) ? 2u : 0u) | ((uint32_t)out_loss(c, v, t) << 2);
-    sp.clr[q] = owned(c, t) ? c.clr_tick[t - c.lo] : 0xffffffffu;
+    sp.clr[q] = target_clr(c, b, t);
   }
   sp.ok = 1;
 }
@@ -831,7 +846,7 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
     const uint32_t t = s_t[1 + lane];
     s_t[50 + lane] = (c.up[t] ? 1u : 0u) | (in_pass(c, t, v) ? 2u : 0u);
     s_t[66 + lane] = (uint32_t)out_loss(c, v, t);
-    s_t[82 + lane] = owned(c, t) ? c.clr_tick[t - c.lo] : 0xffffffffu;
+    s_t[82 + lane] = target_clr(c, b, t);
   }
   lds_order();
   PPROF_ACC(ep.t_tgt, te_t);
@@ -963,11 +978,15 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
       }
       const bool gs_ok = win && gs.key == key;
       // the first four targets' receipt words are loaded beside the slot (their addresses need only
-      // the slot index, not its contents): one round trip where the check needs two
+      // the slot index, not its contents): one round trip where the check needs two.  A target on
+      // another shard (cross-shard receipt filter) has its word, and its slot, in the peer's bitmaps
       auto rword = [&](uint32_t jj) -> uint32_t {
         const uint32_t t = s_t[1 + min(jj, nt - 1)];
-        const uint32_t i = owned(c, t) ? t - c.lo : 0u;
-        return (win && jj < nt) ? c.gbits[(size_t)sl * c.gwords + (i >> 5)] : 0u;
+        if (!(win && jj < nt)) return 0u;
+        if (owned(c, t)) return c.gbits[(size_t)sl * c.gwords + ((t - c.lo) >> 5)];
+        if (!b.rfilter) return 0u;
+        const uint32_t p = t / c.sz;
+        return b.peers->gbits[p][(size_t)sl * b.peers->gwords[p] + ((t - p * c.sz) >> 5)];
       };
       const uint32_t wb0 = rword(0), wb1 = rword(1), wb2 = rword(2), wb3 = rword(3);
       // GossipState.infected beyond its first member (rare: the overflow table, once per pass)
@@ -1020,6 +1039,20 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
           const bool known = gs_ok && s_t[82 + j] < gs.tick && ((word >> (i & 31)) & 1u);
           if (known) mat = false;
           else probe |= 1u << j;
+        } else if (mat && b.rfilter) {
+          // cross-shard receipt filter: the same test against the receiver's shard's slot and bit
+          // (every shard's tick-T timers and segmentation clears precede every emit of the tick, and
+          // no delivery of the tick has run: the unsharded engine's view); without a trusted bit the
+          // message is materialised (its collector is not probed: the receiver flags a duplicate)
+          // (the peer's slot is loaded here, not beside the words: holding four slots' words
+          // through the batch cost the unsharded kernel registers and spills)
+          const uint32_t p = t / c.sz, i = t - p * c.sz;
+          const uint32_t word = j == 0 ? wb0 : j == 1 ? wb1 : j == 2 ? wb2 : j == 3 ? wb3
+                                                 : b.peers->gbits[p][(size_t)sl * b.peers->gwords[p] + (i >> 5)];
+          if ((word >> (i & 31)) & 1u) {
+            const GSlot ps = b.peers->gslot[p][sl];
+            if (ps.key == key && s_t[82 + j] < ps.tick) mat = false;
+          }
         }
         matb |= (mat ? 1u : 0u) << j;
       }
@@ -1294,7 +1327,7 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES, EMIT_OCC) k_gossip_emit(KP, u
       plen = g.len;
       pper = g.period;
       pbase = g.base;
-      sender_pre_load(c, pi, pre);
+      sender_pre_load(c, b, pi, pre);
     }
     const uint32_t nb = min(64u, (ns - k0 + S - 1) / S);
     // the two ends of a sender's slab (its first and last 64 states), loaded one sender ahead
