@@ -8,6 +8,8 @@ runs it finishes, written to tests/golden/config_digests.json.
   live gossips), the digest of that stretch's events, every counter.
   (MembershipProtocolTest.java:1035-1109 testNetworkPartitionDueNoOutboundThenRemoved /
   MembershipProtocolImpl.java:339-357,461-472: partition, removal, re-join by SYNC.)
+* config5_partition_heal_4096: the same schedule at N = 4,096 (healed at period 92, run to 152), the
+  checkpoints over every 64th member and the 8-shard boundaries.
 * config3_churn_4096: bench.py's config-3 schedule (5 % uniform loss, 1 % kills + 1 % fresh joins through
   seed 0 per period) at N = 4,096 for 8 periods; a checkpoint every period: the digest of sampled
   members' full state including their SequenceIdCollectors, the period's events, every counter.
@@ -16,7 +18,7 @@ The oracle is multi-threaded (identical results for every thread count, tests/te
 GPU tests (tests/test_gpu_configs.py) run the same schedules unsharded and over 8 in-process shards
 and must reproduce every checkpoint.
 
-    python tests/golden/make_config_digests.py [config5|config3] [THREADS]
+    python tests/golden/make_config_digests.py [config5|config5b|config3] [THREADS]
 """
 import json
 import os
@@ -38,37 +40,50 @@ from make_scenario_digests import digest, event_digest  # noqa: E402
 from swimgpu import abi  # noqa: E402
 
 C5_N, C5_PARTITION, C5_HEAL, C5_END, C5_EVERY = 1024, 2, 82, 122, 10
+# config 5 at N = 4,096: held past the suspicion timeout (5 x 12 periods + 30), healed at period 92;
+# after the heal the first SYNC across the cut takes ~15-35 periods, so the run goes
+# to period 152; a checkpoint every 10 periods over sampled members (every 64th, the 8-shard
+# boundaries) — a full readback of 4,096 members' gossips is gigabytes per checkpoint
+C5B = {"n": 4096, "heal": 92, "end": 152}
 C3_N, C3_PERIODS = 4096, 8
 
 
-def c5_config(lib):
-    n = C5_N
+def c5_config(lib, n=C5_N):
     return abi.default_config(lib, 0, sync_stagger=1, record_fd_events=0, gossip_capacity=1 << 19,
                               message_capacity=1 << 28, event_capacity=1 << 26, timer_capacity=max(64 * n, n * n // 2),
                               timer_pool_capacity=n * n // 2 + 64 * n, collector_capacity=1 << (2 * n - 1).bit_length())
 
 
-def c5_engine(lib, **cfg_extra):
-    cfg = c5_config(lib)
+def c5_engine(lib, n=C5_N, **cfg_extra):
+    cfg = c5_config(lib, n)
     for k, v in cfg_extra.items():
         setattr(cfg, k, v)
-    e = abi.Engine(lib, cfg, C5_N, C5_N, 5)
-    e.set_seeds([0, C5_N // 2])
+    e = abi.Engine(lib, cfg, n, n, 5)
+    e.set_seeds([0, n // 2])
     return e
 
 
-def c5_run(e, on_checkpoint):
+def c5_members(n):
+    """the members whose full state a checkpoint digests: all at N = 1,024, else every 64th and the
+    8-shard boundaries"""
+    if n == C5_N:
+        return None
+    sz = n // 8
+    return sorted(set(list(range(0, n, 64)) + [k * sz + d for k in range(1, 8) for d in (-1, 0)] + [1, n - 1]))
+
+
+def c5_run(e, on_checkpoint, n=C5_N, heal=C5_HEAL, end=C5_END):
     """the config-5 schedule; on_checkpoint(period, events since the last one) every C5_EVERY periods"""
-    side = (np.arange(C5_N) >= C5_N // 2).astype(np.uint16)
+    side = (np.arange(n) >= n // 2).astype(np.uint16)
     evs = []
-    for p in range(C5_END):
+    for p in range(end):
         if p == C5_PARTITION:
             e.set_partition(side)
-        if p == C5_HEAL:
+        if p == heal:
             e.set_partition(None)
         e.step(1)
-        evs.append(e.drain_events(1 << 26))
-        if (p + 1) % C5_EVERY == 0 or p + 1 == C5_END:
+        evs.append(e.drain_events(1 << 26 if n <= C5_N else 1 << 27))
+        if (p + 1) % C5_EVERY == 0 or p + 1 == end:
             on_checkpoint(p + 1, np.concatenate(evs))
             evs = []
 
@@ -111,6 +126,23 @@ def make_c5(threads):
             "members": "all", "collectors": False, "checkpoints": out}
 
 
+def make_c5b(threads):
+    n = C5B["n"]
+    e = c5_engine(oracle.lib(), n)
+    oracle.set_threads(e, threads)
+    members = c5_members(n)
+    out = {}
+    t0 = time.time()
+
+    def on(p, ev):
+        out[str(p)] = checkpoint(e, ev, members, False)
+        print(f"config5 N={n} period {p}: {len(ev)} events, {time.time() - t0:.0f} s, "
+              f"maxrss {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss >> 20} GB", flush=True)
+    c5_run(e, on, n, C5B["heal"], C5B["end"])
+    return {"n": n, "partition_period": C5_PARTITION, "heal_period": C5B["heal"], "periods": C5B["end"],
+            "members": members, "collectors": False, "checkpoints": out}
+
+
 def make_c3(threads):
     e, sch, members = c3_engine(oracle.lib())
     oracle.set_threads(e, threads)
@@ -134,6 +166,9 @@ def main():
         "source": "tests/golden/make_config_digests.py (CPU oracle)", "runs": {}}
     if which in ("all", "config5"):
         doc["runs"]["config5_partition_heal_1024"] = make_c5(threads)
+        json.dump(doc, open(path, "w"), indent=1, sort_keys=True)
+    if which in ("all", "config5b"):
+        doc["runs"]["config5_partition_heal_4096"] = make_c5b(threads)
         json.dump(doc, open(path, "w"), indent=1, sort_keys=True)
     if which in ("all", "config3"):
         doc["runs"]["config3_churn_4096"] = make_c3(threads)

@@ -197,28 +197,33 @@ def _check_checkpoints(want, got, where):
         assert g["state_sha256"] == w["state_sha256"], f"{where}: state differs at period {p}"
 
 
-@pytest.mark.parametrize("shards", [1, 8])
-def test_config5_partition_heal_1024_matches_oracle(glib, shards):
-    """BASELINE config 5 bit-exact over its whole run at N = 1,024, unsharded and over 8 in-process
-    shards: seeds {0, N/2}, a 2-way partition from period 2, held past the suspicion timeout (every
-    viewer REMOVEs the other side), healed at period 82, run to period 122.  Every 10 periods the
-    digest of EVERY member's full state, the stretch's events and every counter must equal the
-    threaded oracle's committed checkpoints (tests/golden/make_config_digests.py;
+@pytest.mark.parametrize("n,shards", [(1024, 1), (1024, 8), (4096, 1), (4096, 8)])
+def test_config5_partition_heal_matches_oracle_checkpoints(glib, n, shards):
+    """BASELINE config 5 bit-exact over its whole run at N = 1,024 and N = 4,096, unsharded and over 8
+    in-process shards: seeds {0, N/2}, a 2-way partition from period 2, held past the suspicion
+    timeout (every viewer REMOVEs the other side), healed (period 82 / 92), run until every view is
+    all-ALIVE again (period 122 / 152).  Every 10 periods the digest of the members' full state (all
+    1,024; at N = 4,096 every 64th and the shard boundaries), the stretch's events and every counter
+    must equal the threaded oracle's committed checkpoints (tests/golden/make_config_digests.py;
     MembershipProtocolTest.java:1035-1109, MembershipProtocolImpl.java:339-357,461-472).  Then the
     outcome itself: all views all-ALIVE again."""
     import make_config_digests as mk
-    want = _golden_run("config5_partition_heal_1024")
-    # (sharded: every GOSSIP_REQ to another shard is materialised — no cross-shard receipt filter,
-    # DESIGN.md §7 — ~12 M a round in the heal's storm; a shard's inbox and its per-destination
-    # outgoing buffers are sized for them: 2^26 and 2^23 messages)
-    e = mk.c5_engine(glib, local_shards=shards, **({"message_capacity": 1 << 26} if shards > 1 else {}))
+    want = _golden_run(f"config5_partition_heal_{n}")
+    heal, end = want["heal_period"], want["periods"]
+    members = None if want["members"] == "all" else want["members"]
+    assert members == mk.c5_members(n)
+    # (sharded: every GOSSIP_REQ to another shard the receipt filter cannot prove redundant is
+    # materialised — ~12 M a round in the heal's storm at N = 1,024; a shard's inbox and its
+    # per-destination outgoing buffers are sized for them)
+    extra = {"message_capacity": 1 << 26 if n <= 1024 else 1 << 27} if shards > 1 else {}
+    e = mk.c5_engine(glib, n, local_shards=shards, **extra)
     got = {}
     try:
         if shards > 1:
             assert e.shard_info()["world"] == shards
-        mk.c5_run(e, lambda p, ev: got.__setitem__(str(p), mk.checkpoint(e, ev, None, False)))
-        _check_checkpoints(want, got, f"config 5, N = 1,024, {shards} shard(s)")
-        for v in range(mk.C5_N):
+        mk.c5_run(e, lambda p, ev: got.__setitem__(str(p), mk.checkpoint(e, ev, members, False)), n, heal, end)
+        _check_checkpoints(want, got, f"config 5, N = {n}, {shards} shard(s)")
+        for v in range(n):
             row = e.read_view(v)
             assert (((row >> 34) & 1) == 1).all() and (((row >> 32) & 3) == 0).all(), f"view {v} not all-ALIVE"
         st = e.stats()
