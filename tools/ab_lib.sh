@@ -18,7 +18,11 @@ import json, sys
 d = json.loads([l for l in open(sys.argv[3]) if l.startswith("{")][0])
 r = d.get("roofline") or {}
 ss = d.get("steady_state") or {}
-print(json.dumps({"lib": sys.argv[1], "rep": int(sys.argv[2]), "value": d["value"], "window_us": (r.get("avg_window_ms") or 0) * 1e3,
+rf = d.get("roofline_fanout") or {}
+rd = d.get("roofline_deliver") or {}
+print(json.dumps({"lib": sys.argv[1], "rep": int(sys.argv[2]), "value": d["value"], "ms_per_step": d["ms_per_step"],
+                  "emit_ms": rf.get("avg_launch_ms"), "deliver_ms": rd.get("avg_launch_ms"),
+                  "window_us": (r.get("avg_window_ms") or 0) * 1e3,
                   "steady_value": ss.get("value"), "median_call_us": ss.get("median_call_us"),
                   "per_tick_ms": (d.get("per_tick_path") or {}).get("ms_per_step"),
                   "failures_ms": (d.get("failures") or {}).get("ms_per_step")}))
