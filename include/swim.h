@@ -482,7 +482,7 @@ int32_t swim_get_quiet_stats(const swim_engine* e, swim_quiet_stats* out);
 int32_t swim_profile_quiet(swim_engine* e, swim_kernel_profile* out);
 
 /* Profiling builds (-DSWIM_PHASE_PROF, tools/phase_prof.sh) only: per-phase wall-time sums of the
- * instrumented kernels (100 MHz ticks), n <= 48 slots; reset = 1 zeroes them.  The product build and
+ * instrumented kernels (100 MHz ticks), n <= 64 slots; reset = 1 zeroes them.  The product build and
  * the CPU oracle report zeros. */
 int32_t swim_debug_counters(uint64_t* out, uint32_t n, int32_t reset);
 

@@ -1625,7 +1625,7 @@ int32_t swim_profile_enable(swim_engine* e, int32_t) { return e ? SWIM_OK : SWIM
 int32_t swim_set_quiet_path(swim_engine* e, int32_t) { return e ? SWIM_OK : SWIM_EINVAL; }
 int32_t swim_profile_quiet(swim_engine* e, swim_kernel_profile* out) { return swim_profile_merge(e, out); }
 int32_t swim_debug_counters(uint64_t* out, uint32_t n, int32_t) {
-  if (!out || n > 48) return SWIM_EINVAL;
+  if (!out || n > 64) return SWIM_EINVAL;
   std::memset(out, 0, 8ull * n);
   return SWIM_OK;
 }

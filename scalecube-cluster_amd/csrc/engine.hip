@@ -1259,7 +1259,6 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   c.wheel_mask = next_pow2((uint32_t)max_timer + 2) - 1;
   const uint64_t tcap = cf.timer_capacity ? cf.timer_capacity : 2ull * std::max(nl, 1u);
   c.wheel_nq = std::max(1u, (nl + 255) / 256);  // one queue per k_fd workgroup
-  c.gwords = std::max(1u, (nl + 31) / 32);
   // paged wheel (swim_device.h): one (bucket, queue) may take 2x its block's even share of the
   // per-tick capacity (timers cluster on viewers unevenly: a churn tick schedules ~16 timers at each
   // of 256 viewers of a block), at most every (viewer, subject) pair of the block; its page table has
@@ -1353,7 +1352,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
             sd.alloc(&c.fd_next, nl) && sd.alloc(&c.sync_next, nl) && sd.alloc(&c.mflag, nl) &&
             sd.alloc(&c.gs, std::max(nl, 1u)) &&
             sd.alloc(&c.gslot, GSLOTS) && sd.alloc(&c.gpend, GSLOTS) &&
-            sd.alloc(&c.gbits, (size_t)GSLOTS * c.gwords) && sd.alloc(&c.clr_tick, std::max(nl, 1u)) &&
+            sd.alloc(&c.gbits, (size_t)std::max(nl, 1u) * GROW) && sd.alloc(&c.clr_tick, std::max(nl, 1u)) &&
             sd.alloc(&c.gclaim, 2 * GSLOTS) && sd.alloc(&c.gclaim_cnt, 2) &&
             sd.alloc(&c.stats, (size_t)ST_COUNT * ST_REPL) && sd.alloc(&c.err, 1) && sd.alloc(&sd.k, 1) &&
             sd.alloc(&sd.x, 1) && sd.alloc(&b.pg_msgs, (size_t)b.pg_cap * 64) &&
@@ -1416,7 +1415,7 @@ static int32_t alloc_shard(swim_engine* e, Shard& sd, uint32_t shard, uint32_t n
   hipMemsetAsync(c.compact_flag, 0, 4 * (size_t)nl, s);
   hipMemsetAsync(c.gslot, 0, sizeof(GSlot) * GSLOTS, s);
   hipMemsetAsync(c.gpend, 0, sizeof(uint64_t) * GSLOTS, s);
-  hipMemsetAsync(c.gbits, 0, sizeof(uint32_t) * GSLOTS * (size_t)c.gwords, s);
+  hipMemsetAsync(c.gbits, 0, sizeof(uint32_t) * GROW * (size_t)std::max(nl, 1u), s);
   hipMemsetAsync(c.clr_tick, 0, sizeof(uint32_t) * std::max(nl, 1u), s);
   hipMemsetAsync(c.gclaim_cnt, 0, sizeof(uint32_t) * 2, s);
   hipMemsetAsync(c.stats, 0, 8 * (size_t)ST_COUNT * ST_REPL, s);
@@ -1496,7 +1495,6 @@ static int32_t setup_peers_local(swim_engine* e) {
       ph.gslot[p] = pc.gslot;
       ph.gbits[p] = pc.gbits;
       ph.clr_tick[p] = pc.clr_tick;
-      ph.gwords[p] = pc.gwords;
     }
     if (hipMemcpy(sd.peers, &ph, sizeof ph, hipMemcpyHostToDevice) != hipSuccess) return SWIM_EDEVICE;
     sd.b.rfilter = e->rfilter_on ? 1u : 0u;
@@ -2559,13 +2557,13 @@ int32_t swim_profile_deliver(swim_engine* e, swim_kernel_profile* out) {
 // profiling builds (-DSWIM_PHASE_PROF): the per-phase wall-time sums of the instrumented kernels
 // (swim_phases.h g_dbg); reset = 1 zeroes them after the read.  Zeros in the product build.
 int32_t swim_debug_counters(uint64_t* out, uint32_t n, int32_t reset) {
-  if (!out || n > 48) return SWIM_EINVAL;
-  unsigned long long h[48] = {};
+  if (!out || n > 64) return SWIM_EINVAL;
+  unsigned long long h[64] = {};
   if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dbg), sizeof h) != hipSuccess)
     return SWIM_EDEVICE;
   for (uint32_t i = 0; i < n; ++i) out[i] = h[i];
   if (reset) {
-    unsigned long long z[48] = {};
+    unsigned long long z[64] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof z) != hipSuccess) return SWIM_EDEVICE;
   }
   return SWIM_OK;

@@ -139,6 +139,7 @@ struct alignas(16) MemberDev {
   uint32_t pack_seq, init_pend;
   uint32_t w_link1, w_n, w_ready, w_gp;
   uint32_t ctl_tick1;  // 1 + the tick of the member's last control-phase operation (swim_ingest_sync)
+  uint32_t clr_serial;  // slab serial at the member's last collector clear (states below it predate it)
 };
 static_assert(sizeof(MemberDev) == 224, "MemberDev: 224 B (the quiet scan's words in the first 64-B sector)");
 
@@ -381,6 +382,13 @@ constexpr uint32_t INS_INLINE = 8;
 // valid for the gossip `key` from tick `tick` on (a slot is (re)claimed only in k_end_tick, when no
 // other kernel runs, and its bits are zeroed then).
 constexpr uint32_t GSLOTS = 8192;
+// The bits are receiver-major: receiver i's row is GROW words (1 KB), bit sl of it says i accepted
+// slot sl's gossip.  The checks come a receiver at a time: emit tests a sender's few targets against
+// the 64 gossips of a pass (at most 8 lines of each target's row, where a gossip-major layout reads a
+// line per (gossip, target)), and delivery marks one receiver's accepted lanes into one row.  A claim
+// clears one bit of every row (k_end_tick); claims are per new gossip, a few hundred per run.
+constexpr uint32_t GROW = GSLOTS / 32;
+__device__ __forceinline__ size_t rbit_word(uint32_t i, uint32_t sl) { return (size_t)i * GROW + (sl >> 5); }
 struct GSlot {
   uint64_t key;   // (gossiper + 1) << 32 | seq, 0 = unowned
   uint32_t tick;  // bits set from this tick on are trustworthy
@@ -512,8 +520,7 @@ struct Ctx {
   // that k_gossip_emit tests before probing the collector table
   GSlot* gslot;          // [GSLOTS] the gossip owning each bitmap and the tick its bits became valid
   uint64_t* gpend;       // [GSLOTS] gossip waiting to own the slot at the end of the tick (0 = none)
-  uint32_t* gbits;       // [GSLOTS][gwords] bit t - lo: receiver t accepted the owning gossip
-  uint32_t gwords;
+  uint32_t* gbits;       // [nl][GROW] bit sl of row t - lo: receiver t accepted slot sl's owning gossip
   uint32_t* clr_tick;    // per viewer: last tick one of its collectors was cleared
   uint32_t* gclaim;      // [2][GSLOTS] slots to (re)claim at the end of tick T, queue T & 1
   uint32_t* gclaim_cnt;  // [2]
@@ -1041,6 +1048,150 @@ __device__ inline int coll_add_lds(uint2* iv, uint32_t& n, uint32_t x, uint32_t*
   }
   return 1;
 }
+// The same add made by the whole wave (every lane calls it with the same x; n is wave-uniform): the
+// floor by binary search (every lane the same LDS reads), the intervals after the change moved 64 at
+// a time.  One lane moving them one by one cost ~260 moves per add at config 3's churn (collectors of
+// hundreds of intervals: 2.9 x 10^9 moves per delivery launch at N = 16,384).  Same result as
+// coll_add_lds.  (wave_sync: this file's callers define it.)
+template <typename Sync>
+__device__ inline int coll_add_lds_wave(uint2* iv, uint32_t& n, uint32_t x, uint32_t lane, Sync wave_sync,
+                                        uint32_t* moved = nullptr) {
+  int lo = 0, hi = (int)n - 1, fl = -1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    if (iv[mid].x <= x) { fl = mid; lo = mid + 1; } else { hi = mid - 1; }
+  }
+  if (fl >= 0 && x <= iv[fl].y) return 0;
+  const int ce = fl + 1;
+  const bool nf = fl >= 0 && (int64_t)x - 1 == (int64_t)iv[fl].y;
+  const bool nc = ce < (int)n && (int64_t)x + 1 == (int64_t)iv[ce].x;
+  const uint32_t ce_hi = nc ? iv[ce].y : 0u;
+  wave_sync();  // (every lane has read before any lane writes)
+  if (nf && nc) {  // x joins its neighbours: [fl].y takes [ce].y, the intervals after ce move down one
+    for (uint32_t b0 = (uint32_t)ce + 1; b0 < n; b0 += 64) {  // (ascending: a slot is read before it is overwritten)
+      const uint32_t q = b0 + lane;
+      uint2 v = make_uint2(0, 0);
+      if (q < n) v = iv[q];
+      wave_sync();
+      if (q < n) iv[q - 1] = v;
+      wave_sync();
+    }
+    if (lane == 0) iv[fl].y = ce_hi;
+    if (moved) *moved += n - 1 - (uint32_t)ce;
+    n--;
+  } else if (nf) {
+    if (lane == 0) iv[fl].y = x;
+  } else if (nc) {
+    if (lane == 0) iv[ce].x = x;
+  } else {  // a new interval at ce: the intervals from ce on move up one, the top 64 first
+    if ((int)n > ce) {
+      for (int b0 = ce + (int)(((n - 1 - (uint32_t)ce) >> 6) << 6); b0 >= ce; b0 -= 64) {
+        const uint32_t q = (uint32_t)b0 + lane;
+        uint2 v = make_uint2(0, 0);
+        if (q < n) v = iv[q];
+        wave_sync();
+        if (q < n) iv[q + 1] = v;
+        wave_sync();
+      }
+    }
+    if (lane == 0) iv[ce] = make_uint2(x, x);
+    if (moved) *moved += n - (uint32_t)ce;
+    n++;
+  }
+  wave_sync();
+  return 1;
+}
+// coll_add made by the whole wave on a collector too big to stage in LDS (deliver_coop: thousands of
+// intervals in a top-tier block).  The floor by a 64-way search (one gather of 64 pivots per step:
+// 3 steps over 16,382 intervals, where coll_add makes 14 dependent loads), the intervals after the
+// change moved 256 at a time (4 loads in flight per lane, then the 4 stores), where coll_add moves one
+// interval per dependent round trip.  Same result as coll_add; the rare cases that change the entry's
+// tier or inline value (a full block, a run back to one interval) are left to coll_add on lane 0.
+// Every lane calls it with the same x; the return value is wave-uniform.
+// (the 4 loads complete before the first store: one lane's store may land on another lane's next load)
+#define COLL_WAVE_WAIT(v) \
+  __asm__ volatile("" : "+v"(v[0].x), "+v"(v[0].y), "+v"(v[1].x), "+v"(v[1].y), "+v"(v[2].x), "+v"(v[2].y), \
+                   "+v"(v[3].x), "+v"(v[3].y))
+template <typename Sync>
+__device__ inline int coll_add_wave(const Ctx& c, CollEnt* e, uint32_t x, uint32_t lane, Sync wave_sync,
+                                    uint32_t* seg) {
+  const uint32_t meta = rdlane(gload(&e->meta), 0);
+  uint32_t* blk = (meta & 7u) == COLL_SPILLED ? coll_block(c, meta) : nullptr;
+  const uint32_t n = blk ? rdlane(gload(blk), 0) : 0u;
+  const int t = (int)((meta >> 4) & 3u);
+  if (!blk || n <= 2u || n == tier_cap(t)) {  // one lane (coll_add), as before
+    uint32_t r = 0;
+    if (lane == 0) r = coll_add(c, e, x, seg) ? 1u : 0u;
+    r = rdlane(r, 0);
+    wave_sync();
+    return (int)r;
+  }
+  uint2* iv = reinterpret_cast<uint2*>(blk + 4);
+  // floor: the last interval with lo <= x, searched among [a, b) with 64 pivots a step
+  int fl = -1;
+  for (uint32_t a = 0, b = n; a < b;) {
+    const uint32_t step = (b - a + 63u) >> 6;
+    const uint32_t p = a + lane * step;
+    const uint64_t le = __ballot(p < b && gload(&iv[p].x) <= x);
+    if (!le) break;
+    const uint32_t k = 63u - (uint32_t)__clzll((long long)le);
+    fl = (int)(a + k * step);
+    b = min(b, a + (k + 1u) * step);
+    a = (uint32_t)fl + 1u;
+  }
+  const uint2 f = fl >= 0 ? gload(&iv[fl]) : make_uint2(0, 0);
+  if (fl >= 0 && x <= f.y) return 0;
+  const uint32_t ce = (uint32_t)(fl + 1);
+  const uint2 cx = ce < n ? gload(&iv[ce]) : make_uint2(0, 0);
+  const bool nf = fl >= 0 && (int64_t)x - 1 == (int64_t)f.y;
+  const bool nc = ce < n && (int64_t)x + 1 == (int64_t)cx.x;
+  uint32_t n1 = n;
+  if (nf && nc) {  // x joins its neighbours: the intervals after ce move down one, ascending
+    for (uint32_t b0 = ce + 1u; b0 < n; b0 += 256u) {
+      uint2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t q = b0 + (uint32_t)u * 64u + lane;
+        v[u] = q < n ? gload(&iv[q]) : make_uint2(0, 0);
+      }
+      COLL_WAVE_WAIT(v);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t q = b0 + (uint32_t)u * 64u + lane;
+        if (q < n) iv[q - 1] = v[u];
+      }
+    }
+    if (lane == 0) iv[fl].y = cx.y;
+    n1 = n - 1;
+  } else if (nf) {
+    if (lane == 0) iv[fl].y = x;
+  } else if (nc) {
+    if (lane == 0) iv[ce].x = x;
+  } else {  // a new interval at ce: the intervals from ce on move up one, the top 256 first
+    for (int b0 = (int)n - 256; b0 + 256 > (int)ce; b0 -= 256) {
+      uint2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = b0 + u * 64 + (int)lane;
+        v[u] = q >= (int)ce ? gload(&iv[q]) : make_uint2(0, 0);
+      }
+      COLL_WAVE_WAIT(v);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = b0 + u * 64 + (int)lane;
+        if (q >= (int)ce) iv[q + 1] = v[u];
+      }
+    }
+    if (lane == 0) iv[ce] = make_uint2(x, x);
+    n1 = n + 1;
+  }
+  if (lane == 0) {
+    blk[0] = n1;
+    if (seg && n1 > (uint32_t)c.seg_threshold) *seg = 1;
+  }
+  wave_sync();
+  return 1;
+}
 // the staged intervals' home once the run is done (n after it, maxn the most it held): inline when one
 // interval is left; else the entry's block if its tier holds maxn, or a block of the smallest tier that
 // does (coll_add grows one tier at a time at each full insert: the same tier in the end; the old block
@@ -1092,7 +1243,7 @@ __device__ inline void receipt_mark(const Ctx& c, uint32_t r, uint32_t gossiper,
   const uint32_t sl = gslot_of(key);
   if (c.gslot[sl].key == key) {
     const uint32_t i = r - c.lo;
-    atomicOr(&c.gbits[(size_t)sl * c.gwords + (i >> 5)], 1u << (i & 31));
+    atomicOr(&c.gbits[rbit_word(i, sl)], 1u << (sl & 31));
   } else if (c.gpend[sl] == 0ull &&  // (a plain read first: once claimed, the thousands of receivers of a
                                      // new gossip skip the contended compare-and-swap)
              atomicCAS(reinterpret_cast<unsigned long long*>(&c.gpend[sl]), 0ull, (unsigned long long)key) == 0ull) {
@@ -1165,6 +1316,8 @@ __device__ inline void on_removed(const Ctx& c, uint32_t v, uint32_t s) {
   if (e) {
     coll_clear(c, e);
     c.clr_tick[v - c.lo] = (uint32_t)c.T;  // v's receipt bits predating this tick are void
+    MemberDev& m = mem(c, v);
+    m.clr_serial = m.gix_base + gsched(c, v).len;
   }
   c.compact_flag[v - c.lo] = 1u;
 }
@@ -1217,6 +1370,32 @@ __device__ __forceinline__ void gix_note_at(const Ctx& c, MemberDev& m, uint32_t
   if (!m.gix_valid) return;
   if (2 * m.gix_used >= c.gix_mask + 1) { m.gix_valid = 0; return; }
   gix_put(c, m, len, gix_of(c, v), g, s, m.gix_base + pos);
+}
+// A GossipState can outlive its collector entry only if it predates a clear of the member's
+// collectors: while every state in the slab was appended after the last clear (the sweep has dropped
+// the older ones), a sequence id a cleared collector accepts has no state yet, as for any other
+// collector, and the gossip lookup (and the index behind it) is not needed.
+__device__ __forceinline__ bool pre_clear_states(const MemberDev& m) {
+  return (int32_t)(m.clr_serial - m.gix_base) > 0;
+}
+// gix_put for many lanes at once (the whole-wave delivery): a free slot (empty, or a swept gossip's)
+// is taken by compare-and-swap, so lanes racing for one slot each end in a slot of their own.  The
+// slots taken differ from one-by-one inserts, the lookups' answers do not: a key sits in the first
+// slot of its probe sequence that was free when it got there, and a slot never becomes empty again
+// (swept slots stay non-empty until a rebuild).  Returns whether an empty slot was taken.
+__device__ inline bool gix_put_atomic(uint32_t* ix, uint32_t mask, uint32_t base, uint32_t len, uint32_t g, uint32_t s,
+                                      uint32_t serial) {
+  uint32_t h = gix_hash(g, s);
+  for (uint32_t i = 0; i <= mask; ++i, ++h) {
+    uint32_t* slot = ix + (h & mask);
+    uint32_t e = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (e == NONE || e - base >= len) {
+      const uint32_t old = atomicCAS(slot, e, serial);
+      if (old == e) return e == NONE;
+      e = old;
+    }
+  }
+  return false;  // (unreachable at <= half load)
 }
 // slab position of (g, s), or -1
 __device__ inline int32_t gix_find(const Ctx& c, MemberDev& m, uint32_t v, const SlabRef& slab, uint32_t g,

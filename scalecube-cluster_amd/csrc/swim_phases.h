@@ -18,7 +18,7 @@ namespace swimdev {
 // Phase timing for profiling builds only (-DSWIM_PHASE_PROF, tools/phase_prof.sh): per-wave wall
 // time (s_memrealtime, 100 MHz) of the delivery kernel's parts, summed into g_dbg; read with
 // swim_debug_counters.  The product build compiles none of it.
-__device__ unsigned long long g_dbg[48];
+__device__ unsigned long long g_dbg[64];
 #ifdef SWIM_PHASE_PROF
 #define PPROF_T0(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
 #define PPROF_ADD(slot, t0)                                                                          \
@@ -84,7 +84,6 @@ struct Peers {
   const GSlot* gslot[MAXW];
   const uint32_t* gbits[MAXW];
   const uint32_t* clr_tick[MAXW];
-  uint32_t gwords[MAXW];
 };
 // rx_cnt[kind][p]: what peer p produced for this shard this tick (kind 0 GOSSIP_REQs, 1 SYNCs,
 // 2 SYNC_ACKs) and, kind 3, its completed graceful leaves (broadcast)
@@ -983,10 +982,10 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
       auto rword = [&](uint32_t jj) -> uint32_t {
         const uint32_t t = s_t[1 + min(jj, nt - 1)];
         if (!(win && jj < nt)) return 0u;
-        if (owned(c, t)) return c.gbits[(size_t)sl * c.gwords + ((t - c.lo) >> 5)];
+        if (owned(c, t)) return c.gbits[rbit_word(t - c.lo, sl)];
         if (!b.rfilter) return 0u;
         const uint32_t p = t / c.sz;
-        return b.peers->gbits[p][(size_t)sl * b.peers->gwords[p] + ((t - p * c.sz) >> 5)];
+        return b.peers->gbits[p][rbit_word(t - p * c.sz, sl)];
       };
       const uint32_t wb0 = rword(0), wb1 = rword(1), wb2 = rword(2), wb3 = rword(3);
       // GossipState.infected beyond its first member (rare: the overflow table, once per pass)
@@ -1035,8 +1034,8 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
           // targets' probes in one batch
           const uint32_t i = t - c.lo;
           const uint32_t word = j == 0 ? wb0 : j == 1 ? wb1 : j == 2 ? wb2 : j == 3 ? wb3
-                                                 : c.gbits[(size_t)sl * c.gwords + (i >> 5)];
-          const bool known = gs_ok && s_t[82 + j] < gs.tick && ((word >> (i & 31)) & 1u);
+                                                 : c.gbits[rbit_word(i, sl)];
+          const bool known = gs_ok && s_t[82 + j] < gs.tick && ((word >> (sl & 31)) & 1u);
           if (known) mat = false;
           else probe |= 1u << j;
         } else if (mat && b.rfilter) {
@@ -1048,8 +1047,8 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
           // through the batch cost the unsharded kernel registers and spills)
           const uint32_t p = t / c.sz, i = t - p * c.sz;
           const uint32_t word = j == 0 ? wb0 : j == 1 ? wb1 : j == 2 ? wb2 : j == 3 ? wb3
-                                                 : b.peers->gbits[p][(size_t)sl * b.peers->gwords[p] + (i >> 5)];
-          if ((word >> (i & 31)) & 1u) {
+                                                 : b.peers->gbits[p][rbit_word(i, sl)];
+          if ((word >> (sl & 31)) & 1u) {
             const GSlot ps = b.peers->gslot[p][sl];
             if (ps.key == key && s_t[82 + j] < ps.tick) mat = false;
           }
@@ -1148,7 +1147,7 @@ __device__ __forceinline__ unsigned long long gossip_emit_sender(const Ctx& c, c
       sinkw ^= (uint32_t)gload(&c.gslot[sn].key);
       for (uint32_t jj = 0; jj < min(nt, 3u); ++jj) {
         const uint32_t tj = s_t[1 + jj];
-        if (owned(c, tj)) sinkw ^= gload(&c.gbits[(size_t)sn * c.gwords + ((tj - c.lo) >> 5)]);
+        if (owned(c, tj)) sinkw ^= gload(&c.gbits[rbit_word(tj - c.lo, sn)]);
       }
     }
   }
@@ -1210,6 +1209,7 @@ __device__ __forceinline__ void gossip_round(const Ctx& c, const Bufs& b, uint32
             if (base[j].key && (int32_t)coll_size(c, base + j) > c.seg_threshold) {
               coll_clear(c, base + j);
               c.clr_tick[i] = (uint32_t)c.T;
+              c.mem[i].clr_serial = c.mem[i].gix_base + gs.len;
             }
         }
         busy = gs.len != 0;  // else no target selection, no shuffle draw
@@ -1551,21 +1551,17 @@ __device__ __forceinline__ uint32_t warm_gossip_req(const Ctx& c, uint32_t r, co
 }
 
 // onGossipReq (GossipProtocolImpl.java:201-215) for one received message, in canonical order
-__device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, const SlabRef& slab, const GMsgFull& g) {
-  if (g.dup()) return false;  // the collector held it on arrival and only grows until now
-  CollEnt cv;
-  CollEnt* col = coll_ensure_v(c, r, g.gossiper, cv);
-  if (!col) return false;
-  const bool was_cleared = (cv.meta & COLL_CLEARED) != 0;
-  const bool added = coll_add(c, col, g.seq, &c.seg_flag[r - c.lo], &cv);
-  if (!added) return false;
-  receipt_mark(c, r, g.gossiper, g.seq);
+// onGossipReq after the collector accepted the sequence id (and the receipt bit is marked): the
+// gossip's state is appended and onMembershipGossip runs, or — only if `lookup` (the collector was
+// cleared, and states older than the clear are still in the slab) — a state that outlived the clear
+// takes the sender as infected
+__device__ __forceinline__ void gossip_accepted(const Ctx& c, uint32_t r, MemberDev& m, const SlabRef& slab, const GMsgFull& g,
+                                       bool lookup) {
   PPROF_T0(tc);
-  // a GossipState can outlive its collector entry only after a clear
-  const int32_t found = was_cleared ? gix_find(c, m, r, slab, g.gossiper, g.seq) : -1;
+  const int32_t found = lookup ? gix_find(c, m, r, slab, g.gossiper, g.seq) : -1;
   if (found < 0) {
     GossipSched& gs = gsched(c, r);
-    if (gs.len >= c.gcap) { set_err(c, ERR_SLAB); return true; }
+    if (gs.len >= c.gcap) { set_err(c, ERR_SLAB); return; }
     GossipDev ns;
     ns.gossiper = g.gossiper; ns.seq = g.seq; ns.subject = g.subject; ns.status = g.status(); ns.inc = g.inc();
     ns.inf_period = gs.period;
@@ -1599,6 +1595,18 @@ __device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, con
       else set_err(c, ERR_INFECTED);
     }
   }
+}
+__device__ inline bool on_gossip_req(const Ctx& c, uint32_t r, MemberDev& m, const SlabRef& slab, const GMsgFull& g) {
+  if (g.dup()) return false;  // the collector held it on arrival and only grows until now
+  CollEnt cv;
+  CollEnt* col = coll_ensure_v(c, r, g.gossiper, cv);
+  if (!col) return false;
+  const bool was_cleared = (cv.meta & COLL_CLEARED) != 0;
+  const bool added = coll_add(c, col, g.seq, &c.seg_flag[r - c.lo], &cv);
+  if (!added) return false;
+  receipt_mark(c, r, g.gossiper, g.seq);
+  // a GossipState can outlive its collector entry only after a clear
+  gossip_accepted(c, r, m, slab, g, was_cleared && pre_clear_states(m));
   return true;
 }
 
@@ -1622,6 +1630,9 @@ __device__ __forceinline__ void ins_bar() {
 // the inserted members are written — the list k sequential ArrayList.add calls leave.  NT threads
 // cooperate (a workgroup, WG = true, or one wave); every thread of the group calls it.  sP / sS / sR:
 // NT words of LDS each.
+#ifndef INS_U
+#define INS_U 4  // list elements a thread moves per step of apply_ins_batch (1: one, for A/B)
+#endif
 template <int NT, bool WG>
 __device__ __forceinline__ void apply_ins_batch(const Ctx& c, uint32_t v, uint32_t tid, uint32_t* sP, uint32_t* sS, uint32_t* sR) {
   MemberDev& m = mem(c, v);
@@ -1660,25 +1671,34 @@ __device__ __forceinline__ void apply_ins_batch(const Ctx& c, uint32_t v, uint32
       sR[rk] = p;
     }
     ins_bar<WG>();
-    // original element i lands at i + #{j : sR[j] - j <= i} (sR[j] - j is non-decreasing)
+    // original element i lands at i + #{j : sR[j] - j <= i} (sR[j] - j is non-decreasing).  The
+    // elements move tail first, INS_U * NT per step: the step's loads, one group barrier, its stores.
+    // A step stores at or above its lowest source and the next step loads below it, so only a step's
+    // own loads must precede its stores (one barrier a step, where one element a thread took two).
     const uint32_t pmin = sR[0];
-    for (int64_t hi = (int64_t)len; hi > (int64_t)pmin; hi -= NT) {
-      const int64_t lo = hi - NT > (int64_t)pmin ? hi - NT : (int64_t)pmin;
-      const int64_t i = lo + tid;
-      uint32_t val = 0, dest = 0;
-      if (i < hi) {
-        val = pl[i];
-        uint32_t a = 0, z = kb;
-        while (a < z) {
-          const uint32_t mid = (a + z) >> 1;
-          if (sR[mid] - mid <= (uint32_t)i) a = mid + 1; else z = mid;
+    for (int64_t hi = (int64_t)len; hi > (int64_t)pmin; hi -= (int64_t)NT * INS_U) {
+      uint32_t val[INS_U], dest[INS_U];
+#pragma unroll
+      for (int u = 0; u < INS_U; ++u) {
+        const int64_t i = hi - (int64_t)NT * (u + 1) + tid;
+        val[u] = 0;
+        dest[u] = NONE;
+        if (i >= (int64_t)pmin) {
+          val[u] = pl[i];
+          uint32_t a = 0, z = kb;
+          while (a < z) {
+            const uint32_t mid = (a + z) >> 1;
+            if (sR[mid] - mid <= (uint32_t)i) a = mid + 1; else z = mid;
+          }
+          dest[u] = (uint32_t)i + a;
         }
-        dest = (uint32_t)i + a;
       }
       ins_bar<WG>();
-      if (i < hi) pl[dest] = val;
-      ins_bar<WG>();
+#pragma unroll
+      for (int u = 0; u < INS_U; ++u)
+        if (dest[u] != NONE) pl[dest[u]] = val[u];
     }
+    // (the inserted members' slots are no move's destination, and every move's load was waited on)
     if (tid < kb) pl[sP[tid]] = sS[tid];
     len += kb;
     ins_bar<WG>();
@@ -1755,7 +1775,7 @@ __device__ __forceinline__ int big_find(const uint32_t* snd, uint32_t nd, uint32
 // collection follows.
 // lds_perm: an inbox of at most 64 messages keeps its permutation in L.perm instead of pg_perm (the
 // whole-wave delivery reads it from there: no dependent global round trip before its messages).
-__device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L,
+__device__ __forceinline__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L,
                                    bool lds_perm = false) {
   const uint32_t* pt = b.pg_tab + (size_t)i * b.pg_max;
   auto msg_at = [&](uint32_t q) -> const GMsgFull& { return b.pg_msgs[(size_t)pt[q >> 6] * 64 + (q & 63)]; };
@@ -1861,9 +1881,12 @@ __device__ uint32_t rank_big_inbox(const Ctx& c, const Bufs& b, uint32_t i, uint
 //      in rank order (a collector's intervals — and the segmentation flag — see the same sequence of
 //      adds as in the chain); leaders of different gossipers run side by side (two finding one empty
 //      table slot are told apart by ballot, coll_ensure_wave: no compare-and-swap round trip).  A lane whose add fails holds a copy the collector already had:
-//      rejected, as in the chain.  Messages of the member's own gossips, and of gossipers whose
-//      collector was cleared (a GossipState may outlive it: the gix lookup), take the chain's own
-//      onGossipReq at their turn in (c) instead.
+//      rejected, as in the chain.  Messages of the member's own gossips take the chain's own
+//      onGossipReq at their turn in (c) instead.  A collector that was cleared takes its adds here as
+//      well; while states older than the clear are still in the slab (pre_clear_states) its accepted
+//      lanes look their state up at their turn in (c) (a GossipState may outlive the clear: gix_find,
+//      the index rebuilt by the whole wave when needed), which takes one serial step each instead of
+//      a single-lane collector add over thousands of intervals.
 //  (b) receipt marks of the accepted lanes; then which accepted records cannot change the view: the
 //      namespace filter drops them, or they do not override the subject's record as it stands after
 //      the earlier chunks and no earlier lane of the chunk may change that subject
@@ -1889,6 +1912,33 @@ __device__ __forceinline__ uint32_t wave_from_prev(uint32_t v) {
 #endif
 constexpr uint32_t COOP_LIV = 2048;  // intervals of one collector staged in LDS per wave (16 KB)
 constexpr uint32_t COOP_MIN = 16;  // Bufs.coop_min's default (every big inbox: measured best, 16 / 32 / 64)
+// gix_find's rebuild of the slab index made by a whole wave (the first lookup a cleared collector
+// needs in the whole-wave delivery): the table emptied 64 slots at a time, the slab's len states
+// inserted 64 at a time (gix_put_atomic), where one lane takes mask + 1 stores and len dependent
+// inserts (2^19 and ~10^5 at config 3's churn)
+__device__ inline void gix_rebuild_wave(const Ctx& c, MemberDev& m, uint32_t v, const SlabRef& slab, uint32_t len,
+                                        uint32_t lane) {
+  uint32_t* ix = gix_of(c, v);
+  const uint32_t mask = c.gix_mask;
+  const uint32_t base = __builtin_amdgcn_readfirstlane(m.gix_base);
+  for (uint32_t q = lane; q <= mask; q += 64) ix[q] = NONE;
+  wave_sync();
+  uint32_t took = 0;
+  for (uint32_t p0 = 0; p0 < len; p0 += 64) {
+    const uint32_t p = p0 + lane;
+    if (p < len) {
+      const GossipHot h = slab.Hg(p);
+      took += gix_put_atomic(ix, mask, base, len, h.gossiper, h.seq, base + p) ? 1u : 0u;
+    }
+  }
+  took = (uint32_t)wave_sum(took);
+  if (lane == 0) {
+    m.gix_used = took;
+    m.gix_valid = 1;
+  }
+  wave_sync();
+}
+
 __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const Bufs& b, uint32_t i, uint32_t k, uint32_t lane, BigLds& L,
                                            uint2* siv, uint32_t& nfresh) {
   const uint32_t r = c.lo + i;
@@ -1902,6 +1952,10 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
   }
   uint32_t len = __builtin_amdgcn_readfirstlane(gsr.len);
   const uint32_t period = gsr.period;
+  // no state predates the last collector clear: a cleared collector's adds are made in (a) like any
+  // other's, and the slab index need not be kept up (pre_clear_states)
+  const bool pre = pre_clear_states(m);
+  if (!pre && lane == 0 && m.gix_valid) m.gix_valid = 0;
   if (lane == 0 && period > PER_MASK) set_err(c, ERR_INC);  // (2^28 gossip rounds)
   unsigned long long acc = 0;
   // The messages in rank order, pipelined across chunks: a chunk's messages are loaded at the start
@@ -1984,11 +2038,11 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
       PPROF_CNT(30, (unsigned long long)__popcll(__ballot(grp != 0)));  // leaders
       // inline collectors: each leader runs its adds in registers (one store at the end); a run that
       // needs a second interval, and every spilled collector, goes on to the staged pass with the
-      // lanes it has left (rest)
+      // lanes it has left (rest).  A cleared collector takes its adds here too; while states older
+      // than the clear are in the slab its accepted lanes look their state up in (c) (relook)
+      const bool relook_grp = col && (cv.meta & COLL_CLEARED) && pre;
       uint64_t rest = 0;
-      if (col && (cv.meta & COLL_CLEARED)) {
-        for (uint64_t mm = grp; mm; mm &= mm - 1) L.iS[__ffsll((unsigned long long)mm) - 1] = 2;
-      } else if (col && (cv.meta & 7u) == COLL_SPILLED) {
+      if (col && (cv.meta & 7u) == COLL_SPILLED) {
         rest = grp;
       } else if (col) {
         const CollEnt v0 = cv;
@@ -2074,12 +2128,20 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
           PPROF_CNT(39, 1ull);
           continue;
         }
-        if (!COOP_STAGE || n0 + (uint32_t)__popcll(rm) > COOP_LIV) {  // beyond the staging area: coll_add one by one
-          if (lane == l) {
-            if (!spilled) *e = cv;
+        if (!COOP_STAGE || n0 + (uint32_t)__popcll(rm) > COOP_LIV) {  // beyond the staging area
+          if (!COOP_STAGE || !spilled) {  // coll_add one by one
+            if (lane == l) {
+              if (!spilled) *e = cv;
+              for (uint64_t mm = rm; mm; mm &= mm - 1) {
+                const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
+                L.iS[j] = coll_add(c, e, L.iP[j], &c.seg_flag[i]) ? 1u : 0u;
+              }
+            }
+          } else {  // in place in its block, each add by the whole wave
             for (uint64_t mm = rm; mm; mm &= mm - 1) {
               const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
-              L.iS[j] = coll_add(c, e, L.iP[j], &c.seg_flag[i]) ? 1u : 0u;
+              const int a = coll_add_wave(c, e, L.iP[j], lane, [] { wave_sync(); }, &c.seg_flag[i]);
+              if (lane == 0) L.iS[j] = (uint32_t)a;
             }
           }
           wave_sync();
@@ -2099,29 +2161,24 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
         PPROF_T0(tsa);
         uint32_t n = n0;
         uint32_t* dst = nullptr;
-#ifdef SWIM_PHASE_PROF
         uint32_t moved = 0;
-#endif
+        // the leader's adds, made by the whole wave (coll_add_lds_wave: the moves 64 at a time)
+        uint32_t maxn = n;
+        bool seg = false;
+        for (uint64_t mm = rm; mm; mm &= mm - 1) {
+          const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
+          const int a = coll_add_lds_wave(siv, n, L.iP[j], lane, [] { wave_sync(); }, &moved);
+          if (lane == 0) L.iS[j] = (uint32_t)a;
+          seg |= a && n >= 2 && n > (uint32_t)c.seg_threshold;
+          maxn = max(maxn, n);
+        }
+        wave_sync();
         if (lane == l) {
-          uint32_t maxn = n;
-          bool seg = false;
-          for (uint64_t mm = rm; mm; mm &= mm - 1) {
-            const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
-#ifdef SWIM_PHASE_PROF
-            const int a = coll_add_lds(siv, n, L.iP[j], &moved);
-#else
-            const int a = coll_add_lds(siv, n, L.iP[j]);
-#endif
-            L.iS[j] = (uint32_t)a;
-            seg |= a && n >= 2 && n > (uint32_t)c.seg_threshold;
-            maxn = max(maxn, n);
-          }
           if (seg) c.seg_flag[i] = 1;
           dst = coll_place(c, e, meta, n, maxn, siv[0].x, siv[0].y);
         }
-#ifdef SWIM_PHASE_PROF
-        PPROF_CNT(37, (unsigned long long)rdlane(moved, l));
-#endif
+        PPROF_CNT(37, (unsigned long long)moved);
+        (void)moved;
         PPROF_ADD(33, tsa);
         PPROF_T0(tsw);
         n = rdlane(n, l);
@@ -2133,6 +2190,12 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
         wave_sync();
         PPROF_ADD(34, tsw);
       }
+      wave_sync();
+      if (relook_grp)
+        for (uint64_t mm = grp; mm; mm &= mm - 1) {
+          const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
+          if (L.iS[j] == 1u) L.iS[j] = 3u;
+        }
       PPROF_ADD(28, tce);
     }
     wave_sync();
@@ -2145,7 +2208,8 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
     PPROF_ADD(13, tca);
     PPROF_T0(tcb);
     const uint32_t fl = L.iS[lane];
-    const bool accepted = fl == 1u;
+    const bool accepted = fl == 1u || fl == 3u;
+    const bool relook = fl == 3u;  // accepted by a cleared collector: its state is looked up at its turn
     const bool full = (valid && !coop) || fl == 2u;  // the chain's onGossipReq, at its turn
     // (b) receipts; the records that cannot change the view
     const bool user = g.status() >= SWIM_GOSSIP_USER;
@@ -2162,10 +2226,10 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
         noop = !(present && st0 == SWIM_LEAVING) && !is_overrides(g.status(), g.inc(), present, st0, c_inc(cell));
       }
     }
-    bool skip = accepted && noop;
+    bool skip = accepted && noop && !relook;
     // (a lane that may change its subject's record: an accepted non-no-op one, or one taking the
-    // chain's onGossipReq)
-    for (uint64_t mm = __ballot(((accepted && !noop) || full) && !user); mm; mm &= mm - 1) {
+    // chain's onGossipReq or a lookup)
+    for (uint64_t mm = __ballot(((accepted && !noop) || full || relook) && !user); mm; mm &= mm - 1) {
       const uint32_t j = (uint32_t)__ffsll((unsigned long long)mm) - 1;
       const uint32_t sj = rdlane(g.subject, j);
       if (lane > j && !user && g.subject == sj) skip = false;
@@ -2178,8 +2242,15 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
     PPROF_ADD(14, tcb);
     PPROF_CNT(6, (unsigned long long)__popcll(serm));  // lanes taking a serial step
     PPROF_CNT(7, (unsigned long long)__popcll(accm));  // accepted lanes
+    PPROF_CNT(47, (unsigned long long)__popcll(__ballot(full)));  // lanes taking the chain's onGossipReq
     PPROF_T0(tcc);
     const uint64_t below_me = (1ull << lane) - 1;
+    if (pre && __ballot(full || relook) && !__builtin_amdgcn_readfirstlane(m.gix_valid)) {
+      PPROF_T0(tgr);
+      gix_rebuild_wave(c, m, r, slab, len, lane);
+      PPROF_CNT(53, 1ull);
+      PPROF_ADD(54, tgr);
+    }
     GossipDev ns;
     ns.gossiper = g.gossiper; ns.seq = g.seq; ns.subject = g.subject; ns.status = g.status(); ns.inc = g.inc();
     ns.inf_period = period;
@@ -2193,6 +2264,7 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
       const uint64_t below = jn == 64u ? ~0ull : ((1ull << jn) - 1);
       const uint64_t blk = accm & ~serm & below & ~done;  // no-op lanes before the next serial one
       if (blk) {
+        PPROF_T0(tbk);
         uint32_t pos = NONE;
         if ((blk >> lane) & 1ull) {
           const uint32_t p = len + (uint32_t)__popcll(blk & below_me);
@@ -2204,18 +2276,35 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
           }
         }
         len = min(len + (uint32_t)__popcll(blk), c.gcap);
-        if (__builtin_amdgcn_readfirstlane(m.gix_valid))  // (only after a collector clear needed the index)
-          for (uint64_t bm = __ballot(pos != NONE); bm; bm &= bm - 1)
-            if (lane == (uint32_t)__ffsll((unsigned long long)bm) - 1) gix_note_at(c, m, r, g.gossiper, g.seq, pos, len);
+        if (__builtin_amdgcn_readfirstlane(m.gix_valid)) {  // (only after a collector clear needed the index)
+          // the block's states noted in the index together (gix_note_at for every lane at once; at
+          // half load the index is dropped, to be rebuilt by the next lookup)
+          const uint32_t nput = (uint32_t)__popcll(__ballot(pos != NONE));
+          const uint32_t used0 = __builtin_amdgcn_readfirstlane(m.gix_used);
+          PPROF_CNT(48, (unsigned long long)nput);
+          if (2 * (used0 + nput) >= c.gix_mask + 1) {
+            if (lane == 0) m.gix_valid = 0;
+          } else {
+            const bool took = pos != NONE && gix_put_atomic(gix_of(c, r), c.gix_mask, __builtin_amdgcn_readfirstlane(m.gix_base),
+                                                            len, g.gossiper, g.seq,
+                                                            __builtin_amdgcn_readfirstlane(m.gix_base) + pos);
+            const uint32_t nt = (uint32_t)__popcll(__ballot(took));
+            if (lane == 0) m.gix_used = used0 + nt;
+          }
+        }
         done |= blk;
         wave_sync();
+        PPROF_ADD(49, tbk);
       }
       if (!mm) break;
+      PPROF_T0(tsr);
       uint32_t nl = 0;
       if (lane == jn) {
         gsr.len = len;
         if (full) {
           fullacc += on_gossip_req(c, r, m, slab, g) ? 1u : 0u;
+        } else if (relook) {
+          gossip_accepted(c, r, m, slab, g, true);
         } else if (len >= c.gcap) {
           set_err(c, ERR_SLAB);
         } else {
@@ -2233,6 +2322,9 @@ __device__ __forceinline__ unsigned long long deliver_coop(const Ctx& c, const B
       done |= 1ull << jn;
       mm &= mm - 1;
       wave_sync();
+#ifdef SWIM_PHASE_PROF
+      if (rdlane(full || relook ? 1u : 0u, jn)) PPROF_ADD(50, tsr); else PPROF_ADD(51, tsr);
+#endif
     }
     PPROF_ADD(15, tcc);
     acc += (accepted ? 1ull : 0ull) + fullacc;  // (per lane: the caller sums the wave)
@@ -2386,9 +2478,26 @@ __device__ unsigned long long deliver_big_batch(const Ctx& c, const Ctx& cs, con
     const uint32_t np = rdlane(my_pages, j);
     for (uint32_t pg = lane; pg < np; pg += 64)
       if (pg) b.pg_tab[(size_t)i * b.pg_max + pg] = NONE;  // (page 0 is the receiver's own)
+#ifdef SWIM_PHASE_PROF
+    {  // inserts applied: count, receivers, their lists' lengths, the largest batch, the time
+      const uint32_t kk = __builtin_amdgcn_readfirstlane(mem(c, r).ins_rank);
+      if (kk) {
+        PPROF_CNT(41, (unsigned long long)kk);
+        PPROF_CNT(43, 1ull);
+        PPROF_CNT(44, (unsigned long long)__builtin_amdgcn_readfirstlane(mem(c, r).ping_len));
+        if (lane == 0) atomicMax(&g_dbg[42], (unsigned long long)kk);
+      }
+      PPROF_T0(tin);
+      apply_ins_batch<64, false>(c, r, lane, L.iP, L.iS, L.iR);
+      PPROF_ADD(45, tin);
+    }
+#else
     apply_ins_batch<64, false>(c, r, lane, L.iP, L.iS, L.iR);
+#endif
   }
+  PPROF_T0(tcol);
   if (lane < nb && collect) nsync += sync_collect_member(cs, b, c.lo + list[lane]);
+  PPROF_ADD(46, tcol);
   PPROF_ADD(2, tp2);
   return acc;
 }
@@ -3120,16 +3229,36 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
       b.sdq_cnt[(uint32_t)T & DQ_MASK] = 0;  // this tick's delayed SYNC arrivals are in the inboxes
     }
   }
-  // receipt-bitmap slots requested this tick change owner (no other kernel runs now): zeroed bits,
-  // valid from the next tick; the other parity's queue (next tick's) is emptied
+  // receipt-bitmap slots requested this tick change owner (no other kernel runs now): their bit
+  // cleared in every receiver's row, valid from the next tick; the other parity's queue (next tick's)
+  // is emptied.  The claimed bits are gathered per row word in LDS first, so each row is touched once
+  // per claimed word (a few words: claims come with new gossips)
   {
     const uint32_t par = (uint32_t)(T & 1);
-    const uint32_t nclaim = min(c.gclaim_cnt[par], GSLOTS);
-    for (uint32_t q = blockIdx.x; q < nclaim; q += gridDim.x) {
-      const uint32_t sl = c.gclaim[par * GSLOTS + q];
-      uint32_t* bits = c.gbits + (size_t)sl * c.gwords;
-      for (uint32_t w = threadIdx.x; w < c.gwords; w += blockDim.x) bits[w] = 0;
-      if (threadIdx.x == 0) {
+    const uint32_t nclaim = min(c.gclaim_cnt[par], GSLOTS);  // (grid-uniform: nothing writes it now)
+    if (nclaim) {
+      __shared__ uint32_t s_cm[GROW], s_nz[GROW], s_nnz;
+      for (uint32_t w = threadIdx.x; w < GROW; w += blockDim.x) s_cm[w] = 0;
+      if (threadIdx.x == 0) s_nnz = 0;
+      __syncthreads();
+      for (uint32_t q = threadIdx.x; q < nclaim; q += blockDim.x) {
+        const uint32_t sl = c.gclaim[par * GSLOTS + q];
+        atomicOr(&s_cm[sl >> 5], 1u << (sl & 31));
+      }
+      __syncthreads();
+      for (uint32_t w = threadIdx.x; w < GROW; w += blockDim.x)
+        if (s_cm[w]) s_nz[atomicAdd(&s_nnz, 1u)] = w;
+      __syncthreads();
+      if (i < c.nl) {
+        uint32_t* row = c.gbits + (size_t)i * GROW;
+        const uint32_t nnz = s_nnz;
+        for (uint32_t k2 = 0; k2 < nnz; ++k2) {
+          const uint32_t w = s_nz[k2];
+          row[w] &= ~s_cm[w];
+        }
+      }
+      for (uint32_t q = i; q < nclaim; q += gridDim.x * blockDim.x) {
+        const uint32_t sl = c.gclaim[par * GSLOTS + q];
         c.gslot[sl].key = c.gpend[sl];
         c.gslot[sl].tick = (uint32_t)T + 1;
         c.gpend[sl] = 0;

@@ -19,9 +19,11 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 # scratch bytes per thread the hot kernels may use (the per-tick chain, the storm kernels, the
 # quiet windows); measured values in round 5: 80 / 144 / 144 / 0 / 56 / 0 / 0 / 0 (k_gossip_deliver
 # was 28 until onGossipReq's infected-list insert stopped indexing GossipDev.inf at run time: such an
-# index puts the array in scratch; k_deliver_coop runs at its 256-VGPR cap, these are spills)
+# index puts the array in scratch; k_deliver_coop runs at its 256-VGPR cap, these are spills: 88 B
+# in round 6 with the whole-wave slab-index rebuild and the cleared collectors' lookups, whose
+# spills sit around those rare paths — churn's delivery went 460 -> 330 ms per launch with them)
 SCRATCH_MAX = {"k_fd": 128, "k_sync_apply": 256, "k_ack_apply": 256, "k_gossip_deliver": 32,
-               "k_deliver_coop": 64, "k_gossip_emit": 64, "k_quiet_scan": 0, "k_quiet_apply": 0}
+               "k_deliver_coop": 96, "k_gossip_emit": 64, "k_quiet_scan": 0, "k_quiet_apply": 0}
 
 
 @pytest.fixture(scope="module")

@@ -44,7 +44,7 @@ def main():
     sch.run(e, args.warmup, args.warmup + args.steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    d = abi.debug_counters(lib, 48)
+    d = abi.debug_counters(lib, 64)
     dp = e.profile_deliver()
     launches = args.steps * 5  # gossip rounds in the window
     waves = 512 * 4  # DLV_GRID x DLV_WAVES
@@ -71,6 +71,18 @@ def main():
                       "staged_shifted": d[37] / launches,
                       # small collectors (<= 64 intervals) in registers: time, count
                       "reg_pass_us": per(d[38]), "reg_staged": d[39] / launches, "coop_b_us": per(d[14]), "coop_c_us": per(d[15]),
+                      # (c)'s lanes that take the chain's onGossipReq; slab-index rebuilds by a whole wave
+                      "coop_full_lanes": d[47] / launches, "gix_wave_rebuilds": d[53] / launches,
+                      "gix_rebuild_us": per(d[54]),
+                      # (c)'s parts: no-op blocks (and their index notes), serial steps of the chain's
+                      # onGossipReq lanes and of the others
+                      "c_noop_us": per(d[49]), "c_noop_gix_notes": d[48] / launches, "c_full_us": per(d[50]),
+                      "c_serial_us": per(d[51]),
+                      # the big-inbox tail: pingMembers inserts applied (per launch), receivers with
+                      # inserts, their lists' mean length, the largest batch, insert and collection times
+                      "tail_inserts": d[41] / launches, "tail_ins_receivers": d[43] / launches,
+                      "tail_ins_mean_list": d[44] / max(1, d[43]), "tail_ins_max": d[42],
+                      "tail_ins_us": per(d[45]), "tail_collect_us": per(d[46]),
                       "longest_chain_msgs": d[10], "chain_msgs_per_launch": d[11] / launches,
                       "sum_of_wave_longest_chains": d[12] / launches,
                       "messages_per_launch": dp["messages"] / max(1, dp["launches"])}))
