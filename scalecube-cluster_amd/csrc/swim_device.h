@@ -1241,14 +1241,17 @@ __device__ inline void coll_clear(const Ctx& c, CollEnt* e) {
 __device__ inline void receipt_mark(const Ctx& c, uint32_t r, uint32_t gossiper, uint32_t seq) {
   const uint64_t key = gkey(gossiper, seq);
   const uint32_t sl = gslot_of(key);
-  if (c.gslot[sl].key == key) {
+  const uint64_t owner = c.gslot[sl].key;
+  if (owner == key) {
     const uint32_t i = r - c.lo;
     atomicOr(&c.gbits[rbit_word(i, sl)], 1u << (sl & 31));
   } else if (c.gpend[sl] == 0ull &&  // (a plain read first: once claimed, the thousands of receivers of a
                                      // new gossip skip the contended compare-and-swap)
              atomicCAS(reinterpret_cast<unsigned long long*>(&c.gpend[sl]), 0ull, (unsigned long long)key) == 0ull) {
     const uint32_t par = (uint32_t)(c.T & 1);
-    c.gclaim[par * GSLOTS + atomicAdd(&c.gclaim_cnt[par], 1u)] = sl;  // at most one entry per slot
+    // at most one entry per slot; bit 31: the slot had an owner, whose bits the claim must clear (a
+    // never-owned slot's bits are all zero: only an owned slot's gossip sets any)
+    c.gclaim[par * GSLOTS + atomicAdd(&c.gclaim_cnt[par], 1u)] = sl | (owner ? 0x80000000u : 0u);
   }
 }
 

@@ -3242,8 +3242,8 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
       if (threadIdx.x == 0) s_nnz = 0;
       __syncthreads();
       for (uint32_t q = threadIdx.x; q < nclaim; q += blockDim.x) {
-        const uint32_t sl = c.gclaim[par * GSLOTS + q];
-        atomicOr(&s_cm[sl >> 5], 1u << (sl & 31));
+        const uint32_t e = c.gclaim[par * GSLOTS + q];
+        if (e >> 31) atomicOr(&s_cm[(e & 0x7fffffffu) >> 5], 1u << (e & 31));  // (a first owner: nothing to clear)
       }
       __syncthreads();
       for (uint32_t w = threadIdx.x; w < GROW; w += blockDim.x)
@@ -3258,7 +3258,7 @@ __global__ void __launch_bounds__(REB_BLOCK) k_end_tick(KP, int rebase) {
         }
       }
       for (uint32_t q = i; q < nclaim; q += gridDim.x * blockDim.x) {
-        const uint32_t sl = c.gclaim[par * GSLOTS + q];
+        const uint32_t sl = c.gclaim[par * GSLOTS + q] & 0x7fffffffu;
         c.gslot[sl].key = c.gpend[sl];
         c.gslot[sl].tick = (uint32_t)T + 1;
         c.gpend[sl] = 0;

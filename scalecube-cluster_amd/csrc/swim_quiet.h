@@ -215,13 +215,19 @@ __device__ __forceinline__ uint32_t quiet_window(const QuietCtl* q, uint32_t K) 
 // draw), so what the common case decides on — its membership word in v's row, its up and inbound
 // words — is loaded in ONE batch; a candidate that is not a member (a seed, or another draw: rare)
 // takes the general path
-__device__ inline void quiet_sync(const Ctx& c0, uint32_t v, uint64_t t, uint32_t tsz, bool inb_v,
-                                  unsigned long long& nsync, unsigned long long& nack, unsigned long long& nrec) {
+// the first candidate of v's doSync at tick t (the draw: pure arithmetic)
+__device__ __forceinline__ uint32_t quiet_sync_x0(const Ctx& c0, uint32_t v, uint64_t t) {
   Ctx c = c0;
   c.T = t;
-  const uint32_t x0 = next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 0, 0), c.n);
-  uint32_t aw = gld(aux_row(c, v) + x0), up0 = gld(c.up + x0), in0 = gld(c.default_inbound + x0);
-  QUIET_BATCH_WAIT("+v"(aw), "+v"(up0), "+v"(in0));
+  return next_int(draw(c, v, SWIM_STREAM_SYNC_SELECT, 0, 0), c.n);
+}
+// quiet_sync once the candidate's words are in (aw: its membership word in v's row, up0 / in0: its up
+// and inbound words)
+__device__ inline void quiet_sync_with(const Ctx& c0, uint32_t v, uint64_t t, uint32_t tsz, bool inb_v, uint32_t x0,
+                                       uint32_t aw, uint32_t up0, uint32_t in0, unsigned long long& nsync,
+                                       unsigned long long& nack, unsigned long long& nrec) {
+  Ctx c = c0;
+  c.T = t;
   uint32_t tg = x0;
   bool ok = up0 != 0 && in0 != 0;
   if (!(x0 != v && ((aw & A_IN_MEMBERS) || is_seed_of(c, v, x0)))) {
@@ -236,6 +242,13 @@ __device__ inline void quiet_sync(const Ctx& c0, uint32_t v, uint64_t t, uint32_
   const unsigned long long ack = ok && inb_v ? 1ull : 0ull;  // its SYNC_ACK passes v's inbound filter
   nack += ack;
   nrec += (dlv + ack) * tsz;  // onSync's syncMembership over the SYNC's records, onSyncAck's (:385-391)
+}
+__device__ inline void quiet_sync(const Ctx& c, uint32_t v, uint64_t t, uint32_t tsz, bool inb_v,
+                                  unsigned long long& nsync, unsigned long long& nack, unsigned long long& nrec) {
+  const uint32_t x0 = quiet_sync_x0(c, v, t);
+  uint32_t aw = gld(aux_row(c, v) + x0), up0 = gld(c.up + x0), in0 = gld(c.default_inbound + x0);
+  QUIET_BATCH_WAIT("+v"(aw), "+v"(up0), "+v"(in0));
+  quiet_sync_with(c, v, t, tsz, inb_v, x0, aw, up0, in0, nsync, nack, nrec);
 }
 
 // The next window's scan, precomputed (QuietPre).  On a pristine cluster the scan's only per-window
@@ -264,14 +277,38 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
                                                      uint32_t tag_in, uint64_t* pre_out, uint32_t tag_out,
                                                      uint32_t H) {
   const Ctx c = pctx(P, T);
-  uint32_t F;
-  if (q) {
-    F = quiet_window(q, K);
-  } else {
-    const uint64_t key = *pre_in;
-    F = (uint32_t)(key >> 32) == 0xffffffffu - tag_in ? min((uint32_t)key, K) : 0u;
-  }
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
+  // ---- batch 1: the window's length and every word of the thread's first member (they do not
+  // depend on the length: loaded beside it, one round trip where they took two)
+  const bool own0 = gtid < c.nl;
+  uint32_t upw = 0, inbw = 0, fdn = 0, sn0 = 0, gnext = 0, gper = 0, gw2 = 0, gw3 = 0;
+  uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0, m4 = 0, m5 = 0, m6 = 0, m7 = 0, m8 = 0, m9 = 0, m10 = 0, m11 = 0;
+  auto load_member = [&](uint32_t i) {
+    const uint32_t v = c.lo + i;
+    upw = gld(c.up + v), inbw = gld(c.default_inbound + v), fdn = gld(c.fd_next + i), sn0 = gld(c.sync_next + i);
+    const uint4 gw4 = gld4(c.gs + i);
+    const uint4* mp = reinterpret_cast<const uint4*>(c.mem + i);
+    const uint4 w0 = gld4(mp), w1 = gld4(mp + 1), w2 = gld4(mp + 2);
+    // (scalars for the asm operands: a vector component bound to an operand went through scratch)
+    m0 = w0.x, m1 = w0.y, m2 = w0.z, m3 = w0.w, m4 = w1.x, m5 = w1.y, m6 = w1.z, m7 = w1.w, m8 = w2.x, m9 = w2.y,
+    m10 = w2.z, m11 = w2.w;
+    gnext = gw4.x, gper = gw4.y, gw2 = gw4.z, gw3 = gw4.w;
+  };
+  // (loaded unconditionally, a thread past the shard's end reading its last member: a load under a
+  // branch is waited for inside it, where its value is copied to the join's register)
+  load_member(c.nl ? min(gtid, c.nl - 1) : 0u);
+  uint32_t qa = 0, qb = 0, qc = 0, kl = 0, kh = 0;
+  if (q) {
+    qa = gld(&q->tmin), qb = gld(&q->tmax_neg), qc = gld(&q->fail);
+  } else {
+    kl = gld(reinterpret_cast<const uint32_t*>(pre_in)), kh = gld(reinterpret_cast<const uint32_t*>(pre_in) + 1);
+  }
+  QUIET_BATCH_WAIT("+v"(upw), "+v"(inbw), "+v"(fdn), "+v"(sn0), "+v"(gnext), "+v"(gper), "+v"(m0), "+v"(m1),
+                   "+v"(m2), "+v"(m3), "+v"(m4), "+v"(m5), "+v"(m6), "+v"(m7), "+v"(m8), "+v"(m9), "+v"(m10),
+                   "+v"(m11), "+v"(qa), "+v"(qb), "+v"(qc), "+v"(kl), "+v"(kh));
+  // quiet_window(q, K), or the window precomputed by the previous apply
+  const uint32_t F = q ? ((qa != 0xffffffffu && qa != 0xffffffffu - qb) ? 0u : min(qc, K))
+                       : (kh == 0xffffffffu - tag_in ? min(kl, K) : 0u);
   if (gtid == 0) {
     *done = F;
     *next = QuietCtl{0xffffffffu, 0xffffffffu, 0xffffffffu, 0u};
@@ -279,24 +316,44 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
   if (F == 0) return;
   const uint64_t Tend = T + F;
   uint32_t nfail = H;  // this thread's share of the next window's first failing offset (from Tend)
+  // ---- batch 2: the next window's timer buckets (k_quiet_scan's check; four per thread a round) and
+  // the first member's first doSync candidate words, waited for together
+  const uint32_t W = c.wheel_mask + 1, nwq = H ? min(H, W) * c.wheel_nq : 0u;
+  auto qaddr = [&](uint32_t x, uint32_t j) {
+    return c.wheel_cnt + (size_t)((Tend + j) & c.wheel_mask) * c.wheel_nq + (x - j * c.wheel_nq);
+  };
+  // (every load unconditional, from a valid address whose value is then ignored where it does not
+  // apply: see batch 1)
+  const bool bq = gtid < nwq;
+  const uint32_t nq1 = nwq ? nwq - 1 : 0u;
+  const uint32_t xa = min(gtid, nq1), xb = min(gtid + gsz, nq1), xc = min(gtid + 2 * gsz, nq1), xd = min(gtid + 3 * gsz, nq1);
+  const uint32_t ja = xa / c.wheel_nq, jb = xb / c.wheel_nq, jc = xc / c.wheel_nq, jd = xd / c.wheel_nq;
+  uint32_t ca = gld(qaddr(xa, ja)), cb = gld(qaddr(xb, jb)), cc = gld(qaddr(xc, jc)), cd = gld(qaddr(xd, jd));
+  const uint32_t v0 = c.lo + (c.nl ? min(gtid, c.nl - 1) : 0u);
+  const bool sy = own0 && upw != 0 && sn0 != NONE && sn0 < Tend;
+  const uint32_t sx = quiet_sync_x0(c, v0, sy ? sn0 : T);
+  // (a member with no doSync in the window reads words of its own, already in the cache)
+  uint32_t saw = gld(sy ? aux_row(c, v0) + sx : reinterpret_cast<const uint32_t*>(c.gs + (v0 - c.lo))),
+           sup = gld(c.up + (sy ? sx : v0)), sin = gld(c.default_inbound + (sy ? sx : v0));
+  QUIET_BATCH_WAIT("+v"(ca), "+v"(cb), "+v"(cc), "+v"(cd), "+v"(saw), "+v"(sup), "+v"(sin));
   if (H) {
     if (gtid == 0) atomicMin(reinterpret_cast<unsigned long long*>(pre_out), pre_key(tag_out, 0xffffffffu));
-    // the timer buckets of the next window (k_quiet_scan's check): four independent loads per round
-    // trip (a loop of one load each waited for every load: ~4 serial round trips at N = 65,536)
-    const uint32_t W = c.wheel_mask + 1, nwq = min(H, W) * c.wheel_nq;
-    for (uint32_t x0 = gtid; x0 < nwq; x0 += 4 * gsz) {
-      // (past the end: a valid address, its count ignored)
-      const uint32_t xa = x0, xb = min(x0 + gsz, nwq - 1), xc = min(x0 + 2 * gsz, nwq - 1), xd = min(x0 + 3 * gsz, nwq - 1);
-      const uint32_t ja = xa / c.wheel_nq, jb = xb / c.wheel_nq, jc = xc / c.wheel_nq, jd = xd / c.wheel_nq;
-      auto qaddr = [&](uint32_t x, uint32_t j) {
-        return c.wheel_cnt + (size_t)((Tend + j) & c.wheel_mask) * c.wheel_nq + (x - j * c.wheel_nq);
-      };
-      uint32_t ca = *qaddr(xa, ja), cb = *qaddr(xb, jb), cc = *qaddr(xc, jc), cd = *qaddr(xd, jd);
-      QUIET_BATCH_WAIT("+v"(ca), "+v"(cb), "+v"(cc), "+v"(cd));
+    if (bq) {
       if (ca) nfail = min(nfail, ja);
-      if (cb && x0 + gsz < nwq) nfail = min(nfail, jb);
-      if (cc && x0 + 2 * gsz < nwq) nfail = min(nfail, jc);
-      if (cd && x0 + 3 * gsz < nwq) nfail = min(nfail, jd);
+      if (cb && gtid + gsz < nwq) nfail = min(nfail, jb);
+      if (cc && gtid + 2 * gsz < nwq) nfail = min(nfail, jc);
+      if (cd && gtid + 3 * gsz < nwq) nfail = min(nfail, jd);
+    }
+    // further rounds (more bucket queues than four per thread: long precomputed windows)
+    for (uint32_t x0 = gtid + 4 * gsz; x0 < nwq; x0 += 4 * gsz) {
+      const uint32_t xa = x0, xb = min(x0 + gsz, nwq - 1), xc = min(x0 + 2 * gsz, nwq - 1), xd = min(x0 + 3 * gsz, nwq - 1);
+      const uint32_t ka = xa / c.wheel_nq, kb = xb / c.wheel_nq, kc = xc / c.wheel_nq, kd = xd / c.wheel_nq;
+      uint32_t da = *qaddr(xa, ka), db = *qaddr(xb, kb), dc = *qaddr(xc, kc), dd = *qaddr(xd, kd);
+      QUIET_BATCH_WAIT("+v"(da), "+v"(db), "+v"(dc), "+v"(dd));
+      if (da) nfail = min(nfail, ka);
+      if (db && x0 + gsz < nwq) nfail = min(nfail, kb);
+      if (dc && x0 + 2 * gsz < nwq) nfail = min(nfail, kc);
+      if (dd && x0 + 3 * gsz < nwq) nfail = min(nfail, kd);
     }
   }
   if (gtid == 0) {
@@ -310,20 +367,15 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
   unsigned long long npings = 0, nsync = 0, nack = 0, nrec = 0;
   for (uint32_t i = gtid; i < c.nl; i += gsz) {
     const uint32_t v = c.lo + i;
-    // every word the member's window reads, in one batch, waited for once
-    uint32_t upw = gld(c.up + v), inbw = gld(c.default_inbound + v), fdn = gld(c.fd_next + i), sn0 = gld(c.sync_next + i);
-    const uint4 gw4 = gld4(c.gs + i);
-    const uint4* mp = reinterpret_cast<const uint4*>(c.mem + i);
-    const uint4 w0 = gld4(mp), w1 = gld4(mp + 1), w2 = gld4(mp + 2);
-    // (scalars for the asm operands: a vector component bound to an operand went through scratch)
-    uint32_t m0 = w0.x, m1 = w0.y, m2 = w0.z, m3 = w0.w, m4 = w1.x, m5 = w1.y, m6 = w1.z, m7 = w1.w, m8 = w2.x,
-             m9 = w2.y, m10 = w2.z, m11 = w2.w;
-    uint32_t gnext = gw4.x, gper = gw4.y;
-    QUIET_BATCH_WAIT("+v"(upw), "+v"(inbw), "+v"(fdn), "+v"(sn0), "+v"(gnext), "+v"(gper), "+v"(m0), "+v"(m1),
-                     "+v"(m2), "+v"(m3), "+v"(m4), "+v"(m5), "+v"(m6), "+v"(m7), "+v"(m8), "+v"(m9), "+v"(m10),
-                     "+v"(m11));
+    const bool first = i == gtid;
+    if (!first) {  // (a grid smaller than the shard: every word in one batch, waited for once)
+      load_member(i);
+      QUIET_BATCH_WAIT("+v"(upw), "+v"(inbw), "+v"(fdn), "+v"(sn0), "+v"(gnext), "+v"(gper), "+v"(m0), "+v"(m1),
+                       "+v"(m2), "+v"(m3), "+v"(m4), "+v"(m5), "+v"(m6), "+v"(m7), "+v"(m8), "+v"(m9), "+v"(m10),
+                       "+v"(m11));
+    }
     const bool up = upw != 0, inb = inbw != 0;
-    const GossipSched g{gnext, gper, gw4.z, gw4.w};
+    const GossipSched g{gnext, gper, gw2, gw3};
     QuietMem qm;  // (field by field from the words: a memcpy of a uint4 array put it in scratch)
     qm.ack_due = (uint64_t)m1 << 32 | m0;
     qm.relay_due = (uint64_t)m3 << 32 | m2;
@@ -356,9 +408,14 @@ __global__ void __launch_bounds__(256) k_quiet_apply(KP, uint32_t K, const Quiet
       gw.next = g.next + r * c.G;
       if (up) gw.period = g.period + r;
     }
-    // ---- periodic SYNC (the schedule advances while down too, sync_collect_fast)
+    // ---- periodic SYNC (the schedule advances while down too, sync_collect_fast); the first one's
+    // candidate words came with batch 2
     uint32_t sn = sn0;
     if (sn != NONE && sn < Tend) {
+      if (first && sy) {
+        quiet_sync_with(c, v, sn, qm.table_size, inb, sx, saw, sup, sin, nsync, nack, nrec);
+        sn += c.S;
+      }
       for (; sn < Tend; sn += c.S)
         if (up) quiet_sync(c, v, sn, qm.table_size, inb, nsync, nack, nrec);
       c.sync_next[i] = sn;
