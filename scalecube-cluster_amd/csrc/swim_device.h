@@ -375,8 +375,24 @@ struct InsOp {  // deferred pingMembers.add(nextInt(size), member) of an ADDED e
   uint32_t s, phase, minor, next;  // next: the viewer's following op in event order (chain)
 };
 // a viewer's first INS_INLINE ops of a phase sit in its own slots (read in parallel by the list
-// kernel); later ones chain through the shared op array
+// kernel); later ones go to blocks of the shared op array — 8, 16, 32, 64, 128, then 256 ops, each
+// block reserved whole when its first op comes (the one thread that owns the viewer in the phase
+// appends them).  The first op of a block holds the next block's start in `next`: the list kernel
+// hops block to block and reads a batch's ops in parallel, where an op-by-op chain took one
+// dependent load per op (16 K for a joiner's initial SYNC_ACK).
 constexpr uint32_t INS_INLINE = 8;
+// block of beyond-inline op j: its index, j's offset in it and its size
+__device__ __forceinline__ uint32_t ins_block_of(uint32_t j, uint32_t& off, uint32_t& size) {
+  if (j < 248) {
+    const uint32_t b = 31u - (uint32_t)__clz(j / 8 + 1);
+    off = j - 8 * ((1u << b) - 1);
+    size = 8u << b;
+    return b;
+  }
+  off = (j - 248) % 256;
+  size = 256;
+  return 5 + (j - 248) / 256;
+}
 
 // Receipt bitmap slot: gossip (gossiper, seq) hashes to one of GSLOTS slots; the slot's bits are
 // valid for the gossip `key` from tick `tick` on (a slot is (re)claimed only in k_end_tick, when no
@@ -1298,12 +1314,16 @@ __device__ inline void on_added(const Ctx& c, uint32_t v, uint32_t s, uint32_t p
   if (rank < INS_INLINE) {
     c.ins_inline[(size_t)(v - c.lo) * INS_INLINE + rank] = op;
   } else {
-    const uint32_t i = atomicAdd(c.ins_total, 1u);
-    if (i >= c.ins_cap) { set_err(c, ERR_INS); return; }
-    c.ins[i] = op;
-    if (rank == INS_INLINE) m.ins_head = i;
-    else c.ins[m.ins_tail].next = i;
-    m.ins_tail = i;
+    uint32_t off, size;
+    ins_block_of(rank - INS_INLINE, off, size);
+    if (off == 0) {  // a new block: reserved whole, linked from the previous block's first op
+      const uint32_t st = atomicAdd(c.ins_total, size);
+      if (st + size > c.ins_cap) { set_err(c, ERR_INS); return; }
+      if (rank == INS_INLINE) m.ins_head = st;
+      else c.ins[m.ins_tail].next = st;
+      m.ins_tail = st;  // (the current block's start)
+    }
+    c.ins[m.ins_tail + off] = op;
   }
   m.ins_rank = rank + 1;
 }

@@ -1640,7 +1640,7 @@ __device__ __forceinline__ void apply_ins_batch(const Ctx& c, uint32_t v, uint32
   if (k == 0) return;
   uint32_t* pl = ping_list(c, v);
   const InsOp* inl = c.ins_inline + (size_t)(v - c.lo) * INS_INLINE;
-  uint32_t cur = m.ins_head;  // ops beyond the inline ones (thread 0 walks the chain)
+  uint32_t blk = m.ins_head, blk_idx = 0;  // (thread 0: the block its hops have reached)
   uint32_t len = m.ping_len;
   for (uint32_t q0 = 0; q0 < k; q0 += NT) {
     const uint32_t kb = min((uint32_t)NT, k - q0);
@@ -1650,12 +1650,25 @@ __device__ __forceinline__ void apply_ins_batch(const Ctx& c, uint32_t v, uint32
       sS[tid] = op.s;
       sP[tid] = next_int(draw(c, v, SWIM_STREAM_PING_INSERT, op.phase, op.minor), len + tid);
     }
-    if (tid == 0) {
-      for (uint32_t q = max(q0, INS_INLINE); q < q0 + kb; ++q) {
-        const InsOp op = c.ins[cur];
-        sS[q - q0] = op.s;
-        sP[q - q0] = next_int(draw(c, v, SWIM_STREAM_PING_INSERT, op.phase, op.minor), len + (q - q0));
-        cur = op.next;
+    if (q0 + kb > INS_INLINE) {  // the batch's ops in blocks: their starts into sR (thread 0), then the ops
+      uint32_t o, z;
+      const uint32_t b0 = ins_block_of(q0 > INS_INLINE ? q0 - INS_INLINE : 0u, o, z);
+      const uint32_t b1 = ins_block_of(q0 + kb - 1 - INS_INLINE, o, z);
+      if (tid == 0) {
+        for (; blk_idx < b0; ++blk_idx) blk = c.ins[blk].next;
+        sR[0] = blk;
+        for (uint32_t bb = b0 + 1; bb <= b1; ++bb) {
+          blk = c.ins[blk].next;
+          sR[bb - b0] = blk;
+        }
+        blk_idx = b1;
+      }
+      ins_bar<WG>();
+      if (tid < kb && q0 + tid >= INS_INLINE) {
+        const uint32_t bq = ins_block_of(q0 + tid - INS_INLINE, o, z);
+        const InsOp op = c.ins[sR[bq - b0] + o];
+        sS[tid] = op.s;
+        sP[tid] = next_int(draw(c, v, SWIM_STREAM_PING_INSERT, op.phase, op.minor), len + tid);
       }
     }
     ins_bar<WG>();
