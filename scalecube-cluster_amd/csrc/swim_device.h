@@ -404,6 +404,7 @@ constexpr uint32_t GSLOTS = 8192;
 // line per (gossip, target)), and delivery marks one receiver's accepted lanes into one row.  A claim
 // clears one bit of every row (k_end_tick); claims are per new gossip, a few hundred per run.
 constexpr uint32_t GROW = GSLOTS / 32;
+constexpr uint32_t GSLOT_HOLD = 64;  // ticks a claimed slot stays with its gossip before another may take it
 __device__ __forceinline__ size_t rbit_word(uint32_t i, uint32_t sl) { return (size_t)i * GROW + (sl >> 5); }
 struct GSlot {
   uint64_t key;   // (gossiper + 1) << 32 | seq, 0 = unowned
@@ -1257,11 +1258,15 @@ __device__ inline void coll_clear(const Ctx& c, CollEnt* e) {
 __device__ inline void receipt_mark(const Ctx& c, uint32_t r, uint32_t gossiper, uint32_t seq) {
   const uint64_t key = gkey(gossiper, seq);
   const uint32_t sl = gslot_of(key);
-  const uint64_t owner = c.gslot[sl].key;
+  const GSlot gs = c.gslot[sl];
+  const uint64_t owner = gs.key;
   if (owner == key) {
     const uint32_t i = r - c.lo;
     atomicOr(&c.gbits[rbit_word(i, sl)], 1u << (sl & 31));
-  } else if (c.gpend[sl] == 0ull &&  // (a plain read first: once claimed, the thousands of receivers of a
+  } else if ((owner == 0ull || gs.tick + GSLOT_HOLD <= (uint32_t)c.T) &&
+             // (an owner keeps its slot GSLOT_HOLD ticks: two live gossips on one slot would otherwise
+             // take it from each other every tick, each claim clearing a bit in every receiver's row)
+             c.gpend[sl] == 0ull &&  // (a plain read first: once claimed, the thousands of receivers of a
                                      // new gossip skip the contended compare-and-swap)
              atomicCAS(reinterpret_cast<unsigned long long*>(&c.gpend[sl]), 0ull, (unsigned long long)key) == 0ull) {
     const uint32_t par = (uint32_t)(c.T & 1);
